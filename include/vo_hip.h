@@ -1,0 +1,154 @@
+/*
+ * vo_hip.h -- C-ABI of the MI355X (gfx950) back end for the feature-matching +
+ * sliding-window bundle-adjustment hot path of cteufel13/VisualOdometry.
+ *
+ * Plain C: pointers, sizes and status codes only.  The Python host package
+ * (visualodometry_amd/_lib.py) binds it with ctypes; INTEGRATION.md shows the
+ * binding.  Every entry point is host-synchronous unless its name ends in
+ * _async, and returns VO_OK (0) or a negative vo_status.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo root):
+ *   vo_match_knn2_ratio   <- FeatureFrontend.match_frames, SIFT branch,
+ *                            src/modules/frontend.py:86-111
+ *                            (cv2.BFMatcher(cv2.NORM_L2, crossCheck=False)
+ *                             .knnMatch(des0, des1, k=2) at :34/:101 and the
+ *                             Lowe ratio test at :103-109)
+ *   vo_match_knn2         <- the knnMatch(k=2) call alone, frontend.py:101
+ *   vo_ba_*               <- new: the reference has no BA (pyceres/pycolmap
+ *                            are declared in pyproject.toml:11-12 but never
+ *                            imported).  Insertion point: the keyframe hook
+ *                            VisualOdometry._create_keyframe,
+ *                            src/modules/vo.py:252-288.  Projection model of
+ *                            frontend.py:128-140, pose convention T_cw of
+ *                            vo.py:260-261.
+ */
+#ifndef VO_HIP_H
+#define VO_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VO_ABI_VERSION 1
+
+typedef enum {
+  VO_OK = 0,
+  VO_ERR_ARG = -1,      /* bad argument / unsupported shape */
+  VO_ERR_HIP = -2,      /* HIP runtime error */
+  VO_ERR_NOT_SPD = -3,  /* reduced camera system not positive definite */
+  VO_ERR_RCCL = -4,     /* RCCL error */
+  VO_ERR_NOMEM = -5,    /* device allocation failed */
+  VO_ERR_STATE = -6,    /* call out of order (e.g. vo_ba_run before vo_ba_setup) */
+  VO_ERR_NODEV = -7     /* no usable gfx950 device */
+} vo_status;
+
+typedef struct vo_ctx vo_ctx;
+
+/* ---- library / context -------------------------------------------------- */
+int vo_abi_version(void);
+/* Thread-local message for the last failing call on this thread. */
+const char* vo_last_error(void);
+/* Creates a context bound to HIP device `device` with its own stream.  flags: 0.
+ * Returns NULL on failure (vo_last_error() says why). */
+vo_ctx* vo_create(int device, int flags);
+void vo_destroy(vo_ctx* ctx);
+/* The context's HIP stream (hipStream_t), for callers that enqueue on it. */
+void* vo_stream(vo_ctx* ctx);
+int vo_synchronize(vo_ctx* ctx);
+
+/* ---- descriptor matching (knn k=2 + Lowe ratio) --------------------------
+ * des0: (n0, dim) float32 row-major, the "query" (previous keyframe) set;
+ * des1: (n1, dim) float32 row-major, the "train" (current frame) set.
+ * Semantics of OpenCV BFMatcher(NORM_L2).knnMatch(k=2) followed by the
+ * reference ratio test:
+ *   dist(i,j) = sqrtf(sum_d (a_id - b_jd)^2), the two nearest train rows per
+ *   query under the order (dist, j) -- equal distances keep the lower j --,
+ *   and pair (i, j1) is kept iff (double)dist1 < ratio * (double)dist2.
+ *   Queries with n1 < 2 neighbours emit nothing.  Pairs are written in
+ *   ascending query order as int32 (query, train).
+ * Descriptors whose values are all integers in [0, 255] (OpenCV SIFT) take the
+ * exact int8 MFMA path; any other values take the fp32 path, whose per-pair
+ * distance is the k-ordered fmaf chain sum((a-b)^2).
+ * out_pairs capacity: 2*n0 int32.  Empty inputs give *out_count = 0.        */
+int vo_match_knn2_ratio(vo_ctx* ctx, const float* des0, int n0, const float* des1,
+                        int n1, int dim, double ratio, int32_t* out_pairs,
+                        int32_t* out_count);
+
+/* Top-2 per query without the ratio test.  idx_out: (n0, 2) int32 (-1 when
+ * fewer than 2 neighbours exist), dist_out: (n0, 2) float32 distances
+ * (FLT_MAX where idx is -1). */
+int vo_match_knn2(vo_ctx* ctx, const float* des0, int n0, const float* des1, int n1,
+                  int dim, int32_t* idx_out, float* dist_out);
+
+/* Batched frame pairs, device pointers, enqueued on the context stream.
+ * d_des0: (batch, n0, dim), d_des1: (batch, n1, dim) float32 on the device;
+ * d_best: (batch, n0) int32 -- the train index kept for each query by the
+ * ratio test, or -1.  Nothing is copied to the host. */
+int vo_match_batch_async(vo_ctx* ctx, const float* d_des0, const float* d_des1,
+                         int batch, int n0, int n1, int dim, double ratio,
+                         int32_t* d_best);
+
+/* ---- sliding-window bundle adjustment ------------------------------------ */
+typedef struct {
+  int32_t n_poses;   /* N cameras in the window                               */
+  int32_t n_points;  /* L landmarks                                           */
+  int32_t n_obs;     /* M observations                                        */
+  int32_t n_fixed;   /* poses 0..n_fixed-1 are held fixed (gauge)             */
+  double fx, fy, cx, cy;      /* pinhole K, no distortion (frontend.py:139)  */
+  double lambda;              /* Levenberg damping added to every block (>=0) */
+  const int32_t* point_ptr;   /* (n_points+1) CSR: obs of point p are
+                                 point_ptr[p]..point_ptr[p+1]-1               */
+  const int32_t* obs_cam;     /* (n_obs) camera index of each observation    */
+  const float* obs_uv;        /* (n_obs, 2) pixel measurement (float32, as
+                                 FeatureFrontend keypoints, frontend.py:59)   */
+} vo_ba_problem;
+
+/* Uploads the observation structure and builds the static execution plan
+ * (landmark chunks, per-workgroup camera-pair windows, reduced-system profile).
+ * Replaces any previous problem in this context. */
+int vo_ba_setup(vo_ctx* ctx, const vo_ba_problem* prob);
+/* poses: (n_poses, 12) float64 = R_cw row-major (9) then t_cw (3);
+ * points: (n_points, 3) float64. */
+int vo_ba_set_state(vo_ctx* ctx, const double* poses, const double* points);
+int vo_ba_get_state(vo_ctx* ctx, double* poses, double* points);
+/* Runs `iters` pure Gauss-Newton iterations (every step accepted) on the
+ * device-resident state.  cost_out (iters+1 doubles, may be NULL): sum of
+ * squared residuals before each iteration and after the last one.
+ * Returns VO_ERR_NOT_SPD (state left at the last good iterate) if the reduced
+ * camera system is not positive definite. */
+int vo_ba_run(vo_ctx* ctx, int iters, double* cost_out);
+/* Same, enqueued on the context stream with no host synchronisation and no
+ * cost read-back (for timing).  Errors surface at the next synchronous call. */
+int vo_ba_run_async(vo_ctx* ctx, int iters);
+/* One GN iteration with the intermediate quantities exported (parity tests):
+ * S_out: dense (6F, 6F) float64 reduced camera matrix with F = n_poses-n_fixed
+ * (may be NULL), b_out: (6F), dc_out: (6F) pose update (may be NULL),
+ * cost_out: 1 double.  The state is advanced by the step. */
+int vo_ba_step_debug(vo_ctx* ctx, double* S_out, double* b_out, double* dc_out,
+                     double* cost_out);
+/* One-call convenience: setup + set_state + run + get_state. */
+int vo_ba_solve(vo_ctx* ctx, const vo_ba_problem* prob, double* poses, double* points,
+                int iters, double* cost_out);
+
+/* Static plan statistics (for DESIGN.md/bench): fills up to n int64 values:
+ * [0] chunks [1] segments [2] slab blocks [3] reduced blocks [4] profile
+ * blocks [5] track entries [6] bytes read+written per GN iteration
+ * (algorithmic) [7] wide landmarks. Returns count written. */
+int vo_ba_plan_stats(vo_ctx* ctx, int64_t* out, int n);
+
+/* ---- multi-GPU (landmark sharding + RCCL all-reduce) --------------------- */
+/* 128-byte RCCL unique id, created on rank 0 and shared by the caller. */
+int vo_comm_unique_id(char out[128]);
+/* Attaches an RCCL communicator to the context (one process per GPU).  After
+ * this, vo_ba_setup expects THIS rank's landmark shard: every rank passes all
+ * n_poses cameras but only its own points/observations; each GN iteration
+ * all-reduces the partial reduced camera system (S, b, cost) before the
+ * redundant dense pose solve, so all ranks hold identical poses. */
+int vo_comm_init(vo_ctx* ctx, int nranks, int rank, const char id[128]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VO_HIP_H */

@@ -1,0 +1,156 @@
+"""GPU parity of the matcher (vo_match_*) against the CPU oracle -- bit-exact.
+
+Integer indices and float32 distances must be identical to oracle/match_ref
+(OpenCV BFMatcher(NORM_L2).knnMatch(k=2) + ratio test semantics,
+reference src/modules/frontend.py:86-111).
+"""
+
+import numpy as np
+import pytest
+
+from oracle import match_ref
+from visualodometry_amd import matcher
+from visualodometry_amd.synthetic import sift_like_pair, superpoint_like_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_knn2(d0, d1, ctx, oracle="int"):
+    idx, dist = matcher.match_knn2(d0, d1, ctx=ctx)
+    if oracle == "int":
+        ri, rd = match_ref.knn2_int(d0, d1)
+    else:
+        ri, rd = match_ref.knn2_c(d0, d1, nthreads=8)
+    np.testing.assert_array_equal(idx, ri)
+    np.testing.assert_array_equal(dist.view(np.uint32), rd.view(np.uint32))
+    pairs = matcher.match_knn2_ratio(d0, d1, ctx=ctx)
+    np.testing.assert_array_equal(pairs, match_ref.ratio_filter(ri, rd))
+    assert pairs.dtype == np.int64 and pairs.ndim == 2 and pairs.shape[1] == 2
+
+
+@pytest.mark.parametrize("n0,n1,seed", [(512, 512, 0), (1000, 1200, 1), (37, 5, 2), (300, 17, 3),
+                                        (2048, 2048, 4)])
+def test_sift_like_bit_exact(ctx, n0, n1, seed):
+    d0, d1 = sift_like_pair(n0, n1, seed)
+    _check_knn2(d0, d1, ctx)
+
+
+def test_sift_kitti_size_4000(ctx):
+    """BASELINE config: KITTI SIFT, 4000 x 4000 x 128 (config.py:64)."""
+    d0, d1 = sift_like_pair(4000, 4000, 11)
+    _check_knn2(d0, d1, ctx)
+
+
+@pytest.mark.parametrize("dim", [64, 100, 192, 256])
+def test_int_dims(ctx, dim):
+    d0, d1 = sift_like_pair(333, 444, 5, dim=dim)
+    _check_knn2(d0, d1, ctx)
+
+
+def test_int_valued_dim_over_256_takes_float_path(ctx):
+    # integer data with D > 256 runs on the fp32 path; integer sums are exact there too
+    d0, d1 = sift_like_pair(200, 300, 6, dim=320)
+    _check_knn2(d0, d1, ctx)
+
+
+def test_superpoint_like_float_bit_exact(ctx):
+    d0, d1 = superpoint_like_pair(700, 900, 7)
+    _check_knn2(d0, d1, ctx, oracle="c")
+
+
+def test_superpoint_2048(ctx):
+    """BASELINE config 5: SuperPoint-like 2048 x 2048 x 256 (config.py:15)."""
+    d0, d1 = superpoint_like_pair(2048, 2048, 8)
+    _check_knn2(d0, d1, ctx, oracle="c")
+
+
+def test_ties_keep_lower_train_index(ctx):
+    rng = np.random.default_rng(0)
+    base = rng.integers(0, 256, (8, 128)).astype(np.float32)
+    d1 = np.concatenate([base, base, base])  # every row appears 3 times
+    d0 = base.copy()
+    idx, dist = matcher.match_knn2(d0, d1, ctx=ctx)
+    np.testing.assert_array_equal(idx[:, 0], np.arange(8))
+    np.testing.assert_array_equal(idx[:, 1], np.arange(8) + 8)
+    assert (dist[:, :2] == 0).all()
+    # equal best and second distances: 0 < 0.75 * 0 fails -> no match
+    assert matcher.match_knn2_ratio(d0, d1, ctx=ctx).shape == (0, 2)
+
+
+def test_single_train_row_gives_no_matches(ctx):
+    d0, d1 = sift_like_pair(50, 1, 9)
+    idx, dist = matcher.match_knn2(d0, d1, ctx=ctx)
+    assert (idx[:, 0] == 0).all() and (idx[:, 1] == -1).all()
+    assert matcher.match_knn2_ratio(d0, d1, ctx=ctx).shape == (0, 2)
+
+
+def test_empty_inputs(ctx):
+    d = np.zeros((10, 128), np.float32)
+    e = np.zeros((0, 128), np.float32)
+    assert matcher.match_knn2_ratio(e, d, ctx=ctx).shape == (0, 2)
+    assert matcher.match_knn2_ratio(d, e, ctx=ctx).shape == (0, 2)
+    idx, _ = matcher.match_knn2(d, e, ctx=ctx)
+    assert (idx == -1).all()
+
+
+def test_many_to_one(ctx):
+    """No crossCheck (frontend.py:34): several queries may keep the same train row."""
+    rng = np.random.default_rng(3)
+    d1 = rng.integers(0, 256, (64, 128)).astype(np.float32)
+    d0 = np.repeat(d1[:1], 5, axis=0)
+    d0[:, 0] = np.clip(d0[:, 0] + np.arange(5), 0, 255)
+    pairs = matcher.match_knn2_ratio(d0, d1, ctx=ctx)
+    np.testing.assert_array_equal(pairs, match_ref.match_int(d0, d1))
+    assert (pairs[:, 1] == 0).all() and len(pairs) == 5
+
+
+def test_sqrt_collision_rescan(ctx):
+    """d2 = n and n+1 (>= 2^22) that sqrtf maps to the same float: the (dist, j) key
+    must then prefer the lower train index even though its d2 is larger."""
+    # find n with sqrtf(n) == sqrtf(n + 1), n in the reachable range (< 128 * 255^2)
+    n = None
+    for cand in range(4_200_000, 8_000_000, 7):
+        if np.sqrt(np.float32(cand)) == np.sqrt(np.float32(cand + 1)):
+            n = cand
+            break
+    assert n is not None
+    rng = np.random.default_rng(5)
+
+    def vec_with_d2(target):
+        # query = zeros; a train row with sum of squares == target, values 0..255
+        v = np.zeros(128, np.int64)
+        rem = target
+        k = 0
+        while rem > 0:
+            x = int(min(255, np.floor(np.sqrt(rem))))
+            v[k] = x
+            rem -= x * x
+            k += 1
+        assert rem == 0 and k <= 128
+        return rng.permutation(v).astype(np.float32)
+
+    q = np.zeros((1, 128), np.float32)
+    far = vec_with_d2(n + 4000)
+    t = np.stack([far, vec_with_d2(n + 1), far, vec_with_d2(n), far])  # j=1 has the larger d2
+    idx, dist = matcher.match_knn2(q, t, ctx=ctx)
+    ri, rd = match_ref.knn2_int(q, t)
+    np.testing.assert_array_equal(idx, ri)
+    np.testing.assert_array_equal(dist, rd)
+    assert idx[0, 0] == 1 and idx[0, 1] == 3
+
+
+def test_batch_device_matches_single(ctx):
+    import torch
+
+    B, n0, n1 = 4, 500, 600
+    pairs = [sift_like_pair(n0, n1, 100 + b) for b in range(B)]
+    a = torch.tensor(np.stack([p[0] for p in pairs]), device="cuda")
+    b = torch.tensor(np.stack([p[1] for p in pairs]), device="cuda")
+    torch.cuda.synchronize()
+    best = matcher.match_batch_device(a, b, ctx=ctx)
+    matcher.synchronize(ctx)
+    best = best.cpu().numpy()
+    for k in range(B):
+        ref = match_ref.match_int(*pairs[k])
+        got = np.nonzero(best[k] >= 0)[0]
+        np.testing.assert_array_equal(np.stack([got, best[k][got]], 1), ref)

@@ -1,0 +1,156 @@
+"""ctypes binding of ``libvo_hip.so`` (the C-ABI declared in ``include/vo_hip.h``).
+
+The product path has no CPU fallback: if the library or a gfx950 device is
+missing, :func:`context` raises.  ``load()`` alone (no device needed) is used by
+the CPU test-suite to check that every declared symbol is exported.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvo_hip.so"
+HEADER = Path(__file__).resolve().parents[1] / "include" / "vo_hip.h"
+
+VO_OK = 0
+VO_ERR_ARG = -1
+VO_ERR_HIP = -2
+VO_ERR_NOT_SPD = -3
+VO_ERR_RCCL = -4
+VO_ERR_NOMEM = -5
+VO_ERR_STATE = -6
+VO_ERR_NODEV = -7
+STATUS_NAMES = {
+    VO_OK: "ok", VO_ERR_ARG: "bad argument", VO_ERR_HIP: "HIP error",
+    VO_ERR_NOT_SPD: "not positive definite", VO_ERR_RCCL: "RCCL error",
+    VO_ERR_NOMEM: "out of device memory", VO_ERR_STATE: "bad call order",
+    VO_ERR_NODEV: "no gfx950 device",
+}
+
+
+class VoError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class BAProblemC(C.Structure):
+    _fields_ = [
+        ("n_poses", C.c_int32), ("n_points", C.c_int32), ("n_obs", C.c_int32),
+        ("n_fixed", C.c_int32),
+        ("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
+        ("lam", C.c_double),
+        ("point_ptr", C.POINTER(C.c_int32)), ("obs_cam", C.POINTER(C.c_int32)),
+        ("obs_uv", C.POINTER(C.c_float)),
+    ]
+
+
+_P = C.c_void_p
+_I = C.c_int
+_D = C.c_double
+_PI32 = C.POINTER(C.c_int32)
+_PF = C.POINTER(C.c_float)
+_PD = C.POINTER(C.c_double)
+_PI64 = C.POINTER(C.c_int64)
+
+# name -> (restype, argtypes); must cover every function in include/vo_hip.h
+SIGNATURES = {
+    "vo_abi_version": (_I, []),
+    "vo_last_error": (C.c_char_p, []),
+    "vo_create": (_P, [_I, _I]),
+    "vo_destroy": (None, [_P]),
+    "vo_stream": (_P, [_P]),
+    "vo_synchronize": (_I, [_P]),
+    "vo_match_knn2_ratio": (_I, [_P, _PF, _I, _PF, _I, _I, _D, _PI32, _PI32]),
+    "vo_match_knn2": (_I, [_P, _PF, _I, _PF, _I, _I, _PI32, _PF]),
+    "vo_match_batch_async": (_I, [_P, _P, _P, _I, _I, _I, _I, _D, _P]),
+    "vo_ba_setup": (_I, [_P, C.POINTER(BAProblemC)]),
+    "vo_ba_set_state": (_I, [_P, _PD, _PD]),
+    "vo_ba_get_state": (_I, [_P, _PD, _PD]),
+    "vo_ba_run": (_I, [_P, _I, _PD]),
+    "vo_ba_run_async": (_I, [_P, _I]),
+    "vo_ba_step_debug": (_I, [_P, _PD, _PD, _PD, _PD]),
+    "vo_ba_solve": (_I, [_P, C.POINTER(BAProblemC), _PD, _PD, _I, _PD]),
+    "vo_ba_plan_stats": (_I, [_P, _PI64, _I]),
+    "vo_comm_unique_id": (_I, [C.c_char_p]),
+    "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load() -> C.CDLL:
+    """Loads the in-tree library (raises if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not LIB_PATH.exists():
+                raise RuntimeError(
+                    f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                    " (hipcc --offload-arch=gfx950)"
+                )
+            lib = C.CDLL(str(LIB_PATH))
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            if lib.vo_abi_version() != 1:
+                raise RuntimeError("libvo_hip.so ABI mismatch")
+            _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str = "") -> int:
+    if rc < 0:
+        msg = load().vo_last_error().decode(errors="replace")
+        raise VoError(rc, f"{what}: {msg}" if what else msg)
+    return rc
+
+
+class Context:
+    """Owns a ``vo_ctx`` (one gfx950 device + stream)."""
+
+    def __init__(self, device: int = 0):
+        lib = load()
+        h = lib.vo_create(device, 0)
+        if not h:
+            raise VoError(VO_ERR_NODEV, lib.vo_last_error().decode(errors="replace"))
+        self.handle = h
+        self.device = device
+        self.lib = lib
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.vo_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_contexts: dict[int, Context] = {}
+
+
+def context(device: int | None = None) -> Context:
+    """Process-wide default context per device (``VO_DEVICE`` or 0)."""
+    if device is None:
+        device = int(os.environ.get("VO_DEVICE", "0"))
+    with _lock:
+        ctx = _contexts.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        with _lock:
+            _contexts.setdefault(device, ctx)
+            ctx = _contexts[device]
+    return ctx
+
+
+def ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))

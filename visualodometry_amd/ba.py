@@ -1,0 +1,196 @@
+"""Sliding-window bundle adjustment on MI355X (Gauss-Newton with Schur complement).
+
+The reference has no BA: ``pyceres``/``pycolmap`` are declared
+(``pyproject.toml:11-12``) but never imported, and pose comes only from
+``cv2.solvePnPRansac`` (``src/modules/vo.py:135-141``).  This module is the
+build-defined BA API of SURVEY.md §8b, meant to be called from the keyframe
+hook ``VisualOdometry._create_keyframe`` (``src/modules/vo.py:252-288``):
+
+    ba = SlidingWindowBA(K, cfg)
+    result = ba.optimize(window)        # never raises on a degenerate window
+
+Model (identical to ``oracle/ba_ref.py``): residual ``pi(K (R_cw X + t_cw)) - uv``
+with the no-distortion pinhole of ``frontend.py:139``, cost ``sum ||r||^2``,
+left se(3) pose increments, the first ``n_fixed`` poses fixed, pure GN.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import BAProblemC, C, VoError, check, ptr
+
+
+@dataclass
+class BAWindow:
+    """Keyframe window handed to :meth:`SlidingWindowBA.optimize`.
+
+    ``obs_pt`` gives the landmark of each observation in any order; it is
+    grouped by landmark (CSR) before the C-ABI call.
+    """
+
+    poses_cw: np.ndarray  # (N,4,4) float64, world -> camera
+    points: np.ndarray  # (L,3) float64
+    obs_uv: np.ndarray  # (M,2) float32 pixels
+    obs_cam: np.ndarray  # (M,) int
+    obs_pt: np.ndarray  # (M,) int
+    n_fixed: int = 2
+
+
+@dataclass
+class BAResult:
+    poses_cw: np.ndarray
+    points: np.ndarray
+    cost_per_iter: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    status: str = "ok"  # "ok" | "not_spd" | "skipped"
+    message: str = ""
+
+
+def poses_to_rt(poses_cw: np.ndarray) -> np.ndarray:
+    """(N,4,4) -> (N,12) = R row-major, t (the C-ABI pose layout)."""
+    P = np.asarray(poses_cw, dtype=np.float64)
+    out = np.empty((P.shape[0], 12))
+    out[:, :9] = P[:, :3, :3].reshape(-1, 9)
+    out[:, 9:] = P[:, :3, 3]
+    return out
+
+
+def rt_to_poses(rt: np.ndarray) -> np.ndarray:
+    T = np.tile(np.eye(4), (rt.shape[0], 1, 1))
+    T[:, :3, :3] = rt[:, :9].reshape(-1, 3, 3)
+    T[:, :3, 3] = rt[:, 9:]
+    return T
+
+
+def csr_from_obs_pt(n_points: int, obs_pt: np.ndarray):
+    """Stable grouping of observations by landmark -> (order, point_ptr)."""
+    obs_pt = np.asarray(obs_pt, dtype=np.int64)
+    if obs_pt.size and (obs_pt.min() < 0 or obs_pt.max() >= n_points):
+        raise ValueError("obs_pt out of range")
+    order = np.argsort(obs_pt, kind="stable")
+    ptr_ = np.zeros(n_points + 1, dtype=np.int32)
+    ptr_[1:] = np.cumsum(np.bincount(obs_pt, minlength=n_points))
+    return order, ptr_
+
+
+class BASession:
+    """A BA problem resident on one device (structure + state in HBM).
+
+    Thin wrapper of the ``vo_ba_*`` C-ABI: ``setup`` uploads the structure and
+    builds the static plan, ``set_state``/``get_state`` move poses and points,
+    ``run`` performs GN iterations on the device-resident state.
+    """
+
+    def __init__(self, K, point_ptr, obs_cam, obs_uv, n_poses: int, n_fixed: int = 2,
+                 lam: float = 0.0, ctx: _lib.Context | None = None):
+        self.ctx = ctx or _lib.context()
+        self.point_ptr = np.ascontiguousarray(point_ptr, dtype=np.int32)
+        self.obs_cam = np.ascontiguousarray(obs_cam, dtype=np.int32)
+        self.obs_uv = np.ascontiguousarray(obs_uv, dtype=np.float32).reshape(-1, 2)
+        self.n_poses = int(n_poses)
+        self.n_points = self.point_ptr.size - 1
+        self.n_fixed = int(n_fixed)
+        K = np.asarray(K, dtype=np.float64)
+        prob = BAProblemC()
+        prob.n_poses = self.n_poses
+        prob.n_points = self.n_points
+        prob.n_obs = self.obs_cam.size
+        prob.n_fixed = self.n_fixed
+        prob.fx, prob.fy, prob.cx, prob.cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+        prob.lam = float(lam)
+        prob.point_ptr = ptr(self.point_ptr, C.c_int32)
+        prob.obs_cam = ptr(self.obs_cam, C.c_int32)
+        prob.obs_uv = ptr(self.obs_uv, C.c_float)
+        self._prob = prob
+        check(self.ctx.lib.vo_ba_setup(self.ctx.handle, C.byref(prob)), "vo_ba_setup")
+
+    def set_state(self, poses_cw: np.ndarray, points: np.ndarray) -> None:
+        rt = np.ascontiguousarray(poses_to_rt(poses_cw))
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        if rt.shape[0] != self.n_poses or pts.shape[0] != self.n_points:
+            raise ValueError("state shape does not match the problem")
+        check(self.ctx.lib.vo_ba_set_state(self.ctx.handle, ptr(rt, C.c_double), ptr(pts, C.c_double)),
+              "vo_ba_set_state")
+
+    def get_state(self):
+        rt = np.empty((self.n_poses, 12))
+        pts = np.empty((self.n_points, 3))
+        check(self.ctx.lib.vo_ba_get_state(self.ctx.handle, ptr(rt, C.c_double), ptr(pts, C.c_double)),
+              "vo_ba_get_state")
+        return rt_to_poses(rt), pts
+
+    def run(self, iters: int):
+        """``iters`` GN iterations; returns (status_code, costs[iters+1])."""
+        costs = np.empty(iters + 1)
+        rc = self.ctx.lib.vo_ba_run(self.ctx.handle, int(iters), ptr(costs, C.c_double))
+        if rc not in (_lib.VO_OK, _lib.VO_ERR_NOT_SPD):
+            check(rc, "vo_ba_run")
+        return rc, costs
+
+    def run_async(self, iters: int) -> None:
+        check(self.ctx.lib.vo_ba_run_async(self.ctx.handle, int(iters)), "vo_ba_run_async")
+
+    def synchronize(self) -> None:
+        check(self.ctx.lib.vo_synchronize(self.ctx.handle), "vo_synchronize")
+
+    def step_debug(self):
+        """One GN step exporting (rc, S dense, b, dc, cost-before-step)."""
+        F = self.n_poses - self.n_fixed
+        S = np.empty((6 * F, 6 * F))
+        b = np.empty(6 * F)
+        dc = np.empty(6 * F)
+        cost = np.empty(1)
+        rc = self.ctx.lib.vo_ba_step_debug(self.ctx.handle, ptr(S, C.c_double), ptr(b, C.c_double),
+                                           ptr(dc, C.c_double), ptr(cost, C.c_double))
+        if rc not in (_lib.VO_OK, _lib.VO_ERR_NOT_SPD):
+            check(rc, "vo_ba_step_debug")
+        return rc, S, b, dc, float(cost[0])
+
+    def plan_stats(self) -> dict:
+        out = np.zeros(8, dtype=np.int64)
+        n = check(self.ctx.lib.vo_ba_plan_stats(self.ctx.handle, ptr(out, C.c_int64), 8), "stats")
+        keys = ["chunks", "segments", "slab_blocks", "reduced_blocks", "profile_blocks",
+                "track_entries", "algorithmic_bytes_per_iter", "wide_landmarks"]
+        return dict(zip(keys[:n], out[:n].tolist()))
+
+
+class SlidingWindowBA:
+    """``SlidingWindowBA(K, cfg).optimize(window) -> BAResult``.
+
+    ``cfg`` may be a ``VOConfig`` carrying ``ba_iters`` / ``ba_lambda``; any
+    missing knob takes the keyword default.  Degenerate windows come back with
+    ``status != "ok"`` instead of raising, so ``process_frame`` keeps the
+    reference's print-and-continue failure style (``vo.py:240-245``).
+    """
+
+    def __init__(self, K, cfg=None, *, iters: int = 10, lam: float = 0.0, device: int | None = None):
+        self.K = np.asarray(K, dtype=np.float64)
+        self.iters = int(getattr(cfg, "ba_iters", iters))
+        self.lam = float(getattr(cfg, "ba_lambda", lam))
+        self.device = device
+
+    def optimize(self, window: BAWindow) -> BAResult:
+        poses = np.asarray(window.poses_cw, dtype=np.float64)
+        pts = np.asarray(window.points, dtype=np.float64).reshape(-1, 3)
+        n_fixed = min(int(window.n_fixed), poses.shape[0])
+        if poses.shape[0] == 0 or pts.shape[0] == 0 or np.asarray(window.obs_cam).size == 0 \
+                or poses.shape[0] <= n_fixed:
+            return BAResult(poses.copy(), pts.copy(), np.zeros(0), "skipped", "empty window")
+        order, point_ptr = csr_from_obs_pt(pts.shape[0], window.obs_pt)
+        obs_cam = np.asarray(window.obs_cam)[order]
+        obs_uv = np.asarray(window.obs_uv, dtype=np.float32).reshape(-1, 2)[order]
+        ctx = _lib.context(self.device)
+        try:
+            sess = BASession(self.K, point_ptr, obs_cam, obs_uv, poses.shape[0], n_fixed, self.lam, ctx)
+            sess.set_state(poses, pts)
+            rc, costs = sess.run(self.iters)
+            P, X = sess.get_state()
+        except VoError as e:
+            if e.code == _lib.VO_ERR_ARG:
+                return BAResult(poses.copy(), pts.copy(), np.zeros(0), "skipped", str(e))
+            raise
+        status = "ok" if rc == _lib.VO_OK else "not_spd"
+        return BAResult(P, X, costs, status)

@@ -1,0 +1,241 @@
+// extern "C" entry points of libvo_hip.so (declared in include/vo_hip.h).
+#include <cstdarg>
+#include <cstring>
+#include <vector>
+
+#include "vo_ctx.h"
+
+namespace vo {
+
+namespace {
+thread_local std::string g_err;
+}
+
+void set_error(const char* f, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, f);
+  std::vsnprintf(buf, sizeof buf, f, ap);
+  va_end(ap);
+  g_err = buf;
+}
+const char* last_error() { return g_err.c_str(); }
+
+// ba.hip
+void ba_setup(vo_ctx*, const vo_ba_problem*);
+void ba_set_state(vo_ctx*, const double*, const double*);
+void ba_get_state(vo_ctx*, double*, double*);
+int ba_run(vo_ctx*, int, double*, bool);
+int ba_step_debug(vo_ctx*, double*, double*, double*, double*);
+int ba_stats(vo_ctx*, int64_t*, int);
+void comm_unique_id(char out[128]);
+void comm_init(vo_ctx*, int, int, const char*);
+
+namespace {
+
+void bind(vo_ctx* ctx) {
+  VO_REQUIRE(ctx, VO_ERR_ARG, "null vo_ctx");
+  VO_HIP_CHECK(hipSetDevice(ctx->device));
+}
+
+// Host-array matcher call: descriptors staged into the workspace, results copied back.
+void match_host(vo_ctx* ctx, const float* des0, int n0, const float* des1, int n1, int dim,
+                double ratio, int32_t* pairs, int32_t* count, int32_t* idx2, float* dist2) {
+  VO_REQUIRE(n0 >= 0 && n1 >= 0 && dim >= 1, VO_ERR_ARG, "match: bad shape n0=%d n1=%d dim=%d",
+             n0, n1, dim);
+  VO_REQUIRE((n0 == 0 || des0) && (n1 == 0 || des1), VO_ERR_ARG, "match: null descriptors");
+  if (count) *count = 0;
+  if (n0 == 0) return;
+  hipStream_t st = ctx->stream;
+  MatchWorkspace& ws = ctx->match;
+  const size_t b0 = (size_t)n0 * dim * 4, b1 = (size_t)n1 * dim * 4;
+  ws.des.reserve(b0 + b1 + 16);
+  float* d0 = ws.des.as<float>();
+  float* d1 = d0 + (size_t)n0 * dim;
+  VO_HIP_CHECK(hipMemcpyAsync(d0, des0, b0, hipMemcpyHostToDevice, st));
+  if (n1) VO_HIP_CHECK(hipMemcpyAsync(d1, des1, b1, hipMemcpyHostToDevice, st));
+  ws.best.reserve((size_t)n0 * 4);
+  int32_t* d_idx2 = nullptr;
+  float* d_dist2 = nullptr;
+  if (idx2) {
+    ws.top2.reserve((size_t)n0 * 16);
+    d_idx2 = ws.top2.as<int32_t>();
+    d_dist2 = reinterpret_cast<float*>(d_idx2 + 2 * (size_t)n0);
+  }
+  match_run(ctx, d0, d1, 1, n0, n1, dim, ratio, ws.best.as<int32_t>(), d_idx2, d_dist2);
+  if (pairs) {
+    ws.pairs.reserve((size_t)n0 * 8 + 16);
+    int32_t* d_pairs = ws.pairs.as<int32_t>();
+    int32_t* d_count = d_pairs + 2 * (size_t)n0;
+    compact_pairs(ctx, ws.best.as<int32_t>(), n0, d_pairs, d_count);
+    VO_HIP_CHECK(hipMemcpyAsync(count, d_count, 4, hipMemcpyDeviceToHost, st));
+    VO_HIP_CHECK(hipStreamSynchronize(st));
+    if (*count)
+      VO_HIP_CHECK(hipMemcpyAsync(pairs, d_pairs, (size_t)*count * 8, hipMemcpyDeviceToHost, st));
+  }
+  if (idx2) {
+    VO_HIP_CHECK(hipMemcpyAsync(idx2, d_idx2, (size_t)n0 * 8, hipMemcpyDeviceToHost, st));
+    VO_HIP_CHECK(hipMemcpyAsync(dist2, d_dist2, (size_t)n0 * 8, hipMemcpyDeviceToHost, st));
+  }
+  VO_HIP_CHECK(hipStreamSynchronize(st));
+}
+
+}  // namespace
+}  // namespace vo
+
+using vo::guarded;
+
+extern "C" {
+
+int vo_abi_version(void) { return VO_ABI_VERSION; }
+
+const char* vo_last_error(void) { return vo::last_error(); }
+
+vo_ctx* vo_create(int device, int flags) {
+  (void)flags;
+  vo_ctx* out = nullptr;
+  int rc = guarded([&] {
+    int n = 0;
+    VO_HIP_CHECK(hipGetDeviceCount(&n));
+    VO_REQUIRE(device >= 0 && device < n, VO_ERR_NODEV, "vo_create: device %d not present (%d devices)",
+               device, n);
+    hipDeviceProp_t prop;
+    VO_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    VO_REQUIRE(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, VO_ERR_NODEV,
+               "vo_create: device %d is %s; this library is built for gfx950 only", device,
+               prop.gcnArchName);
+    VO_HIP_CHECK(hipSetDevice(device));
+    std::unique_ptr<vo_ctx> c(new vo_ctx);
+    c->device = device;
+    c->num_cus = prop.multiProcessorCount;
+    VO_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    out = c.release();
+  });
+  return rc == VO_OK ? out : nullptr;
+}
+
+void vo_destroy(vo_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  delete ctx;
+}
+
+void* vo_stream(vo_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int vo_synchronize(vo_ctx* ctx) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int vo_match_knn2_ratio(vo_ctx* ctx, const float* des0, int n0, const float* des1, int n1,
+                        int dim, double ratio, int32_t* out_pairs, int32_t* out_count) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(out_pairs && out_count, VO_ERR_ARG, "vo_match_knn2_ratio: null outputs");
+    vo::match_host(ctx, des0, n0, des1, n1, dim, ratio, out_pairs, out_count, nullptr, nullptr);
+  });
+}
+
+int vo_match_knn2(vo_ctx* ctx, const float* des0, int n0, const float* des1, int n1, int dim,
+                  int32_t* idx_out, float* dist_out) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(idx_out && dist_out, VO_ERR_ARG, "vo_match_knn2: null outputs");
+    vo::match_host(ctx, des0, n0, des1, n1, dim, 0.0, nullptr, nullptr, idx_out, dist_out);
+  });
+}
+
+int vo_match_batch_async(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
+                         int n0, int n1, int dim, double ratio, int32_t* d_best) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(d_best && (n0 == 0 || d_des0) && (n1 == 0 || d_des1), VO_ERR_ARG,
+               "vo_match_batch_async: null pointers");
+    vo::match_run(ctx, d_des0, d_des1, batch, n0, n1, dim, ratio, d_best, nullptr, nullptr);
+  });
+}
+
+int vo_ba_setup(vo_ctx* ctx, const vo_ba_problem* prob) {
+  return guarded([&] {
+    vo::bind(ctx);
+    vo::ba_setup(ctx, prob);
+  });
+}
+
+int vo_ba_set_state(vo_ctx* ctx, const double* poses, const double* points) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(poses && points, VO_ERR_ARG, "vo_ba_set_state: null arrays");
+    vo::ba_set_state(ctx, poses, points);
+  });
+}
+
+int vo_ba_get_state(vo_ctx* ctx, double* poses, double* points) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(poses && points, VO_ERR_ARG, "vo_ba_get_state: null arrays");
+    vo::ba_get_state(ctx, poses, points);
+  });
+}
+
+int vo_ba_run(vo_ctx* ctx, int iters, double* cost_out) {
+  int rc = VO_OK;
+  int g = guarded([&] {
+    vo::bind(ctx);
+    rc = vo::ba_run(ctx, iters, cost_out, true);
+  });
+  return g != VO_OK ? g : rc;
+}
+
+int vo_ba_run_async(vo_ctx* ctx, int iters) {
+  return guarded([&] {
+    vo::bind(ctx);
+    vo::ba_run(ctx, iters, nullptr, false);
+  });
+}
+
+int vo_ba_step_debug(vo_ctx* ctx, double* S_out, double* b_out, double* dc_out, double* cost_out) {
+  int rc = VO_OK;
+  int g = guarded([&] {
+    vo::bind(ctx);
+    rc = vo::ba_step_debug(ctx, S_out, b_out, dc_out, cost_out);
+  });
+  return g != VO_OK ? g : rc;
+}
+
+int vo_ba_solve(vo_ctx* ctx, const vo_ba_problem* prob, double* poses, double* points, int iters,
+                double* cost_out) {
+  int rc = vo_ba_setup(ctx, prob);
+  if (rc) return rc;
+  rc = vo_ba_set_state(ctx, poses, points);
+  if (rc) return rc;
+  const int run_rc = vo_ba_run(ctx, iters, cost_out);
+  if (run_rc && run_rc != VO_ERR_NOT_SPD) return run_rc;
+  rc = vo_ba_get_state(ctx, poses, points);
+  return rc ? rc : run_rc;
+}
+
+int vo_ba_plan_stats(vo_ctx* ctx, int64_t* out, int n) {
+  int k = 0;
+  int g = guarded([&] {
+    vo::bind(ctx);
+    k = vo::ba_stats(ctx, out, n);
+  });
+  return g != VO_OK ? g : k;
+}
+
+int vo_comm_unique_id(char out[128]) {
+  return guarded([&] { vo::comm_unique_id(out); });
+}
+
+int vo_comm_init(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
+  return guarded([&] {
+    vo::bind(ctx);
+    vo::comm_init(ctx, nranks, rank, id);
+  });
+}
+
+}  // extern "C"

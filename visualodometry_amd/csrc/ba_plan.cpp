@@ -1,0 +1,267 @@
+// Host-side static planner for the BA Gauss-Newton step (see ba_plan.h).
+#include "ba_plan.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <numeric>
+
+namespace vo {
+
+namespace {
+
+std::string fmt(const char* f, long a = 0, long b = 0, long c = 0) {
+  char buf[256];
+  std::snprintf(buf, sizeof buf, f, a, b, c);
+  return buf;
+}
+
+int find_or_neg(const std::vector<int32_t>& v, int32_t x) {
+  for (size_t i = 0; i < v.size(); ++i)
+    if (v[i] == x) return (int)i;
+  return -1;
+}
+
+}  // namespace
+
+int64_t BAPlan::algorithmic_bytes_per_iter() const {
+  // obs (uv f32x2 + two i32) read by linearise and back-substitute,
+  // points read twice + written once + CSR offset, poses read and written,
+  // S written and read by the solve, rhs written and read.
+  const int64_t F6 = 6ll * n_free;
+  return 2ll * n_obs * 16 + (int64_t)n_points * (2 * 24 + 24 + 4) + (int64_t)n_poses * 2 * 96 +
+         2 * F6 * F6 * 8 + F6 * 8 * 2;
+}
+
+std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_t* point_ptr,
+                       const int32_t* obs_cam, const float* obs_uv, int target_segments) {
+  P = BAPlan();
+  if (N < 1 || L < 0 || M < 0) return fmt("bad sizes n_poses=%ld n_points=%ld n_obs=%ld", N, L, M);
+  if (n_fixed < 0 || n_fixed > N) return fmt("bad n_fixed=%ld (n_poses=%ld)", n_fixed, N);
+  if (point_ptr[0] != 0 || point_ptr[L] != M) return "point_ptr must start at 0 and end at n_obs";
+  for (int p = 0; p < L; ++p)
+    if (point_ptr[p + 1] < point_ptr[p]) return fmt("point_ptr not monotone at %ld", p);
+  for (int o = 0; o < M; ++o)
+    if (obs_cam[o] < 0 || obs_cam[o] >= N) return fmt("obs_cam[%ld]=%ld out of range", o, obs_cam[o]);
+
+  P.n_poses = N;
+  P.n_points = L;
+  P.n_obs = M;
+  P.n_fixed = n_fixed;
+  P.n_free = N - n_fixed;
+
+  // landmarks ordered by first camera: keeps each workgroup's camera window narrow
+  std::vector<int32_t> first(L, N);
+  for (int p = 0; p < L; ++p)
+    for (int o = point_ptr[p]; o < point_ptr[p + 1]; ++o) first[p] = std::min(first[p], obs_cam[o]);
+  P.pt_perm.resize(L);
+  std::iota(P.pt_perm.begin(), P.pt_perm.end(), 0);
+  std::stable_sort(P.pt_perm.begin(), P.pt_perm.end(),
+                   [&](int a, int b) { return first[a] < first[b]; });
+
+  // observations grouped by (landmark, camera) -> track entries
+  P.obs_uv.reserve(2 * (size_t)M);
+  P.obs_cam.reserve(M);
+  P.obs_te.reserve(M);
+  P.pt_te.assign(1, 0);
+  std::vector<int32_t> idx;
+  for (int q = 0; q < L; ++q) {
+    const int p = P.pt_perm[q];
+    idx.resize(point_ptr[p + 1] - point_ptr[p]);
+    std::iota(idx.begin(), idx.end(), point_ptr[p]);
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return obs_cam[a] < obs_cam[b]; });
+    for (size_t k = 0; k < idx.size(); ++k) {
+      const int o = idx[k];
+      if (k == 0 || obs_cam[o] != obs_cam[idx[k - 1]]) {
+        P.te_cam.push_back(obs_cam[o]);
+        P.te_pt.push_back(q);
+        P.te_obs.push_back((int32_t)P.obs_cam.size());
+      }
+      P.obs_uv.push_back(obs_uv[2 * o]);
+      P.obs_uv.push_back(obs_uv[2 * o + 1]);
+      P.obs_cam.push_back(obs_cam[o]);
+      P.obs_te.push_back((int32_t)P.te_cam.size() - 1);
+    }
+    P.pt_te.push_back((int32_t)P.te_cam.size());
+  }
+  P.n_te = (int)P.te_cam.size();
+  P.te_obs.push_back(M);
+  P.te_lcam.assign(P.n_te, -1);
+
+  // ---- chunks and segments
+  const int nseg_target = std::max(1, target_segments);
+  const int64_t seg_obs_target = std::max<int64_t>(1, (M + nseg_target - 1) / nseg_target);
+  struct Seg {
+    int chunk0;
+    std::vector<int32_t> cams;                   // free cameras (unsorted while growing)
+    std::vector<std::pair<int32_t, int32_t>> slots;
+  };
+  std::vector<Seg> segs;
+  std::vector<int32_t> cq;
+  int c_obs = 0, c_te = 0, c_pts = 0;
+  int64_t s_obs = 0;
+  bool seg_open = false;
+  auto open_chunk = [&](int q) {
+    P.chunk_obs.push_back(P.te_obs[P.pt_te[q]]);
+    P.chunk_te.push_back(P.pt_te[q]);
+    P.chunk_pt.push_back(q);
+    c_obs = c_te = c_pts = 0;
+  };
+  for (int q = 0; q < L; ++q) {
+    const int t0 = P.pt_te[q], t1 = P.pt_te[q + 1];
+    const int nob = P.te_obs[t1] - P.te_obs[t0], nte = t1 - t0;
+    cq.clear();
+    for (int t = t0; t < t1; ++t)
+      if (P.te_cam[t] >= n_fixed) cq.push_back(P.te_cam[t] - n_fixed);
+    const int k = (int)cq.size();
+    if (nob > kChunkObs || nte > kChunkTe || k > kSegCams || k * (k + 1) / 2 > kSegSlots)
+      return fmt("landmark %ld is too wide (%ld observations, %ld free cameras); "
+                 "limits: 128 observations, 10 free cameras per landmark",
+                 P.pt_perm[q], nob, k);
+    bool chunk_fits = seg_open && c_obs + nob <= kChunkObs && c_te + nte <= kChunkTe &&
+                      c_pts + 1 <= kChunkPts;
+    bool seg_fits = seg_open;
+    if (seg_open) {
+      Seg& s = segs.back();
+      int ncams = (int)s.cams.size();
+      for (int c : cq) ncams += find_or_neg(s.cams, c) < 0;
+      int nslots = (int)s.slots.size();
+      for (int a = 0; a < k; ++a)
+        for (int b = 0; b <= a; ++b) {
+          const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
+          nslots += std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end();
+        }
+      seg_fits = ncams <= kSegCams && nslots <= kSegSlots;
+    }
+    if (!seg_fits || (!chunk_fits && s_obs >= seg_obs_target)) {
+      segs.push_back(Seg{(int)P.chunk_obs.size(), {}, {}});
+      seg_open = true;
+      s_obs = 0;
+      open_chunk(q);
+    } else if (!chunk_fits) {
+      open_chunk(q);
+    }
+    Seg& s = segs.back();
+    for (int c : cq)
+      if (find_or_neg(s.cams, c) < 0) s.cams.push_back(c);
+    for (int a = 0; a < k; ++a)
+      for (int b = 0; b <= a; ++b) {
+        const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
+        if (std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end()) s.slots.push_back(pr);
+      }
+    c_obs += nob;
+    c_te += nte;
+    c_pts += 1;
+    s_obs += nob;
+  }
+  P.chunk_obs.push_back(M);
+  P.chunk_te.push_back(P.n_te);
+  P.chunk_pt.push_back(L);
+
+  // ---- per segment: sorted windows, slab offsets, per chunk pair and camera lists
+  const int nchunks = (int)P.chunk_obs.size() - 1;
+  P.seg_chunk.assign(1, 0);
+  P.seg_slot_off.assign(1, 0);
+  P.seg_cam_off.assign(1, 0);
+  P.chunk_slot_base.assign(nchunks, 0);
+  P.chunk_cam_base.assign(nchunks, 0);
+  for (size_t si = 0; si < segs.size(); ++si) {
+    Seg& s = segs[si];
+    std::sort(s.cams.begin(), s.cams.end());
+    std::sort(s.slots.begin(), s.slots.end());
+    const int ch0 = s.chunk0;
+    const int ch1 = si + 1 < segs.size() ? segs[si + 1].chunk0 : nchunks;
+    for (auto& pr : s.slots) {
+      P.slot_i.push_back(pr.first);
+      P.slot_j.push_back(pr.second);
+    }
+    for (int c : s.cams) P.segcam_f.push_back(c);
+    P.seg_chunk.push_back(ch1);
+    P.seg_slot_off.push_back((int32_t)P.slot_i.size());
+    P.seg_cam_off.push_back((int32_t)P.segcam_f.size());
+    const int ns = (int)s.slots.size(), nc = (int)s.cams.size();
+    for (int ch = ch0; ch < ch1; ++ch) {
+      const int te0 = P.chunk_te[ch];
+      for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
+        if (P.te_cam[t] >= n_fixed) {
+          const int lc = (int)(std::lower_bound(s.cams.begin(), s.cams.end(), P.te_cam[t] - n_fixed) -
+                               s.cams.begin());
+          P.te_lcam[t] = (int16_t)lc;
+        }
+      // pair lists by slot
+      std::vector<std::vector<uint16_t>> lists(ns);
+      for (int q = P.chunk_pt[ch]; q < P.chunk_pt[ch + 1]; ++q) {
+        for (int x = P.pt_te[q]; x < P.pt_te[q + 1]; ++x) {
+          if (P.te_cam[x] < n_fixed) continue;
+          for (int y = P.pt_te[q]; y <= x; ++y) {
+            if (P.te_cam[y] < n_fixed) continue;
+            const auto pr = std::make_pair(P.te_cam[x] - n_fixed, P.te_cam[y] - n_fixed);
+            const int sl = (int)(std::lower_bound(s.slots.begin(), s.slots.end(), pr) - s.slots.begin());
+            lists[sl].push_back((uint16_t)((x - te0) | ((y - te0) << 8)));
+          }
+        }
+      }
+      P.chunk_slot_base[ch] = (int32_t)P.slot_ptr.size();
+      for (int sl = 0; sl < ns; ++sl) {
+        P.slot_ptr.push_back((int32_t)P.pair_list.size());
+        P.pair_list.insert(P.pair_list.end(), lists[sl].begin(), lists[sl].end());
+      }
+      P.slot_ptr.push_back((int32_t)P.pair_list.size());
+      // camera lists
+      std::vector<std::vector<uint8_t>> cl(nc);
+      for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
+        if (P.te_lcam[t] >= 0) cl[P.te_lcam[t]].push_back((uint8_t)(t - te0));
+      P.chunk_cam_base[ch] = (int32_t)P.cam_ptr.size();
+      for (int c = 0; c < nc; ++c) {
+        P.cam_ptr.push_back((int32_t)P.cam_list.size());
+        P.cam_list.insert(P.cam_list.end(), cl[c].begin(), cl[c].end());
+      }
+      P.cam_ptr.push_back((int32_t)P.cam_list.size());
+    }
+  }
+  if (P.pair_list.empty()) P.pair_list.push_back(0);  // keep device arrays non-empty
+  if (P.cam_list.empty()) P.cam_list.push_back(0);
+  return "";
+}
+
+std::vector<int32_t> local_profile_first(const BAPlan& P) {
+  std::vector<int32_t> first(P.n_free);
+  for (int i = 0; i < P.n_free; ++i) first[i] = i;
+  for (size_t s = 0; s < P.slot_i.size(); ++s)
+    first[P.slot_i[s]] = std::min(first[P.slot_i[s]], P.slot_j[s]);
+  return first;
+}
+
+void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
+  const int F = P.n_free;
+  P.prof_first = first;
+  P.prof_off.assign(F + 1, 0);
+  for (int i = 0; i < F; ++i) P.prof_off[i + 1] = P.prof_off[i] + (i - first[i] + 1);
+  P.prof_last.assign(F, 0);
+  for (int k = 0; k < F; ++k) P.prof_last[k] = k;
+  for (int i = 0; i < F; ++i)
+    for (int k = first[i]; k <= i; ++k) P.prof_last[k] = std::max(P.prof_last[k], i);
+  const int nb = P.prof_off[F];
+  P.prof_diag.assign(nb, 0);
+  for (int i = 0; i < F; ++i) P.prof_diag[P.prof_off[i] + (i - first[i])] = 1;
+  std::vector<std::vector<int32_t>> src(nb);
+  for (size_t s = 0; s < P.slot_i.size(); ++s)
+    src[P.prof_off[P.slot_i[s]] + (P.slot_j[s] - first[P.slot_i[s]])].push_back((int32_t)s);
+  P.prof_src_ptr.assign(1, 0);
+  P.prof_src.clear();
+  for (int b = 0; b < nb; ++b) {
+    P.prof_src.insert(P.prof_src.end(), src[b].begin(), src[b].end());
+    P.prof_src_ptr.push_back((int32_t)P.prof_src.size());
+  }
+  std::vector<std::vector<int32_t>> cb(F);
+  for (size_t e = 0; e < P.segcam_f.size(); ++e) cb[P.segcam_f[e]].push_back((int32_t)e);
+  P.camb_ptr.assign(1, 0);
+  P.camb_src.clear();
+  for (int f = 0; f < F; ++f) {
+    P.camb_src.insert(P.camb_src.end(), cb[f].begin(), cb[f].end());
+    P.camb_ptr.push_back((int32_t)P.camb_src.size());
+  }
+  if (P.prof_src.empty()) P.prof_src.push_back(0);
+  if (P.camb_src.empty()) P.camb_src.push_back(0);
+}
+
+}  // namespace vo

@@ -1,0 +1,79 @@
+// Static execution plan of the BA Gauss-Newton step (host side, built once per
+// window structure by vo_ba_setup).  See DESIGN.md §BA for the data layout.
+//
+// Terminology (domain names):
+//   track entry (te): one (landmark, camera) pair with >= 1 observation; the
+//                     observations of a landmark are grouped by camera so that
+//                     duplicate (landmark, camera) observations simply sum.
+//   chunk:            a run of whole landmarks processed together by one K1
+//                     workgroup pass (<= kChunkObs obs, <= kChunkTe te,
+//                     <= kChunkPts landmarks).
+//   segment:          the run of chunks owned by one K1 workgroup.  Its camera
+//                     window (the free cameras its landmarks see) and its
+//                     camera-pair slots (blocks (i, j), i >= j, of the reduced
+//                     camera matrix S it touches) are accumulated in LDS and
+//                     written once to the slab.
+//   slab:             per-segment partial blocks of S (36 doubles per slot),
+//                     of b (6 per window camera) and of the cost.
+//   profile:          lower block-envelope storage of S: block row i holds
+//                     block columns first[i]..i.  Cholesky preserves it.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace vo {
+
+constexpr int kChunkObs = 128;
+constexpr int kChunkTe = 128;
+constexpr int kChunkPts = 64;
+constexpr int kSegSlots = 64;
+constexpr int kSegCams = 32;
+
+struct BAPlan {
+  int n_poses = 0, n_points = 0, n_obs = 0, n_fixed = 0, n_free = 0, n_te = 0;
+  // internal order -> caller order
+  std::vector<int32_t> pt_perm;   // internal point q -> caller point index
+  // observations in internal order (points by first camera, then camera)
+  std::vector<float> obs_uv;      // 2 per obs
+  std::vector<int32_t> obs_cam, obs_te;
+  // track entries
+  std::vector<int32_t> te_cam, te_pt, te_obs;  // te_obs: n_te+1
+  std::vector<int16_t> te_lcam;                // segment-local free camera, -1 if fixed
+  std::vector<int32_t> pt_te;                  // n_points+1
+  // chunks
+  std::vector<int32_t> chunk_obs, chunk_te, chunk_pt;  // n_chunks+1
+  std::vector<int32_t> chunk_slot_base, chunk_cam_base;  // index into slot_ptr / cam_ptr
+  std::vector<int32_t> slot_ptr;   // per chunk: nslots(seg)+1 offsets into pair_list
+  std::vector<uint16_t> pair_list; // (te_x_local | te_y_local << 8)
+  std::vector<int32_t> cam_ptr;    // per chunk: ncams(seg)+1 offsets into cam_list
+  std::vector<uint8_t> cam_list;   // te local index
+  // segments
+  std::vector<int32_t> seg_chunk, seg_slot_off, seg_cam_off;  // n_seg+1
+  std::vector<int32_t> slot_i, slot_j;   // per slab slot: global free-camera block (i >= j)
+  std::vector<int32_t> segcam_f;         // per slab b entry: free camera
+  // profile of S (block rows over free cameras)
+  std::vector<int32_t> prof_first, prof_off, prof_last;  // F, F+1, F
+  std::vector<int32_t> prof_src_ptr, prof_src;  // per profile block: slab slots
+  std::vector<uint8_t> prof_diag;               // per profile block: 1 if i == j
+  std::vector<int32_t> camb_ptr, camb_src;      // per free camera: slab b entries
+
+  int n_chunks() const { return (int)chunk_obs.size() - 1; }
+  int n_segments() const { return (int)seg_chunk.size() - 1; }
+  int n_slab_slots() const { return (int)slot_i.size(); }
+  int n_prof_blocks() const { return prof_off.empty() ? 0 : prof_off.back(); }
+  int64_t algorithmic_bytes_per_iter() const;
+};
+
+// Builds everything except the profile (needs the global first[] on multi-GPU).
+// Returns an empty string on success, else the error message.
+std::string build_plan(BAPlan& plan, int n_poses, int n_points, int n_obs, int n_fixed,
+                       const int32_t* point_ptr, const int32_t* obs_cam, const float* obs_uv,
+                       int target_segments);
+// first[i] of each free block row touched by this plan (i if untouched).
+std::vector<int32_t> local_profile_first(const BAPlan& plan);
+// Builds the profile and the K2 reduction index from a (possibly all-reduced) first[].
+void build_profile(BAPlan& plan, const std::vector<int32_t>& first);
+
+}  // namespace vo

@@ -1,0 +1,503 @@
+// Brute-force descriptor matcher: knn k=2 + Lowe ratio test on gfx950.
+//
+// Replaces cv2.BFMatcher(cv2.NORM_L2, crossCheck=False).knnMatch(k=2) and the
+// Python ratio loop of FeatureFrontend.match_frames (reference
+// src/modules/frontend.py:86-111).  Semantics:
+//   dist(i,j) = sqrtf(d2(i,j)); the two nearest train rows per query are the two
+//   smallest keys (dist, j) (equal distances keep the lower j -- OpenCV's
+//   insertion scan with strict '<'); keep (i, j1) iff (double)dist1 < ratio *
+//   (double)dist2.
+//
+// Integer path (all values integers in [0,255], as OpenCV SIFT produces): the
+// descriptors are shifted to int8 (a - 128) -- d2 is shift invariant -- and
+// d2 = |a'|^2 + |b'|^2 - 2 a'.b' is computed EXACTLY with
+// v_mfma_i32_16x16x64_i8 (i32 accumulate).  The per-pair epilogue packs
+// (d2 - |a'|^2 + Dp*2^14, column tile) into one u32 so that the running top-2 per
+// (row, lane) is two branch-free ops: m2 = med3(m1, m2, p); m1 = min(m1, p).
+// sqrtf can merge two integer d2 values only when they differ by 1 and are
+// >= 2^22; rows whose second-best d2 reaches 2^22 are re-scanned exactly with
+// sqrt-domain keys (never the case for real SIFT, whose d2 stays below ~1.1e6).
+//
+// Float path (any other values, e.g. SuperPoint): d2 is the k-ordered fmaf
+// chain sum((a_k - b_k)^2) in fp32 and keys are (sqrtf(d2), j) directly.
+#include "vo_ctx.h"
+
+namespace vo {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+constexpr int kKStep = 64;          // K of v_mfma_i32_16x16x64_i8
+constexpr int kMaxDpInt = 256;      // int path keeps A fragments in registers
+constexpr int kRowsPerWave = 64;    // 4 M-tiles of 16 rows
+constexpr int kRowsPerWG = 256;     // 4 waves
+// Key offset: |a'|^2 <= Dp * 128^2 = Dp << 14, so d2 - |a'|^2 + (Dp << 14) >= 0; and
+// d2 - |a'|^2 = sum(b'^2 - 2 a'b') <= Dp * 48896, so the key stays below
+// Dp * 65280 < 2^24 for Dp <= 256: 24 key bits + 8 column-tile bits.
+__host__ __device__ constexpr int norm_off(int Dp) { return Dp << 14; }
+constexpr uint32_t kSent = 0xFFFFFFFFu;
+constexpr int kCollide = 1 << 22;   // sqrtf(n) == sqrtf(n+1) needs n >= 2^22
+constexpr int kFloatTile = 64;      // float path: 64 x 64 pair tile per WG
+constexpr int kFloatKC = 32;        // float path k-chunk staged in LDS
+
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Correctly rounded sqrtf: the f64 sqrt expansion is correctly rounded and
+// 53 >= 2*24 + 2 makes the f64 -> f32 double rounding innocuous.
+__device__ __forceinline__ float sqrtf_rn(float x) { return (float)sqrt((double)x); }
+
+__device__ __forceinline__ uint64_t key64(uint32_t d, uint32_t j) {
+  return ((uint64_t)d << 32) | j;
+}
+
+__device__ __forceinline__ void merge2(uint64_t& a1, uint64_t& a2, uint64_t b1, uint64_t b2) {
+  const uint64_t lo = a1 < b1 ? a1 : b1;
+  const uint64_t hi = a1 < b1 ? b1 : a1;
+  const uint64_t m = a2 < b2 ? a2 : b2;
+  a1 = lo;
+  a2 = hi < m ? hi : m;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = __shfl_xor((uint32_t)v, m, 64);
+  const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// ---- packing: f32 -> int8 (a - 128), squared norms, u8-valued check --------
+// 16 threads per row, each moving 4 consecutive elements per step (coalesced).
+__global__ __launch_bounds__(256) void pack_kernel(
+    const float* __restrict__ des, int n, int dim, int Dp, int n_pad,
+    long in_bstride, long q_bstride, int8_t* __restrict__ q8, int* __restrict__ norms,
+    uint32_t* __restrict__ colconst, int* __restrict__ flag) {
+  const int off = norm_off(Dp);
+  const int b = blockIdx.y;
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int sub = threadIdx.x & 15;
+  if (row >= n_pad) return;
+  const float* src = des + b * in_bstride + (long)row * dim;
+  int8_t* dst = q8 + b * q_bstride + (long)row * Dp;
+  int acc = 0;
+  bool bad = false;
+  for (int e = sub * 4; e < Dp; e += 64) {
+    int q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      q[u] = 0;
+      if (row < n && e + u < dim) {
+        const float v = src[e + u];
+        const bool ok = (v == rintf(v)) && v >= 0.0f && v <= 255.0f;
+        bad |= !ok;
+        q[u] = ok ? (int)v - 128 : 0;
+      }
+      acc += q[u] * q[u];
+    }
+    const uint32_t packed = (uint32_t)(q[0] & 255) | ((uint32_t)(q[1] & 255) << 8) |
+                            ((uint32_t)(q[2] & 255) << 16) | ((uint32_t)(q[3] & 255) << 24);
+    *reinterpret_cast<uint32_t*>(dst + e) = packed;
+  }
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) acc += __shfl_xor(acc, m, 64);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+  if (sub == 0) {
+    norms[b * (long)n_pad + row] = acc;
+    if (colconst) {
+      colconst[b * (long)n_pad + row] =
+          row < n ? (((uint32_t)(acc + off)) << 8) | ((uint32_t)(row >> 4) & 255u) : kSent;
+    }
+  }
+}
+
+// ---- int8 MFMA sweep --------------------------------------------------------
+// WG = 4 waves x 64 query rows; each WG sweeps the train columns of one split
+// (split width w | 4096, so a split never straddles a 4096-column block and the
+// 8-bit column-tile tag in the packed key is monotone in j inside a split).
+template <int KS>
+__global__ __launch_bounds__(256) void match_i8_kernel(
+    const int8_t* __restrict__ qa, const int8_t* __restrict__ qb,
+    const uint32_t* __restrict__ colconst, const int* __restrict__ norma, int n0_pad,
+    int n1_pad, int split_w, long qa_bstride, long qb_bstride, uint4* __restrict__ partial,
+    const int* __restrict__ flag) {
+  if (*flag) return;  // not u8-valued: the float path owns this call
+  constexpr int Dp = KS * kKStep;
+  constexpr int kOff = norm_off(Dp);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int b = blockIdx.z;
+  const int split = blockIdx.y;
+  const int nsplit = gridDim.y;
+  const int rowbase = blockIdx.x * kRowsPerWG + wave * kRowsPerWave;
+  const int8_t* A = qa + b * qa_bstride;
+  const int8_t* B = qb + b * qb_bstride;
+  const uint32_t* cc = colconst + b * (long)n1_pad;
+
+  v4i afrag[4][KS];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      afrag[mt][ks] = *reinterpret_cast<const v4i*>(
+          A + (long)(rowbase + mt * 16 + (lane & 15)) * Dp + ks * kKStep + 16 * (lane >> 4));
+
+  uint32_t m1[4][4], m2[4][4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m1[mt][r] = m2[mt][r] = kSent;
+
+  const int c0 = split * split_w;
+  const int c1 = min(c0 + split_w, n1_pad);
+  const int8_t* bp = B + (long)(c0 + (lane & 15)) * Dp + 16 * (lane >> 4);
+  v4i bnext[KS];
+  uint32_t ccnext = 0;
+  if (c0 < c1) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) bnext[ks] = *reinterpret_cast<const v4i*>(bp + ks * kKStep);
+    ccnext = cc[c0 + (lane & 15)];
+  }
+  for (int c = c0; c < c1; c += 16) {
+    v4i bfrag[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) bfrag[ks] = bnext[ks];
+    const uint32_t ccol = ccnext;
+    if (c + 16 < c1) {
+      bp += 16 * Dp;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) bnext[ks] = *reinterpret_cast<const v4i*>(bp + ks * kKStep);
+      ccnext = cc[c + 16 + (lane & 15)];
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      v4i acc = {0, 0, 0, 0};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], bfrag[ks], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t p = ccol - ((uint32_t)acc[r] << 9);
+        m2[mt][r] = med3_u32(m1[mt][r], m2[mt][r], p);
+        m1[mt][r] = min(m1[mt][r], p);
+      }
+    }
+  }
+
+  // unpack to (d2, j) keys and merge the 16 lanes that share each row
+  const int jblock = c0 & ~4095;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = rowbase + mt * 16 + (lane >> 4) * 4 + r;
+      const int na = norma[b * (long)n0_pad + row];
+      uint64_t k1 = ~0ull, k2 = ~0ull;
+      if (m1[mt][r] != kSent) {
+        const uint32_t d = (m1[mt][r] >> 8) - kOff + na;
+        k1 = key64(d, jblock + 16 * (m1[mt][r] & 255u) + (lane & 15));
+      }
+      if (m2[mt][r] != kSent) {
+        const uint32_t d = (m2[mt][r] >> 8) - kOff + na;
+        k2 = key64(d, jblock + 16 * (m2[mt][r] & 255u) + (lane & 15));
+      }
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) merge2(k1, k2, shfl_xor64(k1, m), shfl_xor64(k2, m));
+      if ((lane & 15) == 0) {
+        partial[((long)b * nsplit + split) * n0_pad + row] =
+            make_uint4((uint32_t)(k1 >> 32), (uint32_t)k1, (uint32_t)(k2 >> 32), (uint32_t)k2);
+      }
+    }
+  }
+}
+
+// ---- fp32 path ---------------------------------------------------------------
+// WG tile: 64 query rows x the split's columns in 64-column tiles; thread
+// (ty, tx) owns rows 4ty..4ty+3 and columns tx + 16c.  Each pair's d2 is the
+// fmaf chain over k in ascending order.  Per thread the columns arrive in
+// ascending j, so a candidate can only enter the top-2 if d2 < d2(second):
+// sqrtf is evaluated only then (exact filter, see header).
+__global__ __launch_bounds__(256) void match_f32_kernel(
+    const float* __restrict__ da, const float* __restrict__ db, int n0, int n1, int dim,
+    int n0_pad, int split_w, long a_bstride, long b_bstride, uint4* __restrict__ partial,
+    const int* __restrict__ flag) {
+  if (!*flag) return;  // u8-valued: the int8 path owns this call
+  __shared__ float sa[kFloatKC][kFloatTile + 1];
+  __shared__ float sb[kFloatKC][kFloatTile + 1];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int b = blockIdx.z, split = blockIdx.y, nsplit = gridDim.y;
+  const int rowbase = blockIdx.x * kFloatTile;
+  const float* A = da + b * a_bstride;
+  const float* B = db + b * b_bstride;
+
+  float s1[4], s2[4], d1st[4], d2nd[4];
+  int j1[4], j2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s1[i] = s2[i] = d1st[i] = d2nd[i] = __builtin_huge_valf();
+    j1[i] = j2[i] = -1;
+  }
+  const int c0 = split * split_w;
+  const int c1 = min(c0 + split_w, n1);
+  for (int ct = c0; ct < c1; ct += kFloatTile) {
+    float acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[i][c] = 0.0f;
+    for (int k0 = 0; k0 < dim; k0 += kFloatKC) {
+      __syncthreads();
+      for (int e = threadIdx.x; e < kFloatKC * kFloatTile; e += 256) {
+        const int rr = e / kFloatKC, kk = e % kFloatKC;
+        const int ga = rowbase + rr, gb = ct + rr, gk = k0 + kk;
+        sa[kk][rr] = (ga < n0 && gk < dim) ? A[(long)ga * dim + gk] : 0.0f;
+        sb[kk][rr] = (gb < n1 && gk < dim) ? B[(long)gb * dim + gk] : 0.0f;
+      }
+      __syncthreads();
+      const int kc = min(kFloatKC, dim - k0);
+      for (int kk = 0; kk < kc; ++kk) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = sa[kk][ty * 4 + i];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bv[c] = sb[kk][tx + 16 * c];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float df = av[i] - bv[c];
+            acc[i][c] = __builtin_fmaf(df, df, acc[i][c]);
+          }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int j = ct + tx + 16 * c;
+      if (j >= c1) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d = acc[i][c];
+        if (d < d2nd[i]) {  // d2 >= d2(second) implies s >= s2: cannot enter
+          const float s = sqrtf_rn(d);
+          if (s < s1[i]) {
+            s2[i] = s1[i]; j2[i] = j1[i]; d2nd[i] = d1st[i];
+            s1[i] = s; j1[i] = j; d1st[i] = d;
+          } else if (s < s2[i]) {
+            s2[i] = s; j2[i] = j; d2nd[i] = d;
+          }
+        }
+      }
+    }
+  }
+  // merge across the 16 tx lanes of each row (keys: float bits of s, j)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint64_t k1 = j1[i] < 0 ? ~0ull : key64(__float_as_uint(s1[i]), (uint32_t)j1[i]);
+    uint64_t k2 = j2[i] < 0 ? ~0ull : key64(__float_as_uint(s2[i]), (uint32_t)j2[i]);
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) merge2(k1, k2, shfl_xor64(k1, m), shfl_xor64(k2, m));
+    const int row = rowbase + ty * 4 + i;
+    if (tx == 0 && row < n0_pad) {
+      partial[((long)b * nsplit + split) * n0_pad + row] =
+          make_uint4((uint32_t)(k1 >> 32), (uint32_t)k1, (uint32_t)(k2 >> 32), (uint32_t)k2);
+    }
+  }
+}
+
+// ---- merge splits, exact near-tie rescan, ratio test ---------------------------
+// One wave per (batch, query row).
+__global__ __launch_bounds__(64) void merge_ratio_kernel(
+    const uint4* __restrict__ partial, int nsplit, int n0, int n0_pad, int n1, int n1_pad,
+    int Dp, const int8_t* __restrict__ qa, const int8_t* __restrict__ qb, long qa_bstride,
+    long qb_bstride, const int* __restrict__ flag, double ratio, int32_t* __restrict__ best,
+    int32_t* __restrict__ idx2, float* __restrict__ dist2) {
+  const int row = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+  const bool fpath = *flag != 0;
+  uint64_t k1 = ~0ull, k2 = ~0ull;
+  for (int s = lane; s < nsplit; s += 64) {
+    const uint4 p = partial[((long)b * nsplit + s) * n0_pad + row];
+    merge2(k1, k2, key64(p.x, p.y), key64(p.z, p.w));
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) merge2(k1, k2, shfl_xor64(k1, m), shfl_xor64(k2, m));
+
+  float s1 = __builtin_huge_valf(), s2 = __builtin_huge_valf();
+  if (!fpath) {
+    // (d2, j) order equals (sqrtf(d2), j) order unless sqrtf merges two
+    // consecutive integers, which needs d2 >= 2^22 (see header).
+    const bool rescan = k2 != ~0ull && (uint32_t)(k2 >> 32) >= (uint32_t)kCollide;
+    if (rescan) {
+      const int8_t* a = qa + b * qa_bstride + (long)row * Dp;
+      const int8_t* bb = qb + b * qb_bstride;
+      uint64_t r1 = ~0ull, r2 = ~0ull;
+      for (int j = lane; j < n1; j += 64) {
+        int d = 0;
+        for (int e = 0; e < Dp; ++e) {
+          const int df = (int)a[e] - (int)bb[(long)j * Dp + e];
+          d += df * df;
+        }
+        const uint64_t kk = key64(__float_as_uint(sqrtf_rn((float)d)), (uint32_t)j);
+        merge2(r1, r2, kk, ~0ull);
+      }
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) merge2(r1, r2, shfl_xor64(r1, m), shfl_xor64(r2, m));
+      k1 = r1;
+      k2 = r2;
+      if (k1 != ~0ull) s1 = __uint_as_float((uint32_t)(k1 >> 32));
+      if (k2 != ~0ull) s2 = __uint_as_float((uint32_t)(k2 >> 32));
+    } else {
+      if (k1 != ~0ull) s1 = sqrtf_rn((float)(uint32_t)(k1 >> 32));
+      if (k2 != ~0ull) s2 = sqrtf_rn((float)(uint32_t)(k2 >> 32));
+    }
+  } else {
+    if (k1 != ~0ull) s1 = __uint_as_float((uint32_t)(k1 >> 32));
+    if (k2 != ~0ull) s2 = __uint_as_float((uint32_t)(k2 >> 32));
+  }
+  if (lane == 0) {
+    const int j1 = k1 == ~0ull ? -1 : (int)(uint32_t)k1;
+    const int j2 = k2 == ~0ull ? -1 : (int)(uint32_t)k2;
+    const long o = (long)b * n0 + row;
+    if (best) best[o] = (j2 >= 0 && (double)s1 < ratio * (double)s2) ? j1 : -1;
+    if (idx2) {
+      idx2[2 * o] = j1;
+      idx2[2 * o + 1] = j2;
+      dist2[2 * o] = j1 >= 0 ? s1 : 3.402823466e+38f;
+      dist2[2 * o + 1] = j2 >= 0 ? s2 : 3.402823466e+38f;
+    }
+  }
+}
+
+// ---- stream compaction of best[] into ascending (query, train) pairs ---------
+__global__ __launch_bounds__(1024) void compact_kernel(const int32_t* __restrict__ best,
+                                                       int n0, int32_t* __restrict__ pairs,
+                                                       int32_t* __restrict__ count) {
+  __shared__ int wsum[16];
+  __shared__ int base;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int start = 0; start < n0; start += 1024) {
+    const int i = start + threadIdx.x;
+    const int v = i < n0 ? best[i] : -1;
+    const unsigned long long mask = __ballot(v >= 0);
+    const int pre = __popcll(mask & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wave] = __popcll(mask);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wave; ++w) off += wsum[w];
+    if (v >= 0) {
+      pairs[2 * (off + pre)] = i;
+      pairs[2 * (off + pre) + 1] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int w = 0; w < 16; ++w) t += wsum[w];
+      base += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *count = base;
+}
+
+int pow2_floor(int x) {
+  int p = 1;
+  while (p * 2 <= x) p *= 2;
+  return p;
+}
+
+}  // namespace
+
+void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch, int n0,
+               int n1, int dim, double ratio, int32_t* d_best, int32_t* d_idx2,
+               float* d_dist2) {
+  VO_REQUIRE(batch >= 1 && n0 >= 0 && n1 >= 0 && dim >= 1, VO_ERR_ARG,
+             "match: bad shape batch=%d n0=%d n1=%d dim=%d", batch, n0, n1, dim);
+  if (n0 == 0) return;
+  hipStream_t st = ctx->stream;
+  MatchWorkspace& ws = ctx->match;
+  const int Dp = ceil_div(dim, kKStep) * kKStep;
+  const bool int_ok = Dp <= kMaxDpInt;
+  const int n0_pad = ceil_div(n0, kRowsPerWG) * kRowsPerWG;
+  const int n1_pad = ceil_div(std::max(n1, 1), 16) * 16;
+
+  // split the train columns so the grid fills the chip (w | 4096, w >= 64)
+  const int row_wgs = n0_pad / kRowsPerWG;
+  const int want = std::max(1, ceil_div(2 * ctx->num_cus, (int64_t)row_wgs * batch));
+  int w = pow2_floor(std::max(1, n1_pad / want));
+  w = std::max(256, std::min(4096, w));
+  const int nsplit = std::max(1, ceil_div(n1_pad, w));
+
+  ws.flag.reserve(sizeof(int));
+  ws.partial.reserve((size_t)batch * nsplit * n0_pad * sizeof(uint4));
+  int* flag = ws.flag.as<int>();
+  VO_HIP_CHECK(hipMemsetAsync(flag, int_ok ? 0 : 1, sizeof(int), st));
+
+  const long qa_bs = (long)n0_pad * Dp, qb_bs = (long)n1_pad * Dp;
+  int8_t* qa = nullptr;
+  int8_t* qb = nullptr;
+  if (int_ok) {
+    ws.q8.reserve((size_t)batch * (qa_bs + qb_bs));
+    ws.norms.reserve((size_t)batch * (n0_pad + n1_pad) * sizeof(int));
+    ws.colconst.reserve((size_t)batch * n1_pad * sizeof(uint32_t));
+    qa = ws.q8.as<int8_t>();
+    qb = qa + batch * qa_bs;
+    int* na = ws.norms.as<int>();
+    int* nb = na + (size_t)batch * n0_pad;
+    dim3 ga(ceil_div((int64_t)n0_pad * 16, 256), batch), gb(ceil_div((int64_t)n1_pad * 16, 256), batch);
+    hipLaunchKernelGGL(pack_kernel, ga, dim3(256), 0, st, d_des0, n0, dim, Dp, n0_pad,
+                       (long)n0 * dim, qa_bs, qa, na, (uint32_t*)nullptr, flag);
+    if (n1 > 0)
+      hipLaunchKernelGGL(pack_kernel, gb, dim3(256), 0, st, d_des1, n1, dim, Dp, n1_pad,
+                         (long)n1 * dim, qb_bs, qb, nb, ws.colconst.as<uint32_t>(), flag);
+    if (n1 > 0) {
+      dim3 grid(row_wgs, nsplit, batch);
+      uint4* part = ws.partial.as<uint4>();
+      switch (Dp / kKStep) {
+        case 1:
+          hipLaunchKernelGGL(match_i8_kernel<1>, grid, dim3(256), 0, st, qa, qb,
+                             ws.colconst.as<uint32_t>(), na, n0_pad, n1_pad, w, qa_bs, qb_bs,
+                             part, flag);
+          break;
+        case 2:
+          hipLaunchKernelGGL(match_i8_kernel<2>, grid, dim3(256), 0, st, qa, qb,
+                             ws.colconst.as<uint32_t>(), na, n0_pad, n1_pad, w, qa_bs, qb_bs,
+                             part, flag);
+          break;
+        case 3:
+          hipLaunchKernelGGL(match_i8_kernel<3>, grid, dim3(256), 0, st, qa, qb,
+                             ws.colconst.as<uint32_t>(), na, n0_pad, n1_pad, w, qa_bs, qb_bs,
+                             part, flag);
+          break;
+        default:
+          hipLaunchKernelGGL(match_i8_kernel<4>, grid, dim3(256), 0, st, qa, qb,
+                             ws.colconst.as<uint32_t>(), na, n0_pad, n1_pad, w, qa_bs, qb_bs,
+                             part, flag);
+          break;
+      }
+    }
+  }
+  if (n1 > 0) {
+    dim3 grid(ceil_div(n0, kFloatTile), nsplit, batch);
+    hipLaunchKernelGGL(match_f32_kernel, grid, dim3(256), 0, st, d_des0, d_des1, n0, n1, dim,
+                       n0_pad, w, (long)n0 * dim, (long)n1 * dim, ws.partial.as<uint4>(), flag);
+  } else {
+    // no train rows: every query has no neighbour
+    VO_HIP_CHECK(hipMemsetAsync(ws.partial.ptr, 0xFF,
+                                (size_t)batch * nsplit * n0_pad * sizeof(uint4), st));
+  }
+  hipLaunchKernelGGL(merge_ratio_kernel, dim3(n0, batch), dim3(64), 0, st,
+                     ws.partial.as<uint4>(), n1 > 0 ? nsplit : 1, n0, n0_pad, n1, n1_pad, Dp,
+                     qa, qb, qa_bs, qb_bs, flag, ratio, d_best, d_idx2, d_dist2);
+  VO_HIP_CHECK(hipGetLastError());
+}
+
+void compact_pairs(vo_ctx* ctx, const int32_t* d_best, int n0, int32_t* d_pairs,
+                   int32_t* d_count) {
+  hipLaunchKernelGGL(compact_kernel, dim3(1), dim3(1024), 0, ctx->stream, d_best, n0,
+                     d_pairs, d_count);
+  VO_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace vo

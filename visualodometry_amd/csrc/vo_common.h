@@ -1,0 +1,80 @@
+// Shared helpers for the vo_hip library (gfx950 only; no CUDA/HIP dual paths).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/vo_hip.h"
+
+namespace vo {
+
+// Thread-local last-error message returned by vo_last_error().
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+const char* last_error();
+
+struct Error {
+  int code;
+};
+
+#define VO_HIP_CHECK(expr)                                                        \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess) {                                                       \
+      ::vo::set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #expr,          \
+                      hipGetErrorString(e_));                                     \
+      throw ::vo::Error{e_ == hipErrorOutOfMemory ? VO_ERR_NOMEM : VO_ERR_HIP};   \
+    }                                                                             \
+  } while (0)
+
+#define VO_REQUIRE(cond, code, ...)   \
+  do {                                \
+    if (!(cond)) {                    \
+      ::vo::set_error(__VA_ARGS__);   \
+      throw ::vo::Error{code};        \
+    }                                 \
+  } while (0)
+
+// Device buffer that grows on demand and is freed with its owner.
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  void reserve(size_t n) {
+    if (n <= bytes) return;
+    if (ptr) VO_HIP_CHECK(hipFree(ptr));
+    ptr = nullptr;
+    bytes = 0;
+    VO_HIP_CHECK(hipMalloc(&ptr, n ? n : 16));
+    bytes = n;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(ptr);
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+  ~DevBuf() { release(); }
+};
+
+inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// Runs `fn`, converting vo::Error into the status code (message already set).
+template <class F>
+int guarded(F&& fn) {
+  try {
+    fn();
+    return VO_OK;
+  } catch (const Error& e) {
+    return e.code;
+  } catch (const std::exception& e) {
+    set_error("internal error: %s", e.what());
+    return VO_ERR_HIP;
+  }
+}
+
+}  // namespace vo

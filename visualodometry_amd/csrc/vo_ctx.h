@@ -1,0 +1,45 @@
+// vo_ctx: one HIP device + stream, the matcher workspace and the BA engine.
+#pragma once
+
+#include <memory>
+
+#include "vo_common.h"
+
+namespace vo {
+
+struct MatchWorkspace {
+  DevBuf des;       // staging for host descriptors (des0 then des1)
+  DevBuf q8;        // packed int8 (a - 128) descriptors, query then train
+  DevBuf norms;     // int32 squared norms of the packed rows
+  DevBuf colconst;  // uint32 per train column (see match.hip)
+  DevBuf partial;   // per (split, row) top-2 partials
+  DevBuf best;      // int32 (batch, n0) best train index or -1
+  DevBuf top2;      // int32 (n0, 2) + float (n0, 2)
+  DevBuf pairs;     // int32 (n0, 2) compacted pairs + count
+  DevBuf flag;      // int32 "descriptors are not 0..255 integers"
+};
+
+class BAEngine;   // ba.hip
+struct Comm;      // ba.hip (RCCL communicator)
+
+}  // namespace vo
+
+struct vo_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int num_cus = 0;
+  vo::MatchWorkspace match;
+  std::unique_ptr<vo::BAEngine> ba;
+  std::unique_ptr<vo::Comm> comm;
+  vo_ctx();
+  ~vo_ctx();
+};
+
+namespace vo {
+// Matcher entry points (match.hip).
+void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch, int n0,
+               int n1, int dim, double ratio, int32_t* d_best, int32_t* d_idx2,
+               float* d_dist2);
+void compact_pairs(vo_ctx* ctx, const int32_t* d_best, int n0, int32_t* d_pairs,
+                   int32_t* d_count);
+}  // namespace vo

@@ -1,0 +1,105 @@
+"""Brute-force descriptor matching on MI355X (knn k=2 + Lowe ratio test).
+
+Drop-in for the SIFT branch of ``FeatureFrontend.match_frames``
+(reference ``src/modules/frontend.py:86-111``): the reference calls
+``cv2.BFMatcher(cv2.NORM_L2, crossCheck=False).knnMatch(des0, des1, k=2)``
+(``:34``, ``:101``) and keeps ``[m.queryIdx, m.trainIdx]`` when
+``m.distance < 0.75 * n.distance`` (``:103-109``).  Here both steps run in
+``libvo_hip.so`` (``vo_match_knn2_ratio``); see DESIGN.md §Matcher for the
+exact semantics and the one documented divergence (no pair passing the test
+returns shape ``(0, 2)``, not the reference's ``(0,)``).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from ._lib import C, check, ptr
+
+RATIO_THRESH = 0.75  # frontend.py:104
+
+
+def _as_des(d) -> np.ndarray:
+    if hasattr(d, "detach"):  # torch tensor, possibly on the GPU (frontend.py:92-95)
+        d = d.detach().cpu().numpy()
+    d = np.asarray(d)
+    if d.ndim == 3 and d.shape[0] == 1:  # (1, N, D) feature-dict layout (frontend.py:71)
+        d = d[0]
+    if d.ndim != 2:
+        raise ValueError(f"descriptors must be (N, D), got shape {d.shape}")
+    return np.ascontiguousarray(d, dtype=np.float32)
+
+
+def match_knn2_ratio(des0, des1, ratio: float = RATIO_THRESH, ctx: _lib.Context | None = None) -> np.ndarray:
+    """Ratio-test matches as an ``int64`` array ``(M, 2)`` of (query, train), ascending query."""
+    a, b = _as_des(des0), _as_des(des1)
+    if a.shape[0] == 0 or b.shape[0] == 0:  # frontend.py:97-98
+        return np.empty((0, 2), dtype=np.int64)
+    if a.shape[1] != b.shape[1]:
+        raise ValueError(f"descriptor dims differ: {a.shape[1]} vs {b.shape[1]}")
+    ctx = ctx or _lib.context()
+    out = np.empty((a.shape[0], 2), dtype=np.int32)
+    cnt = np.zeros(1, dtype=np.int32)
+    check(
+        ctx.lib.vo_match_knn2_ratio(
+            ctx.handle, ptr(a, C.c_float), a.shape[0], ptr(b, C.c_float), b.shape[0], a.shape[1],
+            float(ratio), ptr(out, C.c_int32), ptr(cnt, C.c_int32),
+        ),
+        "vo_match_knn2_ratio",
+    )
+    return out[: int(cnt[0])].astype(np.int64)
+
+
+def match_knn2(des0, des1, ctx: _lib.Context | None = None):
+    """knnMatch(k=2) alone: ``idx (n0, 2) int32`` (-1 = none), ``dist (n0, 2) float32``."""
+    a, b = _as_des(des0), _as_des(des1)
+    n0 = a.shape[0]
+    idx = np.full((n0, 2), -1, dtype=np.int32)
+    dist = np.full((n0, 2), np.finfo(np.float32).max, dtype=np.float32)
+    if n0 == 0:
+        return idx, dist
+    if b.shape[0] and a.shape[1] != b.shape[1]:
+        raise ValueError(f"descriptor dims differ: {a.shape[1]} vs {b.shape[1]}")
+    ctx = ctx or _lib.context()
+    check(
+        ctx.lib.vo_match_knn2(
+            ctx.handle, ptr(a, C.c_float), n0, ptr(b, C.c_float), b.shape[0], a.shape[1],
+            ptr(idx, C.c_int32), ptr(dist, C.c_float),
+        ),
+        "vo_match_knn2",
+    )
+    return idx, dist
+
+
+def match_batch_device(des0, des1, ratio: float = RATIO_THRESH, out=None, ctx: _lib.Context | None = None):
+    """Batched frame pairs on device memory (torch tensors used as plumbing only).
+
+    ``des0`` (B, n0, D) and ``des1`` (B, n1, D) float32 CUDA tensors; returns the
+    (B, n0) int32 tensor of kept train indices (-1 = rejected).  Enqueued on the
+    library stream; the caller synchronises (``synchronize``).
+    """
+    import torch
+
+    if des0.dim() != 3 or des1.dim() != 3 or des0.shape[0] != des1.shape[0] or des0.shape[2] != des1.shape[2]:
+        raise ValueError("expected (B, n0, D) and (B, n1, D)")
+    if des0.dtype != torch.float32 or des1.dtype != torch.float32 or not des0.is_cuda:
+        raise ValueError("expected float32 device tensors")
+    des0, des1 = des0.contiguous(), des1.contiguous()
+    B, n0, D = des0.shape
+    if out is None:
+        out = torch.empty((B, n0), dtype=torch.int32, device=des0.device)
+    ctx = ctx or _lib.context(des0.device.index or 0)
+    check(
+        ctx.lib.vo_match_batch_async(
+            ctx.handle, C.c_void_p(des0.data_ptr()), C.c_void_p(des1.data_ptr()), B, n0,
+            des1.shape[1], D, float(ratio), C.c_void_p(out.data_ptr()),
+        ),
+        "vo_match_batch_async",
+    )
+    return out
+
+
+def synchronize(ctx: _lib.Context | None = None) -> None:
+    ctx = ctx or _lib.context()
+    check(ctx.lib.vo_synchronize(ctx.handle), "vo_synchronize")

@@ -1,0 +1,236 @@
+"""Seeded synthetic inputs for the matcher and the sliding-window BA.
+
+The reference ships no fixtures or data, so every workload
+in tests and bench.py is generated here from a fixed seed, following the
+generator spec of SURVEY.md §8(d):
+
+* BA: KITTI intrinsics (``src/modules/dataset_loader.py:52-54``), a forward
+  trajectory of 1 m per pose with a yaw random walk, landmarks drawn in the
+  frustum of their first camera at depth U[5, 50] m, contiguous tracks of
+  U{2..8} poses clipped to visibility, 1 px pixel noise, and an initial guess
+  perturbed by 0.01 rad / 0.05 m per pose and 2 % of depth per point.
+* Matcher: SIFT-like descriptors (integers 0..255 stored as float32, the
+  layout ``FeatureFrontend.process_image`` produces at
+  ``src/modules/frontend.py:59-67``) and SuperPoint-like L2-normalised
+  float32 descriptors.
+
+Pose convention: ``T_cw`` (world -> camera), as the reference projects with
+``T_cw = inv(T_wc)`` (``src/modules/vo.py:260-261``).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+KITTI_K = np.array(
+    [[718.856, 0.0, 607.1928], [0.0, 718.856, 185.2157], [0.0, 0.0, 1.0]]
+)
+KITTI_WH = (1241, 376)
+
+# (n_poses, n_points, seed) of the BASELINE.json BA configs
+BA_CONFIGS = {
+    "cfg2": (20, 5_000, 2),
+    "cfg3": (50, 20_000, 3),
+    "cfg4": (100, 200_000, 4),
+}
+
+
+@dataclass
+class BAProblemData:
+    """A BA window in the layout of the C-ABI (``include/vo_hip.h``).
+
+    ``obs_*`` are CSR-ordered by point: observations of point ``p`` are
+    ``point_ptr[p]:point_ptr[p+1]``.
+    """
+
+    K: np.ndarray  # (3,3) f64
+    poses_cw: np.ndarray  # (N,4,4) f64 initial guess
+    points: np.ndarray  # (L,3) f64 initial guess
+    point_ptr: np.ndarray  # (L+1,) i32
+    obs_cam: np.ndarray  # (M,) i32
+    obs_uv: np.ndarray  # (M,2) f32
+    n_fixed: int
+    poses_true: np.ndarray  # (N,4,4)
+    points_true: np.ndarray  # (L,3)
+
+    @property
+    def n_poses(self) -> int:
+        return self.poses_cw.shape[0]
+
+    @property
+    def n_points(self) -> int:
+        return self.points.shape[0]
+
+    @property
+    def n_obs(self) -> int:
+        return self.obs_cam.shape[0]
+
+    def obs_point(self) -> np.ndarray:
+        """Point index of each observation (expanded CSR)."""
+        return np.repeat(
+            np.arange(self.n_points, dtype=np.int32), np.diff(self.point_ptr)
+        )
+
+
+def so3_exp(phi: np.ndarray) -> np.ndarray:
+    """Rodrigues for a batch of axis-angle vectors (...,3) -> (...,3,3)."""
+    phi = np.asarray(phi, dtype=np.float64)
+    th = np.linalg.norm(phi, axis=-1)[..., None, None]
+    k = np.zeros(phi.shape[:-1] + (3, 3))
+    k[..., 0, 1], k[..., 0, 2] = -phi[..., 2], phi[..., 1]
+    k[..., 1, 0], k[..., 1, 2] = phi[..., 2], -phi[..., 0]
+    k[..., 2, 0], k[..., 2, 1] = -phi[..., 1], phi[..., 0]
+    small = th < 1e-8
+    ths = np.where(small, 1.0, th)
+    a = np.where(small, 1.0, np.sin(ths) / ths)
+    b = np.where(small, 0.5, (1.0 - np.cos(ths)) / ths**2)
+    eye = np.broadcast_to(np.eye(3), k.shape)
+    return eye + a * k + b * (k @ k)
+
+
+def make_ba_problem(
+    n_poses: int,
+    n_points: int,
+    seed: int,
+    *,
+    noise_px: float = 1.0,
+    n_fixed: int = 2,
+    rot_perturb: float = 0.01,
+    trans_perturb: float = 0.05,
+    point_perturb: float = 0.02,
+    max_track: int = 8,
+) -> BAProblemData:
+    """Synthetic sliding-window BA problem."""
+    rng = np.random.default_rng(seed)
+    K = KITTI_K.copy()
+    W, H = KITTI_WH
+    Kinv = np.linalg.inv(K)
+
+    # --- trajectory: T_wc, 1 m forward per pose along the camera z axis
+    yaw = np.cumsum(np.concatenate([[0.0], rng.normal(0.0, 0.01, n_poses - 1)]))
+    R_wc = so3_exp(np.stack([np.zeros(n_poses), yaw, np.zeros(n_poses)], -1))
+    pos = np.zeros((n_poses, 3))
+    for i in range(1, n_poses):
+        pos[i] = pos[i - 1] + R_wc[i] @ np.array([0.0, 0.0, 1.0])
+    R_cw = np.transpose(R_wc, (0, 2, 1))
+    t_cw = -np.einsum("nij,nj->ni", R_cw, pos)
+    poses_true = np.tile(np.eye(4), (n_poses, 1, 1))
+    poses_true[:, :3, :3] = R_cw
+    poses_true[:, :3, 3] = t_cw
+
+    # --- landmarks: first camera sorted (landmarks are created in keyframe order)
+    first = np.sort(rng.integers(0, n_poses - 1, n_points))
+    want = rng.integers(2, max_track + 1, n_points)
+    pts = np.empty((n_points, 3))
+    tracks_len = np.empty(n_points, dtype=np.int64)
+    todo = np.arange(n_points)
+    for _attempt in range(64):
+        if todo.size == 0:
+            break
+        f = first[todo]
+        u = rng.uniform(0.0, W, todo.size)
+        v = rng.uniform(0.0, H, todo.size)
+        d = rng.uniform(5.0, 50.0, todo.size)
+        ray = (Kinv @ np.stack([u, v, np.ones_like(u)])).T * d[:, None]
+        X = np.einsum("nij,nj->ni", R_wc[f], ray) + pos[f]
+        # visibility run along the following cameras
+        length = np.ones(todo.size, dtype=np.int64)
+        alive = np.ones(todo.size, dtype=bool)
+        for s in range(1, max_track):
+            cam = f + s
+            ok = alive & (cam < n_poses) & (s < want[todo])
+            camc = np.minimum(cam, n_poses - 1)
+            pc = np.einsum("nij,nj->ni", R_cw[camc], X) + t_cw[camc]
+            z = pc[:, 2]
+            zs = np.where(z > 1e-6, z, 1.0)
+            uu = K[0, 0] * pc[:, 0] / zs + K[0, 2]
+            vv = K[1, 1] * pc[:, 1] / zs + K[1, 2]
+            vis = (z > 0.5) & (uu >= 0) & (uu < W) & (vv >= 0) & (vv < H)
+            ok &= vis
+            length += ok
+            alive &= ok
+        good = length >= 2
+        pts[todo[good]] = X[good]
+        tracks_len[todo[good]] = length[good]
+        todo = todo[~good]
+    if todo.size:
+        raise RuntimeError("could not place all landmarks with track >= 2")
+
+    point_ptr = np.zeros(n_points + 1, dtype=np.int64)
+    point_ptr[1:] = np.cumsum(tracks_len)
+    M = int(point_ptr[-1])
+    obs_pt = np.repeat(np.arange(n_points), tracks_len)
+    obs_cam = first[obs_pt] + (np.arange(M) - point_ptr[obs_pt])
+    pc = np.einsum("nij,nj->ni", R_cw[obs_cam], pts[obs_pt]) + t_cw[obs_cam]
+    uv = np.stack(
+        [K[0, 0] * pc[:, 0] / pc[:, 2] + K[0, 2], K[1, 1] * pc[:, 1] / pc[:, 2] + K[1, 2]],
+        -1,
+    )
+    uv = uv + rng.normal(0.0, noise_px, uv.shape)
+
+    # --- initial guess
+    poses0 = poses_true.copy()
+    nf = min(n_fixed, n_poses)
+    dR = so3_exp(rng.normal(0.0, rot_perturb, (n_poses, 3)))
+    dt = rng.normal(0.0, trans_perturb, (n_poses, 3))
+    poses0[nf:, :3, :3] = dR[nf:] @ poses_true[nf:, :3, :3]
+    poses0[nf:, :3, 3] = poses_true[nf:, :3, 3] + dt[nf:]
+    depth = np.einsum("nj,nj->n", R_cw[first][:, 2, :], pts) + t_cw[first][:, 2]
+    points0 = pts + rng.normal(0.0, 1.0, pts.shape) * (point_perturb * depth)[:, None]
+
+    return BAProblemData(
+        K=K,
+        poses_cw=poses0,
+        points=points0,
+        point_ptr=point_ptr.astype(np.int32),
+        obs_cam=obs_cam.astype(np.int32),
+        obs_uv=uv.astype(np.float32),
+        n_fixed=nf,
+        poses_true=poses_true,
+        points_true=pts,
+    )
+
+
+def make_ba_config(name: str, **kw) -> BAProblemData:
+    n, l, seed = BA_CONFIGS[name]
+    return make_ba_problem(n, l, seed, **kw)
+
+
+def sift_like_descriptors(n: int, rng: np.random.Generator, dim: int = 128) -> np.ndarray:
+    """Integer-valued 0..255 float32 descriptors with ~40 % zeros (SIFT-like).
+
+    OpenCV SIFT writes ``saturate_cast<uchar>`` values into its CV_32F
+    descriptor, which ``process_image`` casts to float32 (frontend.py:60).
+    """
+    mag = rng.gamma(1.5, 40.0, (n, dim))
+    mag[rng.random((n, dim)) < 0.4] = 0.0
+    return np.clip(np.rint(mag), 0, 255).astype(np.float32)
+
+
+def sift_like_pair(n0: int, n1: int, seed: int, dim: int = 128, overlap: float = 0.6):
+    """Two descriptor sets where a fraction of set-1 rows are noisy copies of set-0 rows."""
+    rng = np.random.default_rng(seed)
+    d0 = sift_like_descriptors(n0, rng, dim)
+    d1 = sift_like_descriptors(n1, rng, dim)
+    k = int(min(n0, n1) * overlap)
+    src = rng.choice(n0, k, replace=False)
+    dst = rng.choice(n1, k, replace=False)
+    noisy = d0[src] + rng.normal(0.0, 6.0, (k, dim))
+    d1[dst] = np.clip(np.rint(noisy), 0, 255).astype(np.float32)
+    return d0, d1
+
+
+def superpoint_like_pair(n0: int, n1: int, seed: int, dim: int = 256, overlap: float = 0.6):
+    """L2-normalised float32 descriptor sets (SuperPoint-like, D=256)."""
+    rng = np.random.default_rng(seed)
+    d0 = rng.standard_normal((n0, dim)).astype(np.float32)
+    d1 = rng.standard_normal((n1, dim)).astype(np.float32)
+    k = int(min(n0, n1) * overlap)
+    src = rng.choice(n0, k, replace=False)
+    dst = rng.choice(n1, k, replace=False)
+    d1[dst] = d0[src] + 0.3 * rng.standard_normal((k, dim)).astype(np.float32)
+    d0 /= np.linalg.norm(d0, axis=1, keepdims=True)
+    d1 /= np.linalg.norm(d1, axis=1, keepdims=True)
+    return d0.astype(np.float32), d1.astype(np.float32)
