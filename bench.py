@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""Benchmark: BA Gauss-Newton iterations/s on the 50-pose x 20k-landmark window.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1
+it is launched by ``torch.distributed.run`` (one rank per GPU).  A *step* is
+one full GN iteration of the synthetic cfg3 window (BASELINE.json configs[2]:
+50 poses x 20k landmarks, ~83k observations, seed 3): fused back-substitution
++ linearisation + Schur accumulation (K1), slab reduction (K2), [RCCL
+all-reduce of the reduced camera system when N > 1], dense pose solve + pose
+update (K3).  Inputs are resident in HBM before timing starts.  N > 1 shards
+the SAME window's landmarks across ranks (strong scaling, one all-reduce per
+iteration).  Rank 0 prints ONE JSON line.
+
+Also reported in that line: the per-kernel HIP-event durations measured on
+the library stream over the timed region, the roofline of the dominant
+kernel, the CPU baseline (the C oracle, timed on this host's cores) and, at
+N = 1, the secondary metric "descriptor-match Mpairs/sec" (SIFT-like 4000 x
+4000 x 128 frame pairs, batched, int8 MFMA path) with its own roofline.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+I8_PEAK_TOPS = 5000.0  # dense int8 MFMA = 2x the 2.5 PF dense bf16 rate (MI355X_MICROARCH.md)
+METRIC = "BA GN-iters/sec at 50 poses×20k landmarks; descriptor-match Mpairs/sec"
+
+
+def ba_kernel_bytes(kind: str, n_poses: int, n_points: int, n_obs: int, n_free: int,
+                    prof_blocks: int) -> float:
+    """Algorithmic HBM bytes per launch."""
+    if kind == "ba_lin":
+        # obs (uv f32x2 + camera i32 + track-entry i32), points read + written + CSR
+        # offset, old + new poses
+        return 16.0 * n_obs + (24 + 24 + 4) * n_points + 2 * 96 * n_poses
+    if kind == "ba_reduce":
+        return 36 * 8.0 * prof_blocks + 6 * 8.0 * n_free
+    if kind == "ba_solve":
+        return 36 * 8.0 * prof_blocks + 2 * 6 * 8.0 * n_free + 2 * 96 * n_poses
+    return 0.0
+
+
+def cpu_baseline_ba(p, lam: float, budget_s: float = 3.0):
+    from oracle import cref
+
+    threads = min(16, os.cpu_count() or 1)
+    R = cref.BAProblemRef(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, lam)
+    poses, pts = p.poses_cw, p.points
+    ok, poses, pts, *_ = R.step(poses, pts, threads, want_system=False)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ok, poses, pts, *_ = R.step(poses, pts, threads, want_system=False)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= budget_s or n >= 2000:
+            break
+    return {"value": n / dt, "unit": "GN-iters/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ba_ref.c (OpenMP, dense Schur + dense Cholesky) on the same cfg3 "
+                      f"window: {n} GN iterations in {dt:.2f} s on {threads} host threads"}
+
+
+def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: int = 3):
+    from visualodometry_amd import _lib, matcher
+    from visualodometry_amd.synthetic import sift_like_pair
+
+    pairs = [sift_like_pair(n, n, 1000 + b) for b in range(batch)]
+    a = _lib.DeviceArray.from_numpy(ctx, np.stack([q[0] for q in pairs]))
+    b = _lib.DeviceArray.from_numpy(ctx, np.stack([q[1] for q in pairs]))
+    out = _lib.DeviceArray(ctx, (batch, n), np.int32)
+    for _ in range(warmup):
+        matcher.match_batch_device(a, b, out=out, ctx=ctx)
+    matcher.synchronize(ctx)
+    _lib.profile_enable(ctx, True)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        matcher.match_batch_device(a, b, out=out, ctx=ctx)
+    matcher.synchronize(ctx)
+    dt = time.perf_counter() - t0
+    prof = _lib.profile_read(ctx)
+    _lib.profile_enable(ctx, False)
+    # parity guard on frame pair 0 against the oracle (not timed)
+    from oracle import match_ref
+
+    ref = match_ref.match_int(*pairs[0])
+    got = out.numpy()[0]
+    kept = np.nonzero(got >= 0)[0]
+    assert np.array_equal(np.stack([kept, got[kept]], 1), ref), "matcher parity guard failed"
+
+    pairs_total = batch * n * n * calls
+    ms_i8, cnt_i8 = prof.get("match_i8", (0.0, 1))
+    avg_s = ms_i8 / max(cnt_i8, 1) / 1e3
+    tops = 2.0 * 128 * batch * n * n / avg_s / 1e12 if avg_s > 0 else 0.0
+    kern = {k: round(v[0] / v[1] * 1e3, 2) for k, v in prof.items()}
+    res = {
+        "metric": "descriptor-match Mpairs/sec",
+        "value": pairs_total / dt / 1e6,
+        "unit": "Mpairs/s",
+        "dtype": "i8",
+        "config": {"workload": f"SIFT-like (integers 0..255 as f32) {n} x {n} x 128, "
+                               f"{batch} frame pairs per call, knn2 + ratio 0.75", "calls": calls},
+        "kernel_us": kern,
+        "roofline": {"bound": "mfma", "kernel": "match_i8", "achieved": tops, "peak": I8_PEAK_TOPS,
+                     "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS, "traffic": None,
+                     "note": "int8 ops (2*128 per pair) per match_i8 launch / its HIP-event duration"},
+    }
+    # CPU baseline: C oracle on a bounded sample of query rows
+    from oracle import cref
+
+    threads = min(16, os.cpu_count() or 1)
+    rows = 1000
+    t0 = time.perf_counter()
+    cref.knn2(pairs[0][0][:rows], pairs[0][1], threads)
+    cdt = time.perf_counter() - t0
+    res["cpu_baseline"] = {"value": rows * n / cdt / 1e6, "unit": "Mpairs/s", "cores": threads,
+                           "kind": "port",
+                           "sample": f"oracle/match_ref.c knn2 on {rows} x {n} x 128 of frame pair 0, "
+                                     f"{threads} host threads"}
+    return res
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--lam", type=float, default=1.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-matcher", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-kernel HBM bytes per launch from a rocprofv3 --pmc pass")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    from visualodometry_amd import _lib
+    from visualodometry_amd.ba import BASession
+    from visualodometry_amd.shard import shard
+    from visualodometry_amd.synthetic import BA_CONFIGS, make_ba_config
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # control plane only
+
+    ctx = _lib.context(local)
+    if world > 1:
+        uid = [_lib.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        _lib.comm_init(ctx, world, rank, uid[0])
+
+    p = make_ba_config(args.config)
+    (p0, p1), ptr, cam, uv, pts = shard(p.point_ptr, p.obs_cam, p.obs_uv, p.points, world, rank)
+    sess = BASession(p.K, ptr, cam, uv, p.n_poses, p.n_fixed, args.lam, ctx)
+    sess.set_state(p.poses_cw, pts)
+    stats = sess.plan_stats()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    sess.run_async(args.warmup)
+    sess.synchronize()
+    barrier()
+    sess.synchronize()
+    _lib.profile_enable(ctx, True)
+    t0 = time.perf_counter()
+    sess.run_async(args.steps)
+    sess.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    prof = _lib.profile_read(ctx)
+    _lib.profile_enable(ctx, False)
+    dt = t1 - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t[0])
+    # guard: the timed iterations must not have failed (status is checked by a sync run)
+    rc, costs = sess.run(1)
+    if rc != _lib.VO_OK or not np.all(np.isfinite(costs)):
+        print(f"error: BA status {rc}, costs {costs}", file=sys.stderr)
+        return 1
+
+    value = args.steps / dt
+    n_free = p.n_poses - p.n_fixed
+    kern = {}
+    best = None
+    for k, (ms, cnt) in prof.items():
+        avg_us = ms / cnt * 1e3
+        kern[k] = {"avg_us": round(avg_us, 3), "launches": cnt, "total_ms": round(ms, 3)}
+        if best is None or ms > prof[best][0]:
+            best = k
+    nbytes = ba_kernel_bytes(best, p.n_poses, p1 - p0, int(ptr[-1]), n_free, stats["profile_blocks"])
+    avg_s = prof[best][0] / prof[best][1] / 1e3
+    achieved = nbytes / avg_s / 1e9
+    traffic = None
+    if args.traffic_json and Path(args.traffic_json).exists():
+        traffic = json.loads(Path(args.traffic_json).read_text()).get(best)
+    lin_bytes = ba_kernel_bytes("ba_lin", p.n_poses, p1 - p0, int(ptr[-1]), n_free, stats["profile_blocks"])
+    lin_avg = prof["ba_lin"][0] / prof["ba_lin"][1] / 1e3
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "GN-iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{args.config}: synthetic sliding-window BA window, "
+                        f"{p.n_poses} poses x {p.n_points} landmarks, {p.n_obs} observations "
+                        f"(seed {BA_CONFIGS[args.config][2]}, KITTI K, first {p.n_fixed} poses fixed, "
+                        f"lambda={args.lam}); one step = one full GN iteration",
+            "poses": p.n_poses, "landmarks": p.n_points, "observations": p.n_obs,
+            "parallelism": f"landmark-sharded x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
+            "plan": stats,
+        },
+        "kernels": kern,
+        "roofline": {
+            "bound": "hbm", "kernel": best, "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "bytes_per_launch": nbytes,
+            "note": "algorithmic bytes per launch / HIP-event average duration on the library stream",
+        },
+        "roofline_ba_lin": {"achieved": lin_bytes / lin_avg / 1e9, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": lin_bytes / lin_avg / 1e9 / HBM_PEAK_GBS,
+                            "bytes_per_launch": lin_bytes},
+        "algorithmic_bytes_per_iter": stats["algorithmic_bytes_per_iter"],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_ba(p, args.lam)
+        line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
+    if rank == 0 and world == 1 and not args.no_matcher:
+        line["secondary"] = bench_matcher(ctx)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

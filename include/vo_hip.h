@@ -58,6 +58,13 @@ void vo_destroy(vo_ctx* ctx);
 void* vo_stream(vo_ctx* ctx);
 int vo_synchronize(vo_ctx* ctx);
 
+/* Device buffers on the context's device (so callers need no second HIP
+ * runtime in-process).  Copies are synchronous on the context stream. */
+void* vo_device_alloc(vo_ctx* ctx, uint64_t bytes);
+int vo_device_free(vo_ctx* ctx, void* ptr);
+int vo_memcpy_h2d(vo_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+int vo_memcpy_d2h(vo_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+
 /* ---- descriptor matching (knn k=2 + Lowe ratio) --------------------------
  * des0: (n0, dim) float32 row-major, the "query" (previous keyframe) set;
  * des1: (n1, dim) float32 row-major, the "train" (current frame) set.
@@ -137,6 +144,22 @@ int vo_ba_solve(vo_ctx* ctx, const vo_ba_problem* prob, double* poses, double* p
  * blocks [5] track entries [6] bytes read+written per GN iteration
  * (algorithmic) [7] wide landmarks. Returns count written. */
 int vo_ba_plan_stats(vo_ctx* ctx, int64_t* out, int n);
+
+/* Diagnostic only: with VO_BA_STAMPS=1 in the environment at vo_ba_setup, K1
+ * runs a separate stamped instantiation; returns per-phase shader-cycle sums over
+ * all workgroups of the last K1 launch (load, backsub, linobs, reduce, elim,
+ * schur, write).  Returns the count written (0 when stamps are off). */
+int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n);
+
+/* ---- kernel timing (HIP events on the context stream) ---------------------
+ * When enabled, every kernel launch is bracketed by hipEventRecord on the
+ * context stream.  vo_profile_read synchronises and returns, per kernel id,
+ * the summed duration in ms and the launch count, then clears the records.
+ * Ids: 0 ba_lin (K1), 1 ba_reduce (K2), 2 ba_solve (K3), 3 match_pack,
+ *      4 match_i8 (MFMA sweep), 5 match_f32, 6 match_merge.               */
+#define VO_PROFILE_KERNELS 7
+int vo_profile_enable(vo_ctx* ctx, int on);
+int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
 
 /* ---- multi-GPU (landmark sharding + RCCL all-reduce) --------------------- */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the caller. */

@@ -20,13 +20,15 @@ _gpu_ok = None
 
 
 def gpu_available() -> bool:
+    """A gfx950 device reachable through libvo_hip.so itself (no torch in the GPU path)."""
     global _gpu_ok
     if _gpu_ok is None:
-        try:
-            import torch
+        from visualodometry_amd import _lib
 
-            _gpu_ok = bool(torch.cuda.is_available())
-        except Exception:
+        try:
+            _lib.context(int(os.environ.get("VO_DEVICE", "0")))
+            _gpu_ok = True
+        except _lib.VoError:
             _gpu_ok = False
     return _gpu_ok
 

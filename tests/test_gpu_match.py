@@ -140,16 +140,15 @@ def test_sqrt_collision_rescan(ctx):
 
 
 def test_batch_device_matches_single(ctx):
-    import torch
+    from visualodometry_amd._lib import DeviceArray
 
     B, n0, n1 = 4, 500, 600
     pairs = [sift_like_pair(n0, n1, 100 + b) for b in range(B)]
-    a = torch.tensor(np.stack([p[0] for p in pairs]), device="cuda")
-    b = torch.tensor(np.stack([p[1] for p in pairs]), device="cuda")
-    torch.cuda.synchronize()
+    a = DeviceArray.from_numpy(ctx, np.stack([p[0] for p in pairs]))
+    b = DeviceArray.from_numpy(ctx, np.stack([p[1] for p in pairs]))
     best = matcher.match_batch_device(a, b, ctx=ctx)
     matcher.synchronize(ctx)
-    best = best.cpu().numpy()
+    best = best.numpy()
     for k in range(B):
         ref = match_ref.match_int(*pairs[k])
         got = np.nonzero(best[k] >= 0)[0]

@@ -64,6 +64,10 @@ SIGNATURES = {
     "vo_destroy": (None, [_P]),
     "vo_stream": (_P, [_P]),
     "vo_synchronize": (_I, [_P]),
+    "vo_device_alloc": (_P, [_P, C.c_uint64]),
+    "vo_device_free": (_I, [_P, _P]),
+    "vo_memcpy_h2d": (_I, [_P, _P, _P, C.c_uint64]),
+    "vo_memcpy_d2h": (_I, [_P, _P, _P, C.c_uint64]),
     "vo_match_knn2_ratio": (_I, [_P, _PF, _I, _PF, _I, _I, _D, _PI32, _PI32]),
     "vo_match_knn2": (_I, [_P, _PF, _I, _PF, _I, _I, _PI32, _PF]),
     "vo_match_batch_async": (_I, [_P, _P, _P, _I, _I, _I, _I, _D, _P]),
@@ -75,6 +79,9 @@ SIGNATURES = {
     "vo_ba_step_debug": (_I, [_P, _PD, _PD, _PD, _PD]),
     "vo_ba_solve": (_I, [_P, C.POINTER(BAProblemC), _PD, _PD, _I, _PD]),
     "vo_ba_plan_stats": (_I, [_P, _PI64, _I]),
+    "vo_ba_debug_stamps": (_I, [_P, C.POINTER(C.c_uint64), _I]),
+    "vo_profile_enable": (_I, [_P, _I]),
+    "vo_profile_read": (_I, [_P, _PD, _PI64]),
     "vo_comm_unique_id": (_I, [C.c_char_p]),
     "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
 }
@@ -150,6 +157,79 @@ def context(device: int | None = None) -> Context:
             _contexts.setdefault(device, ctx)
             ctx = _contexts[device]
     return ctx
+
+
+class DeviceArray:
+    """A dense array in the context device's HBM (owned; freed on close/GC)."""
+
+    def __init__(self, ctx: "Context", shape, dtype):
+        import numpy as np
+
+        self.ctx = ctx
+        self.shape = tuple(int(x) for x in shape)
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        p = ctx.lib.vo_device_alloc(ctx.handle, self.nbytes)
+        if not p:
+            raise VoError(VO_ERR_NOMEM, ctx.lib.vo_last_error().decode(errors="replace"))
+        self.ptr = p
+
+    @classmethod
+    def from_numpy(cls, ctx: "Context", a) -> "DeviceArray":
+        import numpy as np
+
+        a = np.ascontiguousarray(a)
+        d = cls(ctx, a.shape, a.dtype)
+        check(ctx.lib.vo_memcpy_h2d(ctx.handle, d.ptr, a.ctypes.data, d.nbytes), "vo_memcpy_h2d")
+        return d
+
+    def numpy(self):
+        import numpy as np
+
+        out = np.empty(self.shape, self.dtype)
+        check(self.ctx.lib.vo_memcpy_d2h(self.ctx.handle, out.ctypes.data, self.ptr, self.nbytes),
+              "vo_memcpy_d2h")
+        return out
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self.ctx.lib.vo_device_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+KERNEL_NAMES = ["ba_lin", "ba_reduce", "ba_solve", "match_pack", "match_i8", "match_f32",
+                "match_merge"]
+
+
+def profile_enable(ctx: "Context", on: bool = True) -> None:
+    check(ctx.lib.vo_profile_enable(ctx.handle, int(on)), "vo_profile_enable")
+
+
+def profile_read(ctx: "Context") -> dict:
+    """{kernel: (total_ms, launches)} from HIP events on the library stream."""
+    import numpy as np
+
+    ms = np.zeros(len(KERNEL_NAMES))
+    cnt = np.zeros(len(KERNEL_NAMES), dtype=np.int64)
+    check(ctx.lib.vo_profile_read(ctx.handle, ptr(ms, C.c_double), ptr(cnt, C.c_int64)),
+          "vo_profile_read")
+    return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(KERNEL_NAMES) if cnt[i]}
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    check(load().vo_comm_unique_id(buf), "vo_comm_unique_id")
+    return buf.raw
+
+
+def comm_init(ctx: "Context", nranks: int, rank: int, uid: bytes) -> None:
+    check(ctx.lib.vo_comm_init(ctx.handle, nranks, rank, uid), "vo_comm_init")
 
 
 def ptr(a, ctype):

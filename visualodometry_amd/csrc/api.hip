@@ -21,6 +21,46 @@ void set_error(const char* f, ...) {
 }
 const char* last_error() { return g_err.c_str(); }
 
+hipEvent_t Profiler::get() {
+  if (used == pool.size()) {
+    hipEvent_t e;
+    VO_HIP_CHECK(hipEventCreate(&e));
+    pool.push_back(e);
+  }
+  return pool[used++];
+}
+
+void Profiler::begin(hipStream_t st, int id) {
+  if (!on) return;
+  Rec r{id, get(), get()};
+  VO_HIP_CHECK(hipEventRecord(r.start, st));
+  recs.push_back(r);
+}
+
+void Profiler::end(hipStream_t st) {
+  if (!on || recs.empty()) return;
+  VO_HIP_CHECK(hipEventRecord(recs.back().stop, st));
+}
+
+void Profiler::read(double* ms, int64_t* counts) {
+  for (int k = 0; k < kKCount; ++k) {
+    ms[k] = 0.0;
+    counts[k] = 0;
+  }
+  for (const Rec& r : recs) {
+    float t = 0.0f;
+    VO_HIP_CHECK(hipEventElapsedTime(&t, r.start, r.stop));
+    ms[r.id] += t;
+    counts[r.id] += 1;
+  }
+  recs.clear();
+  used = 0;
+}
+
+Profiler::~Profiler() {
+  for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+}
+
 // ba.hip
 void ba_setup(vo_ctx*, const vo_ba_problem*);
 void ba_set_state(vo_ctx*, const double*, const double*);
@@ -28,6 +68,7 @@ void ba_get_state(vo_ctx*, double*, double*);
 int ba_run(vo_ctx*, int, double*, bool);
 int ba_step_debug(vo_ctx*, double*, double*, double*, double*);
 int ba_stats(vo_ctx*, int64_t*, int);
+int ba_stamps(vo_ctx*, uint64_t*, int);
 void comm_unique_id(char out[128]);
 void comm_init(vo_ctx*, int, int, const char*);
 
@@ -130,6 +171,39 @@ int vo_synchronize(vo_ctx* ctx) {
   });
 }
 
+void* vo_device_alloc(vo_ctx* ctx, uint64_t bytes) {
+  void* p = nullptr;
+  int rc = guarded([&] {
+    vo::bind(ctx);
+    VO_HIP_CHECK(hipMalloc(&p, bytes ? bytes : 16));
+  });
+  return rc == VO_OK ? p : nullptr;
+}
+
+int vo_device_free(vo_ctx* ctx, void* ptr) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (ptr) VO_HIP_CHECK(hipFree(ptr));
+  });
+}
+
+int vo_memcpy_h2d(vo_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    VO_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int vo_memcpy_d2h(vo_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    VO_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
 int vo_match_knn2_ratio(vo_ctx* ctx, const float* des0, int n0, const float* des1, int n1,
                         int dim, double ratio, int32_t* out_pairs, int32_t* out_count) {
   return guarded([&] {
@@ -223,6 +297,34 @@ int vo_ba_plan_stats(vo_ctx* ctx, int64_t* out, int n) {
   int g = guarded([&] {
     vo::bind(ctx);
     k = vo::ba_stats(ctx, out, n);
+  });
+  return g != VO_OK ? g : k;
+}
+
+int vo_profile_enable(vo_ctx* ctx, int on) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->prof.on = on != 0;
+    ctx->prof.recs.clear();
+    ctx->prof.used = 0;
+  });
+}
+
+int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(ms_out && counts_out, VO_ERR_ARG, "vo_profile_read: null outputs");
+    VO_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->prof.read(ms_out, counts_out);
+  });
+}
+
+int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n) {
+  int k = 0;
+  int g = guarded([&] {
+    vo::bind(ctx);
+    k = vo::ba_stamps(ctx, out, n);
   });
   return g != VO_OK ? g : k;
 }

@@ -93,29 +93,34 @@ struct LinArgs {
   const double* pose_old;  // linearisation of the pending step (back-substitution)
   const double* pose_new;  // current linearisation point
   const double* dc;        // pending pose update (6 per free camera)
+  const int* segcam_f;     // free camera of each segment window camera
   const int* status;
+  unsigned long long* stamps;  // diagnostic build only: per segment phase cycles
 };
 
-struct LinShared {
+struct alignas(16) LinShared {
   double win[kSegSlots * 36];
   double bwin[kSegCams * 6];
   double Jc[kChunkObs][12];
   double Jp[kChunkObs][6];
   double r[kChunkObs][2];
-  double Z[kChunkTe][18];  // W, then Z = W L^-T
+  alignas(16) double Z[kChunkTe][18];  // W, then Z = W L^-T (144-B rows, 16-B aligned)
   double bt[kChunkTe][6];  // gc, then bt = -gc + Z h
   double X[kChunkPts][3];
   double L[kChunkPts][6];  // 1/l00, l10, 1/l11, l20, l21, 1/l22
   double h[kChunkPts][3];
-  double red[kLinThreads];
+  double dcw[kSegCams][6];  // pending pose update of the segment's window cameras
   int obs_te[kChunkObs];
   int te_obs[kChunkTe + 1];
   int te_pt[kChunkTe];
-  int te_cam[kChunkTe];
   int te_use[kChunkTe];  // free camera and valid landmark
   int te_lcam[kChunkTe];
   int pt_te[kChunkPts + 1];
   int valid[kChunkPts];
+  int slotp[kSegSlots + 1];  // this chunk's pair list offsets per window slot
+  int camp[kSegCams + 1];    // this chunk's track-entry list offsets per window camera
+  uint16_t pairs[kChunkPairs];
+  uint8_t caml[kChunkTe];
 };
 
 // R1: residual and Jacobians, one lane per observation.
@@ -269,17 +274,45 @@ __device__ __forceinline__ void chunk_linearize(LinShared& S, const LinArgs& A,
   __syncthreads();
 }
 
-template <int MODE>
+// Diagnostic build (VO_BA_STAMPS=1): thread 0 accumulates s_memtime deltas per
+// phase; the production instantiation has kStamp = false and executes none.
+enum { kPhLoad = 0, kPhBacksub, kPhLinObs, kPhReduce, kPhElim, kPhSchur, kPhWrite, kPhCount };
+template <bool kStamp>
+struct Stamper {
+  unsigned long long t = 0, acc[kPhCount] = {};
+  __device__ __forceinline__ void start() {
+    if (kStamp && threadIdx.x == 0) t = __builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void mark(int ph) {
+    if (kStamp && threadIdx.x == 0) {
+      const unsigned long long n = __builtin_amdgcn_s_memtime();
+      acc[ph] += n - t;
+      t = n;
+    }
+  }
+  __device__ __forceinline__ void flush(unsigned long long* out) {
+    if (kStamp && threadIdx.x == 0 && out)
+      for (int k = 0; k < kPhCount; ++k) out[blockIdx.x * kPhCount + k] = acc[k];
+  }
+};
+
+template <int MODE, bool kStamp>
 __global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
   if (A.status && *A.status) return;  // a previous solve failed: state frozen
   __shared__ LinShared S;
+  Stamper<kStamp> st;
+  st.start();
   const int seg = blockIdx.x, tid = threadIdx.x;
   const int nslots = A.seg_slot_off[seg + 1] - A.seg_slot_off[seg];
-  const int ncams = A.seg_cam_off[seg + 1] - A.seg_cam_off[seg];
+  const int cam0 = A.seg_cam_off[seg];
+  const int ncams = A.seg_cam_off[seg + 1] - cam0;
   if (MODE & kAccum) {
     for (int e = tid; e < nslots * 36; e += kLinThreads) S.win[e] = 0.0;
     for (int e = tid; e < ncams * 6; e += kLinThreads) S.bwin[e] = 0.0;
   }
+  if (MODE & kBacksub)
+    for (int e = tid; e < ncams * 6; e += kLinThreads)
+      S.dcw[e / 6][e % 6] = A.dc[6l * A.segcam_f[cam0 + e / 6] + e % 6];
   double cost = 0.0;
   for (int ch = A.seg_chunk[seg]; ch < A.seg_chunk[seg + 1]; ++ch) {
     const int ob0 = A.chunk_obs[ch], nob = A.chunk_obs[ch + 1] - ob0;
@@ -290,12 +323,22 @@ __global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
     for (int t = tid; t <= nte; t += kLinThreads) S.te_obs[t] = A.te_obs[te0 + t] - ob0;
     for (int t = tid; t < nte; t += kLinThreads) {
       S.te_pt[t] = A.te_pt[te0 + t] - p0;
-      S.te_cam[t] = A.te_cam[te0 + t];
       S.te_lcam[t] = A.te_lcam[te0 + t];
     }
     for (int p = tid; p <= npt; p += kLinThreads) S.pt_te[p] = A.pt_te[p0 + p] - te0;
     for (int e = tid; e < npt * 3; e += kLinThreads) S.X[e / 3][e % 3] = A.points[3l * p0 + e];
+    if (MODE & kAccum) {
+      // stage this chunk's static pair and camera lists (coalesced, once per chunk)
+      const int sb = A.chunk_slot_base[ch], cb = A.chunk_cam_base[ch];
+      const int e0 = A.slot_ptr[sb], e1 = A.slot_ptr[sb + nslots];
+      for (int k = tid; k <= nslots; k += kLinThreads) S.slotp[k] = A.slot_ptr[sb + k] - e0;
+      for (int e = e0 + tid; e < e1; e += kLinThreads) S.pairs[e - e0] = A.pair_list[e];
+      const int c0 = A.cam_ptr[cb], c1 = A.cam_ptr[cb + ncams];
+      for (int k = tid; k <= ncams; k += kLinThreads) S.camp[k] = A.cam_ptr[cb + k] - c0;
+      for (int e = c0 + tid; e < c1; e += kLinThreads) S.caml[e - c0] = A.cam_list[e];
+    }
     __syncthreads();
+    st.mark(kPhLoad);
 
     if (MODE & kBacksub) {
       double dummy = 0.0;
@@ -305,7 +348,7 @@ __global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
         double a0 = -S.h[p][0], a1 = -S.h[p][1], a2 = -S.h[p][2];
         for (int t = S.pt_te[p]; t < S.pt_te[p + 1]; ++t) {
           if (!S.te_use[t]) continue;
-          const double* d = A.dc + 6 * (S.te_cam[t] - A.n_fixed);
+          const double* d = S.dcw[S.te_lcam[t]];
 #pragma unroll
           for (int a = 0; a < 6; ++a) {
             a0 -= S.Z[t][3 * a] * d[a];
@@ -326,29 +369,58 @@ __global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
         A.points[3l * (p0 + p) + 2] = S.X[p][2];
       }
       __syncthreads();
+      st.mark(kPhBacksub);
     }
 
     if (!(MODE & kAccum)) {
       lin_obs(S, A, A.pose_new, ob0, nob, cost);  // cost at the updated state
       continue;
     }
-    chunk_linearize(S, A, A.pose_new, ob0, nob, nte, npt, cost);
+    lin_obs(S, A, A.pose_new, ob0, nob, cost);
+    __syncthreads();
+    st.mark(kPhLinObs);
+    lin_reduce(S, A, nte, npt);
+    __syncthreads();
+    st.mark(kPhReduce);
+    lin_eliminate(S, nte);
+    __syncthreads();
+    st.mark(kPhElim);
 
     // R4: Schur blocks into the window; lane owns (slot, row a) and sums its
-    // slot's pair list of this chunk in fixed order.
-    const int sb = A.chunk_slot_base[ch];
+    // slot's pair list of this chunk in fixed order.  The next pair's Z rows are
+    // fetched (16-byte LDS reads) while the current pair's 18 FMAs run.
     for (int item = tid; item < nslots * 6; item += kLinThreads) {
       const int s = item / 6, a = item - 6 * (item / 6);
-      const int e0 = A.slot_ptr[sb + s], e1 = A.slot_ptr[sb + s + 1];
+      const int e0 = S.slotp[s], e1 = S.slotp[s + 1];
       if (e0 == e1) continue;
       double out[6] = {0, 0, 0, 0, 0, 0};
+      int pr = S.pairs[e0];
+      double2 zy[9];
+      double za[3];
+      {
+        const double2* py = reinterpret_cast<const double2*>(S.Z[pr >> 8]);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) zy[k] = py[k];
+        const double* px = &S.Z[pr & 255][3 * a];
+        za[0] = px[0]; za[1] = px[1]; za[2] = px[2];
+      }
       for (int e = e0; e < e1; ++e) {
-        const int pr = A.pair_list[e];
         const int x = pr & 255, y = pr >> 8;
-        const double za0 = S.Z[x][3 * a], za1 = S.Z[x][3 * a + 1], za2 = S.Z[x][3 * a + 2];
+        double2 ny[9];
+        double nz[3];
+        int npr = pr;
+        if (e + 1 < e1) {
+          npr = S.pairs[e + 1];
+          const double2* py = reinterpret_cast<const double2*>(S.Z[npr >> 8]);
+#pragma unroll
+          for (int k = 0; k < 9; ++k) ny[k] = py[k];
+          const double* px = &S.Z[npr & 255][3 * a];
+          nz[0] = px[0]; nz[1] = px[1]; nz[2] = px[2];
+        }
+        const double* zf = reinterpret_cast<const double*>(zy);
 #pragma unroll
         for (int c = 0; c < 6; ++c)
-          out[c] -= za0 * S.Z[y][3 * c] + za1 * S.Z[y][3 * c + 1] + za2 * S.Z[y][3 * c + 2];
+          out[c] -= za[0] * zf[3 * c] + za[1] * zf[3 * c + 1] + za[2] * zf[3 * c + 2];
         if (x == y && S.te_use[x]) {
           for (int o = S.te_obs[x]; o < S.te_obs[x + 1]; ++o) {
             const double ja0 = S.Jc[o][a], ja1 = S.Jc[o][6 + a];
@@ -356,32 +428,41 @@ __global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
             for (int c = 0; c < 6; ++c) out[c] += ja0 * S.Jc[o][c] + ja1 * S.Jc[o][6 + c];
           }
         }
+        if (e + 1 < e1) {
+#pragma unroll
+          for (int k = 0; k < 9; ++k) zy[k] = ny[k];
+          za[0] = nz[0]; za[1] = nz[1]; za[2] = nz[2];
+          pr = npr;
+        }
       }
 #pragma unroll
       for (int c = 0; c < 6; ++c) S.win[36 * s + 6 * a + c] += out[c];
     }
-    const int cb = A.chunk_cam_base[ch];
     for (int item = tid; item < ncams * 6; item += kLinThreads) {
       const int c = item / 6, a = item - 6 * (item / 6);
       double acc = 0.0;
-      for (int e = A.cam_ptr[cb + c]; e < A.cam_ptr[cb + c + 1]; ++e) acc += S.bt[A.cam_list[e]][a];
+      for (int e = S.camp[c]; e < S.camp[c + 1]; ++e) acc += S.bt[S.caml[e]][a];
       S.bwin[6 * c + a] += acc;
     }
+    st.mark(kPhSchur);
   }
   __syncthreads();
   if (MODE & kAccum) {
     double* dst = A.slab + 36l * A.seg_slot_off[seg];
     for (int e = tid; e < nslots * 36; e += kLinThreads) dst[e] = S.win[e];
-    double* dstb = A.slab_b + 6l * A.seg_cam_off[seg];
+    double* dstb = A.slab_b + 6l * cam0;
     for (int e = tid; e < ncams * 6; e += kLinThreads) dstb[e] = S.bwin[e];
   }
-  S.red[tid] = cost;
+  double* red = &S.r[0][0];  // the residual buffer is dead here: reuse it for the cost
+  red[tid] = cost;
   __syncthreads();
   for (int w = kLinThreads / 2; w > 0; w >>= 1) {
-    if (tid < w) S.red[tid] += S.red[tid + w];
+    if (tid < w) red[tid] += red[tid + w];
     __syncthreads();
   }
-  if (tid == 0) A.slab_cost[seg] = S.red[0];
+  if (tid == 0) A.slab_cost[seg] = red[0];
+  st.mark(kPhWrite);
+  st.flush(A.stamps);
 }
 
 // K2: fixed-order reduction of the slabs into [S profile | b | cost].
@@ -391,6 +472,7 @@ struct ReduceArgs {
   const int* prof_src_ptr;
   const int* prof_src;
   const uint8_t* prof_diag;
+  const int* prof_diag_cam;  // free camera of each profile block (its block row)
   const int* camb_ptr;
   const int* camb_src;
   const double* slab;
@@ -400,31 +482,44 @@ struct ReduceArgs {
   const int* status;
 };
 
+// Sums slab entries src[k0..k1) (entry e of each) in fixed order, 4 loads in flight.
+template <int W>
+__device__ __forceinline__ double sum_list(const double* __restrict__ slab, const int* __restrict__ src,
+                                           int k0, int k1, int e) {
+  double acc = 0.0;
+  int k = k0;
+  for (; k + 4 <= k1; k += 4) {
+    const int i0 = src[k], i1 = src[k + 1], i2 = src[k + 2], i3 = src[k + 3];
+    const double v0 = slab[(long)W * i0 + e], v1 = slab[(long)W * i1 + e];
+    const double v2 = slab[(long)W * i2 + e], v3 = slab[(long)W * i3 + e];
+    acc = (((acc + v0) + v1) + v2) + v3;
+  }
+  for (; k < k1; ++k) acc += slab[(long)W * src[k] + e];
+  return acc;
+}
+
+// One workgroup per profile block (lanes 0..35: its entries; on a diagonal block
+// lanes 36..41 also reduce b of that camera); the last workgroup sums the cost.
 __global__ __launch_bounds__(64) void ba_reduce_kernel(ReduceArgs A) {
   if (A.status && *A.status) return;
   const int blk = blockIdx.x, tid = threadIdx.x;
   if (blk < A.nprof) {
     if (tid < 36) {
-      double acc = 0.0;
-      for (int k = A.prof_src_ptr[blk]; k < A.prof_src_ptr[blk + 1]; ++k)
-        acc += A.slab[36l * A.prof_src[k] + tid];
+      double acc = sum_list<36>(A.slab, A.prof_src, A.prof_src_ptr[blk], A.prof_src_ptr[blk + 1], tid);
       if (A.prof_diag[blk] && tid % 7 == 0) acc += A.lambda;
       A.sys[36l * blk + tid] = acc;
+    } else if (tid < 42 && A.prof_diag[blk]) {
+      const int f = A.prof_diag_cam[blk], a = tid - 36;
+      A.sys[36l * A.nprof + 6 * f + a] =
+          sum_list<6>(A.slab_b, A.camb_src, A.camb_ptr[f], A.camb_ptr[f + 1], a);
     }
     return;
   }
-  double* b = A.sys + 36l * A.nprof;
-  for (int v = tid; v < 6 * A.F; v += 64) {
-    const int f = v / 6, a = v - 6 * (v / 6);
-    double acc = 0.0;
-    for (int k = A.camb_ptr[f]; k < A.camb_ptr[f + 1]; ++k) acc += A.slab_b[6l * A.camb_src[k] + a];
-    b[v] = acc;
-  }
-  if (tid == 0) {
-    double c = 0.0;
-    for (int s = 0; s < A.nseg; ++s) c += A.slab_cost[s];
-    b[6 * A.F] = c;
-  }
+  double c = 0.0;  // fixed-order: lane-strided partial sums, then a shuffle tree
+  for (int s = tid; s < A.nseg; s += 64) c += A.slab_cost[s];
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) c += __shfl_xor(c, m, 64);
+  if (tid == 0) A.sys[36l * A.nprof + 6 * A.F] = c;
 }
 
 // K3: profile Cholesky solve S dc = b + pose update.
@@ -434,11 +529,11 @@ struct SolveArgs {
   const int* prof_off;
   const int* prof_last;
   double* sys;         // [S profile | b | cost]; factorised in place on the global path
-  double* linv_glob;   // F*36 scratch (global path)
   double* dc;          // 6F out
   const double* pose_cur;
   double* pose_next;
   int* status;
+  unsigned long long* stamps;  // diagnostic build only
 };
 
 __device__ __forceinline__ void se3_exp_apply(const double* d, const double* T, double* out) {
@@ -485,25 +580,117 @@ __device__ __forceinline__ void se3_exp_apply(const double* d, const double* T, 
   out[11] = Rd[6] * T[9] + Rd[7] * T[10] + Rd[8] * T[11] + td2;
 }
 
+// ---- 6x6 block kernels in registers (packed lower storage, P(i,c) = i(i+1)/2 + c)
+__device__ __forceinline__ constexpr int P6(int i, int c) { return i * (i + 1) / 2 + c; }
+
+// In-place Cholesky a = L L^T; r = 1/diag(L) from v_rsq_f64 + two Newton steps
+// (critical chain per column: rsq + 6 dependent FMAs instead of sqrt + divide).
+__device__ __forceinline__ bool chol6(double (&a)[21], double (&r)[6]) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const double d = a[P6(j, j)];
+    ok = ok && d > 0.0;
+    const double dd = d > 0.0 ? d : 1.0;
+    double q = __builtin_amdgcn_rsq(dd);
+    q = q * (1.5 - 0.5 * dd * q * q);
+    q = q * (1.5 - 0.5 * dd * q * q);
+    r[j] = q;
+    a[P6(j, j)] = dd * q;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) a[P6(i, j)] *= q;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i)
+#pragma unroll
+      for (int c = j + 1; c <= i; ++c) a[P6(i, c)] -= a[P6(i, j)] * a[P6(c, j)];
+  }
+  return ok;
+}
+
+// v <- L^-1 v (forward substitution); also solves x L^T = v for a row vector.
+__device__ __forceinline__ void fwd6(const double (&L)[21], const double (&r)[6], double (&v)[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double s = v[i];
+#pragma unroll
+    for (int m = 0; m < i; ++m) s -= L[P6(i, m)] * v[m];
+    v[i] = s * r[i];
+  }
+}
+
+// v <- L^-T v (back substitution).
+__device__ __forceinline__ void bwd6(const double (&L)[21], const double (&r)[6], double (&v)[6]) {
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double s = v[i];
+#pragma unroll
+    for (int m = i + 1; m < 6; ++m) s -= L[P6(m, i)] * v[m];
+    v[i] = s * r[i];
+  }
+}
+
+// v[lane] for a register array without a runtime index (a runtime index would
+// put the whole array in scratch memory).
+template <int N>
+__device__ __forceinline__ double pick(const double (&v)[N], int lane) {
+  double out = 0.0;
+#pragma unroll
+  for (int e = 0; e < N; ++e) out = lane == e ? v[e] : out;
+  return out;
+}
+
+// Orders wave 0's own LDS (or, on the global path, memory) traffic between its
+// lanes: LDS ops of one wave complete in order; global stores need a fence.
 template <bool kLds>
+__device__ __forceinline__ void wave_sync() {
+  if (!kLds) __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+}
+
+// K3.  Right-looking 6x6-block Cholesky of the profile of S with the forward
+// substitution folded in, then back substitution and the pose update.
+// Phase k (one barrier each), with D_k final at the barrier:
+//   every wave  factors D_k redundantly in registers (no LDS hand-off of L_kk).
+//   wave 0      stores L_kk and y'_k = L_kk^-1 y_k; owns row k+1: its panel block
+//               (steps k-2, k-1 applied on the fly), y_{k+1}, and D_{k+1} -= steps
+//               k-1 and k  -- the critical chain to the next phase.
+//   waves 1-3   trailing update of step k-1 on columns >= k+2, then panel rows
+//               i >= k+2: L_ik = (S_ik - L_i,k-2 L_k,k-2^T - L_i,k-1 L_k,k-1^T) L_kk^-T
+//               and y_i -= L_ik y'_k.
+// Column j > m receives step m exactly once: in the panel of phase j (m = j-2,
+// j-1), from wave 0 in phase j-1 (diagonal block, m = j-2, j-1), else from the
+// trailing update of phase m+1 (j >= m+3).
+enum { kS3Setup = 0, kS3Factor, kS3Wave0, kS3Barrier, kS3Backsub, kS3Store, kS3Panel, kS3Count };
+template <bool kLds, bool kStamp = false>
 __global__ __launch_bounds__(kSolveThreads) void ba_solve_kernel(SolveArgs A) {
+  unsigned long long st_t = 0, st_acc[kS3Count] = {};
+  auto mark = [&](int ph) {
+    if (kStamp && threadIdx.x == 0) {
+      const unsigned long long n = __builtin_amdgcn_s_memtime();
+      if (st_t) st_acc[ph] += n - st_t;
+      st_t = n;
+    }
+  };
+  mark(0);
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int s_fail;
   const int tid = threadIdx.x, F = A.F;
+  const int wave = tid >> 6, lane = tid & 63;
   const bool prior_fail = A.status && *A.status;
   double* Sm;
-  double* Linv;
-  double* y;
+  double* aux;  // Ld (21 per block row), rd (6), y (6), ys (6)
   if (kLds) {
     Sm = dyn;
-    Linv = dyn + 36l * A.nprof;
-    y = Linv + 36l * F;
+    aux = dyn + 36l * A.nprof;
   } else {
     Sm = A.sys;
-    Linv = A.linv_glob;
-    y = dyn;
+    aux = dyn;
   }
-  int* first = reinterpret_cast<int*>(y + 6 * F);
+  double* Ld = aux;                        // packed L_kk
+  double* rd = Ld + 21l * F + (F & 1);     // 1 / diag(L_kk) (16-B aligned)
+  double* y = rd + 6l * F;    // right-hand side, updated by the panel lanes
+  double* ys = y + 6l * F;    // y'_k = L_kk^-1 y_k, then x (back substitution)
+  int* first = reinterpret_cast<int*>(ys + 6l * F + 36);  // after the 36-double wave-0 scratch
   int* off = first + F;
   int* last = off + F + 1;
   if (tid == 0) s_fail = prior_fail ? 1 : 0;
@@ -518,160 +705,201 @@ __global__ __launch_bounds__(kSolveThreads) void ba_solve_kernel(SolveArgs A) {
     for (int i = tid; i <= F; i += kSolveThreads) off[i] = A.prof_off[i];
   }
   __syncthreads();
+  mark(kS3Setup);
+
+  // 6-double row loads as three 16-byte LDS reads (blocks are 288 B, rows 48 B)
+  auto ld6 = [](const double* p, double (&v)[6]) {
+    const double2* q = reinterpret_cast<const double2*>(p);
+    const double2 a0 = q[0], a1 = q[1], a2 = q[2];
+    v[0] = a0.x; v[1] = a0.y; v[2] = a1.x; v[3] = a1.y; v[4] = a2.x; v[5] = a2.y;
+  };
+  auto dot6 = [](const double (&u)[6], const double* w) {
+    const double2* q = reinterpret_cast<const double2*>(w);
+    const double2 a0 = q[0], a1 = q[1], a2 = q[2];
+    return u[0] * a0.x + u[1] * a0.y + u[2] * a1.x + u[3] * a1.y + u[4] * a2.x + u[5] * a2.y;
+  };
 
   for (int k = 0; k < F && !s_fail; ++k) {
-    // (A) factor the diagonal block, invert it, forward-substitute y_k
-    if (tid == 0) {
-      double* D = Sm + 36l * (off[k] + k - first[k]);
-      double Lk[36], Li[36];
-      bool ok = true;
-#pragma unroll
-      for (int e = 0; e < 36; ++e) Lk[e] = Li[e] = 0.0;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        double d = D[6 * j + j];
-#pragma unroll
-        for (int m = 0; m < j; ++m) d -= Lk[6 * j + m] * Lk[6 * j + m];
-        ok = ok && d > 0.0;
-        const double ljj = sqrt(d > 0.0 ? d : 1.0);
-        const double inv = 1.0 / ljj;
-        Lk[6 * j + j] = ljj;
-#pragma unroll
-        for (int i = j + 1; i < 6; ++i) {
-          double s = D[6 * i + j];
-#pragma unroll
-          for (int m = 0; m < j; ++m) s -= Lk[6 * i + m] * Lk[6 * j + m];
-          Lk[6 * i + j] = s * inv;
-        }
-      }
+    // uniform indices of this phase, one LDS round trip
+    const int j = k + 1;
+    const int fk = first[k], ok_ = off[k], lk = last[k];
+    const int fj = j < F ? first[j] : F, oj = j < F ? off[j] : 0;
+    const int lkm1 = k >= 1 ? last[k - 1] : k;
+    auto bk = [&](int col) { return Sm + 36l * (ok_ + col - fk); };  // block (k, col)
+    auto bj = [&](int col) { return Sm + 36l * (oj + col - fj); };   // block (k+1, col)
+    double L[21], r[6];
+    {
+      const double* D = bk(k);
+      double dr[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
-        Li[6 * i + i] = 1.0 / Lk[6 * i + i];
+        ld6(D + 6 * i, dr);
 #pragma unroll
-        for (int j = 0; j < i; ++j) {
-          double s = 0.0;
+        for (int c = 0; c <= i; ++c) L[P6(i, c)] = dr[c];
+      }
+    }
+    const bool ok = chol6(L, r);
+    double yk[6];
+    ld6(y + 6 * k, yk);
+    fwd6(L, r, yk);
+    mark(kS3Factor);
+    if (wave == 0) {
+      if (lane < 21) Ld[21l * k + lane] = pick(L, lane);
+      if (lane < 6) {
+        rd[6l * k + lane] = pick(r, lane);
+        ys[6l * k + lane] = pick(yk, lane);
+      }
+      if (lane == 0 && !(ok && isfinite(yk[0] + yk[1] + yk[2] + yk[3] + yk[4] + yk[5]))) s_fail = 1;
+      mark(kS3Store);
+      // critical chain: row k+1 of the panel (wave 0 owns row k+1) -> y_{k+1},
+      // D_{k+1} -= steps k-1 and k
+      if (j < F && fj <= k) {
+        if (lane < 6) {
+          double* row = bj(k) + 6 * lane;
+          double sv[6], u0[6], u1[6];
+          ld6(row, sv);
+          const bool s0 = k >= 2 && fj <= k - 2 && fk <= k - 2;
+          const bool s1 = k >= 1 && fj <= k - 1 && fk <= k - 1;
+          if (s0) ld6(bj(k - 2) + 6 * lane, u0);
+          if (s1) ld6(bj(k - 1) + 6 * lane, u1);
 #pragma unroll
-          for (int m = j; m < i; ++m) s += Lk[6 * i + m] * Li[6 * m + j];
-          Li[6 * i + j] = -s * Li[6 * i + i];
+          for (int c = 0; c < 6; ++c) {
+            double a = 0.0;
+            if (s0) a += dot6(u0, bk(k - 2) + 6 * c);
+            if (s1) a += dot6(u1, bk(k - 1) + 6 * c);
+            sv[c] -= a;
+          }
+          fwd6(L, r, sv);
+          double a = 0.0;
+#pragma unroll
+          for (int c = 0; c < 6; ++c) {
+            row[c] = sv[c];
+            a += sv[c] * yk[c];
+          }
+          y[6 * j + lane] -= a;
+        }
+        wave_sync<kLds>();
+        mark(kS3Panel);
+        if (lane < 36) {
+          const int rr = lane / 6, cc = lane % 6;
+          double u[6];
+          ld6(bj(k) + 6 * rr, u);
+          double a = dot6(u, bj(k) + 6 * cc);
+          if (k >= 1 && fj <= k - 1) {
+            ld6(bj(k - 1) + 6 * rr, u);
+            a += dot6(u, bj(k - 1) + 6 * cc);
+          }
+          bj(j)[lane] -= a;
+        }
+      } else if (j < F && k >= 1 && fj <= k - 1 && lane < 36) {
+        // row k+1 has no block in column k: D_{k+1} still owes step k-1
+        const int rr = lane / 6, cc = lane % 6;
+        double u[6];
+        ld6(bj(k - 1) + 6 * rr, u);
+        bj(j)[lane] -= dot6(u, bj(k - 1) + 6 * cc);
+      }
+      mark(kS3Wave0);
+    } else {
+      const int t0 = tid - 64, nt = kSolveThreads - 64;
+      // trailing update of step m = k-1 on columns >= k+2
+      if (k >= 1) {
+        const int m = k - 1;
+        const int n = lkm1 - (k + 1);
+        const int ntri = n > 0 ? n * (n + 1) / 2 : 0;
+        for (int item = t0; item < ntri * 6; item += nt) {
+          const int t = item / 6, rr = item % 6;
+          int di = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+          while ((di + 1) * (di + 2) / 2 <= t) ++di;
+          while (di * (di + 1) / 2 > t) --di;
+          const int dj = t - di * (di + 1) / 2;
+          const int i = k + 2 + di, jj = k + 2 + dj;
+          const int fi = first[i], oi = off[i], fjj = first[jj], ojj = off[jj];
+          if (fi > m || fjj > m) continue;
+          double li[6];
+          ld6(Sm + 36l * (oi + m - fi) + 6 * rr, li);
+          const double* Ljm = Sm + 36l * (ojj + m - fjj);
+          double* Sij = Sm + 36l * (oi + jj - fi) + 6 * rr;
+          double sv[6];
+          ld6(Sij, sv);
+#pragma unroll
+          for (int c = 0; c < 6; ++c) Sij[c] = sv[c] - dot6(li, Ljm + 6 * c);
         }
       }
-      double yk[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        double s = 0.0;
-#pragma unroll
-        for (int m = 0; m <= i; ++m) s += Li[6 * i + m] * y[6 * k + m];
-        yk[i] = s;
-      }
-#pragma unroll
-      for (int e = 0; e < 36; ++e) {
-        D[e] = Lk[e];
-        Linv[36l * k + e] = Li[e];
-      }
-#pragma unroll
-      for (int i = 0; i < 6; ++i) y[6 * k + i] = yk[i];
-      if (!ok || !isfinite(yk[0] + yk[1] + yk[2] + yk[3] + yk[4] + yk[5])) s_fail = 1;
-    }
-    __syncthreads();
-    if (s_fail) break;
-    const int lk = last[k];
-    // (B) panel: L_ik = S_ik Linv_kk^T for rows i in (k, last] whose envelope holds k
-    const double* Li = Linv + 36l * k;
-    for (int item = tid; item < (lk - k) * 6; item += kSolveThreads) {
-      const int i = k + 1 + item / 6, r = item % 6;
-      if (first[i] > k) continue;
-      double* row = Sm + 36l * (off[i] + k - first[i]) + 6 * r;
-      double s[6];
-#pragma unroll
-      for (int m = 0; m < 6; ++m) s[m] = row[m];
-#pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m <= c; ++m) acc += s[m] * Li[6 * c + m];
-        row[c] = acc;
-      }
-    }
-    __syncthreads();
-    // (C) trailing update S_ij -= L_ik L_jk^T (k < j <= i <= last) and y_i -= L_ik y_k
-    const int n = lk - k;
-    const int ntri = n * (n + 1) / 2;
-    for (int item = tid; item < ntri * 6 + n * 6; item += kSolveThreads) {
-      if (item < ntri * 6) {
-        const int t = item / 6, r = item % 6;
-        int di = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-        while ((di + 1) * (di + 2) / 2 <= t) ++di;
-        while (di * (di + 1) / 2 > t) --di;
-        const int dj = t - di * (di + 1) / 2;
-        const int i = k + 1 + di, j = k + 1 + dj;
-        if (first[i] > k || first[j] > k) continue;
-        const double* Lik = Sm + 36l * (off[i] + k - first[i]) + 6 * r;
-        const double* Ljk = Sm + 36l * (off[j] + k - first[j]);
-        double* Sij = Sm + 36l * (off[i] + j - first[i]) + 6 * r;
-        double li[6];
-#pragma unroll
-        for (int m = 0; m < 6; ++m) li[m] = Lik[m];
+      // panel rows i >= k+2 of column k with the look-ahead steps k-2, k-1, and y
+      for (int item = t0; item < (lk - k - 1) * 6; item += nt) {
+        const int i = k + 2 + item / 6, rr = item % 6;
+        const int fi = first[i], oi = off[i];
+        if (fi > k) continue;
+        double* row = Sm + 36l * (oi + k - fi) + 6 * rr;
+        double sv[6], u0[6], u1[6];
+        ld6(row, sv);
+        const bool s0 = k >= 2 && fi <= k - 2 && fk <= k - 2;
+        const bool s1 = k >= 1 && fi <= k - 1 && fk <= k - 1;
+        if (s0) ld6(Sm + 36l * (oi + k - 2 - fi) + 6 * rr, u0);
+        if (s1) ld6(Sm + 36l * (oi + k - 1 - fi) + 6 * rr, u1);
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
-          double acc = 0.0;
-#pragma unroll
-          for (int m = 0; m < 6; ++m) acc += li[m] * Ljk[6 * c + m];
-          Sij[c] -= acc;
+          double a = 0.0;
+          if (s0) a += dot6(u0, bk(k - 2) + 6 * c);
+          if (s1) a += dot6(u1, bk(k - 1) + 6 * c);
+          sv[c] -= a;
         }
-      } else {
-        const int v = item - ntri * 6;
-        const int i = k + 1 + v / 6, r = v % 6;
-        if (first[i] > k) continue;
-        const double* Lik = Sm + 36l * (off[i] + k - first[i]) + 6 * r;
-        double acc = 0.0;
+        fwd6(L, r, sv);
+        double a = 0.0;
 #pragma unroll
-        for (int m = 0; m < 6; ++m) acc += Lik[m] * y[6 * k + m];
-        y[6 * i + r] -= acc;
+        for (int c = 0; c < 6; ++c) {
+          row[c] = sv[c];
+          a += sv[c] * yk[c];
+        }
+        y[6 * i + rr] -= a;
       }
     }
     __syncthreads();
+    mark(kS3Barrier);
   }
-  // backward substitution L^T x = y (row oriented: x_k, then y_j -= L_kj^T x_k)
-  if (!s_fail) {
+  // back substitution L^T x = y' on wave 0, in registers (row oriented:
+  // x_k, then ys_j -= L_kj^T x_k for the blocks of row k)
+  if (!s_fail && wave == 0) {
     for (int k = F - 1; k >= 0; --k) {
-      if (tid == 0) {
-        const double* Li = Linv + 36l * k;
-        double x[6];
+      const int fk = first[k], ok_ = off[k];
+      double Lk[21], rk[6], x[6];
 #pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          double acc = 0.0;
+      for (int e = 0; e < 21; ++e) Lk[e] = Ld[21l * k + e];
+      ld6(rd + 6l * k, rk);
+      ld6(ys + 6l * k, x);
+      bwd6(Lk, rk, x);
+      wave_sync<kLds>();
+      if (lane < 6) ys[6l * k + lane] = pick(x, lane);
+      const int nb = k - fk;
+      for (int item = lane; item < nb * 6; item += 64) {
+        const int jj = fk + item / 6, c = item % 6;
+        const double* Lkj = Sm + 36l * (ok_ + jj - fk);
+        double a = 0.0;
 #pragma unroll
-          for (int m = c; m < 6; ++m) acc += Li[6 * m + c] * y[6 * k + m];
-          x[c] = acc;
-        }
-#pragma unroll
-        for (int c = 0; c < 6; ++c) y[6 * k + c] = x[c];
+        for (int rr = 0; rr < 6; ++rr) a += Lkj[6 * rr + c] * x[rr];
+        ys[6 * jj + c] -= a;
       }
-      __syncthreads();
-      const int nb = k - first[k];
-      for (int item = tid; item < nb * 6; item += kSolveThreads) {
-        const int j = first[k] + item / 6, c = item % 6;
-        const double* Lkj = Sm + 36l * (off[k] + j - first[k]);
-        double acc = 0.0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) acc += Lkj[6 * r + c] * y[6 * k + r];
-        y[6 * j + c] -= acc;
-      }
-      __syncthreads();
+      wave_sync<kLds>();
     }
   }
+  __syncthreads();
   const bool failed = s_fail != 0;
-  for (int e = tid; e < 6 * F; e += kSolveThreads) A.dc[e] = failed ? 0.0 : y[e];
+  for (int e = tid; e < 6 * F; e += kSolveThreads) A.dc[e] = failed ? 0.0 : ys[e];
   for (int c = tid; c < A.n_poses; c += kSolveThreads) {
     const double* T = A.pose_cur + 12 * c;
     double* out = A.pose_next + 12 * c;
     if (failed || c < A.n_fixed) {
       for (int e = 0; e < 12; ++e) out[e] = T[e];
     } else {
-      se3_exp_apply(A.dc + 6 * (c - A.n_fixed), T, out);
+      double d[6];
+      for (int e = 0; e < 6; ++e) d[e] = ys[6 * (c - A.n_fixed) + e];
+      se3_exp_apply(d, T, out);
     }
   }
   if (tid == 0 && failed && !prior_fail) *A.status = A.iter_tag;
+  mark(kS3Backsub);
+  if (kStamp && tid == 0 && A.stamps)
+    for (int k = 0; k < kS3Count; ++k) A.stamps[k] = st_acc[k];
 }
 
 template <class T>
@@ -681,9 +909,9 @@ void upload(DevBuf& buf, const std::vector<T>& v, hipStream_t st) {
     VO_HIP_CHECK(hipMemcpyAsync(buf.ptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
 }
 
-size_t solve_lds_bytes(int nprof, int F) {
-  return (36ull * nprof + 36ull * F + 6ull * F) * 8 + (3ull * F + 1) * 4;
-}
+// K3 LDS: [profile (LDS path only) | Ld 21F | rd 6F | y 6F | ys 6F | W0 36 | ints 3F+1]
+size_t solve_aux_bytes(int F) { return (39ull * F + 37) * 8 + (3ull * F + 1) * 4; }
+size_t solve_lds_bytes(int nprof, int F) { return 36ull * nprof * 8 + solve_aux_bytes(F); }
 constexpr size_t kSolveLdsMax = 150 * 1024;
 
 }  // namespace
@@ -699,7 +927,7 @@ class BAEngine {
     VO_REQUIRE(prob->lambda >= 0.0, VO_ERR_ARG, "vo_ba_setup: lambda must be >= 0");
     VO_REQUIRE((prob->n_points == 0 || prob->point_ptr) && (prob->n_obs == 0 || (prob->obs_cam && prob->obs_uv)),
                VO_ERR_ARG, "vo_ba_setup: null arrays");
-    const int target = segments_target();
+    const int target = segments_target(ctx_->num_cus);
     std::vector<int32_t> zero_ptr(1, 0);
     const int32_t* pp = prob->n_points ? prob->point_ptr : zero_ptr.data();
     if (prob->n_points == 0)
@@ -751,8 +979,16 @@ class BAEngine {
     upload(d_prof_src_ptr_, P.prof_src_ptr, st);
     upload(d_prof_src_, P.prof_src, st);
     upload(d_prof_diag_, P.prof_diag, st);
+    {
+      std::vector<int32_t> row(std::max(1, P.n_prof_blocks()), 0);
+      for (int i = 0; i < P.n_free; ++i)
+        for (int b = P.prof_off[i]; b < P.prof_off[i + 1]; ++b) row[b] = i;
+      upload(d_prof_row_, row, st);
+    }
     upload(d_camb_ptr_, P.camb_ptr, st);
     upload(d_camb_src_, P.camb_src, st);
+    upload(d_segcam_f_, P.segcam_f, st);
+    stamps_on_ = getenv("VO_BA_STAMPS") && atoi(getenv("VO_BA_STAMPS")) != 0;
     const int F = P.n_free;
     d_points_.reserve(std::max(1, P.n_points) * 24ull);
     d_pose_[0].reserve(P.n_poses * 96ull);
@@ -767,17 +1003,18 @@ class BAEngine {
     d_status_.reserve(sizeof(int));
     VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
     solve_lds_ = solve_lds_bytes(P.n_prof_blocks(), F) <= kSolveLdsMax;
-    const size_t lds = solve_lds_ ? solve_lds_bytes(P.n_prof_blocks(), F)
-                                  : (6ull * F) * 8 + (3ull * F + 1) * 4;
+    const size_t lds = solve_lds_ ? solve_lds_bytes(P.n_prof_blocks(), F) : solve_aux_bytes(F);
     VO_REQUIRE(lds <= 160 * 1024, VO_ERR_ARG,
                "vo_ba_setup: %d free poses exceed the solver's LDS budget", F);
     solve_lds_size_ = lds;
-    if (solve_lds_)
-      VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<true>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    else
-      VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<false>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<true, false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<true, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<false, false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<false, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     VO_HIP_CHECK(hipStreamSynchronize(st));
     have_problem_ = true;
     have_state_ = false;
@@ -904,9 +1141,10 @@ class BAEngine {
     VO_REQUIRE(have_state_, VO_ERR_STATE, "BA: no state set");
   }
 
-  static int segments_target() {
+  // K1 workgroups: two per CU (its LDS footprint admits two), overridable for tuning.
+  static int segments_target(int num_cus) {
     const char* e = getenv("VO_BA_SEGMENTS");
-    return e ? std::max(1, atoi(e)) : 0;
+    return e ? std::max(1, atoi(e)) : 2 * std::max(1, num_cus);
   }
 
   LinArgs lin_args() {
@@ -942,7 +1180,9 @@ class BAEngine {
     A.pose_old = d_pose_[cur_ ^ 1].as<double>();
     A.pose_new = d_pose_[cur_].as<double>();
     A.dc = d_dc_.as<double>();
+    A.segcam_f = d_segcam_f_.as<int>();
     A.status = d_status_.as<int>();
+    A.stamps = nullptr;
     return A;
   }
 
@@ -955,14 +1195,26 @@ class BAEngine {
     }
     LinArgs A = lin_args();
     dim3 g(nseg), b(kLinThreads);
-    switch (mode) {
-      case kAccum: hipLaunchKernelGGL(ba_lin_kernel<kAccum>, g, b, 0, ctx_->stream, A); break;
-      case kBacksub | kAccum:
-        hipLaunchKernelGGL((ba_lin_kernel<kBacksub | kAccum>), g, b, 0, ctx_->stream, A);
-        break;
-      case kBacksub: hipLaunchKernelGGL(ba_lin_kernel<kBacksub>, g, b, 0, ctx_->stream, A); break;
-      default: hipLaunchKernelGGL(ba_lin_kernel<0>, g, b, 0, ctx_->stream, A); break;
+    ctx_->prof.begin(ctx_->stream, kKBaLin);
+    if (stamps_on_) {
+      d_stamps_.reserve((size_t)nseg * kPhCount * 8);
+      A.stamps = d_stamps_.as<unsigned long long>();
     }
+#define VO_LIN_LAUNCH(M)                                                               \
+  do {                                                                                 \
+    if (stamps_on_)                                                                    \
+      hipLaunchKernelGGL((ba_lin_kernel<M, true>), g, b, 0, ctx_->stream, A);          \
+    else                                                                               \
+      hipLaunchKernelGGL((ba_lin_kernel<M, false>), g, b, 0, ctx_->stream, A);         \
+  } while (0)
+    switch (mode) {
+      case kAccum: VO_LIN_LAUNCH(kAccum); break;
+      case kBacksub | kAccum: VO_LIN_LAUNCH(kBacksub | kAccum); break;
+      case kBacksub: VO_LIN_LAUNCH(kBacksub); break;
+      default: VO_LIN_LAUNCH(0); break;
+    }
+#undef VO_LIN_LAUNCH
+    ctx_->prof.end(ctx_->stream);
     VO_HIP_CHECK(hipGetLastError());
   }
 
@@ -976,6 +1228,7 @@ class BAEngine {
     R.prof_src_ptr = d_prof_src_ptr_.as<int>();
     R.prof_src = d_prof_src_.as<int>();
     R.prof_diag = d_prof_diag_.as<uint8_t>();
+    R.prof_diag_cam = d_prof_row_.as<int>();
     R.camb_ptr = d_camb_ptr_.as<int>();
     R.camb_src = d_camb_src_.as<int>();
     R.slab = d_slab_.as<double>();
@@ -983,7 +1236,9 @@ class BAEngine {
     R.slab_cost = d_slab_cost_.as<double>();
     R.sys = d_sys_.as<double>();
     R.status = d_status_.as<int>();
+    ctx_->prof.begin(ctx_->stream, kKBaReduce);
     hipLaunchKernelGGL(ba_reduce_kernel, dim3(R.nprof + 1), dim3(64), 0, ctx_->stream, R);
+    ctx_->prof.end(ctx_->stream);
     VO_HIP_CHECK(hipGetLastError());
     if (ctx_->comm && ctx_->comm->nranks > 1)
       VO_NCCL_CHECK(ncclAllReduce(d_sys_.ptr, d_sys_.ptr, sys_len_, ncclFloat64, ncclSum,
@@ -1002,17 +1257,29 @@ class BAEngine {
     A.prof_off = d_prof_off_.as<int>();
     A.prof_last = d_prof_last_.as<int>();
     A.sys = d_sys_.as<double>();
-    A.linv_glob = d_linv_.as<double>();
     A.dc = d_dc_.as<double>();
     A.pose_cur = d_pose_[cur_].as<double>();
     A.pose_next = d_pose_[cur_ ^ 1].as<double>();
     A.status = d_status_.as<int>();
-    if (solve_lds_)
-      hipLaunchKernelGGL(ba_solve_kernel<true>, dim3(1), dim3(kSolveThreads), solve_lds_size_,
-                         ctx_->stream, A);
+    A.stamps = nullptr;
+    if (stamps_on_) {
+      d_stamps3_.reserve(kS3Count * 8);
+      A.stamps = d_stamps3_.as<unsigned long long>();
+    }
+    ctx_->prof.begin(ctx_->stream, kKBaSolve);
+    if (solve_lds_ && stamps_on_)
+      hipLaunchKernelGGL((ba_solve_kernel<true, true>), dim3(1), dim3(kSolveThreads),
+                         solve_lds_size_, ctx_->stream, A);
+    else if (solve_lds_)
+      hipLaunchKernelGGL((ba_solve_kernel<true, false>), dim3(1), dim3(kSolveThreads),
+                         solve_lds_size_, ctx_->stream, A);
+    else if (stamps_on_)
+      hipLaunchKernelGGL((ba_solve_kernel<false, true>), dim3(1), dim3(kSolveThreads),
+                         solve_lds_size_, ctx_->stream, A);
     else
-      hipLaunchKernelGGL(ba_solve_kernel<false>, dim3(1), dim3(kSolveThreads), solve_lds_size_,
-                         ctx_->stream, A);
+      hipLaunchKernelGGL((ba_solve_kernel<false, false>), dim3(1), dim3(kSolveThreads),
+                         solve_lds_size_, ctx_->stream, A);
+    ctx_->prof.end(ctx_->stream);
     VO_HIP_CHECK(hipGetLastError());
   }
 
@@ -1069,8 +1336,33 @@ class BAEngine {
   DevBuf d_chunk_obs_, d_chunk_te_, d_chunk_pt_, d_chunk_slot_base_, d_chunk_cam_base_;
   DevBuf d_slot_ptr_, d_pair_list_, d_cam_ptr_, d_cam_list_;
   DevBuf d_seg_chunk_, d_seg_slot_off_, d_seg_cam_off_;
-  DevBuf d_prof_first_, d_prof_off_, d_prof_last_, d_prof_src_ptr_, d_prof_src_, d_prof_diag_;
-  DevBuf d_camb_ptr_, d_camb_src_;
+  DevBuf d_prof_first_, d_prof_off_, d_prof_last_, d_prof_src_ptr_, d_prof_src_, d_prof_diag_,
+      d_prof_row_;
+  DevBuf d_camb_ptr_, d_camb_src_, d_segcam_f_, d_stamps_, d_stamps3_;
+  bool stamps_on_ = false;
+
+ public:
+  // Diagnostic: per-phase cycle sums of the last K1 launch (VO_BA_STAMPS=1 builds).
+  int read_stamps(uint64_t* out, int n) {
+    if (!stamps_on_) return 0;
+    const int nseg = plan_.n_segments();
+    std::vector<unsigned long long> h((size_t)nseg * kPhCount);
+    VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
+    VO_HIP_CHECK(hipMemcpy(h.data(), d_stamps_.ptr, h.size() * 8, hipMemcpyDeviceToHost));
+    int k = std::min(n, (int)kPhCount);
+    for (int i = 0; i < k; ++i) {
+      uint64_t acc = 0;
+      for (int g = 0; g < nseg; ++g) acc += h[(size_t)g * kPhCount + i];
+      out[i] = acc;
+    }
+    if (n >= kPhCount + kS3Count && d_stamps3_.ptr) {
+      VO_HIP_CHECK(hipMemcpy(out + kPhCount, d_stamps3_.ptr, kS3Count * 8, hipMemcpyDeviceToHost));
+      k += kS3Count;
+    }
+    return k;
+  }
+
+ private:
   DevBuf d_points_, d_pose_[2], d_dc_, d_slab_, d_slab_b_, d_slab_cost_, d_sys_, d_linv_;
   DevBuf d_status_, d_cost_, d_cost_tmp_;
 };
@@ -1090,6 +1382,7 @@ int ba_step_debug(vo_ctx* ctx, double* S, double* b, double* dc, double* cost) {
   return ba_engine(ctx)->step_debug(S, b, dc, cost);
 }
 int ba_stats(vo_ctx* ctx, int64_t* out, int n) { return ba_engine(ctx)->stats(out, n); }
+int ba_stamps(vo_ctx* ctx, uint64_t* out, int n) { return ba_engine(ctx)->read_stamps(out, n); }
 
 void comm_unique_id(char out[128]) {
   ncclUniqueId id;

@@ -97,14 +97,14 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   };
   std::vector<Seg> segs;
   std::vector<int32_t> cq;
-  int c_obs = 0, c_te = 0, c_pts = 0;
+  int c_obs = 0, c_te = 0, c_pts = 0, c_pairs = 0;
   int64_t s_obs = 0;
   bool seg_open = false;
   auto open_chunk = [&](int q) {
     P.chunk_obs.push_back(P.te_obs[P.pt_te[q]]);
     P.chunk_te.push_back(P.pt_te[q]);
     P.chunk_pt.push_back(q);
-    c_obs = c_te = c_pts = 0;
+    c_obs = c_te = c_pts = c_pairs = 0;
   };
   for (int q = 0; q < L; ++q) {
     const int t0 = P.pt_te[q], t1 = P.pt_te[q + 1];
@@ -117,8 +117,9 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       return fmt("landmark %ld is too wide (%ld observations, %ld free cameras); "
                  "limits: 128 observations, 10 free cameras per landmark",
                  P.pt_perm[q], nob, k);
+    const int npairs = k * (k + 1) / 2;
     bool chunk_fits = seg_open && c_obs + nob <= kChunkObs && c_te + nte <= kChunkTe &&
-                      c_pts + 1 <= kChunkPts;
+                      c_pts + 1 <= kChunkPts && c_pairs + npairs <= kChunkPairs;
     bool seg_fits = seg_open;
     if (seg_open) {
       Seg& s = segs.back();
@@ -151,6 +152,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     c_obs += nob;
     c_te += nte;
     c_pts += 1;
+    c_pairs += npairs;
     s_obs += nob;
   }
   P.chunk_obs.push_back(M);

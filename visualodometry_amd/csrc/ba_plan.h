@@ -28,6 +28,7 @@ namespace vo {
 constexpr int kChunkObs = 128;
 constexpr int kChunkTe = 128;
 constexpr int kChunkPts = 64;
+constexpr int kChunkPairs = 1024;  // camera-pair (x, y) entries of one chunk, staged in LDS
 constexpr int kSegSlots = 64;
 constexpr int kSegCams = 32;
 

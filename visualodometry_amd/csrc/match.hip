@@ -446,13 +446,16 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
     int* na = ws.norms.as<int>();
     int* nb = na + (size_t)batch * n0_pad;
     dim3 ga(ceil_div((int64_t)n0_pad * 16, 256), batch), gb(ceil_div((int64_t)n1_pad * 16, 256), batch);
+    ctx->prof.begin(st, kKMatchPack);
     hipLaunchKernelGGL(pack_kernel, ga, dim3(256), 0, st, d_des0, n0, dim, Dp, n0_pad,
                        (long)n0 * dim, qa_bs, qa, na, (uint32_t*)nullptr, flag);
     if (n1 > 0)
       hipLaunchKernelGGL(pack_kernel, gb, dim3(256), 0, st, d_des1, n1, dim, Dp, n1_pad,
                          (long)n1 * dim, qb_bs, qb, nb, ws.colconst.as<uint32_t>(), flag);
+    ctx->prof.end(st);
     if (n1 > 0) {
       dim3 grid(row_wgs, nsplit, batch);
+      ctx->prof.begin(st, kKMatchI8);
       uint4* part = ws.partial.as<uint4>();
       switch (Dp / kKStep) {
         case 1:
@@ -476,20 +479,25 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
                              part, flag);
           break;
       }
+      ctx->prof.end(st);
     }
   }
   if (n1 > 0) {
     dim3 grid(ceil_div(n0, kFloatTile), nsplit, batch);
+    ctx->prof.begin(st, kKMatchF32);
     hipLaunchKernelGGL(match_f32_kernel, grid, dim3(256), 0, st, d_des0, d_des1, n0, n1, dim,
                        n0_pad, w, (long)n0 * dim, (long)n1 * dim, ws.partial.as<uint4>(), flag);
+    ctx->prof.end(st);
   } else {
     // no train rows: every query has no neighbour
     VO_HIP_CHECK(hipMemsetAsync(ws.partial.ptr, 0xFF,
                                 (size_t)batch * nsplit * n0_pad * sizeof(uint4), st));
   }
+  ctx->prof.begin(st, kKMatchMerge);
   hipLaunchKernelGGL(merge_ratio_kernel, dim3(n0, batch), dim3(64), 0, st,
                      ws.partial.as<uint4>(), n1 > 0 ? nsplit : 1, n0, n0_pad, n1, n1_pad, Dp,
                      qa, qb, qa_bs, qb_bs, flag, ratio, d_best, d_idx2, d_dist2);
+  ctx->prof.end(st);
   VO_HIP_CHECK(hipGetLastError());
 }
 

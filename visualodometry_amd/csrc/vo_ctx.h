@@ -2,6 +2,7 @@
 #pragma once
 
 #include <memory>
+#include <vector>
 
 #include "vo_common.h"
 
@@ -22,6 +23,26 @@ struct MatchWorkspace {
 class BAEngine;   // ba.hip
 struct Comm;      // ba.hip (RCCL communicator)
 
+// Kernel ids of the event profiler (vo_profile_* in include/vo_hip.h).
+enum KernelId {
+  kKBaLin = 0, kKBaReduce, kKBaSolve, kKMatchPack, kKMatchI8, kKMatchF32, kKMatchMerge,
+  kKCount
+};
+
+// HIP-event timing of individual kernels on the context stream (off by default).
+struct Profiler {
+  bool on = false;
+  struct Rec { int id; hipEvent_t start, stop; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  hipEvent_t get();
+  void begin(hipStream_t st, int id);  // records a start event if on
+  void end(hipStream_t st);            // records the matching stop event
+  void read(double* ms, int64_t* counts);  // after a stream sync; clears the records
+  ~Profiler();
+};
+
 }  // namespace vo
 
 struct vo_ctx {
@@ -29,6 +50,7 @@ struct vo_ctx {
   hipStream_t stream = nullptr;
   int num_cus = 0;
   vo::MatchWorkspace match;
+  vo::Profiler prof;
   std::unique_ptr<vo::BAEngine> ba;
   std::unique_ptr<vo::Comm> comm;
   vo_ctx();

@@ -72,28 +72,27 @@ def match_knn2(des0, des1, ctx: _lib.Context | None = None):
     return idx, dist
 
 
-def match_batch_device(des0, des1, ratio: float = RATIO_THRESH, out=None, ctx: _lib.Context | None = None):
-    """Batched frame pairs on device memory (torch tensors used as plumbing only).
+def match_batch_device(des0: _lib.DeviceArray, des1: _lib.DeviceArray, ratio: float = RATIO_THRESH,
+                       out: _lib.DeviceArray | None = None, ctx: _lib.Context | None = None):
+    """Batched frame pairs already resident in HBM.
 
-    ``des0`` (B, n0, D) and ``des1`` (B, n1, D) float32 CUDA tensors; returns the
-    (B, n0) int32 tensor of kept train indices (-1 = rejected).  Enqueued on the
-    library stream; the caller synchronises (``synchronize``).
+    ``des0`` (B, n0, D) and ``des1`` (B, n1, D) float32 :class:`DeviceArray`;
+    returns the (B, n0) int32 :class:`DeviceArray` of kept train indices
+    (-1 = rejected).  Enqueued on the library stream; call :func:`synchronize`.
     """
-    import torch
-
-    if des0.dim() != 3 or des1.dim() != 3 or des0.shape[0] != des1.shape[0] or des0.shape[2] != des1.shape[2]:
+    if len(des0.shape) != 3 or len(des1.shape) != 3 or des0.shape[0] != des1.shape[0] \
+            or des0.shape[2] != des1.shape[2]:
         raise ValueError("expected (B, n0, D) and (B, n1, D)")
-    if des0.dtype != torch.float32 or des1.dtype != torch.float32 or not des0.is_cuda:
-        raise ValueError("expected float32 device tensors")
-    des0, des1 = des0.contiguous(), des1.contiguous()
+    if des0.dtype != np.float32 or des1.dtype != np.float32:
+        raise ValueError("expected float32 descriptors")
     B, n0, D = des0.shape
+    ctx = ctx or des0.ctx
     if out is None:
-        out = torch.empty((B, n0), dtype=torch.int32, device=des0.device)
-    ctx = ctx or _lib.context(des0.device.index or 0)
+        out = _lib.DeviceArray(ctx, (B, n0), np.int32)
     check(
         ctx.lib.vo_match_batch_async(
-            ctx.handle, C.c_void_p(des0.data_ptr()), C.c_void_p(des1.data_ptr()), B, n0,
-            des1.shape[1], D, float(ratio), C.c_void_p(out.data_ptr()),
+            ctx.handle, C.c_void_p(des0.ptr), C.c_void_p(des1.ptr), B, n0, des1.shape[1], D,
+            float(ratio), C.c_void_p(out.ptr),
         ),
         "vo_match_batch_async",
     )
