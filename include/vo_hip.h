@@ -161,6 +161,13 @@ int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n);
 int vo_profile_enable(vo_ctx* ctx, int on);
 int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
 
+/* Host-only: builds the static plan of `prob` without a device (planner tests,
+ * capacity checks).  Fills up to n int64 values: [0] chunks [1] segments
+ * [2] slab blocks [3] profile blocks [4] track entries [5] max pairs in a chunk
+ * [6] max window slots in a segment [7] max window cameras in a segment.
+ * Returns the count written, or VO_ERR_ARG (vo_last_error() says why). */
+int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* out, int n);
+
 /* ---- multi-GPU (landmark sharding + RCCL all-reduce) --------------------- */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the caller. */
 int vo_comm_unique_id(char out[128]);

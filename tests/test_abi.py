@@ -1,0 +1,51 @@
+"""The C-ABI library builds, loads and exports every symbol include/vo_hip.h declares (no GPU)."""
+
+import re
+
+import numpy as np
+import pytest
+
+from visualodometry_amd import _lib
+
+
+def header_functions():
+    text = _lib.HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(vo_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_loads_and_abi_version():
+    lib = _lib.load()
+    assert lib.vo_abi_version() == 1
+
+
+def test_every_declared_function_is_exported_and_bound():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), f"{n} not exported by libvo_hip.so"
+        assert n in _lib.SIGNATURES, f"{n} has no ctypes signature in _lib.py"
+    assert set(_lib.SIGNATURES) <= set(names)
+
+
+def test_no_device_fails_loudly(monkeypatch):
+    from tests.conftest import gpu_available
+
+    if gpu_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(_lib.VoError) as e:
+        _lib.Context(0)
+    assert e.value.code in (_lib.VO_ERR_NODEV, _lib.VO_ERR_HIP)
+
+
+def test_matcher_has_no_cpu_fallback():
+    from tests.conftest import gpu_available
+
+    if gpu_available():
+        pytest.skip("a GPU is present")
+    from visualodometry_amd import matcher
+
+    d = np.zeros((4, 128), np.float32)
+    with pytest.raises(_lib.VoError):
+        matcher.match_knn2_ratio(d, d)

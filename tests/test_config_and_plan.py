@@ -1,0 +1,71 @@
+"""Drop-in config vs the reference snapshot; host-side BA planner invariants."""
+
+import dataclasses
+import json
+import sys
+
+import numpy as np
+import pytest
+
+from tests.conftest import GOLDEN, ROOT
+from visualodometry_amd import _lib
+from visualodometry_amd.ba import csr_from_obs_pt, plan_probe
+from visualodometry_amd.synthetic import KITTI_K, make_ba_config, make_ba_problem
+
+sys.path.insert(0, str(ROOT / "visualodometry_amd" / "dropin"))
+from config.config import VOConfig, get_config  # noqa: E402
+
+REF = json.loads((GOLDEN / "reference_config.json").read_text())
+
+
+@pytest.mark.parametrize("dataset", ["kitti", "malaga", "parking", "own", "unknown"])
+def test_get_config_matches_reference(dataset):
+    ours = dataclasses.asdict(get_config(dataset))
+    for k, v in REF["get_config"][dataset].items():
+        assert ours[k] == v, (dataset, k)
+
+
+def test_defaults_match_and_ba_is_off():
+    ours = dataclasses.asdict(VOConfig())
+    for k, v in REF["VOConfig_defaults"].items():
+        assert ours[k] == v
+    assert ours["ba_enabled"] is False
+
+
+def test_sift_extension_applies_the_unreachable_branch():
+    c = get_config("kitti", extractor_type="sift")
+    assert c.extractor_type == "sift" and c.sift_n_features == 4000
+    assert get_config("kitti").sift_n_features == REF["get_config"]["kitti"]["sift_n_features"]
+
+
+def test_synthetic_uses_the_reference_kitti_K():
+    np.testing.assert_array_equal(KITTI_K, np.array(REF["K"]["kitti"]))
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4"])
+def test_plan_limits(cfg):
+    p = make_ba_config(cfg)
+    st = plan_probe(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 512)
+    assert st["track_entries"] == p.n_obs  # synthetic windows have no duplicate (landmark, camera)
+    assert st["max_chunk_pairs"] <= 1024
+    assert st["max_segment_slots"] <= 64 and st["max_segment_cameras"] <= 32
+    assert 1 <= st["segments"] <= st["chunks"]
+
+
+def test_plan_rejects_too_wide_landmark():
+    p = make_ba_problem(16, 10, 3)
+    L = p.n_points
+    cams = np.concatenate([p.obs_cam, np.arange(16, dtype=np.int32)])  # landmark L sees 16 cameras
+    uv = np.concatenate([p.obs_uv, np.zeros((16, 2), np.float32)])
+    ptr = np.concatenate([p.point_ptr, [p.point_ptr[-1] + 16]]).astype(np.int32)
+    with pytest.raises(_lib.VoError) as e:
+        plan_probe(p.K, ptr, cams, uv, 16, 2)
+    assert e.value.code == _lib.VO_ERR_ARG and "too wide" in str(e.value)
+    assert L == p.n_points
+
+
+def test_csr_from_obs_pt_is_stable():
+    obs_pt = np.array([2, 0, 1, 0, 2, 2])
+    order, ptr = csr_from_obs_pt(3, obs_pt)
+    np.testing.assert_array_equal(order, [1, 3, 2, 0, 4, 5])
+    np.testing.assert_array_equal(ptr, [0, 2, 3, 6])

@@ -80,6 +80,7 @@ SIGNATURES = {
     "vo_ba_solve": (_I, [_P, C.POINTER(BAProblemC), _PD, _PD, _I, _PD]),
     "vo_ba_plan_stats": (_I, [_P, _PI64, _I]),
     "vo_ba_debug_stamps": (_I, [_P, C.POINTER(C.c_uint64), _I]),
+    "vo_ba_plan_probe": (_I, [C.POINTER(BAProblemC), _I, _PI64, _I]),
     "vo_profile_enable": (_I, [_P, _I]),
     "vo_profile_read": (_I, [_P, _PD, _PI64]),
     "vo_comm_unique_id": (_I, [C.c_char_p]),

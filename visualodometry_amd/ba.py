@@ -76,6 +76,36 @@ def csr_from_obs_pt(n_points: int, obs_pt: np.ndarray):
     return order, ptr_
 
 
+def _problem_struct(K, point_ptr, obs_cam, obs_uv, n_poses, n_fixed, lam):
+    K = np.asarray(K, dtype=np.float64)
+    prob = BAProblemC()
+    prob.n_poses = int(n_poses)
+    prob.n_points = point_ptr.size - 1
+    prob.n_obs = obs_cam.size
+    prob.n_fixed = int(n_fixed)
+    prob.fx, prob.fy, prob.cx, prob.cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+    prob.lam = float(lam)
+    prob.point_ptr = ptr(point_ptr, C.c_int32)
+    prob.obs_cam = ptr(obs_cam, C.c_int32)
+    prob.obs_uv = ptr(obs_uv, C.c_float)
+    return prob
+
+
+def plan_probe(K, point_ptr, obs_cam, obs_uv, n_poses: int, n_fixed: int = 2,
+               target_segments: int = 512) -> dict:
+    """Host-only static plan statistics (no device needed): ``vo_ba_plan_probe``."""
+    point_ptr = np.ascontiguousarray(point_ptr, dtype=np.int32)
+    obs_cam = np.ascontiguousarray(obs_cam, dtype=np.int32)
+    obs_uv = np.ascontiguousarray(obs_uv, dtype=np.float32).reshape(-1, 2)
+    prob = _problem_struct(K, point_ptr, obs_cam, obs_uv, n_poses, n_fixed, 0.0)
+    out = np.zeros(8, dtype=np.int64)
+    n = check(_lib.load().vo_ba_plan_probe(C.byref(prob), int(target_segments),
+                                           ptr(out, C.c_int64), 8), "vo_ba_plan_probe")
+    keys = ["chunks", "segments", "slab_blocks", "profile_blocks", "track_entries",
+            "max_chunk_pairs", "max_segment_slots", "max_segment_cameras"]
+    return dict(zip(keys[:n], out[:n].tolist()))
+
+
 class BASession:
     """A BA problem resident on one device (structure + state in HBM).
 
@@ -93,17 +123,8 @@ class BASession:
         self.n_poses = int(n_poses)
         self.n_points = self.point_ptr.size - 1
         self.n_fixed = int(n_fixed)
-        K = np.asarray(K, dtype=np.float64)
-        prob = BAProblemC()
-        prob.n_poses = self.n_poses
-        prob.n_points = self.n_points
-        prob.n_obs = self.obs_cam.size
-        prob.n_fixed = self.n_fixed
-        prob.fx, prob.fy, prob.cx, prob.cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
-        prob.lam = float(lam)
-        prob.point_ptr = ptr(self.point_ptr, C.c_int32)
-        prob.obs_cam = ptr(self.obs_cam, C.c_int32)
-        prob.obs_uv = ptr(self.obs_uv, C.c_float)
+        prob = _problem_struct(K, self.point_ptr, self.obs_cam, self.obs_uv, self.n_poses,
+                               self.n_fixed, lam)
         self._prob = prob
         check(self.ctx.lib.vo_ba_setup(self.ctx.handle, C.byref(prob)), "vo_ba_setup")
 

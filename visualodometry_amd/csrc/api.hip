@@ -3,6 +3,7 @@
 #include <cstring>
 #include <vector>
 
+#include "ba_plan.h"
 #include "vo_ctx.h"
 
 namespace vo {
@@ -325,6 +326,37 @@ int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n) {
   int g = guarded([&] {
     vo::bind(ctx);
     k = vo::ba_stamps(ctx, out, n);
+  });
+  return g != VO_OK ? g : k;
+}
+
+int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* out, int n) {
+  int k = 0;
+  int g = guarded([&] {
+    VO_REQUIRE(prob && out, VO_ERR_ARG, "vo_ba_plan_probe: null argument");
+    std::vector<int32_t> zero(1, 0);
+    vo::BAPlan P;
+    std::string err = vo::build_plan(P, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed,
+                                     prob->n_points ? prob->point_ptr : zero.data(), prob->obs_cam,
+                                     prob->obs_uv, target_segments);
+    VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_plan_probe: %s", err.c_str());
+    vo::build_profile(P, vo::local_profile_first(P));
+    int64_t max_pairs = 0, max_slots = 0, max_cams = 0;
+    for (int c = 0; c < P.n_chunks(); ++c) {
+      int s = 0;
+      while (s + 1 < P.n_segments() + 1 && P.seg_chunk[s + 1] <= c) ++s;
+      const int ns = P.seg_slot_off[s + 1] - P.seg_slot_off[s];
+      const int b = P.chunk_slot_base[c];
+      max_pairs = std::max<int64_t>(max_pairs, P.slot_ptr[b + ns] - P.slot_ptr[b]);
+    }
+    for (int s = 0; s < P.n_segments(); ++s) {
+      max_slots = std::max<int64_t>(max_slots, P.seg_slot_off[s + 1] - P.seg_slot_off[s]);
+      max_cams = std::max<int64_t>(max_cams, P.seg_cam_off[s + 1] - P.seg_cam_off[s]);
+    }
+    const int64_t v[8] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), P.n_prof_blocks(),
+                          P.n_te, max_pairs, max_slots, max_cams};
+    k = std::min(n, 8);
+    for (int i = 0; i < k; ++i) out[i] = v[i];
   });
   return g != VO_OK ? g : k;
 }

@@ -1,0 +1,88 @@
+"""``VOConfig`` / ``get_config`` -- same fields, defaults and per-dataset values as
+the reference (``src/config/config.py:4-104``), plus the BA knobs of the MI355X
+back end (off by default, so behaviour equals the reference).
+
+The per-dataset tuning is kept as data (``_DATASET_OVERRIDES``).  The reference
+applies its ``extractor_type == "sift"`` overrides right after building a
+default config whose extractor is always ``"superpoint"`` (``config.py:9,51``),
+so they never fire (SURVEY.md §5 "Quirk").  ``get_config(dataset)`` reproduces
+that exactly; ``get_config(dataset, extractor_type="sift")`` is the documented
+extension that selects SIFT and applies those overrides.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+@dataclass
+class VOConfig:
+    """Configuration of the VO pipeline (field set of reference config.py:4-46)."""
+
+    extractor_type: str = "superpoint"  # superpoint or sift
+    global_scale: float = 20.0
+    max_keypoints: int = 2048
+    device: str = "cuda"
+    sift_n_features: int = 2048
+    sift_contrast_threshold: float = 0.03
+    sift_edge_threshold: float = 1.0
+    sift_sigma: float = 1.6
+    min_median_flow: float = 20.0
+    min_inliers: int = 10
+    init_ransac_prob: float = 0.999
+    init_ransac_thresh: float = 1.0
+    min_depth: float = 0.001
+    max_reproj_err: float = 6.0
+    pnp_reproj_err: float = 4.0
+    kf_min_tracked: int = 80
+    turn_thresh: float = 0.01
+    move_thresh: float = 0.01
+    turn_smoothing: float = 0.7
+    trans_smoothing: float = 0.6
+    baseline_lr: float = 0.01
+    scale_clamp_min: float = 0.5
+    scale_clamp_max: float = 3.0
+    # ---- MI355X back end (not in the reference) --------------------------------
+    ba_enabled: bool = False  # sliding-window BA at keyframe creation
+    ba_window: int = 50  # keyframes in the window
+    ba_fixed: int = 2  # oldest keyframes held fixed (gauge)
+    ba_iters: int = 10  # Gauss-Newton iterations per keyframe
+    ba_lambda: float = 1.0  # fixed Levenberg damping (identical in oracle and kernel)
+    match_on_gpu: bool = True  # SIFT matching on the MI355X (knn-2 + ratio test)
+
+
+# dataset -> (overrides always applied, overrides applied when extractor is SIFT)
+_DATASET_OVERRIDES = {
+    "kitti": (
+        dict(min_median_flow=40.0, max_keypoints=2048, max_reproj_err=5.0, pnp_reproj_err=1.0,
+             baseline_lr=0.002, turn_smoothing=0.2, trans_smoothing=0.4),
+        dict(sift_n_features=4000, sift_contrast_threshold=0.02, sift_edge_threshold=2.0,
+             max_reproj_err=5.0, pnp_reproj_err=1.0, turn_smoothing=0.2, trans_smoothing=0.4),
+    ),
+    "malaga": (
+        dict(min_median_flow=30.0, max_keypoints=2048, max_reproj_err=5.0, pnp_reproj_err=2.0,
+             baseline_lr=0.003, turn_smoothing=0.5, trans_smoothing=0.3),
+        dict(sift_n_features=3000, sift_contrast_threshold=0.01, sift_edge_threshold=2.0,
+             max_reproj_err=10.0, min_median_flow=4.0),
+    ),
+    "parking": (
+        dict(min_median_flow=3.0, max_reproj_err=2.0, pnp_reproj_err=1.0),
+        dict(sift_n_features=3000, sift_contrast_threshold=0.01, sift_edge_threshold=2.0,
+             min_median_flow=4.0),
+    ),
+    "own": (dict(baseline_lr=0.001, turn_smoothing=0.2, trans_smoothing=0.6), {}),
+}
+
+
+def get_config(dataset: str, extractor_type: str | None = None) -> VOConfig:
+    """Config for ``dataset`` (reference config.py:49-104); unknown names get the defaults."""
+    cfg = VOConfig()
+    if extractor_type is not None:
+        cfg.extractor_type = extractor_type
+    base, sift = _DATASET_OVERRIDES.get(dataset, ({}, {}))
+    for k, v in base.items():
+        setattr(cfg, k, v)
+    if cfg.extractor_type == "sift":
+        for k, v in sift.items():
+            setattr(cfg, k, v)
+    return cfg
