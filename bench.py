@@ -70,7 +70,8 @@ def cpu_baseline_ba(p, lam: float, budget_s: float = 3.0):
                       f"window: {n} GN iterations in {dt:.2f} s on {threads} host threads"}
 
 
-def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: int = 3):
+def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: int = 3, traffic_all=None):
+    traffic_all = traffic_all or {}
     from visualodometry_amd import _lib, matcher
     from visualodometry_amd.synthetic import sift_like_pair
 
@@ -111,7 +112,7 @@ def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: 
                                f"{batch} frame pairs per call, knn2 + ratio 0.75", "calls": calls},
         "kernel_us": kern,
         "roofline": {"bound": "mfma", "kernel": "match_i8", "achieved": tops, "peak": I8_PEAK_TOPS,
-                     "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS, "traffic": None,
+                     "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS, "traffic": traffic_all.get("match_i8"),
                      "note": "int8 ops (2*128 per pair) per match_i8 launch / its HIP-event duration"},
     }
     # CPU baseline: C oracle on a bounded sample of query rows
@@ -138,8 +139,9 @@ def main() -> int:
     ap.add_argument("--lam", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-matcher", action="store_true")
-    ap.add_argument("--traffic-json", default=None,
-                    help="per-kernel HBM bytes per launch from a rocprofv3 --pmc pass")
+    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "traffic.json"),
+                    help="per-kernel HBM bytes per launch from the committed rocprofv3 --pmc passes "
+                         "(tools/pmc_traffic.py); the timed run itself is never profiled")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -213,9 +215,10 @@ def main() -> int:
     nbytes = ba_kernel_bytes(best, p.n_poses, p1 - p0, int(ptr[-1]), n_free, stats["profile_blocks"])
     avg_s = prof[best][0] / prof[best][1] / 1e3
     achieved = nbytes / avg_s / 1e9
-    traffic = None
+    traffic_all = {}
     if args.traffic_json and Path(args.traffic_json).exists():
-        traffic = json.loads(Path(args.traffic_json).read_text()).get(best)
+        traffic_all = json.loads(Path(args.traffic_json).read_text())
+    traffic = traffic_all.get(best)
     lin_bytes = ba_kernel_bytes("ba_lin", p.n_poses, p1 - p0, int(ptr[-1]), n_free, stats["profile_blocks"])
     lin_avg = prof["ba_lin"][0] / prof["ba_lin"][1] / 1e3
     line = {
@@ -256,7 +259,7 @@ def main() -> int:
         line["cpu_baseline"] = cpu_baseline_ba(p, args.lam)
         line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
     if rank == 0 and world == 1 and not args.no_matcher:
-        line["secondary"] = bench_matcher(ctx)
+        line["secondary"] = bench_matcher(ctx, traffic_all=traffic_all)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

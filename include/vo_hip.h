@@ -133,7 +133,7 @@ int vo_ba_run_async(vo_ctx* ctx, int iters);
  * S_out: dense (6F, 6F) float64 reduced camera matrix with F = n_poses-n_fixed
  * (may be NULL), b_out: (6F), dc_out: (6F) pose update (may be NULL),
  * cost_out: 1 double.  The state is advanced by the step. */
-int vo_ba_step_debug(vo_ctx* ctx, double* S_out, double* b_out, double* dc_out,
+int vo_ba_gn_step(vo_ctx* ctx, double* S_out, double* b_out, double* dc_out,
                      double* cost_out);
 /* One-call convenience: setup + set_state + run + get_state. */
 int vo_ba_solve(vo_ctx* ctx, const vo_ba_problem* prob, double* poses, double* points,

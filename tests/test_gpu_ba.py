@@ -31,7 +31,7 @@ def _session(p, ctx, lam=1.0):
 def test_step_matches_numpy_oracle(ctx, lam):
     p = make_ba_problem(8, 300, 21)
     s = _session(p, ctx, lam)
-    rc, S, b, dc, cost = s.step_debug()
+    rc, S, b, dc, cost = s.gn_step()
     assert rc == _lib.VO_OK
     st = ba_ref.BAState.from_poses(p.poses_cw, p.points)
     struct = ba_ref.BAStructure(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_fixed, p.n_poses)
@@ -127,7 +127,7 @@ def test_degenerate_landmarks_frozen(ctx):
     cam2[ptr2[2] : ptr2[3]] = np.arange(ptr2[3] - ptr2[2]) % 2
     s = BASession(p.K, ptr2, cam2, uv2, p.n_poses, 2, 0.0, ctx)  # no damping: 1-obs V is singular
     s.set_state(p.poses_cw, p.points)
-    rc, S, b, dc, cost = s.step_debug()
+    rc, S, b, dc, cost = s.gn_step()
     assert rc == _lib.VO_OK
     st = ba_ref.BAState.from_poses(p.poses_cw, p.points)
     struct = ba_ref.BAStructure(p.K, ptr2, cam2, uv2, 2, p.n_poses)

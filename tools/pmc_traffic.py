@@ -1,0 +1,65 @@
+"""HBM traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+Follows /opt/skills/guides/MI355X_MICROARCH.md §HBM: the counters are in KB
+(x1024), and on gfx950 FETCH_SIZE tallies exactly half the bytes of a wide
+coalesced read, so reads are doubled.  The two counters cannot share a pass
+(TCC slots), hence two runs of the same command.
+
+    python tools/pmc_traffic.py FETCH_DIR/run_counter_collection.csv \
+        WRITE_DIR/run_counter_collection.csv -o profiles/traffic.json
+"""
+
+import argparse
+import csv
+import json
+from collections import defaultdict
+
+SHORT = [("ba_lin_kernel", "ba_lin"), ("ba_reduce_kernel", "ba_reduce"), ("ba_solve_kernel", "ba_solve"),
+         ("pack_kernel", "match_pack"), ("match_i8_kernel", "match_i8"), ("match_f32_kernel", "match_f32"),
+         ("merge_ratio_kernel", "match_merge"), ("compact_kernel", "match_compact")]
+
+
+def short_name(kernel: str):
+    for key, s in SHORT:
+        if key in kernel:
+            return s
+    return None
+
+
+def per_launch(path: str, counter: str):
+    acc = defaultdict(float)  # (short, dispatch) -> value (summed over counter instances)
+    with open(path, newline="") as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != counter:
+                continue
+            s = short_name(row["Kernel_Name"])
+            if s:
+                acc[(s, row["Dispatch_Id"])] += float(row["Counter_Value"])
+    out = defaultdict(list)
+    for (s, _), v in acc.items():
+        out[s].append(v)
+    return {s: sum(v) / len(v) for s, v in out.items()}, {s: len(v) for s, v in out.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_csv")
+    ap.add_argument("write_csv")
+    ap.add_argument("-o", "--out", required=True)
+    a = ap.parse_args()
+    fetch, nf = per_launch(a.fetch_csv, "FETCH_SIZE")
+    write, nw = per_launch(a.write_csv, "WRITE_SIZE")
+    res = {"_method": "bytes/launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024, gfx950 FETCH_SIZE half-count "
+                      "correction per MI355X_MICROARCH.md; separate --pmc passes",
+           "_raw_kb": {}}
+    for s in sorted(set(fetch) | set(write)):
+        fk, wk = fetch.get(s, 0.0), write.get(s, 0.0)
+        res[s] = (2 * fk + wk) * 1024
+        res["_raw_kb"][s] = {"FETCH_SIZE": fk, "WRITE_SIZE": wk, "launches": [nf.get(s, 0), nw.get(s, 0)]}
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -76,7 +76,7 @@ SIGNATURES = {
     "vo_ba_get_state": (_I, [_P, _PD, _PD]),
     "vo_ba_run": (_I, [_P, _I, _PD]),
     "vo_ba_run_async": (_I, [_P, _I]),
-    "vo_ba_step_debug": (_I, [_P, _PD, _PD, _PD, _PD]),
+    "vo_ba_gn_step": (_I, [_P, _PD, _PD, _PD, _PD]),
     "vo_ba_solve": (_I, [_P, C.POINTER(BAProblemC), _PD, _PD, _I, _PD]),
     "vo_ba_plan_stats": (_I, [_P, _PI64, _I]),
     "vo_ba_debug_stamps": (_I, [_P, C.POINTER(C.c_uint64), _I]),

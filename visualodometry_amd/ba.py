@@ -157,17 +157,17 @@ class BASession:
     def synchronize(self) -> None:
         check(self.ctx.lib.vo_synchronize(self.ctx.handle), "vo_synchronize")
 
-    def step_debug(self):
+    def gn_step(self):
         """One GN step exporting (rc, S dense, b, dc, cost-before-step)."""
         F = self.n_poses - self.n_fixed
         S = np.empty((6 * F, 6 * F))
         b = np.empty(6 * F)
         dc = np.empty(6 * F)
         cost = np.empty(1)
-        rc = self.ctx.lib.vo_ba_step_debug(self.ctx.handle, ptr(S, C.c_double), ptr(b, C.c_double),
+        rc = self.ctx.lib.vo_ba_gn_step(self.ctx.handle, ptr(S, C.c_double), ptr(b, C.c_double),
                                            ptr(dc, C.c_double), ptr(cost, C.c_double))
         if rc not in (_lib.VO_OK, _lib.VO_ERR_NOT_SPD):
-            check(rc, "vo_ba_step_debug")
+            check(rc, "vo_ba_gn_step")
         return rc, S, b, dc, float(cost[0])
 
     def plan_stats(self) -> dict:

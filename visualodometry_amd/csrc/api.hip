@@ -67,7 +67,7 @@ void ba_setup(vo_ctx*, const vo_ba_problem*);
 void ba_set_state(vo_ctx*, const double*, const double*);
 void ba_get_state(vo_ctx*, double*, double*);
 int ba_run(vo_ctx*, int, double*, bool);
-int ba_step_debug(vo_ctx*, double*, double*, double*, double*);
+int ba_gn_step(vo_ctx*, double*, double*, double*, double*);
 int ba_stats(vo_ctx*, int64_t*, int);
 int ba_stamps(vo_ctx*, uint64_t*, int);
 void comm_unique_id(char out[128]);
@@ -272,11 +272,11 @@ int vo_ba_run_async(vo_ctx* ctx, int iters) {
   });
 }
 
-int vo_ba_step_debug(vo_ctx* ctx, double* S_out, double* b_out, double* dc_out, double* cost_out) {
+int vo_ba_gn_step(vo_ctx* ctx, double* S_out, double* b_out, double* dc_out, double* cost_out) {
   int rc = VO_OK;
   int g = guarded([&] {
     vo::bind(ctx);
-    rc = vo::ba_step_debug(ctx, S_out, b_out, dc_out, cost_out);
+    rc = vo::ba_gn_step(ctx, S_out, b_out, dc_out, cost_out);
   });
   return g != VO_OK ? g : rc;
 }

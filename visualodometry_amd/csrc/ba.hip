@@ -1082,7 +1082,7 @@ class BAEngine {
     return VO_OK;
   }
 
-  int step_debug(double* S_out, double* b_out, double* dc_out, double* cost_out) {
+  int gn_step(double* S_out, double* b_out, double* dc_out, double* cost_out) {
     require_state();
     hipStream_t st = ctx_->stream;
     const BAPlan& P = plan_;
@@ -1119,7 +1119,7 @@ class BAEngine {
     if (status) {
       VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
       VO_HIP_CHECK(hipStreamSynchronize(st));
-      set_error("vo_ba_step_debug: reduced camera system not positive definite");
+      set_error("vo_ba_gn_step: reduced camera system not positive definite");
       return VO_ERR_NOT_SPD;
     }
     return VO_OK;
@@ -1141,10 +1141,12 @@ class BAEngine {
     VO_REQUIRE(have_state_, VO_ERR_STATE, "BA: no state set");
   }
 
-  // K1 workgroups: two per CU (its LDS footprint admits two), overridable for tuning.
+  // Planner target of 4 segments per CU (K1's LDS footprint admits two resident
+  // workgroups per CU; the planner's chunk packing leaves ~2.6 per CU at cfg3,
+  // measured best of 128..2048 -- profiles/r01_segment_sweep.md).  Overridable.
   static int segments_target(int num_cus) {
     const char* e = getenv("VO_BA_SEGMENTS");
-    return e ? std::max(1, atoi(e)) : 2 * std::max(1, num_cus);
+    return e ? std::max(1, atoi(e)) : 4 * std::max(1, num_cus);
   }
 
   LinArgs lin_args() {
@@ -1378,8 +1380,8 @@ void ba_set_state(vo_ctx* ctx, const double* poses, const double* pts) {
 }
 void ba_get_state(vo_ctx* ctx, double* poses, double* pts) { ba_engine(ctx)->get_state(poses, pts); }
 int ba_run(vo_ctx* ctx, int iters, double* cost, bool sync) { return ba_engine(ctx)->run(iters, cost, sync); }
-int ba_step_debug(vo_ctx* ctx, double* S, double* b, double* dc, double* cost) {
-  return ba_engine(ctx)->step_debug(S, b, dc, cost);
+int ba_gn_step(vo_ctx* ctx, double* S, double* b, double* dc, double* cost) {
+  return ba_engine(ctx)->gn_step(S, b, dc, cost);
 }
 int ba_stats(vo_ctx* ctx, int64_t* out, int n) { return ba_engine(ctx)->stats(out, n); }
 int ba_stamps(vo_ctx* ctx, uint64_t* out, int n) { return ba_engine(ctx)->read_stamps(out, n); }

@@ -12,6 +12,7 @@ extension that selects SIFT and applies those overrides.
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 
@@ -75,8 +76,18 @@ _DATASET_OVERRIDES = {
 
 
 def get_config(dataset: str, extractor_type: str | None = None) -> VOConfig:
-    """Config for ``dataset`` (reference config.py:49-104); unknown names get the defaults."""
+    """Config for ``dataset`` (reference config.py:49-104); unknown names get the defaults.
+
+    ``src/main.py`` calls ``get_config(dataset)`` only (``main.py:54``), so two
+    environment switches reach the back end without touching it:
+    ``VO_AMD_EXTRACTOR=sift`` (as ``extractor_type``) and ``VO_AMD_BA=1``
+    (``ba_enabled``).  Unset, the result equals the reference's.
+    """
     cfg = VOConfig()
+    if extractor_type is None:
+        extractor_type = os.environ.get("VO_AMD_EXTRACTOR") or None
+    if os.environ.get("VO_AMD_BA", "0") not in ("", "0"):
+        cfg.ba_enabled = True
     if extractor_type is not None:
         cfg.extractor_type = extractor_type
     base, sift = _DATASET_OVERRIDES.get(dataset, ({}, {}))

@@ -1,0 +1,225 @@
+"""Runtime hooks that put the MI355X matcher and BA under the reference's VO loop.
+
+Nothing of the reference is copied: :func:`install` patches two methods of the
+reference's own classes once they are imported (cv2 etc. are the caller's
+environment):
+
+* ``FeatureFrontend.match_frames`` (reference ``src/modules/frontend.py:78-113``),
+  SIFT branch -> :func:`visualodometry_amd.matcher.match_knn2_ratio`.  The
+  LightGlue branch (``:80-84``) is left to the original method.
+* ``VisualOdometry._create_keyframe`` (``src/modules/vo.py:252-288``) is wrapped:
+  the original triangulates and rotates the keyframe, then
+  :class:`KeyframeWindow` records the new keyframe and, if ``cfg.ba_enabled``,
+  runs :class:`~visualodometry_amd.ba.SlidingWindowBA` on the last
+  ``cfg.ba_window`` keyframes and writes poses and map points back
+  (SURVEY.md §8a row a11).
+
+The reference keeps only the current keyframe's observation of a freshly
+triangulated point (``vo.py:277-284``); the window also records the previous
+keyframe's observation of it (the other ray of the triangulation), which is
+what makes a two-keyframe landmark constrain BA at all.
+"""
+
+from __future__ import annotations
+
+from collections import deque
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ..ba import BAResult, BAWindow, SlidingWindowBA
+
+
+def _np(x) -> np.ndarray:
+    if hasattr(x, "detach"):
+        x = x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def _keypoints(feats: dict) -> np.ndarray:
+    kp = _np(feats["keypoints"])
+    return kp[0] if kp.ndim == 3 else kp
+
+
+@dataclass
+class KeyframeRecord:
+    T_wc: np.ndarray  # (4,4) f64 camera -> world (the reference's pose storage, vo.py:19)
+    uv: np.ndarray  # (N,2) f32 keypoints
+    ids: np.ndarray  # (N,) int landmark id per keypoint, -1 if none
+    extra_uv: list = field(default_factory=list)  # observations added after the keyframe was made
+    extra_ids: list = field(default_factory=list)
+
+
+class KeyframeWindow:
+    """The last ``size`` keyframes and their landmark observations.
+
+    ``max_track`` caps the observations of one landmark to its most recent
+    keyframes: the BA planner handles at most 10 free cameras per landmark
+    (DESIGN.md §BA layout).
+    """
+
+    def __init__(self, size: int = 50, n_fixed: int = 2, max_track: int = 10):
+        self.size = int(size)
+        self.n_fixed = int(n_fixed)
+        self.max_track = int(max_track)
+        self.frames: deque[KeyframeRecord] = deque(maxlen=self.size)
+
+    def reset(self) -> None:
+        self.frames.clear()
+
+    def add(self, T_wc, uv, ids, prev_uv=None, prev_ids=None) -> None:
+        """Append a keyframe; ``prev_uv/prev_ids`` are new observations of the previous keyframe."""
+        if prev_ids is not None and len(prev_ids) and self.frames:
+            last = self.frames[-1]
+            last.extra_uv.append(np.asarray(prev_uv, np.float32).reshape(-1, 2))
+            last.extra_ids.append(np.asarray(prev_ids, np.int64))
+        self.frames.append(KeyframeRecord(np.array(T_wc, np.float64), np.asarray(uv, np.float32).reshape(-1, 2),
+                                          np.array(ids, np.int64)))
+
+    def observations(self, map_points: dict):
+        """-> (obs_kf, obs_uv, obs_id) of every window observation of a landmark still in the map."""
+        kf, uv, pid = [], [], []
+        for k, fr in enumerate(self.frames):
+            us = [fr.uv] + fr.extra_uv
+            ids = [fr.ids] + fr.extra_ids
+            u = np.concatenate(us)
+            i = np.concatenate(ids)
+            keep = (i >= 0) & np.fromiter((int(x) in map_points for x in i), bool, i.size)
+            kf.append(np.full(int(keep.sum()), k, np.int32))
+            uv.append(u[keep])
+            pid.append(i[keep])
+        if not kf:
+            return np.zeros(0, np.int32), np.zeros((0, 2), np.float32), np.zeros(0, np.int64)
+        return np.concatenate(kf), np.concatenate(uv), np.concatenate(pid)
+
+    def build(self, map_points: dict):
+        """-> (BAWindow, landmark ids) or (None, None) if the window has nothing to adjust."""
+        if len(self.frames) <= self.n_fixed:
+            return None, None
+        kf, uv, pid = self.observations(map_points)
+        if pid.size == 0:
+            return None, None
+        # group by landmark, newest keyframe first; rank the distinct keyframes of each landmark
+        order = np.lexsort((-kf, pid))
+        kf, uv, pid = kf[order], uv[order], pid[order]
+        new_pt = np.r_[True, pid[1:] != pid[:-1]]
+        new_kf = new_pt | np.r_[True, kf[1:] != kf[:-1]]
+        grp = np.cumsum(new_pt) - 1
+        c = np.cumsum(new_kf)
+        kf_rank = c - c[new_pt][grp]  # 0 = newest keyframe of this landmark
+        keep = kf_rank < self.max_track
+        kf, uv, pid, grp, new_kf = kf[keep], uv[keep], pid[keep], grp[keep], new_kf[keep]
+        ids = pid[new_pt[keep]]  # the newest keyframe of every landmark is always kept
+        n_kf = np.bincount(grp, weights=new_kf, minlength=ids.size)
+        inv = grp
+        good = n_kf >= 2  # a landmark needs two distinct keyframes to be constrained
+        if not good.any():
+            return None, None
+        sel = good[inv]
+        kf, uv, inv = kf[sel], uv[sel], inv[sel]
+        remap = -np.ones(ids.size, np.int64)
+        remap[good] = np.arange(int(good.sum()))
+        lm_ids = ids[good]
+        points = np.stack([np.asarray(map_points[int(i)], np.float64).reshape(3) for i in lm_ids])
+        poses_cw = np.stack([np.linalg.inv(fr.T_wc) for fr in self.frames])
+        w = BAWindow(poses_cw=poses_cw, points=points, obs_uv=uv.astype(np.float32), obs_cam=kf.astype(np.int32),
+                     obs_pt=remap[inv].astype(np.int32), n_fixed=self.n_fixed)
+        return w, lm_ids
+
+    def write_back(self, res: BAResult, lm_ids, map_points: dict) -> None:
+        for fr, P in zip(self.frames, res.poses_cw):
+            fr.T_wc = np.linalg.inv(P)
+        for i, X in zip(lm_ids, res.points):
+            old = map_points[int(i)]
+            map_points[int(i)] = np.asarray(X, dtype=np.asarray(old).dtype).reshape(np.shape(old))
+
+
+def _wrap_create_keyframe(orig):
+    def _create_keyframe(self, curr_feats, curr_ids, ref_indices, curr_indices):
+        cfg = self.cfg
+        win = getattr(self, "_vo_amd_window", None)
+        if win is None:
+            win = KeyframeWindow(getattr(cfg, "ba_window", 50), getattr(cfg, "ba_fixed", 2))
+            self._vo_amd_window = win
+        prev = self.keyframe
+        if prev is not None and not win.frames:  # the window starts at the keyframe before the first
+            win.add(prev["T_wc"], _keypoints(prev["feats"]), prev["ids"])
+        first_new = self.next_pt_id
+        ref_indices = np.asarray(ref_indices)
+        curr_indices = np.asarray(curr_indices)
+        no_id = curr_ids[curr_indices] == -1
+        orig(self, curr_feats, curr_ids, ref_indices, curr_indices)
+        # the previous keyframe saw every newly triangulated point (vo.py:265-284)
+        cand = curr_indices[no_id]
+        new_ids = curr_ids[cand]
+        # a current keypoint matched by several reference keypoints (no cross-check,
+        # frontend.py:34) had its id overwritten in the loop: its other ray is ambiguous
+        uniq, cnt = np.unique(cand, return_counts=True)
+        is_new = (new_ids >= first_new) & np.isin(cand, uniq[cnt == 1])
+        prev_uv = _keypoints(prev["feats"])[ref_indices[no_id][is_new]] if prev is not None else None
+        win.add(self.T_wc, _keypoints(curr_feats), curr_ids, prev_uv, new_ids[is_new])
+        if getattr(cfg, "ba_enabled", False):
+            self._vo_amd_last_ba = run_window_ba(self, win)
+
+    _create_keyframe._vo_amd_wrapped = orig
+    return _create_keyframe
+
+
+def run_window_ba(vo, win: KeyframeWindow):
+    """Adjust the window and write poses/points back into the VO state; never raises on bad windows."""
+    window, lm_ids = win.build(vo.map_points)
+    if window is None:
+        return None
+    cfg = vo.cfg
+    ba = getattr(vo, "_vo_amd_ba", None)
+    if ba is None:
+        ba = SlidingWindowBA(vo.K, cfg)
+        vo._vo_amd_ba = ba
+    res = ba.optimize(window)
+    if res.status != "ok" or not np.all(np.isfinite(res.cost_per_iter)) or \
+            res.cost_per_iter[-1] > res.cost_per_iter[0]:
+        print(f"BA: window rejected ({res.status} {res.message})")
+        return res
+    win.write_back(res, lm_ids, vo.map_points)
+    T_wc = win.frames[-1].T_wc.copy()
+    vo.T_wc = T_wc
+    vo.keyframe["T_wc"] = T_wc.copy()
+    vo.last_pos = T_wc[:3, 3].copy()
+    return res
+
+
+def _wrap_reset(orig):
+    def _reset_system(self):
+        orig(self)
+        win = getattr(self, "_vo_amd_window", None)
+        if win is not None:
+            win.reset()
+
+    _reset_system._vo_amd_wrapped = orig
+    return _reset_system
+
+
+def _wrap_match_frames(orig):
+    from .. import matcher
+
+    def match_frames(self, feats0, feats1):
+        if getattr(self.conf, "extractor_type", None) == "sift" and getattr(self.conf, "match_on_gpu", True):
+            return matcher.match_knn2_ratio(feats0["descriptors"], feats1["descriptors"])
+        return orig(self, feats0, feats1)
+
+    match_frames._vo_amd_wrapped = orig
+    return match_frames
+
+
+def install(frontend_cls=None, vo_cls=None) -> None:
+    """Patch the reference classes (imported from ``modules.*`` when not given). Idempotent."""
+    if frontend_cls is None:
+        from modules.frontend import FeatureFrontend as frontend_cls  # the reference's module
+    if vo_cls is None:
+        from modules.vo import VisualOdometry as vo_cls
+    if not hasattr(frontend_cls.match_frames, "_vo_amd_wrapped"):
+        frontend_cls.match_frames = _wrap_match_frames(frontend_cls.match_frames)
+    if not hasattr(vo_cls._create_keyframe, "_vo_amd_wrapped"):
+        vo_cls._create_keyframe = _wrap_create_keyframe(vo_cls._create_keyframe)
+    if not hasattr(vo_cls._reset_system, "_vo_amd_wrapped"):
+        vo_cls._reset_system = _wrap_reset(vo_cls._reset_system)
