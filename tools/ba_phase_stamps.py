@@ -18,7 +18,7 @@ from visualodometry_amd.ba import BASession  # noqa: E402
 from visualodometry_amd.synthetic import make_ba_config  # noqa: E402
 
 PHASES = ["load", "backsub", "lin_obs", "reduce", "eliminate", "schur", "write"]
-K3 = ["k3_setup", "k3_factor", "k3_w0_dupdate", "k3_barrier", "k3_backsub+update", "k3_w0_store", "k3_w0_panel"]
+K3 = ["k3_setup", "k3_factor(rest)", "k3_backsub", "k3_tail", "k3_data", "k3_chol", "k3_panel", "k3_trail", "k3_barrier"]
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg3"
 p = make_ba_config(cfg)

@@ -58,7 +58,7 @@ struct Comm {
 namespace {
 
 constexpr int kLinThreads = 128;
-constexpr int kSolveThreads = 256;
+constexpr int kBsWindow = 10;  // K3 back substitution: register window of block rows
 constexpr double kPivotRelEps = 1e-12;  // == oracle/ba_ref.py PIVOT_REL_EPS
 constexpr double kExpTaylor = 1e-4;     // == oracle/ba_ref.py EXP_TAYLOR_THETA
 enum { kBacksub = 1, kAccum = 2 };
@@ -525,9 +525,11 @@ __global__ __launch_bounds__(64) void ba_reduce_kernel(ReduceArgs A) {
 // K3: profile Cholesky solve S dc = b + pose update.
 struct SolveArgs {
   int F, nprof, n_poses, n_fixed, iter_tag;
-  const int* prof_first;
-  const int* prof_off;
-  const int* prof_last;
+  int max_panel, max_row_span;  // most panel blocks in a column; max k - first[k]
+  long lds_kf, lds_y, lds_panel, lds_tab;  // LDS offsets in doubles (solve_lds_layout)
+  SolveTableLayout tl;
+  const int* tab;      // BAPlan::solve_tab
+  double* cost_out;    // if set: receives the cost of this linearisation (sys tail)
   double* sys;         // [S profile | b | cost]; factorised in place on the global path
   double* dc;          // 6F out
   const double* pose_cur;
@@ -546,7 +548,8 @@ __device__ __forceinline__ void se3_exp_apply(const double* d, const double* T, 
     B = 0.5 - th2 / 24.0;
     C = 1.0 / 6.0 - th2 / 120.0;
   } else {
-    const double s = sin(th), c = cos(th);
+    double s, c;
+    sincos(th, &s, &c);
     A = s / th;
     B = (1.0 - c) / (th * th);
     C = (th - s) / (th * th * th);
@@ -583,8 +586,9 @@ __device__ __forceinline__ void se3_exp_apply(const double* d, const double* T, 
 // ---- 6x6 block kernels in registers (packed lower storage, P(i,c) = i(i+1)/2 + c)
 __device__ __forceinline__ constexpr int P6(int i, int c) { return i * (i + 1) / 2 + c; }
 
-// In-place Cholesky a = L L^T; r = 1/diag(L) from v_rsq_f64 + two Newton steps
-// (critical chain per column: rsq + 6 dependent FMAs instead of sqrt + divide).
+// In-place Cholesky a = L L^T; r = 1/diag(L) from v_rsq_f64 + one Newton step
+// (critical chain per column: rsq + 3 dependent ops instead of sqrt + divide; the
+// step takes the ~2^-23 estimate to ~1e-14 relative).
 __device__ __forceinline__ bool chol6(double (&a)[21], double (&r)[6]) {
   bool ok = true;
 #pragma unroll
@@ -593,7 +597,6 @@ __device__ __forceinline__ bool chol6(double (&a)[21], double (&r)[6]) {
     ok = ok && d > 0.0;
     const double dd = d > 0.0 ? d : 1.0;
     double q = __builtin_amdgcn_rsq(dd);
-    q = q * (1.5 - 0.5 * dd * q * q);
     q = q * (1.5 - 0.5 * dd * q * q);
     r[j] = q;
     a[P6(j, j)] = dd * q;
@@ -648,21 +651,41 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // K3.  Right-looking 6x6-block Cholesky of the profile of S with the forward
-// substitution folded in, then back substitution and the pose update.
-// Phase k (one barrier each), with D_k final at the barrier:
-//   every wave  factors D_k redundantly in registers (no LDS hand-off of L_kk).
-//   wave 0      stores L_kk and y'_k = L_kk^-1 y_k; owns row k+1: its panel block
-//               (steps k-2, k-1 applied on the fly), y_{k+1}, and D_{k+1} -= steps
-//               k-1 and k  -- the critical chain to the next phase.
-//   waves 1-3   trailing update of step k-1 on columns >= k+2, then panel rows
-//               i >= k+2: L_ik = (S_ik - L_i,k-2 L_k,k-2^T - L_i,k-1 L_k,k-1^T) L_kk^-T
-//               and y_i -= L_ik y'_k.
-// Column j > m receives step m exactly once: in the panel of phase j (m = j-2,
-// j-1), from wave 0 in phase j-1 (diagonal block, m = j-2, j-1), else from the
-// trailing update of phase m+1 (j >= m+3).
-enum { kS3Setup = 0, kS3Factor, kS3Wave0, kS3Barrier, kS3Backsub, kS3Store, kS3Panel, kS3Count };
-template <bool kLds, bool kStamp = false>
-__global__ __launch_bounds__(kSolveThreads) void ba_solve_kernel(SolveArgs A) {
+// substitution folded in, then back substitution and the pose update; one
+// workgroup of four waves, one barrier per block column k:
+//   every wave   reads D_k, factors it in registers (L_kk, 1/diag) and computes the
+//                WHOLE panel L_ik = S_ik L_kk^-T (one lane per row) into its own
+//                private LDS copy -- so the trailing update below needs no barrier;
+//   trailing     S_ij -= L_ik L_jk^T over the panel's lower block triangle (this
+//                includes D_{k+1}), one lane per (block, row), rows interleaved over
+//                the waves, each reading only its own wave's panel copy;
+//   wave 1       y_i -= L_ik y'_k with y'_k = L_kk^-1 y_k;
+//   wave 2       keeps L_kk, 1/diag and y'_k for the back substitution;
+//   wave 3       (next column) writes the panel into the profile blocks (i, k).
+// The per-column panel rows and trailing blocks come from the host-built step
+// table (BAPlan::solve_tab), staged in LDS with the profile.
+enum { kS3Setup = 0, kS3Factor, kS3Backsub, kS3Tail, kS3Data, kS3Chol, kS3Panel, kS3Trail, kS3Barrier, kS3Count };
+
+struct SolveLds {
+  size_t prof, kf, y, panel, tab, total;
+};
+// LDS image: [profile 36*nprof (LDS path)] [per column: L 21 + pad 3 | r 6 | y'/x 6]
+// [y 6F] [4 private panels, 36 doubles per block] [step table ints]
+SolveLds solve_lds_layout(bool lds_profile, int nprof, int F, int max_panel, int tab_len) {
+  SolveLds L;
+  L.prof = 0;
+  L.kf = lds_profile ? 36ull * nprof : 0;
+  L.y = L.kf + 36ull * F;
+  L.panel = L.y + 6ull * F;
+  L.tab = L.panel + 4ull * 36 * std::max(1, max_panel);
+  L.total = L.tab * 8 + 4ull * std::max(1, tab_len);
+  return L;
+}
+
+template <bool kLds, bool kStamp, int NW>
+__global__ __launch_bounds__(64 * NW) void ba_solve_kernel(SolveArgs A) {
+  constexpr int kThr = 64 * NW;
+  constexpr int wY = NW > 1 ? 1 : 0, wK = NW > 2 ? 2 : NW - 1, wC = NW - 1;  // role waves
   unsigned long long st_t = 0, st_acc[kS3Count] = {};
   auto mark = [&](int ph) {
     if (kStamp && threadIdx.x == 0) {
@@ -672,46 +695,67 @@ __global__ __launch_bounds__(kSolveThreads) void ba_solve_kernel(SolveArgs A) {
     }
   };
   mark(0);
+  // stamped build only: wait for outstanding LDS / a VALU result before a stamp
+  auto settle = [&](double v) {
+    if (kStamp) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      (void)__builtin_amdgcn_readfirstlane(__double2hiint(v));
+    }
+  };
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int s_fail;
   const int tid = threadIdx.x, F = A.F;
   const int wave = tid >> 6, lane = tid & 63;
   const bool prior_fail = A.status && *A.status;
-  double* Sm;
-  double* aux;  // Ld (21 per block row), rd (6), y (6), ys (6)
-  if (kLds) {
-    Sm = dyn;
-    aux = dyn + 36l * A.nprof;
-  } else {
-    Sm = A.sys;
-    aux = dyn;
+  double* Sm = kLds ? dyn : A.sys;
+  double* kf = dyn + A.lds_kf;       // 36 per column
+  double* y = dyn + A.lds_y;         // 6F
+  double* Pw = dyn + A.lds_panel + 36l * A.max_panel * wave;  // this wave's panel copy
+  int* tab = reinterpret_cast<int*>(dyn + A.lds_tab);
+  const int* t_diag = tab + A.tl.diag;
+  const int* t_off = tab + A.tl.off;
+  const int* t_first = tab + A.tl.first;
+  const int* t_sptr = tab + A.tl.step_ptr;
+  const int* t_pi = tab + A.tl.panel_i;
+  const int* t_pblk = tab + A.tl.panel_blk;
+  const int* t_iptr = tab + A.tl.item_ptr;
+  const int* t_iblk = tab + A.tl.item_blk;
+  const int* t_iq = tab + A.tl.item_q;
+  if (tid == 0) {
+    s_fail = prior_fail ? 1 : 0;
+    if (A.cost_out) *A.cost_out = A.sys[36l * A.nprof + 6l * F];
   }
-  double* Ld = aux;                        // packed L_kk
-  double* rd = Ld + 21l * F + (F & 1);     // 1 / diag(L_kk) (16-B aligned)
-  double* y = rd + 6l * F;    // right-hand side, updated by the panel lanes
-  double* ys = y + 6l * F;    // y'_k = L_kk^-1 y_k, then x (back substitution)
-  int* first = reinterpret_cast<int*>(ys + 6l * F + 36);  // after the 36-double wave-0 scratch
-  int* off = first + F;
-  int* last = off + F + 1;
-  if (tid == 0) s_fail = prior_fail ? 1 : 0;
   if (!prior_fail) {
-    if (kLds)
-      for (int e = tid; e < 36 * A.nprof; e += kSolveThreads) Sm[e] = A.sys[e];
-    for (int e = tid; e < 6 * F; e += kSolveThreads) y[e] = A.sys[36l * A.nprof + e];
-    for (int i = tid; i < F; i += kSolveThreads) {
-      first[i] = A.prof_first[i];
-      last[i] = A.prof_last[i];
+    if (kLds) {  // profile -> LDS: 16-byte loads, four in flight per thread
+      const double2* src = reinterpret_cast<const double2*>(A.sys);
+      double2* dst = reinterpret_cast<double2*>(Sm);
+      const int n2 = 18 * A.nprof;
+      int e = tid;
+      for (; e + 7 * kThr < n2; e += 8 * kThr) {
+        double2 a[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = src[e + u * kThr];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dst[e + u * kThr] = a[u];
+      }
+      for (; e < n2; e += kThr) dst[e] = src[e];
     }
-    for (int i = tid; i <= F; i += kSolveThreads) off[i] = A.prof_off[i];
+    for (int e = tid; e < 6 * F; e += kThr) y[e] = A.sys[36l * A.nprof + e];
+    for (int e = tid; e < A.tl.len; e += kThr) tab[e] = A.tab[e];
   }
   __syncthreads();
   mark(kS3Setup);
 
-  // 6-double row loads as three 16-byte LDS reads (blocks are 288 B, rows 48 B)
   auto ld6 = [](const double* p, double (&v)[6]) {
     const double2* q = reinterpret_cast<const double2*>(p);
     const double2 a0 = q[0], a1 = q[1], a2 = q[2];
     v[0] = a0.x; v[1] = a0.y; v[2] = a1.x; v[3] = a1.y; v[4] = a2.x; v[5] = a2.y;
+  };
+  auto st6 = [](double* p, const double (&v)[6]) {
+    double2* q = reinterpret_cast<double2*>(p);
+    q[0] = make_double2(v[0], v[1]);
+    q[1] = make_double2(v[2], v[3]);
+    q[2] = make_double2(v[4], v[5]);
   };
   auto dot6 = [](const double (&u)[6], const double* w) {
     const double2* q = reinterpret_cast<const double2*>(w);
@@ -719,17 +763,54 @@ __global__ __launch_bounds__(kSolveThreads) void ba_solve_kernel(SolveArgs A) {
     return u[0] * a0.x + u[1] * a0.y + u[2] * a1.x + u[3] * a1.y + u[4] * a2.x + u[5] * a2.y;
   };
 
-  for (int k = 0; k < F && !s_fail; ++k) {
-    // uniform indices of this phase, one LDS round trip
-    const int j = k + 1;
-    const int fk = first[k], ok_ = off[k], lk = last[k];
-    const int fj = j < F ? first[j] : F, oj = j < F ? off[j] : 0;
-    const int lkm1 = k >= 1 ? last[k - 1] : k;
-    auto bk = [&](int col) { return Sm + 36l * (ok_ + col - fk); };  // block (k, col)
-    auto bj = [&](int col) { return Sm + 36l * (oj + col - fj); };   // block (k+1, col)
-    double L[21], r[6];
+  // Per-column descriptors from the static step table, loaded one column ahead so
+  // that after each barrier only the data loads (one LDS round trip) precede chol6.
+  struct Desc {
+    int p0, nb, i0, nt, diag, pblk, pi, blk0, q0;
+  };
+  const int tfi = lane * NW + wave;  // this lane's first trailing (block, row) item
+  auto desc1 = [&](int k, Desc& d) {
+    d.p0 = t_sptr[k];
+    d.nb = t_sptr[k + 1] - d.p0;
+    d.i0 = t_iptr[k];
+    d.nt = 6 * (t_iptr[k + 1] - d.i0);
+    d.diag = t_diag[k];
+  };
+  auto desc2 = [&](Desc& d) {
+    d.pblk = d.pi = d.blk0 = d.q0 = 0;
+    if (lane < 6 * d.nb) {
+      d.pblk = t_pblk[d.p0 + lane / 6];
+      d.pi = t_pi[d.p0 + lane / 6];
+    }
+    if (tfi < d.nt) {
+      d.blk0 = t_iblk[d.i0 + tfi / 6];
+      d.q0 = t_iq[d.i0 + tfi / 6];
+    }
+  };
+  Desc cur{}, nxt{};
+  if (F > 0 && !prior_fail) {
+    desc1(0, cur);
+    desc2(cur);
+  }
+  bool bad = false;
+  bool prev_row = false;
+  int prev_blk = 0, prev_p0 = 0, prev_nb = 0;
+  double sv[6] = {0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < F && !prior_fail; ++k) {
+    // wave 3: its previous panel row (still in registers) -> profile block (i, k-1), for
+    // the back substitution; nobody touches blocks (i, k-1) from column k on
+    if (wave == wC) {
+      if (prev_row) st6(Sm + 36l * prev_blk + 6 * (lane % 6), sv);
+      for (int r = lane + 64; r < 6 * prev_nb; r += 64) {
+        double v[6];
+        ld6(Pw + 6 * r, v);
+        st6(Sm + 36l * t_pblk[prev_p0 + r / 6] + 6 * (r % 6), v);
+      }
+    }
+    // data loads of column k
+    double L[21], r[6], yk[6], s0[6];
     {
-      const double* D = bk(k);
+      const double* D = Sm + 36l * cur.diag;
       double dr[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
@@ -738,166 +819,214 @@ __global__ __launch_bounds__(kSolveThreads) void ba_solve_kernel(SolveArgs A) {
         for (int c = 0; c <= i; ++c) L[P6(i, c)] = dr[c];
       }
     }
-    const bool ok = chol6(L, r);
-    double yk[6];
     ld6(y + 6 * k, yk);
-    fwd6(L, r, yk);
-    mark(kS3Factor);
-    if (wave == 0) {
-      if (lane < 21) Ld[21l * k + lane] = pick(L, lane);
-      if (lane < 6) {
-        rd[6l * k + lane] = pick(r, lane);
-        ys[6l * k + lane] = pick(yk, lane);
-      }
-      if (lane == 0 && !(ok && isfinite(yk[0] + yk[1] + yk[2] + yk[3] + yk[4] + yk[5]))) s_fail = 1;
-      mark(kS3Store);
-      // critical chain: row k+1 of the panel (wave 0 owns row k+1) -> y_{k+1},
-      // D_{k+1} -= steps k-1 and k
-      if (j < F && fj <= k) {
-        if (lane < 6) {
-          double* row = bj(k) + 6 * lane;
-          double sv[6], u0[6], u1[6];
-          ld6(row, sv);
-          const bool s0 = k >= 2 && fj <= k - 2 && fk <= k - 2;
-          const bool s1 = k >= 1 && fj <= k - 1 && fk <= k - 1;
-          if (s0) ld6(bj(k - 2) + 6 * lane, u0);
-          if (s1) ld6(bj(k - 1) + 6 * lane, u1);
-#pragma unroll
-          for (int c = 0; c < 6; ++c) {
-            double a = 0.0;
-            if (s0) a += dot6(u0, bk(k - 2) + 6 * c);
-            if (s1) a += dot6(u1, bk(k - 1) + 6 * c);
-            sv[c] -= a;
-          }
-          fwd6(L, r, sv);
-          double a = 0.0;
-#pragma unroll
-          for (int c = 0; c < 6; ++c) {
-            row[c] = sv[c];
-            a += sv[c] * yk[c];
-          }
-          y[6 * j + lane] -= a;
-        }
-        wave_sync<kLds>();
-        mark(kS3Panel);
-        if (lane < 36) {
-          const int rr = lane / 6, cc = lane % 6;
-          double u[6];
-          ld6(bj(k) + 6 * rr, u);
-          double a = dot6(u, bj(k) + 6 * cc);
-          if (k >= 1 && fj <= k - 1) {
-            ld6(bj(k - 1) + 6 * rr, u);
-            a += dot6(u, bj(k - 1) + 6 * cc);
-          }
-          bj(j)[lane] -= a;
-        }
-      } else if (j < F && k >= 1 && fj <= k - 1 && lane < 36) {
-        // row k+1 has no block in column k: D_{k+1} still owes step k-1
-        const int rr = lane / 6, cc = lane % 6;
-        double u[6];
-        ld6(bj(k - 1) + 6 * rr, u);
-        bj(j)[lane] -= dot6(u, bj(k - 1) + 6 * cc);
-      }
-      mark(kS3Wave0);
-    } else {
-      const int t0 = tid - 64, nt = kSolveThreads - 64;
-      // trailing update of step m = k-1 on columns >= k+2
-      if (k >= 1) {
-        const int m = k - 1;
-        const int n = lkm1 - (k + 1);
-        const int ntri = n > 0 ? n * (n + 1) / 2 : 0;
-        for (int item = t0; item < ntri * 6; item += nt) {
-          const int t = item / 6, rr = item % 6;
-          int di = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-          while ((di + 1) * (di + 2) / 2 <= t) ++di;
-          while (di * (di + 1) / 2 > t) --di;
-          const int dj = t - di * (di + 1) / 2;
-          const int i = k + 2 + di, jj = k + 2 + dj;
-          const int fi = first[i], oi = off[i], fjj = first[jj], ojj = off[jj];
-          if (fi > m || fjj > m) continue;
-          double li[6];
-          ld6(Sm + 36l * (oi + m - fi) + 6 * rr, li);
-          const double* Ljm = Sm + 36l * (ojj + m - fjj);
-          double* Sij = Sm + 36l * (oi + jj - fi) + 6 * rr;
-          double sv[6];
-          ld6(Sij, sv);
-#pragma unroll
-          for (int c = 0; c < 6; ++c) Sij[c] = sv[c] - dot6(li, Ljm + 6 * c);
-        }
-      }
-      // panel rows i >= k+2 of column k with the look-ahead steps k-2, k-1, and y
-      for (int item = t0; item < (lk - k - 1) * 6; item += nt) {
-        const int i = k + 2 + item / 6, rr = item % 6;
-        const int fi = first[i], oi = off[i];
-        if (fi > k) continue;
-        double* row = Sm + 36l * (oi + k - fi) + 6 * rr;
-        double sv[6], u0[6], u1[6];
-        ld6(row, sv);
-        const bool s0 = k >= 2 && fi <= k - 2 && fk <= k - 2;
-        const bool s1 = k >= 1 && fi <= k - 1 && fk <= k - 1;
-        if (s0) ld6(Sm + 36l * (oi + k - 2 - fi) + 6 * rr, u0);
-        if (s1) ld6(Sm + 36l * (oi + k - 1 - fi) + 6 * rr, u1);
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          double a = 0.0;
-          if (s0) a += dot6(u0, bk(k - 2) + 6 * c);
-          if (s1) a += dot6(u1, bk(k - 1) + 6 * c);
-          sv[c] -= a;
-        }
-        fwd6(L, r, sv);
-        double a = 0.0;
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          row[c] = sv[c];
-          a += sv[c] * yk[c];
-        }
-        y[6 * i + rr] -= a;
-      }
+    const bool prow = lane < 6 * cur.nb;
+    if (prow) ld6(Sm + 36l * cur.pblk + 6 * (lane % 6), sv);
+    if (tfi < cur.nt) ld6(Sm + 36l * cur.blk0 + 6 * (tfi % 6), s0);
+    if (k + 1 < F) desc1(k + 1, nxt);
+    settle(L[0] + sv[0] + s0[0] + yk[0]);
+    mark(kS3Data);
+    const bool ok = chol6(L, r);
+    settle(r[5]);
+    mark(kS3Chol);
+    if (wave == wY || wave == wK) fwd6(L, r, yk);  // y'_k: wave 1 updates y, wave 2 keeps it
+    if (wave == wK && lane == 0)
+      bad = bad || !ok || !isfinite(yk[0] + yk[1] + yk[2] + yk[3] + yk[4] + yk[5]);
+    // panel (every wave, its own copy); wave 1 also updates y
+    if (prow) {
+      fwd6(L, r, sv);
+      st6(Pw + 6 * lane, sv);
+      if (wave == wY) y[6 * cur.pi + lane % 6] -= sv[0] * yk[0] + sv[1] * yk[1] + sv[2] * yk[2] +
+                                                 sv[3] * yk[3] + sv[4] * yk[4] + sv[5] * yk[5];
     }
+    for (int rr = lane + 64; rr < 6 * cur.nb; rr += 64) {  // panels wider than 10 blocks
+      double v[6];
+      ld6(Sm + 36l * t_pblk[cur.p0 + rr / 6] + 6 * (rr % 6), v);
+      fwd6(L, r, v);
+      st6(Pw + 6 * rr, v);
+      if (wave == wY) y[6 * t_pi[cur.p0 + rr / 6] + rr % 6] -= v[0] * yk[0] + v[1] * yk[1] + v[2] * yk[2] +
+                                                               v[3] * yk[3] + v[4] * yk[4] + v[5] * yk[5];
+    }
+    if (wave == wK && lane == 0) {
+      double* o = kf + 36l * k;
+#pragma unroll
+      for (int e = 0; e < 20; e += 2) reinterpret_cast<double2*>(o)[e / 2] = make_double2(L[e], L[e + 1]);
+      reinterpret_cast<double2*>(o)[10] = make_double2(L[20], 0.0);
+      st6(o + 24, r);
+      st6(o + 30, yk);
+    }
+    wave_sync<true>();
+    settle(sv[5]);
+    mark(kS3Panel);
+    // trailing update from this wave's panel copy
+    for (int t = tfi; t < cur.nt; t += kThr) {
+      double s[6];
+      int blk, q;
+      if (t == tfi) {
+#pragma unroll
+        for (int c = 0; c < 6; ++c) s[c] = s0[c];
+        blk = cur.blk0;
+        q = cur.q0;
+      } else {
+        blk = t_iblk[cur.i0 + t / 6];
+        q = t_iq[cur.i0 + t / 6];
+        ld6(Sm + 36l * blk + 6 * (t % 6), s);
+      }
+      const int rr = t % 6;
+      double a[6];
+      ld6(Pw + 36 * (q & 0xffff) + 6 * rr, a);
+      const double* B = Pw + 36 * (q >> 16);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) s[c] -= dot6(a, B + 6 * c);
+      st6(Sm + 36l * blk + 6 * rr, s);
+    }
+    settle(0.0);
+    mark(kS3Trail);
+    if (k + 1 < F) desc2(nxt);  // static table: its latency hides in the barrier wait
+    prev_row = prow;
+    prev_blk = cur.pblk;
+    prev_p0 = cur.p0;
+    prev_nb = cur.nb;
+    cur = nxt;
     __syncthreads();
     mark(kS3Barrier);
   }
-  // back substitution L^T x = y' on wave 0, in registers (row oriented:
-  // x_k, then ys_j -= L_kj^T x_k for the blocks of row k)
+  if (wave == wK && lane == 0 && bad) s_fail = 1;
+  __syncthreads();
+  mark(kS3Factor);
+  // Back substitution L^T x = y' on wave 0.
   if (!s_fail && wave == 0) {
-    for (int k = F - 1; k >= 0; --k) {
-      const int fk = first[k], ok_ = off[k];
-      double Lk[21], rk[6], x[6];
+    if (A.max_row_span < kBsWindow) {
+      // Register-resident form (every row of L spans < kBsWindow blocks).  Lane
+      // (g, c), g < kBsWindow, c < 6, accumulates component c of y'_j for the one block
+      // row j = g (mod kBsWindow) inside the window [k - kBsWindow, k - 1] of step k.
+      // Step k: y_k (group k mod W) -> 12 readlanes -> x_k = L_kk^-T y_k in every lane
+      // -> each lane subtracts (L_kj^T x_k)_c for its j in row k.  L_kk, 1/diag, the
+      // L_kj columns and the entering y'_{k-W} come from LDS one step ahead.
+      constexpr int W = kBsWindow;
+      const int g = lane / 6, c = lane % 6;
+      const bool act = lane < 6 * W;
+      auto jj_of = [&](int k) {  // block row of group g in the window of step k
+        const int m = ((k - 1 - g) % W + W) % W;
+        return k - 1 - m;
+      };
+      auto load_L = [&](int k, double (&Lk)[21], double (&rk)[6]) {
+        const double* o = kf + 36l * k;
 #pragma unroll
-      for (int e = 0; e < 21; ++e) Lk[e] = Ld[21l * k + e];
-      ld6(rd + 6l * k, rk);
-      ld6(ys + 6l * k, x);
-      bwd6(Lk, rk, x);
-      wave_sync<kLds>();
-      if (lane < 6) ys[6l * k + lane] = pick(x, lane);
-      const int nb = k - fk;
-      for (int item = lane; item < nb * 6; item += 64) {
-        const int jj = fk + item / 6, c = item % 6;
-        const double* Lkj = Sm + 36l * (ok_ + jj - fk);
-        double a = 0.0;
+        for (int e2 = 0; e2 < 20; e2 += 2) {
+          const double2 v = reinterpret_cast<const double2*>(o)[e2 / 2];
+          Lk[e2] = v.x;
+          Lk[e2 + 1] = v.y;
+        }
+        Lk[20] = o[20];
+        ld6(o + 24, rk);
+      };
+      // column c of block (k, jj_of(k)) or 0; (fk, ok) = (first[k], off[k]) were read a step
+      // earlier.  Loads are unconditional (clamped addresses, select afterwards): a load
+      // under a branch makes the waitcnt pass drain every outstanding prefetch.
+      auto load_col = [&](int k, int fk, int okk, double (&col)[6]) {
+        const int jj = jj_of(k);
+        const bool on = act && jj >= fk && jj < k;
+        const double* b = Sm + 36l * (on ? okk + jj - fk : 0) + c;
 #pragma unroll
-        for (int rr = 0; rr < 6; ++rr) a += Lkj[6 * rr + c] * x[rr];
-        ys[6 * jj + c] -= a;
+        for (int rr = 0; rr < 6; ++rr) {
+          const double v = b[6 * rr];
+          col[rr] = on ? v : 0.0;
+        }
+      };
+      double acc = 0.0;
+      {
+        const int jj = jj_of(F);
+        if (act && jj >= 0) acc = kf[36l * jj + 30 + c];
       }
-      wave_sync<kLds>();
+      // Two register sets used alternately (the loop is unrolled by two), so the
+      // prefetched operands are never copied (each VALU op costs a wave 4 cycles).
+      struct Ops {
+        double L[21], r[6], col[6];
+        int f, o;  // first[], off[] of the step after the one these operands serve
+      };
+      Ops s0, s1;
+      load_L(F - 1, s0.L, s0.r);
+      load_col(F - 1, t_first[F - 1], t_off[F - 1], s0.col);
+      s0.f = t_first[F >= 2 ? F - 2 : 0];
+      s0.o = t_off[F >= 2 ? F - 2 : 0];
+      auto step = [&](int k, Ops& cur, Ops& nxt) {
+        const int kn = k > 0 ? k - 1 : 0, kn2 = k > 1 ? k - 2 : 0;
+        nxt.f = t_first[kn2];
+        nxt.o = t_off[kn2];
+        load_L(kn, nxt.L, nxt.r);
+        load_col(kn, cur.f, cur.o, nxt.col);
+        const int ent = k - W;  // block row entering the window of step k
+        const double init_v = kf[36l * (ent >= 0 ? ent : 0) + 30 + c];
+        const double init = ent >= 0 ? init_v : 0.0;
+        const int src = 6 * (k % W);
+        double x[6];
+#pragma unroll
+        for (int cc = 0; cc < 6; ++cc) {
+          const int lo = __builtin_amdgcn_readlane(__double2loint(acc), src + cc);
+          const int hi = __builtin_amdgcn_readlane(__double2hiint(acc), src + cc);
+          x[cc] = __hiloint2double(hi, lo);
+        }
+        bwd6(cur.L, cur.r, x);
+        if (lane == 0) st6(kf + 36l * k + 30, x);
+        if (g == k % W) acc = init;
+        acc -= cur.col[0] * x[0] + cur.col[1] * x[1] + cur.col[2] * x[2] + cur.col[3] * x[3] +
+               cur.col[4] * x[4] + cur.col[5] * x[5];
+      };
+      int k = F - 1;
+      for (; k >= 1; k -= 2) {
+        step(k, s0, s1);
+        step(k - 1, s1, s0);
+      }
+      if (k == 0) step(0, s0, s1);
+    } else {
+      // Wide rows: x_k, then y'_j -= L_kj^T x_k through LDS, one lane per (block, column).
+      for (int k = F - 1; k >= 0; --k) {
+        const double* o = kf + 36l * k;
+        double Lk[21], rk[6], x[6];
+#pragma unroll
+        for (int e2 = 0; e2 < 20; e2 += 2) {
+          const double2 v = reinterpret_cast<const double2*>(o)[e2 / 2];
+          Lk[e2] = v.x;
+          Lk[e2 + 1] = v.y;
+        }
+        Lk[20] = o[20];
+        ld6(o + 24, rk);
+        ld6(o + 30, x);
+        bwd6(Lk, rk, x);
+        const int fk = t_first[k], ok_ = t_off[k];
+        wave_sync<true>();
+        if (lane == 0) st6(kf + 36l * k + 30, x);
+        for (int t = lane; t < 6 * (k - fk); t += 64) {
+          const int jj = fk + t / 6, cc = t % 6;
+          const double* Lkj = Sm + 36l * (ok_ + jj - fk);
+          double a = 0.0;
+#pragma unroll
+          for (int rr = 0; rr < 6; ++rr) a += Lkj[6 * rr + cc] * x[rr];
+          kf[36l * jj + 30 + cc] -= a;
+        }
+        wave_sync<true>();
+      }
     }
   }
   __syncthreads();
+  mark(kS3Backsub);
   const bool failed = s_fail != 0;
-  for (int e = tid; e < 6 * F; e += kSolveThreads) A.dc[e] = failed ? 0.0 : ys[e];
-  for (int c = tid; c < A.n_poses; c += kSolveThreads) {
+  for (int e = tid; e < 6 * F; e += kThr) A.dc[e] = failed ? 0.0 : kf[36l * (e / 6) + 30 + e % 6];
+  for (int c = tid; c < A.n_poses; c += kThr) {
     const double* T = A.pose_cur + 12 * c;
     double* out = A.pose_next + 12 * c;
     if (failed || c < A.n_fixed) {
       for (int e = 0; e < 12; ++e) out[e] = T[e];
     } else {
+      const double* d6 = kf + 36l * (c - A.n_fixed) + 30;
       double d[6];
-      for (int e = 0; e < 6; ++e) d[e] = ys[6 * (c - A.n_fixed) + e];
+      for (int e = 0; e < 6; ++e) d[e] = d6[e];
       se3_exp_apply(d, T, out);
     }
   }
   if (tid == 0 && failed && !prior_fail) *A.status = A.iter_tag;
-  mark(kS3Backsub);
+  mark(kS3Tail);
   if (kStamp && tid == 0 && A.stamps)
     for (int k = 0; k < kS3Count; ++k) A.stamps[k] = st_acc[k];
 }
@@ -909,10 +1038,7 @@ void upload(DevBuf& buf, const std::vector<T>& v, hipStream_t st) {
     VO_HIP_CHECK(hipMemcpyAsync(buf.ptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
 }
 
-// K3 LDS: [profile (LDS path only) | Ld 21F | rd 6F | y 6F | ys 6F | W0 36 | ints 3F+1]
-size_t solve_aux_bytes(int F) { return (39ull * F + 37) * 8 + (3ull * F + 1) * 4; }
-size_t solve_lds_bytes(int nprof, int F) { return 36ull * nprof * 8 + solve_aux_bytes(F); }
-constexpr size_t kSolveLdsMax = 150 * 1024;
+constexpr size_t kSolveLdsMax = 160 * 1024 - 64;  // gfx950: 160 KiB per workgroup (+ s_fail)
 
 }  // namespace
 
@@ -1002,19 +1128,30 @@ class BAEngine {
     d_linv_.reserve(std::max(1, F) * 288ull);
     d_status_.reserve(sizeof(int));
     VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
-    solve_lds_ = solve_lds_bytes(P.n_prof_blocks(), F) <= kSolveLdsMax;
-    const size_t lds = solve_lds_ ? solve_lds_bytes(P.n_prof_blocks(), F) : solve_aux_bytes(F);
-    VO_REQUIRE(lds <= 160 * 1024, VO_ERR_ARG,
-               "vo_ba_setup: %d free poses exceed the solver's LDS budget", F);
+    upload(d_solve_tab_, P.solve_tab, st);
+    {
+      const SolveTableLayout& TL = P.solve_layout;
+      const SolveLds in_lds = solve_lds_layout(true, P.n_prof_blocks(), F, TL.max_panel, TL.len);
+      solve_lds_ = in_lds.total <= kSolveLdsMax;
+      solve_layout_ = solve_lds_ ? in_lds : solve_lds_layout(false, P.n_prof_blocks(), F, TL.max_panel, TL.len);
+      VO_REQUIRE(solve_layout_.total <= kSolveLdsMax, VO_ERR_ARG,
+                 "vo_ba_setup: %d free poses / panel of %d blocks exceed the solver's LDS budget", F,
+                 TL.max_panel);
+    }
+    const size_t lds = solve_layout_.total;
     solve_lds_size_ = lds;
-    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<true, false>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<true, true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<false, false>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<false, true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    {
+      const char* w = getenv("VO_K3_WAVES");
+      solve_waves_ = w ? atoi(w) : 4;
+      if (solve_waves_ != 1 && solve_waves_ != 2) solve_waves_ = 4;
+      const int l = (int)lds;
+      set_solve_lds<true, false, 1>(l); set_solve_lds<true, true, 1>(l);
+      set_solve_lds<false, false, 1>(l); set_solve_lds<false, true, 1>(l);
+      set_solve_lds<true, false, 2>(l); set_solve_lds<true, true, 2>(l);
+      set_solve_lds<false, false, 2>(l); set_solve_lds<false, true, 2>(l);
+      set_solve_lds<true, false, 4>(l); set_solve_lds<true, true, 4>(l);
+      set_solve_lds<false, false, 4>(l); set_solve_lds<false, true, 4>(l);
+    }
     VO_HIP_CHECK(hipStreamSynchronize(st));
     have_problem_ = true;
     have_state_ = false;
@@ -1247,7 +1384,28 @@ class BAEngine {
                                   ctx_->comm->comm, ctx_->stream));
   }
 
-  void enqueue_solve(int iter_tag) {
+  template <bool kL, bool kS>
+  void launch_solve_t(const SolveArgs& A) {
+    if (solve_waves_ == 1)
+      hipLaunchKernelGGL((ba_solve_kernel<kL, kS, 1>), dim3(1), dim3(64), solve_lds_size_, ctx_->stream, A);
+    else if (solve_waves_ == 2)
+      hipLaunchKernelGGL((ba_solve_kernel<kL, kS, 2>), dim3(1), dim3(128), solve_lds_size_, ctx_->stream, A);
+    else
+      hipLaunchKernelGGL((ba_solve_kernel<kL, kS, 4>), dim3(1), dim3(256), solve_lds_size_, ctx_->stream, A);
+  }
+  void launch_solve(const SolveArgs& A) {
+    if (solve_lds_ && stamps_on_) launch_solve_t<true, true>(A);
+    else if (solve_lds_) launch_solve_t<true, false>(A);
+    else if (stamps_on_) launch_solve_t<false, true>(A);
+    else launch_solve_t<false, false>(A);
+  }
+  template <bool kL, bool kS, int NW>
+  static void set_solve_lds(int lds) {
+    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<kL, kS, NW>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  }
+
+  void enqueue_solve(int iter_tag, double* cost_slot = nullptr) {
     const BAPlan& P = plan_;
     SolveArgs A;
     A.F = P.n_free;
@@ -1255,9 +1413,16 @@ class BAEngine {
     A.n_poses = P.n_poses;
     A.n_fixed = P.n_fixed;
     A.iter_tag = iter_tag;
-    A.prof_first = d_prof_first_.as<int>();
-    A.prof_off = d_prof_off_.as<int>();
-    A.prof_last = d_prof_last_.as<int>();
+    A.max_panel = std::max(1, P.solve_layout.max_panel);
+    A.max_row_span = 0;
+    for (int k = 0; k < P.n_free; ++k) A.max_row_span = std::max(A.max_row_span, k - P.prof_first[k]);
+    A.lds_kf = (long)solve_layout_.kf;
+    A.lds_y = (long)solve_layout_.y;
+    A.lds_panel = (long)solve_layout_.panel;
+    A.lds_tab = (long)solve_layout_.tab;
+    A.tl = P.solve_layout;
+    A.tab = d_solve_tab_.as<int>();
+    A.cost_out = cost_slot;
     A.sys = d_sys_.as<double>();
     A.dc = d_dc_.as<double>();
     A.pose_cur = d_pose_[cur_].as<double>();
@@ -1269,18 +1434,7 @@ class BAEngine {
       A.stamps = d_stamps3_.as<unsigned long long>();
     }
     ctx_->prof.begin(ctx_->stream, kKBaSolve);
-    if (solve_lds_ && stamps_on_)
-      hipLaunchKernelGGL((ba_solve_kernel<true, true>), dim3(1), dim3(kSolveThreads),
-                         solve_lds_size_, ctx_->stream, A);
-    else if (solve_lds_)
-      hipLaunchKernelGGL((ba_solve_kernel<true, false>), dim3(1), dim3(kSolveThreads),
-                         solve_lds_size_, ctx_->stream, A);
-    else if (stamps_on_)
-      hipLaunchKernelGGL((ba_solve_kernel<false, true>), dim3(1), dim3(kSolveThreads),
-                         solve_lds_size_, ctx_->stream, A);
-    else
-      hipLaunchKernelGGL((ba_solve_kernel<false, false>), dim3(1), dim3(kSolveThreads),
-                         solve_lds_size_, ctx_->stream, A);
+    launch_solve(A);
     ctx_->prof.end(ctx_->stream);
     VO_HIP_CHECK(hipGetLastError());
   }
@@ -1288,9 +1442,7 @@ class BAEngine {
   void iteration(double* d_cost_slot, int iter_tag) {
     enqueue_lin(pending_ ? (kBacksub | kAccum) : kAccum);
     enqueue_reduce();
-    VO_HIP_CHECK(hipMemcpyAsync(d_cost_slot, d_sys_.as<double>() + sys_len_ - 1, 8,
-                                hipMemcpyDeviceToDevice, ctx_->stream));
-    enqueue_solve(iter_tag);
+    enqueue_solve(iter_tag, d_cost_slot);  // K3 also stores the cost (no extra copy node)
     cur_ ^= 1;
     pending_ = true;
   }
@@ -1334,6 +1486,9 @@ class BAEngine {
   bool have_problem_ = false, have_state_ = false, pending_ = false, solve_lds_ = false;
   int cur_ = 0;
   size_t sys_len_ = 0, solve_lds_size_ = 0;
+  SolveLds solve_layout_{};
+  int solve_waves_ = 4;
+  DevBuf d_solve_tab_;
   DevBuf d_obs_uv_, d_obs_cam_, d_obs_te_, d_te_cam_, d_te_pt_, d_te_obs_, d_te_lcam_, d_pt_te_;
   DevBuf d_chunk_obs_, d_chunk_te_, d_chunk_pt_, d_chunk_slot_base_, d_chunk_cam_base_;
   DevBuf d_slot_ptr_, d_pair_list_, d_cam_ptr_, d_cam_list_;

@@ -264,6 +264,50 @@ void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
   }
   if (P.prof_src.empty()) P.prof_src.push_back(0);
   if (P.camb_src.empty()) P.camb_src.push_back(0);
+
+  // K3 step tables
+  auto blk = [&](int i, int j) { return P.prof_off[i] + (j - first[i]); };
+  std::vector<int32_t> sptr{0}, pi, pblk, iptr{0}, iblk, iq;
+  int maxnb = 0;
+  for (int k = 0; k < F; ++k) {
+    std::vector<int> rows;
+    for (int i = k + 1; i <= P.prof_last[k]; ++i)
+      if (first[i] <= k) rows.push_back(i);
+    const int nb = (int)rows.size();
+    maxnb = std::max(maxnb, nb);
+    for (int i : rows) {
+      pi.push_back(i);
+      pblk.push_back(blk(i, k));
+    }
+    sptr.push_back((int32_t)pi.size());
+    for (int q1 = 0; q1 < nb; ++q1)
+      for (int q2 = 0; q2 <= q1; ++q2) {
+        iblk.push_back(blk(rows[q1], rows[q2]));
+        iq.push_back(q1 | (q2 << 16));
+      }
+    iptr.push_back((int32_t)iblk.size());
+  }
+  SolveTableLayout& L = P.solve_layout;
+  std::vector<int32_t>& T = P.solve_tab;
+  T.clear();
+  auto put = [&](int& o, const std::vector<int32_t>& v) {
+    o = (int)T.size();
+    T.insert(T.end(), v.begin(), v.end());
+  };
+  std::vector<int32_t> diag(F), offv(P.prof_off.begin(), P.prof_off.begin() + F);
+  for (int k = 0; k < F; ++k) diag[k] = blk(k, k);
+  put(L.diag, diag);
+  put(L.off, offv);
+  put(L.first, first);
+  put(L.step_ptr, sptr);
+  put(L.panel_i, pi);
+  put(L.panel_blk, pblk);
+  put(L.item_ptr, iptr);
+  put(L.item_blk, iblk);
+  put(L.item_q, iq);
+  L.len = (int)T.size();
+  L.max_panel = maxnb;
+  if (T.empty()) T.push_back(0);
 }
 
 }  // namespace vo

@@ -32,6 +32,12 @@ constexpr int kChunkPairs = 1024;  // camera-pair (x, y) entries of one chunk, s
 constexpr int kSegSlots = 64;
 constexpr int kSegCams = 32;
 
+struct SolveTableLayout {
+  int diag = 0, off = 0, first = 0, step_ptr = 0, panel_i = 0, panel_blk = 0, item_ptr = 0,
+      item_blk = 0, item_q = 0, len = 0;
+  int max_panel = 0;  // most panel blocks in one column
+};
+
 struct BAPlan {
   int n_poses = 0, n_points = 0, n_obs = 0, n_fixed = 0, n_free = 0, n_te = 0;
   // internal order -> caller order
@@ -59,6 +65,12 @@ struct BAPlan {
   std::vector<int32_t> prof_src_ptr, prof_src;  // per profile block: slab slots
   std::vector<uint8_t> prof_diag;               // per profile block: 1 if i == j
   std::vector<int32_t> camb_ptr, camb_src;      // per free camera: slab b entries
+  // K3 step tables (one packed int array, staged in LDS): for block column k,
+  //   panel rows   i in (k, last[k]] with first[i] <= k       -> i, profile block (i, k)
+  //   trailing     blocks (i_q1, i_q2), q2 <= q1 of the panel  -> profile block, q1 | q2 << 16
+  // plus diag[k] (profile block (k, k)), off[k], first[k].
+  std::vector<int32_t> solve_tab;
+  SolveTableLayout solve_layout;
 
   int n_chunks() const { return (int)chunk_obs.size() - 1; }
   int n_segments() const { return (int)seg_chunk.size() - 1; }
