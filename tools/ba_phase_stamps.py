@@ -17,7 +17,7 @@ from visualodometry_amd import _lib  # noqa: E402
 from visualodometry_amd.ba import BASession  # noqa: E402
 from visualodometry_amd.synthetic import make_ba_config  # noqa: E402
 
-PHASES = ["load", "backsub", "lin_obs", "reduce", "eliminate", "schur", "write"]
+PHASES = ["load", "backsub", "lin_obs", "reduce", "eliminate", "schur_pairs", "write", "schur_cams", "unused"]
 K3 = ["k3_setup", "k3_factor(rest)", "k3_backsub", "k3_tail", "k3_data", "k3_chol", "k3_panel", "k3_trail", "k3_barrier"]
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg3"

@@ -57,7 +57,7 @@ struct Comm {
 
 namespace {
 
-constexpr int kLinThreads = 128;
+constexpr int kLinThreads = 256;
 constexpr int kBsWindow = 10;  // K3 back substitution: register window of block rows
 constexpr double kPivotRelEps = 1e-12;  // == oracle/ba_ref.py PIVOT_REL_EPS
 constexpr double kExpTaylor = 1e-4;     // == oracle/ba_ref.py EXP_TAYLOR_THETA
@@ -83,6 +83,9 @@ struct LinArgs {
   const uint16_t* pair_list;
   const int* cam_ptr;
   const uint8_t* cam_list;
+  const int* camo_ptr;
+  const uint8_t* camo_list;
+  const int* segcam_diag;
   const int* seg_chunk;
   const int* seg_slot_off;
   const int* seg_cam_off;
@@ -119,8 +122,11 @@ struct alignas(16) LinShared {
   int valid[kChunkPts];
   int slotp[kSegSlots + 1];  // this chunk's pair list offsets per window slot
   int camp[kSegCams + 1];    // this chunk's track-entry list offsets per window camera
+  int camop[kSegCams + 1];   // this chunk's observation list offsets per window camera
+  int dslot[kSegCams];       // diagonal slot of each window camera
   uint16_t pairs[kChunkPairs];
   uint8_t caml[kChunkTe];
+  uint8_t camol[kChunkObs];
 };
 
 // R1: residual and Jacobians, one lane per observation.
@@ -245,6 +251,10 @@ __device__ __forceinline__ void lin_eliminate(LinShared& S, int nte) {
       for (int e = 0; e < 18; ++e) S.Z[t][e] = 0.0;
 #pragma unroll
       for (int e = 0; e < 6; ++e) S.bt[t][e] = 0.0;
+      // frozen landmark: its observations leave U too (gc was formed from Jc already)
+      for (int o = S.te_obs[t]; o < S.te_obs[t + 1]; ++o)
+#pragma unroll
+        for (int e = 0; e < 12; ++e) S.Jc[o][e] = 0.0;
       continue;
     }
     const double i00 = S.L[p][0], l10 = S.L[p][1], i11 = S.L[p][2];
@@ -276,7 +286,7 @@ __device__ __forceinline__ void chunk_linearize(LinShared& S, const LinArgs& A,
 
 // Diagnostic build (VO_BA_STAMPS=1): thread 0 accumulates s_memtime deltas per
 // phase; the production instantiation has kStamp = false and executes none.
-enum { kPhLoad = 0, kPhBacksub, kPhLinObs, kPhReduce, kPhElim, kPhSchur, kPhWrite, kPhCount };
+enum { kPhLoad = 0, kPhBacksub, kPhLinObs, kPhReduce, kPhElim, kPhSchur, kPhWrite, kPhSchurU, kPhSchurB, kPhCount };
 template <bool kStamp>
 struct Stamper {
   unsigned long long t = 0, acc[kPhCount] = {};
@@ -336,6 +346,10 @@ __global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
       const int c0 = A.cam_ptr[cb], c1 = A.cam_ptr[cb + ncams];
       for (int k = tid; k <= ncams; k += kLinThreads) S.camp[k] = A.cam_ptr[cb + k] - c0;
       for (int e = c0 + tid; e < c1; e += kLinThreads) S.caml[e - c0] = A.cam_list[e];
+      const int q0 = A.camo_ptr[cb], q1 = A.camo_ptr[cb + ncams];
+      for (int k = tid; k <= ncams; k += kLinThreads) S.camop[k] = A.camo_ptr[cb + k] - q0;
+      for (int e = q0 + tid; e < q1; e += kLinThreads) S.camol[e - q0] = A.camo_list[e];
+      for (int k = tid; k < ncams; k += kLinThreads) S.dslot[k] = A.segcam_diag[cam0 + k];
     }
     __syncthreads();
     st.mark(kPhLoad);
@@ -387,64 +401,97 @@ __global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
     st.mark(kPhElim);
 
     // R4: Schur blocks into the window; lane owns (slot, row a) and sums its
-    // slot's pair list of this chunk in fixed order.  The next pair's Z rows are
-    // fetched (16-byte LDS reads) while the current pair's 18 FMAs run.
+    // slot's pair list of this chunk in fixed order.  Unrolled by two with two
+    // register sets: pair e+2's Z rows are fetched (16-byte LDS reads, indices read
+    // two pairs ahead, clamped -- no branches) while pair e+1's 18 FMAs run.  On a
+    // diagonal slot the U = Jc^T Jc terms of its track entries follow in a second loop.
     for (int item = tid; item < nslots * 6; item += kLinThreads) {
       const int s = item / 6, a = item - 6 * (item / 6);
       const int e0 = S.slotp[s], e1 = S.slotp[s + 1];
       if (e0 == e1) continue;
       double out[6] = {0, 0, 0, 0, 0, 0};
-      int pr = S.pairs[e0];
-      double2 zy[9];
-      double za[3];
-      {
+      auto zrow = [&](int pr, double (&za)[3], double2 (&zy)[9]) {
         const double2* py = reinterpret_cast<const double2*>(S.Z[pr >> 8]);
 #pragma unroll
         for (int k = 0; k < 9; ++k) zy[k] = py[k];
         const double* px = &S.Z[pr & 255][3 * a];
-        za[0] = px[0]; za[1] = px[1]; za[2] = px[2];
-      }
-      for (int e = e0; e < e1; ++e) {
-        const int x = pr & 255, y = pr >> 8;
-        double2 ny[9];
-        double nz[3];
-        int npr = pr;
-        if (e + 1 < e1) {
-          npr = S.pairs[e + 1];
-          const double2* py = reinterpret_cast<const double2*>(S.Z[npr >> 8]);
-#pragma unroll
-          for (int k = 0; k < 9; ++k) ny[k] = py[k];
-          const double* px = &S.Z[npr & 255][3 * a];
-          nz[0] = px[0]; nz[1] = px[1]; nz[2] = px[2];
-        }
+        za[0] = px[0];
+        za[1] = px[1];
+        za[2] = px[2];
+      };
+      auto accum = [&](const double (&za)[3], const double2 (&zy)[9]) {
         const double* zf = reinterpret_cast<const double*>(zy);
 #pragma unroll
         for (int c = 0; c < 6; ++c)
           out[c] -= za[0] * zf[3 * c] + za[1] * zf[3 * c + 1] + za[2] * zf[3 * c + 2];
-        if (x == y && S.te_use[x]) {
-          for (int o = S.te_obs[x]; o < S.te_obs[x + 1]; ++o) {
-            const double ja0 = S.Jc[o][a], ja1 = S.Jc[o][6 + a];
-#pragma unroll
-            for (int c = 0; c < 6; ++c) out[c] += ja0 * S.Jc[o][c] + ja1 * S.Jc[o][6 + c];
-          }
-        }
-        if (e + 1 < e1) {
-#pragma unroll
-          for (int k = 0; k < 9; ++k) zy[k] = ny[k];
-          za[0] = nz[0]; za[1] = nz[1]; za[2] = nz[2];
-          pr = npr;
-        }
+      };
+      const int last = e1 - 1;
+      const int p0 = S.pairs[e0];
+      double zaA[3], zaB[3];
+      double2 zyA[9], zyB[9];
+      zrow(p0, zaA, zyA);
+      zrow(S.pairs[min(e0 + 1, last)], zaB, zyB);
+      // indices of the pairs two ahead, read one iteration before their rows are fetched
+      int pc = S.pairs[min(e0 + 2, last)], pd = S.pairs[min(e0 + 3, last)];
+      int e = e0;
+      for (; e + 2 <= e1; e += 2) {
+        const int pe = S.pairs[min(e + 4, last)], pf = S.pairs[min(e + 5, last)];
+        accum(zaA, zyA);
+        zrow(pc, zaA, zyA);
+        accum(zaB, zyB);
+        zrow(pd, zaB, zyB);
+        pc = pe;
+        pd = pf;
       }
+      if (e < e1) accum(zaA, zyA);
 #pragma unroll
       for (int c = 0; c < 6; ++c) S.win[36 * s + 6 * a + c] += out[c];
     }
+    st.mark(kPhSchur);
+    __syncthreads();  // the diagonal slots receive U below
+    // per window camera c, row a: U_c row a = sum over its observations of Jc^T Jc
+    // (static observation list, indices read ahead) and b_c[a] = sum of bt over its
+    // track entries
     for (int item = tid; item < ncams * 6; item += kLinThreads) {
       const int c = item / 6, a = item - 6 * (item / 6);
+      const int q0 = S.camop[c], q1 = S.camop[c + 1];
+      double out[6] = {0, 0, 0, 0, 0, 0};
+      if (q1 > q0) {
+        const int ql = q1 - 1;
+        int on = S.camol[q0];
+        for (int q = q0; q < q1; ++q) {
+          const int o = on;
+          on = S.camol[min(q + 1, ql)];
+          const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
+          double j[12];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            const double2 v = jr[k];
+            j[2 * k] = v.x;
+            j[2 * k + 1] = v.y;
+          }
+          const double ja0 = S.Jc[o][a], ja1 = S.Jc[o][6 + a];
+#pragma unroll
+          for (int cc = 0; cc < 6; ++cc) out[cc] += ja0 * j[cc] + ja1 * j[6 + cc];
+        }
+      }
       double acc = 0.0;
-      for (int e = S.camp[c]; e < S.camp[c + 1]; ++e) acc += S.bt[S.caml[e]][a];
+      const int e0 = S.camp[c], e1 = S.camp[c + 1];
+      if (e1 > e0) {
+        const int el = e1 - 1;
+        int xn = S.caml[e0];
+        for (int e = e0; e < e1; ++e) {
+          const int x = xn;
+          xn = S.caml[min(e + 1, el)];
+          acc += S.bt[x][a];
+        }
+      }
       S.bwin[6 * c + a] += acc;
+      double* w = &S.win[36 * S.dslot[c] + 6 * a];
+#pragma unroll
+      for (int cc = 0; cc < 6; ++cc) w[cc] += out[cc];
     }
-    st.mark(kPhSchur);
+    st.mark(kPhSchurU);
   }
   __syncthreads();
   if (MODE & kAccum) {
@@ -482,44 +529,71 @@ struct ReduceArgs {
   const int* status;
 };
 
-// Sums slab entries src[k0..k1) (entry e of each) in fixed order, 4 loads in flight.
+// Sums slab entries src[k0 + part + j*stride] (entry e of each), j = 0, 1, ..., in fixed
+// order with 4 independent loads in flight.
 template <int W>
-__device__ __forceinline__ double sum_list(const double* __restrict__ slab, const int* __restrict__ src,
-                                           int k0, int k1, int e) {
+__device__ __forceinline__ double sum_strided(const double* __restrict__ slab, const int* __restrict__ src,
+                                              int k0, int k1, int part, int stride, int e) {
   double acc = 0.0;
-  int k = k0;
-  for (; k + 4 <= k1; k += 4) {
-    const int i0 = src[k], i1 = src[k + 1], i2 = src[k + 2], i3 = src[k + 3];
+  int k = k0 + part;
+  for (; k + 3 * stride < k1; k += 4 * stride) {
+    const int i0 = src[k], i1 = src[k + stride], i2 = src[k + 2 * stride], i3 = src[k + 3 * stride];
     const double v0 = slab[(long)W * i0 + e], v1 = slab[(long)W * i1 + e];
     const double v2 = slab[(long)W * i2 + e], v3 = slab[(long)W * i3 + e];
     acc = (((acc + v0) + v1) + v2) + v3;
   }
-  for (; k < k1; ++k) acc += slab[(long)W * src[k] + e];
+  for (; k < k1; k += stride) acc += slab[(long)W * src[k] + e];
   return acc;
 }
 
-// One workgroup per profile block (lanes 0..35: its entries; on a diagonal block
-// lanes 36..41 also reduce b of that camera); the last workgroup sums the cost.
-__global__ __launch_bounds__(64) void ba_reduce_kernel(ReduceArgs A) {
+constexpr int kRedThreads = 256;
+constexpr int kRedSParts = 7;   // 7 x 36 lanes per S block
+constexpr int kRedBParts = 42;  // 42 x 6 lanes per rhs block
+
+// One workgroup per profile block: 7 strided partial sums per S entry and, on a
+// diagonal block, 42 per rhs entry of that camera, combined in fixed order (the
+// result is bitwise reproducible).  The last workgroup sums the cost.
+__global__ __launch_bounds__(kRedThreads) void ba_reduce_kernel(ReduceArgs A) {
   if (A.status && *A.status) return;
+  __shared__ double part[kRedBParts * 6 > kRedSParts * 36 ? kRedBParts * 6 : kRedSParts * 36];
   const int blk = blockIdx.x, tid = threadIdx.x;
   if (blk < A.nprof) {
+    const bool diag = A.prof_diag[blk];
+    const int k0 = A.prof_src_ptr[blk], k1 = A.prof_src_ptr[blk + 1];
+    if (tid < kRedSParts * 36)
+      part[tid] = sum_strided<36>(A.slab, A.prof_src, k0, k1, tid / 36, kRedSParts, tid % 36);
+    __syncthreads();
     if (tid < 36) {
-      double acc = sum_list<36>(A.slab, A.prof_src, A.prof_src_ptr[blk], A.prof_src_ptr[blk + 1], tid);
-      if (A.prof_diag[blk] && tid % 7 == 0) acc += A.lambda;
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < kRedSParts; ++q) acc += part[36 * q + tid];
+      if (diag && tid % 7 == 0) acc += A.lambda;
       A.sys[36l * blk + tid] = acc;
-    } else if (tid < 42 && A.prof_diag[blk]) {
-      const int f = A.prof_diag_cam[blk], a = tid - 36;
-      A.sys[36l * A.nprof + 6 * f + a] =
-          sum_list<6>(A.slab_b, A.camb_src, A.camb_ptr[f], A.camb_ptr[f + 1], a);
+    }
+    if (!diag) return;
+    __syncthreads();
+    const int f = A.prof_diag_cam[blk];
+    if (tid < kRedBParts * 6)
+      part[tid] = sum_strided<6>(A.slab_b, A.camb_src, A.camb_ptr[f], A.camb_ptr[f + 1], tid / 6,
+                                 kRedBParts, tid % 6);
+    __syncthreads();
+    if (tid < 6) {
+      double acc = 0.0;
+      for (int q = 0; q < kRedBParts; ++q) acc += part[6 * q + tid];
+      A.sys[36l * A.nprof + 6 * f + tid] = acc;
     }
     return;
   }
-  double c = 0.0;  // fixed-order: lane-strided partial sums, then a shuffle tree
-  for (int s = tid; s < A.nseg; s += 64) c += A.slab_cost[s];
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1) c += __shfl_xor(c, m, 64);
-  if (tid == 0) A.sys[36l * A.nprof + 6 * A.F] = c;
+  // cost: fixed-order lane-strided partial sums, then a fixed tree over the 256 lanes
+  double c = 0.0;
+  for (int s = tid; s < A.nseg; s += kRedThreads) c += A.slab_cost[s];
+  part[tid] = c;
+  __syncthreads();
+  for (int m = kRedThreads / 2; m > 0; m >>= 1) {
+    if (tid < m) part[tid] += part[tid + m];
+    __syncthreads();
+  }
+  if (tid == 0) A.sys[36l * A.nprof + 6 * A.F] = part[0];
 }
 
 // K3: profile Cholesky solve S dc = b + pose update.
@@ -1114,6 +1188,9 @@ class BAEngine {
     upload(d_camb_ptr_, P.camb_ptr, st);
     upload(d_camb_src_, P.camb_src, st);
     upload(d_segcam_f_, P.segcam_f, st);
+    upload(d_camo_ptr_, P.camo_ptr, st);
+    upload(d_camo_list_, P.camo_list, st);
+    upload(d_segcam_diag_, P.segcam_diag, st);
     stamps_on_ = getenv("VO_BA_STAMPS") && atoi(getenv("VO_BA_STAMPS")) != 0;
     const int F = P.n_free;
     d_points_.reserve(std::max(1, P.n_points) * 24ull);
@@ -1309,6 +1386,9 @@ class BAEngine {
     A.pair_list = d_pair_list_.as<uint16_t>();
     A.cam_ptr = d_cam_ptr_.as<int>();
     A.cam_list = d_cam_list_.as<uint8_t>();
+    A.camo_ptr = d_camo_ptr_.as<int>();
+    A.camo_list = d_camo_list_.as<uint8_t>();
+    A.segcam_diag = d_segcam_diag_.as<int>();
     A.seg_chunk = d_seg_chunk_.as<int>();
     A.seg_slot_off = d_seg_slot_off_.as<int>();
     A.seg_cam_off = d_seg_cam_off_.as<int>();
@@ -1376,7 +1456,7 @@ class BAEngine {
     R.sys = d_sys_.as<double>();
     R.status = d_status_.as<int>();
     ctx_->prof.begin(ctx_->stream, kKBaReduce);
-    hipLaunchKernelGGL(ba_reduce_kernel, dim3(R.nprof + 1), dim3(64), 0, ctx_->stream, R);
+    hipLaunchKernelGGL(ba_reduce_kernel, dim3(R.nprof + 1), dim3(kRedThreads), 0, ctx_->stream, R);
     ctx_->prof.end(ctx_->stream);
     VO_HIP_CHECK(hipGetLastError());
     if (ctx_->comm && ctx_->comm->nranks > 1)
@@ -1460,7 +1540,7 @@ class BAEngine {
     R.slab_cost = d_slab_cost_.as<double>();
     R.sys = d_cost_tmp();
     R.status = d_status_.as<int>();
-    hipLaunchKernelGGL(ba_reduce_kernel, dim3(1), dim3(64), 0, ctx_->stream, R);
+    hipLaunchKernelGGL(ba_reduce_kernel, dim3(1), dim3(kRedThreads), 0, ctx_->stream, R);
     VO_HIP_CHECK(hipGetLastError());
     if (ctx_->comm && ctx_->comm->nranks > 1)
       VO_NCCL_CHECK(ncclAllReduce(R.sys, R.sys, 1, ncclFloat64, ncclSum, ctx_->comm->comm,
@@ -1496,6 +1576,7 @@ class BAEngine {
   DevBuf d_prof_first_, d_prof_off_, d_prof_last_, d_prof_src_ptr_, d_prof_src_, d_prof_diag_,
       d_prof_row_;
   DevBuf d_camb_ptr_, d_camb_src_, d_segcam_f_, d_stamps_, d_stamps3_;
+  DevBuf d_camo_ptr_, d_camo_list_, d_segcam_diag_;
   bool stamps_on_ = false;
 
  public:

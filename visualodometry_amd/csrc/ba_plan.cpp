@@ -176,7 +176,12 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       P.slot_i.push_back(pr.first);
       P.slot_j.push_back(pr.second);
     }
-    for (int c : s.cams) P.segcam_f.push_back(c);
+    for (int c : s.cams) {
+      P.segcam_f.push_back(c);
+      const auto d = std::make_pair(c, c);
+      P.segcam_diag.push_back(
+          (int32_t)(std::lower_bound(s.slots.begin(), s.slots.end(), d) - s.slots.begin()));
+    }
     P.seg_chunk.push_back(ch1);
     P.seg_slot_off.push_back((int32_t)P.slot_i.size());
     P.seg_cam_off.push_back((int32_t)P.segcam_f.size());
@@ -212,16 +217,27 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       std::vector<std::vector<uint8_t>> cl(nc);
       for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
         if (P.te_lcam[t] >= 0) cl[P.te_lcam[t]].push_back((uint8_t)(t - te0));
+      std::vector<std::vector<uint8_t>> co(nc);
+      const int ob0 = P.chunk_obs[ch];
+      for (int o = ob0; o < P.chunk_obs[ch + 1]; ++o) {
+        const int t = P.obs_te[o];
+        if (P.te_lcam[t] >= 0) co[P.te_lcam[t]].push_back((uint8_t)(o - ob0));
+      }
       P.chunk_cam_base[ch] = (int32_t)P.cam_ptr.size();
       for (int c = 0; c < nc; ++c) {
         P.cam_ptr.push_back((int32_t)P.cam_list.size());
         P.cam_list.insert(P.cam_list.end(), cl[c].begin(), cl[c].end());
+        P.camo_ptr.push_back((int32_t)P.camo_list.size());
+        P.camo_list.insert(P.camo_list.end(), co[c].begin(), co[c].end());
       }
       P.cam_ptr.push_back((int32_t)P.cam_list.size());
+      P.camo_ptr.push_back((int32_t)P.camo_list.size());
     }
   }
   if (P.pair_list.empty()) P.pair_list.push_back(0);  // keep device arrays non-empty
   if (P.cam_list.empty()) P.cam_list.push_back(0);
+  if (P.camo_list.empty()) P.camo_list.push_back(0);
+  if (P.segcam_diag.empty()) P.segcam_diag.push_back(0);
   return "";
 }
 

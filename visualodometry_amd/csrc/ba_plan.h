@@ -56,10 +56,13 @@ struct BAPlan {
   std::vector<uint16_t> pair_list; // (te_x_local | te_y_local << 8)
   std::vector<int32_t> cam_ptr;    // per chunk: ncams(seg)+1 offsets into cam_list
   std::vector<uint8_t> cam_list;   // te local index
+  std::vector<int32_t> camo_ptr;   // same indexing as cam_ptr: offsets into camo_list
+  std::vector<uint8_t> camo_list;  // observation local index (U = Jc^T Jc of the camera)
   // segments
   std::vector<int32_t> seg_chunk, seg_slot_off, seg_cam_off;  // n_seg+1
   std::vector<int32_t> slot_i, slot_j;   // per slab slot: global free-camera block (i >= j)
   std::vector<int32_t> segcam_f;         // per slab b entry: free camera
+  std::vector<int32_t> segcam_diag;      // per slab b entry: its diagonal slot within the segment
   // profile of S (block rows over free cameras)
   std::vector<int32_t> prof_first, prof_off, prof_last;  // F, F+1, F
   std::vector<int32_t> prof_src_ptr, prof_src;  // per profile block: slab slots
