@@ -600,7 +600,7 @@ __global__ __launch_bounds__(kRedThreads) void ba_reduce_kernel(ReduceArgs A) {
 struct SolveArgs {
   int F, nprof, n_poses, n_fixed, iter_tag;
   int max_panel, max_row_span;  // most panel blocks in a column; max k - first[k]
-  long lds_kf, lds_y, lds_panel, lds_tab;  // LDS offsets in doubles (solve_lds_layout)
+  long lds_kf, lds_y, lds_panel, lds_pose, lds_tab;  // LDS offsets in doubles (solve_lds_layout)
   SolveTableLayout tl;
   const int* tab;      // BAPlan::solve_tab
   double* cost_out;    // if set: receives the cost of this linearisation (sys tail)
@@ -658,6 +658,10 @@ __device__ __forceinline__ void se3_exp_apply(const double* d, const double* T, 
 }
 
 // ---- 6x6 block kernels in registers (packed lower storage, P(i,c) = i(i+1)/2 + c)
+#ifndef VO_CHOL_NEWTON
+#define VO_CHOL_NEWTON 1
+#endif
+constexpr bool kCholNewton = VO_CHOL_NEWTON != 0;
 __device__ __forceinline__ constexpr int P6(int i, int c) { return i * (i + 1) / 2 + c; }
 
 // In-place Cholesky a = L L^T; r = 1/diag(L) from v_rsq_f64 + one Newton step
@@ -671,7 +675,7 @@ __device__ __forceinline__ bool chol6(double (&a)[21], double (&r)[6]) {
     ok = ok && d > 0.0;
     const double dd = d > 0.0 ? d : 1.0;
     double q = __builtin_amdgcn_rsq(dd);
-    q = q * (1.5 - 0.5 * dd * q * q);
+    if (kCholNewton) q = q * (1.5 - 0.5 * dd * q * q);
     r[j] = q;
     a[P6(j, j)] = dd * q;
 #pragma unroll
@@ -740,18 +744,35 @@ __device__ __forceinline__ void wave_sync() {
 // table (BAPlan::solve_tab), staged in LDS with the profile.
 enum { kS3Setup = 0, kS3Factor, kS3Backsub, kS3Tail, kS3Data, kS3Chol, kS3Panel, kS3Trail, kS3Barrier, kS3Count };
 
+// dst[i] = src[i], i < n: U loads in flight per thread.  Loads and stores are
+// unconditional with a clamped index (an out-of-range slot rewrites dst[n-1] with
+// src[n-1]): a predicated load is sunk into its store's branch and serialises.
+template <typename T, int U>
+__device__ __forceinline__ void copy_in(T* dst, const T* __restrict__ src, int n, int tid, int nthr) {
+  if (n <= 0) return;
+  for (int e = tid; e < n; e += U * nthr) {
+    T a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = src[min(e + u * nthr, n - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) dst[min(e + u * nthr, n - 1)] = a[u];
+  }
+}
+
 struct SolveLds {
-  size_t prof, kf, y, panel, tab, total;
+  size_t prof, kf, y, panel, pose, tab, total;
 };
 // LDS image: [profile 36*nprof (LDS path)] [per column: L 21 + pad 3 | r 6 | y'/x 6]
 // [y 6F] [4 private panels, 36 doubles per block] [step table ints]
-SolveLds solve_lds_layout(bool lds_profile, int nprof, int F, int max_panel, int tab_len) {
+SolveLds solve_lds_layout(bool lds_profile, int nprof, int F, int max_panel, int tab_len,
+                          int n_poses) {
   SolveLds L;
   L.prof = 0;
   L.kf = lds_profile ? 36ull * nprof : 0;
   L.y = L.kf + 36ull * F;
   L.panel = L.y + 6ull * F;
-  L.tab = L.panel + 4ull * 36 * std::max(1, max_panel);
+  L.pose = L.panel + 4ull * 36 * std::max(1, max_panel);
+  L.tab = L.pose + 12ull * n_poses;
   L.total = L.tab * 8 + 4ull * std::max(1, tab_len);
   return L;
 }
@@ -800,23 +821,14 @@ __global__ __launch_bounds__(64 * NW) void ba_solve_kernel(SolveArgs A) {
     if (A.cost_out) *A.cost_out = A.sys[36l * A.nprof + 6l * F];
   }
   if (!prior_fail) {
-    if (kLds) {  // profile -> LDS: 16-byte loads, four in flight per thread
-      const double2* src = reinterpret_cast<const double2*>(A.sys);
-      double2* dst = reinterpret_cast<double2*>(Sm);
-      const int n2 = 18 * A.nprof;
-      int e = tid;
-      for (; e + 7 * kThr < n2; e += 8 * kThr) {
-        double2 a[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) a[u] = src[e + u * kThr];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) dst[e + u * kThr] = a[u];
-      }
-      for (; e < n2; e += kThr) dst[e] = src[e];
-    }
-    for (int e = tid; e < 6 * F; e += kThr) y[e] = A.sys[36l * A.nprof + e];
-    for (int e = tid; e < A.tl.len; e += kThr) tab[e] = A.tab[e];
+    // global -> LDS, every load of a batch in flight before the stores
+    if (kLds) copy_in<double2, 16>(reinterpret_cast<double2*>(Sm), reinterpret_cast<const double2*>(A.sys),
+                                   18 * A.nprof, tid, kThr);
+    copy_in<double, 4>(y, A.sys + 36l * A.nprof, 6 * F, tid, kThr);
+    copy_in<int, 8>(tab, A.tab, A.tl.len, tid, kThr);
   }
+  double* pose_l = dyn + A.lds_pose;  // current poses, staged early for the tail
+  copy_in<double, 4>(pose_l, A.pose_cur, 12 * A.n_poses, tid, kThr);
   __syncthreads();
   mark(kS3Setup);
 
@@ -1088,7 +1100,7 @@ __global__ __launch_bounds__(64 * NW) void ba_solve_kernel(SolveArgs A) {
   const bool failed = s_fail != 0;
   for (int e = tid; e < 6 * F; e += kThr) A.dc[e] = failed ? 0.0 : kf[36l * (e / 6) + 30 + e % 6];
   for (int c = tid; c < A.n_poses; c += kThr) {
-    const double* T = A.pose_cur + 12 * c;
+    const double* T = pose_l + 12 * c;
     double* out = A.pose_next + 12 * c;
     if (failed || c < A.n_fixed) {
       for (int e = 0; e < 12; ++e) out[e] = T[e];
@@ -1208,9 +1220,9 @@ class BAEngine {
     upload(d_solve_tab_, P.solve_tab, st);
     {
       const SolveTableLayout& TL = P.solve_layout;
-      const SolveLds in_lds = solve_lds_layout(true, P.n_prof_blocks(), F, TL.max_panel, TL.len);
+      const SolveLds in_lds = solve_lds_layout(true, P.n_prof_blocks(), F, TL.max_panel, TL.len, P.n_poses);
       solve_lds_ = in_lds.total <= kSolveLdsMax;
-      solve_layout_ = solve_lds_ ? in_lds : solve_lds_layout(false, P.n_prof_blocks(), F, TL.max_panel, TL.len);
+      solve_layout_ = solve_lds_ ? in_lds : solve_lds_layout(false, P.n_prof_blocks(), F, TL.max_panel, TL.len, P.n_poses);
       VO_REQUIRE(solve_layout_.total <= kSolveLdsMax, VO_ERR_ARG,
                  "vo_ba_setup: %d free poses / panel of %d blocks exceed the solver's LDS budget", F,
                  TL.max_panel);
@@ -1500,6 +1512,7 @@ class BAEngine {
     A.lds_y = (long)solve_layout_.y;
     A.lds_panel = (long)solve_layout_.panel;
     A.lds_tab = (long)solve_layout_.tab;
+    A.lds_pose = (long)solve_layout_.pose;
     A.tl = P.solve_layout;
     A.tab = d_solve_tab_.as<int>();
     A.cost_out = cost_slot;
