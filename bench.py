@@ -162,7 +162,8 @@ def main() -> int:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)  # control plane only
 
-    ctx = _lib.context(local)
+    # VO_BENCH_DEVICE pins every rank to one device (rehearsing N > 1 on a one-GPU box)
+    ctx = _lib.context(int(os.environ.get("VO_BENCH_DEVICE", local)))
     if world > 1:
         uid = [_lib.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)

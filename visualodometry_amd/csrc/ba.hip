@@ -1455,7 +1455,9 @@ class BAEngine {
     R.nprof = P.n_prof_blocks();
     R.F = P.n_free;
     R.nseg = std::max(P.n_segments(), plan_.n_segments() > 0 ? 0 : 1);
-    R.lambda = prob_.lambda;
+    // damping on the camera diagonal: added once -- by rank 0 only when the partial
+    // systems of the landmark shards are all-reduced
+    R.lambda = (ctx_->comm && ctx_->comm->rank > 0) ? 0.0 : prob_.lambda;
     R.prof_src_ptr = d_prof_src_ptr_.as<int>();
     R.prof_src = d_prof_src_.as<int>();
     R.prof_diag = d_prof_diag_.as<uint8_t>();
