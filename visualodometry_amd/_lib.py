@@ -12,7 +12,8 @@ import os
 import threading
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libvo_hip.so"
+# VO_LIB_PATH selects an alternative build of the same library (tuning experiments)
+LIB_PATH = Path(os.environ.get("VO_LIB_PATH") or Path(__file__).resolve().parent / "lib" / "libvo_hip.so")
 HEADER = Path(__file__).resolve().parents[1] / "include" / "vo_hip.h"
 
 VO_OK = 0

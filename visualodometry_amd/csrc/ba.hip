@@ -500,7 +500,8 @@ __global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
     double* dstb = A.slab_b + 6l * cam0;
     for (int e = tid; e < ncams * 6; e += kLinThreads) dstb[e] = S.bwin[e];
   }
-  double* red = &S.r[0][0];  // the residual buffer is dead here: reuse it for the cost
+  static_assert(kChunkTe * 18 >= kLinThreads, "cost reduction scratch");
+  double* red = &S.Z[0][0];  // Z is dead after the last chunk: reuse it for the cost
   red[tid] = cost;
   __syncthreads();
   for (int w = kLinThreads / 2; w > 0; w >>= 1) {

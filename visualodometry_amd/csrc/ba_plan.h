@@ -25,10 +25,13 @@
 
 namespace vo {
 
-constexpr int kChunkObs = 128;
-constexpr int kChunkTe = 128;
-constexpr int kChunkPts = 64;
-constexpr int kChunkPairs = 1024;  // camera-pair (x, y) entries of one chunk, staged in LDS
+#ifndef VO_CHUNK_OBS
+#define VO_CHUNK_OBS 64  // 64-observation chunks: ~50 KB LDS per K1 workgroup, 3 per CU (profiles/r01_chunk_sweep.md)
+#endif
+constexpr int kChunkObs = VO_CHUNK_OBS;
+constexpr int kChunkTe = VO_CHUNK_OBS;
+constexpr int kChunkPts = VO_CHUNK_OBS / 2;
+constexpr int kChunkPairs = 8 * VO_CHUNK_OBS;  // camera-pair (x, y) entries of one chunk, staged in LDS
 constexpr int kSegSlots = 64;
 constexpr int kSegCams = 32;
 
