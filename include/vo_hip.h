@@ -148,7 +148,10 @@ int vo_ba_plan_stats(vo_ctx* ctx, int64_t* out, int n);
 /* Diagnostic only: with VO_BA_STAMPS=1 in the environment at vo_ba_setup, K1
  * runs a separate stamped instantiation; returns per-phase shader-cycle sums over
  * all workgroups of the last K1 launch (load, backsub, linobs, reduce, elim,
- * schur, write).  Returns the count written (0 when stamps are off). */
+ * schur_pairs, write, schur_cams, then two unused slots) followed by the K3 phase
+ * cycles.  With n < 0 it instead writes up to -n raw per-segment values (10 per
+ * segment, the last two the absolute start and end time of that workgroup).
+ * Returns the count written (0 when stamps are off). */
 int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n);
 
 /* ---- kernel timing (HIP events on the context stream) ---------------------

@@ -17,8 +17,8 @@ from visualodometry_amd import _lib  # noqa: E402
 from visualodometry_amd.ba import BASession  # noqa: E402
 from visualodometry_amd.synthetic import make_ba_config  # noqa: E402
 
-PHASES = ["load", "backsub", "lin_obs", "reduce", "eliminate", "schur_pairs", "write", "schur_cams", "unused"]
-K3 = ["k3_setup", "k3_factor(rest)", "k3_backsub", "k3_tail", "k3_data", "k3_chol", "k3_panel", "k3_trail", "k3_barrier"]
+PHASES = ["load", "backsub", "lin_obs", "reduce", "eliminate", "schur_pairs", "write", "schur_cams", "-", "-"]
+K3 = ["k3_setup", "-", "k3_backsub", "k3_tail", "k3_sides", "-", "k3_merge", "k3_separator", "-"]
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg3"
 p = make_ba_config(cfg)
@@ -30,10 +30,26 @@ s.synchronize()
 out = np.zeros(len(PHASES) + len(K3), dtype=np.uint64)
 n = _lib.check(ctx.lib.vo_ba_debug_stamps(ctx.handle, out.ctypes.data_as(_lib.C.POINTER(_lib.C.c_uint64)),
                                            len(out)))
-tot = float(out[: len(PHASES)].sum())
+tot = float(out[:8].sum())
 print(cfg, s.plan_stats())
-for k in range(min(n, len(PHASES))):
+for k in range(min(n, 8)):
     print(f"{PHASES[k]:18s} {int(out[k]):14d} cycles (sum over WGs)  {100 * out[k] / tot:5.1f} %")
 t3 = float(out[len(PHASES):].sum())
 for k in range(len(PHASES), n):
     print(f"{K3[k - len(PHASES)]:18s} {int(out[k]):14d} cycles (one WG)  {100 * out[k] / max(t3, 1):5.1f} %")
+
+# per-workgroup timeline of the last K1 launch (start/end absolute stamps)
+nseg = s.plan_stats()["segments"]
+raw = np.zeros(nseg * 10, dtype=np.uint64)
+k = ctx.lib.vo_ba_debug_stamps(ctx.handle, raw.ctypes.data_as(_lib.C.POINTER(_lib.C.c_uint64)), -raw.size)
+if k > 0:
+    r = raw[:k].reshape(-1, 10).astype(np.int64)
+    t0, t1 = r[:, 8], r[:, 9]
+    base = t0.min()
+    dur = t1 - t0
+    print(f"K1 workgroups: {len(r)}  start spread {t0.max() - base} cyc  end of last {t1.max() - base} cyc")
+    print(f"  duration min/median/p90/max: {dur.min()} {int(np.median(dur))} {int(np.percentile(dur, 90))} {dur.max()}")
+    order = np.argsort(t0)
+    print("  first 5 starts", (t0[order[:5]] - base).tolist(), " last 5 starts", (t0[order[-5:]] - base).tolist())
+    slow = np.argsort(dur)[-5:]
+    print("  slowest segments", slow.tolist(), dur[slow].tolist())

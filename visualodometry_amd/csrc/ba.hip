@@ -79,6 +79,10 @@ struct LinArgs {
   const int* chunk_pt;
   const int* chunk_slot_base;
   const int* chunk_cam_base;
+  const int4* chunk_hdr;  // kChunkHdr ints per chunk (BAPlan::chunk_hdr)
+  const int* seg_acam_off;
+  const int* seg_acam;
+  const uint8_t* obs_acam;
   const int* slot_ptr;
   const uint16_t* pair_list;
   const int* cam_ptr;
@@ -127,21 +131,26 @@ struct alignas(16) LinShared {
   uint16_t pairs[kChunkPairs];
   uint8_t caml[kChunkTe];
   uint8_t camol[kChunkObs];
+  double pose_o[kSegAllCams][12];  // poses of every camera the segment sees: pending step's
+  double pose_n[kSegAllCams][12];  // linearisation point (back substitution) and the new one
+  float2 uv[kChunkObs];
+  uint8_t acam[kChunkObs];         // observation -> index into pose_o / pose_n
 };
+// three K1 workgroups per CU (the cfg3 plan then runs in a single round)
+static_assert(sizeof(LinShared) <= 160 * 1024 / 3, "K1 LDS image");
 
 // R1: residual and Jacobians, one lane per observation.
-__device__ __forceinline__ void lin_obs(LinShared& S, const LinArgs& A, const double* pose,
-                                        int ob0, int nob, double& cost) {
+__device__ __forceinline__ void lin_obs(LinShared& S, const LinArgs& A, const double (*pose)[12],
+                                        int nob, double& cost) {
   for (int o = threadIdx.x; o < nob; o += kLinThreads) {
-    const int cam = A.obs_cam[ob0 + o];
-    const double* T = pose + 12 * cam;
+    const double* T = pose[S.acam[o]];
     const int q = S.te_pt[S.obs_te[o]];
     const double X0 = S.X[q][0], X1 = S.X[q][1], X2 = S.X[q][2];
     const double x = T[0] * X0 + T[1] * X1 + T[2] * X2 + T[9];
     const double y = T[3] * X0 + T[4] * X1 + T[5] * X2 + T[10];
     const double z = T[6] * X0 + T[7] * X1 + T[8] * X2 + T[11];
     const double iz = 1.0 / z;
-    const float2 m = A.obs_uv[ob0 + o];
+    const float2 m = S.uv[o];
     const double r0 = A.fx * x * iz + A.cx - (double)m.x;
     const double r1 = A.fy * y * iz + A.cy - (double)m.y;
     cost += r0 * r0 + r1 * r1;
@@ -274,9 +283,9 @@ __device__ __forceinline__ void lin_eliminate(LinShared& S, int nte) {
 }
 
 __device__ __forceinline__ void chunk_linearize(LinShared& S, const LinArgs& A,
-                                                const double* pose, int ob0, int nob,
+                                                const double (*pose)[12], int nob,
                                                 int nte, int npt, double& cost) {
-  lin_obs(S, A, pose, ob0, nob, cost);
+  lin_obs(S, A, pose, nob, cost);
   __syncthreads();
   lin_reduce(S, A, nte, npt);
   __syncthreads();
@@ -286,12 +295,27 @@ __device__ __forceinline__ void chunk_linearize(LinShared& S, const LinArgs& A,
 
 // Diagnostic build (VO_BA_STAMPS=1): thread 0 accumulates s_memtime deltas per
 // phase; the production instantiation has kStamp = false and executes none.
-enum { kPhLoad = 0, kPhBacksub, kPhLinObs, kPhReduce, kPhElim, kPhSchur, kPhWrite, kPhSchurU, kPhSchurB, kPhCount };
+// dst[i] = src[i] + add, i < n, by the workgroup: U loads per thread issued before
+// any store; loads are unconditional (clamped index) so none is sunk into a branch.
+template <typename T, int U, typename Src, typename V>
+__device__ __forceinline__ void stage(T* dst, const Src* __restrict__ src, int n, V add) {
+  if (n <= 0) return;
+  for (int e = threadIdx.x; e < n; e += U * kLinThreads) {
+    Src a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = src[min(e + u * kLinThreads, n - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (e + u * kLinThreads < n) dst[e + u * kLinThreads] = (T)(a[u] + add);
+  }
+}
+
+enum { kPhLoad = 0, kPhBacksub, kPhLinObs, kPhReduce, kPhElim, kPhSchur, kPhWrite, kPhSchurU, kPhT0, kPhT1, kPhCount };
 template <bool kStamp>
 struct Stamper {
   unsigned long long t = 0, acc[kPhCount] = {};
   __device__ __forceinline__ void start() {
-    if (kStamp && threadIdx.x == 0) t = __builtin_amdgcn_s_memtime();
+    if (kStamp && threadIdx.x == 0) acc[kPhT0] = t = __builtin_amdgcn_s_memtime();
   }
   __device__ __forceinline__ void mark(int ph) {
     if (kStamp && threadIdx.x == 0) {
@@ -301,13 +325,14 @@ struct Stamper {
     }
   }
   __device__ __forceinline__ void flush(unsigned long long* out) {
+    if (kStamp && threadIdx.x == 0) acc[kPhT1] = __builtin_amdgcn_s_memtime();  // absolute
     if (kStamp && threadIdx.x == 0 && out)
       for (int k = 0; k < kPhCount; ++k) out[blockIdx.x * kPhCount + k] = acc[k];
   }
 };
 
 template <int MODE, bool kStamp>
-__global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
+__global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  // 3 per CU: <= 168 VGPRs
   if (A.status && *A.status) return;  // a previous solve failed: state frozen
   __shared__ LinShared S;
   Stamper<kStamp> st;
@@ -323,40 +348,81 @@ __global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
   if (MODE & kBacksub)
     for (int e = tid; e < ncams * 6; e += kLinThreads)
       S.dcw[e / 6][e % 6] = A.dc[6l * A.segcam_f[cam0 + e / 6] + e % 6];
+  {  // poses of the segment's cameras, once per segment
+    const int a0 = A.seg_acam_off[seg], na = A.seg_acam_off[seg + 1] - a0;
+    for (int e = tid; e < 12 * na; e += kLinThreads) {
+      const long g = 12l * A.seg_acam[a0 + e / 12] + e % 12;
+      S.pose_n[e / 12][e % 12] = A.pose_new[g];
+      if (MODE & kBacksub) S.pose_o[e / 12][e % 12] = A.pose_old[g];
+    }
+  }
   double cost = 0.0;
   for (int ch = A.seg_chunk[seg]; ch < A.seg_chunk[seg + 1]; ++ch) {
-    const int ob0 = A.chunk_obs[ch], nob = A.chunk_obs[ch + 1] - ob0;
-    const int te0 = A.chunk_te[ch], nte = A.chunk_te[ch + 1] - te0;
-    const int p0 = A.chunk_pt[ch], npt = A.chunk_pt[ch + 1] - p0;
-    __syncthreads();  // previous chunk fully consumed
-    for (int o = tid; o < nob; o += kLinThreads) S.obs_te[o] = A.obs_te[ob0 + o] - te0;
-    for (int t = tid; t <= nte; t += kLinThreads) S.te_obs[t] = A.te_obs[te0 + t] - ob0;
-    for (int t = tid; t < nte; t += kLinThreads) {
-      S.te_pt[t] = A.te_pt[te0 + t] - p0;
-      S.te_lcam[t] = A.te_lcam[te0 + t];
-    }
-    for (int p = tid; p <= npt; p += kLinThreads) S.pt_te[p] = A.pt_te[p0 + p] - te0;
-    for (int e = tid; e < npt * 3; e += kLinThreads) S.X[e / 3][e % 3] = A.points[3l * p0 + e];
+    // one uniform header load, then every list load of the chunk in flight at once
+    const int4 h0 = A.chunk_hdr[4l * ch], h1 = A.chunk_hdr[4l * ch + 1], h2 = A.chunk_hdr[4l * ch + 2],
+               h3 = A.chunk_hdr[4l * ch + 3];
+    const int ob0 = h0.x, nob = h0.y, te0 = h0.z, nte = h0.w, p0 = h1.x, npt = h1.y;
+    const int sb = h1.z, cb = h1.w, e0 = h2.x, e1 = h2.y, c0 = h2.z, c1 = h2.w, q0 = h3.x, q1 = h3.y;
+    // every staging load of this thread first (unconditional: an empty list reads its
+    // array's first element), then -- after the previous chunk is consumed -- the stores
+    const int i0 = tid, i1 = tid + kLinThreads;
+    auto ld = [&](const auto* src, const auto* base, int n, int i) {
+      return n > 0 ? src[min(i, n - 1)] : base[0];
+    };
+    const int v_obs_te = ld(A.obs_te + ob0, A.obs_te, nob, i0);
+    const int v_te_obs = ld(A.te_obs + te0, A.te_obs, nte + 1, i0);
+    const int v_te_pt = ld(A.te_pt + te0, A.te_pt, nte, i0);
+    const int v_te_lcam = ld(A.te_lcam + te0, A.te_lcam, nte, i0);
+    const int v_pt_te = ld(A.pt_te + p0, A.pt_te, npt + 1, i0);
+    const double v_x = ld(A.points + 3l * p0, A.points, 3 * npt, i0);
+    const int v_acam = ld(A.obs_acam + ob0, A.obs_acam, nob, i0);
+    const float v_uv = ld(&A.obs_uv[ob0].x, &A.obs_uv[0].x, 2 * nob, i0);
+    int v_slotp = 0, v_pair0 = 0, v_pair1 = 0, v_camp = 0, v_caml = 0, v_camop = 0, v_camol = 0,
+        v_dslot = 0;
     if (MODE & kAccum) {
-      // stage this chunk's static pair and camera lists (coalesced, once per chunk)
-      const int sb = A.chunk_slot_base[ch], cb = A.chunk_cam_base[ch];
-      const int e0 = A.slot_ptr[sb], e1 = A.slot_ptr[sb + nslots];
-      for (int k = tid; k <= nslots; k += kLinThreads) S.slotp[k] = A.slot_ptr[sb + k] - e0;
-      for (int e = e0 + tid; e < e1; e += kLinThreads) S.pairs[e - e0] = A.pair_list[e];
-      const int c0 = A.cam_ptr[cb], c1 = A.cam_ptr[cb + ncams];
-      for (int k = tid; k <= ncams; k += kLinThreads) S.camp[k] = A.cam_ptr[cb + k] - c0;
-      for (int e = c0 + tid; e < c1; e += kLinThreads) S.caml[e - c0] = A.cam_list[e];
-      const int q0 = A.camo_ptr[cb], q1 = A.camo_ptr[cb + ncams];
-      for (int k = tid; k <= ncams; k += kLinThreads) S.camop[k] = A.camo_ptr[cb + k] - q0;
-      for (int e = q0 + tid; e < q1; e += kLinThreads) S.camol[e - q0] = A.camo_list[e];
-      for (int k = tid; k < ncams; k += kLinThreads) S.dslot[k] = A.segcam_diag[cam0 + k];
+      v_slotp = ld(A.slot_ptr + sb, A.slot_ptr, nslots + 1, i0);
+      v_pair0 = ld(A.pair_list + e0, A.pair_list, e1 - e0, i0);
+      v_pair1 = ld(A.pair_list + e0, A.pair_list, e1 - e0, i1);
+      v_camp = ld(A.cam_ptr + cb, A.cam_ptr, ncams + 1, i0);
+      v_caml = ld(A.cam_list + c0, A.cam_list, c1 - c0, i0);
+      v_camop = ld(A.camo_ptr + cb, A.camo_ptr, ncams + 1, i0);
+      v_camol = ld(A.camo_list + q0, A.camo_list, q1 - q0, i0);
+      v_dslot = ld(A.segcam_diag + cam0, A.segcam_diag, ncams, i0);
+    }
+    __syncthreads();  // previous chunk fully consumed
+    if (i0 < nob) {
+      S.obs_te[i0] = v_obs_te - te0;
+      S.acam[i0] = (uint8_t)v_acam;
+    }
+    if (i0 <= nte) S.te_obs[i0] = v_te_obs - ob0;
+    if (i0 < nte) {
+      S.te_pt[i0] = v_te_pt - p0;
+      S.te_lcam[i0] = v_te_lcam;
+    }
+    if (i0 <= npt) S.pt_te[i0] = v_pt_te - te0;
+    if (i0 < 3 * npt) (&S.X[0][0])[i0] = v_x;
+    if (i0 < 2 * nob) (&S.uv[0].x)[i0] = v_uv;
+    static_assert(3 * kChunkPts <= kLinThreads && 2 * kChunkObs <= kLinThreads &&
+                      kChunkTe < kLinThreads && kChunkPairs <= 2 * kLinThreads,
+                  "one staging element per thread (two for the pair list)");
+    if (MODE & kAccum) {
+      if (i0 <= nslots) S.slotp[i0] = v_slotp - e0;
+      if (i0 < e1 - e0) S.pairs[i0] = (uint16_t)v_pair0;
+      if (i1 < e1 - e0) S.pairs[i1] = (uint16_t)v_pair1;
+      if (i0 <= ncams) {
+        S.camp[i0] = v_camp - c0;
+        S.camop[i0] = v_camop - q0;
+      }
+      if (i0 < c1 - c0) S.caml[i0] = (uint8_t)v_caml;
+      if (i0 < q1 - q0) S.camol[i0] = (uint8_t)v_camol;
+      if (i0 < ncams) S.dslot[i0] = v_dslot;
     }
     __syncthreads();
     st.mark(kPhLoad);
 
     if (MODE & kBacksub) {
       double dummy = 0.0;
-      chunk_linearize(S, A, A.pose_old, ob0, nob, nte, npt, dummy);
+      chunk_linearize(S, A, S.pose_o, nob, nte, npt, dummy);
       for (int p = tid; p < npt; p += kLinThreads) {
         if (!S.valid[p]) continue;
         double a0 = -S.h[p][0], a1 = -S.h[p][1], a2 = -S.h[p][2];
@@ -387,10 +453,10 @@ __global__ __launch_bounds__(kLinThreads) void ba_lin_kernel(LinArgs A) {
     }
 
     if (!(MODE & kAccum)) {
-      lin_obs(S, A, A.pose_new, ob0, nob, cost);  // cost at the updated state
+      lin_obs(S, A, S.pose_n, nob, cost);  // cost at the updated state
       continue;
     }
-    lin_obs(S, A, A.pose_new, ob0, nob, cost);
+    lin_obs(S, A, S.pose_n, nob, cost);
     __syncthreads();
     st.mark(kPhLinObs);
     lin_reduce(S, A, nte, npt);
@@ -1118,6 +1184,299 @@ __global__ __launch_bounds__(64 * NW) void ba_solve_kernel(SolveArgs A) {
     for (int k = 0; k < kS3Count; ++k) A.stamps[k] = st_acc[k];
 }
 
+// ---- K3, two-sided variant (BAPlan::solve2_tab, TwoSidedLayout) ---------------------
+__device__ __forceinline__ void ld6g(const double* p, double (&v)[6]) {
+  const double2* q = reinterpret_cast<const double2*>(p);
+  const double2 a0 = q[0], a1 = q[1], a2 = q[2];
+  v[0] = a0.x; v[1] = a0.y; v[2] = a1.x; v[3] = a1.y; v[4] = a2.x; v[5] = a2.y;
+}
+__device__ __forceinline__ void st6g(double* p, const double (&v)[6]) {
+  double2* q = reinterpret_cast<double2*>(p);
+  q[0] = make_double2(v[0], v[1]);
+  q[1] = make_double2(v[2], v[3]);
+  q[2] = make_double2(v[4], v[5]);
+}
+__device__ __forceinline__ double dot6g(const double (&u)[6], const double* w) {
+  const double2* q = reinterpret_cast<const double2*>(w);
+  const double2 a0 = q[0], a1 = q[1], a2 = q[2];
+  return u[0] * a0.x + u[1] * a0.y + u[2] * a1.x + u[3] * a1.y + u[4] * a2.x + u[5] * a2.y;
+}
+
+struct Solve2Args {
+  SolveArgs base;
+  TwoSidedLayout tl;
+  const int* tab;  // BAPlan::solve2_tab
+  long lds_kf, lds_y, lds_panel, lds_pose, lds_tab;
+};
+
+// LDS image: [profile 36*nprof | shadow blocks 36*nshadow | per column 36 (L, 1/diag, y')
+// | y 6F + shadow rhs 6s | 4 private panels | poses | step table]
+SolveLds solve2_lds_layout(int nprof, int F, const TwoSidedLayout& T, int n_poses) {
+  SolveLds L;
+  L.prof = 0;
+  L.kf = 36ull * (nprof + T.nshadow);
+  L.y = L.kf + 36ull * F;
+  L.panel = L.y + 6ull * F + 6ull * T.s + ((6ull * F + 6ull * T.s) & 1);
+  L.pose = L.panel + 4ull * 36 * std::max(1, T.max_panel);
+  L.tab = L.pose + 12ull * n_poses;
+  L.total = L.tab * 8 + 4ull * std::max(1, T.len);
+  return L;
+}
+
+// One workgroup of four waves.  Phase p of the sides: waves 0-1 run top-down step p,
+// waves 2-3 bottom-up step m+p (each wave computes its step's whole panel into its own
+// panel copy, so the trailing update needs no barrier); one barrier per phase.  Then
+// the shadows are merged, the separator is factored by all four waves, and the back
+// substitution runs separator first, then top (wave 0) and bottom (wave 2) together.
+template <bool kStamp>
+__global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
+  const SolveArgs& A = A2.base;
+  const TwoSidedLayout& T = A2.tl;
+  unsigned long long st_t = 0, st_acc[kS3Count] = {};
+  auto mark = [&](int ph) {
+    if (kStamp && threadIdx.x == 0) {
+      const unsigned long long n = __builtin_amdgcn_s_memtime();
+      if (st_t) st_acc[ph] += n - st_t;
+      st_t = n;
+    }
+  };
+  mark(0);
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  __shared__ int s_fail;
+  const int tid = threadIdx.x, F = A.F;
+  const int wave = tid >> 6, lane = tid & 63;
+  const bool prior_fail = A.status && *A.status;
+  double* Sm = dyn;
+  double* kf = dyn + A2.lds_kf;
+  double* y = dyn + A2.lds_y;
+  double* Pw = dyn + A2.lds_panel + 36l * T.max_panel * wave;
+  double* pose_l = dyn + A2.lds_pose;
+  int* tab = reinterpret_cast<int*>(dyn + A2.lds_tab);
+  const int* t_col = tab + T.col;
+  const int* t_mode = tab + T.mode;
+  const int* t_diag = tab + T.diag;
+  const int* t_sptr = tab + T.step_ptr;
+  const int* t_pblk = tab + T.panel_blk;
+  const int* t_py = tab + T.panel_y;
+  const int* t_iptr = tab + T.item_ptr;
+  const int* t_iblk = tab + T.item_blk;
+  const int* t_iq = tab + T.item_q;
+  const int* t_merge = tab + T.merge_main;
+  const int* t_cptr = tab + T.colb_ptr;
+  const int* t_colb = tab + T.colb;
+  const int* t_off = tab + T.off;
+  const int* t_first = tab + T.first;
+  const int m = T.m, s = T.s, nbot = T.nbot;
+  if (tid == 0) {
+    s_fail = prior_fail ? 1 : 0;
+    if (A.cost_out) *A.cost_out = A.sys[36l * A.nprof + 6l * F];
+  }
+  if (!prior_fail) {
+    copy_in<double2, 16>(reinterpret_cast<double2*>(Sm), reinterpret_cast<const double2*>(A.sys),
+                         18 * A.nprof, tid, 256);
+    copy_in<double, 4>(y, A.sys + 36l * A.nprof, 6 * F, tid, 256);
+    copy_in<int, 8>(tab, A2.tab, T.len, tid, 256);
+    for (int e = tid; e < 36 * T.nshadow; e += 256) Sm[36l * A.nprof + e] = 0.0;
+    for (int e = tid; e < 6 * s; e += 256) y[6 * F + e] = 0.0;
+  }
+  copy_in<double, 4>(pose_l, A.pose_cur, 12 * A.n_poses, tid, 256);
+  __syncthreads();
+  mark(kS3Setup);
+
+  bool bad = false, prev_row = false;
+  int prev_blk = 0;
+  double sv[6] = {0, 0, 0, 0, 0, 0};
+  // One elimination step t on a group of gnw waves (gw: this wave's index in it); roles
+  // (group-local): wY updates y, wK keeps (L, 1/diag, y') and the failure flag, wC
+  // writes the previous step's panel into the profile.
+  auto step = [&](int t, int gw, int gnw, int wY, int wK, int wC) {
+    const int k = t_col[t], md = t_mode[t];
+    const int p0 = t_sptr[t], nb = t_sptr[t + 1] - p0;
+    const int i0 = t_iptr[t], nt = 6 * (t_iptr[t + 1] - i0);
+    const bool prow = lane < 6 * nb;
+    const int rr = lane % 6, qi = p0 + (prow ? lane / 6 : 0);
+    const int pblk = nb > 0 ? t_pblk[qi] : 0, pyi = nb > 0 ? t_py[qi] : 0;
+    const int tfi = lane * gnw + gw;
+    const int blk0 = tfi < nt ? t_iblk[i0 + tfi / 6] : 0, q0 = tfi < nt ? t_iq[i0 + tfi / 6] : 0;
+    if (gw == wC && prev_row) st6g(Sm + 36l * prev_blk + 6 * rr, sv);
+    double L[21], r[6], yk[6], s0[6];
+    {
+      const double* D = Sm + 36l * t_diag[t];
+      double dr[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        ld6g(D + 6 * i, dr);
+#pragma unroll
+        for (int c = 0; c <= i; ++c) L[P6(i, c)] = dr[c];
+      }
+    }
+    ld6g(y + 6 * k, yk);
+    if (md == 0) {
+      ld6g(Sm + 36l * pblk + 6 * rr, sv);  // row rr of block (i, k)
+    } else {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) sv[c] = Sm[36l * pblk + 6 * c + rr];  // column rr of block (k, j)
+    }
+    ld6g(Sm + 36l * blk0 + 6 * (tfi % 6), s0);
+    const bool ok = chol6(L, r);
+    if (gw == wY || gw == wK) fwd6(L, r, yk);
+    if (gw == wK && lane == 0)
+      bad = bad || !ok || !isfinite(yk[0] + yk[1] + yk[2] + yk[3] + yk[4] + yk[5]);
+    fwd6(L, r, sv);
+    if (prow) {
+      st6g(Pw + 6 * lane, sv);
+      if (gw == wY) y[pyi + rr] -= sv[0] * yk[0] + sv[1] * yk[1] + sv[2] * yk[2] + sv[3] * yk[3] +
+                                   sv[4] * yk[4] + sv[5] * yk[5];
+    }
+    if (gw == wK && lane == 0) {
+      double* o = kf + 36l * k;
+#pragma unroll
+      for (int e = 0; e < 20; e += 2) reinterpret_cast<double2*>(o)[e / 2] = make_double2(L[e], L[e + 1]);
+      reinterpret_cast<double2*>(o)[10] = make_double2(L[20], 0.0);
+      st6g(o + 24, r);
+      st6g(o + 30, yk);
+    }
+    wave_sync<true>();
+    {
+      const int rq = tfi % 6;
+      double a[6];
+      ld6g(Pw + 36 * (q0 & 0xffff) + 6 * rq, a);
+      const double* B = Pw + 36 * (q0 >> 16);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) s0[c] -= dot6g(a, B + 6 * c);
+      if (tfi < nt) st6g(Sm + 36l * blk0 + 6 * rq, s0);
+    }
+    for (int t2 = tfi + 64 * gnw; t2 < nt; t2 += 64 * gnw) {
+      const int blk = t_iblk[i0 + t2 / 6], q = t_iq[i0 + t2 / 6], rq = t2 % 6;
+      double sr[6], a[6];
+      ld6g(Sm + 36l * blk + 6 * rq, sr);
+      ld6g(Pw + 36 * (q & 0xffff) + 6 * rq, a);
+      const double* B = Pw + 36 * (q >> 16);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) sr[c] -= dot6g(a, B + 6 * c);
+      st6g(Sm + 36l * blk + 6 * rq, sr);
+    }
+    prev_row = prow;
+    prev_blk = pblk;
+  };
+
+  // sides
+  const int g = wave >> 1, gw = wave & 1;
+  const int P = m > nbot ? m : nbot;
+  for (int p = 0; p < P && !prior_fail; ++p) {
+    const int t = g == 0 ? (p < m ? p : -1) : (p < nbot ? m + p : -1);
+    if (t >= 0) step(t, gw, 2, 0, 1, 1);
+    __syncthreads();
+  }
+  if (gw == 1 && prev_row) st6g(Sm + 36l * prev_blk + 6 * (lane % 6), sv);
+  prev_row = false;
+  __syncthreads();
+  mark(kS3Data);
+  // merge the bottom side's separator contributions (fixed order)
+  if (!prior_fail) {
+    for (int e = tid; e < 36 * T.nshadow; e += 256) {
+      const int mb = t_merge[e / 36];
+      if (mb >= 0) Sm[36l * mb + e % 36] += Sm[36l * (A.nprof + e / 36) + e % 36];
+    }
+    for (int e = tid; e < 6 * s; e += 256) y[6 * m + e] += y[6 * F + e];
+  }
+  __syncthreads();
+  mark(kS3Panel);
+  // separator
+  for (int t = m + nbot; t < F && !prior_fail; ++t) {
+    step(t, wave, 4, 1, 2, 3);
+    __syncthreads();
+  }
+  if (wave == 3 && prev_row) st6g(Sm + 36l * prev_blk + 6 * (lane % 6), sv);
+  if (bad) s_fail = 1;
+  __syncthreads();
+  mark(kS3Trail);
+
+  // back substitution: x_k = L_kk^-T y'_k, then y'_j -= B^T x_k for the blocks B of row
+  // k (j < k) and/or of column k in the bottom rows (i > k), one lane per (block, column)
+  auto solve_k = [&](int k, double (&x)[6]) {
+    const double* o = kf + 36l * k;
+    double Lk[21], rk[6];
+#pragma unroll
+    for (int e = 0; e < 20; e += 2) {
+      const double2 v = reinterpret_cast<const double2*>(o)[e / 2];
+      Lk[e] = v.x;
+      Lk[e + 1] = v.y;
+    }
+    Lk[20] = o[20];
+    ld6g(o + 24, rk);
+    ld6g(o + 30, x);
+    bwd6(Lk, rk, x);
+    wave_sync<true>();
+    if (lane == 0) st6g(kf + 36l * k + 30, x);
+  };
+  auto scatter_row = [&](int k, const double (&x)[6]) {
+    const int fk = t_first[k], ok_ = t_off[k];
+    for (int t = lane; t < 6 * (k - fk); t += 64) {
+      const int jj = fk + t / 6, c = t % 6;
+      const double* B = Sm + 36l * (ok_ + jj - fk);
+      double a = 0.0;
+#pragma unroll
+      for (int r2 = 0; r2 < 6; ++r2) a += B[6 * r2 + c] * x[r2];
+      kf[36l * jj + 30 + c] -= a;
+    }
+  };
+  auto scatter_col = [&](int k, const double (&x)[6]) {
+    const int c0 = t_cptr[k - m], nc = t_cptr[k - m + 1] - c0;
+    for (int t = lane; t < 6 * nc; t += 64) {
+      const int i = t_colb[2 * (c0 + t / 6)], b = t_colb[2 * (c0 + t / 6) + 1], c = t % 6;
+      const double* B = Sm + 36l * b;
+      double a = 0.0;
+#pragma unroll
+      for (int r2 = 0; r2 < 6; ++r2) a += B[6 * r2 + c] * x[r2];
+      kf[36l * i + 30 + c] -= a;
+    }
+  };
+  if (!s_fail && wave == 0)
+    for (int k = m + s - 1; k >= m; --k) {
+      double x[6];
+      solve_k(k, x);
+      scatter_row(k, x);
+      scatter_col(k, x);
+      wave_sync<true>();
+    }
+  __syncthreads();
+  if (!s_fail && wave == 0)
+    for (int k = m - 1; k >= 0; --k) {
+      double x[6];
+      solve_k(k, x);
+      scatter_row(k, x);
+      wave_sync<true>();
+    }
+  if (!s_fail && wave == 2)
+    for (int k = m + s; k < F; ++k) {
+      double x[6];
+      solve_k(k, x);
+      scatter_col(k, x);
+      wave_sync<true>();
+    }
+  __syncthreads();
+  mark(kS3Backsub);
+  const bool failed = s_fail != 0;
+  for (int e = tid; e < 6 * F; e += 256) A.dc[e] = failed ? 0.0 : kf[36l * (e / 6) + 30 + e % 6];
+  for (int c = tid; c < A.n_poses; c += 256) {
+    const double* Tp = pose_l + 12 * c;
+    double* out = A.pose_next + 12 * c;
+    if (failed || c < A.n_fixed) {
+      for (int e = 0; e < 12; ++e) out[e] = Tp[e];
+    } else {
+      const double* d6 = kf + 36l * (c - A.n_fixed) + 30;
+      double d[6];
+      for (int e = 0; e < 6; ++e) d[e] = d6[e];
+      se3_exp_apply(d, Tp, out);
+    }
+  }
+  if (tid == 0 && failed && !prior_fail) *A.status = A.iter_tag;
+  mark(kS3Tail);
+  if (kStamp && tid == 0 && A.stamps)
+    for (int k = 0; k < kS3Count; ++k) A.stamps[k] = st_acc[k];
+}
+
 template <class T>
 void upload(DevBuf& buf, const std::vector<T>& v, hipStream_t st) {
   buf.reserve(std::max<size_t>(v.size(), 1) * sizeof(T));
@@ -1179,6 +1538,10 @@ class BAEngine {
     upload(d_chunk_pt_, P.chunk_pt, st);
     upload(d_chunk_slot_base_, P.chunk_slot_base, st);
     upload(d_chunk_cam_base_, P.chunk_cam_base, st);
+    upload(d_chunk_hdr_, P.chunk_hdr, st);
+    upload(d_seg_acam_off_, P.seg_acam_off, st);
+    upload(d_seg_acam_, P.seg_acam, st);
+    upload(d_obs_acam_, P.obs_acam, st);
     upload(d_slot_ptr_, P.slot_ptr, st);
     upload(d_pair_list_, P.pair_list, st);
     upload(d_cam_ptr_, P.cam_ptr, st);
@@ -1230,6 +1593,23 @@ class BAEngine {
     }
     const size_t lds = solve_layout_.total;
     solve_lds_size_ = lds;
+    {  // two-sided K3 when its LDS image fits (profile + shadows in LDS)
+      const TwoSidedLayout& T2 = P.solve2_layout;
+      solve2_ = false;
+      if (T2.enabled && !getenv("VO_K3_V2")) {
+        solve2_layout_ = solve2_lds_layout(P.n_prof_blocks(), F, T2, P.n_poses);
+        if (solve2_layout_.total <= kSolveLdsMax) {
+          solve2_ = true;
+          upload(d_solve2_tab_, P.solve2_tab, st);
+          VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve2_kernel<false>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)solve2_layout_.total));
+          VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve2_kernel<true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)solve2_layout_.total));
+        }
+      }
+    }
     {
       const char* w = getenv("VO_K3_WAVES");
       solve_waves_ = w ? atoi(w) : 4;
@@ -1395,6 +1775,10 @@ class BAEngine {
     A.chunk_pt = d_chunk_pt_.as<int>();
     A.chunk_slot_base = d_chunk_slot_base_.as<int>();
     A.chunk_cam_base = d_chunk_cam_base_.as<int>();
+    A.chunk_hdr = d_chunk_hdr_.as<int4>();
+    A.seg_acam_off = d_seg_acam_off_.as<int>();
+    A.seg_acam = d_seg_acam_.as<int>();
+    A.obs_acam = d_obs_acam_.as<uint8_t>();
     A.slot_ptr = d_slot_ptr_.as<int>();
     A.pair_list = d_pair_list_.as<uint16_t>();
     A.cam_ptr = d_cam_ptr_.as<int>();
@@ -1489,6 +1873,22 @@ class BAEngine {
       hipLaunchKernelGGL((ba_solve_kernel<kL, kS, 4>), dim3(1), dim3(256), solve_lds_size_, ctx_->stream, A);
   }
   void launch_solve(const SolveArgs& A) {
+    if (solve2_) {
+      Solve2Args A2;
+      A2.base = A;
+      A2.tl = plan_.solve2_layout;
+      A2.tab = d_solve2_tab_.as<int>();
+      A2.lds_kf = (long)solve2_layout_.kf;
+      A2.lds_y = (long)solve2_layout_.y;
+      A2.lds_panel = (long)solve2_layout_.panel;
+      A2.lds_pose = (long)solve2_layout_.pose;
+      A2.lds_tab = (long)solve2_layout_.tab;
+      if (stamps_on_)
+        hipLaunchKernelGGL((ba_solve2_kernel<true>), dim3(1), dim3(256), solve2_layout_.total, ctx_->stream, A2);
+      else
+        hipLaunchKernelGGL((ba_solve2_kernel<false>), dim3(1), dim3(256), solve2_layout_.total, ctx_->stream, A2);
+      return;
+    }
     if (solve_lds_ && stamps_on_) launch_solve_t<true, true>(A);
     else if (solve_lds_) launch_solve_t<true, false>(A);
     else if (stamps_on_) launch_solve_t<false, true>(A);
@@ -1584,9 +1984,13 @@ class BAEngine {
   size_t sys_len_ = 0, solve_lds_size_ = 0;
   SolveLds solve_layout_{};
   int solve_waves_ = 4;
+  bool solve2_ = false;
+  SolveLds solve2_layout_{};
+  DevBuf d_solve2_tab_;
   DevBuf d_solve_tab_;
   DevBuf d_obs_uv_, d_obs_cam_, d_obs_te_, d_te_cam_, d_te_pt_, d_te_obs_, d_te_lcam_, d_pt_te_;
-  DevBuf d_chunk_obs_, d_chunk_te_, d_chunk_pt_, d_chunk_slot_base_, d_chunk_cam_base_;
+  DevBuf d_chunk_obs_, d_chunk_te_, d_chunk_pt_, d_chunk_slot_base_, d_chunk_cam_base_, d_chunk_hdr_;
+  DevBuf d_seg_acam_off_, d_seg_acam_, d_obs_acam_;
   DevBuf d_slot_ptr_, d_pair_list_, d_cam_ptr_, d_cam_list_;
   DevBuf d_seg_chunk_, d_seg_slot_off_, d_seg_cam_off_;
   DevBuf d_prof_first_, d_prof_off_, d_prof_last_, d_prof_src_ptr_, d_prof_src_, d_prof_diag_,
@@ -1603,6 +2007,11 @@ class BAEngine {
     std::vector<unsigned long long> h((size_t)nseg * kPhCount);
     VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
     VO_HIP_CHECK(hipMemcpy(h.data(), d_stamps_.ptr, h.size() * 8, hipMemcpyDeviceToHost));
+    if (n < 0) {  // raw per-segment rows (kPhCount values each; the last two are absolute times)
+      const int k = std::min<int>(-n, (int)h.size());
+      std::copy(h.begin(), h.begin() + k, out);
+      return k;
+    }
     int k = std::min(n, (int)kPhCount);
     for (int i = 0; i < k; ++i) {
       uint64_t acc = 0;

@@ -93,6 +93,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   struct Seg {
     int chunk0;
     std::vector<int32_t> cams;                   // free cameras (unsorted while growing)
+    std::vector<int32_t> acams;                  // all cameras (unsorted while growing)
     std::vector<std::pair<int32_t, int32_t>> slots;
   };
   std::vector<Seg> segs;
@@ -112,10 +113,13 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     cq.clear();
     for (int t = t0; t < t1; ++t)
       if (P.te_cam[t] >= n_fixed) cq.push_back(P.te_cam[t] - n_fixed);
+    if (t1 - t0 > kSegAllCams)
+      return fmt("landmark %ld is too wide (%ld cameras); limit: %ld cameras per landmark", P.pt_perm[q],
+                 t1 - t0, (long)kSegAllCams);
     const int k = (int)cq.size();
     if (nob > kChunkObs || nte > kChunkTe || k > kSegCams || k * (k + 1) / 2 > kSegSlots)
       return fmt("landmark %ld is too wide (%ld observations, %ld free cameras); "
-                 "limits: 128 observations, 10 free cameras per landmark",
+                 "limits: 64 observations, 10 free cameras per landmark",
                  P.pt_perm[q], nob, k);
     const int npairs = k * (k + 1) / 2;
     bool chunk_fits = seg_open && c_obs + nob <= kChunkObs && c_te + nte <= kChunkTe &&
@@ -131,10 +135,12 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
           const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
           nslots += std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end();
         }
-      seg_fits = ncams <= kSegCams && nslots <= kSegSlots;
+      int nacams = (int)s.acams.size();
+      for (int t = t0; t < t1; ++t) nacams += find_or_neg(s.acams, P.te_cam[t]) < 0;
+      seg_fits = ncams <= kSegCams && nslots <= kSegSlots && nacams <= kSegAllCams;
     }
     if (!seg_fits || (!chunk_fits && s_obs >= seg_obs_target)) {
-      segs.push_back(Seg{(int)P.chunk_obs.size(), {}, {}});
+      segs.push_back(Seg{(int)P.chunk_obs.size(), {}, {}, {}});
       seg_open = true;
       s_obs = 0;
       open_chunk(q);
@@ -144,6 +150,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     Seg& s = segs.back();
     for (int c : cq)
       if (find_or_neg(s.cams, c) < 0) s.cams.push_back(c);
+    for (int t = t0; t < t1; ++t)
+      if (find_or_neg(s.acams, P.te_cam[t]) < 0) s.acams.push_back(P.te_cam[t]);
     for (int a = 0; a < k; ++a)
       for (int b = 0; b <= a; ++b) {
         const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
@@ -164,6 +172,9 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   P.seg_chunk.assign(1, 0);
   P.seg_slot_off.assign(1, 0);
   P.seg_cam_off.assign(1, 0);
+  P.seg_acam_off.assign(1, 0);
+  P.seg_acam.clear();
+  P.obs_acam.assign(std::max(M, 1), 0);
   P.chunk_slot_base.assign(nchunks, 0);
   P.chunk_cam_base.assign(nchunks, 0);
   for (size_t si = 0; si < segs.size(); ++si) {
@@ -176,6 +187,12 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       P.slot_i.push_back(pr.first);
       P.slot_j.push_back(pr.second);
     }
+    std::sort(s.acams.begin(), s.acams.end());
+    P.seg_acam.insert(P.seg_acam.end(), s.acams.begin(), s.acams.end());
+    P.seg_acam_off.push_back((int32_t)P.seg_acam.size());
+    for (int o = P.chunk_obs[ch0]; o < P.chunk_obs[ch1]; ++o)
+      P.obs_acam[o] = (uint8_t)(std::lower_bound(s.acams.begin(), s.acams.end(), P.obs_cam[o]) -
+                                s.acams.begin());
     for (int c : s.cams) {
       P.segcam_f.push_back(c);
       const auto d = std::make_pair(c, c);
@@ -237,8 +254,154 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   if (P.pair_list.empty()) P.pair_list.push_back(0);  // keep device arrays non-empty
   if (P.cam_list.empty()) P.cam_list.push_back(0);
   if (P.camo_list.empty()) P.camo_list.push_back(0);
+  // chunk headers: ob0 nob te0 nte p0 npt sb cb e0 e1 c0 c1 q0 q1 (+2 spare)
+  P.chunk_hdr.assign((size_t)std::max(nchunks, 1) * kChunkHdr, 0);
+  for (size_t si = 0; si + 1 < P.seg_chunk.size(); ++si) {
+    const int ns = P.seg_slot_off[si + 1] - P.seg_slot_off[si];
+    const int nc = P.seg_cam_off[si + 1] - P.seg_cam_off[si];
+    for (int ch = P.seg_chunk[si]; ch < P.seg_chunk[si + 1]; ++ch) {
+      int32_t* h = &P.chunk_hdr[(size_t)ch * kChunkHdr];
+      const int sb = P.chunk_slot_base[ch], cb = P.chunk_cam_base[ch];
+      h[0] = P.chunk_obs[ch];
+      h[1] = P.chunk_obs[ch + 1] - P.chunk_obs[ch];
+      h[2] = P.chunk_te[ch];
+      h[3] = P.chunk_te[ch + 1] - P.chunk_te[ch];
+      h[4] = P.chunk_pt[ch];
+      h[5] = P.chunk_pt[ch + 1] - P.chunk_pt[ch];
+      h[6] = sb;
+      h[7] = cb;
+      h[8] = P.slot_ptr[sb];
+      h[9] = P.slot_ptr[sb + ns];
+      h[10] = P.cam_ptr[cb];
+      h[11] = P.cam_ptr[cb + nc];
+      h[12] = P.camo_ptr[cb];
+      h[13] = P.camo_ptr[cb + nc];
+    }
+  }
   if (P.segcam_diag.empty()) P.segcam_diag.push_back(0);
   return "";
+}
+
+// Two-sided K3 tables (see TwoSidedLayout); leaves solve2_layout.enabled = 0 when the
+// profile is not monotone or too small to profit.
+static void build_two_sided(BAPlan& P) {
+  const int F = P.n_free;
+  const std::vector<int32_t>& first = P.prof_first;
+  TwoSidedLayout& L = P.solve2_layout;
+  L = TwoSidedLayout();
+  P.solve2_tab.assign(1, 0);
+  int w = 0;
+  for (int i = 0; i < F; ++i) {
+    if (i > 0 && first[i] < first[i - 1]) return;  // not monotone
+    w = std::max(w, i - first[i]);
+  }
+  const int s = std::max(1, w);
+  const int m = (F - s) / 2, nbot = F - m - s;
+  if (m < 4 || nbot < 4) return;
+  auto blk = [&](int i, int j) { return P.prof_off[i] + (j - first[i]); };
+  auto in_sep = [&](int i) { return i >= m && i < m + s; };
+  const int nprof = P.n_prof_blocks();
+  auto shadow = [&](int a, int b) { return nprof + (a - m) * (a - m + 1) / 2 + (b - m); };
+  std::vector<int32_t> col, mode, diag, sptr{0}, pblk, py, iptr{0}, iblk, iq;
+  int maxnb = 0;
+  auto add_items = [&](const std::vector<int>& rows, bool bottom) {
+    const int nb = (int)rows.size();
+    for (int q1 = 0; q1 < nb; ++q1)
+      for (int q2 = 0; q2 <= q1; ++q2) {
+        const int a = rows[q1], b = rows[q2];  // a >= b (rows ascending)
+        iblk.push_back(bottom && in_sep(a) && in_sep(b) ? shadow(a, b) : blk(a, b));
+        iq.push_back(q1 | (q2 << 16));
+      }
+    iptr.push_back((int32_t)iblk.size());
+  };
+  // top steps (top-down, panels may include separator rows)
+  for (int k = 0; k < m; ++k) {
+    std::vector<int> rows;
+    for (int i = k + 1; i <= P.prof_last[k]; ++i)
+      if (first[i] <= k) rows.push_back(i);
+    col.push_back(k);
+    mode.push_back(0);
+    diag.push_back(blk(k, k));
+    for (int i : rows) {
+      pblk.push_back(blk(i, k));
+      py.push_back(6 * i);
+    }
+    sptr.push_back((int32_t)pblk.size());
+    maxnb = std::max(maxnb, (int)rows.size());
+    add_items(rows, false);
+  }
+  // bottom steps (bottom-up: row k's blocks (k, j), j in [first[k], k))
+  for (int k = F - 1; k >= m + s; --k) {
+    std::vector<int> rows;
+    for (int j = first[k]; j < k; ++j) rows.push_back(j);
+    col.push_back(k);
+    mode.push_back(1);
+    diag.push_back(blk(k, k));
+    for (int j : rows) {
+      pblk.push_back(blk(k, j));
+      py.push_back(in_sep(j) ? 6 * F + 6 * (j - m) : 6 * j);
+    }
+    sptr.push_back((int32_t)pblk.size());
+    maxnb = std::max(maxnb, (int)rows.size());
+    add_items(rows, true);
+  }
+  // separator steps (top-down within the separator)
+  for (int k = m; k < m + s; ++k) {
+    std::vector<int> rows;
+    for (int i = k + 1; i < m + s; ++i)
+      if (first[i] <= k) rows.push_back(i);
+    col.push_back(k);
+    mode.push_back(0);
+    diag.push_back(blk(k, k));
+    for (int i : rows) {
+      pblk.push_back(blk(i, k));
+      py.push_back(6 * i);
+    }
+    sptr.push_back((int32_t)pblk.size());
+    maxnb = std::max(maxnb, (int)rows.size());
+    add_items(rows, false);
+  }
+  std::vector<int32_t> merge;
+  for (int a = m; a < m + s; ++a)
+    for (int b = m; b <= a; ++b) merge.push_back(first[a] <= b ? blk(a, b) : -1);
+  // column lists for the bottom back substitution: k >= m, bottom rows i > k
+  std::vector<int32_t> cptr{0}, cl;
+  for (int k = m; k < F; ++k) {
+    for (int i = std::max(k + 1, m + s); i < F; ++i)
+      if (first[i] <= k) {
+        cl.push_back(i);
+        cl.push_back(blk(i, k));
+      }
+    cptr.push_back((int32_t)(cl.size() / 2));
+  }
+  std::vector<int32_t>& T = P.solve2_tab;
+  T.clear();
+  auto put = [&](int& o, const std::vector<int32_t>& v) {
+    o = (int)T.size();
+    T.insert(T.end(), v.begin(), v.end());
+  };
+  std::vector<int32_t> offv(P.prof_off.begin(), P.prof_off.begin() + F);
+  put(L.col, col);
+  put(L.mode, mode);
+  put(L.diag, diag);
+  put(L.step_ptr, sptr);
+  put(L.panel_blk, pblk);
+  put(L.panel_y, py);
+  put(L.item_ptr, iptr);
+  put(L.item_blk, iblk);
+  put(L.item_q, iq);
+  put(L.merge_main, merge);
+  put(L.colb_ptr, cptr);
+  put(L.colb, cl);
+  put(L.off, offv);
+  put(L.first, first);
+  L.len = (int)T.size();
+  L.m = m;
+  L.s = s;
+  L.nbot = nbot;
+  L.nshadow = s * (s + 1) / 2;
+  L.max_panel = maxnb;
+  L.enabled = maxnb <= 10 ? 1 : 0;  // one lane per panel row per wave
 }
 
 std::vector<int32_t> local_profile_first(const BAPlan& P) {
@@ -324,6 +487,7 @@ void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
   L.len = (int)T.size();
   L.max_panel = maxnb;
   if (T.empty()) T.push_back(0);
+  build_two_sided(P);
 }
 
 }  // namespace vo

@@ -33,12 +33,33 @@ constexpr int kChunkTe = VO_CHUNK_OBS;
 constexpr int kChunkPts = VO_CHUNK_OBS / 2;
 constexpr int kChunkPairs = 8 * VO_CHUNK_OBS;  // camera-pair (x, y) entries of one chunk, staged in LDS
 constexpr int kSegSlots = 64;
-constexpr int kSegCams = 32;
+constexpr int kChunkHdr = 16;
+constexpr int kSegCams = 24;     // free (window) cameras of a segment
+constexpr int kSegAllCams = 16;  // all cameras its observations reference (poses staged in LDS)
 
 struct SolveTableLayout {
   int diag = 0, off = 0, first = 0, step_ptr = 0, panel_i = 0, panel_blk = 0, item_ptr = 0,
       item_blk = 0, item_q = 0, len = 0;
   int max_panel = 0;  // most panel blocks in one column
+};
+
+// Two-sided ("twisted") K3 plan, used when the profile is monotone (first[] non
+// decreasing) and wide enough.  With w = max(i - first[i]) and a separator
+// [m, m+s), s = w, the top columns 0..m-1 are eliminated top-down and the bottom
+// rows F-1..m+s bottom-up (row panels: L~_{j,k} = (C_k^-1 S_{k,j})^T, stored in
+// block (k, j) as rows of L~_{j,k}) concurrently; the two sides meet only in the
+// separator-separator blocks and separator rhs, which the bottom side accumulates
+// in shadow copies (blocks nprof + sh, rhs 6F + 6(j - m)) merged before the
+// separator is factored top-down.  Steps are numbered: top 0..m-1, bottom
+// m..m+nbot-1 (rows F-1 down to m+s), separator after that.
+struct TwoSidedLayout {
+  int enabled = 0, m = 0, s = 0, nbot = 0, nshadow = 0;
+  int col = 0, mode = 0, diag = 0, step_ptr = 0, panel_blk = 0, panel_y = 0, item_ptr = 0,
+      item_blk = 0, item_q = 0;
+  int merge_main = 0;           // per shadow block: its profile block, -1 if none
+  int colb_ptr = 0, colb = 0;   // per k >= m: (bottom row i > k, block (i, k)) pairs
+  int off = 0, first = 0, len = 0;
+  int max_panel = 0;
 };
 
 struct BAPlan {
@@ -55,6 +76,9 @@ struct BAPlan {
   // chunks
   std::vector<int32_t> chunk_obs, chunk_te, chunk_pt;  // n_chunks+1
   std::vector<int32_t> chunk_slot_base, chunk_cam_base;  // index into slot_ptr / cam_ptr
+  // per chunk, kChunkHdr ints: every offset K1 needs to stage the chunk, so that one
+  // (uniform) load precedes all list loads -- see ChunkHdr in ba.hip
+  std::vector<int32_t> chunk_hdr;
   std::vector<int32_t> slot_ptr;   // per chunk: nslots(seg)+1 offsets into pair_list
   std::vector<uint16_t> pair_list; // (te_x_local | te_y_local << 8)
   std::vector<int32_t> cam_ptr;    // per chunk: ncams(seg)+1 offsets into cam_list
@@ -66,6 +90,8 @@ struct BAPlan {
   std::vector<int32_t> slot_i, slot_j;   // per slab slot: global free-camera block (i >= j)
   std::vector<int32_t> segcam_f;         // per slab b entry: free camera
   std::vector<int32_t> segcam_diag;      // per slab b entry: its diagonal slot within the segment
+  std::vector<int32_t> seg_acam_off, seg_acam;  // per segment: every camera its observations see
+  std::vector<uint8_t> obs_acam;                // per observation: index into its segment's seg_acam
   // profile of S (block rows over free cameras)
   std::vector<int32_t> prof_first, prof_off, prof_last;  // F, F+1, F
   std::vector<int32_t> prof_src_ptr, prof_src;  // per profile block: slab slots
@@ -77,6 +103,8 @@ struct BAPlan {
   // plus diag[k] (profile block (k, k)), off[k], first[k].
   std::vector<int32_t> solve_tab;
   SolveTableLayout solve_layout;
+  std::vector<int32_t> solve2_tab;
+  TwoSidedLayout solve2_layout;
 
   int n_chunks() const { return (int)chunk_obs.size() - 1; }
   int n_segments() const { return (int)seg_chunk.size() - 1; }
