@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "ba_plan.h"
@@ -1289,15 +1290,21 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   // One elimination step t on a group of gnw waves (gw: this wave's index in it); roles
   // (group-local): wY updates y, wK keeps (L, 1/diag, y') and the failure flag, wC
   // writes the previous step's panel into the profile.
-  auto step = [&](int t, int gw, int gnw, int wY, int wK, int wC) {
+  // kPairs: each trailing task covers rows {rp, rp+3} of one block (2-wave groups: one
+  // round of tasks over 128 lanes); otherwise one row per task.
+  auto step = [&](int t, int gw, int gnw, int wY, int wK, int wC, auto pairs_tag) {
+    constexpr bool kPairs = decltype(pairs_tag)::value;
     const int k = t_col[t], md = t_mode[t];
     const int p0 = t_sptr[t], nb = t_sptr[t + 1] - p0;
     const int i0 = t_iptr[t], nt = 6 * (t_iptr[t + 1] - i0);
     const bool prow = lane < 6 * nb;
     const int rr = lane % 6, qi = p0 + (prow ? lane / 6 : 0);
     const int pblk = nb > 0 ? t_pblk[qi] : 0, pyi = nb > 0 ? t_py[qi] : 0;
-    const int tfi = lane * gnw + gw;
-    const int blk0 = tfi < nt ? t_iblk[i0 + tfi / 6] : 0, q0 = tfi < nt ? t_iq[i0 + tfi / 6] : 0;
+    // trailing tasks: (block item, row or row pair), one per lane per round
+    constexpr int kRows = kPairs ? 2 : 1, kPer = 6 / kRows;
+    const int ntask = nt / kRows, tfi = lane * gnw + gw;
+    const int it0 = tfi < ntask ? tfi / kPer : 0, rp0 = tfi % kPer;
+    const int blk0 = tfi < ntask ? t_iblk[i0 + it0] : 0, q0 = tfi < ntask ? t_iq[i0 + it0] : 0;
     if (gw == wC && prev_row) st6g(Sm + 36l * prev_blk + 6 * rr, sv);
     double L[21], r[6], yk[6], s0[6];
     {
@@ -1317,7 +1324,9 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
 #pragma unroll
       for (int c = 0; c < 6; ++c) sv[c] = Sm[36l * pblk + 6 * c + rr];  // column rr of block (k, j)
     }
-    ld6g(Sm + 36l * blk0 + 6 * (tfi % 6), s0);
+    double s1[6];
+    ld6g(Sm + 36l * blk0 + 6 * rp0, s0);
+    if (kPairs) ld6g(Sm + 36l * blk0 + 6 * (rp0 + 3), s1);
     const bool ok = chol6(L, r);
     if (gw == wY || gw == wK) fwd6(L, r, yk);
     if (gw == wK && lane == 0)
@@ -1337,24 +1346,31 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
       st6g(o + 30, yk);
     }
     wave_sync<true>();
-    {
-      const int rq = tfi % 6;
-      double a[6];
-      ld6g(Pw + 36 * (q0 & 0xffff) + 6 * rq, a);
-      const double* B = Pw + 36 * (q0 >> 16);
-#pragma unroll
-      for (int c = 0; c < 6; ++c) s0[c] -= dot6g(a, B + 6 * c);
-      if (tfi < nt) st6g(Sm + 36l * blk0 + 6 * rq, s0);
-    }
-    for (int t2 = tfi + 64 * gnw; t2 < nt; t2 += 64 * gnw) {
-      const int blk = t_iblk[i0 + t2 / 6], q = t_iq[i0 + t2 / 6], rq = t2 % 6;
-      double sr[6], a[6];
-      ld6g(Sm + 36l * blk + 6 * rq, sr);
-      ld6g(Pw + 36 * (q & 0xffff) + 6 * rq, a);
+    auto task = [&](int blk, int q, int rp, double (&x0)[6], double (&x1)[6], bool store) {
+      double a0[6], a1[6], bq[6];
+      ld6g(Pw + 36 * (q & 0xffff) + 6 * rp, a0);
+      if (kPairs) ld6g(Pw + 36 * (q & 0xffff) + 6 * (rp + 3), a1);
       const double* B = Pw + 36 * (q >> 16);
 #pragma unroll
-      for (int c = 0; c < 6; ++c) sr[c] -= dot6g(a, B + 6 * c);
-      st6g(Sm + 36l * blk + 6 * rq, sr);
+      for (int c = 0; c < 6; ++c) {
+        ld6g(B + 6 * c, bq);
+        x0[c] -= a0[0] * bq[0] + a0[1] * bq[1] + a0[2] * bq[2] + a0[3] * bq[3] + a0[4] * bq[4] + a0[5] * bq[5];
+        if (kPairs)
+          x1[c] -= a1[0] * bq[0] + a1[1] * bq[1] + a1[2] * bq[2] + a1[3] * bq[3] + a1[4] * bq[4] + a1[5] * bq[5];
+      }
+      if (store) {
+        st6g(Sm + 36l * blk + 6 * rp, x0);
+        if (kPairs) st6g(Sm + 36l * blk + 6 * (rp + 3), x1);
+      }
+    };
+    task(blk0, q0, rp0, s0, s1, tfi < ntask);
+    for (int t2 = tfi + 64 * gnw; t2 < ntask; t2 += 64 * gnw) {
+      const int it = t2 / kPer, rp = t2 % kPer;
+      const int blk = t_iblk[i0 + it], q = t_iq[i0 + it];
+      double x0[6], x1[6];
+      ld6g(Sm + 36l * blk + 6 * rp, x0);
+      if (kPairs) ld6g(Sm + 36l * blk + 6 * (rp + 3), x1);
+      task(blk, q, rp, x0, x1, true);
     }
     prev_row = prow;
     prev_blk = pblk;
@@ -1365,7 +1381,7 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   const int P = m > nbot ? m : nbot;
   for (int p = 0; p < P && !prior_fail; ++p) {
     const int t = g == 0 ? (p < m ? p : -1) : (p < nbot ? m + p : -1);
-    if (t >= 0) step(t, gw, 2, 0, 1, 1);
+    if (t >= 0) step(t, gw, 2, 0, 1, 1, std::true_type{});
     __syncthreads();
   }
   if (gw == 1 && prev_row) st6g(Sm + 36l * prev_blk + 6 * (lane % 6), sv);
@@ -1384,7 +1400,7 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   mark(kS3Panel);
   // separator
   for (int t = m + nbot; t < F && !prior_fail; ++t) {
-    step(t, wave, 4, 1, 2, 3);
+    step(t, wave, 4, 1, 2, 3, std::false_type{});
     __syncthreads();
   }
   if (wave == 3 && prev_row) st6g(Sm + 36l * prev_blk + 6 * (lane % 6), sv);
