@@ -31,11 +31,14 @@ constexpr int kKStep = 64;          // K of v_mfma_i32_16x16x64_i8
 constexpr int kMaxDpInt = 256;      // int path keeps A fragments in registers
 constexpr int kRowsPerWave = 64;    // 4 M-tiles of 16 rows
 constexpr int kRowsPerWG = 256;     // 4 waves
-// Key offset: |a'|^2 <= Dp * 128^2 = Dp << 14, so d2 - |a'|^2 + (Dp << 14) >= 0; and
-// d2 - |a'|^2 = sum(b'^2 - 2 a'b') <= Dp * 48896, so the key stays below
-// Dp * 65280 < 2^24 for Dp <= 256: 24 key bits + 8 column-tile bits.
-__host__ __device__ constexpr int norm_off(int Dp) { return Dp << 14; }
-constexpr uint32_t kSent = 0xFFFFFFFFu;
+// Key range: |a'|^2 <= Dp * 128^2 and d2 - |a'|^2 = sum(b'^2 - 2 a'b') <= Dp * 48896, so
+// d2 - |a'|^2 lies in [-Dp * 16384, Dp * 48896]: 24 key bits + 8 column-tile bits.
+// int8 path keys are kept in max form: ((2 a'.b' - |b'|^2 + off) << 8) | (255 - tile)
+// = ((off - (d2 - |a'|^2)) << 8) | (255 - tile), off = Dp * 48896 + 1, so a valid key is
+// in [1 << 8, (Dp * 65280 + 1) << 8] (< 2^32 for Dp <= 256) and larger = closer; ties in
+// d2 prefer the lower column tile (lower train index), and 0 (padding) never wins.  One
+// v_lshl_add_u32 forms a key from the MFMA dot product.
+__host__ __device__ constexpr uint32_t max_off(int Dp) { return (uint32_t)Dp * 48896u + 1u; }
 constexpr int kCollide = 1 << 22;   // sqrtf(n) == sqrtf(n+1) needs n >= 2^22
 constexpr int kFloatTile = 64;      // float path: 64 x 64 pair tile per WG
 constexpr int kFloatKC = 32;        // float path k-chunk staged in LDS
@@ -74,7 +77,6 @@ __global__ __launch_bounds__(256) void pack_kernel(
     const float* __restrict__ des, int n, int dim, int Dp, int n_pad,
     long in_bstride, long q_bstride, int8_t* __restrict__ q8, int* __restrict__ norms,
     uint32_t* __restrict__ colconst, int* __restrict__ flag) {
-  const int off = norm_off(Dp);
   const int b = blockIdx.y;
   const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
   const int sub = threadIdx.x & 15;
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(256) void pack_kernel(
     norms[b * (long)n_pad + row] = acc;
     if (colconst) {
       colconst[b * (long)n_pad + row] =
-          row < n ? (((uint32_t)(acc + off)) << 8) | ((uint32_t)(row >> 4) & 255u) : kSent;
+          row < n ? ((max_off(Dp) - (uint32_t)acc) << 8) | (255u - ((uint32_t)(row >> 4) & 255u)) : 0u;
     }
   }
 }
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(256) void match_i8_kernel(
     const int* __restrict__ flag) {
   if (*flag) return;  // not u8-valued: the float path owns this call
   constexpr int Dp = KS * kKStep;
-  constexpr int kOff = norm_off(Dp);
+  constexpr uint32_t kOffMax = max_off(Dp);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int b = blockIdx.z;
@@ -147,42 +149,56 @@ __global__ __launch_bounds__(256) void match_i8_kernel(
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) m1[mt][r] = m2[mt][r] = kSent;
+    for (int r = 0; r < 4; ++r) m1[mt][r] = m2[mt][r] = 0u;
 
   const int c0 = split * split_w;
   const int c1 = min(c0 + split_w, n1_pad);
-  const int8_t* bp = B + (long)(c0 + (lane & 15)) * Dp + 16 * (lane >> 4);
-  v4i bnext[KS];
-  uint32_t ccnext = 0;
-  if (c0 < c1) {
+  const int8_t* bbase = B + (long)(lane & 15) * Dp + 16 * (lane >> 4);
+  // B fragments of column tile c (clamped to the last tile: loads are unconditional)
+  auto loadb = [&](int c, v4i (&bf)[KS], uint32_t& ccv) {
+    const int cl = min(c, c1 - 16);
+    const int8_t* bp = bbase + (long)cl * Dp;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) bnext[ks] = *reinterpret_cast<const v4i*>(bp + ks * kKStep);
-    ccnext = cc[c0 + (lane & 15)];
-  }
-  for (int c = c0; c < c1; c += 16) {
-    v4i bfrag[KS];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) bfrag[ks] = bnext[ks];
-    const uint32_t ccol = ccnext;
-    if (c + 16 < c1) {
-      bp += 16 * Dp;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) bnext[ks] = *reinterpret_cast<const v4i*>(bp + ks * kKStep);
-      ccnext = cc[c + 16 + (lane & 15)];
-    }
+    for (int ks = 0; ks < KS; ++ks) bf[ks] = *reinterpret_cast<const v4i*>(bp + ks * kKStep);
+    ccv = cc[cl + (lane & 15)];
+  };
+  // one 16-column tile: the four row tiles' MFMAs into separate accumulators, then the
+  // top-2 update (v_lshl_add_u32 + v_med3_u32 + v_max_u32 per pair)
+  auto tile = [&](const v4i (&bf)[KS], uint32_t ccol) {
+    v4i acc[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      v4i acc = {0, 0, 0, 0};
+      acc[mt] = v4i{0, 0, 0, 0};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], bfrag[ks], acc, 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], bf[ks], acc[mt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const uint32_t p = ccol - ((uint32_t)acc[r] << 9);
+        const uint32_t p = ((uint32_t)acc[mt][r] << 9) + ccol;
         m2[mt][r] = med3_u32(m1[mt][r], m2[mt][r], p);
-        m1[mt][r] = min(m1[mt][r], p);
+        m1[mt][r] = max(m1[mt][r], p);
+      }
+  };
+  if (c0 < c1) {
+    // four tile buffers: the fragments of tile c+64 load while tiles c..c+48 compute
+    v4i bf[4][KS];
+    uint32_t cq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) loadb(c0 + 16 * u, bf[u], cq[u]);
+    int c = c0;
+    for (; c + 64 <= c1; c += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        tile(bf[u], cq[u]);
+        loadb(c + 64 + 16 * u, bf[u], cq[u]);
       }
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (c + 16 * u < c1) tile(bf[u], cq[u]);
   }
 
   // unpack to (d2, j) keys and merge the 16 lanes that share each row
@@ -194,13 +210,13 @@ __global__ __launch_bounds__(256) void match_i8_kernel(
       const int row = rowbase + mt * 16 + (lane >> 4) * 4 + r;
       const int na = norma[b * (long)n0_pad + row];
       uint64_t k1 = ~0ull, k2 = ~0ull;
-      if (m1[mt][r] != kSent) {
-        const uint32_t d = (m1[mt][r] >> 8) - kOff + na;
-        k1 = key64(d, jblock + 16 * (m1[mt][r] & 255u) + (lane & 15));
+      if (m1[mt][r] != 0u) {
+        const uint32_t d = kOffMax - (m1[mt][r] >> 8) + na;
+        k1 = key64(d, jblock + 16 * (255u - (m1[mt][r] & 255u)) + (lane & 15));
       }
-      if (m2[mt][r] != kSent) {
-        const uint32_t d = (m2[mt][r] >> 8) - kOff + na;
-        k2 = key64(d, jblock + 16 * (m2[mt][r] & 255u) + (lane & 15));
+      if (m2[mt][r] != 0u) {
+        const uint32_t d = kOffMax - (m2[mt][r] >> 8) + na;
+        k2 = key64(d, jblock + 16 * (255u - (m2[mt][r] & 255u)) + (lane & 15));
       }
 #pragma unroll
       for (int m = 1; m < 16; m <<= 1) merge2(k1, k2, shfl_xor64(k1, m), shfl_xor64(k2, m));
@@ -424,7 +440,11 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
 
   // split the train columns so the grid fills the chip (w | 4096, w >= 64)
   const int row_wgs = n0_pad / kRowsPerWG;
-  const int want = std::max(1, ceil_div(2 * ctx->num_cus, (int64_t)row_wgs * batch));
+  static const int wgs_per_cu = [] {
+    const char* e = getenv("VO_MATCH_WGS_PER_CU");
+    return e ? std::max(1, atoi(e)) : 2;
+  }();
+  const int want = std::max(1, ceil_div(wgs_per_cu * ctx->num_cus, (int64_t)row_wgs * batch));
   int w = pow2_floor(std::max(1, n1_pad / want));
   w = std::max(256, std::min(4096, w));
   const int nsplit = std::max(1, ceil_div(n1_pad, w));
