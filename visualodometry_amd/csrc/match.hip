@@ -153,18 +153,34 @@ __global__ __launch_bounds__(256) void match_i8_kernel(
 
   const int c0 = split * split_w;
   const int c1 = min(c0 + split_w, n1_pad);
-  const int8_t* bbase = B + (long)(lane & 15) * Dp + 16 * (lane >> 4);
-  // B fragments of column tile c (clamped to the last tile: loads are unconditional)
-  auto loadb = [&](int c, v4i (&bf)[KS], uint32_t& ccv) {
-    const int cl = min(c, c1 - 16);
-    const int8_t* bp = bbase + (long)cl * Dp;
+  // B is staged per 64-column chunk in LDS, shared by the four waves (one global fetch
+  // per workgroup instead of one per wave): 4 threads per column, rows padded to
+  // Dp + 16 bytes so a wave's 16-lane ds_read_b128 groups hit distinct banks.
+  constexpr int kRow = Dp + 16;
+  __shared__ __attribute__((aligned(16))) int8_t sB[2][64 * kRow];
+  __shared__ uint32_t sC[2][64];
+  const int tid = threadIdx.x;
+  auto gload = [&](int cbase, v4i (&g)[KS], uint32_t& gc) {
+    const int col = min(cbase + (tid >> 2), c1 - 1);  // clamped, unconditional
+    const int8_t* src = B + (long)col * Dp + (tid & 3) * 16 * KS;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) bf[ks] = *reinterpret_cast<const v4i*>(bp + ks * kKStep);
-    ccv = cc[cl + (lane & 15)];
+    for (int ks = 0; ks < KS; ++ks) g[ks] = *reinterpret_cast<const v4i*>(src + 16 * ks);
+    gc = cc[min(cbase + (tid & 63), c1 - 1)];
+  };
+  auto sstore = [&](int buf, const v4i (&g)[KS], uint32_t gc) {
+    int8_t* dst = &sB[buf][(tid >> 2) * kRow + (tid & 3) * 16 * KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<v4i*>(dst + 16 * ks) = g[ks];
+    if (tid < 64) sC[buf][tid] = gc;
   };
   // one 16-column tile: the four row tiles' MFMAs into separate accumulators, then the
   // top-2 update (v_lshl_add_u32 + v_med3_u32 + v_max_u32 per pair)
-  auto tile = [&](const v4i (&bf)[KS], uint32_t ccol) {
+  auto tile = [&](int buf, int u) {
+    v4i bf[KS];
+    const int8_t* fp = &sB[buf][(16 * u + (lane & 15)) * kRow + 16 * (lane >> 4)];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) bf[ks] = *reinterpret_cast<const v4i*>(fp + ks * kKStep);
+    const uint32_t ccol = sC[buf][16 * u + (lane & 15)];
     v4i acc[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -182,23 +198,22 @@ __global__ __launch_bounds__(256) void match_i8_kernel(
         m1[mt][r] = max(m1[mt][r], p);
       }
   };
-  if (c0 < c1) {
-    // four tile buffers: the fragments of tile c+64 load while tiles c..c+48 compute
-    v4i bf[4][KS];
-    uint32_t cq[4];
+  if (c0 < c1) {  // uniform over the workgroup (split bounds)
+    const int nchunk = (c1 - c0 + 63) / 64;
+    v4i g[KS];
+    uint32_t gc;
+    gload(c0, g, gc);
+    sstore(0, g, gc);
+    __syncthreads();
+    for (int ch = 0; ch < nchunk; ++ch) {
+      const int buf = ch & 1, cb = c0 + 64 * ch;
+      if (ch + 1 < nchunk) gload(cb + 64, g, gc);  // in flight during this chunk
 #pragma unroll
-    for (int u = 0; u < 4; ++u) loadb(c0 + 16 * u, bf[u], cq[u]);
-    int c = c0;
-    for (; c + 64 <= c1; c += 64) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        tile(bf[u], cq[u]);
-        loadb(c + 64 + 16 * u, bf[u], cq[u]);
-      }
+      for (int u = 0; u < 4; ++u)
+        if (cb + 16 * u < c1) tile(buf, u);
+      if (ch + 1 < nchunk) sstore(buf ^ 1, g, gc);
+      __syncthreads();
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (c + 16 * u < c1) tile(bf[u], cq[u]);
   }
 
   // unpack to (d2, j) keys and merge the 16 lanes that share each row
