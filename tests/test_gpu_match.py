@@ -153,3 +153,29 @@ def test_batch_device_matches_single(ctx):
         ref = match_ref.match_int(*pairs[k])
         got = np.nonzero(best[k] >= 0)[0]
         np.testing.assert_array_equal(np.stack([got, best[k][got]], 1), ref)
+
+
+def test_int_and_float_calls_alternate_on_one_context(ctx):
+    """The per-call "not 0..255 integers" flag is a generation tag (no reset between
+    calls): an integer call right after a float call must take the int8 path again."""
+    s0, s1 = sift_like_pair(300, 400, 21)
+    f0, f1 = superpoint_like_pair(300, 400, 22)
+    for _ in range(2):
+        _check_knn2(s0, s1, ctx)
+        _check_knn2(f0, f1, ctx, oracle="c")
+    # one non-integer value in the train side alone switches the whole call
+    g1 = s1.copy()
+    g1[7, 3] += 0.5
+    _check_knn2(s0, g1, ctx, oracle="c")
+    _check_knn2(s0, s1, ctx)
+
+
+def test_duplicate_train_rows_across_lanes_tiles_and_splits(ctx):
+    """500 distinct rows, each repeated 8 times at shuffled positions among 4000 train rows:
+    exact d2 ties inside a 16-lane group, across column tiles and across splits must all
+    resolve to the lower train index, as in the oracle."""
+    rng = np.random.default_rng(31)
+    base = rng.integers(0, 256, (500, 128)).astype(np.float32)
+    d1 = base[rng.permutation(np.repeat(np.arange(500), 8))]
+    d0 = np.concatenate([base[:300], rng.integers(0, 256, (700, 128)).astype(np.float32)])
+    _check_knn2(d0, d1, ctx)

@@ -14,9 +14,9 @@ import csv
 import json
 from collections import defaultdict
 
-SHORT = [("ba_lin_kernel", "ba_lin"), ("ba_reduce_kernel", "ba_reduce"), ("ba_solve_kernel", "ba_solve"),
-         ("pack_kernel", "match_pack"), ("match_i8_kernel", "match_i8"), ("match_f32_kernel", "match_f32"),
-         ("merge_ratio_kernel", "match_merge"), ("compact_kernel", "match_compact")]
+SHORT = [("ba_lin_kernel", "ba_lin"), ("ba_reduce_kernel", "ba_reduce"), ("ba_solve_kernel", "ba_solve"), ("ba_solve2_kernel", "ba_solve"),
+         ("pack_kernel", "match_pack"), ("match_kernel", "match_i8"),
+         ("merge_kernel", "match_merge"), ("no_train_kernel", "match_none"), ("compact_kernel", "match_compact")]
 
 
 def short_name(kernel: str):

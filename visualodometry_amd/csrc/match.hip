@@ -49,6 +49,17 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
   return r;
 }
 
+// One step of a 16-lane top-2 reduction on u32 keys (larger = better): merge this
+// lane's (M1 >= M2) with the pair of the lane `Ctrl` (a DPP row rotation) away.
+// second(a1, a2, b1, b2) = med3(a1, b1, max(a2, b2)) since max(a2, b2) <= max(a1, b1).
+template <int Ctrl>
+__device__ __forceinline__ void row_top2_step(uint32_t& M1, uint32_t& M2) {
+  const uint32_t b1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)M1, Ctrl, 0xF, 0xF, false);
+  const uint32_t b2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)M2, Ctrl, 0xF, 0xF, false);
+  M2 = med3_u32(M1, b1, max(M2, b2));
+  M1 = max(M1, b1);
+}
+
 // Correctly rounded sqrtf: the f64 sqrt expansion is correctly rounded and
 // 53 >= 2*24 + 2 makes the f64 -> f32 double rounding innocuous.
 __device__ __forceinline__ float sqrtf_rn(float x) { return (float)sqrt((double)x); }
@@ -72,30 +83,55 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
 }
 
 // ---- packing: f32 -> int8 (a - 128), squared norms, u8-valued check --------
-// 16 threads per row, each moving 4 consecutive elements per step (coalesced).
-__global__ __launch_bounds__(256) void pack_kernel(
-    const float* __restrict__ des, int n, int dim, int Dp, int n_pad,
-    long in_bstride, long q_bstride, int8_t* __restrict__ q8, int* __restrict__ norms,
-    uint32_t* __restrict__ colconst, int* __restrict__ flag) {
+// One launch packs both sides (workgroups [0, a.wgs) the queries, the rest the train
+// rows).  16 threads per row, each moving 4 consecutive elements per step (one float4
+// when the rows are 16-byte aligned).  A value that is not an integer in [0,255]
+// stamps the call's generation into *flag: every later kernel of the call then takes
+// the fp32 path, and no memset is needed between calls.
+struct PackSide {
+  const float* des;
+  int n, n_pad, wgs;
+  long in_bstride, q_bstride;
+  int8_t* q8;
+  int* norms;
+  uint32_t* colconst;  // train side only
+};
+
+__global__ __launch_bounds__(256) void pack_kernel(PackSide sa, PackSide sb, int dim, int Dp,
+                                                   int vec4, uint32_t* __restrict__ flag,
+                                                   uint32_t gen) {
+  const bool is_b = (int)blockIdx.x >= sa.wgs;
+  const PackSide P = is_b ? sb : sa;
   const int b = blockIdx.y;
-  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int row = (((int)blockIdx.x - (is_b ? sa.wgs : 0)) * 256 + (int)threadIdx.x) >> 4;
   const int sub = threadIdx.x & 15;
-  if (row >= n_pad) return;
-  const float* src = des + b * in_bstride + (long)row * dim;
-  int8_t* dst = q8 + b * q_bstride + (long)row * Dp;
+  if (row >= P.n_pad) return;
+  const bool live_row = row < P.n;
+  const float* src = P.des + b * P.in_bstride + (long)row * dim;
+  int8_t* dst = P.q8 + b * P.q_bstride + (long)row * Dp;
   int acc = 0;
   bool bad = false;
   for (int e = sub * 4; e < Dp; e += 64) {
+    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (live_row) {
+      if (vec4) {
+        if (e < dim) {
+          const float4 t = *reinterpret_cast<const float4*>(src + e);
+          v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (e + u < dim) v[u] = src[e + u];
+      }
+    }
     int q[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      q[u] = 0;
-      if (row < n && e + u < dim) {
-        const float v = src[e + u];
-        const bool ok = (v == rintf(v)) && v >= 0.0f && v <= 255.0f;
-        bad |= !ok;
-        q[u] = ok ? (int)v - 128 : 0;
-      }
+      const bool live = live_row && e + u < dim;
+      const bool ok = (v[u] == rintf(v[u])) && v[u] >= 0.0f && v[u] <= 255.0f;
+      bad |= live && !ok;
+      q[u] = live && ok ? (int)v[u] - 128 : 0;
       acc += q[u] * q[u];
     }
     const uint32_t packed = (uint32_t)(q[0] & 255) | ((uint32_t)(q[1] & 255) << 8) |
@@ -104,27 +140,49 @@ __global__ __launch_bounds__(256) void pack_kernel(
   }
 #pragma unroll
   for (int m = 1; m < 16; m <<= 1) acc += __shfl_xor(acc, m, 64);
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+  if (__any(bad) && (threadIdx.x & 63) == 0) *flag = gen;  // every writer stores the same value
   if (sub == 0) {
-    norms[b * (long)n_pad + row] = acc;
-    if (colconst) {
-      colconst[b * (long)n_pad + row] =
-          row < n ? ((max_off(Dp) - (uint32_t)acc) << 8) | (255u - ((uint32_t)(row >> 4) & 255u)) : 0u;
+    P.norms[b * (long)P.n_pad + row] = acc;
+    if (is_b) {
+      P.colconst[b * (long)P.n_pad + row] =
+          live_row ? ((max_off(Dp) - (uint32_t)acc) << 8) | (255u - ((uint32_t)(row >> 4) & 255u)) : 0u;
     }
   }
 }
 
-// ---- int8 MFMA sweep --------------------------------------------------------
-// WG = 4 waves x 64 query rows; each WG sweeps the train columns of one split
-// (split width w | 4096, so a split never straddles a 4096-column block and the
-// 8-bit column-tile tag in the packed key is monotone in j inside a split).
+// ---- fused sweep + merge + ratio test ----------------------------------------
+// Grid (n0_pad / 256, nsplit, batch); a workgroup owns 256 query rows x one split of
+// train columns (split width w | 4096, so a split never straddles a 4096-column block
+// and the 8-bit column-tile tag in the packed key is monotone in j inside a split).
+// It writes one top-2 partial per row; merge_kernel combines the nsplit partials.
+struct MatchArgs {
+  const int8_t* qa;
+  const int8_t* qb;
+  const uint32_t* colconst;
+  const int* norma;
+  const float* da;
+  const float* db;
+  int n0, n1, dim, Dp, n0_pad, n1_pad, split_w, force_f32;
+  long qa_bstride, qb_bstride, a_bstride, b_bstride;
+  uint4* partial;
+  const uint32_t* flag;
+  uint32_t gen;
+  double ratio;
+  int32_t* best;
+  int32_t* idx2;
+  float* dist2;
+};
+
+// int8 MFMA sweep of one workgroup: 4 waves x 64 query rows
 template <int KS>
-__global__ __launch_bounds__(256) void match_i8_kernel(
-    const int8_t* __restrict__ qa, const int8_t* __restrict__ qb,
-    const uint32_t* __restrict__ colconst, const int* __restrict__ norma, int n0_pad,
-    int n1_pad, int split_w, long qa_bstride, long qb_bstride, uint4* __restrict__ partial,
-    const int* __restrict__ flag) {
-  if (*flag) return;  // not u8-valued: the float path owns this call
+__device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
+  const int8_t* qa = p.qa;
+  const int8_t* qb = p.qb;
+  const uint32_t* colconst = p.colconst;
+  const int* norma = p.norma;
+  const int n0_pad = p.n0_pad, n1_pad = p.n1_pad, split_w = p.split_w;
+  const long qa_bstride = p.qa_bstride, qb_bstride = p.qb_bstride;
+  uint4* partial = p.partial;
   constexpr int Dp = KS * kKStep;
   constexpr uint32_t kOffMax = max_off(Dp);
   const int lane = threadIdx.x & 63;
@@ -173,27 +231,41 @@ __global__ __launch_bounds__(256) void match_i8_kernel(
     for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<v4i*>(dst + 16 * ks) = g[ks];
     if (tid < 64) sC[buf][tid] = gc;
   };
-  // one 16-column tile: the four row tiles' MFMAs into separate accumulators, then the
-  // top-2 update (v_lshl_add_u32 + v_med3_u32 + v_max_u32 per pair)
-  auto tile = [&](int buf, int u) {
+  // One 16-column tile: its B fragments and column constants from LDS (frag), the
+  // four row tiles' MFMAs into separate accumulators (mm), then the top-2 update
+  // (epi: v_lshl_add_u32 + v_med3_u32 + v_max_u32 per pair).
+  struct Frag {
     v4i bf[KS];
+    uint32_t cc;
+  };
+  struct Acc {
+    v4i v[4];
+  };
+  auto frag = [&](int buf, int u) {
+    Frag f;
     const int8_t* fp = &sB[buf][(16 * u + (lane & 15)) * kRow + 16 * (lane >> 4)];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) bf[ks] = *reinterpret_cast<const v4i*>(fp + ks * kKStep);
-    const uint32_t ccol = sC[buf][16 * u + (lane & 15)];
-    v4i acc[4];
+    for (int ks = 0; ks < KS; ++ks) f.bf[ks] = *reinterpret_cast<const v4i*>(fp + ks * kKStep);
+    f.cc = sC[buf][16 * u + (lane & 15)];
+    return f;
+  };
+  auto mm = [&](const Frag& f) {
+    Acc a;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      acc[mt] = v4i{0, 0, 0, 0};
+      a.v[mt] = v4i{0, 0, 0, 0};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        acc[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], bf[ks], acc[mt], 0, 0, 0);
+        a.v[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], f.bf[ks], a.v[mt], 0, 0, 0);
     }
+    return a;
+  };
+  auto epi = [&](const Acc& a, uint32_t ccol) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const uint32_t p = ((uint32_t)acc[mt][r] << 9) + ccol;
+        const uint32_t p = ((uint32_t)a.v[mt][r] << 9) + ccol;
         m2[mt][r] = med3_u32(m1[mt][r], m2[mt][r], p);
         m1[mt][r] = max(m1[mt][r], p);
       }
@@ -210,55 +282,68 @@ __global__ __launch_bounds__(256) void match_i8_kernel(
       if (ch + 1 < nchunk) gload(cb + 64, g, gc);  // in flight during this chunk
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (cb + 16 * u < c1) tile(buf, u);
+        if (cb + 16 * u < c1) {
+          const Frag f = frag(buf, u);
+          epi(mm(f), f.cc);
+        }
       if (ch + 1 < nchunk) sstore(buf ^ 1, g, gc);
       __syncthreads();
     }
   }
 
-  // unpack to (d2, j) keys and merge the 16 lanes that share each row
+  // Merge the 16 lanes that share each row (one DPP row) on the u32 keys: within a
+  // split they are comparable across lanes, and equal keys mean equal d2 and tile, where
+  // the lower lane (lower j) must win -- recovered by ballot after the value reduction.
+  // Rotations by 1, 2, 4, 8 combine disjoint lane sets, so the top-2 merge is exact.
   const int jblock = c0 & ~4095;
+  const int gshift = lane & 48;  // this lane's 16-lane group in a ballot mask
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = rowbase + mt * 16 + (lane >> 4) * 4 + r;
-      const int na = norma[b * (long)n0_pad + row];
-      uint64_t k1 = ~0ull, k2 = ~0ull;
-      if (m1[mt][r] != 0u) {
-        const uint32_t d = kOffMax - (m1[mt][r] >> 8) + na;
-        k1 = key64(d, jblock + 16 * (255u - (m1[mt][r] & 255u)) + (lane & 15));
-      }
-      if (m2[mt][r] != 0u) {
-        const uint32_t d = kOffMax - (m2[mt][r] >> 8) + na;
-        k2 = key64(d, jblock + 16 * (255u - (m2[mt][r] & 255u)) + (lane & 15));
-      }
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) merge2(k1, k2, shfl_xor64(k1, m), shfl_xor64(k2, m));
+      const uint32_t a1 = m1[mt][r], a2 = m2[mt][r];
+      uint32_t M1 = a1, M2 = a2;
+      row_top2_step<0x121>(M1, M2);  // row_ror:1
+      row_top2_step<0x122>(M1, M2);  // row_ror:2
+      row_top2_step<0x124>(M1, M2);  // row_ror:4
+      row_top2_step<0x128>(M1, M2);  // row_ror:8
+      const uint32_t g1 = (uint32_t)(__ballot(a1 == M1) >> gshift) & 0xFFFFu;
+      const uint32_t g2 = (uint32_t)(__ballot(a1 == M2 || a2 == M2) >> gshift) & 0xFFFFu;
+      const uint32_t l1 = __builtin_ctz(g1 | 0x10000u);
+      // M2 == M1 (two lanes tie exactly): the next such lane; else the lowest holder of M2
+      const uint32_t l2 = __builtin_ctz((M2 == M1 ? g1 & ~(1u << l1) : g2) | 0x10000u);
       if ((lane & 15) == 0) {
-        partial[((long)b * nsplit + split) * n0_pad + row] =
-            make_uint4((uint32_t)(k1 >> 32), (uint32_t)k1, (uint32_t)(k2 >> 32), (uint32_t)k2);
+        const int row = rowbase + mt * 16 + (lane >> 4) * 4 + r;
+        const int na = norma[b * (long)n0_pad + row];
+        uint4 q = make_uint4(~0u, ~0u, ~0u, ~0u);
+        if (M1 != 0u) {
+          q.x = kOffMax - (M1 >> 8) + na;
+          q.y = jblock + 16 * (255u - (M1 & 255u)) + l1;
+        }
+        if (M2 != 0u) {
+          q.z = kOffMax - (M2 >> 8) + na;
+          q.w = jblock + 16 * (255u - (M2 & 255u)) + l2;
+        }
+        partial[((long)b * nsplit + split) * n0_pad + row] = q;
       }
     }
   }
 }
 
-// ---- fp32 path ---------------------------------------------------------------
-// WG tile: 64 query rows x the split's columns in 64-column tiles; thread
-// (ty, tx) owns rows 4ty..4ty+3 and columns tx + 16c.  Each pair's d2 is the
-// fmaf chain over k in ascending order.  Per thread the columns arrive in
-// ascending j, so a candidate can only enter the top-2 if d2 < d2(second):
-// sqrtf is evaluated only then (exact filter, see header).
-__global__ __launch_bounds__(256) void match_f32_kernel(
-    const float* __restrict__ da, const float* __restrict__ db, int n0, int n1, int dim,
-    int n0_pad, int split_w, long a_bstride, long b_bstride, uint4* __restrict__ partial,
-    const int* __restrict__ flag) {
-  if (!*flag) return;  // u8-valued: the int8 path owns this call
+// fp32 sweep of one 64-row tile: thread (ty, tx) owns rows 4ty..4ty+3 and columns
+// tx + 16c.  Each pair's d2 is the fmaf chain over k in ascending order.  Per thread
+// the columns arrive in ascending j, so a candidate can only enter the top-2 if
+// d2 < d2(second): sqrtf is evaluated only then (exact filter, see header).
+__device__ __forceinline__ void sweep_f32(const MatchArgs& p, int rowbase) {
+  const float* da = p.da;
+  const float* db = p.db;
+  const int n0 = p.n0, n1 = p.n1, dim = p.dim, n0_pad = p.n0_pad, split_w = p.split_w;
+  const long a_bstride = p.a_bstride, b_bstride = p.b_bstride;
+  uint4* partial = p.partial;
   __shared__ float sa[kFloatKC][kFloatTile + 1];
   __shared__ float sb[kFloatKC][kFloatTile + 1];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int b = blockIdx.z, split = blockIdx.y, nsplit = gridDim.y;
-  const int rowbase = blockIdx.x * kFloatTile;
   const float* A = da + b * a_bstride;
   const float* B = db + b * b_bstride;
 
@@ -336,66 +421,91 @@ __global__ __launch_bounds__(256) void match_f32_kernel(
   }
 }
 
-// ---- merge splits, exact near-tie rescan, ratio test ---------------------------
-// One wave per (batch, query row).
-__global__ __launch_bounds__(64) void merge_ratio_kernel(
-    const uint4* __restrict__ partial, int nsplit, int n0, int n0_pad, int n1, int n1_pad,
-    int Dp, const int8_t* __restrict__ qa, const int8_t* __restrict__ qb, long qa_bstride,
-    long qb_bstride, const int* __restrict__ flag, double ratio, int32_t* __restrict__ best,
-    int32_t* __restrict__ idx2, float* __restrict__ dist2) {
-  const int row = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
-  const bool fpath = *flag != 0;
+// Merge of the nsplit partials, one thread per query row (256-row workgroups), then
+// the exact near-tie rescan (rare; a whole wave per flagged row) and the ratio test.
+__global__ __launch_bounds__(256) void merge_kernel(MatchArgs p, int nsplit) {
+  const bool fpath = p.force_f32 || *p.flag == p.gen;  // uniform
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kRowsPerWG + threadIdx.x;
   uint64_t k1 = ~0ull, k2 = ~0ull;
-  for (int s = lane; s < nsplit; s += 64) {
-    const uint4 p = partial[((long)b * nsplit + s) * n0_pad + row];
-    merge2(k1, k2, key64(p.x, p.y), key64(p.z, p.w));
+  for (int s = 0; s < nsplit; ++s) {
+    const uint4 q = p.partial[((long)b * nsplit + s) * p.n0_pad + row];
+    merge2(k1, k2, key64(q.x, q.y), key64(q.z, q.w));
   }
-#pragma unroll
-  for (int m = 1; m < 64; m <<= 1) merge2(k1, k2, shfl_xor64(k1, m), shfl_xor64(k2, m));
-
   float s1 = __builtin_huge_valf(), s2 = __builtin_huge_valf();
   if (!fpath) {
     // (d2, j) order equals (sqrtf(d2), j) order unless sqrtf merges two
     // consecutive integers, which needs d2 >= 2^22 (see header).
-    const bool rescan = k2 != ~0ull && (uint32_t)(k2 >> 32) >= (uint32_t)kCollide;
+    const bool rescan = row < p.n0 && k2 != ~0ull && (uint32_t)(k2 >> 32) >= (uint32_t)kCollide;
+    uint64_t todo = __ballot(rescan);
     if (rescan) {
-      const int8_t* a = qa + b * qa_bstride + (long)row * Dp;
-      const int8_t* bb = qb + b * qb_bstride;
-      uint64_t r1 = ~0ull, r2 = ~0ull;
-      for (int j = lane; j < n1; j += 64) {
-        int d = 0;
-        for (int e = 0; e < Dp; ++e) {
-          const int df = (int)a[e] - (int)bb[(long)j * Dp + e];
-          d += df * df;
-        }
-        const uint64_t kk = key64(__float_as_uint(sqrtf_rn((float)d)), (uint32_t)j);
-        merge2(r1, r2, kk, ~0ull);
-      }
-#pragma unroll
-      for (int m = 1; m < 64; m <<= 1) merge2(r1, r2, shfl_xor64(r1, m), shfl_xor64(r2, m));
-      k1 = r1;
-      k2 = r2;
-      if (k1 != ~0ull) s1 = __uint_as_float((uint32_t)(k1 >> 32));
-      if (k2 != ~0ull) s2 = __uint_as_float((uint32_t)(k2 >> 32));
+      k1 = k2 = ~0ull;
     } else {
       if (k1 != ~0ull) s1 = sqrtf_rn((float)(uint32_t)(k1 >> 32));
       if (k2 != ~0ull) s2 = sqrtf_rn((float)(uint32_t)(k2 >> 32));
+    }
+    // the whole wave re-scans each flagged row with sqrt-domain keys
+    const int8_t* bb = p.qb + b * p.qb_bstride;
+    while (todo) {
+      const int l = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const int8_t* a = p.qa + b * p.qa_bstride + (long)(row - lane + l) * p.Dp;
+      uint64_t r1 = ~0ull, r2 = ~0ull;
+      for (int j = lane; j < p.n1; j += 64) {
+        int d = 0;
+        for (int e = 0; e < p.Dp; ++e) {
+          const int df = (int)a[e] - (int)bb[(long)j * p.Dp + e];
+          d += df * df;
+        }
+        merge2(r1, r2, key64(__float_as_uint(sqrtf_rn((float)d)), (uint32_t)j), ~0ull);
+      }
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) merge2(r1, r2, shfl_xor64(r1, m), shfl_xor64(r2, m));
+      if (lane == l) {
+        k1 = r1;
+        k2 = r2;
+        if (k1 != ~0ull) s1 = __uint_as_float((uint32_t)(k1 >> 32));
+        if (k2 != ~0ull) s2 = __uint_as_float((uint32_t)(k2 >> 32));
+      }
     }
   } else {
     if (k1 != ~0ull) s1 = __uint_as_float((uint32_t)(k1 >> 32));
     if (k2 != ~0ull) s2 = __uint_as_float((uint32_t)(k2 >> 32));
   }
-  if (lane == 0) {
+  if (row < p.n0) {
     const int j1 = k1 == ~0ull ? -1 : (int)(uint32_t)k1;
     const int j2 = k2 == ~0ull ? -1 : (int)(uint32_t)k2;
-    const long o = (long)b * n0 + row;
-    if (best) best[o] = (j2 >= 0 && (double)s1 < ratio * (double)s2) ? j1 : -1;
-    if (idx2) {
-      idx2[2 * o] = j1;
-      idx2[2 * o + 1] = j2;
-      dist2[2 * o] = j1 >= 0 ? s1 : 3.402823466e+38f;
-      dist2[2 * o + 1] = j2 >= 0 ? s2 : 3.402823466e+38f;
+    const long o = (long)b * p.n0 + row;
+    if (p.best) p.best[o] = (j2 >= 0 && (double)s1 < p.ratio * (double)s2) ? j1 : -1;
+    if (p.idx2) {
+      p.idx2[2 * o] = j1;
+      p.idx2[2 * o + 1] = j2;
+      p.dist2[2 * o] = j1 >= 0 ? s1 : 3.402823466e+38f;
+      p.dist2[2 * o + 1] = j2 >= 0 ? s2 : 3.402823466e+38f;
     }
+  }
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void match_kernel(MatchArgs p) {
+  const bool fpath = p.force_f32 || *p.flag == p.gen;  // uniform
+  if (!fpath) {
+    sweep_i8<KS>(p);
+  } else {
+#pragma unroll 1
+    for (int t = 0; t < kRowsPerWG / kFloatTile; ++t)
+      sweep_f32(p, blockIdx.x * kRowsPerWG + t * kFloatTile);
+  }
+}
+
+// n1 == 0: no query has a neighbour
+__global__ void no_train_kernel(int total, int32_t* best, int32_t* idx2, float* dist2) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= total) return;
+  if (best) best[o] = -1;
+  if (idx2) {
+    idx2[2 * o] = idx2[2 * o + 1] = -1;
+    dist2[2 * o] = dist2[2 * o + 1] = 3.402823466e+38f;
   }
 }
 
@@ -464,74 +574,78 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
   w = std::max(256, std::min(4096, w));
   const int nsplit = std::max(1, ceil_div(n1_pad, w));
 
-  ws.flag.reserve(sizeof(int));
+  ws.flag.reserve(sizeof(uint32_t));
   ws.partial.reserve((size_t)batch * nsplit * n0_pad * sizeof(uint4));
-  int* flag = ws.flag.as<int>();
-  VO_HIP_CHECK(hipMemsetAsync(flag, int_ok ? 0 : 1, sizeof(int), st));
+  // generation tag of this call (see pack_kernel); 0 is the reset value of the flag
+  if (++ws.gen == 0 || ws.flag_fresh) {
+    VO_HIP_CHECK(hipMemsetAsync(ws.flag.ptr, 0, sizeof(uint32_t), st));
+    ws.gen = 1;
+    ws.flag_fresh = false;
+  }
+  uint32_t* flag = ws.flag.as<uint32_t>();
 
-  const long qa_bs = (long)n0_pad * Dp, qb_bs = (long)n1_pad * Dp;
-  int8_t* qa = nullptr;
-  int8_t* qb = nullptr;
+  MatchArgs a{};
+  a.da = d_des0;
+  a.db = d_des1;
+  a.n0 = n0;
+  a.n1 = n1;
+  a.dim = dim;
+  a.Dp = Dp;
+  a.n0_pad = n0_pad;
+  a.n1_pad = n1_pad;
+  a.split_w = w;
+  a.force_f32 = int_ok ? 0 : 1;
+  a.a_bstride = (long)n0 * dim;
+  a.b_bstride = (long)n1 * dim;
+  a.partial = ws.partial.as<uint4>();
+  a.flag = flag;
+  a.gen = ws.gen;
+  a.ratio = ratio;
+  a.best = d_best;
+  a.idx2 = d_idx2;
+  a.dist2 = d_dist2;
+  if (n1 == 0) {
+    const int total = batch * n0;
+    hipLaunchKernelGGL(no_train_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, total,
+                       d_best, d_idx2, d_dist2);
+    VO_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (int_ok) {
-    ws.q8.reserve((size_t)batch * (qa_bs + qb_bs));
+    a.qa_bstride = (long)n0_pad * Dp;
+    a.qb_bstride = (long)n1_pad * Dp;
+    ws.q8.reserve((size_t)batch * (a.qa_bstride + a.qb_bstride));
     ws.norms.reserve((size_t)batch * (n0_pad + n1_pad) * sizeof(int));
     ws.colconst.reserve((size_t)batch * n1_pad * sizeof(uint32_t));
-    qa = ws.q8.as<int8_t>();
-    qb = qa + batch * qa_bs;
+    int8_t* qa = ws.q8.as<int8_t>();
+    int8_t* qb = qa + batch * a.qa_bstride;
     int* na = ws.norms.as<int>();
     int* nb = na + (size_t)batch * n0_pad;
-    dim3 ga(ceil_div((int64_t)n0_pad * 16, 256), batch), gb(ceil_div((int64_t)n1_pad * 16, 256), batch);
+    a.qa = qa;
+    a.qb = qb;
+    a.colconst = ws.colconst.as<uint32_t>();
+    a.norma = na;
+    PackSide pa{d_des0, n0, n0_pad, ceil_div((int64_t)n0_pad * 16, 256), a.a_bstride,
+                a.qa_bstride, qa, na, nullptr};
+    PackSide pb{d_des1, n1, n1_pad, ceil_div((int64_t)n1_pad * 16, 256), a.b_bstride,
+                a.qb_bstride, qb, nb, ws.colconst.as<uint32_t>()};
+    const int vec4 = dim % 4 == 0 && (uintptr_t)d_des0 % 16 == 0 && (uintptr_t)d_des1 % 16 == 0;
     ctx->prof.begin(st, kKMatchPack);
-    hipLaunchKernelGGL(pack_kernel, ga, dim3(256), 0, st, d_des0, n0, dim, Dp, n0_pad,
-                       (long)n0 * dim, qa_bs, qa, na, (uint32_t*)nullptr, flag);
-    if (n1 > 0)
-      hipLaunchKernelGGL(pack_kernel, gb, dim3(256), 0, st, d_des1, n1, dim, Dp, n1_pad,
-                         (long)n1 * dim, qb_bs, qb, nb, ws.colconst.as<uint32_t>(), flag);
+    hipLaunchKernelGGL(pack_kernel, dim3(pa.wgs + pb.wgs, batch), dim3(256), 0, st, pa, pb, dim,
+                       Dp, vec4, flag, ws.gen);
     ctx->prof.end(st);
-    if (n1 > 0) {
-      dim3 grid(row_wgs, nsplit, batch);
-      ctx->prof.begin(st, kKMatchI8);
-      uint4* part = ws.partial.as<uint4>();
-      switch (Dp / kKStep) {
-        case 1:
-          hipLaunchKernelGGL(match_i8_kernel<1>, grid, dim3(256), 0, st, qa, qb,
-                             ws.colconst.as<uint32_t>(), na, n0_pad, n1_pad, w, qa_bs, qb_bs,
-                             part, flag);
-          break;
-        case 2:
-          hipLaunchKernelGGL(match_i8_kernel<2>, grid, dim3(256), 0, st, qa, qb,
-                             ws.colconst.as<uint32_t>(), na, n0_pad, n1_pad, w, qa_bs, qb_bs,
-                             part, flag);
-          break;
-        case 3:
-          hipLaunchKernelGGL(match_i8_kernel<3>, grid, dim3(256), 0, st, qa, qb,
-                             ws.colconst.as<uint32_t>(), na, n0_pad, n1_pad, w, qa_bs, qb_bs,
-                             part, flag);
-          break;
-        default:
-          hipLaunchKernelGGL(match_i8_kernel<4>, grid, dim3(256), 0, st, qa, qb,
-                             ws.colconst.as<uint32_t>(), na, n0_pad, n1_pad, w, qa_bs, qb_bs,
-                             part, flag);
-          break;
-      }
-      ctx->prof.end(st);
-    }
   }
-  if (n1 > 0) {
-    dim3 grid(ceil_div(n0, kFloatTile), nsplit, batch);
-    ctx->prof.begin(st, kKMatchF32);
-    hipLaunchKernelGGL(match_f32_kernel, grid, dim3(256), 0, st, d_des0, d_des1, n0, n1, dim,
-                       n0_pad, w, (long)n0 * dim, (long)n1 * dim, ws.partial.as<uint4>(), flag);
-    ctx->prof.end(st);
-  } else {
-    // no train rows: every query has no neighbour
-    VO_HIP_CHECK(hipMemsetAsync(ws.partial.ptr, 0xFF,
-                                (size_t)batch * nsplit * n0_pad * sizeof(uint4), st));
+  dim3 grid(row_wgs, nsplit, batch);
+  ctx->prof.begin(st, kKMatchI8);
+  switch (int_ok ? Dp / kKStep : 1) {
+    case 1: hipLaunchKernelGGL(match_kernel<1>, grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(match_kernel<2>, grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(match_kernel<3>, grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(match_kernel<4>, grid, dim3(256), 0, st, a); break;
   }
+  ctx->prof.end(st);
   ctx->prof.begin(st, kKMatchMerge);
-  hipLaunchKernelGGL(merge_ratio_kernel, dim3(n0, batch), dim3(64), 0, st,
-                     ws.partial.as<uint4>(), n1 > 0 ? nsplit : 1, n0, n0_pad, n1, n1_pad, Dp,
-                     qa, qb, qa_bs, qb_bs, flag, ratio, d_best, d_idx2, d_dist2);
+  hipLaunchKernelGGL(merge_kernel, dim3(row_wgs, batch), dim3(256), 0, st, a, nsplit);
   ctx->prof.end(st);
   VO_HIP_CHECK(hipGetLastError());
 }

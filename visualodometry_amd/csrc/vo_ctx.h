@@ -17,7 +17,9 @@ struct MatchWorkspace {
   DevBuf best;      // int32 (batch, n0) best train index or -1
   DevBuf top2;      // int32 (n0, 2) + float (n0, 2)
   DevBuf pairs;     // int32 (n0, 2) compacted pairs + count
-  DevBuf flag;      // int32 "descriptors are not 0..255 integers"
+  DevBuf flag;      // uint32: == gen when this call's descriptors are not 0..255 integers
+  uint32_t gen = 0;         // generation tag of the current call
+  bool flag_fresh = true;   // flag not yet zeroed
 };
 
 class BAEngine;   // ba.hip
