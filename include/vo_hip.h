@@ -167,7 +167,9 @@ int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
 /* Host-only: builds the static plan of `prob` without a device (planner tests,
  * capacity checks).  Fills up to n int64 values: [0] chunks [1] segments
  * [2] slab blocks [3] profile blocks [4] track entries [5] max pairs in a chunk
- * [6] max window slots in a segment [7] max window cameras in a segment.
+ * [6] max window slots in a segment [7] max window cameras in a segment
+ * [8] free poses F [9] widest profile row span (blocks) [10] two-sided K3
+ * layout usable [11] its rows per side m [12] separator rows s [13] bottom rows. 
  * Returns the count written, or VO_ERR_ARG (vo_last_error() says why). */
 int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* out, int n);
 

@@ -98,11 +98,12 @@ def plan_probe(K, point_ptr, obs_cam, obs_uv, n_poses: int, n_fixed: int = 2,
     obs_cam = np.ascontiguousarray(obs_cam, dtype=np.int32)
     obs_uv = np.ascontiguousarray(obs_uv, dtype=np.float32).reshape(-1, 2)
     prob = _problem_struct(K, point_ptr, obs_cam, obs_uv, n_poses, n_fixed, 0.0)
-    out = np.zeros(8, dtype=np.int64)
+    out = np.zeros(14, dtype=np.int64)
     n = check(_lib.load().vo_ba_plan_probe(C.byref(prob), int(target_segments),
-                                           ptr(out, C.c_int64), 8), "vo_ba_plan_probe")
+                                           ptr(out, C.c_int64), 14), "vo_ba_plan_probe")
     keys = ["chunks", "segments", "slab_blocks", "profile_blocks", "track_entries",
-            "max_chunk_pairs", "max_segment_slots", "max_segment_cameras"]
+            "max_chunk_pairs", "max_segment_slots", "max_segment_cameras", "free_poses",
+            "max_row_span", "two_sided", "two_sided_m", "two_sided_s", "two_sided_nbot"]
     return dict(zip(keys[:n], out[:n].tolist()))
 
 

@@ -353,9 +353,13 @@ int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* ou
       max_slots = std::max<int64_t>(max_slots, P.seg_slot_off[s + 1] - P.seg_slot_off[s]);
       max_cams = std::max<int64_t>(max_cams, P.seg_cam_off[s + 1] - P.seg_cam_off[s]);
     }
-    const int64_t v[8] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), P.n_prof_blocks(),
-                          P.n_te, max_pairs, max_slots, max_cams};
-    k = std::min(n, 8);
+    int span = 0;
+    for (int r = 0; r < P.n_free; ++r) span = std::max(span, r - P.prof_first[r]);
+    const vo::TwoSidedLayout& T = P.solve2_layout;
+    const int64_t v[14] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), P.n_prof_blocks(),
+                           P.n_te, max_pairs, max_slots, max_cams, P.n_free, span,
+                           T.enabled, T.m, T.s, T.nbot};
+    k = std::min(n, 14);
     for (int i = 0; i < k; ++i) out[i] = v[i];
   });
   return g != VO_OK ? g : k;

@@ -182,6 +182,44 @@ __device__ __forceinline__ void lin_obs(LinShared& S, const LinArgs& A, const do
   }
 }
 
+// Landmark p of the chunk: V = sum Jp^T Jp (+lambda) and g = sum Jp^T r over its
+// observations (S.r may hold r + Jc dc, see chunk_backsub), the pivot-tested 3x3
+// Cholesky V = L L^T (same sequence as oracle/ba_ref.py point_block_valid) and
+// h = L^-1 g.  l = (1/l00, l10, 1/l11, l20, l21, 1/l22).
+__device__ __forceinline__ bool point_block(const LinShared& S, const LinArgs& A, int p,
+                                            double (&l)[6], double (&h)[3]) {
+  double v00 = 0, v01 = 0, v02 = 0, v11 = 0, v12 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
+  const int o0 = S.te_obs[S.pt_te[p]], o1 = S.te_obs[S.pt_te[p + 1]];
+  for (int o = o0; o < o1; ++o) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const double a = S.Jp[o][3 * k], b = S.Jp[o][3 * k + 1], c = S.Jp[o][3 * k + 2];
+      const double rk = S.r[o][k];
+      v00 += a * a; v01 += a * b; v02 += a * c;
+      v11 += b * b; v12 += b * c; v22 += c * c;
+      g0 += a * rk; g1 += b * rk; g2 += c * rk;
+    }
+  }
+  v00 += A.lambda; v11 += A.lambda; v22 += A.lambda;
+  const double eps = kPivotRelEps * (v00 + v11 + v22);
+  bool ok = v00 > eps;
+  const double l00 = sqrt(ok ? v00 : 1.0);
+  const double l10 = v01 / l00, l20 = v02 / l00;
+  const double d1 = v11 - l10 * l10;
+  ok = ok && d1 > eps;
+  const double l11 = sqrt(ok ? d1 : 1.0);
+  const double l21 = (v12 - l20 * l10) / l11;
+  const double d2 = v22 - l20 * l20 - l21 * l21;
+  ok = ok && d2 > eps;
+  const double l22 = sqrt(ok ? d2 : 1.0);
+  const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+  l[0] = i00; l[1] = l10; l[2] = i11; l[3] = l20; l[4] = l21; l[5] = i22;
+  h[0] = g0 * i00;
+  h[1] = (g1 - l10 * h[0]) * i11;
+  h[2] = (g2 - l20 * h[0] - l21 * h[1]) * i22;
+  return ok;
+}
+
 // R2: per track entry W, gc; per landmark V (+lambda), pivot-tested Cholesky, h.
 __device__ __forceinline__ void lin_reduce(LinShared& S, const LinArgs& A, int nte, int npt) {
   for (int t = threadIdx.x; t < nte; t += kLinThreads) {
@@ -211,41 +249,14 @@ __device__ __forceinline__ void lin_reduce(LinShared& S, const LinArgs& A, int n
     for (int e = 0; e < 6; ++e) S.bt[t][e] = g[e];
   }
   for (int p = threadIdx.x; p < npt; p += kLinThreads) {
-    double v00 = 0, v01 = 0, v02 = 0, v11 = 0, v12 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
-    const int o0 = S.te_obs[S.pt_te[p]], o1 = S.te_obs[S.pt_te[p + 1]];
-    for (int o = o0; o < o1; ++o) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const double a = S.Jp[o][3 * k], b = S.Jp[o][3 * k + 1], c = S.Jp[o][3 * k + 2];
-        const double rk = S.r[o][k];
-        v00 += a * a; v01 += a * b; v02 += a * c;
-        v11 += b * b; v12 += b * c; v22 += c * c;
-        g0 += a * rk; g1 += b * rk; g2 += c * rk;
-      }
-    }
-    v00 += A.lambda; v11 += A.lambda; v22 += A.lambda;
-    // pivot test: same sequence as oracle/ba_ref.py point_block_valid
-    const double eps = kPivotRelEps * (v00 + v11 + v22);
-    bool ok = v00 > eps;
-    const double l00 = sqrt(ok ? v00 : 1.0);
-    const double l10 = v01 / l00, l20 = v02 / l00;
-    const double d1 = v11 - l10 * l10;
-    ok = ok && d1 > eps;
-    const double l11 = sqrt(ok ? d1 : 1.0);
-    const double l21 = (v12 - l20 * l10) / l11;
-    const double d2 = v22 - l20 * l20 - l21 * l21;
-    ok = ok && d2 > eps;
-    const double l22 = sqrt(ok ? d2 : 1.0);
-    const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+    double l[6], h[3];
+    const bool ok = point_block(S, A, p, l, h);
     S.valid[p] = ok;
-    S.L[p][0] = i00; S.L[p][1] = l10; S.L[p][2] = i11;
-    S.L[p][3] = l20; S.L[p][4] = l21; S.L[p][5] = i22;
-    const double h0 = g0 * i00;
-    const double h1 = (g1 - l10 * h0) * i11;
-    const double h2 = (g2 - l20 * h0 - l21 * h1) * i22;
-    S.h[p][0] = ok ? h0 : 0.0;
-    S.h[p][1] = ok ? h1 : 0.0;
-    S.h[p][2] = ok ? h2 : 0.0;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) S.L[p][e] = l[e];
+    S.h[p][0] = ok ? h[0] : 0.0;
+    S.h[p][1] = ok ? h[1] : 0.0;
+    S.h[p][2] = ok ? h[2] : 0.0;
   }
 }
 
@@ -292,6 +303,59 @@ __device__ __forceinline__ void chunk_linearize(LinShared& S, const LinArgs& A,
   __syncthreads();
   lin_eliminate(S, nte);
   __syncthreads();
+}
+
+// Back-substitution of the pending step at its linearisation point (pose_o):
+// dp = -V^-1 sum_o Jp_o^T (r_o + Jc_o dc_cam(o)) -- algebraically the Schur
+// back-substitution -V^-1 (g + sum_t W_t^T dc) without forming W or Z.  V, the pivot
+// test and the Cholesky are point_block's, so a landmark frozen in the pending step's
+// camera system (invalid V) is not moved; fixed cameras contribute dc = 0.
+__device__ __forceinline__ void chunk_backsub(LinShared& S, const LinArgs& A, int nob, int npt,
+                                              int p0) {
+  for (int o = threadIdx.x; o < nob; o += kLinThreads) {
+    const double* T = S.pose_o[S.acam[o]];
+    const int te = S.obs_te[o];
+    const int q = S.te_pt[te];
+    const double X0 = S.X[q][0], X1 = S.X[q][1], X2 = S.X[q][2];
+    const double x = T[0] * X0 + T[1] * X1 + T[2] * X2 + T[9];
+    const double y = T[3] * X0 + T[4] * X1 + T[5] * X2 + T[10];
+    const double z = T[6] * X0 + T[7] * X1 + T[8] * X2 + T[11];
+    const double iz = 1.0 / z;
+    const float2 m = S.uv[o];
+    double r0 = A.fx * x * iz + A.cx - (double)m.x;
+    double r1 = A.fy * y * iz + A.cy - (double)m.y;
+    const double j00 = A.fx * iz, j02 = -A.fx * x * iz * iz;
+    const double j11 = A.fy * iz, j12 = -A.fy * y * iz * iz;
+    const int lc = S.te_lcam[te];
+    if (lc >= 0) {  // + Jc dc (rows of lin_obs's Jc)
+      const double* d = S.dcw[lc];
+      r0 += j00 * d[0] + j02 * d[2] + (j02 * y) * d[3] + (j00 * z - j02 * x) * d[4] - (j00 * y) * d[5];
+      r1 += j11 * d[1] + j12 * d[2] + (j12 * y - j11 * z) * d[3] - (j12 * x) * d[4] + (j11 * x) * d[5];
+    }
+    S.r[o][0] = r0;
+    S.r[o][1] = r1;
+    double* jp = S.Jp[o];
+    jp[0] = j00 * T[0] + j02 * T[6];
+    jp[1] = j00 * T[1] + j02 * T[7];
+    jp[2] = j00 * T[2] + j02 * T[8];
+    jp[3] = j11 * T[3] + j12 * T[6];
+    jp[4] = j11 * T[4] + j12 * T[7];
+    jp[5] = j11 * T[5] + j12 * T[8];
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < npt; p += kLinThreads) {
+    double l[6], h[3];
+    if (!point_block(S, A, p, l, h)) continue;
+    const double x2 = -h[2] * l[5];
+    const double x1 = (-h[1] - l[4] * x2) * l[2];
+    const double x0 = (-h[0] - l[1] * x1 - l[3] * x2) * l[0];
+    S.X[p][0] += x0;
+    S.X[p][1] += x1;
+    S.X[p][2] += x2;
+    A.points[3l * (p0 + p)] = S.X[p][0];
+    A.points[3l * (p0 + p) + 1] = S.X[p][1];
+    A.points[3l * (p0 + p) + 2] = S.X[p][2];
+  }
 }
 
 // Diagnostic build (VO_BA_STAMPS=1): thread 0 accumulates s_memtime deltas per
@@ -422,33 +486,7 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
     st.mark(kPhLoad);
 
     if (MODE & kBacksub) {
-      double dummy = 0.0;
-      chunk_linearize(S, A, S.pose_o, nob, nte, npt, dummy);
-      for (int p = tid; p < npt; p += kLinThreads) {
-        if (!S.valid[p]) continue;
-        double a0 = -S.h[p][0], a1 = -S.h[p][1], a2 = -S.h[p][2];
-        for (int t = S.pt_te[p]; t < S.pt_te[p + 1]; ++t) {
-          if (!S.te_use[t]) continue;
-          const double* d = S.dcw[S.te_lcam[t]];
-#pragma unroll
-          for (int a = 0; a < 6; ++a) {
-            a0 -= S.Z[t][3 * a] * d[a];
-            a1 -= S.Z[t][3 * a + 1] * d[a];
-            a2 -= S.Z[t][3 * a + 2] * d[a];
-          }
-        }
-        const double i00 = S.L[p][0], l10 = S.L[p][1], i11 = S.L[p][2];
-        const double l20 = S.L[p][3], l21 = S.L[p][4], i22 = S.L[p][5];
-        const double x2 = a2 * i22;
-        const double x1 = (a1 - l21 * x2) * i11;
-        const double x0 = (a0 - l10 * x1 - l20 * x2) * i00;
-        S.X[p][0] += x0;
-        S.X[p][1] += x1;
-        S.X[p][2] += x2;
-        A.points[3l * (p0 + p)] = S.X[p][0];
-        A.points[3l * (p0 + p) + 1] = S.X[p][1];
-        A.points[3l * (p0 + p) + 2] = S.X[p][2];
-      }
+      chunk_backsub(S, A, nob, npt, p0);
       __syncthreads();
       st.mark(kPhBacksub);
     }
@@ -1328,6 +1366,7 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
     ld6g(Sm + 36l * blk0 + 6 * rp0, s0);
     if (kPairs) ld6g(Sm + 36l * blk0 + 6 * (rp0 + 3), s1);
     const bool ok = chol6(L, r);
+    if (kPairs) mark(kS3Factor);  // sub-phase stamps (top side, wave 0): loads + chol6
     if (gw == wY || gw == wK) fwd6(L, r, yk);
     if (gw == wK && lane == 0)
       bad = bad || !ok || !isfinite(yk[0] + yk[1] + yk[2] + yk[3] + yk[4] + yk[5]);
@@ -1346,6 +1385,7 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
       st6g(o + 30, yk);
     }
     wave_sync<true>();
+    if (kPairs) mark(kS3Chol);  // panel solve + store
     auto task = [&](int blk, int q, int rp, double (&x0)[6], double (&x1)[6], bool store) {
       double a0[6], a1[6], bq[6];
       ld6g(Pw + 36 * (q & 0xffff) + 6 * rp, a0);
@@ -1372,6 +1412,7 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
       if (kPairs) ld6g(Sm + 36l * blk + 6 * (rp + 3), x1);
       task(blk, q, rp, x0, x1, true);
     }
+    if (kPairs) mark(kS3Barrier);  // trailing tasks
     prev_row = prow;
     prev_blk = pblk;
   };
@@ -1383,6 +1424,7 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
     const int t = g == 0 ? (p < m ? p : -1) : (p < nbot ? m + p : -1);
     if (t >= 0) step(t, gw, 2, 0, 1, 1, std::true_type{});
     __syncthreads();
+    mark(kS3Data);  // barrier wait
   }
   if (gw == 1 && prev_row) st6g(Sm + 36l * prev_blk + 6 * (lane % 6), sv);
   prev_row = false;
