@@ -1246,6 +1246,7 @@ struct Solve2Args {
   TwoSidedLayout tl;
   const int* tab;  // BAPlan::solve2_tab
   long lds_kf, lds_y, lds_panel, lds_pose, lds_tab;
+  int stamp_thread;  // diagnostic build: the thread whose clock the stamps follow
 };
 
 // LDS image: [profile 36*nprof | shadow blocks 36*nshadow | per column 36 (L, 1/diag, y')
@@ -1273,7 +1274,7 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   const TwoSidedLayout& T = A2.tl;
   unsigned long long st_t = 0, st_acc[kS3Count] = {};
   auto mark = [&](int ph) {
-    if (kStamp && threadIdx.x == 0) {
+    if (kStamp && (int)threadIdx.x == A2.stamp_thread) {
       const unsigned long long n = __builtin_amdgcn_s_memtime();
       if (st_t) st_acc[ph] += n - st_t;
       st_t = n;
@@ -1324,7 +1325,7 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
 
   bool bad = false, prev_row = false;
   int prev_blk = 0;
-  double sv[6] = {0, 0, 0, 0, 0, 0};
+  double sv[6] = {0, 0, 0, 0, 0, 0}, sv_prev[6] = {0, 0, 0, 0, 0, 0};
   // One elimination step t on a group of gnw waves (gw: this wave's index in it); roles
   // (group-local): wY updates y, wK keeps (L, 1/diag, y') and the failure flag, wC
   // writes the previous step's panel into the profile.
@@ -1343,7 +1344,6 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
     const int ntask = nt / kRows, tfi = lane * gnw + gw;
     const int it0 = tfi < ntask ? tfi / kPer : 0, rp0 = tfi % kPer;
     const int blk0 = tfi < ntask ? t_iblk[i0 + it0] : 0, q0 = tfi < ntask ? t_iq[i0 + it0] : 0;
-    if (gw == wC && prev_row) st6g(Sm + 36l * prev_blk + 6 * rr, sv);
     double L[21], r[6], yk[6], s0[6];
     {
       const double* D = Sm + 36l * t_diag[t];
@@ -1365,6 +1365,9 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
     double s1[6];
     ld6g(Sm + 36l * blk0 + 6 * rp0, s0);
     if (kPairs) ld6g(Sm + 36l * blk0 + 6 * (rp0 + 3), s1);
+    // the previous step's panel row goes to the profile only now: LDS completes in order,
+    // so a store ahead of this step's loads would delay them (the block is not read here)
+    if (gw == wC && prev_row) st6g(Sm + 36l * prev_blk + 6 * (lane % 6), sv_prev);
     const bool ok = chol6(L, r);
     if (kPairs) mark(kS3Factor);  // sub-phase stamps (top side, wave 0): loads + chol6
     if (gw == wY || gw == wK) fwd6(L, r, yk);
@@ -1376,45 +1379,55 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
       if (gw == wY) y[pyi + rr] -= sv[0] * yk[0] + sv[1] * yk[1] + sv[2] * yk[2] + sv[3] * yk[3] +
                                    sv[4] * yk[4] + sv[5] * yk[5];
     }
-    if (gw == wK && lane == 0) {
-      double* o = kf + 36l * k;
-#pragma unroll
-      for (int e = 0; e < 20; e += 2) reinterpret_cast<double2*>(o)[e / 2] = make_double2(L[e], L[e + 1]);
-      reinterpret_cast<double2*>(o)[10] = make_double2(L[20], 0.0);
-      st6g(o + 24, r);
-      st6g(o + 30, yk);
-    }
     wave_sync<true>();
     if (kPairs) mark(kS3Chol);  // panel solve + store
-    auto task = [&](int blk, int q, int rp, double (&x0)[6], double (&x1)[6], bool store) {
-      double a0[6], a1[6], bq[6];
-      ld6g(Pw + 36 * (q & 0xffff) + 6 * rp, a0);
-      if (kPairs) ld6g(Pw + 36 * (q & 0xffff) + 6 * (rp + 3), a1);
+    // trailing task: rows rp (and rp + 3) of block blk -= (panel rows of block q&0xffff)
+    // x (panel block q>>16)^T.  Operands are loaded first (TaskOps), then combined.
+    struct TaskOps {
+      double a0[6], a1[6], bq[6][6];
+    };
+    auto task_load = [&](int q, int rp, TaskOps& o) {
+      ld6g(Pw + 36 * (q & 0xffff) + 6 * rp, o.a0);
+      if (kPairs) ld6g(Pw + 36 * (q & 0xffff) + 6 * (rp + 3), o.a1);
       const double* B = Pw + 36 * (q >> 16);
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        ld6g(B + 6 * c, bq);
-        x0[c] -= a0[0] * bq[0] + a0[1] * bq[1] + a0[2] * bq[2] + a0[3] * bq[3] + a0[4] * bq[4] + a0[5] * bq[5];
-        if (kPairs)
-          x1[c] -= a1[0] * bq[0] + a1[1] * bq[1] + a1[2] * bq[2] + a1[3] * bq[3] + a1[4] * bq[4] + a1[5] * bq[5];
-      }
-      if (store) {
-        st6g(Sm + 36l * blk + 6 * rp, x0);
-        if (kPairs) st6g(Sm + 36l * blk + 6 * (rp + 3), x1);
-      }
+      for (int c = 0; c < 6; ++c) ld6g(B + 6 * c, o.bq[c]);
     };
-    task(blk0, q0, rp0, s0, s1, tfi < ntask);
+    auto task_fma = [&](const TaskOps& o, double (&x0)[6], double (&x1)[6]) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+          x0[c] = __builtin_fma(-o.a0[e], o.bq[c][e], x0[c]);
+          if (kPairs) x1[c] = __builtin_fma(-o.a1[e], o.bq[c][e], x1[c]);
+        }
+    };
+    {
+      TaskOps o;
+      task_load(q0, rp0, o);
+      task_fma(o, s0, s1);
+      if (tfi < ntask) {
+        st6g(Sm + 36l * blk0 + 6 * rp0, s0);
+        if (kPairs) st6g(Sm + 36l * blk0 + 6 * (rp0 + 3), s1);
+      }
+    }
     for (int t2 = tfi + 64 * gnw; t2 < ntask; t2 += 64 * gnw) {
       const int it = t2 / kPer, rp = t2 % kPer;
       const int blk = t_iblk[i0 + it], q = t_iq[i0 + it];
       double x0[6], x1[6];
       ld6g(Sm + 36l * blk + 6 * rp, x0);
       if (kPairs) ld6g(Sm + 36l * blk + 6 * (rp + 3), x1);
-      task(blk, q, rp, x0, x1, true);
+      TaskOps o;
+      task_load(q, rp, o);
+      task_fma(o, x0, x1);
+      st6g(Sm + 36l * blk + 6 * rp, x0);
+      if (kPairs) st6g(Sm + 36l * blk + 6 * (rp + 3), x1);
     }
     if (kPairs) mark(kS3Barrier);  // trailing tasks
     prev_row = prow;
     prev_blk = pblk;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) sv_prev[c] = sv[c];
   };
 
   // sides
@@ -1447,6 +1460,32 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   }
   if (wave == 3 && prev_row) st6g(Sm + 36l * prev_blk + 6 * (lane % 6), sv);
   if (bad) s_fail = 1;
+  __syncthreads();
+  // The factored columns for the back substitution, all at once (lane k): L_kk, 1/diag
+  // and y'_k = L_kk^-1 y_k recomputed from the final D_k and y_k, which no later step
+  // writes -- the same operations on the same values as in the elimination, so bitwise
+  // what it used.  (Stored there by one lane per step, the 17 writes queued every
+  // later LDS access of that wave.)
+  if (!prior_fail)
+    for (int k = tid; k < F; k += 256) {
+      double L[21], r[6], yk[6], dr[6];
+      const double* D = Sm + 36l * (t_off[k] + k - t_first[k]);  // block (k, k)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        ld6g(D + 6 * i, dr);
+#pragma unroll
+        for (int c = 0; c <= i; ++c) L[P6(i, c)] = dr[c];
+      }
+      ld6g(y + 6 * k, yk);
+      chol6(L, r);
+      fwd6(L, r, yk);
+      double* kc = kf + 36l * k;
+#pragma unroll
+      for (int e = 0; e < 20; e += 2) reinterpret_cast<double2*>(kc)[e / 2] = make_double2(L[e], L[e + 1]);
+      reinterpret_cast<double2*>(kc)[10] = make_double2(L[20], 0.0);
+      st6g(kc + 24, r);
+      st6g(kc + 30, yk);
+    }
   __syncthreads();
   mark(kS3Trail);
 
@@ -1531,7 +1570,7 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   }
   if (tid == 0 && failed && !prior_fail) *A.status = A.iter_tag;
   mark(kS3Tail);
-  if (kStamp && tid == 0 && A.stamps)
+  if (kStamp && tid == A2.stamp_thread && A.stamps)
     for (int k = 0; k < kS3Count; ++k) A.stamps[k] = st_acc[k];
 }
 
@@ -1941,6 +1980,7 @@ class BAEngine {
       A2.lds_panel = (long)solve2_layout_.panel;
       A2.lds_pose = (long)solve2_layout_.pose;
       A2.lds_tab = (long)solve2_layout_.tab;
+      A2.stamp_thread = 64 * std::min(3, std::max(0, getenv("VO_K3_STAMP_WAVE") ? atoi(getenv("VO_K3_STAMP_WAVE")) : 0));
       if (stamps_on_)
         hipLaunchKernelGGL((ba_solve2_kernel<true>), dim3(1), dim3(256), solve2_layout_.total, ctx_->stream, A2);
       else
