@@ -18,8 +18,8 @@ from visualodometry_amd.ba import BASession  # noqa: E402
 from visualodometry_amd.synthetic import make_ba_config  # noqa: E402
 
 PHASES = ["load", "backsub", "lin_obs", "reduce", "eliminate", "schur_pairs", "write", "schur_cams", "-", "-"]
-K3 = ["k3_setup", "k3_side_chol", "k3_backsub", "k3_tail", "k3_side_barrier", "k3_side_panel", "k3_merge",
-      "k3_separator", "k3_side_tasks"]
+K3 = ["k3_setup", "k3_side_chol", "k3_backsub", "k3_tail", "k3_side_barrier", "k3_side_midbar", "k3_merge",
+      "k3_separator", "k3_side_tasks", "k3_side_panel"]
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg3"
 p = make_ba_config(cfg)

@@ -773,6 +773,9 @@ __device__ __forceinline__ constexpr int P6(int i, int c) { return i * (i + 1) /
 // In-place Cholesky a = L L^T; r = 1/diag(L) from v_rsq_f64 + one Newton step
 // (critical chain per column: rsq + 3 dependent ops instead of sqrt + divide; the
 // step takes the ~2^-23 estimate to ~1e-14 relative).
+// kDiag = false leaves a[P6(j, j)] unfactored: no solve reads L's diagonal (fwd6/bwd6
+// use r = 1/l_jj), only the stored factor does.
+template <bool kDiag = true>
 __device__ __forceinline__ bool chol6(double (&a)[21], double (&r)[6]) {
   bool ok = true;
 #pragma unroll
@@ -783,7 +786,7 @@ __device__ __forceinline__ bool chol6(double (&a)[21], double (&r)[6]) {
     double q = __builtin_amdgcn_rsq(dd);
     if (kCholNewton) q = q * (1.5 - 0.5 * dd * q * q);
     r[j] = q;
-    a[P6(j, j)] = dd * q;
+    if (kDiag) a[P6(j, j)] = dd * q;
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) a[P6(i, j)] *= q;
 #pragma unroll
@@ -848,7 +851,7 @@ __device__ __forceinline__ void wave_sync() {
 //   wave 3       (next column) writes the panel into the profile blocks (i, k).
 // The per-column panel rows and trailing blocks come from the host-built step
 // table (BAPlan::solve_tab), staged in LDS with the profile.
-enum { kS3Setup = 0, kS3Factor, kS3Backsub, kS3Tail, kS3Data, kS3Chol, kS3Panel, kS3Trail, kS3Barrier, kS3Count };
+enum { kS3Setup = 0, kS3Factor, kS3Backsub, kS3Tail, kS3Data, kS3Chol, kS3Panel, kS3Trail, kS3Barrier, kS3Mid, kS3Count };
 
 // dst[i] = src[i], i < n: U loads in flight per thread.  Loads and stores are
 // unconditional with a clamped index (an out-of-range slot rewrites dst[n-1] with
@@ -1289,7 +1292,6 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   double* Sm = dyn;
   double* kf = dyn + A2.lds_kf;
   double* y = dyn + A2.lds_y;
-  double* Pw = dyn + A2.lds_panel + 36l * T.max_panel * wave;
   double* pose_l = dyn + A2.lds_pose;
   int* tab = reinterpret_cast<int*>(dyn + A2.lds_tab);
   const int* t_col = tab + T.col;
@@ -1301,6 +1303,7 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   const int* t_iptr = tab + T.item_ptr;
   const int* t_iblk = tab + T.item_blk;
   const int* t_iq = tab + T.item_q;
+  const int* t_ipri = tab + T.item_pri;
   const int* t_merge = tab + T.merge_main;
   const int* t_cptr = tab + T.colb_ptr;
   const int* t_colb = tab + T.colb;
@@ -1323,126 +1326,128 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   __syncthreads();
   mark(kS3Setup);
 
-  bool bad = false, prev_row = false;
-  int prev_blk = 0;
-  double sv[6] = {0, 0, 0, 0, 0, 0}, sv_prev[6] = {0, 0, 0, 0, 0, 0};
+  bool bad = false;
   // One elimination step t on a group of gnw waves (gw: this wave's index in it); roles
   // (group-local): wY updates y, wK keeps (L, 1/diag, y') and the failure flag, wC
   // writes the previous step's panel into the profile.
   // kPairs: each trailing task covers rows {rp, rp+3} of one block (2-wave groups: one
   // round of tasks over 128 lanes); otherwise one row per task.
-  auto step = [&](int t, int gw, int gnw, int wY, int wK, int wC, auto pairs_tag) {
-    constexpr bool kPairs = decltype(pairs_tag)::value;
-    const int k = t_col[t], md = t_mode[t];
-    const int p0 = t_sptr[t], nb = t_sptr[t + 1] - p0;
-    const int i0 = t_iptr[t], nt = 6 * (t_iptr[t + 1] - i0);
-    const bool prow = lane < 6 * nb;
-    const int rr = lane % 6, qi = p0 + (prow ? lane / 6 : 0);
-    const int pblk = nb > 0 ? t_pblk[qi] : 0, pyi = nb > 0 ? t_py[qi] : 0;
-    // trailing tasks: (block item, row or row pair), one per lane per round
-    constexpr int kRows = kPairs ? 2 : 1, kPer = 6 / kRows;
-    const int ntask = nt / kRows, tfi = lane * gnw + gw;
-    const int it0 = tfi < ntask ? tfi / kPer : 0, rp0 = tfi % kPer;
-    const int blk0 = tfi < ntask ? t_iblk[i0 + it0] : 0, q0 = tfi < ntask ? t_iq[i0 + it0] : 0;
-    double L[21], r[6], yk[6], s0[6];
+  // Per-step table entries (k, mode, panel range, item range, look-ahead items) and the
+  // panel wave's lane entries (its panel block and y row).
+  struct StepTab {
+    int k, md, p0, nb, i0, nit, npri, diag, pblk, pyi;
+  };
+  auto tabs = [&](int t, StepTab& s) {
+    s.k = t_col[t];
+    s.md = t_mode[t];
+    s.p0 = t_sptr[t];
+    s.nb = t_sptr[t + 1] - s.p0;
+    s.i0 = t_iptr[t];
+    s.nit = t_iptr[t + 1] - s.i0;
+    s.npri = t_ipri[t];
+    s.diag = t_diag[t];
+    const int qi = s.p0 + (lane < 6 * s.nb ? lane / 6 : 0);
+    s.pblk = s.nb > 0 ? t_pblk[qi] : 0;
+    s.pyi = s.nb > 0 ? t_py[qi] : 0;
+  };
+  // Panel of a step (one wave, one lane per panel row): factor the diagonal block, solve
+  // the panel rows, write them into the profile blocks they replace, update y.
+  auto panel = [&](const StepTab& st) {
+    const bool prow = lane < 6 * st.nb;
+    const int rr = lane % 6;
+    double L[21], r[6], yk[6], sv[6];
     {
-      const double* D = Sm + 36l * t_diag[t];
-      double dr[6];
+      // lower triangle of the diagonal block: row i needs its first i + 1 entries
+      const double2* D = reinterpret_cast<const double2*>(Sm + 36l * st.diag);
 #pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        ld6g(D + 6 * i, dr);
+      for (int i = 0; i < 6; ++i)
 #pragma unroll
-        for (int c = 0; c <= i; ++c) L[P6(i, c)] = dr[c];
-      }
+        for (int c = 0; c <= i; c += 2) {
+          const double2 v = D[3 * i + c / 2];
+          L[P6(i, c)] = v.x;
+          if (c + 1 <= i) L[P6(i, c + 1)] = v.y;
+        }
     }
-    ld6g(y + 6 * k, yk);
-    if (md == 0) {
-      ld6g(Sm + 36l * pblk + 6 * rr, sv);  // row rr of block (i, k)
+    ld6g(y + 6 * st.k, yk);
+    if (st.md == 0) {
+      ld6g(Sm + 36l * st.pblk + 6 * rr, sv);  // row rr of block (i, k)
     } else {
 #pragma unroll
-      for (int c = 0; c < 6; ++c) sv[c] = Sm[36l * pblk + 6 * c + rr];  // column rr of block (k, j)
+      for (int c = 0; c < 6; ++c) sv[c] = Sm[36l * st.pblk + 6 * c + rr];  // column rr of block (k, j)
     }
-    double s1[6];
-    ld6g(Sm + 36l * blk0 + 6 * rp0, s0);
-    if (kPairs) ld6g(Sm + 36l * blk0 + 6 * (rp0 + 3), s1);
-    // the previous step's panel row goes to the profile only now: LDS completes in order,
-    // so a store ahead of this step's loads would delay them (the block is not read here)
-    if (gw == wC && prev_row) st6g(Sm + 36l * prev_blk + 6 * (lane % 6), sv_prev);
-    const bool ok = chol6(L, r);
-    if (kPairs) mark(kS3Factor);  // sub-phase stamps (top side, wave 0): loads + chol6
-    if (gw == wY || gw == wK) fwd6(L, r, yk);
-    if (gw == wK && lane == 0)
-      bad = bad || !ok || !isfinite(yk[0] + yk[1] + yk[2] + yk[3] + yk[4] + yk[5]);
+    __builtin_amdgcn_sched_barrier(0);
+    const bool ok = chol6<false>(L, r);
+    fwd6(L, r, yk);
+    if (lane == 0) bad = bad || !ok || !isfinite(yk[0] + yk[1] + yk[2] + yk[3] + yk[4] + yk[5]);
     fwd6(L, r, sv);
     if (prow) {
-      st6g(Pw + 6 * lane, sv);
-      if (gw == wY) y[pyi + rr] -= sv[0] * yk[0] + sv[1] * yk[1] + sv[2] * yk[2] + sv[3] * yk[3] +
-                                   sv[4] * yk[4] + sv[5] * yk[5];
+      // the panel row of L (bottom side: row of L~ in block (k, j)) replaces the block row
+      st6g(Sm + 36l * st.pblk + 6 * rr, sv);
+      y[st.pyi + rr] -= sv[0] * yk[0] + sv[1] * yk[1] + sv[2] * yk[2] + sv[3] * yk[3] +
+                        sv[4] * yk[4] + sv[5] * yk[5];
     }
-    wave_sync<true>();
-    if (kPairs) mark(kS3Chol);  // panel solve + store
-    // trailing task: rows rp (and rp + 3) of block blk -= (panel rows of block q&0xffff)
-    // x (panel block q>>16)^T.  Operands are loaded first (TaskOps), then combined.
-    struct TaskOps {
-      double a0[6], a1[6], bq[6][6];
-    };
-    auto task_load = [&](int q, int rp, TaskOps& o) {
-      ld6g(Pw + 36 * (q & 0xffff) + 6 * rp, o.a0);
-      if (kPairs) ld6g(Pw + 36 * (q & 0xffff) + 6 * (rp + 3), o.a1);
-      const double* B = Pw + 36 * (q >> 16);
+  };
+  // Trailing tasks [ta, tb) of a step over nl lanes (this lane: li): rows rp (and rp + 3
+  // with kPairs) of the item's block -= (rows of panel block q & 0xffff) x (panel block
+  // q >> 16)^T, the panel blocks already holding L.
+  auto tasks = [&](const StepTab& st, int ta, int tb, int li, int nl, auto pairs_tag) {
+    constexpr bool kPairs = decltype(pairs_tag)::value;
+    constexpr int kPer = kPairs ? 3 : 6;
+    for (int t2 = ta + li; t2 < tb; t2 += nl) {
+      const int it = t2 / kPer, rp = t2 % kPer;
+      const int blk = t_iblk[st.i0 + it], q = t_iq[st.i0 + it];
+      double x0[6], x1[6], a0[6], a1[6], bq[6][6];
+      ld6g(Sm + 36l * blk + 6 * rp, x0);
+      if (kPairs) ld6g(Sm + 36l * blk + 6 * (rp + 3), x1);
+      ld6g(Sm + 36l * (q & 0xffff) + 6 * rp, a0);
+      if (kPairs) ld6g(Sm + 36l * (q & 0xffff) + 6 * (rp + 3), a1);
+      const double* B = Sm + 36l * (q >> 16);
 #pragma unroll
-      for (int c = 0; c < 6; ++c) ld6g(B + 6 * c, o.bq[c]);
-    };
-    auto task_fma = [&](const TaskOps& o, double (&x0)[6], double (&x1)[6]) {
+      for (int c = 0; c < 6; ++c) ld6g(B + 6 * c, bq[c]);
 #pragma unroll
       for (int c = 0; c < 6; ++c)
 #pragma unroll
         for (int e = 0; e < 6; ++e) {
-          x0[c] = __builtin_fma(-o.a0[e], o.bq[c][e], x0[c]);
-          if (kPairs) x1[c] = __builtin_fma(-o.a1[e], o.bq[c][e], x1[c]);
+          x0[c] = __builtin_fma(-a0[e], bq[c][e], x0[c]);
+          if (kPairs) x1[c] = __builtin_fma(-a1[e], bq[c][e], x1[c]);
         }
-    };
-    {
-      TaskOps o;
-      task_load(q0, rp0, o);
-      task_fma(o, s0, s1);
-      if (tfi < ntask) {
-        st6g(Sm + 36l * blk0 + 6 * rp0, s0);
-        if (kPairs) st6g(Sm + 36l * blk0 + 6 * (rp0 + 3), s1);
-      }
-    }
-    for (int t2 = tfi + 64 * gnw; t2 < ntask; t2 += 64 * gnw) {
-      const int it = t2 / kPer, rp = t2 % kPer;
-      const int blk = t_iblk[i0 + it], q = t_iq[i0 + it];
-      double x0[6], x1[6];
-      ld6g(Sm + 36l * blk + 6 * rp, x0);
-      if (kPairs) ld6g(Sm + 36l * blk + 6 * (rp + 3), x1);
-      TaskOps o;
-      task_load(q, rp, o);
-      task_fma(o, x0, x1);
       st6g(Sm + 36l * blk + 6 * rp, x0);
       if (kPairs) st6g(Sm + 36l * blk + 6 * (rp + 3), x1);
     }
-    if (kPairs) mark(kS3Barrier);  // trailing tasks
-    prev_row = prow;
-    prev_blk = pblk;
-#pragma unroll
-    for (int c = 0; c < 6; ++c) sv_prev[c] = sv[c];
   };
 
-  // sides
+  // Sides, with look-ahead: in phase p, wave A of a side (gw 0) applies the step's items
+  // on the next step's line and then factors that next step's panel, while wave B applies
+  // the remaining items; one barrier per phase.  Disjoint blocks: A writes the next
+  // line and panel, B the rest of the trailing window; both read the current panel.
   const int g = wave >> 1, gw = wave & 1;
   const int P = m > nbot ? m : nbot;
+  const int nside = g == 0 ? m : nbot, tbase = g == 0 ? 0 : m;
+  StepTab cur, nxt;
+  if (!prior_fail) {
+    tabs(tbase, cur);
+    if (gw == 0) panel(cur);
+  }
+  __syncthreads();
+  mark(kS3Factor);
   for (int p = 0; p < P && !prior_fail; ++p) {
-    const int t = g == 0 ? (p < m ? p : -1) : (p < nbot ? m + p : -1);
-    if (t >= 0) step(t, gw, 2, 0, 1, 1, std::true_type{});
+    if (p < nside) {
+      const bool more = p + 1 < nside;
+      tabs(tbase + (more ? p + 1 : p), nxt);
+      if (gw == 0) {
+        tasks(cur, 0, 3 * cur.npri, lane, 64, std::true_type{});
+        mark(kS3Barrier);
+        if (more) panel(nxt);
+        mark(kS3Mid);
+      } else {
+        tasks(cur, 3 * cur.npri, 3 * cur.nit, lane, 64, std::true_type{});
+        mark(kS3Barrier);
+      }
+      cur = nxt;
+    }
     __syncthreads();
     mark(kS3Data);  // barrier wait
   }
-  if (gw == 1 && prev_row) st6g(Sm + 36l * prev_blk + 6 * (lane % 6), sv);
-  prev_row = false;
-  __syncthreads();
-  mark(kS3Data);
   // merge the bottom side's separator contributions (fixed order)
   if (!prior_fail) {
     for (int e = tid; e < 36 * T.nshadow; e += 256) {
@@ -1453,12 +1458,24 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   }
   __syncthreads();
   mark(kS3Panel);
-  // separator
+  // separator, same look-ahead: wave 0 the next line and panel, waves 1-3 the rest
+  if (!prior_fail && m + nbot < F) {
+    tabs(m + nbot, cur);
+    if (wave == 0) panel(cur);
+  }
+  __syncthreads();
   for (int t = m + nbot; t < F && !prior_fail; ++t) {
-    step(t, wave, 4, 1, 2, 3, std::false_type{});
+    const bool more = t + 1 < F;
+    tabs(more ? t + 1 : t, nxt);
+    if (wave == 0) {
+      tasks(cur, 0, 6 * cur.npri, lane, 64, std::false_type{});
+      if (more) panel(nxt);
+    } else {
+      tasks(cur, 6 * cur.npri, 6 * cur.nit, tid - 64, 192, std::false_type{});
+    }
+    cur = nxt;
     __syncthreads();
   }
-  if (wave == 3 && prev_row) st6g(Sm + 36l * prev_blk + 6 * (lane % 6), sv);
   if (bad) s_fail = 1;
   __syncthreads();
   // The factored columns for the back substitution, all at once (lane k): L_kk, 1/diag

@@ -302,17 +302,29 @@ static void build_two_sided(BAPlan& P) {
   auto in_sep = [&](int i) { return i >= m && i < m + s; };
   const int nprof = P.n_prof_blocks();
   auto shadow = [&](int a, int b) { return nprof + (a - m) * (a - m + 1) / 2 + (b - m); };
-  std::vector<int32_t> col, mode, diag, sptr{0}, pblk, py, iptr{0}, iblk, iq;
+  std::vector<int32_t> col, mode, diag, sptr{0}, pblk, py, iptr{0}, iblk, iq, ipri;
   int maxnb = 0;
-  auto add_items = [&](const std::vector<int>& rows, bool bottom) {
+  // item_q: the two panel blocks (profile indices) whose rows form the update of the
+  // item's block: (rows of block lo16) x (block hi16)^T
+  // Items of one step, those of the look-ahead line first (ipri of them): the blocks of
+  // the next step's column (top / separator: b == lk) or row (bottom: a == lk), which the
+  // panel wave updates before it factors that next step.
+  auto add_items = [&](const std::vector<int>& rows, const std::vector<int32_t>& pb, bool bottom,
+                       int lk) {
     const int nb = (int)rows.size();
-    for (int q1 = 0; q1 < nb; ++q1)
-      for (int q2 = 0; q2 <= q1; ++q2) {
-        const int a = rows[q1], b = rows[q2];  // a >= b (rows ascending)
-        iblk.push_back(bottom && in_sep(a) && in_sep(b) ? shadow(a, b) : blk(a, b));
-        iq.push_back(q1 | (q2 << 16));
-      }
+    int npri = 0;
+    for (int pass = 0; pass < 2; ++pass)
+      for (int q1 = 0; q1 < nb; ++q1)
+        for (int q2 = 0; q2 <= q1; ++q2) {
+          const int a = rows[q1], b = rows[q2];  // a >= b (rows ascending)
+          const bool pri = bottom ? a == lk : b == lk;
+          if (pri != (pass == 0)) continue;
+          npri += pri;
+          iblk.push_back(bottom && in_sep(a) && in_sep(b) ? shadow(a, b) : blk(a, b));
+          iq.push_back(pb[q1] | (pb[q2] << 16));
+        }
     iptr.push_back((int32_t)iblk.size());
+    ipri.push_back(npri);
   };
   // top steps (top-down, panels may include separator rows)
   for (int k = 0; k < m; ++k) {
@@ -322,13 +334,15 @@ static void build_two_sided(BAPlan& P) {
     col.push_back(k);
     mode.push_back(0);
     diag.push_back(blk(k, k));
+    std::vector<int32_t> pb;
     for (int i : rows) {
+      pb.push_back(blk(i, k));
       pblk.push_back(blk(i, k));
       py.push_back(6 * i);
     }
     sptr.push_back((int32_t)pblk.size());
     maxnb = std::max(maxnb, (int)rows.size());
-    add_items(rows, false);
+    add_items(rows, pb, false, k + 1);
   }
   // bottom steps (bottom-up: row k's blocks (k, j), j in [first[k], k))
   for (int k = F - 1; k >= m + s; --k) {
@@ -337,13 +351,15 @@ static void build_two_sided(BAPlan& P) {
     col.push_back(k);
     mode.push_back(1);
     diag.push_back(blk(k, k));
+    std::vector<int32_t> pb;
     for (int j : rows) {
+      pb.push_back(blk(k, j));
       pblk.push_back(blk(k, j));
       py.push_back(in_sep(j) ? 6 * F + 6 * (j - m) : 6 * j);
     }
     sptr.push_back((int32_t)pblk.size());
     maxnb = std::max(maxnb, (int)rows.size());
-    add_items(rows, true);
+    add_items(rows, pb, true, k - 1);
   }
   // separator steps (top-down within the separator)
   for (int k = m; k < m + s; ++k) {
@@ -353,13 +369,15 @@ static void build_two_sided(BAPlan& P) {
     col.push_back(k);
     mode.push_back(0);
     diag.push_back(blk(k, k));
+    std::vector<int32_t> pb;
     for (int i : rows) {
+      pb.push_back(blk(i, k));
       pblk.push_back(blk(i, k));
       py.push_back(6 * i);
     }
     sptr.push_back((int32_t)pblk.size());
     maxnb = std::max(maxnb, (int)rows.size());
-    add_items(rows, false);
+    add_items(rows, pb, false, k + 1);
   }
   std::vector<int32_t> merge;
   for (int a = m; a < m + s; ++a)
@@ -390,6 +408,7 @@ static void build_two_sided(BAPlan& P) {
   put(L.item_ptr, iptr);
   put(L.item_blk, iblk);
   put(L.item_q, iq);
+  put(L.item_pri, ipri);
   put(L.merge_main, merge);
   put(L.colb_ptr, cptr);
   put(L.colb, cl);
@@ -401,7 +420,8 @@ static void build_two_sided(BAPlan& P) {
   L.nbot = nbot;
   L.nshadow = s * (s + 1) / 2;
   L.max_panel = maxnb;
-  L.enabled = maxnb <= 10 ? 1 : 0;  // one lane per panel row per wave
+  // one lane per panel row of the panel wave; item_q packs two 16-bit block indices
+  L.enabled = maxnb <= 10 && nprof + L.nshadow < 65536 ? 1 : 0;
 }
 
 std::vector<int32_t> local_profile_first(const BAPlan& P) {

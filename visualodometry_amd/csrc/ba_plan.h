@@ -56,6 +56,7 @@ struct TwoSidedLayout {
   int enabled = 0, m = 0, s = 0, nbot = 0, nshadow = 0;
   int col = 0, mode = 0, diag = 0, step_ptr = 0, panel_blk = 0, panel_y = 0, item_ptr = 0,
       item_blk = 0, item_q = 0;
+  int item_pri = 0;             // per step: leading items on the look-ahead line
   int merge_main = 0;           // per shadow block: its profile block, -1 if none
   int colb_ptr = 0, colb = 0;   // per k >= m: (bottom row i > k, block (i, k)) pairs
   int off = 0, first = 0, len = 0;
