@@ -17,7 +17,9 @@ from visualodometry_amd import _lib  # noqa: E402
 from visualodometry_amd.ba import BASession  # noqa: E402
 from visualodometry_amd.synthetic import make_ba_config  # noqa: E402
 
-PHASES = ["load", "backsub", "lin_obs", "reduce", "eliminate", "schur_pairs", "write", "schur_cams", "-", "-"]
+PHASES = ["load", "backsub", "lin_obs", "reduce", "eliminate", "schur_pairs", "write", "schur_cams", "-", "-",
+          "n_obs", "n_te", "n_pts", "n_pairs", "n_slots", "n_cams"]
+NPH = len(PHASES)
 K3 = ["k3_setup", "k3_side_chol", "k3_backsub", "k3_tail", "k3_side_barrier", "k3_side_midbar", "k3_merge",
       "k3_separator", "k3_side_tasks", "k3_side_panel"]
 
@@ -41,10 +43,10 @@ for k in range(len(PHASES), n):
 
 # per-workgroup timeline of the last K1 launch (start/end absolute stamps)
 nseg = s.plan_stats()["segments"]
-raw = np.zeros(nseg * 10, dtype=np.uint64)
+raw = np.zeros(nseg * NPH, dtype=np.uint64)
 k = ctx.lib.vo_ba_debug_stamps(ctx.handle, raw.ctypes.data_as(_lib.C.POINTER(_lib.C.c_uint64)), -raw.size)
 if k > 0:
-    r = raw[:k].reshape(-1, 10).astype(np.int64)
+    r = raw[:k].reshape(-1, NPH).astype(np.int64)
     t0, t1 = r[:, 8], r[:, 9]
     base = t0.min()
     dur = t1 - t0
@@ -54,3 +56,6 @@ if k > 0:
     print("  first 5 starts", (t0[order[:5]] - base).tolist(), " last 5 starts", (t0[order[-5:]] - base).tolist())
     slow = np.argsort(dur)[-5:]
     print("  slowest segments", slow.tolist(), dur[slow].tolist())
+    if len(sys.argv) > 2:  # per-segment rows for cost-model fitting: duration, phases, counts
+        np.savetxt(sys.argv[2], np.column_stack([dur, r[:, :8], r[:, 10:16]]), fmt="%d",
+                   header="dur " + " ".join(PHASES[:8]) + " " + " ".join(PHASES[10:16]))

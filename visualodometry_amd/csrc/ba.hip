@@ -358,6 +358,29 @@ __device__ __forceinline__ void chunk_backsub(LinShared& S, const LinArgs& A, in
   }
 }
 
+// Lanes per Schur item: the largest power of two <= 8 that keeps every item's parts in
+// one pass of the workgroup (parts of an item are adjacent lanes of one wave).
+__device__ __forceinline__ int parts_for(int items) {
+  return items * 8 <= kLinThreads ? 8 : items * 4 <= kLinThreads ? 4 : items * 2 <= kLinThreads ? 2 : 1;
+}
+
+template <int Ctrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), Ctrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), Ctrl, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum of the np (2, 4 or 8) adjacent lanes' values, valid in the first lane of each
+// group: a fixed butterfly (xor 1, xor 2 within quads, then row_shl:4), so the order of
+// the additions never depends on timing.  Every lane of the wave must execute it.
+__device__ __forceinline__ double sum_parts(double v, int np) {
+  v += dpp_f64<0xB1>(v);               // quad_perm [1,0,3,2]
+  if (np >= 4) v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
+  if (np >= 8) v += dpp_f64<0x104>(v); // row_shl:4 (lane 8g + 0 reads 8g + 4)
+  return v;
+}
+
 // Diagnostic build (VO_BA_STAMPS=1): thread 0 accumulates s_memtime deltas per
 // phase; the production instantiation has kStamp = false and executes none.
 // dst[i] = src[i] + add, i < n, by the workgroup: U loads per thread issued before
@@ -375,7 +398,10 @@ __device__ __forceinline__ void stage(T* dst, const Src* __restrict__ src, int n
   }
 }
 
-enum { kPhLoad = 0, kPhBacksub, kPhLinObs, kPhReduce, kPhElim, kPhSchur, kPhWrite, kPhSchurU, kPhT0, kPhT1, kPhCount };
+enum { kPhLoad = 0, kPhBacksub, kPhLinObs, kPhReduce, kPhElim, kPhSchur, kPhWrite, kPhSchurU, kPhT0, kPhT1,
+       // per-segment work counts (cost-model fitting): observations, track entries,
+       // landmarks, pair-list entries, window slots, window cameras
+       kPhObs, kPhTe, kPhPts, kPhPairs, kPhSlots, kPhCams, kPhCount };
 template <bool kStamp>
 struct Stamper {
   unsigned long long t = 0, acc[kPhCount] = {};
@@ -388,6 +414,9 @@ struct Stamper {
       acc[ph] += n - t;
       t = n;
     }
+  }
+  __device__ __forceinline__ void count(int k, int v) {
+    if (kStamp && threadIdx.x == 0) acc[k] += (unsigned long long)v;
   }
   __device__ __forceinline__ void flush(unsigned long long* out) {
     if (kStamp && threadIdx.x == 0) acc[kPhT1] = __builtin_amdgcn_s_memtime();  // absolute
@@ -422,12 +451,18 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
     }
   }
   double cost = 0.0;
+  st.count(kPhSlots, nslots);
+  st.count(kPhCams, ncams);
   for (int ch = A.seg_chunk[seg]; ch < A.seg_chunk[seg + 1]; ++ch) {
     // one uniform header load, then every list load of the chunk in flight at once
     const int4 h0 = A.chunk_hdr[4l * ch], h1 = A.chunk_hdr[4l * ch + 1], h2 = A.chunk_hdr[4l * ch + 2],
                h3 = A.chunk_hdr[4l * ch + 3];
     const int ob0 = h0.x, nob = h0.y, te0 = h0.z, nte = h0.w, p0 = h1.x, npt = h1.y;
     const int sb = h1.z, cb = h1.w, e0 = h2.x, e1 = h2.y, c0 = h2.z, c1 = h2.w, q0 = h3.x, q1 = h3.y;
+    st.count(kPhObs, nob);
+    st.count(kPhTe, nte);
+    st.count(kPhPts, npt);
+    st.count(kPhPairs, e1 - e0);
     // every staging load of this thread first (unconditional: an empty list reads its
     // array's first element), then -- after the previous chunk is consumed -- the stores
     const int i0 = tid, i1 = tid + kLinThreads;
@@ -505,96 +540,120 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
     __syncthreads();
     st.mark(kPhElim);
 
-    // R4: Schur blocks into the window; lane owns (slot, row a) and sums its
-    // slot's pair list of this chunk in fixed order.  Unrolled by two with two
-    // register sets: pair e+2's Z rows are fetched (16-byte LDS reads, indices read
-    // two pairs ahead, clamped -- no branches) while pair e+1's 18 FMAs run.  On a
-    // diagonal slot the U = Jc^T Jc terms of its track entries follow in a second loop.
-    for (int item = tid; item < nslots * 6; item += kLinThreads) {
-      const int s = item / 6, a = item - 6 * (item / 6);
-      const int e0 = S.slotp[s], e1 = S.slotp[s + 1];
-      if (e0 == e1) continue;
-      double out[6] = {0, 0, 0, 0, 0, 0};
-      auto zrow = [&](int pr, double (&za)[3], double2 (&zy)[9]) {
-        const double2* py = reinterpret_cast<const double2*>(S.Z[pr >> 8]);
+    // R4: Schur blocks into the window.  Item (slot, row a) sums its slot's pair list of
+    // this chunk; with few slots (narrow segments: two cameras, many two-view landmarks)
+    // an item's list is split over np lanes (pairs e0 + part + j np) whose partial rows
+    // are combined by a fixed DPP butterfly -- deterministic, no LDS scratch.  Unrolled by
+    // two with two register sets: pair j+2's Z rows are fetched (16-byte LDS reads,
+    // indices read two pairs ahead, clamped -- no branches) while pair j+1's 18 FMAs run.
+    {
+      const int items = nslots * 6;
+      const int np = parts_for(items);
+      for (int base = 0; base < items * np; base += kLinThreads) {
+        const int idx = base + tid, item = idx / np, part = idx % np;
+        const int s = item / 6, a = item - 6 * (item / 6);
+        double out[6] = {0, 0, 0, 0, 0, 0};
+        const int e0 = item < items ? S.slotp[s] + part : 0, e1 = item < items ? S.slotp[s + 1] : 0;
+        if (e0 < e1) {
+          auto zrow = [&](int pr, double (&za)[3], double2 (&zy)[9]) {
+            const double2* py = reinterpret_cast<const double2*>(S.Z[pr >> 8]);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) zy[k] = py[k];
-        const double* px = &S.Z[pr & 255][3 * a];
-        za[0] = px[0];
-        za[1] = px[1];
-        za[2] = px[2];
-      };
-      auto accum = [&](const double (&za)[3], const double2 (&zy)[9]) {
-        const double* zf = reinterpret_cast<const double*>(zy);
+            for (int k = 0; k < 9; ++k) zy[k] = py[k];
+            const double* px = &S.Z[pr & 255][3 * a];
+            za[0] = px[0];
+            za[1] = px[1];
+            za[2] = px[2];
+          };
+          auto accum = [&](const double (&za)[3], const double2 (&zy)[9]) {
+            const double* zf = reinterpret_cast<const double*>(zy);
 #pragma unroll
-        for (int c = 0; c < 6; ++c)
-          out[c] -= za[0] * zf[3 * c] + za[1] * zf[3 * c + 1] + za[2] * zf[3 * c + 2];
-      };
-      const int last = e1 - 1;
-      const int p0 = S.pairs[e0];
-      double zaA[3], zaB[3];
-      double2 zyA[9], zyB[9];
-      zrow(p0, zaA, zyA);
-      zrow(S.pairs[min(e0 + 1, last)], zaB, zyB);
-      // indices of the pairs two ahead, read one iteration before their rows are fetched
-      int pc = S.pairs[min(e0 + 2, last)], pd = S.pairs[min(e0 + 3, last)];
-      int e = e0;
-      for (; e + 2 <= e1; e += 2) {
-        const int pe = S.pairs[min(e + 4, last)], pf = S.pairs[min(e + 5, last)];
-        accum(zaA, zyA);
-        zrow(pc, zaA, zyA);
-        accum(zaB, zyB);
-        zrow(pd, zaB, zyB);
-        pc = pe;
-        pd = pf;
+            for (int c = 0; c < 6; ++c)
+              out[c] -= za[0] * zf[3 * c] + za[1] * zf[3 * c + 1] + za[2] * zf[3 * c + 2];
+          };
+          const int n = (e1 - e0 + np - 1) / np;  // this part's pairs
+          auto pid = [&](int j) { return (int)S.pairs[e0 + min(j, n - 1) * np]; };
+          double zaA[3], zaB[3];
+          double2 zyA[9], zyB[9];
+          zrow(pid(0), zaA, zyA);
+          zrow(pid(1), zaB, zyB);
+          int pc = pid(2), pd = pid(3);
+          int j = 0;
+          for (; j + 2 <= n; j += 2) {
+            const int pe = pid(j + 4), pf = pid(j + 5);
+            accum(zaA, zyA);
+            zrow(pc, zaA, zyA);
+            accum(zaB, zyB);
+            zrow(pd, zaB, zyB);
+            pc = pe;
+            pd = pf;
+          }
+          if (j < n) accum(zaA, zyA);
+        }
+        if (np > 1)
+#pragma unroll
+          for (int c = 0; c < 6; ++c) out[c] = sum_parts(out[c], np);
+        if (item < items && part == 0)
+#pragma unroll
+          for (int c = 0; c < 6; ++c) S.win[36 * s + 6 * a + c] += out[c];
       }
-      if (e < e1) accum(zaA, zyA);
-#pragma unroll
-      for (int c = 0; c < 6; ++c) S.win[36 * s + 6 * a + c] += out[c];
     }
     st.mark(kPhSchur);
     __syncthreads();  // the diagonal slots receive U below
     // per window camera c, row a: U_c row a = sum over its observations of Jc^T Jc
     // (static observation list, indices read ahead) and b_c[a] = sum of bt over its
-    // track entries
-    for (int item = tid; item < ncams * 6; item += kLinThreads) {
-      const int c = item / 6, a = item - 6 * (item / 6);
-      const int q0 = S.camop[c], q1 = S.camop[c + 1];
-      double out[6] = {0, 0, 0, 0, 0, 0};
-      if (q1 > q0) {
-        const int ql = q1 - 1;
-        int on = S.camol[q0];
-        for (int q = q0; q < q1; ++q) {
-          const int o = on;
-          on = S.camol[min(q + 1, ql)];
-          const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
-          double j[12];
+    // track entries; split over np lanes like the pairs when the window is narrow
+    {
+      const int items = ncams * 6;
+      const int np = parts_for(items);
+      for (int base = 0; base < items * np; base += kLinThreads) {
+        const int idx = base + tid, item = idx / np, part = idx % np;
+        const int c = item / 6, a = item - 6 * (item / 6);
+        double out[6] = {0, 0, 0, 0, 0, 0};
+        double acc = 0.0;
+        if (item < items) {
+          const int q0 = S.camop[c] + part, q1 = S.camop[c + 1];
+          if (q1 > q0) {
+            const int ql = q1 - 1;
+            int on = S.camol[q0];
+            for (int q = q0; q < q1; q += np) {
+              const int o = on;
+              on = S.camol[min(q + np, ql)];
+              const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
+              double j[12];
 #pragma unroll
-          for (int k = 0; k < 6; ++k) {
-            const double2 v = jr[k];
-            j[2 * k] = v.x;
-            j[2 * k + 1] = v.y;
+              for (int k = 0; k < 6; ++k) {
+                const double2 v = jr[k];
+                j[2 * k] = v.x;
+                j[2 * k + 1] = v.y;
+              }
+              const double ja0 = S.Jc[o][a], ja1 = S.Jc[o][6 + a];
+#pragma unroll
+              for (int cc = 0; cc < 6; ++cc) out[cc] += ja0 * j[cc] + ja1 * j[6 + cc];
+            }
           }
-          const double ja0 = S.Jc[o][a], ja1 = S.Jc[o][6 + a];
+          const int e0 = S.camp[c] + part, e1 = S.camp[c + 1];
+          if (e1 > e0) {
+            const int el = e1 - 1;
+            int xn = S.caml[e0];
+            for (int e = e0; e < e1; e += np) {
+              const int x = xn;
+              xn = S.caml[min(e + np, el)];
+              acc += S.bt[x][a];
+            }
+          }
+        }
+        if (np > 1) {
 #pragma unroll
-          for (int cc = 0; cc < 6; ++cc) out[cc] += ja0 * j[cc] + ja1 * j[6 + cc];
+          for (int cc = 0; cc < 6; ++cc) out[cc] = sum_parts(out[cc], np);
+          acc = sum_parts(acc, np);
+        }
+        if (item < items && part == 0) {
+          S.bwin[6 * c + a] += acc;
+          double* w = &S.win[36 * S.dslot[c] + 6 * a];
+#pragma unroll
+          for (int cc = 0; cc < 6; ++cc) w[cc] += out[cc];
         }
       }
-      double acc = 0.0;
-      const int e0 = S.camp[c], e1 = S.camp[c + 1];
-      if (e1 > e0) {
-        const int el = e1 - 1;
-        int xn = S.caml[e0];
-        for (int e = e0; e < e1; ++e) {
-          const int x = xn;
-          xn = S.caml[min(e + 1, el)];
-          acc += S.bt[x][a];
-        }
-      }
-      S.bwin[6 * c + a] += acc;
-      double* w = &S.win[36 * S.dslot[c] + 6 * a];
-#pragma unroll
-      for (int cc = 0; cc < 6; ++cc) w[cc] += out[cc];
     }
     st.mark(kPhSchurU);
   }
