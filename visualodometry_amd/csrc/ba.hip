@@ -81,6 +81,8 @@ struct LinArgs {
   const int* chunk_slot_base;
   const int* chunk_cam_base;
   const int4* chunk_hdr;  // kChunkHdr ints per chunk (BAPlan::chunk_hdr)
+  const ChunkImg* chunk_img;  // BAPlan::chunk_img
+  const int* seg_hdr;     // kSegHdr ints per segment (BAPlan::seg_hdr)
   const int* seg_acam_off;
   const int* seg_acam;
   const uint8_t* obs_acam;
@@ -107,6 +109,7 @@ struct LinArgs {
 };
 
 struct alignas(16) LinShared {
+  ChunkImg img;  // static chunk lists (BAPlan::chunk_img), staged as one image
   double win[kSegSlots * 36];
   double bwin[kSegCams * 6];
   double Jc[kChunkObs][12];
@@ -118,24 +121,10 @@ struct alignas(16) LinShared {
   double L[kChunkPts][6];  // 1/l00, l10, 1/l11, l20, l21, 1/l22
   double h[kChunkPts][3];
   double dcw[kSegCams][6];  // pending pose update of the segment's window cameras
-  int obs_te[kChunkObs];
-  int te_obs[kChunkTe + 1];
-  int te_pt[kChunkTe];
   int te_use[kChunkTe];  // free camera and valid landmark
-  int te_lcam[kChunkTe];
-  int pt_te[kChunkPts + 1];
   int valid[kChunkPts];
-  int slotp[kSegSlots + 1];  // this chunk's pair list offsets per window slot
-  int camp[kSegCams + 1];    // this chunk's track-entry list offsets per window camera
-  int camop[kSegCams + 1];   // this chunk's observation list offsets per window camera
-  int dslot[kSegCams];       // diagonal slot of each window camera
-  uint16_t pairs[kChunkPairs];
-  uint8_t caml[kChunkTe];
-  uint8_t camol[kChunkObs];
   double pose_o[kSegAllCams][12];  // poses of every camera the segment sees: pending step's
   double pose_n[kSegAllCams][12];  // linearisation point (back substitution) and the new one
-  float2 uv[kChunkObs];
-  uint8_t acam[kChunkObs];         // observation -> index into pose_o / pose_n
 };
 // three K1 workgroups per CU (the cfg3 plan then runs in a single round)
 static_assert(sizeof(LinShared) <= 160 * 1024 / 3, "K1 LDS image");
@@ -144,14 +133,14 @@ static_assert(sizeof(LinShared) <= 160 * 1024 / 3, "K1 LDS image");
 __device__ __forceinline__ void lin_obs(LinShared& S, const LinArgs& A, const double (*pose)[12],
                                         int nob, double& cost) {
   for (int o = threadIdx.x; o < nob; o += kLinThreads) {
-    const double* T = pose[S.acam[o]];
-    const int q = S.te_pt[S.obs_te[o]];
+    const double* T = pose[S.img.acam[o]];
+    const int q = S.img.te_pt[S.img.obs_te[o]];
     const double X0 = S.X[q][0], X1 = S.X[q][1], X2 = S.X[q][2];
     const double x = T[0] * X0 + T[1] * X1 + T[2] * X2 + T[9];
     const double y = T[3] * X0 + T[4] * X1 + T[5] * X2 + T[10];
     const double z = T[6] * X0 + T[7] * X1 + T[8] * X2 + T[11];
     const double iz = 1.0 / z;
-    const float2 m = S.uv[o];
+    const float2 m = reinterpret_cast<const float2*>(S.img.uv)[o];
     const double r0 = A.fx * x * iz + A.cx - (double)m.x;
     const double r1 = A.fy * y * iz + A.cy - (double)m.y;
     cost += r0 * r0 + r1 * r1;
@@ -189,7 +178,7 @@ __device__ __forceinline__ void lin_obs(LinShared& S, const LinArgs& A, const do
 __device__ __forceinline__ bool point_block(const LinShared& S, const LinArgs& A, int p,
                                             double (&l)[6], double (&h)[3]) {
   double v00 = 0, v01 = 0, v02 = 0, v11 = 0, v12 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
-  const int o0 = S.te_obs[S.pt_te[p]], o1 = S.te_obs[S.pt_te[p + 1]];
+  const int o0 = S.img.te_obs[S.img.pt_te[p]], o1 = S.img.te_obs[S.img.pt_te[p + 1]];
   for (int o = o0; o < o1; ++o) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -228,7 +217,7 @@ __device__ __forceinline__ void lin_reduce(LinShared& S, const LinArgs& A, int n
     for (int e = 0; e < 18; ++e) W[e] = 0.0;
 #pragma unroll
     for (int e = 0; e < 6; ++e) g[e] = 0.0;
-    for (int o = S.te_obs[t]; o < S.te_obs[t + 1]; ++o) {
+    for (int o = S.img.te_obs[t]; o < S.img.te_obs[t + 1]; ++o) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const double rk = S.r[o][k];
@@ -264,8 +253,8 @@ __device__ __forceinline__ void lin_reduce(LinShared& S, const LinArgs& A, int n
 // cameras; zero otherwise (frozen landmarks leave the camera system).
 __device__ __forceinline__ void lin_eliminate(LinShared& S, int nte) {
   for (int t = threadIdx.x; t < nte; t += kLinThreads) {
-    const int p = S.te_pt[t];
-    const bool use = S.valid[p] && S.te_lcam[t] >= 0;
+    const int p = S.img.te_pt[t];
+    const bool use = S.valid[p] && S.img.te_lcam[t] >= 0;
     S.te_use[t] = use;
     if (!use) {
 #pragma unroll
@@ -273,7 +262,7 @@ __device__ __forceinline__ void lin_eliminate(LinShared& S, int nte) {
 #pragma unroll
       for (int e = 0; e < 6; ++e) S.bt[t][e] = 0.0;
       // frozen landmark: its observations leave U too (gc was formed from Jc already)
-      for (int o = S.te_obs[t]; o < S.te_obs[t + 1]; ++o)
+      for (int o = S.img.te_obs[t]; o < S.img.te_obs[t + 1]; ++o)
 #pragma unroll
         for (int e = 0; e < 12; ++e) S.Jc[o][e] = 0.0;
       continue;
@@ -313,20 +302,20 @@ __device__ __forceinline__ void chunk_linearize(LinShared& S, const LinArgs& A,
 __device__ __forceinline__ void chunk_backsub(LinShared& S, const LinArgs& A, int nob, int npt,
                                               int p0) {
   for (int o = threadIdx.x; o < nob; o += kLinThreads) {
-    const double* T = S.pose_o[S.acam[o]];
-    const int te = S.obs_te[o];
-    const int q = S.te_pt[te];
+    const double* T = S.pose_o[S.img.acam[o]];
+    const int te = S.img.obs_te[o];
+    const int q = S.img.te_pt[te];
     const double X0 = S.X[q][0], X1 = S.X[q][1], X2 = S.X[q][2];
     const double x = T[0] * X0 + T[1] * X1 + T[2] * X2 + T[9];
     const double y = T[3] * X0 + T[4] * X1 + T[5] * X2 + T[10];
     const double z = T[6] * X0 + T[7] * X1 + T[8] * X2 + T[11];
     const double iz = 1.0 / z;
-    const float2 m = S.uv[o];
+    const float2 m = reinterpret_cast<const float2*>(S.img.uv)[o];
     double r0 = A.fx * x * iz + A.cx - (double)m.x;
     double r1 = A.fy * y * iz + A.cy - (double)m.y;
     const double j00 = A.fx * iz, j02 = -A.fx * x * iz * iz;
     const double j11 = A.fy * iz, j12 = -A.fy * y * iz * iz;
-    const int lc = S.te_lcam[te];
+    const int lc = S.img.te_lcam[te];
     if (lc >= 0) {  // + Jc dc (rows of lin_obs's Jc)
       const double* d = S.dcw[lc];
       r0 += j00 * d[0] + j02 * d[2] + (j02 * y) * d[3] + (j00 * z - j02 * x) * d[4] - (j00 * y) * d[5];
@@ -427,96 +416,60 @@ struct Stamper {
 
 template <int MODE, bool kStamp>
 __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  // 3 per CU: <= 168 VGPRs
-  if (A.status && *A.status) return;  // a previous solve failed: state frozen
   __shared__ LinShared S;
   Stamper<kStamp> st;
   st.start();
   const int seg = blockIdx.x, tid = threadIdx.x;
-  const int nslots = A.seg_slot_off[seg + 1] - A.seg_slot_off[seg];
-  const int cam0 = A.seg_cam_off[seg];
-  const int ncams = A.seg_cam_off[seg + 1] - cam0;
+  // one load level: the status word, the segment header (uniform) and this thread's
+  // camera ids (fixed offsets in the header); then poses and the pending update
+  const int* SH = A.seg_hdr + (long)kSegHdr * seg;
+  const int4* SH4 = reinterpret_cast<const int4*>(SH);
+  const int16_t* SH16 = reinterpret_cast<const int16_t*>(SH);
+  const int stat = A.status ? *A.status : 0;
+  const int4 g0 = SH4[0], g1 = SH4[1];
+  int4 h0 = SH4[8], h1 = SH4[9], h2 = SH4[10], h3 = SH4[11];  // first chunk's header
+  const int i_acam = SH16[16 + min(tid / 12, kSegAllCams - 1)];
+  const int i_wcam = SH16[32 + min(tid / 6, kSegCams - 1)];
+  if (stat) return;  // a previous solve failed: state frozen
+  const int nslots = g0.x, slot_off = g0.y, cam0 = g0.z, ncams = g0.w, na = g1.x;
+  const int ch0 = g1.y, ch1 = g1.z;
+  static_assert(12 * kSegAllCams <= kLinThreads && 6 * kSegCams <= kLinThreads,
+                "one pose / update element per thread");
+  if (MODE & kBacksub)
+    if (tid < ncams * 6) S.dcw[tid / 6][tid % 6] = A.dc[6l * i_wcam + tid % 6];
+  if (tid < 12 * na) {  // poses of the segment's cameras, once per segment
+    const long g = 12l * i_acam + tid % 12;
+    S.pose_n[tid / 12][tid % 12] = A.pose_new[g];
+    if (MODE & kBacksub) S.pose_o[tid / 12][tid % 12] = A.pose_old[g];
+  }
   if (MODE & kAccum) {
     for (int e = tid; e < nslots * 36; e += kLinThreads) S.win[e] = 0.0;
     for (int e = tid; e < ncams * 6; e += kLinThreads) S.bwin[e] = 0.0;
   }
-  if (MODE & kBacksub)
-    for (int e = tid; e < ncams * 6; e += kLinThreads)
-      S.dcw[e / 6][e % 6] = A.dc[6l * A.segcam_f[cam0 + e / 6] + e % 6];
-  {  // poses of the segment's cameras, once per segment
-    const int a0 = A.seg_acam_off[seg], na = A.seg_acam_off[seg + 1] - a0;
-    for (int e = tid; e < 12 * na; e += kLinThreads) {
-      const long g = 12l * A.seg_acam[a0 + e / 12] + e % 12;
-      S.pose_n[e / 12][e % 12] = A.pose_new[g];
-      if (MODE & kBacksub) S.pose_o[e / 12][e % 12] = A.pose_old[g];
-    }
-  }
   double cost = 0.0;
   st.count(kPhSlots, nslots);
   st.count(kPhCams, ncams);
-  for (int ch = A.seg_chunk[seg]; ch < A.seg_chunk[seg + 1]; ++ch) {
-    // one uniform header load, then every list load of the chunk in flight at once
-    const int4 h0 = A.chunk_hdr[4l * ch], h1 = A.chunk_hdr[4l * ch + 1], h2 = A.chunk_hdr[4l * ch + 2],
-               h3 = A.chunk_hdr[4l * ch + 3];
-    const int ob0 = h0.x, nob = h0.y, te0 = h0.z, nte = h0.w, p0 = h1.x, npt = h1.y;
-    const int sb = h1.z, cb = h1.w, e0 = h2.x, e1 = h2.y, c0 = h2.z, c1 = h2.w, q0 = h3.x, q1 = h3.y;
+  for (int ch = ch0; ch < ch1; ++ch) {
+    // this chunk's header is in registers (segment header, or prefetched one chunk
+    // ahead); every list load of the chunk is in flight at once
+    const int chn = min(ch + 1, ch1 - 1);
+    const int4 n0 = A.chunk_hdr[4l * chn], n1 = A.chunk_hdr[4l * chn + 1], n2 = A.chunk_hdr[4l * chn + 2],
+               n3 = A.chunk_hdr[4l * chn + 3];
+    const int nob = h0.y, nte = h0.w, p0 = h1.x, npt = h1.y, e0 = h2.x, e1 = h2.y;
     st.count(kPhObs, nob);
     st.count(kPhTe, nte);
     st.count(kPhPts, npt);
     st.count(kPhPairs, e1 - e0);
-    // every staging load of this thread first (unconditional: an empty list reads its
-    // array's first element), then -- after the previous chunk is consumed -- the stores
-    const int i0 = tid, i1 = tid + kLinThreads;
-    auto ld = [&](const auto* src, const auto* base, int n, int i) {
-      return n > 0 ? src[min(i, n - 1)] : base[0];
-    };
-    const int v_obs_te = ld(A.obs_te + ob0, A.obs_te, nob, i0);
-    const int v_te_obs = ld(A.te_obs + te0, A.te_obs, nte + 1, i0);
-    const int v_te_pt = ld(A.te_pt + te0, A.te_pt, nte, i0);
-    const int v_te_lcam = ld(A.te_lcam + te0, A.te_lcam, nte, i0);
-    const int v_pt_te = ld(A.pt_te + p0, A.pt_te, npt + 1, i0);
-    const double v_x = ld(A.points + 3l * p0, A.points, 3 * npt, i0);
-    const int v_acam = ld(A.obs_acam + ob0, A.obs_acam, nob, i0);
-    const float v_uv = ld(&A.obs_uv[ob0].x, &A.obs_uv[0].x, 2 * nob, i0);
-    int v_slotp = 0, v_pair0 = 0, v_pair1 = 0, v_camp = 0, v_caml = 0, v_camop = 0, v_camol = 0,
-        v_dslot = 0;
-    if (MODE & kAccum) {
-      v_slotp = ld(A.slot_ptr + sb, A.slot_ptr, nslots + 1, i0);
-      v_pair0 = ld(A.pair_list + e0, A.pair_list, e1 - e0, i0);
-      v_pair1 = ld(A.pair_list + e0, A.pair_list, e1 - e0, i1);
-      v_camp = ld(A.cam_ptr + cb, A.cam_ptr, ncams + 1, i0);
-      v_caml = ld(A.cam_list + c0, A.cam_list, c1 - c0, i0);
-      v_camop = ld(A.camo_ptr + cb, A.camo_ptr, ncams + 1, i0);
-      v_camol = ld(A.camo_list + q0, A.camo_list, q1 - q0, i0);
-      v_dslot = ld(A.segcam_diag + cam0, A.segcam_diag, ncams, i0);
-    }
+    // staging: one 16-byte load of the chunk image and the chunk's landmark positions
+    // (state), both issued before the previous chunk is released
+    constexpr int kImgVec = (int)(sizeof(ChunkImg) / 16);
+    static_assert(kImgVec <= kLinThreads && 3 * kChunkPts <= kLinThreads, "one staging element per thread");
+    const uint4 v_img = reinterpret_cast<const uint4*>(A.chunk_img + ch)[min(tid, kImgVec - 1)];
+    const int i0 = tid;
+    const double v_x = A.points[3l * p0 + min(i0, max(3 * npt - 1, 0))];
     __syncthreads();  // previous chunk fully consumed
-    if (i0 < nob) {
-      S.obs_te[i0] = v_obs_te - te0;
-      S.acam[i0] = (uint8_t)v_acam;
-    }
-    if (i0 <= nte) S.te_obs[i0] = v_te_obs - ob0;
-    if (i0 < nte) {
-      S.te_pt[i0] = v_te_pt - p0;
-      S.te_lcam[i0] = v_te_lcam;
-    }
-    if (i0 <= npt) S.pt_te[i0] = v_pt_te - te0;
+    if (tid < kImgVec) reinterpret_cast<uint4*>(&S.img)[tid] = v_img;
     if (i0 < 3 * npt) (&S.X[0][0])[i0] = v_x;
-    if (i0 < 2 * nob) (&S.uv[0].x)[i0] = v_uv;
-    static_assert(3 * kChunkPts <= kLinThreads && 2 * kChunkObs <= kLinThreads &&
-                      kChunkTe < kLinThreads && kChunkPairs <= 2 * kLinThreads,
-                  "one staging element per thread (two for the pair list)");
-    if (MODE & kAccum) {
-      if (i0 <= nslots) S.slotp[i0] = v_slotp - e0;
-      if (i0 < e1 - e0) S.pairs[i0] = (uint16_t)v_pair0;
-      if (i1 < e1 - e0) S.pairs[i1] = (uint16_t)v_pair1;
-      if (i0 <= ncams) {
-        S.camp[i0] = v_camp - c0;
-        S.camop[i0] = v_camop - q0;
-      }
-      if (i0 < c1 - c0) S.caml[i0] = (uint8_t)v_caml;
-      if (i0 < q1 - q0) S.camol[i0] = (uint8_t)v_camol;
-      if (i0 < ncams) S.dslot[i0] = v_dslot;
-    }
     __syncthreads();
     st.mark(kPhLoad);
 
@@ -528,6 +481,10 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
 
     if (!(MODE & kAccum)) {
       lin_obs(S, A, S.pose_n, nob, cost);  // cost at the updated state
+      h0 = n0;
+      h1 = n1;
+      h2 = n2;
+      h3 = n3;
       continue;
     }
     lin_obs(S, A, S.pose_n, nob, cost);
@@ -553,7 +510,7 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
         const int idx = base + tid, item = idx / np, part = idx % np;
         const int s = item / 6, a = item - 6 * (item / 6);
         double out[6] = {0, 0, 0, 0, 0, 0};
-        const int e0 = item < items ? S.slotp[s] + part : 0, e1 = item < items ? S.slotp[s + 1] : 0;
+        const int e0 = item < items ? S.img.slotp[s] + part : 0, e1 = item < items ? S.img.slotp[s + 1] : 0;
         if (e0 < e1) {
           auto zrow = [&](int pr, double (&za)[3], double2 (&zy)[9]) {
             const double2* py = reinterpret_cast<const double2*>(S.Z[pr >> 8]);
@@ -571,7 +528,7 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
               out[c] -= za[0] * zf[3 * c] + za[1] * zf[3 * c + 1] + za[2] * zf[3 * c + 2];
           };
           const int n = (e1 - e0 + np - 1) / np;  // this part's pairs
-          auto pid = [&](int j) { return (int)S.pairs[e0 + min(j, n - 1) * np]; };
+          auto pid = [&](int j) { return (int)S.img.pairs[e0 + min(j, n - 1) * np]; };
           double zaA[3], zaB[3];
           double2 zyA[9], zyB[9];
           zrow(pid(0), zaA, zyA);
@@ -611,13 +568,13 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
         double out[6] = {0, 0, 0, 0, 0, 0};
         double acc = 0.0;
         if (item < items) {
-          const int q0 = S.camop[c] + part, q1 = S.camop[c + 1];
+          const int q0 = S.img.camop[c] + part, q1 = S.img.camop[c + 1];
           if (q1 > q0) {
             const int ql = q1 - 1;
-            int on = S.camol[q0];
+            int on = S.img.camol[q0];
             for (int q = q0; q < q1; q += np) {
               const int o = on;
-              on = S.camol[min(q + np, ql)];
+              on = S.img.camol[min(q + np, ql)];
               const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
               double j[12];
 #pragma unroll
@@ -631,13 +588,13 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
               for (int cc = 0; cc < 6; ++cc) out[cc] += ja0 * j[cc] + ja1 * j[6 + cc];
             }
           }
-          const int e0 = S.camp[c] + part, e1 = S.camp[c + 1];
+          const int e0 = S.img.camp[c] + part, e1 = S.img.camp[c + 1];
           if (e1 > e0) {
             const int el = e1 - 1;
-            int xn = S.caml[e0];
+            int xn = S.img.caml[e0];
             for (int e = e0; e < e1; e += np) {
               const int x = xn;
-              xn = S.caml[min(e + np, el)];
+              xn = S.img.caml[min(e + np, el)];
               acc += S.bt[x][a];
             }
           }
@@ -649,17 +606,21 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
         }
         if (item < items && part == 0) {
           S.bwin[6 * c + a] += acc;
-          double* w = &S.win[36 * S.dslot[c] + 6 * a];
+          double* w = &S.win[36 * S.img.dslot[c] + 6 * a];
 #pragma unroll
           for (int cc = 0; cc < 6; ++cc) w[cc] += out[cc];
         }
       }
     }
     st.mark(kPhSchurU);
+    h0 = n0;
+    h1 = n1;
+    h2 = n2;
+    h3 = n3;
   }
   __syncthreads();
   if (MODE & kAccum) {
-    double* dst = A.slab + 36l * A.seg_slot_off[seg];
+    double* dst = A.slab + 36l * slot_off;
     for (int e = tid; e < nslots * 36; e += kLinThreads) dst[e] = S.win[e];
     double* dstb = A.slab_b + 6l * cam0;
     for (int e = tid; e < ncams * 6; e += kLinThreads) dstb[e] = S.bwin[e];
@@ -1712,6 +1673,8 @@ class BAEngine {
     upload(d_chunk_slot_base_, P.chunk_slot_base, st);
     upload(d_chunk_cam_base_, P.chunk_cam_base, st);
     upload(d_chunk_hdr_, P.chunk_hdr, st);
+    upload(d_chunk_img_, P.chunk_img, st);
+    upload(d_seg_hdr_, P.seg_hdr, st);
     upload(d_seg_acam_off_, P.seg_acam_off, st);
     upload(d_seg_acam_, P.seg_acam, st);
     upload(d_obs_acam_, P.obs_acam, st);
@@ -1949,6 +1912,8 @@ class BAEngine {
     A.chunk_slot_base = d_chunk_slot_base_.as<int>();
     A.chunk_cam_base = d_chunk_cam_base_.as<int>();
     A.chunk_hdr = d_chunk_hdr_.as<int4>();
+    A.chunk_img = d_chunk_img_.as<ChunkImg>();
+    A.seg_hdr = d_seg_hdr_.as<int>();
     A.seg_acam_off = d_seg_acam_off_.as<int>();
     A.seg_acam = d_seg_acam_.as<int>();
     A.obs_acam = d_obs_acam_.as<uint8_t>();
@@ -2163,7 +2128,7 @@ class BAEngine {
   DevBuf d_solve2_tab_;
   DevBuf d_solve_tab_;
   DevBuf d_obs_uv_, d_obs_cam_, d_obs_te_, d_te_cam_, d_te_pt_, d_te_obs_, d_te_lcam_, d_pt_te_;
-  DevBuf d_chunk_obs_, d_chunk_te_, d_chunk_pt_, d_chunk_slot_base_, d_chunk_cam_base_, d_chunk_hdr_;
+  DevBuf d_chunk_obs_, d_chunk_te_, d_chunk_pt_, d_chunk_slot_base_, d_chunk_cam_base_, d_chunk_hdr_, d_seg_hdr_, d_chunk_img_;
   DevBuf d_seg_acam_off_, d_seg_acam_, d_obs_acam_;
   DevBuf d_slot_ptr_, d_pair_list_, d_cam_ptr_, d_cam_list_;
   DevBuf d_seg_chunk_, d_seg_slot_off_, d_seg_cam_off_;

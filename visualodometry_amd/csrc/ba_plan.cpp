@@ -36,6 +36,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
                        const int32_t* obs_cam, const float* obs_uv, int target_segments) {
   P = BAPlan();
   if (N < 1 || L < 0 || M < 0) return fmt("bad sizes n_poses=%ld n_points=%ld n_obs=%ld", N, L, M);
+  if (N > 32767) return fmt("n_poses=%ld exceeds the 32767 camera ids of a segment header", N);
   if (n_fixed < 0 || n_fixed > N) return fmt("bad n_fixed=%ld (n_poses=%ld)", n_fixed, N);
   if (point_ptr[0] != 0 || point_ptr[L] != M) return "point_ptr must start at 0 and end at n_obs";
   for (int p = 0; p < L; ++p)
@@ -277,6 +278,58 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       h[12] = P.camo_ptr[cb];
       h[13] = P.camo_ptr[cb + nc];
     }
+  }
+  // chunk LDS images
+  P.chunk_img.assign((size_t)std::max(nchunks, 1), ChunkImg());
+  for (size_t si = 0; si + 1 < P.seg_chunk.size(); ++si) {
+    const int ns = P.seg_slot_off[si + 1] - P.seg_slot_off[si];
+    const int nc = P.seg_cam_off[si + 1] - P.seg_cam_off[si];
+    const int cam0 = P.seg_cam_off[si];
+    for (int ch = P.seg_chunk[si]; ch < P.seg_chunk[si + 1]; ++ch) {
+      ChunkImg& g = P.chunk_img[ch];
+      const int32_t* h = &P.chunk_hdr[(size_t)ch * kChunkHdr];
+      const int ob0 = h[0], nob = h[1], te0 = h[2], nte = h[3], p0 = h[4], npt = h[5];
+      const int sb = h[6], cb = h[7], e0 = h[8], e1 = h[9], c0 = h[10], c1 = h[11], q0 = h[12], q1 = h[13];
+      for (int i = 0; i < nob; ++i) {
+        g.obs_te[i] = P.obs_te[ob0 + i] - te0;
+        g.uv[2 * i] = P.obs_uv[2 * (ob0 + i)];
+        g.uv[2 * i + 1] = P.obs_uv[2 * (ob0 + i) + 1];
+        g.acam[i] = P.obs_acam[ob0 + i];
+      }
+      for (int i = 0; i <= nte; ++i) g.te_obs[i] = P.te_obs[te0 + i] - ob0;
+      for (int i = 0; i < nte; ++i) {
+        g.te_pt[i] = P.te_pt[te0 + i] - p0;
+        g.te_lcam[i] = P.te_lcam[te0 + i];
+      }
+      for (int i = 0; i <= npt; ++i) g.pt_te[i] = P.pt_te[p0 + i] - te0;
+      for (int i = 0; i <= ns; ++i) g.slotp[i] = P.slot_ptr[sb + i] - e0;
+      for (int i = 0; i < e1 - e0; ++i) g.pairs[i] = P.pair_list[e0 + i];
+      for (int i = 0; i <= nc; ++i) {
+        g.camp[i] = P.cam_ptr[cb + i] - c0;
+        g.camop[i] = P.camo_ptr[cb + i] - q0;
+      }
+      for (int i = 0; i < c1 - c0; ++i) g.caml[i] = P.cam_list[c0 + i];
+      for (int i = 0; i < q1 - q0; ++i) g.camol[i] = P.camo_list[q0 + i];
+      for (int i = 0; i < nc; ++i) g.dslot[i] = P.segcam_diag[cam0 + i];
+    }
+  }
+  // segment headers (kSegHdr)
+  const int nseg = (int)P.seg_chunk.size() - 1;
+  P.seg_hdr.assign((size_t)std::max(nseg, 1) * kSegHdr, 0);
+  for (int si = 0; si < nseg; ++si) {
+    int32_t* h = &P.seg_hdr[(size_t)si * kSegHdr];
+    h[0] = P.seg_slot_off[si + 1] - P.seg_slot_off[si];
+    h[1] = P.seg_slot_off[si];
+    h[2] = P.seg_cam_off[si];
+    h[3] = P.seg_cam_off[si + 1] - P.seg_cam_off[si];
+    h[4] = P.seg_acam_off[si + 1] - P.seg_acam_off[si];
+    h[5] = P.seg_chunk[si];
+    h[6] = P.seg_chunk[si + 1];
+    int16_t* h16 = reinterpret_cast<int16_t*>(h);
+    for (int i = 0; i < h[4]; ++i) h16[16 + i] = (int16_t)P.seg_acam[P.seg_acam_off[si] + i];
+    for (int i = 0; i < h[3]; ++i) h16[32 + i] = (int16_t)P.segcam_f[P.seg_cam_off[si] + i];
+    if (h[6] > h[5])
+      std::copy(&P.chunk_hdr[(size_t)h[5] * kChunkHdr], &P.chunk_hdr[(size_t)(h[5] + 1) * kChunkHdr], h + 32);
   }
   if (P.segcam_diag.empty()) P.segcam_diag.push_back(0);
   return "";

@@ -34,8 +34,37 @@ constexpr int kChunkPts = VO_CHUNK_OBS / 2;
 constexpr int kChunkPairs = 8 * VO_CHUNK_OBS;  // camera-pair (x, y) entries of one chunk, staged in LDS
 constexpr int kSegSlots = 64;
 constexpr int kChunkHdr = 16;
+
 constexpr int kSegCams = 24;     // free (window) cameras of a segment
 constexpr int kSegAllCams = 16;  // all cameras its observations reference (poses staged in LDS)
+
+// Per segment, kSegHdr ints: [0] nslots [1] slot offset [2] first window camera [3] window
+// cameras [4] cameras seen [5] first chunk [6] end chunk [7] spare | [8..15] cameras seen
+// (16 x int16) | [16..27] free camera of each window camera (24 x int16) | [28..31] spare |
+// [32..47] the first chunk's header.  One uniform load level gives K1 every segment
+// offset; per-thread camera ids sit at fixed offsets (no dependent load).
+constexpr int kSegHdr = 48;
+
+// Per chunk, the static part of K1's LDS staging as one image (offsets already made
+// chunk-relative, types as K1 reads them): staging a chunk is one 16-byte load and one
+// LDS store per thread instead of a load per list.  Unused entries are zero.
+struct alignas(16) ChunkImg {
+  int32_t obs_te[kChunkObs];       // observation -> chunk track entry
+  int32_t te_obs[kChunkTe + 1];    // track entry -> first chunk observation
+  int32_t te_pt[kChunkTe];         // track entry -> chunk landmark
+  int32_t te_lcam[kChunkTe];       // track entry -> window camera, -1 if fixed
+  int32_t pt_te[kChunkPts + 1];    // landmark -> first chunk track entry
+  int32_t slotp[kSegSlots + 1];    // window slot -> first pair-list entry
+  int32_t camp[kSegCams + 1];      // window camera -> first track-entry list entry
+  int32_t camop[kSegCams + 1];     // window camera -> first observation list entry
+  int32_t dslot[kSegCams];         // window camera -> its diagonal slot
+  uint16_t pairs[kChunkPairs];     // (te_x | te_y << 8) by slot
+  uint8_t caml[kChunkTe];          // track entries by window camera
+  uint8_t camol[kChunkObs];        // observations by window camera
+  alignas(8) float uv[2 * kChunkObs];
+  uint8_t acam[kChunkObs];         // observation -> camera seen (pose index in LDS)
+};
+static_assert(sizeof(ChunkImg) % 16 == 0, "16-byte staging granules");
 
 struct SolveTableLayout {
   int diag = 0, off = 0, first = 0, step_ptr = 0, panel_i = 0, panel_blk = 0, item_ptr = 0,
@@ -80,6 +109,8 @@ struct BAPlan {
   // per chunk, kChunkHdr ints: every offset K1 needs to stage the chunk, so that one
   // (uniform) load precedes all list loads -- see ChunkHdr in ba.hip
   std::vector<int32_t> chunk_hdr;
+  std::vector<int32_t> seg_hdr;  // kSegHdr ints per segment
+  std::vector<ChunkImg> chunk_img;
   std::vector<int32_t> slot_ptr;   // per chunk: nslots(seg)+1 offsets into pair_list
   std::vector<uint16_t> pair_list; // (te_x_local | te_y_local << 8)
   std::vector<int32_t> cam_ptr;    // per chunk: ncams(seg)+1 offsets into cam_list
