@@ -1526,69 +1526,67 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
   __syncthreads();
   mark(kS3Trail);
 
-  // back substitution: x_k = L_kk^-T y'_k, then y'_j -= B^T x_k for the blocks B of row
-  // k (j < k) and/or of column k in the bottom rows (i > k), one lane per (block, column)
-  auto solve_k = [&](int k, double (&x)[6]) {
-    const double* o = kf + 36l * k;
-    double Lk[21], rk[6];
+  // One wave's back substitution over k = kb, kb + dir, ... (!= ke): x_k = L_kk^-T y'_k,
+  // then y'_i -= B^T x_k for the rows coupled to k -- up: block (k, j), j in [first[k], k);
+  // down: block (i, k) from the column list.  Every load of a step (L_kk, y'_k, each
+  // coupled row's y' and B column) is issued at once, so a step costs one LDS round
+  // trip; x_k is stored by six lanes, one 8-byte store each.
+  auto bs_run = [&](int kb, int ke, int dir, bool up, bool down) {
+    for (int k = kb; k != ke; k += dir) {
+      const int fk = t_first[k], okk = t_off[k];
+      const int nup = up ? k - fk : 0;
+      const int cb = down ? t_cptr[k - m] : 0, ndn = down ? t_cptr[k - m + 1] - cb : 0;
+      const int nt = 6 * (nup + ndn);
+      double Lk[21], rk[6], x[6];
+      {
+        const double* o = kf + 36l * k;
 #pragma unroll
-    for (int e = 0; e < 20; e += 2) {
-      const double2 v = reinterpret_cast<const double2*>(o)[e / 2];
-      Lk[e] = v.x;
-      Lk[e + 1] = v.y;
-    }
-    Lk[20] = o[20];
-    ld6g(o + 24, rk);
-    ld6g(o + 30, x);
-    bwd6(Lk, rk, x);
-    wave_sync<true>();
-    if (lane == 0) st6g(kf + 36l * k + 30, x);
-  };
-  auto scatter_row = [&](int k, const double (&x)[6]) {
-    const int fk = t_first[k], ok_ = t_off[k];
-    for (int t = lane; t < 6 * (k - fk); t += 64) {
-      const int jj = fk + t / 6, c = t % 6;
-      const double* B = Sm + 36l * (ok_ + jj - fk);
-      double a = 0.0;
+        for (int e = 0; e < 20; e += 2) {
+          const double2 v = reinterpret_cast<const double2*>(o)[e / 2];
+          Lk[e] = v.x;
+          Lk[e + 1] = v.y;
+        }
+        Lk[20] = o[20];
+        ld6g(o + 24, rk);
+        ld6g(o + 30, x);
+      }
+      // this lane's coupled (row, column c) pairs: t = lane, lane + 64
+      double yv[2], col[2][6];
+      int yrow[2];
 #pragma unroll
-      for (int r2 = 0; r2 < 6; ++r2) a += B[6 * r2 + c] * x[r2];
-      kf[36l * jj + 30 + c] -= a;
-    }
-  };
-  auto scatter_col = [&](int k, const double (&x)[6]) {
-    const int c0 = t_cptr[k - m], nc = t_cptr[k - m + 1] - c0;
-    for (int t = lane; t < 6 * nc; t += 64) {
-      const int i = t_colb[2 * (c0 + t / 6)], b = t_colb[2 * (c0 + t / 6) + 1], c = t % 6;
-      const double* B = Sm + 36l * b;
-      double a = 0.0;
+      for (int h = 0; h < 2; ++h) {
+        const int tt = lane + 64 * h, tq = min(tt, max(nt - 1, 0)) / 6, cc = tt % 6;
+        int row, blk;
+        if (tq < nup) {
+          row = fk + tq;
+          blk = okk + tq;  // block (k, fk + tq)
+        } else {
+          const int q = cb + tq - nup;
+          row = t_colb[2 * q];
+          blk = t_colb[2 * q + 1];  // block (row, k)
+        }
+        yrow[h] = tt < nt ? row : -1;
+        yv[h] = kf[36l * row + 30 + cc];
+        const double* B = Sm + 36l * blk + cc;
 #pragma unroll
-      for (int r2 = 0; r2 < 6; ++r2) a += B[6 * r2 + c] * x[r2];
-      kf[36l * i + 30 + c] -= a;
-    }
-  };
-  if (!s_fail && wave == 0)
-    for (int k = m + s - 1; k >= m; --k) {
-      double x[6];
-      solve_k(k, x);
-      scatter_row(k, x);
-      scatter_col(k, x);
+        for (int rr = 0; rr < 6; ++rr) col[h][rr] = B[6 * rr];
+      }
+      bwd6(Lk, rk, x);
+      if (lane < 6) kf[36l * k + 30 + lane] = pick<6>(x, lane);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (yrow[h] >= 0)
+          kf[36l * yrow[h] + 30 + (lane + 64 * h) % 6] =
+              yv[h] - (col[h][0] * x[0] + col[h][1] * x[1] + col[h][2] * x[2] + col[h][3] * x[3] +
+                       col[h][4] * x[4] + col[h][5] * x[5]);
       wave_sync<true>();
     }
+  };
+  if (!s_fail && wave == 0) bs_run(m + s - 1, m - 1, -1, true, true);
   __syncthreads();
-  if (!s_fail && wave == 0)
-    for (int k = m - 1; k >= 0; --k) {
-      double x[6];
-      solve_k(k, x);
-      scatter_row(k, x);
-      wave_sync<true>();
-    }
-  if (!s_fail && wave == 2)
-    for (int k = m + s; k < F; ++k) {
-      double x[6];
-      solve_k(k, x);
-      scatter_col(k, x);
-      wave_sync<true>();
-    }
+  // top rows descending (wave 0) and bottom rows ascending (wave 2) concurrently
+  if (!s_fail && wave == 0) bs_run(m - 1, -1, -1, true, false);
+  if (!s_fail && wave == 2) bs_run(m + s, F, 1, false, true);
   __syncthreads();
   mark(kS3Backsub);
   const bool failed = s_fail != 0;
