@@ -82,6 +82,8 @@ struct LinArgs {
   const int* chunk_cam_base;
   const int4* chunk_hdr;  // kChunkHdr ints per chunk (BAPlan::chunk_hdr)
   const ChunkImg* chunk_img;  // BAPlan::chunk_img
+  const int* slab_pos;        // BAPlan::slab_pos (window slot -> slab row)
+  const int* cam_pos;         // BAPlan::cam_pos (window camera -> rhs slab row)
   const int* seg_hdr;     // kSegHdr ints per segment (BAPlan::seg_hdr)
   const int* seg_acam_off;
   const int* seg_acam;
@@ -110,6 +112,8 @@ struct LinArgs {
 
 struct alignas(16) LinShared {
   ChunkImg img;  // static chunk lists (BAPlan::chunk_img), staged as one image
+  int spos[kSegSlots];  // slab row of each window slot
+  int cpos[kSegCams];   // rhs slab row of each window camera
   double win[kSegSlots * 36];
   double bwin[kSegCams * 6];
   double Jc[kChunkObs][12];
@@ -445,6 +449,8 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
   if (MODE & kAccum) {
     for (int e = tid; e < nslots * 36; e += kLinThreads) S.win[e] = 0.0;
     for (int e = tid; e < ncams * 6; e += kLinThreads) S.bwin[e] = 0.0;
+    if (tid < nslots) S.spos[tid] = A.slab_pos[slot_off + tid];
+    if (tid < ncams) S.cpos[tid] = A.cam_pos[cam0 + tid];
   }
   double cost = 0.0;
   st.count(kPhSlots, nslots);
@@ -619,11 +625,9 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
     h3 = n3;
   }
   __syncthreads();
-  if (MODE & kAccum) {
-    double* dst = A.slab + 36l * slot_off;
-    for (int e = tid; e < nslots * 36; e += kLinThreads) dst[e] = S.win[e];
-    double* dstb = A.slab_b + 6l * cam0;
-    for (int e = tid; e < ncams * 6; e += kLinThreads) dstb[e] = S.bwin[e];
+  if (MODE & kAccum) {  // window slots to their profile-major slab rows (K2 reads them in order)
+    for (int e = tid; e < nslots * 36; e += kLinThreads) A.slab[36l * S.spos[e / 36] + e % 36] = S.win[e];
+    for (int e = tid; e < ncams * 6; e += kLinThreads) A.slab_b[6l * S.cpos[e / 6] + e % 6] = S.bwin[e];
   }
   static_assert(kChunkTe * 18 >= kLinThreads, "cost reduction scratch");
   double* red = &S.Z[0][0];  // Z is dead after the last chunk: reuse it for the cost
@@ -655,26 +659,29 @@ struct ReduceArgs {
   const int* status;
 };
 
-// Sums slab entries src[k0 + part + j*stride] (entry e of each), j = 0, 1, ..., in fixed
-// order with 4 independent loads in flight.
+// Sums slab rows k0 + part + j*stride (entry e of each, rows of W doubles), j = 0, 1, ...,
+// in fixed order with 4 independent loads in flight.  K1 wrote each block's window slots
+// to consecutive rows in prof_src order, so this is the former gather, bit for bit.
 template <int W>
-__device__ __forceinline__ double sum_strided(const double* __restrict__ slab, const int* __restrict__ src,
-                                              int k0, int k1, int part, int stride, int e) {
+__device__ __forceinline__ double sum_rows(const double* __restrict__ slab, int k0, int k1, int part,
+                                           int stride, int e) {
   double acc = 0.0;
   int k = k0 + part;
   for (; k + 3 * stride < k1; k += 4 * stride) {
-    const int i0 = src[k], i1 = src[k + stride], i2 = src[k + 2 * stride], i3 = src[k + 3 * stride];
-    const double v0 = slab[(long)W * i0 + e], v1 = slab[(long)W * i1 + e];
-    const double v2 = slab[(long)W * i2 + e], v3 = slab[(long)W * i3 + e];
+    const double v0 = slab[(long)W * k + e], v1 = slab[(long)W * (k + stride) + e];
+    const double v2 = slab[(long)W * (k + 2 * stride) + e], v3 = slab[(long)W * (k + 3 * stride) + e];
     acc = (((acc + v0) + v1) + v2) + v3;
   }
-  for (; k < k1; k += stride) acc += slab[(long)W * src[k] + e];
+  for (; k < k1; k += stride) acc += slab[(long)W * k + e];
   return acc;
 }
 
-constexpr int kRedThreads = 256;
-constexpr int kRedSParts = 7;   // 7 x 36 lanes per S block
-constexpr int kRedBParts = 42;  // 42 x 6 lanes per rhs block
+#ifndef VO_RED_THREADS
+#define VO_RED_THREADS 256
+#endif
+constexpr int kRedThreads = VO_RED_THREADS;
+constexpr int kRedSParts = kRedThreads / 36;  // partial sums per S block entry
+constexpr int kRedBParts = kRedThreads / 6;   // partial sums per rhs entry
 
 // One workgroup per profile block: 7 strided partial sums per S entry and, on a
 // diagonal block, 42 per rhs entry of that camera, combined in fixed order (the
@@ -687,7 +694,7 @@ __global__ __launch_bounds__(kRedThreads) void ba_reduce_kernel(ReduceArgs A) {
     const bool diag = A.prof_diag[blk];
     const int k0 = A.prof_src_ptr[blk], k1 = A.prof_src_ptr[blk + 1];
     if (tid < kRedSParts * 36)
-      part[tid] = sum_strided<36>(A.slab, A.prof_src, k0, k1, tid / 36, kRedSParts, tid % 36);
+      part[tid] = sum_rows<36>(A.slab, k0, k1, tid / 36, kRedSParts, tid % 36);
     __syncthreads();
     if (tid < 36) {
       double acc = 0.0;
@@ -700,8 +707,7 @@ __global__ __launch_bounds__(kRedThreads) void ba_reduce_kernel(ReduceArgs A) {
     __syncthreads();
     const int f = A.prof_diag_cam[blk];
     if (tid < kRedBParts * 6)
-      part[tid] = sum_strided<6>(A.slab_b, A.camb_src, A.camb_ptr[f], A.camb_ptr[f + 1], tid / 6,
-                                 kRedBParts, tid % 6);
+      part[tid] = sum_rows<6>(A.slab_b, A.camb_ptr[f], A.camb_ptr[f + 1], tid / 6, kRedBParts, tid % 6);
     __syncthreads();
     if (tid < 6) {
       double acc = 0.0;
@@ -1672,6 +1678,8 @@ class BAEngine {
     upload(d_chunk_cam_base_, P.chunk_cam_base, st);
     upload(d_chunk_hdr_, P.chunk_hdr, st);
     upload(d_chunk_img_, P.chunk_img, st);
+    upload(d_slab_pos_, P.slab_pos, st);
+    upload(d_cam_pos_, P.cam_pos, st);
     upload(d_seg_hdr_, P.seg_hdr, st);
     upload(d_seg_acam_off_, P.seg_acam_off, st);
     upload(d_seg_acam_, P.seg_acam, st);
@@ -1911,6 +1919,8 @@ class BAEngine {
     A.chunk_cam_base = d_chunk_cam_base_.as<int>();
     A.chunk_hdr = d_chunk_hdr_.as<int4>();
     A.chunk_img = d_chunk_img_.as<ChunkImg>();
+    A.slab_pos = d_slab_pos_.as<int>();
+    A.cam_pos = d_cam_pos_.as<int>();
     A.seg_hdr = d_seg_hdr_.as<int>();
     A.seg_acam_off = d_seg_acam_off_.as<int>();
     A.seg_acam = d_seg_acam_.as<int>();
@@ -2126,7 +2136,7 @@ class BAEngine {
   DevBuf d_solve2_tab_;
   DevBuf d_solve_tab_;
   DevBuf d_obs_uv_, d_obs_cam_, d_obs_te_, d_te_cam_, d_te_pt_, d_te_obs_, d_te_lcam_, d_pt_te_;
-  DevBuf d_chunk_obs_, d_chunk_te_, d_chunk_pt_, d_chunk_slot_base_, d_chunk_cam_base_, d_chunk_hdr_, d_seg_hdr_, d_chunk_img_;
+  DevBuf d_chunk_obs_, d_chunk_te_, d_chunk_pt_, d_chunk_slot_base_, d_chunk_cam_base_, d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;
   DevBuf d_seg_acam_off_, d_seg_acam_, d_obs_acam_;
   DevBuf d_slot_ptr_, d_pair_list_, d_cam_ptr_, d_cam_list_;
   DevBuf d_seg_chunk_, d_seg_slot_off_, d_seg_cam_off_;

@@ -514,6 +514,10 @@ void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
     P.camb_src.insert(P.camb_src.end(), cb[f].begin(), cb[f].end());
     P.camb_ptr.push_back((int32_t)P.camb_src.size());
   }
+  P.slab_pos.assign(std::max<size_t>(P.slot_i.size(), 1), 0);
+  for (size_t k = 0; k < P.prof_src.size(); ++k) P.slab_pos[P.prof_src[k]] = (int32_t)k;
+  P.cam_pos.assign(std::max<size_t>(P.segcam_f.size(), 1), 0);
+  for (size_t k = 0; k < P.camb_src.size(); ++k) P.cam_pos[P.camb_src[k]] = (int32_t)k;
   if (P.prof_src.empty()) P.prof_src.push_back(0);
   if (P.camb_src.empty()) P.camb_src.push_back(0);
 

@@ -109,6 +109,10 @@ struct BAPlan {
   // per chunk, kChunkHdr ints: every offset K1 needs to stage the chunk, so that one
   // (uniform) load precedes all list loads -- see ChunkHdr in ba.hip
   std::vector<int32_t> chunk_hdr;
+  // slab positions: window slot s of the plan -> its row in the profile-major slab
+  // (the inverse of prof_src), window camera e -> its row in the camera-major rhs slab
+  // (the inverse of camb_src); K1 writes there so K2 reads contiguous rows
+  std::vector<int32_t> slab_pos, cam_pos;
   std::vector<int32_t> seg_hdr;  // kSegHdr ints per segment
   std::vector<ChunkImg> chunk_img;
   std::vector<int32_t> slot_ptr;   // per chunk: nslots(seg)+1 offsets into pair_list
