@@ -86,6 +86,7 @@ SIGNATURES = {
     "vo_profile_read": (_I, [_P, _PD, _PI64]),
     "vo_comm_unique_id": (_I, [C.c_char_p]),
     "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
+    "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
 }
 
 _lib = None
@@ -232,6 +233,13 @@ def comm_unique_id() -> bytes:
 
 def comm_init(ctx: "Context", nranks: int, rank: int, uid: bytes) -> None:
     check(ctx.lib.vo_comm_init(ctx.handle, nranks, rank, uid), "vo_comm_init")
+
+
+def comm_init_loopback(ctx: "Context", nranks: int, rank: int, group: bytes) -> None:
+    """Test stand-in for :func:`comm_init`: joins the in-process loopback group ``group``
+    (contexts of this process, one host thread each); see vo_comm_init_loopback."""
+    gid = C.create_string_buffer(group[:128].ljust(128, b"\0"), 128)
+    check(ctx.lib.vo_comm_init_loopback(ctx.handle, nranks, rank, gid), "vo_comm_init_loopback")
 
 
 def ptr(a, ctype):

@@ -72,6 +72,7 @@ int ba_stats(vo_ctx*, int64_t*, int);
 int ba_stamps(vo_ctx*, uint64_t*, int);
 void comm_unique_id(char out[128]);
 void comm_init(vo_ctx*, int, int, const char*);
+void comm_init_loopback(vo_ctx*, int, int, const char*);
 
 namespace {
 
@@ -373,6 +374,13 @@ int vo_comm_init(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
   return guarded([&] {
     vo::bind(ctx);
     vo::comm_init(ctx, nranks, rank, id);
+  });
+}
+
+int vo_comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
+  return guarded([&] {
+    vo::bind(ctx);
+    vo::comm_init_loopback(ctx, nranks, rank, id);
   });
 }
 

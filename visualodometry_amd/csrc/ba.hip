@@ -33,18 +33,17 @@
 #include <type_traits>
 #include <vector>
 
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <type_traits>
+
 #include "ba_plan.h"
 #include "vo_ctx.h"
 
 namespace vo {
-
-struct Comm {
-  ncclComm_t comm = nullptr;
-  int nranks = 1, rank = 0;
-  ~Comm() {
-    if (comm) ncclCommDestroy(comm);
-  }
-};
 
 #define VO_NCCL_CHECK(expr)                                                          \
   do {                                                                               \
@@ -55,6 +54,71 @@ struct Comm {
       throw ::vo::Error{VO_ERR_RCCL};                                                \
     }                                                                                \
   } while (0)
+
+// In-process loopback group (vo_comm_init_loopback): N contexts of one process, each
+// driven by its own host thread, stand in for N RCCL ranks so that the sharded BA path
+// can be tested on one device.  Each all-reduce copies to the host, meets the others at
+// a barrier and reduces in rank order (every member computes the identical result).
+struct LoopGroup {
+  int nranks = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::vector<char>> slot;
+  int arrived = 0;
+  long gen = 0;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const long g = gen;
+    if (++arrived == nranks) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+
+struct Comm {
+  ncclComm_t comm = nullptr;
+  std::shared_ptr<LoopGroup> loop;
+  int nranks = 1, rank = 0;
+  ~Comm() {
+    if (comm) ncclCommDestroy(comm);
+  }
+  // in-place all-reduce of n elements (int32 min or float64 sum) on the context stream
+  template <class T>
+  void allreduce(T* dbuf, size_t n, bool is_min, hipStream_t st);
+};
+
+template <class T>
+void Comm::allreduce(T* dbuf, size_t n, bool is_min, hipStream_t st) {
+  if (!loop) {
+    const ncclDataType_t ty = std::is_same<T, double>::value ? ncclFloat64 : ncclInt32;
+    VO_NCCL_CHECK(ncclAllReduce(dbuf, dbuf, n, ty, is_min ? ncclMin : ncclSum, comm, st));
+    return;
+  }
+  LoopGroup& G = *loop;
+  std::vector<T> mine(n);
+  VO_HIP_CHECK(hipMemcpyAsync(mine.data(), dbuf, n * sizeof(T), hipMemcpyDeviceToHost, st));
+  VO_HIP_CHECK(hipStreamSynchronize(st));
+  {
+    std::lock_guard<std::mutex> lk(G.mu);
+    G.slot[rank].assign(reinterpret_cast<const char*>(mine.data()),
+                        reinterpret_cast<const char*>(mine.data()) + n * sizeof(T));
+  }
+  G.barrier();
+  std::vector<T> out(n);
+  for (int r = 0; r < nranks; ++r) {
+    const T* v = reinterpret_cast<const T*>(G.slot[r].data());
+    for (size_t i = 0; i < n; ++i)
+      out[i] = r == 0 ? v[i] : is_min ? std::min(out[i], v[i]) : out[i] + v[i];
+  }
+  G.barrier();  // every member has read every slot
+  VO_HIP_CHECK(hipMemcpyAsync(dbuf, out.data(), n * sizeof(T), hipMemcpyHostToDevice, st));
+  VO_HIP_CHECK(hipStreamSynchronize(st));
+}
+
 
 namespace {
 
@@ -1649,8 +1713,7 @@ class BAEngine {
     if (ctx_->comm && ctx_->comm->nranks > 1 && !first.empty()) {
       DevBuf tmp;
       upload(tmp, first, ctx_->stream);
-      VO_NCCL_CHECK(ncclAllReduce(tmp.ptr, tmp.ptr, first.size(), ncclInt32, ncclMin,
-                                  ctx_->comm->comm, ctx_->stream));
+      ctx_->comm->allreduce(tmp.as<int32_t>(), first.size(), true, ctx_->stream);
       VO_HIP_CHECK(hipMemcpyAsync(first.data(), tmp.ptr, first.size() * 4, hipMemcpyDeviceToHost,
                                   ctx_->stream));
       VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
@@ -2005,8 +2068,7 @@ class BAEngine {
     ctx_->prof.end(ctx_->stream);
     VO_HIP_CHECK(hipGetLastError());
     if (ctx_->comm && ctx_->comm->nranks > 1)
-      VO_NCCL_CHECK(ncclAllReduce(d_sys_.ptr, d_sys_.ptr, sys_len_, ncclFloat64, ncclSum,
-                                  ctx_->comm->comm, ctx_->stream));
+      ctx_->comm->allreduce(d_sys_.as<double>(), sys_len_, false, ctx_->stream);
   }
 
   template <bool kL, bool kS>
@@ -2106,8 +2168,7 @@ class BAEngine {
     hipLaunchKernelGGL(ba_reduce_kernel, dim3(1), dim3(kRedThreads), 0, ctx_->stream, R);
     VO_HIP_CHECK(hipGetLastError());
     if (ctx_->comm && ctx_->comm->nranks > 1)
-      VO_NCCL_CHECK(ncclAllReduce(R.sys, R.sys, 1, ncclFloat64, ncclSum, ctx_->comm->comm,
-                                  ctx_->stream));
+      ctx_->comm->allreduce(R.sys, 1, false, ctx_->stream);
     VO_HIP_CHECK(hipMemcpyAsync(d_cost_slot, R.sys, 8, hipMemcpyDeviceToDevice, ctx_->stream));
   }
 
@@ -2199,6 +2260,30 @@ void comm_unique_id(char out[128]) {
   VO_NCCL_CHECK(ncclGetUniqueId(&id));
   static_assert(sizeof(id) == 128, "unexpected ncclUniqueId size");
   memcpy(out, &id, 128);
+}
+
+void comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
+  VO_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, VO_ERR_ARG, "vo_comm_init_loopback: bad rank");
+  static std::mutex reg_mu;
+  static std::map<std::string, std::weak_ptr<LoopGroup>> reg;
+  std::shared_ptr<LoopGroup> g;
+  {
+    std::lock_guard<std::mutex> lk(reg_mu);
+    const std::string key(id, 128);
+    g = reg[key].lock();
+    if (!g) {
+      g = std::make_shared<LoopGroup>();
+      g->nranks = nranks;
+      g->slot.resize(nranks);
+      reg[key] = g;
+    }
+  }
+  VO_REQUIRE(g->nranks == nranks, VO_ERR_ARG, "vo_comm_init_loopback: group size mismatch");
+  std::unique_ptr<Comm> c(new Comm);
+  c->nranks = nranks;
+  c->rank = rank;
+  c->loop = g;
+  ctx->comm = std::move(c);
 }
 
 void comm_init(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
