@@ -278,8 +278,12 @@ __device__ __forceinline__ bool point_block(const LinShared& S, const LinArgs& A
 }
 
 // R2: per track entry W, gc; per landmark V (+lambda), pivot-tested Cholesky, h.
+// The track-entry loop (threads [0, 128)) and the landmark loop (threads [128, 256)) are
+// independent and run on different waves concurrently.
 __device__ __forceinline__ void lin_reduce(LinShared& S, const LinArgs& A, int nte, int npt) {
-  for (int t = threadIdx.x; t < nte; t += kLinThreads) {
+  constexpr int kHalf = kLinThreads / 2;
+  static_assert(kChunkTe <= kHalf && kChunkPts <= kHalf, "one track entry / landmark per thread");
+  for (int t = threadIdx.x; t < nte && t < kHalf; t += kHalf) {
     double W[18], g[6];
 #pragma unroll
     for (int e = 0; e < 18; ++e) W[e] = 0.0;
@@ -305,7 +309,7 @@ __device__ __forceinline__ void lin_reduce(LinShared& S, const LinArgs& A, int n
 #pragma unroll
     for (int e = 0; e < 6; ++e) S.bt[t][e] = g[e];
   }
-  for (int p = threadIdx.x; p < npt; p += kLinThreads) {
+  for (int p = (int)threadIdx.x - kHalf; p >= 0 && p < npt; p += kHalf) {
     double l[6], h[3];
     const bool ok = point_block(S, A, p, l, h);
     S.valid[p] = ok;
