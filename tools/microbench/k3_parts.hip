@@ -140,6 +140,44 @@ __global__ __launch_bounds__(256) void parts(double* out, unsigned long long* cy
     }
     T1(6, 21);
   }
+  if (wave == 0) {
+    // 8. back-substitution step chain: L_kk (11 b128) + y'_k (3 b128) + per lane one
+    //    coupled row's y' (b64) and B column (6 b64), bwd6, x by 6 lanes, y' update; 28 steps
+    double* kf = lds + 4096;   // 36 doubles per k
+    double* Sm = lds + 6144;
+    T0();
+    for (int k = 27; k >= 0; --k) {
+      double Lk[21], rk[6], x[6];
+      const double* o = kf + 36 * (k & 31);
+      for (int e = 0; e < 20; e += 2) {
+        const double2 v = reinterpret_cast<const double2*>(o)[e / 2];
+        Lk[e] = v.x;
+        Lk[e + 1] = v.y;
+      }
+      Lk[20] = o[20];
+      for (int e = 0; e < 6; ++e) rk[e] = o[24 + e];
+      for (int e = 0; e < 6; ++e) x[e] = o[30 + e];
+      const int row = (k + 1 + lane / 6) & 31, cc = lane % 6;
+      const double yv = kf[36 * row + 30 + cc];
+      double col[6];
+      const double* B = Sm + 36 * ((k * 7 + lane / 6) & 31) + cc;
+      for (int rr = 0; rr < 6; ++rr) col[rr] = B[6 * rr];
+      for (int i = 5; i >= 0; --i) {
+        double s = x[i];
+        for (int mm = i + 1; mm < 6; ++mm) s -= Lk[P6(mm, i)] * x[mm];
+        x[i] = s * rk[i];
+      }
+      if (lane < 6) {
+        double v = 0.0;
+        for (int e = 0; e < 6; ++e) v = lane == e ? x[e] : v;
+        kf[36 * (k & 31) + 30 + lane] = v;
+      }
+      if (lane < 42)
+        kf[36 * row + 30 + cc] = yv - (col[0] * x[0] + col[1] * x[1] + col[2] * x[2] + col[3] * x[3] + col[4] * x[4] + col[5] * x[5]);
+      __builtin_amdgcn_wave_barrier();
+    }
+    T1(7, 28);
+  }
   // 6. barrier with four waves (no other work)
   __syncthreads();
   T0();
@@ -168,5 +206,6 @@ int main() {
   printf("task (16 b128 ld, 72 fma, st)  %llu cyc\n", h[4]);
   printf("__syncthreads, 4 waves         %llu cyc\n", h[5]);
   printf("panel part of a step (1 wave)  %llu cyc\n", h[6]);
+  printf("back-substitution step         %llu cyc\n", h[7]);
   return 0;
 }
