@@ -82,12 +82,17 @@ def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: 
     for _ in range(warmup):
         matcher.match_batch_device(a, b, out=out, ctx=ctx)
     matcher.synchronize(ctx)
-    _lib.profile_enable(ctx, True)
+    # the value: back-to-back calls with no per-kernel events
     t0 = time.perf_counter()
     for _ in range(calls):
         matcher.match_batch_device(a, b, out=out, ctx=ctx)
     matcher.synchronize(ctx)
     dt = time.perf_counter() - t0
+    # per-kernel averages: a second region with HIP events around every launch
+    _lib.profile_enable(ctx, True)
+    for _ in range(calls):
+        matcher.match_batch_device(a, b, out=out, ctx=ctx)
+    matcher.synchronize(ctx)
     prof = _lib.profile_read(ctx)
     _lib.profile_enable(ctx, False)
     # parity guard on frame pair 0 against the oracle (not timed)
