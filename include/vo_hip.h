@@ -159,8 +159,8 @@ int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n);
  * context stream.  vo_profile_read synchronises and returns, per kernel id,
  * the summed duration in ms and the launch count, then clears the records.
  * Ids: 0 ba_lin (K1), 1 ba_reduce (K2), 2 ba_solve (K3), 3 match_pack,
- *      4 match_i8 (MFMA sweep), 5 match_f32, 6 match_merge.               */
-#define VO_PROFILE_KERNELS 7
+ *      4 match_i8 (MFMA sweep), 5 match_f32, 6 match_merge, 7 triangulate. */
+#define VO_PROFILE_KERNELS 8
 int vo_profile_enable(vo_ctx* ctx, int on);
 int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
 
@@ -172,6 +172,25 @@ int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
  * layout usable [11] its rows per side m [12] separator rows s [13] bottom rows. 
  * Returns the count written, or VO_ERR_ARG (vo_last_error() says why). */
 int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* out, int n);
+
+/* ---- triangulation ----------------------------------- */
+/* Replaces triangulate_points (reference src/modules/frontend.py:115-148):
+ * cv2.triangulatePoints(P1, P2, pts1.T, pts2.T) (DLT + SVD per point, float32
+ * homogeneous output), dehomogenisation in float32, depth in camera 2 > min_depth
+ * (:134-135) and the cv2.projectPoints reprojection error in image 2 <
+ * max_reproj_err (:139-143).  P1, P2: 3x4 row-major K @ T_cw[:3, :] (as the caller
+ * forms them, :127-128); T_cw2: 3x4 row-major [R | t]; K: 3x3 row-major.  pts1,
+ * pts2: n x 2 float32.  Writes the float32 triangulation of EVERY point (n x 3) and
+ * its mask (n bytes, 1 = kept); the reference returns pts3d[mask], mask.
+ * Host buffers; synchronous. */
+int vo_triangulate(vo_ctx* ctx, const double* P1, const double* P2, const double* T_cw2,
+                   const double* K, const float* pts1, const float* pts2, int n,
+                   double min_depth, double max_reproj_err, float* pts3d_out, uint8_t* mask_out);
+/* Device-buffer variant (points and outputs in HBM; matrices on the host); enqueued
+ * on the context stream, returns without synchronising. */
+int vo_triangulate_async(vo_ctx* ctx, const double* P1, const double* P2, const double* T_cw2,
+                         const double* K, const float* d_pts1, const float* d_pts2, int n,
+                         double min_depth, double max_reproj_err, float* d_pts3d, uint8_t* d_mask);
 
 /* ---- multi-GPU (landmark sharding + RCCL all-reduce) --------------------- */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the caller. */

@@ -148,3 +148,39 @@ def test_env_switches(monkeypatch):
     monkeypatch.setenv("VO_AMD_BA", "1")
     c = get_config("kitti")
     assert c.extractor_type == "sift" and c.ba_enabled and c.sift_n_features == 4000
+
+
+def test_install_patches_triangulate_points_in_both_modules():
+    """``vo.py`` imports ``triangulate_points`` by name (vo.py:6): install() replaces it in
+    the frontend module and in the VO module; with ``triangulate_on_gpu`` off the
+    original runs, otherwise the HIP library (no CPU path)."""
+    import sys
+    import types
+
+    calls = []
+
+    def orig(T1, T2, p1, p2, K, cfg):
+        calls.append(1)
+        return "orig"
+
+    fm, vm = types.ModuleType("_fake_frontend_mod"), types.ModuleType("_fake_vo_mod")
+    fm.triangulate_points = orig
+    vm.triangulate_points = orig
+    F = type("F", (_Front,), {"__module__": fm.__name__})
+    V = type("V", (FakeVO,), {"__module__": vm.__name__})
+    sys.modules[fm.__name__], sys.modules[vm.__name__] = fm, vm
+    try:
+        hooks.install(F, V)
+        hooks.install(F, V)  # idempotent
+        for m in (fm, vm):
+            assert m.triangulate_points._vo_amd_wrapped is orig
+            off = types.SimpleNamespace(triangulate_on_gpu=False)
+            assert m.triangulate_points(None, None, [], [], None, off) == "orig"
+        on = types.SimpleNamespace(triangulate_on_gpu=True, min_depth=0.001, max_reproj_err=6.0)
+        # empty input returns before touching the device, as the reference does
+        pts, mask = fm.triangulate_points(np.eye(4), np.eye(4), np.zeros((0, 2)), np.zeros((0, 2)), np.eye(3), on)
+        assert pts.shape == (0, 3) and mask.shape == (0,)
+        with pytest.raises(_lib.VoError):  # a real call needs the HIP device: never a CPU path
+            fm.triangulate_points(np.eye(4), np.eye(4), np.ones((3, 2)), np.ones((3, 2)), np.eye(3), on)
+    finally:
+        del sys.modules[fm.__name__], sys.modules[vm.__name__]

@@ -85,6 +85,9 @@ SIGNATURES = {
     "vo_profile_enable": (_I, [_P, _I]),
     "vo_profile_read": (_I, [_P, _PD, _PI64]),
     "vo_comm_unique_id": (_I, [C.c_char_p]),
+    "vo_triangulate": (_I, [_P, _PD, _PD, _PD, _PD, _PF, _PF, _I, C.c_double, C.c_double, _PF,
+                            C.POINTER(C.c_uint8)]),
+    "vo_triangulate_async": (_I, [_P, _PD, _PD, _PD, _PD, _P, _P, _I, C.c_double, C.c_double, _P, _P]),
     "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
 }
@@ -207,7 +210,7 @@ class DeviceArray:
 
 
 KERNEL_NAMES = ["ba_lin", "ba_reduce", "ba_solve", "match_pack", "match_i8", "match_f32",
-                "match_merge"]
+                "match_merge", "triangulate"]
 
 
 def profile_enable(ctx: "Context", on: bool = True) -> None:

@@ -224,6 +224,43 @@ int vo_match_knn2(vo_ctx* ctx, const float* des0, int n0, const float* des1, int
   });
 }
 
+int vo_triangulate(vo_ctx* ctx, const double* P1, const double* P2, const double* T_cw2,
+                   const double* K, const float* pts1, const float* pts2, int n,
+                   double min_depth, double max_reproj_err, float* pts3d_out, uint8_t* mask_out) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(P1 && P2 && T_cw2 && K && n >= 0, VO_ERR_ARG, "vo_triangulate: bad arguments");
+    if (n == 0) return;
+    VO_REQUIRE(pts1 && pts2 && pts3d_out && mask_out, VO_ERR_ARG, "vo_triangulate: null arrays");
+    const size_t in = (size_t)n * 2 * sizeof(float), out3 = (size_t)n * 3 * sizeof(float);
+    ctx->match.tri.reserve(2 * in + out3 + (size_t)n + 64);
+    char* base = ctx->match.tri.as<char>();
+    float* d1 = reinterpret_cast<float*>(base);
+    float* d2 = reinterpret_cast<float*>(base + in);
+    float* d3 = reinterpret_cast<float*>(base + 2 * in);
+    uint8_t* dm = reinterpret_cast<uint8_t*>(base + 2 * in + out3);
+    hipStream_t st = ctx->stream;
+    VO_HIP_CHECK(hipMemcpyAsync(d1, pts1, in, hipMemcpyHostToDevice, st));
+    VO_HIP_CHECK(hipMemcpyAsync(d2, pts2, in, hipMemcpyHostToDevice, st));
+    vo::tri_run(ctx, P1, P2, T_cw2, K, d1, d2, n, min_depth, max_reproj_err, d3, dm);
+    VO_HIP_CHECK(hipMemcpyAsync(pts3d_out, d3, out3, hipMemcpyDeviceToHost, st));
+    VO_HIP_CHECK(hipMemcpyAsync(mask_out, dm, (size_t)n, hipMemcpyDeviceToHost, st));
+    VO_HIP_CHECK(hipStreamSynchronize(st));
+  });
+}
+
+int vo_triangulate_async(vo_ctx* ctx, const double* P1, const double* P2, const double* T_cw2,
+                         const double* K, const float* d_pts1, const float* d_pts2, int n,
+                         double min_depth, double max_reproj_err, float* d_pts3d, uint8_t* d_mask) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(P1 && P2 && T_cw2 && K && n >= 0, VO_ERR_ARG, "vo_triangulate_async: bad arguments");
+    if (n == 0) return;
+    VO_REQUIRE(d_pts1 && d_pts2 && d_pts3d && d_mask, VO_ERR_ARG, "vo_triangulate_async: null arrays");
+    vo::tri_run(ctx, P1, P2, T_cw2, K, d_pts1, d_pts2, n, min_depth, max_reproj_err, d_pts3d, d_mask);
+  });
+}
+
 int vo_match_batch_async(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
                          int n0, int n1, int dim, double ratio, int32_t* d_best) {
   return guarded([&] {

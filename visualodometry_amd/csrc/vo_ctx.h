@@ -18,6 +18,7 @@ struct MatchWorkspace {
   DevBuf top2;      // int32 (n0, 2) + float (n0, 2)
   DevBuf pairs;     // int32 (n0, 2) compacted pairs + count
   DevBuf flag;      // uint32: == gen when this call's descriptors are not 0..255 integers
+  DevBuf tri;       // triangulation staging: pts1, pts2, pts3d, mask
   uint32_t gen = 0;         // generation tag of the current call
   bool flag_fresh = true;   // flag not yet zeroed
 };
@@ -28,7 +29,7 @@ struct Comm;      // ba.hip (RCCL communicator)
 // Kernel ids of the event profiler (vo_profile_* in include/vo_hip.h).
 enum KernelId {
   kKBaLin = 0, kKBaReduce, kKBaSolve, kKMatchPack, kKMatchI8, kKMatchF32, kKMatchMerge,
-  kKCount
+  kKTriangulate, kKCount
 };
 
 // HIP-event timing of individual kernels on the context stream (off by default).
@@ -66,4 +67,8 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
                float* d_dist2);
 void compact_pairs(vo_ctx* ctx, const int32_t* d_best, int n0, int32_t* d_pairs,
                    int32_t* d_count);
+// Triangulation entry point (tri.hip): host matrices, device points.
+void tri_run(vo_ctx* ctx, const double* P1, const double* P2, const double* T_cw2, const double* K,
+             const float* d_pts1, const float* d_pts2, int n, double min_depth, double max_reproj_err,
+             float* d_pts3d, uint8_t* d_mask);
 }  // namespace vo

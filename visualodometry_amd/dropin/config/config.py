@@ -50,6 +50,7 @@ class VOConfig:
     ba_iters: int = 10  # Gauss-Newton iterations per keyframe
     ba_lambda: float = 1.0  # fixed Levenberg damping (identical in oracle and kernel)
     match_on_gpu: bool = True  # SIFT matching on the MI355X (knn-2 + ratio test)
+    triangulate_on_gpu: bool = True  # triangulate_points on the MI355X (DLT + filters)
 
 
 # dataset -> (overrides always applied, overrides applied when extractor is SIFT)

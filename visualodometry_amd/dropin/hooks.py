@@ -7,6 +7,9 @@ environment):
 * ``FeatureFrontend.match_frames`` (reference ``src/modules/frontend.py:78-113``),
   SIFT branch -> :func:`visualodometry_amd.matcher.match_knn2_ratio`.  The
   LightGlue branch (``:80-84``) is left to the original method.
+* ``triangulate_points`` (``src/modules/frontend.py:115-148``, imported by name into
+  ``vo.py``) -> :func:`visualodometry_amd.triangulate.triangulate_points` in both
+  modules (``cfg.triangulate_on_gpu``, default on).
 * ``VisualOdometry._create_keyframe`` (``src/modules/vo.py:252-288``) is wrapped:
   the original triangulates and rotates the keyframe, then
   :class:`KeyframeWindow` records the new keyframe and, if ``cfg.ba_enabled``,
@@ -211,12 +214,35 @@ def _wrap_match_frames(orig):
     return match_frames
 
 
+def _wrap_triangulate(orig):
+    from .. import triangulate
+
+    def triangulate_points(T_cw1, T_cw2, pts1, pts2, K, config):
+        if getattr(config, "triangulate_on_gpu", True):
+            return triangulate.triangulate_points(T_cw1, T_cw2, pts1, pts2, K, config)
+        return orig(T_cw1, T_cw2, pts1, pts2, K, config)
+
+    triangulate_points._vo_amd_wrapped = orig
+    return triangulate_points
+
+
 def install(frontend_cls=None, vo_cls=None) -> None:
-    """Patch the reference classes (imported from ``modules.*`` when not given). Idempotent."""
+    """Patch the reference classes (imported from ``modules.*`` when not given). Idempotent.
+
+    ``triangulate_points`` (``frontend.py:115``) is a module function that ``vo.py``
+    imports by name (``vo.py:6``), so it is replaced in both modules.
+    """
+    import sys
+
     if frontend_cls is None:
         from modules.frontend import FeatureFrontend as frontend_cls  # the reference's module
     if vo_cls is None:
         from modules.vo import VisualOdometry as vo_cls
+    for name in dict.fromkeys((frontend_cls.__module__, vo_cls.__module__)):
+        mod = sys.modules.get(name)
+        f = getattr(mod, "triangulate_points", None) if mod is not None else None
+        if f is not None and not hasattr(f, "_vo_amd_wrapped"):
+            mod.triangulate_points = _wrap_triangulate(f)
     if not hasattr(frontend_cls.match_frames, "_vo_amd_wrapped"):
         frontend_cls.match_frames = _wrap_match_frames(frontend_cls.match_frames)
     if not hasattr(vo_cls._create_keyframe, "_vo_amd_wrapped"):

@@ -234,3 +234,62 @@ def superpoint_like_pair(n0: int, n1: int, seed: int, dim: int = 256, overlap: f
     d0 /= np.linalg.norm(d0, axis=1, keepdims=True)
     d1 /= np.linalg.norm(d1, axis=1, keepdims=True)
     return d0.astype(np.float32), d1.astype(np.float32)
+
+
+def triangulation_case(n: int, seed: int, noise_px: float = 0.5, outlier_frac: float = 0.1,
+                       behind_frac: float = 0.05):
+    """Two-view triangulation input of the reference's shape (``vo.py:266-275``): KITTI K,
+    camera 2 one metre ahead of camera 1 with a small yaw, points in front of both, image
+    points float32 with ``noise_px`` noise.  A fraction of the correspondences are gross
+    outliers (camera 2 point moved by 30-100 px) and a fraction lie behind both cameras.
+    Cases sit far from the reference's thresholds (reprojection error << 2 px for
+    inliers, >> 10 px for outliers) so that masks are comparable exactly.
+
+    Returns (T_cw1, T_cw2, pts1 (n,2) f32, pts2 (n,2) f32, K, X (n,3) f64, kind (n,) int:
+    0 inlier, 1 outlier, 2 behind).
+    """
+    rng = np.random.default_rng(seed)
+    K = np.array([[718.856, 0.0, 607.1928], [0.0, 718.856, 185.2157], [0.0, 0.0, 1.0]])
+    T_cw1 = np.eye(4)
+    yaw = rng.normal(0.0, 0.02)
+    R = so3_exp(np.array([0.0, yaw, 0.0]))
+    C2 = np.array([rng.normal(0, 0.05), rng.normal(0, 0.02), 1.0])  # camera 2 centre (world)
+    T_cw2 = np.eye(4)
+    T_cw2[:3, :3] = R.T
+    T_cw2[:3, 3] = -R.T @ C2
+    kind = np.zeros(n, dtype=np.int64)
+    u = rng.permutation(n)
+    n_out, n_beh = int(outlier_frac * n), int(behind_frac * n)
+    kind[u[:n_out]] = 1
+    kind[u[n_out:n_out + n_beh]] = 2
+    depth = rng.uniform(5.0, 50.0, n)
+    # keep >= 150 px from the epipole of the forward motion (enough parallax)
+    e1 = K @ C2
+    e1 = e1[:2] / e1[2]
+    px = np.empty((n, 2))
+    filled = 0
+    while filled < n:
+        c = np.stack([rng.uniform(50, 1190, 4 * n), rng.uniform(30, 345, 4 * n)], 1)
+        c = c[np.linalg.norm(c - e1, axis=1) > 150.0][: n - filled]
+        px[filled:filled + len(c)] = c
+        filled += len(c)
+    ray = np.linalg.solve(K, np.concatenate([px, np.ones((n, 1))], 1).T).T
+    X = ray * depth[:, None]
+    X[kind == 2] *= -1.0  # behind both cameras
+    def proj(T, Xw):
+        Xc = (T[:3, :3] @ Xw.T).T + T[:3, 3]
+        q = (K @ Xc.T).T
+        return q[:, :2] / q[:, 2:3]
+    p1 = proj(T_cw1, X) + rng.normal(0, noise_px, (n, 2))
+    p2 = proj(T_cw2, X) + rng.normal(0, noise_px, (n, 2))
+    # outliers: moved 30-100 px across the epipolar line of their camera-1 point
+    R21 = T_cw2[:3, :3]
+    t21 = T_cw2[:3, 3]
+    tx = np.array([[0, -t21[2], t21[1]], [t21[2], 0, -t21[0]], [-t21[1], t21[0], 0]])
+    Ki = np.linalg.inv(K)
+    Fm = Ki.T @ tx @ R21 @ Ki
+    lines = (Fm @ np.concatenate([p1, np.ones((n, 1))], 1).T).T
+    nrm = lines[:, :2] / np.linalg.norm(lines[:, :2], axis=1, keepdims=True)
+    d = rng.uniform(30, 100, n) * np.where(rng.random(n) < 0.5, -1.0, 1.0)
+    p2[kind == 1] += (nrm * d[:, None])[kind == 1]
+    return T_cw1, T_cw2, p1.astype(np.float32), p2.astype(np.float32), K, X, kind
