@@ -14,6 +14,9 @@
  *                             .knnMatch(des0, des1, k=2) at :34/:101 and the
  *                             Lowe ratio test at :103-109)
  *   vo_match_knn2         <- the knnMatch(k=2) call alone, frontend.py:101
+ *   vo_triangulate        <- triangulate_points, src/modules/frontend.py:115-148
+ *   vo_pnp_ransac         <- cv2.solvePnPRansac in the tracking step,
+ *                            src/modules/vo.py:135-141
  *   vo_ba_*               <- new: the reference has no BA (pyceres/pycolmap
  *                            are declared in pyproject.toml:11-12 but never
  *                            imported).  Insertion point: the keyframe hook
@@ -159,8 +162,9 @@ int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n);
  * context stream.  vo_profile_read synchronises and returns, per kernel id,
  * the summed duration in ms and the launch count, then clears the records.
  * Ids: 0 ba_lin (K1), 1 ba_reduce (K2), 2 ba_solve (K3), 3 match_pack,
- *      4 match_i8 (MFMA sweep), 5 match_f32, 6 match_merge, 7 triangulate. */
-#define VO_PROFILE_KERNELS 8
+ *      4 match_i8 (MFMA sweep), 5 match_f32, 6 match_merge, 7 triangulate,
+ *      8 pnp_hyp, 9 pnp_score, 10 pnp_final. */
+#define VO_PROFILE_KERNELS 11
 int vo_profile_enable(vo_ctx* ctx, int on);
 int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
 
@@ -191,6 +195,35 @@ int vo_triangulate(vo_ctx* ctx, const double* P1, const double* P2, const double
 int vo_triangulate_async(vo_ctx* ctx, const double* P1, const double* P2, const double* T_cw2,
                          const double* K, const float* d_pts1, const float* d_pts2, int n,
                          double min_depth, double max_reproj_err, float* d_pts3d, uint8_t* d_mask);
+
+/* ---- PnP-RANSAC ------------------------------------- */
+/* Replaces cv2.solvePnPRansac(objpts, imgpts, K, None, reprojectionError=reproj_err,
+ * iterationsCount=iterations, confidence=confidence) with SOLVEPNP_ITERATIVE, as the
+ * tracking step calls it (reference src/modules/vo.py:135-141; map points and
+ * keypoints are float32, vo.py:130-134).  objpts: n x 3 float32, imgpts: n x 2
+ * float32, K: 3x3 row-major (no distortion).  RANSAC of OpenCV 4.12: cv::RNG((uint64)-1)
+ * subsets of 5 points, EPnP per subset, float32 squared reprojection error <=
+ * (float)(reproj_err^2), best = first model with the most inliers (> 4), the niters
+ * update of RANSACUpdateNumIters; then a Levenberg-Marquardt refinement on the
+ * inliers.  n == 5: EPnP on all points, all inliers.  n < 5: failure.
+ * Outputs: rvec (3), tvec (3) (the pose T_cw, Rodrigues vector), mask (n bytes, 1 =
+ * inlier of the best RANSAC model), *success_out = 1/0 (solvePnPRansac's retval).
+ * Host buffers; synchronous. */
+int vo_pnp_ransac(vo_ctx* ctx, const float* objpts, const float* imgpts, int n, const double* K,
+                  int iterations, double reproj_err, double confidence, double* rvec_out,
+                  double* tvec_out, uint8_t* mask_out, int32_t* success_out);
+/* Batch of frames, points in HBM: frame f owns points offsets[f]..offsets[f+1]-1 of
+ * d_objpts (total x 3) / d_imgpts (total x 2); offsets is a HOST array (batch+1,
+ * offsets[0] = 0).  d_pose: (batch, 6) float64 = rvec, tvec; d_mask: (total) bytes;
+ * d_status: (batch, 2) int32 = success, inlier count.  Enqueued on the context stream
+ * (the subsets are regenerated and uploaded only when the frame layout changes). */
+int vo_pnp_ransac_batch_async(vo_ctx* ctx, const float* d_objpts, const float* d_imgpts,
+                              const int32_t* offsets, int batch, const double* K, int iterations,
+                              double reproj_err, double confidence, double* d_pose, uint8_t* d_mask,
+                              int32_t* d_status);
+/* Host only: the RANSAC subsets the cv::RNG((uint64)-1) stream gives for `count` points
+ * (iterations x 5 int32), for parity tests. */
+int vo_pnp_subsets(int count, int iterations, int32_t* out);
 
 /* ---- multi-GPU (landmark sharding + RCCL all-reduce) --------------------- */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the caller. */

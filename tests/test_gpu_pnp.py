@@ -1,0 +1,105 @@
+"""GPU parity of PnP-RANSAC (vo_pnp_ransac) against the oracle (reference
+``src/modules/vo.py:135-141``; oracle/pnp_ref.py).
+
+Success flags and inlier masks (the reference uses the inlier indices,
+``vo.py:206-209``) must be identical; rvec/tvec within 1e-5 relative (the north_star
+floating-point tolerance).  The kernel keeps the oracle's operation order without FMA
+contraction, but the SVD rotations, hypot/log/pow/sin/cos and the order of the
+refinement's sums still round differently, so the synthetic cases keep the planted
+outliers far (>= 25 px) from the thresholds.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import pnp_ref as P
+from visualodometry_amd import _lib, pnp
+from visualodometry_amd.synthetic import pnp_case
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(got, ref):
+    ok, rv, tv, mask = got
+    rok, rrv, rtv, rmask, _ = ref
+    assert ok == rok
+    np.testing.assert_array_equal(mask, rmask)
+    if ok:
+        np.testing.assert_allclose(rv, rrv, rtol=1e-5, atol=1e-8)
+        np.testing.assert_allclose(tv, rtv, rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("n,seed", [(6, 0), (12, 1), (100, 2), (600, 3), (2000, 4)])
+@pytest.mark.parametrize("thr", [1.0, 2.0, 4.0])  # the reference's per-dataset pnp_reproj_err
+def test_matches_oracle(ctx, n, seed, thr):
+    X, uv, K, T, out = pnp_case(n, seed, noise_px=0.3, outlier_frac=0.2 if n > 12 else 0.0)
+    _check(pnp.pnp_ransac(X, uv, K, thr, ctx=ctx), P.solve_pnp_ransac(X, uv, K, thr))
+
+
+@pytest.mark.parametrize("iters,conf", [(1, 0.99), (20, 0.5), (300, 0.999)])
+def test_iterations_and_confidence(ctx, iters, conf):
+    X, uv, K, T, out = pnp_case(400, 9, noise_px=0.3, outlier_frac=0.45)
+    _check(pnp.pnp_ransac(X, uv, K, 2.0, iters, conf, ctx=ctx),
+           P.solve_pnp_ransac(X, uv, K, 2.0, iters, conf))
+
+
+def test_drop_in_signature(ctx):
+    X, uv, K, T, out = pnp_case(800, 5, noise_px=0.3, outlier_frac=0.3)
+    ok, rvec, tvec, inliers = pnp.solvePnPRansac(X, uv, K, None, reprojectionError=1.0, ctx=ctx)
+    rok, rrv, rtv, rmask, _ = P.solve_pnp_ransac(X, uv, K, 1.0)
+    assert ok and rvec.shape == (3, 1) and tvec.shape == (3, 1)
+    assert inliers.dtype == np.int32 and inliers.shape[1] == 1
+    np.testing.assert_array_equal(inliers[:, 0], np.flatnonzero(rmask))
+    assert not out[inliers[:, 0]].any()
+    np.testing.assert_allclose(rvec[:, 0], rrv, rtol=1e-5, atol=1e-8)
+    R = P.rodrigues_to_mat(rvec[:, 0][None])[0]
+    assert np.abs(R - T[:3, :3]).max() < 2e-3
+
+
+def test_edge_cases(ctx):
+    X, uv, K, T, _ = pnp_case(5, 4, noise_px=0.0, outlier_frac=0.0)
+    _check(pnp.pnp_ransac(X, uv, K, 1.0, ctx=ctx), P.solve_pnp_ransac(X, uv, K, 1.0))  # EPnP on all 5
+    ok, rv, tv, mask = pnp.pnp_ransac(X[:4], uv[:4], K, 1.0, ctx=ctx)
+    assert not ok and not mask.any()
+    ok, rv, tv, mask = pnp.pnp_ransac(np.zeros((0, 3)), np.zeros((0, 2)), K, 1.0, ctx=ctx)
+    assert not ok and mask.shape == (0,)
+    ok, rvec, tvec, inliers = pnp.solvePnPRansac(X[:3], uv[:3], K, None, ctx=ctx)
+    assert not ok and inliers is None
+    rng = np.random.default_rng(5)  # pure noise: no model has more than 4 inliers
+    Xn = (rng.uniform(-5, 5, (50, 3)) + [0, 0, 20]).astype(np.float32)
+    un = rng.uniform(0, 1000, (50, 2)).astype(np.float32)
+    _check(pnp.pnp_ransac(Xn, un, K, 0.5, ctx=ctx), P.solve_pnp_ransac(Xn, un, K, 0.5))
+    with pytest.raises(ValueError):
+        pnp.solvePnPRansac(X, uv, K, np.ones(5), ctx=ctx)
+
+
+def test_batch_matches_single_calls(ctx):
+    sizes = [0, 3, 5, 6, 250, 1000, 17, 600]
+    cases = [pnp_case(max(n, 1), 20 + i, noise_px=0.3, outlier_frac=0.25 if n > 20 else 0.0)
+             for i, n in enumerate(sizes)]
+    Xs = [c[0][:n] for c, n in zip(cases, sizes)]
+    Us = [c[1][:n] for c, n in zip(cases, sizes)]
+    K = cases[0][2]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    dX = _lib.DeviceArray.from_numpy(ctx, np.concatenate(Xs))
+    dU = _lib.DeviceArray.from_numpy(ctx, np.concatenate(Us))
+    dP = _lib.DeviceArray(ctx, (len(sizes), 6), np.float64)
+    dM = _lib.DeviceArray(ctx, (int(off[-1]),), np.uint8)
+    dS = _lib.DeviceArray(ctx, (len(sizes), 2), np.int32)
+    for rep in range(2):  # the second call reuses the cached subsets
+        pnp.pnp_ransac_device(dX, dU, off, K, 2.0, dP, dM, dS, ctx=ctx)
+        pose, mask, st = dP.numpy(), dM.numpy().astype(bool), dS.numpy()
+        for f, n in enumerate(sizes):
+            ref = P.solve_pnp_ransac(Xs[f], Us[f], K, 2.0)
+            got = (bool(st[f, 0]), pose[f, :3], pose[f, 3:], mask[off[f]:off[f + 1]])
+            _check(got, ref)
+            assert st[f, 1] == ref[3].sum()
+
+
+def test_large_frame_properties(ctx):
+    """20k correspondences: outliers rejected, pose recovered (size-independent checks)."""
+    X, uv, K, T, out = pnp_case(20_000, 31, noise_px=0.3, outlier_frac=0.3)
+    ok, rv, tv, mask = pnp.pnp_ransac(X, uv, K, 2.0, ctx=ctx)
+    assert ok and not (mask & out).any() and mask.sum() > 0.8 * (~out).sum()
+    R = P.rodrigues_to_mat(rv[None])[0]
+    assert np.abs(R - T[:3, :3]).max() < 1e-3 and np.abs(tv - T[:3, 3]).max() < 0.02

@@ -88,6 +88,9 @@ SIGNATURES = {
     "vo_triangulate": (_I, [_P, _PD, _PD, _PD, _PD, _PF, _PF, _I, C.c_double, C.c_double, _PF,
                             C.POINTER(C.c_uint8)]),
     "vo_triangulate_async": (_I, [_P, _PD, _PD, _PD, _PD, _P, _P, _I, C.c_double, C.c_double, _P, _P]),
+    "vo_pnp_ransac": (_I, [_P, _PF, _PF, _I, _PD, _I, _D, _D, _PD, _PD, C.POINTER(C.c_uint8), _PI32]),
+    "vo_pnp_ransac_batch_async": (_I, [_P, _P, _P, _PI32, _I, _PD, _I, _D, _D, _P, _P, _P]),
+    "vo_pnp_subsets": (_I, [_I, _I, _PI32]),
     "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
 }
@@ -210,7 +213,7 @@ class DeviceArray:
 
 
 KERNEL_NAMES = ["ba_lin", "ba_reduce", "ba_solve", "match_pack", "match_i8", "match_f32",
-                "match_merge", "triangulate"]
+                "match_merge", "triangulate", "pnp_hyp", "pnp_score", "pnp_final"]
 
 
 def profile_enable(ctx: "Context", on: bool = True) -> None:

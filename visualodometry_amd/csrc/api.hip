@@ -261,6 +261,67 @@ int vo_triangulate_async(vo_ctx* ctx, const double* P1, const double* P2, const 
   });
 }
 
+int vo_pnp_ransac(vo_ctx* ctx, const float* objpts, const float* imgpts, int n, const double* K,
+                  int iterations, double reproj_err, double confidence, double* rvec_out,
+                  double* tvec_out, uint8_t* mask_out, int32_t* success_out) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(K && n >= 0 && rvec_out && tvec_out && success_out, VO_ERR_ARG,
+               "vo_pnp_ransac: bad arguments");
+    VO_REQUIRE(n == 0 || (objpts && imgpts && mask_out), VO_ERR_ARG, "vo_pnp_ransac: null arrays");
+    *success_out = 0;
+    for (int k = 0; k < 3; ++k) rvec_out[k] = tvec_out[k] = 0.0;
+    if (n == 0) return;
+    const size_t bx = (size_t)n * 12, bu = (size_t)n * 8, bp = 64, bm = (size_t)n;
+    vo::DevBuf& st = ctx->pnp.stage;
+    st.reserve(bx + bu + bp + 16 + bm + 64);
+    char* base = st.as<char>();
+    float* dX = reinterpret_cast<float*>(base);
+    float* dU = reinterpret_cast<float*>(base + bx);
+    double* dP = reinterpret_cast<double*>(base + ((bx + bu + 15) & ~size_t(15)));
+    int32_t* dS = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(dP) + bp);
+    uint8_t* dM = reinterpret_cast<uint8_t*>(dS + 4);
+    hipStream_t s = ctx->stream;
+    VO_HIP_CHECK(hipMemcpyAsync(dX, objpts, bx, hipMemcpyHostToDevice, s));
+    VO_HIP_CHECK(hipMemcpyAsync(dU, imgpts, bu, hipMemcpyHostToDevice, s));
+    const int32_t offs[2] = {0, n};
+    vo::pnp_run(ctx, dX, dU, offs, 1, K, iterations, reproj_err, confidence, dP, dM, dS);
+    double pose[6];
+    int32_t status[2];
+    VO_HIP_CHECK(hipMemcpyAsync(pose, dP, sizeof pose, hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipMemcpyAsync(status, dS, sizeof status, hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipMemcpyAsync(mask_out, dM, bm, hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipStreamSynchronize(s));
+    for (int k = 0; k < 3; ++k) {
+      rvec_out[k] = pose[k];
+      tvec_out[k] = pose[3 + k];
+    }
+    *success_out = status[0];
+  });
+}
+
+int vo_pnp_ransac_batch_async(vo_ctx* ctx, const float* d_objpts, const float* d_imgpts,
+                              const int32_t* offsets, int batch, const double* K, int iterations,
+                              double reproj_err, double confidence, double* d_pose, uint8_t* d_mask,
+                              int32_t* d_status) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(offsets && K && batch >= 0 && d_pose && d_status, VO_ERR_ARG,
+               "vo_pnp_ransac_batch_async: bad arguments");
+    VO_REQUIRE(batch == 0 || offsets[batch] == 0 || (d_objpts && d_imgpts && d_mask), VO_ERR_ARG,
+               "vo_pnp_ransac_batch_async: null arrays");
+    vo::pnp_run(ctx, d_objpts, d_imgpts, offsets, batch, K, iterations, reproj_err, confidence, d_pose,
+                d_mask, d_status);
+  });
+}
+
+int vo_pnp_subsets(int count, int iterations, int32_t* out) {
+  return guarded([&] {
+    VO_REQUIRE(count > 5 && iterations >= 0 && out, VO_ERR_ARG, "vo_pnp_subsets: need count > 5");
+    vo::pnp_subsets(count, iterations, out);
+  });
+}
+
 int vo_match_batch_async(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
                          int n0, int n1, int dim, double ratio, int32_t* d_best) {
   return guarded([&] {

@@ -23,13 +23,24 @@ struct MatchWorkspace {
   bool flag_fresh = true;   // flag not yet zeroed
 };
 
+// PnP-RANSAC workspace (pnp.hip): RANSAC subsets cached per frame layout.
+struct PnpWorkspace {
+  DevBuf sub;     // int32 (batch, H, 5) subsets
+  DevBuf off;     // int32 (batch + 1) frame offsets
+  DevBuf models;  // double (batch, H, 16)
+  DevBuf counts;  // int32 (batch, H)
+  DevBuf stage;   // host-call staging: points, outputs
+  std::vector<int32_t> offsets;  // layout the cached subsets were made for
+  int H = 0;
+};
+
 class BAEngine;   // ba.hip
 struct Comm;      // ba.hip (RCCL communicator)
 
 // Kernel ids of the event profiler (vo_profile_* in include/vo_hip.h).
 enum KernelId {
   kKBaLin = 0, kKBaReduce, kKBaSolve, kKMatchPack, kKMatchI8, kKMatchF32, kKMatchMerge,
-  kKTriangulate, kKCount
+  kKTriangulate, kKPnpHyp, kKPnpScore, kKPnpFinal, kKCount
 };
 
 // HIP-event timing of individual kernels on the context stream (off by default).
@@ -53,6 +64,7 @@ struct vo_ctx {
   hipStream_t stream = nullptr;
   int num_cus = 0;
   vo::MatchWorkspace match;
+  vo::PnpWorkspace pnp;
   vo::Profiler prof;
   std::unique_ptr<vo::BAEngine> ba;
   std::unique_ptr<vo::Comm> comm;
@@ -71,4 +83,9 @@ void compact_pairs(vo_ctx* ctx, const int32_t* d_best, int n0, int32_t* d_pairs,
 void tri_run(vo_ctx* ctx, const double* P1, const double* P2, const double* T_cw2, const double* K,
              const float* d_pts1, const float* d_pts2, int n, double min_depth, double max_reproj_err,
              float* d_pts3d, uint8_t* d_mask);
+// PnP-RANSAC entry point (pnp.hip): device points, host offsets and K.
+void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* offsets, int batch,
+             const double* K, int iterations, double reproj_err, double confidence, double* d_pose,
+             uint8_t* d_mask, int32_t* d_status);
+void pnp_subsets(int count, int iters, int32_t* out);
 }  // namespace vo

@@ -293,3 +293,35 @@ def triangulation_case(n: int, seed: int, noise_px: float = 0.5, outlier_frac: f
     d = rng.uniform(30, 100, n) * np.where(rng.random(n) < 0.5, -1.0, 1.0)
     p2[kind == 1] += (nrm * d[:, None])[kind == 1]
     return T_cw1, T_cw2, p1.astype(np.float32), p2.astype(np.float32), K, X, kind
+
+
+def pnp_case(n: int, seed: int, noise_px: float = 0.3, outlier_frac: float = 0.25):
+    """A tracking-step input of the reference's shape (``vo.py:129-141``): ``n`` map points
+    (float32, as ``map_points`` holds them, ``vo.py:281``) seen by a camera with KITTI K
+    at a random pose, their float32 keypoints with ``noise_px`` noise, and a fraction of
+    gross outliers (keypoint moved 25-200 px).  Points sit 5-50 m in front of the camera.
+
+    Returns (X (n,3) f32, uv (n,2) f32, K, T_cw (4,4), is_outlier (n,) bool)."""
+    rng = np.random.default_rng(seed)
+    K = KITTI_K.copy()
+    W, H = KITTI_WH
+    px = np.stack([rng.uniform(20, W - 20, n), rng.uniform(20, H - 20, n)], 1)
+    depth = rng.uniform(5.0, 50.0, n)
+    ray = np.linalg.solve(K, np.concatenate([px, np.ones((n, 1))], 1).T).T
+    Xc = ray * depth[:, None]
+    R = so3_exp(rng.normal(0, 0.2, 3))
+    t = rng.normal(0, 2.0, 3)
+    T_cw = np.eye(4)
+    T_cw[:3, :3] = R
+    T_cw[:3, 3] = t
+    Xw = (R.T @ (Xc - t).T).T
+    X32 = Xw.astype(np.float32)
+    pc = (R @ X32.astype(np.float64).T).T + t
+    q = (K @ pc.T).T
+    uv = q[:, :2] / q[:, 2:3] + rng.normal(0, noise_px, (n, 2))
+    out = np.zeros(n, dtype=bool)
+    out[rng.permutation(n)[: int(outlier_frac * n)]] = True
+    ang = rng.uniform(0, 2 * np.pi, n)
+    mag = rng.uniform(25, 200, n)
+    uv[out] += np.stack([np.cos(ang), np.sin(ang)], 1)[out] * mag[out, None]
+    return X32, uv.astype(np.float32), K, T_cw, out
