@@ -51,6 +51,8 @@ class VOConfig:
     ba_lambda: float = 1.0  # fixed Levenberg damping (identical in oracle and kernel)
     match_on_gpu: bool = True  # SIFT matching on the MI355X (knn-2 + ratio test)
     triangulate_on_gpu: bool = True  # triangulate_points on the MI355X (DLT + filters)
+    pnp_on_gpu: bool = True  # cv2.solvePnPRansac of the tracking step on the MI355X
+    map_store_arrays: bool = True  # map_points as an id-indexed array store (MapStore)
 
 
 # dataset -> (overrides always applied, overrides applied when extractor is SIFT)

@@ -1,8 +1,8 @@
 """Runtime hooks that put the MI355X matcher and BA under the reference's VO loop.
 
-Nothing of the reference is copied: :func:`install` patches two methods of the
-reference's own classes once they are imported (cv2 etc. are the caller's
-environment):
+Nothing of the reference is copied: :func:`install` patches methods of the
+reference's own classes and names of its modules once they are imported (cv2 etc.
+are the caller's environment):
 
 * ``FeatureFrontend.match_frames`` (reference ``src/modules/frontend.py:78-113``),
   SIFT branch -> :func:`visualodometry_amd.matcher.match_knn2_ratio`.  The
@@ -31,6 +31,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from ..ba import BAResult, BAWindow, SlidingWindowBA
+from ..mapstore import MAX_POINTS, MapStore
 
 
 def _np(x) -> np.ndarray:
@@ -87,7 +88,10 @@ class KeyframeWindow:
             ids = [fr.ids] + fr.extra_ids
             u = np.concatenate(us)
             i = np.concatenate(ids)
-            keep = (i >= 0) & np.fromiter((int(x) in map_points for x in i), bool, i.size)
+            if isinstance(map_points, MapStore):
+                keep = map_points.contains(i)
+            else:
+                keep = (i >= 0) & np.fromiter((int(x) in map_points for x in i), bool, i.size)
             kf.append(np.full(int(keep.sum()), k, np.int32))
             uv.append(u[keep])
             pid.append(i[keep])
@@ -123,7 +127,10 @@ class KeyframeWindow:
         remap = -np.ones(ids.size, np.int64)
         remap[good] = np.arange(int(good.sum()))
         lm_ids = ids[good]
-        points = np.stack([np.asarray(map_points[int(i)], np.float64).reshape(3) for i in lm_ids])
+        if isinstance(map_points, MapStore):
+            points = map_points.gather(lm_ids).astype(np.float64)
+        else:
+            points = np.stack([np.asarray(map_points[int(i)], np.float64).reshape(3) for i in lm_ids])
         poses_cw = np.stack([np.linalg.inv(fr.T_wc) for fr in self.frames])
         w = BAWindow(poses_cw=poses_cw, points=points, obs_uv=uv.astype(np.float32), obs_cam=kf.astype(np.int32),
                      obs_pt=remap[inv].astype(np.int32), n_fixed=self.n_fixed)
@@ -132,6 +139,9 @@ class KeyframeWindow:
     def write_back(self, res: BAResult, lm_ids, map_points: dict) -> None:
         for fr, P in zip(self.frames, res.poses_cw):
             fr.T_wc = np.linalg.inv(P)
+        if isinstance(map_points, MapStore):
+            map_points.scatter(lm_ids, res.points)
+            return
         for i, X in zip(lm_ids, res.points):
             old = map_points[int(i)]
             map_points[int(i)] = np.asarray(X, dtype=np.asarray(old).dtype).reshape(np.shape(old))
@@ -191,15 +201,48 @@ def run_window_ba(vo, win: KeyframeWindow):
     return res
 
 
+def _use_map_store(vo) -> None:
+    if getattr(vo.cfg, "map_store_arrays", True) and not isinstance(vo.map_points, MapStore):
+        store = MapStore()
+        for pid, X in vo.map_points.items():
+            store[pid] = X
+        vo.map_points = store
+
+
+def _wrap_init(orig):
+    def __init__(self, *args, **kw):  # VisualOdometry(K, config), vo.py:9
+        orig(self, *args, **kw)
+        _PNP_ON_GPU[0] = bool(getattr(self.cfg, "pnp_on_gpu", True))
+        _use_map_store(self)
+
+    __init__._vo_amd_wrapped = orig
+    return __init__
+
+
+def _wrap_prune(orig):
+    def _prune_map(self):
+        if isinstance(self.map_points, MapStore):
+            self.map_points.prune_below(self.next_pt_id - MAX_POINTS)  # vo.py:38-47
+        else:
+            orig(self)
+
+    _prune_map._vo_amd_wrapped = orig
+    return _prune_map
+
+
 def _wrap_reset(orig):
     def _reset_system(self):
         orig(self)
+        _use_map_store(self)
         win = getattr(self, "_vo_amd_window", None)
         if win is not None:
             win.reset()
 
     _reset_system._vo_amd_wrapped = orig
     return _reset_system
+
+
+_PNP_ON_GPU = [True]  # set from the VO config at construction (cfg.pnp_on_gpu)
 
 
 def _wrap_match_frames(orig):
@@ -226,6 +269,25 @@ def _wrap_triangulate(orig):
     return triangulate_points
 
 
+class Cv2Proxy:
+    """Stands in for the ``cv2`` module inside ``modules.vo``: ``solvePnPRansac`` runs on
+    the MI355X, every other attribute is the real cv2's."""
+
+    def __init__(self, real, enabled=lambda: True):
+        self._vo_amd_real = real
+        self._enabled = enabled
+
+    def __getattr__(self, name):
+        return getattr(self._vo_amd_real, name)
+
+    def solvePnPRansac(self, objectPoints, imagePoints, cameraMatrix, distCoeffs=None, *args, **kw):
+        if self._enabled():
+            from .. import pnp
+
+            return pnp.solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, *args, **kw)
+        return self._vo_amd_real.solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, *args, **kw)
+
+
 def install(frontend_cls=None, vo_cls=None) -> None:
     """Patch the reference classes (imported from ``modules.*`` when not given). Idempotent.
 
@@ -249,3 +311,11 @@ def install(frontend_cls=None, vo_cls=None) -> None:
         vo_cls._create_keyframe = _wrap_create_keyframe(vo_cls._create_keyframe)
     if not hasattr(vo_cls._reset_system, "_vo_amd_wrapped"):
         vo_cls._reset_system = _wrap_reset(vo_cls._reset_system)
+    if not hasattr(vo_cls.__init__, "_vo_amd_wrapped"):
+        vo_cls.__init__ = _wrap_init(vo_cls.__init__)
+    if hasattr(vo_cls, "_prune_map") and not hasattr(vo_cls._prune_map, "_vo_amd_wrapped"):
+        vo_cls._prune_map = _wrap_prune(vo_cls._prune_map)
+    vo_mod = sys.modules.get(vo_cls.__module__)
+    real_cv2 = getattr(vo_mod, "cv2", None) if vo_mod is not None else None
+    if real_cv2 is not None and not isinstance(real_cv2, Cv2Proxy):
+        vo_mod.cv2 = Cv2Proxy(real_cv2, lambda: _PNP_ON_GPU[0])
