@@ -31,6 +31,11 @@ absent from this image, so this follows its published source, module by module):
 
 Build-defined, documented divergences (no OpenCV to pin against):
 
+* ``hypot(p, beta)`` in the Jacobi rotation is ``sqrt(p*p + beta*beta)``: only correctly
+  rounded operations, so the GPU reproduces it bit for bit (libm hypot differs in the last
+  ulp between libraries).  This matters: with 5 points ``M^T M`` has a two-dimensional
+  null space whose computed basis is decided by rounding, and one ulp in one rotation
+  changes individual EPnP hypotheses completely (tests/test_pnp_host_math.py).
 * ``cvSolve(L, rho, CV_SVD)`` (least squares on 6 x {3,4,5} systems) uses the same
   Householder ``qr_solve`` as the Gauss-Newton steps: the same least-squares solution
   for full column rank.
@@ -146,7 +151,7 @@ def jacobi_svd(At: np.ndarray, want_vt: bool = True):
                 with np.errstate(divide="ignore", invalid="ignore"):
                     p = p * 2
                     beta = a - b
-                    gamma = np.hypot(p, beta)
+                    gamma = np.sqrt(p * p + beta * beta)  # hypot from correctly rounded ops only
                     neg = beta < 0
                     delta = (gamma - beta) * 0.5
                     s_n = np.sqrt(delta / gamma)
@@ -440,7 +445,7 @@ def rodrigues_to_vec(R: np.ndarray) -> np.ndarray:
     s = np.sqrt((rx * rx + ry * ry + rz * rz) * 0.25)
     c = (R[:, 0, 0] + R[:, 1, 1] + R[:, 2, 2] - 1) * 0.5
     c = np.clip(c, -1.0, 1.0)
-    theta = np.arccos(c)
+    theta = np.array([math.acos(x) for x in c])  # libm acos, as OpenCV's std::acos
     out = np.empty((R.shape[0], 3))
     for b in range(R.shape[0]):
         if s[b] < 1e-5:
@@ -469,7 +474,8 @@ def rodrigues_to_mat(r: np.ndarray) -> np.ndarray:
     nz = theta >= DBL_EPSILON
     if nz.any():
         th = theta[nz]
-        c, s = np.cos(th), np.sin(th)
+        c = np.array([math.cos(x) for x in th])  # libm, as OpenCV
+        s = np.array([math.sin(x) for x in th])
         c1 = 1.0 - c
         u = r[nz] * (1.0 / th)[:, None]
         x, y, z = u[:, 0], u[:, 1], u[:, 2]

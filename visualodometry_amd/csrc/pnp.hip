@@ -25,6 +25,7 @@
 #include <cstring>
 #include <vector>
 
+#include "pnp_math.h"
 #include "vo_ctx.h"
 
 #pragma clang fp contract(off)
@@ -32,601 +33,13 @@
 namespace vo {
 namespace {
 
-constexpr int kPts = 5;            // EPnP model points (solvePnPRansac: model_points = 5)
-constexpr int kModel = 16;         // doubles per model: R (9), t (3), rvec (3), valid (1)
-constexpr double kDblEps = 2.220446049250313e-16;
-constexpr double kDblMin = 2.2250738585072014e-308;
-constexpr double kFltEps = 1.1920928955078125e-07;
-constexpr int kLmMaxIters = 20;
 // CvLevMarq's lambda = 10^lg, lg in [-16, 16] (decimal literals: correctly rounded)
 __constant__ double kPow10[33] = {1e-16, 1e-15, 1e-14, 1e-13, 1e-12, 1e-11, 1e-10, 1e-9, 1e-8, 1e-7, 1e-6,
                                   1e-5,  1e-4,  1e-3,  1e-2,  1e-1,  1e0,   1e1,   1e2,  1e3,  1e4,  1e5,
                                   1e6,   1e7,   1e8,   1e9,   1e10,  1e11,  1e12,  1e13, 1e14, 1e15, 1e16};
 
-struct Cam {
-  double fu, fv, uc, vc;
-};
 
-// ---------------------------------------------------------------- Jacobi SVD
-// JacobiSVDImpl_ (OpenCV core/lapack.cpp) on the rows of A (rotated in place): W[i] ends
-// as the norm of row i (unsorted); Vt accumulates the rotations when WANT_V.
-template <int N, int M, bool WANT_V>
-__device__ __forceinline__ void jacobi_rows(double (&A)[N][M], double (&W)[N], double (&Vt)[N][N]) {
-  constexpr double eps = 10.0 * kDblEps;
-  constexpr int max_sweeps = M > 30 ? M : 30;
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    double sd = 0.0;
-#pragma unroll
-    for (int k = 0; k < M; ++k) sd = sd + A[i][k] * A[i][k];
-    W[i] = sd;
-    if (WANT_V) {
-#pragma unroll
-      for (int k = 0; k < N; ++k) Vt[i][k] = i == k ? 1.0 : 0.0;
-    }
-  }
-  for (int sweep = 0; sweep < max_sweeps; ++sweep) {
-    bool changed = false;
-#pragma unroll
-    for (int i = 0; i < N - 1; ++i) {
-#pragma unroll
-      for (int j = i + 1; j < N; ++j) {
-        const double a = W[i], b = W[j];
-        double p = 0.0;
-#pragma unroll
-        for (int k = 0; k < M; ++k) p = p + A[i][k] * A[j][k];
-        if (!(fabs(p) <= eps * sqrt(a * b))) {
-          p = p * 2.0;
-          const double beta = a - b, gamma = hypot(p, beta);
-          double c, s;
-          if (beta < 0) {
-            const double delta = (gamma - beta) * 0.5;
-            s = sqrt(delta / gamma);
-            c = p / (gamma * s * 2.0);
-          } else {
-            c = sqrt((gamma + beta) / (gamma * 2.0));
-            s = p / (gamma * c * 2.0);
-          }
-          double na = 0.0, nb = 0.0;
-#pragma unroll
-          for (int k = 0; k < M; ++k) {
-            const double ai = A[i][k], aj = A[j][k];
-            const double t0 = c * ai + s * aj;
-            const double t1 = -s * ai + c * aj;
-            A[i][k] = t0;
-            A[j][k] = t1;
-            na = na + t0 * t0;
-            nb = nb + t1 * t1;
-          }
-          W[i] = na;
-          W[j] = nb;
-          changed = true;
-          if (WANT_V) {
-#pragma unroll
-            for (int k = 0; k < N; ++k) {
-              const double vi = Vt[i][k], vj = Vt[j][k];
-              Vt[i][k] = c * vi + s * vj;
-              Vt[j][k] = -s * vi + c * vj;
-            }
-          }
-        }
-      }
-    }
-    if (!changed) break;
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    double sd = 0.0;
-#pragma unroll
-    for (int k = 0; k < M; ++k) sd = sd + A[i][k] * A[i][k];
-    W[i] = sqrt(sd);
-  }
-}
-
-// Position of each singular value in the descending order (the selection sort of
-// JacobiSVDImpl_; equal values keep their index order, which the selection sort also
-// does unless three or more tie -- never for the non-degenerate inputs used here).
-template <int N>
-__device__ __forceinline__ void desc_rank(const double (&W)[N], int (&rank)[N]) {
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    int r = 0;
-#pragma unroll
-    for (int k = 0; k < N; ++k) r += (W[k] > W[i] || (k < i && W[k] == W[i])) ? 1 : 0;
-    rank[i] = r;
-  }
-}
-
-// ---------------------------------------------------------------- EPnP helpers
-__device__ __forceinline__ double dot3(const double* a, const double* b) {
-  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
-}
-
-// epnp::qr_solve (Householder least squares); X is left unchanged if a column is zero.
-template <int NR, int NC>
-__device__ __forceinline__ void qr_solve(double (&A)[NR][NC], double (&b)[NR], double (&X)[NC]) {
-  double A1[NC], A2[NC];
-#pragma unroll
-  for (int k = 0; k < NC; ++k) {
-    double eta = fabs(A[k][k]);
-#pragma unroll
-    for (int i = k + 1; i < NR; ++i) {
-      const double e = fabs(A[i][k]);
-      eta = eta < e ? e : eta;
-    }
-    if (eta == 0.0) return;
-    const double inv_eta = 1.0 / eta;
-    double sum2 = 0.0;
-#pragma unroll
-    for (int i = k; i < NR; ++i) {
-      A[i][k] = A[i][k] * inv_eta;
-      sum2 = sum2 + A[i][k] * A[i][k];
-    }
-    double sigma = sqrt(sum2);
-    if (A[k][k] < 0) sigma = -sigma;
-    A[k][k] = A[k][k] + sigma;
-    A1[k] = sigma * A[k][k];
-    A2[k] = -eta * sigma;
-#pragma unroll
-    for (int j = k + 1; j < NC; ++j) {
-      double s = 0.0;
-#pragma unroll
-      for (int i = k; i < NR; ++i) s = s + A[i][k] * A[i][j];
-      const double tau = s / A1[k];
-#pragma unroll
-      for (int i = k; i < NR; ++i) A[i][j] = A[i][j] - tau * A[i][k];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < NC; ++j) {
-    double tau = 0.0;
-#pragma unroll
-    for (int i = j; i < NR; ++i) tau = tau + A[i][j] * b[i];
-    tau = tau / A1[j];
-#pragma unroll
-    for (int i = j; i < NR; ++i) b[i] = b[i] - tau * A[i][j];
-  }
-  X[NC - 1] = b[NC - 1] / A2[NC - 1];
-#pragma unroll
-  for (int i = NC - 2; i >= 0; --i) {
-    double s = 0.0;
-#pragma unroll
-    for (int j = i + 1; j < NC; ++j) s = s + A[i][j] * X[j];
-    X[i] = (b[i] - s) / A2[i];
-  }
-}
-
-struct EpnpState {
-  double pw[kPts][3];
-  double us[kPts][2];
-  double alphas[kPts][4];
-  double cws[4][3];
-  double v[4][12];  // v[i] = ut row 11 - i (right singular vectors, smallest first)
-  double L[6][10];
-  double rho[6];
-};
-
-__device__ __forceinline__ void gauss_newton(const EpnpState& S, double (&betas)[4]) {
-  double x[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int it = 0; it < 5; ++it) {
-    double A[6][4], b[6];
-    const double b0 = betas[0], b1 = betas[1], b2 = betas[2], b3 = betas[3];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const double* l = S.L[i];
-      A[i][0] = 2 * l[0] * b0 + l[1] * b1 + l[3] * b2 + l[6] * b3;
-      A[i][1] = l[1] * b0 + 2 * l[2] * b1 + l[4] * b2 + l[7] * b3;
-      A[i][2] = l[3] * b0 + l[4] * b1 + 2 * l[5] * b2 + l[8] * b3;
-      A[i][3] = l[6] * b0 + l[7] * b1 + l[8] * b2 + 2 * l[9] * b3;
-      b[i] = S.rho[i] - (l[0] * b0 * b0 + l[1] * b0 * b1 + l[2] * b1 * b1 + l[3] * b0 * b2 +
-                         l[4] * b1 * b2 + l[5] * b2 * b2 + l[6] * b0 * b3 + l[7] * b1 * b3 +
-                         l[8] * b2 * b3 + l[9] * b3 * b3);
-    }
-    qr_solve<6, 4>(A, b, x);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) betas[i] = betas[i] + x[i];
-  }
-}
-
-// compute_R_and_t: control points in the camera frame, sign, Procrustes, mean pixel error.
-__device__ __forceinline__ double compute_R_and_t(const EpnpState& S, const Cam& K, const double (&betas)[4],
-                                                  double (&R)[3][3], double (&t)[3]) {
-  double ccs[4][3];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ccs[j][k] = 0.0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) ccs[j][k] = ccs[j][k] + betas[i] * S.v[i][3 * j + k];
-  double pcs[kPts][3];
-#pragma unroll
-  for (int p = 0; p < kPts; ++p)
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-      pcs[p][k] = S.alphas[p][0] * ccs[0][k] + S.alphas[p][1] * ccs[1][k] + S.alphas[p][2] * ccs[2][k] +
-                  S.alphas[p][3] * ccs[3][k];
-  if (pcs[0][2] < 0.0) {  // solve_for_sign
-#pragma unroll
-    for (int p = 0; p < kPts; ++p)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) pcs[p][k] = -pcs[p][k];
-  }
-  // estimate_R_and_t
-  double pc0[3] = {0.0, 0.0, 0.0}, pw0[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-  for (int p = 0; p < kPts; ++p)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      pc0[k] = pc0[k] + pcs[p][k];
-      pw0[k] = pw0[k] + S.pw[p][k];
-    }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    pc0[k] = pc0[k] / kPts;
-    pw0[k] = pw0[k] / kPts;
-  }
-  double abt[3][3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-#pragma unroll
-    for (int b = 0; b < 3; ++b) abt[a][b] = 0.0;
-#pragma unroll
-  for (int p = 0; p < kPts; ++p)
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) abt[a][b] = abt[a][b] + (pcs[p][a] - pc0[a]) * (S.pw[p][b] - pw0[b]);
-  // SVD of abt: JacobiSVD on the rows of abt^T; R = U V^T = sum_k u_k v_k^T
-  double At[3][3], W[3], Vt[3][3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-#pragma unroll
-    for (int b = 0; b < 3; ++b) At[a][b] = abt[b][a];
-  jacobi_rows<3, 3, true>(At, W, Vt);
-  double iw[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) iw[k] = 1.0 / W[k];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) s = s + (At[k][i] * iw[k]) * Vt[k][j];
-      R[i][j] = s;
-    }
-  const double det = R[0][0] * R[1][1] * R[2][2] + R[0][1] * R[1][2] * R[2][0] + R[0][2] * R[1][0] * R[2][1] -
-                     R[0][2] * R[1][1] * R[2][0] - R[0][1] * R[1][0] * R[2][2] - R[0][0] * R[1][2] * R[2][1];
-  if (det < 0) {
-    R[2][0] = -R[2][0];
-    R[2][1] = -R[2][1];
-    R[2][2] = -R[2][2];
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) t[k] = pc0[k] - dot3(R[k], pw0);
-  // reprojection_error
-  double err = 0.0;
-#pragma unroll
-  for (int p = 0; p < kPts; ++p) {
-    const double Xc = dot3(R[0], S.pw[p]) + t[0];
-    const double Yc = dot3(R[1], S.pw[p]) + t[1];
-    const double inv_Zc = 1.0 / (dot3(R[2], S.pw[p]) + t[2]);
-    const double ue = K.uc + K.fu * Xc * inv_Zc;
-    const double ve = K.vc + K.fv * Yc * inv_Zc;
-    const double du = S.us[p][0] - ue, dv = S.us[p][1] - ve;
-    err = err + sqrt(du * du + dv * dv);
-  }
-  return err / kPts;
-}
-
-// epnp::compute_pose on 5 correspondences.  Returns false for a degenerate subset.
-__device__ bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) {
-  bool ok = true;
-  // choose_control_points: centroid + PCA of the points
-  double c0[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-  for (int p = 0; p < kPts; ++p)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) c0[k] = c0[k] + S.pw[p][k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) c0[k] = c0[k] / kPts;
-  {
-    double P[3][3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) P[a][b] = 0.0;
-#pragma unroll
-    for (int p = 0; p < kPts; ++p) {
-      double d[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) d[k] = S.pw[p][k] - c0[k];
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) P[a][b] = P[a][b] + d[a] * d[b];
-    }
-    double At[3][3], W[3], dummy[3][3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) At[a][b] = P[b][a];
-    jacobi_rows<3, 3, false>(At, W, dummy);
-    int rk[3];
-    desc_rank<3>(W, rk);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) S.cws[0][k] = c0[k];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      ok &= W[i] > kDblMin;
-      const double s = 1.0 / W[i];
-      const double kk = sqrt(W[i] / kPts);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        double val = c0[k] + kk * (At[i][k] * s);
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          if (rk[i] == q) S.cws[q + 1][k] = val;
-      }
-    }
-  }
-  // compute_barycentric_coordinates: alphas = CC^-1 (p - c0), CC^-1 from its SVD
-  {
-    double At[3][3], W[3], Vt[3][3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 1; j < 4; ++j) At[j - 1][i] = S.cws[j][i] - S.cws[0][i];  // rows of CC^T
-    jacobi_rows<3, 3, true>(At, W, Vt);
-    double iw[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      ok &= W[k] > kDblMin;
-      iw[k] = 1.0 / W[k];
-    }
-    double ci[3][3];  // CC^-1 = V diag(1/w) U^T
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        double s = 0.0;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) s = s + Vt[k][i] * iw[k] * (At[k][j] * iw[k]);
-        ci[i][j] = s;
-      }
-#pragma unroll
-    for (int p = 0; p < kPts; ++p) {
-      const double d0 = S.pw[p][0] - S.cws[0][0], d1 = S.pw[p][1] - S.cws[0][1], d2 = S.pw[p][2] - S.cws[0][2];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) S.alphas[p][1 + j] = ci[j][0] * d0 + ci[j][1] * d1 + ci[j][2] * d2;
-      S.alphas[p][0] = 1.0 - S.alphas[p][1] - S.alphas[p][2] - S.alphas[p][3];
-    }
-  }
-  // M (2n x 12), M^T M, its four smallest right singular vectors
-  {
-    double A[12][12];
-#pragma unroll
-    for (int a = 0; a < 12; ++a)
-#pragma unroll
-      for (int b = 0; b < 12; ++b) A[a][b] = 0.0;
-#pragma unroll
-    for (int p = 0; p < kPts; ++p) {
-      double m1[12], m2[12];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const double al = S.alphas[p][c];
-        m1[3 * c] = al * K.fu;
-        m1[3 * c + 1] = 0.0;
-        m1[3 * c + 2] = al * (K.uc - S.us[p][0]);
-        m2[3 * c] = 0.0;
-        m2[3 * c + 1] = al * K.fv;
-        m2[3 * c + 2] = al * (K.vc - S.us[p][1]);
-      }
-#pragma unroll
-      for (int a = 0; a < 12; ++a)
-#pragma unroll
-        for (int b = 0; b < 12; ++b) A[a][b] = A[a][b] + m1[a] * m1[b];
-#pragma unroll
-      for (int a = 0; a < 12; ++a)
-#pragma unroll
-        for (int b = 0; b < 12; ++b) A[a][b] = A[a][b] + m2[a] * m2[b];
-    }
-    double W[12], dummy[12][12];
-    jacobi_rows<12, 12, false>(A, W, dummy);  // M^T M is symmetric: its rows are A^T's
-    int rk[12];
-    desc_rank<12>(W, rk);
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      ok &= W[i] > kDblMin;
-      const double s = 1.0 / W[i];
-#pragma unroll
-      for (int k = 0; k < 12; ++k) {
-        const double val = A[i][k] * s;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (rk[i] == 11 - q) S.v[q][k] = val;
-      }
-    }
-  }
-  // compute_L_6x10, compute_rho
-  {
-    constexpr int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
-    double dv[4][6][3];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dv[i][j][k] = S.v[i][3 * pa[j] + k] - S.v[i][3 * pb[j] + k];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      double* row = S.L[i];
-      row[0] = dot3(dv[0][i], dv[0][i]);
-      row[1] = 2.0 * dot3(dv[0][i], dv[1][i]);
-      row[2] = dot3(dv[1][i], dv[1][i]);
-      row[3] = 2.0 * dot3(dv[0][i], dv[2][i]);
-      row[4] = 2.0 * dot3(dv[1][i], dv[2][i]);
-      row[5] = dot3(dv[2][i], dv[2][i]);
-      row[6] = 2.0 * dot3(dv[0][i], dv[3][i]);
-      row[7] = 2.0 * dot3(dv[1][i], dv[3][i]);
-      row[8] = 2.0 * dot3(dv[2][i], dv[3][i]);
-      row[9] = dot3(dv[3][i], dv[3][i]);
-      double e[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) e[k] = S.cws[pa[i]][k] - S.cws[pb[i]][k];
-      S.rho[i] = dot3(e, e);
-    }
-  }
-  // three beta approximations, each refined by Gauss-Newton; keep the lowest error
-  double bestR[3][3], bestt[3], best_err = 0.0;
-  for (int kind = 1; kind <= 3; ++kind) {
-    double betas[4] = {0.0, 0.0, 0.0, 0.0};
-    double rho[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) rho[i] = S.rho[i];
-    if (kind == 1) {  // [B11 B12 B13 B14]
-      double A[6][4], x[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        A[i][0] = S.L[i][0];
-        A[i][1] = S.L[i][1];
-        A[i][2] = S.L[i][3];
-        A[i][3] = S.L[i][6];
-      }
-      qr_solve<6, 4>(A, rho, x);
-      if (x[0] < 0) {
-        betas[0] = sqrt(-x[0]);
-        betas[1] = -x[1] / betas[0];
-        betas[2] = -x[2] / betas[0];
-        betas[3] = -x[3] / betas[0];
-      } else {
-        betas[0] = sqrt(x[0]);
-        betas[1] = x[1] / betas[0];
-        betas[2] = x[2] / betas[0];
-        betas[3] = x[3] / betas[0];
-      }
-    } else if (kind == 2) {  // [B11 B12 B22]
-      double A[6][3], x[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) A[i][c] = S.L[i][c];
-      qr_solve<6, 3>(A, rho, x);
-      if (x[0] < 0) {
-        betas[0] = sqrt(-x[0]);
-        betas[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
-      } else {
-        betas[0] = sqrt(x[0]);
-        betas[1] = (x[2] > 0) ? sqrt(x[2]) : 0.0;
-      }
-      if (x[1] < 0) betas[0] = -betas[0];
-    } else {  // [B11 B12 B22 B13 B23]
-      double A[6][5], x[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int c = 0; c < 5; ++c) A[i][c] = S.L[i][c];
-      qr_solve<6, 5>(A, rho, x);
-      if (x[0] < 0) {
-        betas[0] = sqrt(-x[0]);
-        betas[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
-      } else {
-        betas[0] = sqrt(x[0]);
-        betas[1] = (x[2] > 0) ? sqrt(x[2]) : 0.0;
-      }
-      if (x[1] < 0) betas[0] = -betas[0];
-      betas[2] = x[3] / betas[0];
-    }
-    gauss_newton(S, betas);
-    double Rk[3][3], tk[3];
-    const double e = compute_R_and_t(S, K, betas, Rk, tk);
-    if (kind == 1 || e < best_err) {
-      best_err = e;
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        bestt[a] = tk[a];
-#pragma unroll
-        for (int b = 0; b < 3; ++b) bestR[a][b] = Rk[a][b];
-      }
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    t[a] = bestt[a];
-    ok &= isfinite(t[a]);
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      R[a][b] = bestR[a][b];
-      ok &= isfinite(R[a][b]);
-    }
-  }
-  return ok;
-}
-
-// ---------------------------------------------------------------- Rodrigues
-// Matrix -> vector (calibration.cpp); R's columns are first scaled to unit norm, which is
-// what OpenCV's U Vt re-orthonormalisation does to an already orthonormal R.
-__device__ void rodrigues_to_vec(const double (&Rin)[3][3], double (&r)[3]) {
-  double R[3][3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const double nrm = sqrt(Rin[0][j] * Rin[0][j] + Rin[1][j] * Rin[1][j] + Rin[2][j] * Rin[2][j]);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) R[i][j] = Rin[i][j] / nrm;
-  }
-  const double rx = R[2][1] - R[1][2], ry = R[0][2] - R[2][0], rz = R[1][0] - R[0][1];
-  const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
-  double c = (R[0][0] + R[1][1] + R[2][2] - 1) * 0.5;
-  c = c > 1. ? 1. : c < -1. ? -1. : c;
-  const double theta = acos(c);
-  if (s < 1e-5) {
-    if (c > 0) {
-      r[0] = r[1] = r[2] = 0.0;
-    } else {
-      double t = (R[0][0] + 1) * 0.5;
-      double r0 = sqrt(t > 0. ? t : 0.);
-      t = (R[1][1] + 1) * 0.5;
-      double r1 = sqrt(t > 0. ? t : 0.) * (R[0][1] < 0 ? -1. : 1.);
-      t = (R[2][2] + 1) * 0.5;
-      double r2 = sqrt(t > 0. ? t : 0.) * (R[0][2] < 0 ? -1. : 1.);
-      if (fabs(r0) < fabs(r1) && fabs(r0) < fabs(r2) && (R[1][2] > 0) != (r1 * r2 > 0)) r2 = -r2;
-      const double th = theta / sqrt(r0 * r0 + r1 * r1 + r2 * r2);
-      r[0] = r0 * th;
-      r[1] = r1 * th;
-      r[2] = r2 * th;
-    }
-  } else {
-    double vth = 1 / (2 * s);
-    vth = vth * theta;
-    r[0] = rx * vth;
-    r[1] = ry * vth;
-    r[2] = rz * vth;
-  }
-}
-
-__device__ void rodrigues_to_mat(const double (&r)[3], double (&R)[3][3]) {
-  const double theta = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
-  if (theta < kDblEps) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) R[i][j] = i == j ? 1.0 : 0.0;
-    return;
-  }
-  const double c = cos(theta), s = sin(theta), c1 = 1.0 - c;
-  const double it = 1.0 / theta;
-  const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
-  const double rrt[3][3] = {{x * x, x * y, x * z}, {x * y, y * y, y * z}, {x * z, y * z, z * z}};
-  const double rx[3][3] = {{0.0, -z, y}, {z, 0.0, -x}, {-y, x, 0.0}};
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) R[i][j] = c * (i == j ? 1.0 : 0.0) + c1 * rrt[i][j] + s * rx[i][j];
-}
+using namespace pnpm;
 
 // ---------------------------------------------------------------- kernels
 struct PnpArgs {
@@ -728,21 +141,6 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a) {
   if (threadIdx.x == 0) a.counts[g] = s_count;
 }
 
-// RANSACUpdateNumIters (ptsetreg.cpp)
-__device__ int update_num_iters(double p, double ep, int model_points, int max_iters) {
-  p = p > 0. ? p : 0.;
-  p = p < 1. ? p : 1.;
-  ep = ep > 0. ? ep : 0.;
-  ep = ep < 1. ? ep : 1.;
-  double num = 1. - p;
-  num = num > kDblMin ? num : kDblMin;
-  double denom = 1. - pow(1. - ep, (double)model_points);
-  if (denom < kDblMin) return 0;
-  num = log(num);
-  denom = log(denom);
-  return denom >= 0 || -num >= max_iters * (-denom) ? max_iters : (int)rint(num / denom);
-}
-
 // Sum of one double over a wave in a fixed order (butterfly).
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -803,74 +201,6 @@ __device__ __forceinline__ void lm_reduce(double (&acc)[kNe], double* red, doubl
     out[k] = ((red[k] + red[kNe + k]) + red[2 * kNe + k]) + red[3 * kNe + k];
   }
   __syncthreads();
-}
-
-__device__ void se3_exp(const double (&d)[6], double (&R)[3][3], double (&t)[3]) {
-  const double px = d[3], py = d[4], pz = d[5];
-  const double th = sqrt(px * px + py * py + pz * pz);
-  const double K[3][3] = {{0.0, -pz, py}, {pz, 0.0, -px}, {-py, px, 0.0}};
-  double K2[3][3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) K2[i][j] = K[i][0] * K[0][j] + K[i][1] * K[1][j] + K[i][2] * K[2][j];
-  double a, b, c;
-  if (th < 1e-4) {
-    a = 1.0;
-    b = 0.5;
-    c = 1.0 / 6.0;
-  } else {
-    a = sin(th) / th;
-    b = (1 - cos(th)) / (th * th);
-    c = (th - sin(th)) / (th * th * th);
-  }
-  double V[3][3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const double I = i == j ? 1.0 : 0.0;
-      R[i][j] = I + a * K[i][j] + b * K2[i][j];
-      V[i][j] = I + b * K[i][j] + c * K2[i][j];
-    }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) t[i] = V[i][0] * d[0] + V[i][1] * d[1] + V[i][2] * d[2];
-}
-
-// 6x6 SPD solve (Cholesky); false if not positive definite.
-__device__ bool chol_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[6]) {
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    double d = A[j][j];
-#pragma unroll
-    for (int k = 0; k < j; ++k) d = d - A[j][k] * A[j][k];
-    if (!(d > 0.0)) return false;
-    d = sqrt(d);
-    A[j][j] = d;
-#pragma unroll
-    for (int i = j + 1; i < 6; ++i) {
-      double s = A[i][j];
-#pragma unroll
-      for (int k = 0; k < j; ++k) s = s - A[i][k] * A[j][k];
-      A[i][j] = s / d;
-    }
-  }
-  double y[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    double s = b[i];
-#pragma unroll
-    for (int k = 0; k < i; ++k) s = s - A[i][k] * y[k];
-    y[i] = s / A[i][i];
-  }
-#pragma unroll
-  for (int i = 5; i >= 0; --i) {
-    double s = y[i];
-#pragma unroll
-    for (int k = i + 1; k < 6; ++k) s = s - A[k][i] * x[k];
-    x[i] = s / A[i][i];
-  }
-  return true;
 }
 
 __global__ __launch_bounds__(256) void pnp_final_kernel(PnpArgs a) {
