@@ -52,3 +52,60 @@ def test_hypotheses_bitwise_equal_oracle(exe, seed, noise, frac):
     np.testing.assert_array_equal(h[ok, 9:12], t[ok])
     np.testing.assert_array_equal(h[ok, 12:15], rv[ok])
     np.testing.assert_array_equal(h[ok, 15:24], P.rodrigues_to_mat(rv[ok]).reshape(-1, 9))
+
+
+def host_full(exe, X, uv, K, thr, iters=100, conf=0.99):
+    """One frame through the three kernels' logic on the host (pnp_host_check full)."""
+    from visualodometry_amd import pnp
+
+    X = np.ascontiguousarray(X, np.float32).reshape(-1, 3)
+    uv = np.ascontiguousarray(uv, np.float32).reshape(-1, 2)
+    n = X.shape[0]
+    H = max(int(iters), 1)
+    sub = pnp.ransac_subsets(n, H) if n > 5 else np.zeros((H, 5), np.int32)
+    with tempfile.TemporaryDirectory() as d:
+        fi, fo = os.path.join(d, "in"), os.path.join(d, "out")
+        with open(fi, "wb") as f:
+            np.array([n, H], np.int32).tofile(f)
+            np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2]]).tofile(f)
+            np.array([thr * thr], np.float32).tofile(f)
+            np.array([conf], np.float64).tofile(f)
+            X.tofile(f)
+            uv.tofile(f)
+            sub.astype(np.int32).tofile(f)
+        subprocess.run([str(exe), "full", fi, fo], check=True)
+        raw = open(fo, "rb").read()
+    pose = np.frombuffer(raw[:48], np.float64)
+    st = np.frombuffer(raw[48:56], np.int32)
+    mask = np.frombuffer(raw[56:], np.uint8).astype(bool)
+    return bool(st[0]), pose[:3].copy(), pose[3:].copy(), mask, int(st[1])
+
+
+@pytest.mark.parametrize("n,seed,thr,frac", [(6, 0, 1.0, 0.0), (12, 1, 2.0, 0.0), (100, 2, 1.0, 0.2),
+                                             (600, 3, 2.0, 0.25), (2000, 4, 4.0, 0.2), (400, 9, 2.0, 0.45)])
+def test_full_pipeline_matches_oracle(exe, n, seed, thr, frac):
+    """Subsets, hypotheses, scores, the RANSAC replay, the inlier mask and the LM refinement
+    with pnp_final_kernel's reduction order: the mask exactly, the pose within 1e-5."""
+    X, uv, K, T, out = pnp_case(n, seed, noise_px=0.3, outlier_frac=frac)
+    ok, rv, tv, mask, cnt = host_full(exe, X, uv, K, thr)
+    rok, rrv, rtv, rmask, _ = P.solve_pnp_ransac(X, uv, K, thr)
+    assert ok == rok and cnt == rmask.sum()
+    np.testing.assert_array_equal(mask, rmask)
+    np.testing.assert_allclose(rv, rrv, rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(tv, rtv, rtol=1e-5, atol=1e-8)
+
+
+def test_full_pipeline_edge_cases(exe):
+    X, uv, K, T, _ = pnp_case(5, 4, noise_px=0.0, outlier_frac=0.0)
+    ok, rv, tv, mask, cnt = host_full(exe, X, uv, K, 1.0)
+    rok, rrv, rtv, rmask, _ = P.solve_pnp_ransac(X, uv, K, 1.0)
+    assert ok and rok and mask.all() and cnt == 5
+    np.testing.assert_allclose(rv, rrv, rtol=1e-12)
+    ok, *_ = host_full(exe, X[:4], uv[:4], K, 1.0)
+    assert not ok
+    for iters, conf in ((1, 0.99), (20, 0.5), (300, 0.999)):
+        X, uv, K, T, out = pnp_case(400, 9, noise_px=0.3, outlier_frac=0.45)
+        got = host_full(exe, X, uv, K, 2.0, iters, conf)
+        ref = P.solve_pnp_ransac(X, uv, K, 2.0, iters, conf)
+        assert got[0] == ref[0]
+        np.testing.assert_array_equal(got[3], ref[3])

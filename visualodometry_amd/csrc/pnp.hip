@@ -33,12 +33,6 @@
 namespace vo {
 namespace {
 
-// CvLevMarq's lambda = 10^lg, lg in [-16, 16] (decimal literals: correctly rounded)
-__constant__ double kPow10[33] = {1e-16, 1e-15, 1e-14, 1e-13, 1e-12, 1e-11, 1e-10, 1e-9, 1e-8, 1e-7, 1e-6,
-                                  1e-5,  1e-4,  1e-3,  1e-2,  1e-1,  1e0,   1e1,   1e2,  1e3,  1e4,  1e5,
-                                  1e6,   1e7,   1e8,   1e9,   1e10,  1e11,  1e12,  1e13, 1e14, 1e15, 1e16};
-
-
 using namespace pnpm;
 
 // ---------------------------------------------------------------- kernels
@@ -58,25 +52,10 @@ struct PnpArgs {
   int batch, H;
 };
 
-__device__ __forceinline__ float2 project_f32(const double* R, const double* t, float3 Xf, const Cam& K) {
-  const double X = Xf.x, Y = Xf.y, Z = Xf.z;
-  const double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
-  const double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
-  const double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
-  const double zi = z != 0.0 ? 1.0 / z : 1.0;
-  return make_float2((float)((x * zi) * K.fu + K.uc), (float)((y * zi) * K.fv + K.vc));
-}
-
-__device__ __forceinline__ bool is_inlier(const double* R, const double* t, float3 X, float2 q, const Cam& K,
-                                          float thr2) {
-  const float2 p = project_f32(R, t, X, K);
-  const float dx = q.x - p.x, dy = q.y - p.y;
-  const float e = dx * dx + dy * dy;
-  return e <= thr2;
-}
-
-__device__ __forceinline__ float3 load3(const float* X, int i) {
-  return make_float3(X[3l * i], X[3l * i + 1], X[3l * i + 2]);
+__device__ __forceinline__ void load3(const float* X, int i, float (&M)[3]) {
+  M[0] = X[3l * i];
+  M[1] = X[3l * i + 1];
+  M[2] = X[3l * i + 2];
 }
 
 __global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a) {
@@ -94,10 +73,11 @@ __global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a) {
 #pragma unroll
   for (int p = 0; p < kPts; ++p) {
     const int i = o + (n == kPts ? p : a.subsets[(size_t)g * kPts + p]);
-    const float3 X = load3(a.X, i);
-    S.pw[p][0] = X.x;
-    S.pw[p][1] = X.y;
-    S.pw[p][2] = X.z;
+    float M[3];
+    load3(a.X, i, M);
+    S.pw[p][0] = M[0];
+    S.pw[p][1] = M[1];
+    S.pw[p][2] = M[2];
     S.us[p][0] = a.uv[2l * i];
     S.us[p][1] = a.uv[2l * i + 1];
   }
@@ -133,7 +113,9 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a) {
     int cnt = 0;
     for (int i = threadIdx.x; i < n; i += 256) {
       const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
-      cnt += is_inlier(R, t, load3(a.X, o + i), q, a.K, a.thr2) ? 1 : 0;
+      float M[3];
+      load3(a.X, o + i, M);
+      cnt += is_inlier(R, t, M, q.x, q.y, a.K, a.thr2) ? 1 : 0;
     }
     if (cnt) atomicAdd(&s_count, cnt);
   }
@@ -148,43 +130,17 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-constexpr int kNe = 28;  // 21 (upper J^T J) + 6 (J^T r) + 1 (cost)
-
-// Normal equations of the inliers at (R, t): the partial sums of this thread.
+// Normal equations of the inliers at (R, t): this thread's partial sums (points i = tid mod 256).
 __device__ __forceinline__ void lm_accumulate(const PnpArgs& a, int o, int n, const double* R, const double* t,
                                               double (&acc)[kNe]) {
 #pragma unroll
   for (int k = 0; k < kNe; ++k) acc[k] = 0.0;
   for (int i = threadIdx.x; i < n; i += 256) {
     if (!a.mask[o + i]) continue;
-    const float3 Xf = load3(a.X, o + i);
+    float M[3];
+    load3(a.X, o + i, M);
     const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
-    const double X = Xf.x, Y = Xf.y, Z = Xf.z;
-    const double pc0 = R[0] * X + R[1] * Y + R[2] * Z + t[0];
-    const double pc1 = R[3] * X + R[4] * Y + R[5] * Z + t[1];
-    const double pc2 = R[6] * X + R[7] * Y + R[8] * Z + t[2];
-    const double zi = 1.0 / pc2;
-    const double r0 = a.K.fu * pc0 * zi + a.K.uc - (double)q.x;
-    const double r1 = a.K.fv * pc1 * zi + a.K.vc - (double)q.y;
-    // J = [J_proj | -J_proj [pc]x]  (left se(3) increment, as oracle/pnp_ref.py _normal_eq)
-    const double Jp[2][3] = {{a.K.fu * zi, 0.0, -a.K.fu * pc0 * zi * zi}, {0.0, a.K.fv * zi, -a.K.fv * pc1 * zi * zi}};
-    const double sk[3][3] = {{0.0, -pc2, pc1}, {pc2, 0.0, -pc0}, {-pc1, pc0, 0.0}};
-    double J0[6], J1[6];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      J0[c] = Jp[0][c];
-      J1[c] = Jp[1][c];
-      J0[3 + c] = -(Jp[0][0] * sk[0][c] + Jp[0][1] * sk[1][c] + Jp[0][2] * sk[2][c]);
-      J1[3 + c] = -(Jp[1][0] * sk[0][c] + Jp[1][1] * sk[1][c] + Jp[1][2] * sk[2][c]);
-    }
-    int e = 0;
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-      for (int c = r; c < 6; ++c) acc[e++] += J0[r] * J0[c] + J1[r] * J1[c];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) acc[21 + r] += J0[r] * r0 + J1[r] * r1;
-    acc[27] += r0 * r0 + r1 * r1;
+    lm_point(R, t, M, q.x, q.y, a.K, acc);
   }
 }
 
@@ -254,111 +210,44 @@ __global__ __launch_bounds__(256) void pnp_final_kernel(PnpArgs a) {
   int cnt = 0;
   for (int i = threadIdx.x; i < n; i += 256) {
     const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
-    const bool in = is_inlier(R, t, load3(a.X, o + i), q, a.K, a.thr2);
+    float M[3];
+    load3(a.X, o + i, M);
+    const bool in = is_inlier(R, t, M, q.x, q.y, a.K, a.thr2);
     a.mask[o + i] = in ? 1 : 0;
     cnt += in ? 1 : 0;
   }
   if (cnt) atomicAdd(&s_count, cnt);
-  // lm_accumulate reads mask[o + i] for the same i this thread wrote (same stride)
-  // Levenberg-Marquardt on the inliers (oracle/pnp_ref.py refine_lm)
+  // lm_accumulate reads mask[o + i] for the same i this thread wrote (same stride).
+  // Levenberg-Marquardt on the inliers: thread 0 holds the state (pnp_math.h LmState),
+  // every pass evaluates the normal equations at the pose in s_R/s_t.
   double acc[kNe];
   lm_accumulate(a, o, n, R, t, acc);
   lm_reduce(acc, s_red, s_ne);
-  // thread 0 keeps the LM state
-  double cR[3][3], ct[3], A[21], g[6], cost = 0.0;
-  int lg = -3, accepted = 0;
-  double delta[6];
+  LmState lm;
   if (threadIdx.x == 0) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      ct[i] = t[i];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) cR[i][j] = R[3 * i + j];
-    }
-#pragma unroll
-    for (int k = 0; k < 21; ++k) A[k] = s_ne[k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) g[k] = s_ne[21 + k];
-    cost = s_ne[27];
+    lm.init(R, t, s_ne);
+    s_go = lm.propose(s_R, s_t) ? 1 : 0;
   }
-  for (;;) {
-    if (threadIdx.x == 0) {
-      int go = 0;
-      if (accepted < kLmMaxIters) {
-        const double lam = kPow10[lg + 16];
-        double An[6][6];
-        int e = 0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-          for (int c = r; c < 6; ++c) {
-            An[r][c] = An[c][r] = A[e++];
-          }
-#pragma unroll
-        for (int r = 0; r < 6; ++r) An[r][r] = An[r][r] * (1.0 + lam);
-        double ng[6];
-#pragma unroll
-        for (int r = 0; r < 6; ++r) ng[r] = -g[r];
-        if (chol_solve6(An, ng, delta)) {
-          double dR[3][3], dt[3];
-          se3_exp(delta, dR, dt);
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) s_R[3 * i + j] = dR[i][0] * cR[0][j] + dR[i][1] * cR[1][j] + dR[i][2] * cR[2][j];
-            s_t[i] = dR[i][0] * ct[0] + dR[i][1] * ct[1] + dR[i][2] * ct[2] + dt[i];
-          }
-          go = 1;
-        }
-      }
-      s_go = go;
-    }
-    __syncthreads();
-    if (!s_go) break;
+  __syncthreads();
+  while (s_go) {
     double nR[9], nt[3];
 #pragma unroll
     for (int k = 0; k < 9; ++k) nR[k] = s_R[k];
 #pragma unroll
     for (int k = 0; k < 3; ++k) nt[k] = s_t[k];
     lm_accumulate(a, o, n, nR, nt, acc);
-    lm_reduce(acc, s_red, s_ne);
-    int stop = 0;
-    if (threadIdx.x == 0) {
-      const double costn = s_ne[27];
-      if (costn <= cost) {
-        const double dn = sqrt(delta[0] * delta[0] + delta[1] * delta[1] + delta[2] * delta[2] +
-                               delta[3] * delta[3] + delta[4] * delta[4] + delta[5] * delta[5]);
-        const double tn = sqrt(ct[0] * ct[0] + ct[1] * ct[1] + ct[2] * ct[2]);
-        const bool small = dn <= kFltEps * (1.0 + tn);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          ct[i] = nt[i];
-#pragma unroll
-          for (int j = 0; j < 3; ++j) cR[i][j] = nR[3 * i + j];
-        }
-#pragma unroll
-        for (int k = 0; k < 21; ++k) A[k] = s_ne[k];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) g[k] = s_ne[21 + k];
-        cost = costn;
-        lg = lg - 1 > -16 ? lg - 1 : -16;
-        ++accepted;
-        stop = small ? 1 : 0;
-      } else {
-        ++lg;
-        stop = lg > 16 ? 1 : 0;
-      }
-      s_go = !stop;
-    }
+    lm_reduce(acc, s_red, s_ne);  // ends with a barrier: every thread has read s_R/s_t
+    if (threadIdx.x == 0) s_go = lm.update(nR, nt, s_ne) && lm.propose(s_R, s_t) ? 1 : 0;
     __syncthreads();
-    if (!s_go) break;
   }
   if (threadIdx.x == 0) {
-    double rv[3];
-    rodrigues_to_vec(cR, rv);
+    double Rf[3][3], rv[3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Rf[i][j] = lm.R[3 * i + j];
+    rodrigues_to_vec(Rf, rv);
     for (int k = 0; k < 3; ++k) {
       a.pose[6 * f + k] = rv[k];
-      a.pose[6 * f + 3 + k] = ct[k];
+      a.pose[6 * f + 3 + k] = lm.t[k];
     }
     a.status[2 * f] = 1;
     a.status[2 * f + 1] = s_count;

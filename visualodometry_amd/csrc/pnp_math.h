@@ -696,5 +696,139 @@ VO_HD bool chol_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[6]) 
 }
 
 
+
+// ---------------------------------------------------------------- scoring and refinement
+// cvProjectPoints2Internal without distortion: X = R M + t left to right, z = 1/Z, float32.
+VO_HD void project_f32(const double* R, const double* t, const float* M, const Cam& K, float& u, float& v) {
+  const double X = M[0], Y = M[1], Z = M[2];
+  const double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+  const double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+  const double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+  const double zi = z != 0.0 ? 1.0 / z : 1.0;
+  u = (float)((x * zi) * K.fu + K.uc);
+  v = (float)((y * zi) * K.fv + K.vc);
+}
+
+// PnPRansacCallback::computeError + findInliers: float32 dx*dx + dy*dy <= (float)thr^2.
+VO_HD bool is_inlier(const double* R, const double* t, const float* M, float qx, float qy, const Cam& K,
+                     float thr2) {
+  float u, v;
+  project_f32(R, t, M, K, u, v);
+  const float dx = qx - u, dy = qy - v;
+  const float e = dx * dx + dy * dy;
+  return e <= thr2;
+}
+
+constexpr int kNe = 28;  // normal equations: 21 (upper J^T J) + 6 (J^T r) + 1 (cost)
+
+// Adds one inlier's terms to the normal equations at (R, t): J = [J_proj | -J_proj [pc]x]
+// (left se(3) increment), r = projection - measurement (oracle/pnp_ref.py _normal_eq).
+VO_HD void lm_point(const double* R, const double* t, const float* M, float qx, float qy, const Cam& K,
+                    double (&acc)[kNe]) {
+  const double X = M[0], Y = M[1], Z = M[2];
+  const double pc0 = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+  const double pc1 = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+  const double pc2 = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+  const double zi = 1.0 / pc2;
+  const double r0 = K.fu * pc0 * zi + K.uc - (double)qx;
+  const double r1 = K.fv * pc1 * zi + K.vc - (double)qy;
+  const double Jp[2][3] = {{K.fu * zi, 0.0, -K.fu * pc0 * zi * zi}, {0.0, K.fv * zi, -K.fv * pc1 * zi * zi}};
+  const double sk[3][3] = {{0.0, -pc2, pc1}, {pc2, 0.0, -pc0}, {-pc1, pc0, 0.0}};
+  double J0[6], J1[6];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    J0[c] = Jp[0][c];
+    J1[c] = Jp[1][c];
+    J0[3 + c] = -(Jp[0][0] * sk[0][c] + Jp[0][1] * sk[1][c] + Jp[0][2] * sk[2][c]);
+    J1[3 + c] = -(Jp[1][0] * sk[0][c] + Jp[1][1] * sk[1][c] + Jp[1][2] * sk[2][c]);
+  }
+  int e = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = r; c < 6; ++c) acc[e++] += J0[r] * J0[c] + J1[r] * J1[c];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) acc[21 + r] += J0[r] * r0 + J1[r] * r1;
+  acc[27] += r0 * r0 + r1 * r1;
+}
+
+// 10^e for CvLevMarq's lambda, e in [-16, 16] (decimal literals: correctly rounded, equal to
+// Python's 10.0 ** e).
+VO_HD double pow10i(int e) {
+  switch (e) {
+    case -16: return 1e-16; case -15: return 1e-15; case -14: return 1e-14; case -13: return 1e-13;
+    case -12: return 1e-12; case -11: return 1e-11; case -10: return 1e-10; case -9: return 1e-9;
+    case -8: return 1e-8;   case -7: return 1e-7;   case -6: return 1e-6;   case -5: return 1e-5;
+    case -4: return 1e-4;   case -3: return 1e-3;   case -2: return 1e-2;   case -1: return 1e-1;
+    case 0: return 1e0;     case 1: return 1e1;     case 2: return 1e2;     case 3: return 1e3;
+    case 4: return 1e4;     case 5: return 1e5;     case 6: return 1e6;     case 7: return 1e7;
+    case 8: return 1e8;     case 9: return 1e9;     case 10: return 1e10;   case 11: return 1e11;
+    case 12: return 1e12;   case 13: return 1e13;   case 14: return 1e14;   case 15: return 1e15;
+    default: return 1e16;
+  }
+}
+
+// Levenberg-Marquardt control of oracle/pnp_ref.py refine_lm (CvLevMarq's schedule): the
+// caller evaluates the normal equations at the poses this proposes.
+struct LmState {
+  double R[9], t[3], A[21], g[6], cost, delta[6];
+  int lg, accepted;
+
+  VO_HD void init(const double* R0, const double* t0, const double* ne) {
+    for (int k = 0; k < 9; ++k) R[k] = R0[k];
+    for (int k = 0; k < 3; ++k) t[k] = t0[k];
+    for (int k = 0; k < 21; ++k) A[k] = ne[k];
+    for (int k = 0; k < 6; ++k) g[k] = ne[21 + k];
+    cost = ne[27];
+    lg = -3;
+    accepted = 0;
+  }
+  // Candidate (nR, nt) = exp(delta^) (R, t) with (A + lambda diag A) delta = -g; false when
+  // the refinement is over (20 accepted steps, or the damped system is not SPD).
+  VO_HD bool propose(double* nR, double* nt) {
+    if (accepted >= kLmMaxIters) return false;
+    const double lam = pow10i(lg);
+    double An[6][6];
+    int e = 0;
+    for (int r = 0; r < 6; ++r)
+      for (int c = r; c < 6; ++c) {
+        An[r][c] = A[e];
+        An[c][r] = A[e];
+        ++e;
+      }
+    for (int r = 0; r < 6; ++r) An[r][r] = An[r][r] * (1.0 + lam);
+    double ng[6];
+    for (int r = 0; r < 6; ++r) ng[r] = -g[r];
+    if (!chol_solve6(An, ng, delta)) return false;
+    double dR[3][3], dt[3];
+    se3_exp(delta, dR, dt);
+    for (int i = 0; i < 3; ++i) {
+      for (int j = 0; j < 3; ++j) nR[3 * i + j] = dR[i][0] * R[j] + dR[i][1] * R[3 + j] + dR[i][2] * R[6 + j];
+      nt[i] = dR[i][0] * t[0] + dR[i][1] * t[1] + dR[i][2] * t[2] + dt[i];
+    }
+    return true;
+  }
+  // Accepts or rejects the candidate given its normal equations; false when done.
+  VO_HD bool update(const double* nR, const double* nt, const double* ne) {
+    const double costn = ne[27];
+    if (costn <= cost) {
+      const double dn = sqrt(delta[0] * delta[0] + delta[1] * delta[1] + delta[2] * delta[2] +
+                             delta[3] * delta[3] + delta[4] * delta[4] + delta[5] * delta[5]);
+      const double tn = sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+      const bool small = dn <= kFltEps * (1.0 + tn);
+      for (int k = 0; k < 9; ++k) R[k] = nR[k];
+      for (int k = 0; k < 3; ++k) t[k] = nt[k];
+      for (int k = 0; k < 21; ++k) A[k] = ne[k];
+      for (int k = 0; k < 6; ++k) g[k] = ne[21 + k];
+      cost = costn;
+      lg = lg - 1 > -16 ? lg - 1 : -16;
+      ++accepted;
+      return !small;
+    }
+    ++lg;
+    return lg <= 16;
+  }
+};
+
 }  // namespace pnpm
 }  // namespace vo
