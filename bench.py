@@ -200,7 +200,7 @@ PNP_FLOPS_PER_HYP = 68_000  # EPnP: 12x12 Jacobi SVD (431 pair checks x ~26 + 31
 PNP_FLOPS_PER_EVAL = 40     # scoring: R X + t, 1/z, pixel, float32 error (fp64 + fp32 ops) per point x hypothesis
 
 
-def bench_pnp(ctx, batch: int = 64, n: int = 1000, calls: int = 20, warmup: int = 3, thr: float = 1.0):
+def bench_pnp(ctx, batch: int = 256, n: int = 1000, calls: int = 20, warmup: int = 3, thr: float = 1.0):
     """device-resident PnP-RANSAC throughput (frames/s), batched frames."""
     from oracle import pnp_ref
     from visualodometry_amd import _lib, pnp
@@ -253,6 +253,14 @@ def bench_pnp(ctx, batch: int = 64, n: int = 1000, calls: int = 20, warmup: int 
                              "/ its HIP-event duration; every hypothesis is solved (the serial loop's early exit "
                              "is replayed afterwards)"},
     }
+    # single-frame latency through the host-buffer entry point (the reference's per-frame call)
+    X0, U0 = cases[0][0], cases[0][1]
+    for _ in range(3):
+        pnp.pnp_ransac(X0, U0, K, thr, ctx=ctx)
+    t0 = time.perf_counter()
+    for _ in range(20):
+        pnp.pnp_ransac(X0, U0, K, thr, ctx=ctx)
+    res["single_frame_ms"] = (time.perf_counter() - t0) / 20 * 1e3
     frames = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 3.0 and frames < batch:

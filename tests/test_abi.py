@@ -49,3 +49,15 @@ def test_matcher_has_no_cpu_fallback():
     d = np.zeros((4, 128), np.float32)
     with pytest.raises(_lib.VoError):
         matcher.match_knn2_ratio(d, d)
+
+
+def test_pnp_host_entry_points_validate_arguments():
+    """vo_pnp_subsets runs on the host; bad arguments come back as VO_ERR_ARG with a message."""
+    import ctypes as C
+
+    lib = _lib.load()
+    out = np.zeros((4, 5), np.int32)
+    assert lib.vo_pnp_subsets(5, 4, out.ctypes.data_as(C.POINTER(C.c_int32))) == _lib.VO_ERR_ARG
+    assert b"count > 5" in lib.vo_last_error()
+    assert lib.vo_pnp_subsets(6, 4, out.ctypes.data_as(C.POINTER(C.c_int32))) == _lib.VO_OK
+    assert all(len(set(r)) == 5 for r in out)
