@@ -17,6 +17,8 @@
  *   vo_triangulate        <- triangulate_points, src/modules/frontend.py:115-148
  *   vo_pnp_ransac         <- cv2.solvePnPRansac in the tracking step,
  *                            src/modules/vo.py:135-141
+ *   vo_sift_detect        <- the detection half of SIFT detectAndCompute,
+ *                            src/modules/frontend.py:27-32,55
  *   vo_ba_*               <- new: the reference has no BA (pyceres/pycolmap
  *                            are declared in pyproject.toml:11-12 but never
  *                            imported).  Insertion point: the keyframe hook
@@ -163,8 +165,9 @@ int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n);
  * the summed duration in ms and the launch count, then clears the records.
  * Ids: 0 ba_lin (K1), 1 ba_reduce (K2), 2 ba_solve (K3), 3 match_pack,
  *      4 match_i8 (MFMA sweep), 5 match_f32, 6 match_merge, 7 triangulate,
- *      8 pnp_hyp, 9 pnp_score, 10 pnp_final. */
-#define VO_PROFILE_KERNELS 11
+ *      8 pnp_hyp, 9 pnp_score, 10 pnp_final, 11 sift_pyramid (all upsample, blur
+ *      and downsample launches of one call), 12 sift_extrema (all octaves). */
+#define VO_PROFILE_KERNELS 13
 int vo_profile_enable(vo_ctx* ctx, int on);
 int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
 
@@ -224,6 +227,35 @@ int vo_pnp_ransac_batch_async(vo_ctx* ctx, const float* d_objpts, const float* d
 /* Host only: the RANSAC subsets the cv::RNG((uint64)-1) stream gives for `count` points
  * (iterations x 5 int32), for parity tests. */
 int vo_pnp_subsets(int count, int iterations, int32_t* out);
+
+/* ---- SIFT keypoint detection (detection half) -------- */
+/* Replaces the keypoint detection of cv2.SIFT_create(nfeatures, contrastThreshold,
+ * edgeThreshold, sigma).detectAndCompute(gray, None) (reference
+ * src/modules/frontend.py:27-32,55): doubled base image, Gaussian / DoG pyramid of
+ * n_layers + 3 levels per octave, 26-neighbour extrema of DoG levels 1..n_layers beyond a
+ * 5-pixel border with |v| > floor(0.5 contrast / n_layers * 255), adjustLocalExtrema
+ * (sub-pixel fit, contrast and edge tests).  Orientation assignment, the nfeatures cut
+ * and descriptors are not included.  img: h x w uint8 row-major.
+ * Per keypoint, in (octave, candidate level, row, column) order:
+ *   kp_f[8]: x, y (input-image pixels), size, response, xi, 0, 0, 0
+ *   kp_i[8]: image, OpenCV's octave word (first octave -1), candidate level, level,
+ *            row, column (octave pixels, after refinement), candidate row, column.
+ * *count receives the number found; at most `capacity` are written.  Host buffers. */
+int vo_sift_detect(vo_ctx* ctx, const uint8_t* img, int h, int w, double contrast, double edge, double sigma,
+                   int n_layers, int capacity, float* kp_f, int32_t* kp_i, int32_t* count);
+/* Batch of equally sized images in HBM (d_imgs: batch x h x w uint8); keypoints of all
+ * images appended to d_kpf / d_kpi in no particular order, *d_count (device int32) = total
+ * found.  Enqueued on the context stream. */
+int vo_sift_detect_batch_async(vo_ctx* ctx, const uint8_t* d_imgs, int batch, int h, int w, double contrast,
+                               double edge, double sigma, int n_layers, int capacity, float* d_kpf,
+                               int32_t* d_kpi, int32_t* d_count);
+/* Parity/debug: the Gaussian (g_out) and DoG (d_out) pyramids of one image in the pitched
+ * layout vo_sift_layout describes (g_floats / d_floats = capacities in floats). */
+int vo_sift_pyramid(vo_ctx* ctx, const uint8_t* img, int h, int w, double sigma, int n_layers, float* g_out,
+                    int64_t g_floats, float* d_out, int64_t d_floats);
+/* Host only: [n_octaves, G floats per image, DoG floats per image] then per octave
+ * [h, w, pitch, G offset, DoG offset]; returns the count of values (writes up to n). */
+int vo_sift_layout(int h, int w, int n_layers, int64_t* out, int n);
 
 /* ---- multi-GPU (landmark sharding + RCCL all-reduce) --------------------- */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the caller. */

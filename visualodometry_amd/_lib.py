@@ -91,6 +91,10 @@ SIGNATURES = {
     "vo_pnp_ransac": (_I, [_P, _PF, _PF, _I, _PD, _I, _D, _D, _PD, _PD, C.POINTER(C.c_uint8), _PI32]),
     "vo_pnp_ransac_batch_async": (_I, [_P, _P, _P, _PI32, _I, _PD, _I, _D, _D, _P, _P, _P]),
     "vo_pnp_subsets": (_I, [_I, _I, _PI32]),
+    "vo_sift_detect": (_I, [_P, C.POINTER(C.c_uint8), _I, _I, _D, _D, _D, _I, _I, _PF, _PI32, _PI32]),
+    "vo_sift_detect_batch_async": (_I, [_P, _P, _I, _I, _I, _D, _D, _D, _I, _I, _P, _P, _P]),
+    "vo_sift_pyramid": (_I, [_P, C.POINTER(C.c_uint8), _I, _I, _D, _I, _PF, C.c_int64, _PF, C.c_int64]),
+    "vo_sift_layout": (_I, [_I, _I, _I, _PI64, _I]),
     "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
 }
@@ -213,7 +217,8 @@ class DeviceArray:
 
 
 KERNEL_NAMES = ["ba_lin", "ba_reduce", "ba_solve", "match_pack", "match_i8", "match_f32",
-                "match_merge", "triangulate", "pnp_hyp", "pnp_score", "pnp_final"]
+                "match_merge", "triangulate", "pnp_hyp", "pnp_score", "pnp_final", "sift_pyramid",
+                "sift_extrema"]
 
 
 def profile_enable(ctx: "Context", on: bool = True) -> None:

@@ -1,5 +1,7 @@
 // extern "C" entry points of libvo_hip.so (declared in include/vo_hip.h).
 #include <cstdarg>
+#include <algorithm>
+#include <array>
 #include <cstring>
 #include <vector>
 
@@ -313,6 +315,95 @@ int vo_pnp_ransac_batch_async(vo_ctx* ctx, const float* d_objpts, const float* d
     vo::pnp_run(ctx, d_objpts, d_imgpts, offsets, batch, K, iterations, reproj_err, confidence, d_pose,
                 d_mask, d_status);
   });
+}
+
+int vo_sift_detect(vo_ctx* ctx, const uint8_t* img, int h, int w, double contrast, double edge, double sigma,
+                   int n_layers, int capacity, float* kp_f, int32_t* kp_i, int32_t* count) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(img && count && capacity >= 0 && (capacity == 0 || (kp_f && kp_i)), VO_ERR_ARG,
+               "vo_sift_detect: bad arguments");
+    VO_REQUIRE(h >= 1 && w >= 1, VO_ERR_ARG, "vo_sift_detect: empty image %dx%d", h, w);
+    vo::SiftWorkspace& ws = ctx->sift;
+    const size_t nimg = (size_t)h * w;
+    const size_t cap = (size_t)std::max(capacity, 1);
+    ws.img.reserve(nimg);
+    ws.kp.reserve(cap * 64 + 64);
+    float* dF = ws.kp.as<float>();
+    int32_t* dI = reinterpret_cast<int32_t*>(dF + cap * 8);
+    int32_t* dC = dI + cap * 8;
+    hipStream_t s = ctx->stream;
+    VO_HIP_CHECK(hipMemcpyAsync(ws.img.ptr, img, nimg, hipMemcpyHostToDevice, s));
+    vo::sift_run(ctx, ws.img.as<uint8_t>(), 1, h, w, contrast, edge, sigma, n_layers, capacity, dF, dI, dC, nullptr,
+                 nullptr, nullptr);
+    int32_t found = 0;
+    VO_HIP_CHECK(hipMemcpyAsync(&found, dC, 4, hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipStreamSynchronize(s));
+    const int k = std::min(found, capacity);
+    *count = found;
+    if (k == 0) return;
+    std::vector<float> F((size_t)k * 8);
+    std::vector<int32_t> I((size_t)k * 8);
+    VO_HIP_CHECK(hipMemcpyAsync(F.data(), dF, F.size() * 4, hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipMemcpyAsync(I.data(), dI, I.size() * 4, hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipStreamSynchronize(s));
+    // (image, octave, candidate level, candidate row, candidate column): OpenCV's loop order
+    std::vector<int> ord(k);
+    for (int i = 0; i < k; ++i) ord[i] = i;
+    auto key = [&](int i) {
+      const int32_t* q = &I[(size_t)i * 8];
+      return std::array<int64_t, 6>{q[0], q[1] & 255, q[2], q[6], q[7], i};
+    };
+    std::sort(ord.begin(), ord.end(), [&](int a, int b) { return key(a) < key(b); });
+    for (int i = 0; i < k; ++i) {
+      std::memcpy(kp_f + (size_t)i * 8, &F[(size_t)ord[i] * 8], 32);
+      std::memcpy(kp_i + (size_t)i * 8, &I[(size_t)ord[i] * 8], 32);
+    }
+  });
+}
+
+int vo_sift_detect_batch_async(vo_ctx* ctx, const uint8_t* d_imgs, int batch, int h, int w, double contrast,
+                               double edge, double sigma, int n_layers, int capacity, float* d_kpf,
+                               int32_t* d_kpi, int32_t* d_count) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(d_imgs && d_count && capacity >= 0 && (capacity == 0 || (d_kpf && d_kpi)), VO_ERR_ARG,
+               "vo_sift_detect_batch_async: bad arguments");
+    vo::sift_run(ctx, d_imgs, batch, h, w, contrast, edge, sigma, n_layers, capacity, d_kpf, d_kpi, d_count,
+                 nullptr, nullptr, nullptr);
+  });
+}
+
+int vo_sift_pyramid(vo_ctx* ctx, const uint8_t* img, int h, int w, double sigma, int n_layers, float* g_out,
+                    int64_t g_floats, float* d_out, int64_t d_floats) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(img && g_out && d_out && h >= 1 && w >= 1, VO_ERR_ARG, "vo_sift_pyramid: bad arguments");
+    int64_t lay[3];
+    vo::sift_layout(h, w, n_layers, lay, 3);
+    VO_REQUIRE(g_floats >= lay[1] && d_floats >= lay[2], VO_ERR_ARG,
+               "vo_sift_pyramid: outputs too small (%lld/%lld floats needed)", (long long)lay[1], (long long)lay[2]);
+    vo::SiftWorkspace& ws = ctx->sift;
+    ws.img.reserve((size_t)h * w);
+    ws.kp.reserve(64);
+    hipStream_t s = ctx->stream;
+    VO_HIP_CHECK(hipMemcpyAsync(ws.img.ptr, img, (size_t)h * w, hipMemcpyHostToDevice, s));
+    float *G = nullptr, *D = nullptr;
+    vo::sift_run(ctx, ws.img.as<uint8_t>(), 1, h, w, 0.04, 10.0, sigma, n_layers, 0, nullptr, nullptr,
+                 ws.kp.as<int32_t>(), &G, &D, nullptr);
+    VO_HIP_CHECK(hipMemcpyAsync(g_out, G, (size_t)lay[1] * 4, hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipMemcpyAsync(d_out, D, (size_t)lay[2] * 4, hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipStreamSynchronize(s));
+  });
+}
+
+int vo_sift_layout(int h, int w, int n_layers, int64_t* out, int n) {
+  int rc = 0;
+  const int st = guarded([&] {
+    VO_REQUIRE(h >= 1 && w >= 1 && n_layers >= 1 && out && n >= 0, VO_ERR_ARG, "vo_sift_layout: bad arguments");
+    rc = vo::sift_layout(h, w, n_layers, out, n);
+  });
+  return st == VO_OK ? rc : st;
 }
 
 int vo_pnp_subsets(int count, int iterations, int32_t* out) {

@@ -1,0 +1,424 @@
+// SIFT keypoint detection (scale space, DoG, extrema, sub-pixel refinement) on gfx950.
+//
+// Replaces the detection half of cv2.SIFT_create(...).detectAndCompute(gray, None) at
+// reference src/modules/frontend.py:27-32,55 (OpenCV 4.12 sift.dispatch.cpp /
+// sift.simd.hpp), restated with its arithmetic in oracle/sift_ref.py; this file keeps that
+// operation order in float32 with FMA contraction off, so every pyramid level is bitwise
+// the oracle's and the extremum decisions are exact.
+//
+// A batch of equally sized images is processed level by level (one launch per pyramid
+// level for the whole batch, grid.z = image):
+//   sift_upsample_kernel  uint8 -> float32 doubled image (INTER_LINEAR, exact)
+//   sift_blur_kernel      one Gaussian level: a 64 x 16 output tile, its (16 + 2r) x
+//                         (64 + 2r) input tile staged in LDS (BORDER_REFLECT_101), the row
+//                         pass for the tile's rows into LDS, the column pass, and the DoG
+//                         D_{i-1} = G_i - G_{i-1} written beside G_i (HBM-bound: 16 B/pixel)
+//   sift_down_kernel      next octave's level 0 = every other pixel of level nOctaveLayers
+//   sift_extrema_kernel   per octave: one thread per DoG pixel of levels 1..nOctaveLayers,
+//                         the 26-neighbour test, then adjustLocalExtrema for the (rare)
+//                         candidates; accepted keypoints appended with an atomic counter
+//                         and put in (image, octave, level, row, column) order on the host.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "vo_ctx.h"
+
+#pragma clang fp contract(off)
+
+namespace vo {
+namespace {
+
+constexpr int kBorder = 5;        // SIFT_IMG_BORDER
+constexpr int kMaxInterp = 5;     // SIFT_MAX_INTERP_STEPS
+constexpr int kTileW = 64, kTileH = 16, kMaxR = 32;
+constexpr int kKpFloats = 8;      // x, y, size, response, xi, (pad) per keypoint
+constexpr int kKpInts = 8;        // image, octave word, candidate level, level, row, col, cand row, cand col
+
+struct Taps {
+  float k[2 * kMaxR + 1];
+  int r;
+};
+
+__global__ __launch_bounds__(256) void sift_upsample_kernel(const uint8_t* __restrict__ src, int h, int w,
+                                                            int src_stride, float* __restrict__ dst, int pitch,
+                                                            long dst_stride) {
+  const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int b = blockIdx.z;
+  const int W2 = 2 * w, H2 = 2 * h;
+  if (x >= W2 || y >= H2) return;
+  // source coordinate (d + 0.5) / 2 - 0.5: even d -> (d/2 - 1, 3/4), odd -> (d/2, 1/4);
+  // clamped to the edge pixel at both borders
+  auto axis = [](int d, int n, int& s0, int& s1, float& a0, float& a1) {
+    const int s = (d & 1) ? (d >> 1) : (d >> 1) - 1;
+    float f = (d & 1) ? 0.25f : 0.75f;
+    if (s < 0 || s + 1 >= n) f = 0.0f;
+    s0 = s < 0 ? 0 : (s + 1 >= n ? n - 1 : s);
+    s1 = s + 1 < n ? (s + 1 < 0 ? 0 : s + 1) : n - 1;
+    a0 = 1.0f - f;
+    a1 = f;
+  };
+  int x0, x1, y0, y1;
+  float ax0, ax1, ay0, ay1;
+  axis(x, w, x0, x1, ax0, ax1);
+  axis(y, h, y0, y1, ay0, ay1);
+  const uint8_t* S = src + (long)b * src_stride;
+  const float r0 = (float)S[(long)y0 * w + x0] * ax0 + (float)S[(long)y0 * w + x1] * ax1;
+  const float r1 = (float)S[(long)y1 * w + x0] * ax0 + (float)S[(long)y1 * w + x1] * ax1;
+  dst[(long)b * dst_stride + (long)y * pitch + x] = r0 * ay0 + r1 * ay1;
+}
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  const int period = 2 * n - 2;
+  i = i < 0 ? -i : i;
+  i = i % period;
+  return i >= n ? period - i : i;
+}
+
+// One Gaussian level (and the DoG beside it when prev != nullptr).
+__global__ __launch_bounds__(256) void sift_blur_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                        const float* __restrict__ prev, float* __restrict__ dog,
+                                                        int h, int w, int pitch, long stride, Taps T) {
+  __shared__ float in[(kTileH + 2 * kMaxR) * (kTileW + 2 * kMaxR)];
+  __shared__ float tmp[(kTileH + 2 * kMaxR) * kTileW];
+  const int r = T.r, tw = kTileW + 2 * r, th = kTileH + 2 * r;
+  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH;
+  const long base = (long)blockIdx.z * stride;
+  const float* S = src + base;
+  for (int e = threadIdx.x; e < tw * th; e += 256) {
+    const int ty = e / tw, tx = e - ty * tw;
+    const int gy = reflect101(y0 + ty - r, h), gx = reflect101(x0 + tx - r, w);
+    in[e] = S[(long)gy * pitch + gx];
+  }
+  __syncthreads();
+  // row pass for every staged row: tmp(ty, tx) = sum_j k_j in(ty, tx + j)
+  for (int e = threadIdx.x; e < th * kTileW; e += 256) {
+    const int ty = e / kTileW, tx = e - ty * kTileW;
+    const float* row = in + ty * tw + tx;
+    float s = 0.0f;
+    for (int j = 0; j <= 2 * r; ++j) s = s + T.k[j] * row[j];
+    tmp[e] = s;
+  }
+  __syncthreads();
+  // column pass: 64 columns x 16 rows, 4 rows per thread
+  const int tx = threadIdx.x & 63, ty0 = threadIdx.x >> 6;
+  const int gx = x0 + tx;
+  for (int q = 0; q < kTileH / 4; ++q) {
+    const int ty = ty0 + 4 * q, gy = y0 + ty;
+    float s = 0.0f;
+    for (int j = 0; j <= 2 * r; ++j) s = s + T.k[j] * tmp[(ty + j) * kTileW + tx];
+    if (gx < w && gy < h) {
+      const long o = base + (long)gy * pitch + gx;
+      dst[o] = s;
+      if (prev) dog[o] = s - prev[o];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void sift_down_kernel(const float* __restrict__ src, int src_pitch, long src_stride,
+                                                        float* __restrict__ dst, int h, int w, int pitch, long stride) {
+  const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (x >= w || y >= h) return;
+  dst[(long)blockIdx.z * stride + (long)y * pitch + x] =
+      src[(long)blockIdx.z * src_stride + (long)(2 * y) * src_pitch + 2 * x];
+}
+
+struct ExtArgs {
+  const float* dog;  // octave's DoG levels: level l of image b at dog + b * img_stride + l * lvl_stride
+  long img_stride, lvl_stride;
+  int h, w, pitch, n_layers, octave, threshold, capacity;
+  float contrast, edge, sigma;
+  float* kp_f;       // (capacity, kKpFloats)
+  int32_t* kp_i;     // (capacity, kKpInts)
+  int32_t* count;
+};
+
+__device__ __forceinline__ float at(const float* L, int pitch, int r, int c) { return L[(long)r * pitch + c]; }
+
+// Matx33f::solve(DECOMP_LU): Cramer's rule with the determinant in float; zeros if singular.
+__device__ __forceinline__ void solve3(const float (&a)[3][3], const float (&b)[3], float (&x)[3]) {
+  const float det = a[0][0] * (a[1][1] * a[2][2] - a[2][1] * a[1][2]) - a[0][1] * (a[1][0] * a[2][2] - a[2][0] * a[1][2]) +
+                    a[0][2] * (a[1][0] * a[2][1] - a[2][0] * a[1][1]);
+  if (det == 0.0f) {
+    x[0] = x[1] = x[2] = 0.0f;
+    return;
+  }
+  const float d = __fdiv_rn(1.0f, det);
+  x[0] = d * (b[0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) - a[0][1] * (b[1] * a[2][2] - a[1][2] * b[2]) +
+              a[0][2] * (b[1] * a[2][1] - a[1][1] * b[2]));
+  x[1] = d * (a[0][0] * (b[1] * a[2][2] - a[1][2] * b[2]) - b[0] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
+              a[0][2] * (a[1][0] * b[2] - b[1] * a[2][0]));
+  x[2] = d * (a[0][0] * (a[1][1] * b[2] - b[1] * a[2][1]) - a[0][1] * (a[1][0] * b[2] - b[1] * a[2][0]) +
+              b[0] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]));
+}
+
+__global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int r = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int lz = blockIdx.z % A.n_layers, b = blockIdx.z / A.n_layers;
+  const int layer0 = lz + 1;
+  if (c < kBorder || c >= A.w - kBorder || r < kBorder || r >= A.h - kBorder) return;
+  const float* D = A.dog + (long)b * A.img_stride;
+  const float* img = D + (long)layer0 * A.lvl_stride;
+  const float val = at(img, A.pitch, r, c);
+  if (!(fabsf(val) > (float)A.threshold)) return;
+  const float* prv = img - A.lvl_stride;
+  const float* nxt = img + A.lvl_stride;
+  bool is_max = val > 0, is_min = val < 0;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      const float a = at(prv, A.pitch, r + dy, c + dx), n = at(nxt, A.pitch, r + dy, c + dx);
+      is_max = is_max && val >= a && val >= n;
+      is_min = is_min && val <= a && val <= n;
+      if (dy != 0 || dx != 0) {
+        const float s = at(img, A.pitch, r + dy, c + dx);
+        is_max = is_max && val >= s;
+        is_min = is_min && val <= s;
+      }
+    }
+  if (!is_max && !is_min) return;
+  // adjustLocalExtrema (oracle/sift_ref.py adjust_local_extremum)
+  const float img_scale = 1.0f / 255.0f;
+  const float deriv_scale = img_scale * 0.5f, second = img_scale, cross = img_scale * 0.25f;
+  float xi = 0.0f, xr = 0.0f, xc = 0.0f;
+  int layer = layer0, rr = r, cc = c, i = 0;
+  for (; i < kMaxInterp; ++i) {
+    const float* I = D + (long)layer * A.lvl_stride;
+    const float* P = I - A.lvl_stride;
+    const float* N = I + A.lvl_stride;
+    const int p = A.pitch;
+    const float dD[3] = {(at(I, p, rr, cc + 1) - at(I, p, rr, cc - 1)) * deriv_scale,
+                         (at(I, p, rr + 1, cc) - at(I, p, rr - 1, cc)) * deriv_scale,
+                         (at(N, p, rr, cc) - at(P, p, rr, cc)) * deriv_scale};
+    const float v2 = at(I, p, rr, cc) * 2.0f;
+    const float dxx = (at(I, p, rr, cc + 1) + at(I, p, rr, cc - 1) - v2) * second;
+    const float dyy = (at(I, p, rr + 1, cc) + at(I, p, rr - 1, cc) - v2) * second;
+    const float dss = (at(N, p, rr, cc) + at(P, p, rr, cc) - v2) * second;
+    const float dxy = (at(I, p, rr + 1, cc + 1) - at(I, p, rr + 1, cc - 1) - at(I, p, rr - 1, cc + 1) +
+                       at(I, p, rr - 1, cc - 1)) * cross;
+    const float dxs = (at(N, p, rr, cc + 1) - at(N, p, rr, cc - 1) - at(P, p, rr, cc + 1) + at(P, p, rr, cc - 1)) * cross;
+    const float dys = (at(N, p, rr + 1, cc) - at(N, p, rr - 1, cc) - at(P, p, rr + 1, cc) + at(P, p, rr - 1, cc)) * cross;
+    const float H[3][3] = {{dxx, dxy, dxs}, {dxy, dyy, dys}, {dxs, dys, dss}};
+    float X[3];
+    solve3(H, dD, X);
+    xi = -X[2];
+    xr = -X[1];
+    xc = -X[0];
+    if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+    const float lim = (float)(2147483647 / 3);
+    if (fabsf(xi) > lim || fabsf(xr) > lim || fabsf(xc) > lim) return;
+    cc += (int)rint(xc);
+    rr += (int)rint(xr);
+    layer += (int)rint(xi);
+    if (layer < 1 || layer > A.n_layers || cc < kBorder || cc >= A.w - kBorder || rr < kBorder || rr >= A.h - kBorder)
+      return;
+  }
+  if (i >= kMaxInterp) return;
+  const float* I = D + (long)layer * A.lvl_stride;
+  const float* P = I - A.lvl_stride;
+  const float* N = I + A.lvl_stride;
+  const int p = A.pitch;
+  const float dD[3] = {(at(I, p, rr, cc + 1) - at(I, p, rr, cc - 1)) * deriv_scale,
+                       (at(I, p, rr + 1, cc) - at(I, p, rr - 1, cc)) * deriv_scale,
+                       (at(N, p, rr, cc) - at(P, p, rr, cc)) * deriv_scale};
+  const float t = (0.0f + dD[0] * xc + dD[1] * xr) + dD[2] * xi;
+  const float contr = at(I, p, rr, cc) * img_scale + t * 0.5f;
+  if (fabsf(contr) * (float)A.n_layers < A.contrast) return;
+  const float v2 = at(I, p, rr, cc) * 2.0f;
+  const float dxx = (at(I, p, rr, cc + 1) + at(I, p, rr, cc - 1) - v2) * second;
+  const float dyy = (at(I, p, rr + 1, cc) + at(I, p, rr - 1, cc) - v2) * second;
+  const float dxy = (at(I, p, rr + 1, cc + 1) - at(I, p, rr + 1, cc - 1) - at(I, p, rr - 1, cc + 1) +
+                     at(I, p, rr - 1, cc - 1)) * cross;
+  const float tr = dxx + dyy, det = dxx * dyy - dxy * dxy;
+  if (det <= 0.0f || tr * tr * A.edge >= (A.edge + 1.0f) * (A.edge + 1.0f) * det) return;
+  const int slot = atomicAdd(A.count, 1);
+  if (slot >= A.capacity) return;
+  const float scale = (float)(1 << A.octave);
+  float* F = A.kp_f + (long)slot * kKpFloats;
+  F[0] = ((float)cc + xc) * scale;
+  F[1] = ((float)rr + xr) * scale;
+  F[2] = A.sigma * powf(2.0f, ((float)layer + xi) / (float)A.n_layers) * scale * 2.0f;
+  F[3] = fabsf(contr);
+  F[4] = xi;
+  F[5] = F[6] = F[7] = 0.0f;
+  int32_t* Q = A.kp_i + (long)slot * kKpInts;
+  Q[0] = b;
+  Q[1] = A.octave + (layer << 8) + ((int)rint(((double)xi + 0.5) * 255) << 16);
+  Q[2] = layer0;
+  Q[3] = layer;
+  Q[4] = rr;
+  Q[5] = cc;
+  Q[6] = r;
+  Q[7] = c;
+}
+
+Taps make_taps(double sigma) {
+  // getGaussianKernelBitExact's structure in double (oracle/sift_ref.py gaussian_kernel)
+  const int n = (int)std::nearbyint(sigma * 4 * 2 + 1) | 1;
+  VO_REQUIRE(n <= 2 * kMaxR + 1, VO_ERR_ARG, "sift: sigma %g needs %d taps (max %d)", sigma, n, 2 * kMaxR + 1);
+  const double scale2x = -0.125 / (sigma * sigma);
+  const int n2 = (n - 1) / 2;
+  std::vector<double> vals(n2);
+  double total = 0.0;
+  int x = 1 - n;
+  for (int i = 0; i < n2; ++i, x += 2) {
+    vals[i] = std::exp((double)(x * x) * scale2x);
+    total += vals[i];
+  }
+  total *= 2.0;
+  total += 1.0;
+  if ((n & 1) == 0) total += 1.0;
+  const double mul1 = 1.0 / total;
+  Taps T;
+  T.r = n / 2;
+  for (int i = 0; i < n2; ++i) T.k[i] = T.k[n - 1 - i] = (float)(vals[i] * mul1);
+  for (int i = n2; i <= n - 1 - n2; ++i) T.k[i] = (float)mul1;
+  return T;
+}
+
+}  // namespace
+
+// Pyramid geometry of a batch (host): octave sizes, pitches and buffer offsets.
+struct SiftGeom {
+  int h2, w2, n_oct, n_layers;
+  std::vector<int> oh, ow, op;        // per octave
+  std::vector<long> g_off, d_off;     // per octave: first level's offset (floats) in G / DoG
+  long g_img, d_img;                  // floats per image
+};
+
+static SiftGeom sift_geom(int h, int w, int n_layers) {
+  SiftGeom g;
+  g.h2 = 2 * h;
+  g.w2 = 2 * w;
+  g.n_layers = n_layers;
+  g.n_oct = (int)std::nearbyint(std::log((double)std::min(g.h2, g.w2)) / std::log(2.0) - 2) + 1;
+  long go = 0, dofs = 0;
+  int oh = g.h2, ow = g.w2;
+  for (int o = 0; o < g.n_oct; ++o) {
+    if (o) {
+      oh /= 2;
+      ow /= 2;
+    }
+    const int pitch = ((ow + 63) / 64) * 64;
+    g.oh.push_back(oh);
+    g.ow.push_back(ow);
+    g.op.push_back(pitch);
+    g.g_off.push_back(go);
+    g.d_off.push_back(dofs);
+    go += (long)(n_layers + 3) * oh * pitch;
+    dofs += (long)(n_layers + 2) * oh * pitch;
+  }
+  g.g_img = go;
+  g.d_img = dofs;
+  return g;
+}
+
+void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double contrast, double edge,
+              double sigma, int n_layers, int capacity, float* d_kpf, int32_t* d_kpi, int32_t* d_count,
+              float** g_out, float** d_out, int64_t* layout) {
+  VO_REQUIRE(batch >= 1 && h >= 1 && w >= 1 && n_layers >= 1 && n_layers <= 8 && sigma > 0 && capacity >= 0,
+             VO_ERR_ARG, "sift: bad arguments (batch %d, %dx%d, layers %d, sigma %g)", batch, h, w, n_layers, sigma);
+  const SiftGeom g = sift_geom(h, w, n_layers);
+  VO_REQUIRE(g.n_oct >= 1, VO_ERR_ARG, "sift: image %dx%d too small", h, w);
+  SiftWorkspace& ws = ctx->sift;
+  ws.g.reserve((size_t)batch * g.g_img * sizeof(float));
+  ws.d.reserve((size_t)batch * g.d_img * sizeof(float));
+  float* G = ws.g.as<float>();
+  float* Dg = ws.d.as<float>();
+  hipStream_t st = ctx->stream;
+  VO_HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(int32_t), st));
+  const std::vector<double> sig = [&] {
+    std::vector<double> s(n_layers + 3);
+    s[0] = sigma;
+    const double k = std::pow(2.0, 1.0 / n_layers);
+    for (int i = 1; i < n_layers + 3; ++i) {
+      const double prev = std::pow(k, (double)(i - 1)) * sigma, total = prev * k;
+      s[i] = std::sqrt(total * total - prev * prev);
+    }
+    return s;
+  }();
+  const float sf = (float)sigma;
+  const float sig_diff = sqrtf(std::max(sf * sf - 0.5f * 0.5f * 4, 0.01f));
+  const int threshold = (int)std::floor(0.5 * contrast / n_layers * 255);
+  ctx->prof.begin(st, kKSiftPyramid);
+  for (int o = 0; o < g.n_oct; ++o) {
+    const int oh = g.oh[o], ow = g.ow[o], op = g.op[o];
+    const long lvl = (long)oh * op;
+    float* Go = G + g.g_off[o];
+    float* Do = Dg + g.d_off[o];
+    const dim3 px(ceil_div(ow, 64), ceil_div(oh, 4), batch);
+    const dim3 tiles(ceil_div(ow, kTileW), ceil_div(oh, kTileH), batch);
+    if (o == 0) {
+      // the doubled image goes to level 1's slot, which its own blur overwrites later
+      hipLaunchKernelGGL(sift_upsample_kernel, px, dim3(256), 0, st, d_img, h, w, h * w, Go + lvl, op, g.g_img);
+      hipLaunchKernelGGL(sift_blur_kernel, tiles, dim3(256), 0, st, Go + lvl, Go, (const float*)nullptr,
+                         (float*)nullptr, oh, ow, op, g.g_img, make_taps((double)sig_diff));
+    } else {
+      const long src = g.g_off[o - 1] + (long)n_layers * g.oh[o - 1] * g.op[o - 1];
+      hipLaunchKernelGGL(sift_down_kernel, px, dim3(256), 0, st, G + src, g.op[o - 1], g.g_img, Go, oh, ow, op,
+                         g.g_img);
+    }
+    for (int i = 1; i < n_layers + 3; ++i)
+      hipLaunchKernelGGL(sift_blur_kernel, tiles, dim3(256), 0, st, Go + (i - 1) * lvl, Go + i * lvl,
+                         Go + (i - 1) * lvl, Do + (i - 1) * lvl, oh, ow, op, g.g_img, make_taps(sig[i]));
+    VO_HIP_CHECK(hipGetLastError());
+  }
+  ctx->prof.end(st);
+  ctx->prof.begin(st, kKSiftExtrema);
+  for (int o = 0; o < g.n_oct; ++o) {
+    const int oh = g.oh[o], ow = g.ow[o];
+    if (oh <= 2 * kBorder || ow <= 2 * kBorder) continue;
+    ExtArgs A;
+    A.dog = Dg + g.d_off[o];
+    A.img_stride = g.d_img;
+    A.lvl_stride = (long)oh * g.op[o];
+    A.h = oh;
+    A.w = ow;
+    A.pitch = g.op[o];
+    A.n_layers = n_layers;
+    A.octave = o;
+    A.threshold = threshold;
+    A.capacity = capacity;
+    A.contrast = (float)contrast;
+    A.edge = (float)edge;
+    A.sigma = sf;
+    A.kp_f = d_kpf;
+    A.kp_i = d_kpi;
+    A.count = d_count;
+    hipLaunchKernelGGL(sift_extrema_kernel, dim3(ceil_div(ow, 64), ceil_div(oh, 4), batch * n_layers), dim3(256),
+                       0, st, A);
+  }
+  ctx->prof.end(st);
+  VO_HIP_CHECK(hipGetLastError());
+  if (g_out) *g_out = G;
+  if (d_out) *d_out = Dg;
+  if (layout) {
+    layout[0] = g.n_oct;
+    layout[1] = g.g_img;
+    layout[2] = g.d_img;
+  }
+}
+
+// Host: the pyramid geometry (n_oct, then per octave h, w, pitch, G offset, DoG offset).
+int sift_layout(int h, int w, int n_layers, int64_t* out, int n) {
+  const SiftGeom g = sift_geom(h, w, n_layers);
+  std::vector<int64_t> v = {g.n_oct, g.g_img, g.d_img};
+  for (int o = 0; o < g.n_oct; ++o) {
+    v.push_back(g.oh[o]);
+    v.push_back(g.ow[o]);
+    v.push_back(g.op[o]);
+    v.push_back(g.g_off[o]);
+    v.push_back(g.d_off[o]);
+  }
+  const int m = std::min<int>(n, (int)v.size());
+  for (int i = 0; i < m; ++i) out[i] = v[i];
+  return (int)v.size();
+}
+
+}  // namespace vo

@@ -34,13 +34,20 @@ struct PnpWorkspace {
   int H = 0;
 };
 
+// SIFT detection workspace (sift.hip): Gaussian and DoG pyramids of a batch.
+struct SiftWorkspace {
+  DevBuf g, d;     // float pyramids (pitched, all octaves)
+  DevBuf img;      // host-call staging: the uint8 image
+  DevBuf kp;       // host-call staging: keypoints + count
+};
+
 class BAEngine;   // ba.hip
 struct Comm;      // ba.hip (RCCL communicator)
 
 // Kernel ids of the event profiler (vo_profile_* in include/vo_hip.h).
 enum KernelId {
   kKBaLin = 0, kKBaReduce, kKBaSolve, kKMatchPack, kKMatchI8, kKMatchF32, kKMatchMerge,
-  kKTriangulate, kKPnpHyp, kKPnpScore, kKPnpFinal, kKCount
+  kKTriangulate, kKPnpHyp, kKPnpScore, kKPnpFinal, kKSiftPyramid, kKSiftExtrema, kKCount
 };
 
 // HIP-event timing of individual kernels on the context stream (off by default).
@@ -65,6 +72,7 @@ struct vo_ctx {
   int num_cus = 0;
   vo::MatchWorkspace match;
   vo::PnpWorkspace pnp;
+  vo::SiftWorkspace sift;
   vo::Profiler prof;
   std::unique_ptr<vo::BAEngine> ba;
   std::unique_ptr<vo::Comm> comm;
@@ -88,4 +96,9 @@ void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* of
              const double* K, int iterations, double reproj_err, double confidence, double* d_pose,
              uint8_t* d_mask, int32_t* d_status);
 void pnp_subsets(int count, int iters, int32_t* out);
+// SIFT detection (sift.hip): device images, device keypoint outputs (unsorted).
+void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double contrast, double edge,
+              double sigma, int n_layers, int capacity, float* d_kpf, int32_t* d_kpi, int32_t* d_count,
+              float** g_out, float** d_out, int64_t* layout);
+int sift_layout(int h, int w, int n_layers, int64_t* out, int n);
 }  // namespace vo

@@ -325,3 +325,26 @@ def pnp_case(n: int, seed: int, noise_px: float = 0.3, outlier_frac: float = 0.2
     mag = rng.uniform(25, 200, n)
     uv[out] += np.stack([np.cos(ang), np.sin(ang)], 1)[out] * mag[out, None]
     return X32, uv.astype(np.float32), K, T_cw, out
+
+
+def sift_scene(h: int = 376, w: int = 1241, seed: int = 0, n_blobs: int = 400, n_boxes: int = 60) -> np.ndarray:
+    """A uint8 grayscale image of KITTI's size (``image_0``, ``dataset_loader.py:63``) with
+    SIFT-detectable structure: a smooth vertical gradient, Gaussian blobs of 2-10 px
+    sigma (light and dark), axis-aligned boxes (edges and corners) and 2 gray levels of
+    noise."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    im = 70.0 + 60.0 * yy / h
+    for _ in range(n_boxes):
+        y0, x0 = rng.integers(0, h - 10), rng.integers(0, w - 10)
+        bh, bw = rng.integers(8, 60), rng.integers(8, 120)
+        im[y0:y0 + bh, x0:x0 + bw] += rng.uniform(-50, 50)
+    for _ in range(n_blobs):
+        cy, cx, s = rng.uniform(0, h), rng.uniform(0, w), rng.uniform(2, 10)
+        r = int(4 * s)
+        y0, y1 = max(int(cy) - r, 0), min(int(cy) + r + 1, h)
+        x0, x1 = max(int(cx) - r, 0), min(int(cx) + r + 1, w)
+        g = np.exp(-((yy[y0:y1, x0:x1] - cy) ** 2 + (xx[y0:y1, x0:x1] - cx) ** 2) / (2 * s * s))
+        im[y0:y1, x0:x1] += rng.choice([-1.0, 1.0]) * rng.uniform(40, 90) * g
+    im += rng.normal(0, 2.0, im.shape)
+    return np.clip(np.rint(im), 0, 255).astype(np.uint8)
