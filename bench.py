@@ -273,6 +273,80 @@ def bench_pnp(ctx, batch: int = 256, n: int = 1000, calls: int = 20, warmup: int
     return res
 
 
+def sift_bytes_per_image(h: int, w: int, n_layers: int = 3) -> float:
+    """Algorithmic HBM bytes of one image's detection: the uint8 read and
+    float32 write of the doubled image; per octave level 0 (blur or downsample: 4 B read + 4 B
+    written per pixel), n_layers + 2 blurred levels (4 B read, G and DoG written: 12 B) and
+    the extrema pass (3 DoG levels read per candidate level: 36 B)."""
+    from visualodometry_amd import sift
+
+    L = sift.layout(h, w, n_layers)
+    total = h * w + 4.0 * 4 * h * w
+    for o in L["octaves"]:
+        px = o["h"] * o["w"]
+        total += px * (8 + 12 * (n_layers + 2) + 12 * n_layers)
+    return total
+
+
+def bench_sift(ctx, batch: int = 8, h: int = 376, w: int = 1241, calls: int = 10, warmup: int = 2,
+               contrast: float = 0.02, edge: float = 2.0):
+    """SURVEY §8f row 3 (detection half): device-resident SIFT keypoint detection, images/s."""
+    from oracle import sift_ref
+    from visualodometry_amd import _lib, sift
+    from visualodometry_amd.synthetic import sift_scene
+
+    imgs = np.stack([sift_scene(h, w, seed=200 + b) for b in range(batch)])
+    cap = 1 << 18
+    dI = _lib.DeviceArray.from_numpy(ctx, imgs)
+    dF = _lib.DeviceArray(ctx, (cap, 8), np.float32)
+    dK = _lib.DeviceArray(ctx, (cap, 8), np.int32)
+    dC = _lib.DeviceArray(ctx, (1,), np.int32)
+    run = lambda: sift.detect_device(dI, contrast, edge, 1.6, 3, dF, dK, dC, ctx=ctx)  # noqa: E731
+    for _ in range(warmup):
+        run()
+    _lib.load().vo_synchronize(ctx.handle)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        run()
+    _lib.load().vo_synchronize(ctx.handle)
+    dt = time.perf_counter() - t0
+    _lib.profile_enable(ctx, True)
+    for _ in range(calls):
+        run()
+    prof = _lib.profile_read(ctx)
+    _lib.profile_enable(ctx, False)
+    kern = {k: round(v[0] / v[1] * 1e3, 2) for k, v in prof.items() if k.startswith("sift")}
+    # parity guard against the oracle on image 0 (not timed)
+    ref = sift_ref.detect(imgs[0], contrast, edge, 1.6)
+    got = sift.detect(imgs[0], contrast, edge, 1.6, ctx=ctx)
+    assert np.array_equal(got["pt"], ref["pt"]) and np.array_equal(got["octave"], ref["octave"]), \
+        "SIFT parity guard failed"
+    nbytes = sift_bytes_per_image(h, w) * batch
+    pyr_s = kern.get("sift_pyramid", 0.0) / 1e6
+    ext_s = kern.get("sift_extrema", 0.0) / 1e6
+    gbs = nbytes / (pyr_s + ext_s) / 1e9 if pyr_s + ext_s > 0 else 0.0
+    res = {
+        "metric": "SIFT detection images/sec",
+        "value": batch * calls / dt,
+        "unit": "images/s",
+        "dtype": "f32",
+        "config": {"workload": f"{batch} synthetic {w}x{h} uint8 images per call (KITTI image_0 size), doubled "
+                               f"base, 9 octaves x 6 levels, contrastThreshold {contrast}, edgeThreshold {edge} "
+                               "(KITTI SIFT config), detection only (no orientation / descriptors)",
+                   "calls": calls, "keypoints_image0": int(len(ref["pt"]))},
+        "kernel_us": kern,
+        "roofline": {"bound": "hbm", "kernel": "sift_pyramid+sift_extrema", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "bytes_per_call": nbytes,
+                     "note": "algorithmic bytes (bench.sift_bytes_per_image) / the summed HIP-event spans of "
+                             "the pyramid and extrema launches (launch gaps included)"},
+    }
+    t0 = time.perf_counter()
+    sift_ref.detect(imgs[1], contrast, edge, 1.6)
+    res["cpu_baseline"] = {"value": 1.0 / (time.perf_counter() - t0), "unit": "images/s", "cores": 1,
+                           "kind": "port", "sample": "oracle/sift_ref.py (numpy) on image 1"}
+    return res
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -415,6 +489,7 @@ def main() -> int:
         line["secondary"] = bench_matcher(ctx, traffic_all=traffic_all)
         line["triangulate"] = bench_triangulate(ctx)
         line["pnp"] = bench_pnp(ctx)
+        line["sift"] = bench_sift(ctx)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
