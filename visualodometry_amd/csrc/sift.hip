@@ -81,7 +81,8 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 // One Gaussian level (and the DoG beside it when prev != nullptr).
 __global__ __launch_bounds__(256) void sift_blur_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                         const float* __restrict__ prev, float* __restrict__ dog,
-                                                        int h, int w, int pitch, long stride, Taps T) {
+                                                        int h, int w, int pitch, long stride, long dog_stride,
+                                                        Taps T) {
   __shared__ float in[(kTileH + 2 * kMaxR) * (kTileW + 2 * kMaxR)];
   __shared__ float tmp[(kTileH + 2 * kMaxR) * kTileW];
   const int r = T.r, tw = kTileW + 2 * r, th = kTileH + 2 * r;
@@ -113,7 +114,8 @@ __global__ __launch_bounds__(256) void sift_blur_kernel(const float* __restrict_
     if (gx < w && gy < h) {
       const long o = base + (long)gy * pitch + gx;
       dst[o] = s;
-      if (prev) dog[o] = s - prev[o];
+      // the DoG buffer holds n_layers + 2 levels per image against G's n_layers + 3
+      if (prev) dog[(long)blockIdx.z * dog_stride + (long)gy * pitch + gx] = s - prev[o];
     }
   }
 }
@@ -358,7 +360,7 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
       // the doubled image goes to level 1's slot, which its own blur overwrites later
       hipLaunchKernelGGL(sift_upsample_kernel, px, dim3(256), 0, st, d_img, h, w, h * w, Go + lvl, op, g.g_img);
       hipLaunchKernelGGL(sift_blur_kernel, tiles, dim3(256), 0, st, Go + lvl, Go, (const float*)nullptr,
-                         (float*)nullptr, oh, ow, op, g.g_img, make_taps((double)sig_diff));
+                         (float*)nullptr, oh, ow, op, g.g_img, g.d_img, make_taps((double)sig_diff));
     } else {
       const long src = g.g_off[o - 1] + (long)n_layers * g.oh[o - 1] * g.op[o - 1];
       hipLaunchKernelGGL(sift_down_kernel, px, dim3(256), 0, st, G + src, g.op[o - 1], g.g_img, Go, oh, ow, op,
@@ -366,7 +368,7 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
     }
     for (int i = 1; i < n_layers + 3; ++i)
       hipLaunchKernelGGL(sift_blur_kernel, tiles, dim3(256), 0, st, Go + (i - 1) * lvl, Go + i * lvl,
-                         Go + (i - 1) * lvl, Do + (i - 1) * lvl, oh, ow, op, g.g_img, make_taps(sig[i]));
+                         Go + (i - 1) * lvl, Do + (i - 1) * lvl, oh, ow, op, g.g_img, g.d_img, make_taps(sig[i]));
     VO_HIP_CHECK(hipGetLastError());
   }
   ctx->prof.end(st);

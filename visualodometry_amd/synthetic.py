@@ -336,7 +336,7 @@ def sift_scene(h: int = 376, w: int = 1241, seed: int = 0, n_blobs: int = 400, n
     yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
     im = 70.0 + 60.0 * yy / h
     for _ in range(n_boxes):
-        y0, x0 = rng.integers(0, h - 10), rng.integers(0, w - 10)
+        y0, x0 = rng.integers(0, max(h - 10, 1)), rng.integers(0, max(w - 10, 1))
         bh, bw = rng.integers(8, 60), rng.integers(8, 120)
         im[y0:y0 + bh, x0:x0 + bw] += rng.uniform(-50, 50)
     for _ in range(n_blobs):
