@@ -166,8 +166,10 @@ int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n);
  * Ids: 0 ba_lin (K1), 1 ba_reduce (K2), 2 ba_solve (K3), 3 match_pack,
  *      4 match_i8 (MFMA sweep), 5 match_f32, 6 match_merge, 7 triangulate,
  *      8 pnp_hyp, 9 pnp_score, 10 pnp_final, 11 sift_pyramid (all upsample, blur
- *      and downsample launches of one call), 12 sift_extrema (all octaves). */
-#define VO_PROFILE_KERNELS 13
+ *      and downsample launches of one call), 12 sift_extrema (all octaves),
+ *      13 sift_orient, 14 sift_select (sort keys, segmented sort, duplicate removal,
+ *      retainBest, compaction), 15 sift_desc. */
+#define VO_PROFILE_KERNELS 16
 int vo_profile_enable(vo_ctx* ctx, int on);
 int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
 
@@ -253,6 +255,36 @@ int vo_sift_detect_batch_async(vo_ctx* ctx, const uint8_t* d_imgs, int batch, in
  * layout vo_sift_layout describes (g_floats / d_floats = capacities in floats). */
 int vo_sift_pyramid(vo_ctx* ctx, const uint8_t* img, int h, int w, double sigma, int n_layers, float* g_out,
                     int64_t g_floats, float* d_out, int64_t d_floats);
+/* ---- SIFT detectAndCompute ------------------------- */
+/* One keypoint as cv::KeyPoint holds it after detectAndCompute: pt (x, y) and size in
+ * input-image pixels, angle in degrees, response, OpenCV's octave word (first octave -1);
+ * image = index in the batch. */
+typedef struct vo_sift_keypoint {
+  float x, y, size, angle, response;
+  int32_t octave, image, reserved;
+} vo_sift_keypoint;
+/* Replaces cv2.SIFT_create(nfeatures, contrastThreshold, edgeThreshold, sigma)
+ * .detectAndCompute(gray, None) (reference src/modules/frontend.py:27-32,55; OpenCV 4.12
+ * sift.dispatch.cpp / sift.simd.hpp): the detection above, then calcOrientationHist (one
+ * keypoint per histogram peak >= 0.8 max), KeyPointsFilter::removeDuplicatedSorted,
+ * retainBest(nfeatures) when nfeatures > 0 (every keypoint whose response is >= the
+ * nfeatures-th largest), and calcSIFTDescriptor (4 x 4 x 8, clipped at 0.2, scaled to 512,
+ * saturate_cast<uchar>, stored as float).  Keypoints come out in removeDuplicatedSorted's
+ * order (x asc, y asc, size desc, angle asc, response desc, octave desc); OpenCV's order
+ * after retainBest is implementation-defined.  capacity bounds the
+ * oriented keypoints considered (before the nfeatures cut) and the output; *count = the
+ * number written; VO_ERR_ARG when a capacity overflowed.  Host buffers:
+ * kps[capacity], desc[capacity x 128]. */
+int vo_sift_detect_and_compute(vo_ctx* ctx, const uint8_t* img, int h, int w, int nfeatures, double contrast,
+                               double edge, double sigma, int n_layers, int capacity, vo_sift_keypoint* kps,
+                               float* desc, int32_t* count);
+/* Batch of equally sized images in HBM (d_imgs: batch x h x w uint8).  Per image b:
+ * d_kps[b * capacity + i], d_desc[(b * capacity + i) * 128], i < d_counts[b]
+ * (d_counts[b] = -1 when a capacity overflowed).  Enqueued on the context stream. */
+int vo_sift_detect_and_compute_batch_async(vo_ctx* ctx, const uint8_t* d_imgs, int batch, int h, int w,
+                                           int nfeatures, double contrast, double edge, double sigma,
+                                           int n_layers, int capacity, vo_sift_keypoint* d_kps, float* d_desc,
+                                           int32_t* d_counts);
 /* Host only: [n_octaves, G floats per image, DoG floats per image] then per octave
  * [h, w, pitch, G offset, DoG offset]; returns the count of values (writes up to n). */
 int vo_sift_layout(int h, int w, int n_layers, int64_t* out, int n);

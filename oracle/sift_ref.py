@@ -317,3 +317,293 @@ def _pack(kps):
         "xi": a[:, 9].astype(np.float32),
         "index": a[:, :4].astype(np.int32),  # (octave, level, row, column)
     }
+
+
+# ---------------------------------------------------------------------------------------
+# Orientation, keypoint filtering and descriptors (the rest of detectAndCompute).
+#
+# OpenCV 4.12 sift.simd.hpp / sift.dispatch.cpp / keypoint.cpp, restated:
+#
+# * ``calcOrientationHist``: 36-bin histogram over a (2 radius + 1)^2 window of the Gaussian
+#   level the extremum was refined on, radius = cvRound(4.5 scl), sigma = 1.5 scl with
+#   scl = size / 2 / 2^octave; samples strictly inside the image (1 .. rows-2); dx, dy
+#   central differences; weight exp32f((i^2 + j^2) * -1 / (2 sigma^2)); bin
+#   cvRound(n / 360 * angle) wrapped; ``temphist[bin] += w * mag`` in sample order;
+#   [1 4 6 4 1] / 16 circular smoothing; every local peak >= 0.8 max gives a keypoint with
+#   the parabolically interpolated angle ``360 - 10 * bin`` (0 when within FLT_EPSILON of
+#   360).
+# * ``removeDuplicatedSorted``: sort by (x asc, y asc, size desc, angle asc, response desc,
+#   octave desc), drop entries equal to the kept predecessor in (x, y, size, angle).
+# * ``retainBest(nfeatures)``: when more than nfeatures remain, keep every keypoint whose
+#   response is >= the nfeatures-th largest response (ties at the boundary are all kept).
+# * ``calcSIFTDescriptor`` (d = 4, n = 8): the window rotated by the keypoint angle,
+#   hist_width = 3 scl, radius = cvRound(hist_width * sqrt2 * (d + 1) / 2) clipped to the
+#   image diagonal; trilinear votes of exp32f-weighted magnitudes into a (d+2)^2 (n+2)
+#   histogram in sample order; orientation wrap; L2 norm, clip at 0.2 * norm, renormalise to
+#   512 and saturate_cast<uchar> (round half to even, clamp 0..255), stored as float32.
+#
+# Build-defined where OpenCV's result depends on the CPU it runs on: OpenCV's SIMD paths of
+# exp32f / fastAtan2 / magnitude / the histogram smoothing / the norm sums use FMA where
+# the CPU has it, so this file (and csrc/sift.hip) follows the scalar fallback of each
+# routine with no FMA; cosf / sinf are ``(float)cos((double)x)``; the keypoint size's
+# ``powf(2, e)`` is ``(float)pow(2.0, (double)e)``.  retainBest's nth_element / partition
+# leave an implementation-defined order: the output here is the removeDuplicatedSorted
+# order, filtered.  Against OpenCV itself this is parity unpinned (cv2 absent).
+# ---------------------------------------------------------------------------------------
+
+SIFT_ORI_HIST_BINS = 36
+SIFT_ORI_SIG_FCTR = np.float32(1.5)
+SIFT_ORI_RADIUS = np.float32(3 * 1.5)
+SIFT_ORI_PEAK_RATIO = np.float32(0.8)
+SIFT_DESCR_WIDTH = 4
+SIFT_DESCR_HIST_BINS = 8
+SIFT_DESCR_SCL_FCTR = np.float32(3.0)
+SIFT_DESCR_MAG_THR = np.float32(0.2)
+SIFT_INT_DESCR_FCTR = np.float32(512.0)
+FLT_EPSILON = np.float32(1.1920928955078125e-07)
+
+_f = np.float32
+
+# cv::hal::exp32f (core/src/mathfuncs_core.simd.hpp), scalar path
+EXPTAB_SCALE = 6
+EXPPOLY_32F_A0 = .9670371139572337719125840413672004409288e-2
+EXP_TAB = np.array([2.0 ** (j / 64.0) * EXPPOLY_32F_A0 for j in range(64)], dtype=np.float64).astype(np.float32)
+EXP_A4 = _f(1.000000000000002438532970795181890933776 / EXPPOLY_32F_A0)
+EXP_A3 = _f(.6931471805521448196800669615864773144641 / EXPPOLY_32F_A0)
+EXP_A2 = _f(.2402265109513301490103372422686535526573 / EXPPOLY_32F_A0)
+EXP_A1 = _f(.5550339366753125211915322047004666939128e-1 / EXPPOLY_32F_A0)
+EXP_PRESCALE = _f(1.4426950408889634073599246810019 * (1 << EXPTAB_SCALE))
+EXP_POSTSCALE = _f(1.0 / (1 << EXPTAB_SCALE))
+_EXP_MAX = 3000.0 * (1 << EXPTAB_SCALE)
+EXP_MINVAL = _f(-_EXP_MAX / (1.4426950408889634073599246810019 * (1 << EXPTAB_SCALE)))
+EXP_MAXVAL = _f(_EXP_MAX / (1.4426950408889634073599246810019 * (1 << EXPTAB_SCALE)))
+
+
+def exp32f(x: np.ndarray) -> np.ndarray:
+    """``cv::hal::exp32f`` scalar loop: clamp, scale by 64/ln2, split into cvRound integer and
+    fraction, 2^(int>>6) from the exponent bits times the 64-entry table times a quartic."""
+    x0 = np.minimum(np.maximum(np.asarray(x, _f), EXP_MINVAL), EXP_MAXVAL)
+    x0 = (x0 * EXP_PRESCALE).astype(_f)
+    xi = np.rint(x0).astype(np.int32)  # saturate_cast<int>(float) = cvRound
+    x0 = ((x0 - xi.astype(_f)) * EXP_POSTSCALE).astype(_f)
+    t = (xi >> EXPTAB_SCALE) + 127
+    t = np.where((t & ~255) == 0, t, np.where(t < 0, 0, 255)).astype(np.int32)
+    buf = (t.astype(np.uint32) << np.uint32(23)).view(np.float32)
+    poly = ((((x0 + EXP_A1) * x0 + EXP_A2) * x0 + EXP_A3) * x0 + EXP_A4).astype(_f)
+    return ((buf * EXP_TAB[xi & 63]).astype(_f) * poly).astype(_f)
+
+
+_RAD2DEG = _f(180 / math.pi)
+ATAN_P1 = _f(_f(0.9997878412794807) * _RAD2DEG)
+ATAN_P3 = _f(_f(-0.3258083974640975) * _RAD2DEG)
+ATAN_P5 = _f(_f(0.1555786518463281) * _RAD2DEG)
+ATAN_P7 = _f(_f(-0.04432655554792128) * _RAD2DEG)
+_DBL_EPS_F = _f(2.220446049250313e-16)
+
+
+def fast_atan2(y: np.ndarray, x: np.ndarray) -> np.ndarray:
+    """``cv::fastAtan2`` in degrees (core/src/mathfuncs_core.simd.hpp ``atan_f32``)."""
+    y = np.asarray(y, _f)
+    x = np.asarray(x, _f)
+    ax, ay = np.abs(x), np.abs(y)
+    ge = ax >= ay
+    num = np.where(ge, ay, ax)
+    den = (np.where(ge, ax, ay) + _DBL_EPS_F).astype(_f)
+    c = (num / den).astype(_f)
+    c2 = (c * c).astype(_f)
+    a = ((((ATAN_P7 * c2 + ATAN_P5) * c2 + ATAN_P3) * c2 + ATAN_P1) * c).astype(_f)
+    a = np.where(ge, a, _f(90) - a).astype(_f)
+    a = np.where(x < 0, _f(180) - a, a).astype(_f)
+    return np.where(y < 0, _f(360) - a, a).astype(_f)
+
+
+def magnitude(x: np.ndarray, y: np.ndarray) -> np.ndarray:
+    x = np.asarray(x, _f)
+    y = np.asarray(y, _f)
+    return np.sqrt((x * x + y * y).astype(_f)).astype(_f)
+
+
+def cos_sin_deg(ori: float) -> tuple:
+    """cosf / sinf of ``ori * (float)(CV_PI/180)`` as ``(float)cos((double)x)``."""
+    a = float(_f(ori) * _f(math.pi / 180))
+    return _f(math.cos(a)), _f(math.sin(a))
+
+
+def orientation_hist(img: np.ndarray, px: int, py: int, radius: int, sigma, n: int = SIFT_ORI_HIST_BINS):
+    """``calcOrientationHist`` -> (smoothed hist (n,) float32, max)."""
+    rows, cols = img.shape
+    sigma = _f(sigma)
+    expf_scale = _f(-1) / ((_f(2) * sigma) * sigma)
+    ii, jj = np.meshgrid(np.arange(-radius, radius + 1), np.arange(-radius, radius + 1), indexing="ij")
+    y = py + ii
+    x = px + jj
+    ok = (y > 0) & (y < rows - 1) & (x > 0) & (x < cols - 1)
+    ii, jj, y, x = ii[ok], jj[ok], y[ok], x[ok]  # row-major sample order
+    dx = (img[y, x + 1] - img[y, x - 1]).astype(_f)
+    dy = (img[y - 1, x] - img[y + 1, x]).astype(_f)
+    W = ((ii * ii + jj * jj).astype(_f) * expf_scale).astype(_f)
+    W = exp32f(W)
+    ori = fast_atan2(dy, dx)
+    mag = magnitude(dx, dy)
+    bins = np.rint((_f(n) / _f(360)) * ori).astype(np.int64)
+    bins = np.where(bins >= n, bins - n, bins)
+    bins = np.where(bins < 0, bins + n, bins)
+    temp = np.zeros(n, _f)
+    np.add.at(temp, bins, (W * mag).astype(_f))  # sequential, in sample order
+    tp = np.concatenate([temp[-2:], temp, temp[:2]])
+    hist = ((tp[0:n] + tp[4:n + 4]) * _f(1 / 16) + (tp[1:n + 1] + tp[3:n + 3]) * _f(4 / 16) +
+            tp[2:n + 2] * _f(6 / 16)).astype(_f)
+    return hist, _f(hist.max())
+
+
+def orientation_peaks(hist: np.ndarray, omax) -> list:
+    """Angles (degrees, float32) of the histogram peaks >= 0.8 max, in bin order."""
+    n = hist.size
+    mag_thr = _f(_f(omax) * SIFT_ORI_PEAK_RATIO)
+    out = []
+    for j in range(n):
+        l, r2 = (j - 1) if j > 0 else n - 1, (j + 1) if j < n - 1 else 0
+        if hist[j] > hist[l] and hist[j] > hist[r2] and hist[j] >= mag_thr:
+            b = _f(_f(j) + (_f(0.5) * (hist[l] - hist[r2])) / ((hist[l] - _f(2) * hist[j]) + hist[r2]))
+            b = _f(n) + b if b < 0 else (b - _f(n) if b >= n else b)
+            angle = _f(_f(360) - _f(_f(360.0 / n) * _f(b)))
+            if abs(angle - _f(360)) < FLT_EPSILON:
+                angle = _f(0)
+            out.append(angle)
+    return out
+
+
+def descriptor(img: np.ndarray, x: float, y: float, ori, scl, d: int = SIFT_DESCR_WIDTH,
+               n: int = SIFT_DESCR_HIST_BINS) -> np.ndarray:
+    """``calcSIFTDescriptor`` -> (d*d*n,) float32 holding integers 0..255."""
+    rows, cols = img.shape
+    ptx, pty = cv_round(float(x)), cv_round(float(y))
+    ori = _f(ori)
+    cos_t, sin_t = cos_sin_deg(ori)
+    bins_per_rad = _f(n) / _f(360)
+    exp_scale = _f(-1) / _f(d * d * 0.5)
+    hist_width = _f(SIFT_DESCR_SCL_FCTR * _f(scl))
+    radius = cv_round(float(_f(_f(_f(hist_width * _f(1.4142135623730951)) * _f(d + 1)) * _f(0.5))))
+    radius = min(radius, int(math.sqrt(float(cols) * cols + float(rows) * rows)))
+    cos_t = _f(cos_t / hist_width)
+    sin_t = _f(sin_t / hist_width)
+    ii, jj = np.meshgrid(np.arange(-radius, radius + 1), np.arange(-radius, radius + 1), indexing="ij")
+    ii, jj = ii.ravel(), jj.ravel()
+    fi, fj = ii.astype(_f), jj.astype(_f)
+    c_rot = (fj * cos_t - fi * sin_t).astype(_f)
+    r_rot = (fj * sin_t + fi * cos_t).astype(_f)
+    half = _f(d // 2)
+    rbin = ((r_rot + half) - _f(0.5)).astype(_f)
+    cbin = ((c_rot + half) - _f(0.5)).astype(_f)
+    r = pty + ii
+    c = ptx + jj
+    ok = ((rbin > -1) & (rbin < d) & (cbin > -1) & (cbin < d) & (r > 0) & (r < rows - 1) & (c > 0) & (c < cols - 1))
+    r, c, rbin, cbin, c_rot, r_rot = r[ok], c[ok], rbin[ok], cbin[ok], c_rot[ok], r_rot[ok]
+    dx = (img[r, c + 1] - img[r, c - 1]).astype(_f)
+    dy = (img[r - 1, c] - img[r + 1, c]).astype(_f)
+    W = ((c_rot * c_rot + r_rot * r_rot) * exp_scale).astype(_f)
+    Ori = fast_atan2(dy, dx)
+    Mag = magnitude(dx, dy)
+    W = exp32f(W)
+    obin = ((Ori - ori) * bins_per_rad).astype(_f)
+    mag = (Mag * W).astype(_f)
+    r0 = np.floor(rbin).astype(np.int64)
+    c0 = np.floor(cbin).astype(np.int64)
+    o0 = np.floor(obin).astype(np.int64)
+    rb = (rbin - r0.astype(_f)).astype(_f)
+    cb = (cbin - c0.astype(_f)).astype(_f)
+    ob = (obin - o0.astype(_f)).astype(_f)
+    o0 = np.where(o0 < 0, o0 + n, o0)
+    o0 = np.where(o0 >= n, o0 - n, o0)
+    v_r1 = (mag * rb).astype(_f)
+    v_r0 = (mag - v_r1).astype(_f)
+    v_rc11 = (v_r1 * cb).astype(_f)
+    v_rc10 = (v_r1 - v_rc11).astype(_f)
+    v_rc01 = (v_r0 * cb).astype(_f)
+    v_rc00 = (v_r0 - v_rc01).astype(_f)
+    v = {}
+    for key, base in (("11", v_rc11), ("10", v_rc10), ("01", v_rc01), ("00", v_rc00)):
+        v[key + "1"] = (base * ob).astype(_f)
+        v[key + "0"] = (base - v[key + "1"]).astype(_f)
+    idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0
+    s1, s2 = n + 2, (d + 2) * (n + 2)
+    order = [(0, "000"), (1, "001"), (s1, "010"), (s1 + 1, "011"), (s2, "100"), (s2 + 1, "101"),
+             (s2 + s1, "110"), (s2 + s1 + 1, "111")]
+    tgt = np.stack([idx + off for off, _ in order], 1).ravel()  # sample-major: sample order per bin
+    val = np.stack([v[k] for _, k in order], 1).ravel()
+    hist = np.zeros((d + 2) * (d + 2) * (n + 2), _f)
+    np.add.at(hist, tgt, val)
+    raw = np.empty(d * d * n, _f)
+    for i in range(d):
+        for j in range(d):
+            b = ((i + 1) * (d + 2) + (j + 1)) * (n + 2)
+            hist[b] = _f(hist[b] + hist[b + n])
+            hist[b + 1] = _f(hist[b + 1] + hist[b + n + 1])
+            raw[(i * d + j) * n:(i * d + j + 1) * n] = hist[b:b + n]
+    nrm2 = _f(0)
+    for k in range(raw.size):
+        nrm2 = _f(nrm2 + _f(raw[k] * raw[k]))
+    thr = _f(_f(np.sqrt(nrm2)) * SIFT_DESCR_MAG_THR)
+    raw = np.minimum(raw, thr)
+    nrm2 = _f(0)
+    for k in range(raw.size):
+        nrm2 = _f(nrm2 + _f(raw[k] * raw[k]))
+    nrm2 = _f(SIFT_INT_DESCR_FCTR / max(_f(np.sqrt(nrm2)), FLT_EPSILON))
+    return np.clip(np.rint((raw * nrm2).astype(_f)), 0, 255).astype(_f)
+
+
+def _sort_key(k):
+    # KeyPoint12_LessThan: x asc, y asc, size desc, angle asc, response desc, octave desc
+    return (k["x"], k["y"], -k["size"], k["angle"], -k["response"], -k["octave"])
+
+
+def detect_and_compute(gray: np.ndarray, nfeatures: int = 0, contrast: float = 0.04, edge: float = 10.0,
+                       sigma: float = 1.6, n_layers: int = 3, with_descriptors: bool = True) -> dict:
+    """``SIFT_create(nfeatures, nOctaveLayers, contrastThreshold, edgeThreshold, sigma)
+    .detectAndCompute(gray, None)`` -> dict: pt (N, 2), size, angle, response, octave (as
+    cv::KeyPoint holds them) and descriptors (N, 128) float32."""
+    pyr = gaussian_pyramid(gray, sigma, n_layers)
+    det = detect(gray, contrast, edge, sigma, n_layers)
+    kps = []
+    for i in range(len(det["pt"])):
+        o, layer, r, c = (int(v) for v in det["index"][i])
+        size2 = _f(det["size"][i] * _f(2))  # back to doubled-image units (exact)
+        scl_octv = _f(_f(size2 * _f(0.5)) / _f(1 << o))
+        hist, omax = orientation_hist(pyr[o][layer], c, r, cv_round(float(SIFT_ORI_RADIUS * scl_octv)),
+                                      _f(SIFT_ORI_SIG_FCTR * scl_octv))
+        word = int(det["octave"][i])
+        word_pre = (word & ~255) | (((word & 255) + 1) & 255)
+        for ang in orientation_peaks(hist, omax):
+            kps.append(dict(x=_f(det["pt"][i, 0] * _f(2)), y=_f(det["pt"][i, 1] * _f(2)), size=size2, angle=ang,
+                            response=_f(det["response"][i]), octave=word_pre, o=o, layer=layer))
+    kps.sort(key=_sort_key)
+    uniq = []
+    for k in kps:  # removeDuplicatedSorted
+        if uniq and (uniq[-1]["x"] == k["x"] and uniq[-1]["y"] == k["y"] and uniq[-1]["size"] == k["size"] and
+                     uniq[-1]["angle"] == k["angle"]):
+            continue
+        uniq.append(k)
+    if nfeatures > 0 and len(uniq) > nfeatures:  # retainBest
+        t = np.sort(np.array([k["response"] for k in uniq], _f))[::-1][nfeatures - 1]
+        uniq = [k for k in uniq if k["response"] >= t]
+    N = len(uniq)
+    desc = np.zeros((N, SIFT_DESCR_WIDTH ** 2 * SIFT_DESCR_HIST_BINS), _f)
+    if with_descriptors:
+        for i, k in enumerate(uniq):
+            # calcDescriptors: the octave's image, pt and size in octave pixels (exact scalings)
+            s = _f(1.0 / (1 << k["o"]))
+            ang = _f(_f(360) - k["angle"])
+            if abs(ang - _f(360)) < FLT_EPSILON:
+                ang = _f(0)
+            desc[i] = descriptor(pyr[k["o"]][k["layer"]], _f(k["x"] * s), _f(k["y"] * s), ang,
+                                 _f(_f(k["size"] * s) * _f(0.5)))
+    half = _f(0.5)
+    octs = np.array([(k["octave"] & ~255) | (((k["octave"] & 255) + FIRST_OCTAVE) & 255) for k in uniq], np.int64)
+    return {
+        "pt": np.array([[k["x"] * half, k["y"] * half] for k in uniq], _f).reshape(N, 2),
+        "size": np.array([k["size"] * half for k in uniq], _f),
+        "angle": np.array([k["angle"] for k in uniq], _f),
+        "response": np.array([k["response"] for k in uniq], _f),
+        "octave": octs.astype(np.int32),
+        "descriptors": desc,
+    }

@@ -3,9 +3,12 @@
 
 The kernels keep the oracle's float32 operation order with FMA contraction off, so
 every Gaussian and DoG level must be bitwise equal, and the keypoints identical: the
-same extrema in the same order, positions, responses and offsets bit for bit, octave
-words exact.  Only the size goes through ``powf`` (the device's and the host's can differ
-by an ulp): within 1e-6 relative.
+same extrema in the same order, positions, responses, offsets and sizes bit for bit,
+octave words exact (the size's 2^e is (float)exp2((double)e) on both sides).
+
+detectAndCompute (orientation, removeDuplicatedSorted, retainBest, descriptors): the same
+keypoints in the same order with every field bit for bit, and the descriptors (integers
+0..255 stored as float32) identical.
 """
 
 import numpy as np
@@ -25,7 +28,7 @@ def _check_kp(got, ref):
     np.testing.assert_array_equal(got["pt"], ref["pt"])
     np.testing.assert_array_equal(got["response"], ref["response"])
     np.testing.assert_array_equal(got["xi"], ref["xi"])
-    np.testing.assert_allclose(got["size"], ref["size"], rtol=1e-6)
+    np.testing.assert_array_equal(got["size"], ref["size"])
 
 
 @pytest.mark.parametrize("h,w,seed", [(64, 80, 0), (120, 200, 1), (376, 1241, 2)])
@@ -74,3 +77,78 @@ def test_batch_matches_single(ctx):
         assert sel.sum() == len(ref["pt"])
         np.testing.assert_array_equal(F[sel][order][:, :2] * np.float32(0.5), ref["pt"])
         np.testing.assert_array_equal(F[sel][order][:, 3], ref["response"])
+
+
+def _check_full(got, ref):
+    assert len(got["pt"]) == len(ref["pt"])
+    for k in ("pt", "size", "angle", "response", "octave", "descriptors"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+@pytest.mark.parametrize("nfeatures,contrast,edge", [(0, 0.04, 10.0), (0, 0.02, 2.0), (150, 0.02, 2.0),
+                                                     (2048, 0.03, 1.0)])
+def test_detect_and_compute_matches_oracle(ctx, nfeatures, contrast, edge):
+    img = sift_scene(188, 620, seed=11, n_blobs=150)
+    got = sift.detect_and_compute(img, nfeatures, contrast, edge, 1.6, ctx=ctx)
+    ref = S.detect_and_compute(img, nfeatures, contrast, edge, 1.6)
+    _check_full(got, ref)
+
+
+def test_detect_and_compute_kitti_size(ctx):
+    # KITTI image_0 size with the reference's KITTI SIFT settings (config.py:64-66)
+    img = sift_scene(376, 1241, seed=7)
+    got = sift.detect_and_compute(img, 4000, 0.02, 2.0, 1.6, ctx=ctx)
+    ref = S.detect_and_compute(img, 4000, 0.02, 2.0, 1.6)
+    assert len(ref["pt"]) > 300
+    _check_full(got, ref)
+    # the nfeatures cut binds: 300 strongest (plus boundary ties)
+    got = sift.detect_and_compute(img, 300, 0.02, 2.0, 1.6, ctx=ctx)
+    ref = S.detect_and_compute(img, 300, 0.02, 2.0, 1.6)
+    _check_full(got, ref)
+
+
+def test_detect_and_compute_edge_cases(ctx):
+    flat = np.full((64, 64), 128, np.uint8)
+    r = sift.detect_and_compute(flat, ctx=ctx)
+    assert len(r["pt"]) == 0 and r["descriptors"].shape == (0, 128)
+    kps, des = sift.SIFT_create(nfeatures=10).detectAndCompute(flat, None)
+    assert kps == () and des is None
+    for h, w in ((23, 31), (11, 11), (100, 33)):
+        img = sift_scene(h, w, seed=h * w, n_blobs=5, n_boxes=2)
+        _check_full(sift.detect_and_compute(img, 0, 0.02, 2.0, 1.6, ctx=ctx), S.detect_and_compute(img, 0, 0.02, 2.0, 1.6))
+    img = sift_scene(188, 620, seed=11, n_blobs=150)
+    with pytest.raises(_lib.VoError):
+        sift.detect_and_compute(img, 0, 0.02, 2.0, 1.6, capacity=8, ctx=ctx)
+    # the context stays usable after the overflow
+    _check_full(sift.detect_and_compute(img, 50, 0.02, 2.0, 1.6, ctx=ctx), S.detect_and_compute(img, 50, 0.02, 2.0, 1.6))
+
+
+def test_sift_create_drop_in(ctx):
+    img = sift_scene(188, 620, seed=5, n_blobs=120)
+    det = sift.SIFT_create(nfeatures=4000, contrastThreshold=0.02, edgeThreshold=2.0, sigma=1.6)
+    kps, des = det.detectAndCompute(img, None)
+    ref = S.detect_and_compute(img, 4000, 0.02, 2.0, 1.6)
+    pts = np.array([k.pt for k in kps], dtype=np.float32)  # frontend.py:59
+    np.testing.assert_array_equal(pts, ref["pt"])
+    np.testing.assert_array_equal(np.array(des, dtype=np.float32), ref["descriptors"])
+    assert all(k.octave == o for k, o in zip(kps, ref["octave"]))
+
+
+def test_detect_and_compute_batch(ctx):
+    imgs = np.stack([sift_scene(188, 620, seed=s, n_blobs=100) for s in range(3)])
+    cap = 4096
+    dI = _lib.DeviceArray.from_numpy(ctx, imgs)
+    dK = _lib.DeviceArray(ctx, (3, cap, 8), np.int32)
+    dD = _lib.DeviceArray(ctx, (3, cap, 128), np.float32)
+    dC = _lib.DeviceArray(ctx, (3,), np.int32)
+    sift.detect_and_compute_device(dI, 200, 0.02, 2.0, 1.6, 3, dK, dD, dC, ctx=ctx)
+    counts = dC.numpy()
+    K = sift.unpack_device_keypoints(dK.numpy())
+    D = dD.numpy()
+    for b in range(3):
+        ref = S.detect_and_compute(imgs[b], 200, 0.02, 2.0, 1.6)
+        n = counts[b]
+        assert n == len(ref["pt"])
+        assert np.all(K[b, :n]["image"] == b)
+        got = sift._kp_dict(K[b, :n], D[b, :n])
+        _check_full(got, ref)

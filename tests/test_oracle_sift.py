@@ -93,3 +93,60 @@ def test_scene_detection_is_ordered_and_consistent():
     np.testing.assert_array_equal(o + 1, idx[:, 0])
     assert np.all((kp["octave"] >> 8 & 255) == idx[:, 1])
     assert np.all(np.abs(kp["xi"]) < 0.5)
+
+
+# ---- orientation / descriptors / keypoint filtering (oracle known answers) ---------------
+
+def test_exp32f_and_fast_atan2_accuracy():
+    x = np.linspace(-40, 0, 20001).astype(np.float32)
+    ref = np.exp(x.astype(np.float64))
+    assert np.max(np.abs(S.exp32f(x) - ref) / ref) < 2e-6
+    rng = np.random.default_rng(0)
+    y, xx = rng.normal(size=(2, 5000)).astype(np.float32)
+    a = S.fast_atan2(y, xx)
+    ref = np.degrees(np.arctan2(y, xx)) % 360
+    err = np.abs(a - ref)
+    assert np.max(np.minimum(err, 360 - err)) < 0.01  # OpenCV documents ~0.3 deg; this is tighter
+    assert np.all((a >= 0) & (a <= 360))
+
+
+def test_orientation_of_ramps():
+    x = np.arange(64, dtype=np.float32)
+    ramp = np.tile(2 * x, (64, 1)).astype(np.float32)
+    h, m = S.orientation_hist(ramp, 32, 32, 8, 3.0)
+    assert S.orientation_peaks(h, m) == [0.0]  # 360 - 0 snaps to 0
+    h, m = S.orientation_hist(np.ascontiguousarray(ramp.T), 32, 32, 8, 3.0)
+    assert S.orientation_peaks(h, m) == [90.0]  # dy = I(y-1) - I(y+1) < 0: gradient at 270
+    h, m = S.orientation_hist(np.full((32, 32), 5, np.float32), 16, 16, 6, 2.0)
+    assert m == 0 and S.orientation_peaks(h, m) == []
+
+
+def test_descriptor_known_answers():
+    x = np.arange(64, dtype=np.float32)
+    ramp = np.tile(2 * x, (64, 1)).astype(np.float32)
+    d = S.descriptor(ramp, 32.0, 32.0, 0.0, 2.0).reshape(16, 8)
+    assert d[:, 1:].sum() == 0 and np.all(d[:, 0] > 0)        # every vote in orientation bin 0
+    assert np.array_equal(d[:, 0].reshape(4, 4), d[:, 0].reshape(4, 4).T)  # symmetric window
+    assert S.descriptor(np.full((64, 64), 7, np.float32), 32.0, 32.0, 10.0, 2.0).sum() == 0
+    # rotating the window by 90 degrees on the transposed ramp gives the same descriptor
+    d90 = S.descriptor(np.ascontiguousarray(ramp.T), 32.0, 32.0, 270.0, 2.0).reshape(16, 8)
+    assert d90[:, 1:].sum() == 0 and np.abs(d90[:, 0] - d[:, 0]).max() <= 1
+
+
+def test_detect_and_compute_filtering():
+    img = sift_scene(188, 620, seed=3, n_blobs=150)
+    full = S.detect_and_compute(img, 0, 0.02, 2.0, 1.6, with_descriptors=False)
+    n = len(full["pt"])
+    assert n > 100
+    keys = list(zip(full["pt"][:, 0], full["pt"][:, 1], -full["size"], full["angle"]))
+    assert keys == sorted(keys) and len(set(keys)) == n  # sorted, no duplicates
+    cut = S.detect_and_compute(img, n // 3, 0.02, 2.0, 1.6, with_descriptors=False)
+    thr = np.sort(full["response"])[::-1][n // 3 - 1]
+    assert len(cut["pt"]) >= n // 3
+    assert np.all(cut["response"] >= thr)
+    assert np.sum(full["response"] >= thr) == len(cut["pt"])  # every tie at the boundary kept
+    big = S.detect_and_compute(img, 10 * n, 0.02, 2.0, 1.6, with_descriptors=False)
+    assert len(big["pt"]) == n
+    # orientation duplicates share the extremum: same pt/size, different angles
+    pts = {(a, b) for a, b in full["pt"]}
+    assert len(pts) < n

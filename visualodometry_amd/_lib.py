@@ -95,6 +95,8 @@ SIGNATURES = {
     "vo_sift_detect_batch_async": (_I, [_P, _P, _I, _I, _I, _D, _D, _D, _I, _I, _P, _P, _P]),
     "vo_sift_pyramid": (_I, [_P, C.POINTER(C.c_uint8), _I, _I, _D, _I, _PF, C.c_int64, _PF, C.c_int64]),
     "vo_sift_layout": (_I, [_I, _I, _I, _PI64, _I]),
+    "vo_sift_detect_and_compute": (_I, [_P, C.POINTER(C.c_uint8), _I, _I, _I, _D, _D, _D, _I, _I, _P, _PF, _PI32]),
+    "vo_sift_detect_and_compute_batch_async": (_I, [_P, _P, _I, _I, _I, _I, _D, _D, _D, _I, _I, _P, _P, _P]),
     "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
 }
@@ -218,7 +220,7 @@ class DeviceArray:
 
 KERNEL_NAMES = ["ba_lin", "ba_reduce", "ba_solve", "match_pack", "match_i8", "match_f32",
                 "match_merge", "triangulate", "pnp_hyp", "pnp_score", "pnp_final", "sift_pyramid",
-                "sift_extrema"]
+                "sift_extrema", "sift_orient", "sift_select", "sift_desc"]
 
 
 def profile_enable(ctx: "Context", on: bool = True) -> None:

@@ -397,6 +397,66 @@ int vo_sift_pyramid(vo_ctx* ctx, const uint8_t* img, int h, int w, double sigma,
   });
 }
 
+// detectAndCompute of a device batch: detection into the workspace's candidate list, then
+// orientation / filtering / descriptors into the caller's buffers.
+static void sift_full(vo_ctx* ctx, const uint8_t* d_imgs, int batch, int h, int w, int nfeatures, double contrast,
+               double edge, double sigma, int n_layers, int capacity, vo_sift_keypoint* d_kps, float* d_desc,
+               int32_t* d_counts) {
+  VO_REQUIRE(d_imgs && d_kps && d_desc && d_counts && batch >= 1 && capacity >= 1 && nfeatures >= 0, VO_ERR_ARG,
+             "sift detectAndCompute: bad arguments");
+  vo::SiftWorkspace& ws = ctx->sift;
+  const int cand_cap = (int)std::min<int64_t>((int64_t)batch * capacity, 1 << 24);
+  ws.cand.reserve((size_t)cand_cap * 64 + 64);
+  float* cf = ws.cand.as<float>();
+  int32_t* ci = reinterpret_cast<int32_t*>(cf + (size_t)cand_cap * 8);
+  int32_t* cc = ci + (size_t)cand_cap * 8;
+  float* G = nullptr;
+  vo::sift_run(ctx, d_imgs, batch, h, w, contrast, edge, sigma, n_layers, cand_cap, cf, ci, cc, &G, nullptr,
+               nullptr);
+  vo::sift_describe(ctx, batch, h, w, n_layers, sigma, nfeatures, capacity, cf, ci, cc, cand_cap, G, d_kps, d_desc,
+                    d_counts);
+}
+
+int vo_sift_detect_and_compute(vo_ctx* ctx, const uint8_t* img, int h, int w, int nfeatures, double contrast,
+                               double edge, double sigma, int n_layers, int capacity, vo_sift_keypoint* kps,
+                               float* desc, int32_t* count) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(img && kps && desc && count && capacity >= 1 && h >= 1 && w >= 1, VO_ERR_ARG,
+               "vo_sift_detect_and_compute: bad arguments");
+    vo::SiftWorkspace& ws = ctx->sift;
+    const size_t nimg = (size_t)h * w;
+    ws.img.reserve(nimg);
+    ws.out.reserve((size_t)capacity * (sizeof(vo_sift_keypoint) + 128 * sizeof(float)) + 64);
+    vo_sift_keypoint* dK = ws.out.as<vo_sift_keypoint>();
+    float* dD = reinterpret_cast<float*>(dK + capacity);
+    int32_t* dC = reinterpret_cast<int32_t*>(dD + (size_t)capacity * 128);
+    hipStream_t s = ctx->stream;
+    VO_HIP_CHECK(hipMemcpyAsync(ws.img.ptr, img, nimg, hipMemcpyHostToDevice, s));
+    sift_full(ctx, ws.img.as<uint8_t>(), 1, h, w, nfeatures, contrast, edge, sigma, n_layers, capacity, dK, dD, dC);
+    int32_t n = 0;
+    VO_HIP_CHECK(hipMemcpyAsync(&n, dC, 4, hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipStreamSynchronize(s));
+    VO_REQUIRE(n >= 0, VO_ERR_ARG, "vo_sift_detect_and_compute: more than capacity=%d keypoints", capacity);
+    *count = n;
+    if (n == 0) return;
+    VO_HIP_CHECK(hipMemcpyAsync(kps, dK, (size_t)n * sizeof(vo_sift_keypoint), hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipMemcpyAsync(desc, dD, (size_t)n * 128 * sizeof(float), hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipStreamSynchronize(s));
+  });
+}
+
+int vo_sift_detect_and_compute_batch_async(vo_ctx* ctx, const uint8_t* d_imgs, int batch, int h, int w,
+                                           int nfeatures, double contrast, double edge, double sigma,
+                                           int n_layers, int capacity, vo_sift_keypoint* d_kps, float* d_desc,
+                                           int32_t* d_counts) {
+  return guarded([&] {
+    vo::bind(ctx);
+    sift_full(ctx, d_imgs, batch, h, w, nfeatures, contrast, edge, sigma, n_layers, capacity, d_kps, d_desc,
+              d_counts);
+  });
+}
+
 int vo_sift_layout(int h, int w, int n_layers, int64_t* out, int n) {
   int rc = 0;
   const int st = guarded([&] {

@@ -245,7 +245,8 @@ __global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
   float* F = A.kp_f + (long)slot * kKpFloats;
   F[0] = ((float)cc + xc) * scale;
   F[1] = ((float)rr + xr) * scale;
-  F[2] = A.sigma * powf(2.0f, ((float)layer + xi) / (float)A.n_layers) * scale * 2.0f;
+  // powf(2, e) as (float)exp2((double)e): correctly rounded on host and device alike
+  F[2] = A.sigma * (float)exp2((double)(((float)layer + xi) / (float)A.n_layers)) * scale * 2.0f;
   F[3] = fabsf(contr);
   F[4] = xi;
   F[5] = F[6] = F[7] = 0.0f;

@@ -1,0 +1,608 @@
+// SIFT orientation assignment, keypoint filtering and descriptors on gfx950.
+//
+// The second half of cv2.SIFT_create(nfeatures, contrastThreshold, edgeThreshold, sigma)
+// .detectAndCompute(gray, None) (reference src/modules/frontend.py:27-32,55; OpenCV 4.12
+// sift.simd.hpp calcOrientationHist / calcSIFTDescriptor, sift.dispatch.cpp
+// detectAndCompute, keypoint.cpp removeDuplicatedSorted / retainBest), restated in
+// oracle/sift_ref.py.  FMA contraction is off and every histogram bin is summed in
+// OpenCV's sample order (row-major over the window), so orientations and descriptors are
+// bitwise the oracle's.
+//
+// After sift_run (sift.hip) has left the refined extrema in a candidate list:
+//   sift_orient_kernel    one 64-lane workgroup per extremum: the window's samples are
+//                         evaluated 64 at a time into LDS (bin, weighted magnitude), then
+//                         lane b < 36 sums the samples of bin b in sample order; [1 4 6 4 1]
+//                         smoothing, peaks >= 0.8 max appended per image with the
+//                         parabolic angle
+//   sift_keys_kernel      64-bit (x bits, y bits) sort keys per image region
+//   rocprim segmented radix sort (one segment per image): x asc, then y asc
+//   sift_select_kernel    one workgroup per image: runs of equal (x, y) ordered by (size
+//                         desc, angle asc, response desc, octave desc), duplicates in
+//                         (x, y, size, angle) dropped (removeDuplicatedSorted), the
+//                         nfeatures-th largest response found by a 4-pass radix select
+//                         (retainBest keeps every response >= it), ordered compaction
+//   sift_desc_kernel      one 256-thread workgroup per kept keypoint: phase 1 evaluates
+//                         the rotated window (gradient, fastAtan2, magnitude, exp32f) into
+//                         an LDS grid; phase 2 gives each of the 16 x 10 interior
+//                         (cell, orientation) bins a lane that walks the bounding box of
+//                         its cell's rotated footprint in sample order and adds its
+//                         trilinear share; phase 3 folds the circular orientation bins,
+//                         clips at 0.2 of the norm, renormalises to 512 and rounds.
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "sift_math.h"
+#include "vo_ctx.h"
+
+#pragma clang fp contract(off)
+
+namespace vo {
+namespace {
+
+using namespace siftm;
+
+constexpr int kMaxOct = 16;
+constexpr int kOriBins = 36;
+constexpr int kOriChunk = 1024;
+constexpr int kD = 4, kN = 8, kDesc = kD * kD * kN;
+constexpr int kMaxDescR = 40;                   // LDS window (2R+1)^2 samples
+constexpr int kGrid = (2 * kMaxDescR + 1) * (2 * kMaxDescR + 1);
+constexpr int kOkpFloats = 8;                   // x, y, size, angle, response (doubled-image units), octave word
+constexpr float kFltEps = 1.1920928955078125e-07f;
+
+struct Octaves {
+  int oh[kMaxOct], ow[kMaxOct], op[kMaxOct];
+  long off[kMaxOct];  // floats from the image's G base to the octave's level 0
+  long g_img;         // floats per image
+  int n_layers;
+};
+
+__device__ __forceinline__ const float* level_ptr(const float* G, const Octaves& O, int b, int o, int layer) {
+  return G + (long)b * O.g_img + O.off[o] + (long)layer * O.oh[o] * O.op[o];
+}
+
+// ---- orientation -------------------------------------------------------------------
+struct OriArgs {
+  const float* G;
+  Octaves O;
+  const float* cand_f;        // sift_run records (x, y, size, response, xi) in doubled-image units
+  const int32_t* cand_i;      // (image, octave word, cand level, level, row, col, cand row, cand col)
+  const int32_t* cand_count;
+  int cand_cap, cap_img;
+  float* okp;                 // (batch, cap_img, 8)
+  int32_t* img_count;         // (batch)
+  ExpTab tab;
+};
+
+__global__ __launch_bounds__(64) void sift_orient_kernel(OriArgs A) {
+  __shared__ int s_bin[kOriChunk];
+  __shared__ float s_val[kOriChunk];
+  __shared__ float s_th[kOriBins + 4];
+  __shared__ float s_h[kOriBins];
+  const int lane = threadIdx.x;
+  const int ncand = min(*A.cand_count, A.cand_cap);
+  for (int ci = blockIdx.x; ci < ncand; ci += gridDim.x) {
+    const float* F = A.cand_f + (long)ci * 8;
+    const int32_t* Q = A.cand_i + (long)ci * 8;
+    const int b = Q[0], word = Q[1], layer = Q[3], pr = Q[4], pc = Q[5];
+    const int o = word & 255;
+    const float size2 = F[2];
+    const float scl = size2 * 0.5f / (float)(1 << o);
+    const int radius = (int)rintf(4.5f * scl);
+    const float sigma = 1.5f * scl;
+    const float expf_scale = __fdiv_rn(-1.f, 2.f * sigma * sigma);
+    const float* img = level_ptr(A.G, A.O, b, o, layer);
+    const int rows = A.O.oh[o], cols = A.O.ow[o], pitch = A.O.op[o];
+    const int side = 2 * radius + 1, len = side * side;
+    float acc = 0.0f;
+    for (int k0 = 0; k0 < len; k0 += kOriChunk) {
+      const int kn = min(kOriChunk, len - k0);
+      for (int t = lane; t < kn; t += 64) {
+        const int k = k0 + t, i = k / side - radius, j = k % side - radius;
+        const int y = pr + i, x = pc + j;
+        int bin = -1;
+        float v = 0.0f;
+        if (y > 0 && y < rows - 1 && x > 0 && x < cols - 1) {
+          const float dx = img[(long)y * pitch + x + 1] - img[(long)y * pitch + x - 1];
+          const float dy = img[(long)(y - 1) * pitch + x] - img[(long)(y + 1) * pitch + x];
+          const float w = exp32f((float)(i * i + j * j) * expf_scale, A.tab.v);
+          const float ori = fast_atan2_deg(dy, dx);
+          const float mag = sqrt_rn(dx * dx + dy * dy);
+          bin = (int)rintf(((float)kOriBins / 360.f) * ori);
+          if (bin >= kOriBins) bin -= kOriBins;
+          if (bin < 0) bin += kOriBins;
+          v = w * mag;
+        }
+        s_bin[t] = bin;
+        s_val[t] = v;
+      }
+      __syncthreads();
+      // lane b sums the samples of bin b in sample order (+0.0 elsewhere: an identity,
+      // every partial sum is >= +0)
+      if (lane < kOriBins)
+        for (int t = 0; t < kn; ++t) acc = acc + (s_bin[t] == lane ? s_val[t] : 0.0f);
+      __syncthreads();
+    }
+    if (lane < kOriBins) s_th[lane + 2] = acc;
+    __syncthreads();
+    if (lane < 2) {
+      s_th[lane] = s_th[kOriBins + lane];             // temphist[-2], [-1]
+      s_th[kOriBins + 2 + lane] = s_th[2 + lane];     // temphist[n], [n+1]
+    }
+    __syncthreads();
+    float h = 0.0f;
+    if (lane < kOriBins) {
+      const float* T = s_th + 2 + lane;
+      h = (T[-2] + T[2]) * (1.f / 16.f) + (T[-1] + T[1]) * (4.f / 16.f) + T[0] * (6.f / 16.f);
+      s_h[lane] = h;
+    }
+    float m = lane < kOriBins ? h : -1.0f;
+    for (int s = 32; s >= 1; s >>= 1) m = fmaxf(m, __shfl_xor(m, s));
+    __syncthreads();
+    if (lane < kOriBins) {
+      const float mag_thr = m * 0.8f;
+      const int l = lane > 0 ? lane - 1 : kOriBins - 1, r2 = lane < kOriBins - 1 ? lane + 1 : 0;
+      const float hl = s_h[l], hr = s_h[r2];
+      if (h > hl && h > hr && h >= mag_thr) {
+        float bin = (float)lane + __fdiv_rn(0.5f * (hl - hr), (hl - 2.0f * h) + hr);
+        bin = bin < 0 ? (float)kOriBins + bin : (bin >= kOriBins ? bin - (float)kOriBins : bin);
+        float angle = 360.f - (360.f / kOriBins) * bin;
+        if (fabsf(angle - 360.f) < kFltEps) angle = 0.f;
+        const int slot = atomicAdd(A.img_count + b, 1);
+        if (slot < A.cap_img) {
+          float* R = A.okp + ((long)b * A.cap_img + slot) * kOkpFloats;
+          R[0] = F[0];
+          R[1] = F[1];
+          R[2] = size2;
+          R[3] = angle;
+          R[4] = F[3];
+          R[5] = __int_as_float(word);
+          R[6] = 0.0f;
+          R[7] = 0.0f;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- sort keys, segments -------------------------------------------------------------
+__global__ __launch_bounds__(256) void sift_keys_kernel(const float* __restrict__ okp, const int32_t* __restrict__ img_count,
+                                                        int cap_img, int batch, uint64_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ vals, int32_t* __restrict__ seg_beg,
+                                                        int32_t* __restrict__ seg_end) {
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  const int b = (int)(g / cap_img), s = (int)(g - (long)b * cap_img);
+  if (b >= batch) return;
+  if (s == 0) {
+    seg_beg[b] = b * cap_img;
+    seg_end[b] = b * cap_img + min(img_count[b], cap_img);
+  }
+  if (s >= min(img_count[b], cap_img)) return;
+  const float* R = okp + g * kOkpFloats;
+  // x, y > 0 (>= 4.5 octave pixels): the float bit patterns order like the values
+  keys[g] = ((uint64_t)__float_as_uint(R[0]) << 32) | __float_as_uint(R[1]);
+  vals[g] = (uint32_t)g;
+}
+
+// ---- removeDuplicatedSorted + retainBest + ordered compaction ------------------------
+struct SelArgs {
+  const float* okp;
+  const uint64_t* keys;  // sorted per image
+  uint32_t* vals;        // sorted per image (ties re-ordered in place)
+  const int32_t* img_count;
+  const int32_t* cand_count;
+  int cand_cap, cap_img, nfeatures;
+  uint32_t* sel;         // (batch, cap_img) record indices in output order
+  int32_t* sel_count;    // (batch): kept, or -1 when a capacity overflowed
+};
+
+__device__ __forceinline__ bool kp_less2(const float* a, const float* b) {
+  // KeyPoint12_LessThan after equal (x, y): size desc, angle asc, response desc, octave desc
+  if (a[2] != b[2]) return a[2] > b[2];
+  if (a[3] != b[3]) return a[3] < b[3];
+  if (a[4] != b[4]) return a[4] > b[4];
+  return __float_as_int(a[5]) > __float_as_int(b[5]);
+}
+
+constexpr int kSelThreads = 1024;
+constexpr int kMaxCapImg = 32768;
+
+__global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
+  __shared__ uint8_t keep[kMaxCapImg];
+  __shared__ int s_hist[256];
+  __shared__ int s_scan[kSelThreads];
+  __shared__ int s_total;
+  __shared__ uint32_t s_prefix, s_rank;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const long base = (long)b * A.cap_img;
+  const int cnt = A.img_count[b];
+  if (*A.cand_count > A.cand_cap || cnt > A.cap_img) {
+    if (tid == 0) A.sel_count[b] = -1;
+    return;
+  }
+  const int n = cnt;
+  const uint64_t* K = A.keys + base;
+  uint32_t* V = A.vals + base;
+  // runs of equal (x, y): insertion sort by the rest of the comparator (runs are short)
+  for (int i = tid; i < n; i += kSelThreads) {
+    if (i + 1 < n && K[i + 1] == K[i] && (i == 0 || K[i - 1] != K[i])) {
+      int e = i + 1;
+      while (e < n && K[e] == K[i]) ++e;
+      for (int p = i + 1; p < e; ++p) {
+        const uint32_t v = V[p];
+        const float* rv = A.okp + (long)v * kOkpFloats;
+        int q = p - 1;
+        while (q >= i && kp_less2(rv, A.okp + (long)V[q] * kOkpFloats)) {
+          V[q + 1] = V[q];
+          --q;
+        }
+        V[q + 1] = v;
+      }
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  int local = 0;
+  for (int i = tid; i < n; i += kSelThreads) {
+    bool k = true;
+    if (i > 0) {
+      const float* a = A.okp + (long)V[i - 1] * kOkpFloats;
+      const float* c = A.okp + (long)V[i] * kOkpFloats;
+      k = !(a[0] == c[0] && a[1] == c[1] && a[2] == c[2] && a[3] == c[3]);
+    }
+    keep[i] = k;
+    local += k;
+  }
+  if (tid == 0) s_total = 0;
+  __syncthreads();
+  atomicAdd(&s_total, local);
+  __syncthreads();
+  const int kept = s_total;
+  if (A.nfeatures > 0 && kept > A.nfeatures) {
+    // the nfeatures-th largest response among the kept: radix select, 8 bits per pass
+    if (tid == 0) {
+      s_prefix = 0;
+      s_rank = (uint32_t)A.nfeatures;
+    }
+    uint32_t mask = 0;
+    for (int pass = 3; pass >= 0; --pass) {
+      if (tid < 256) s_hist[tid] = 0;
+      __syncthreads();
+      const uint32_t prefix = s_prefix;
+      for (int i = tid; i < n; i += kSelThreads) {
+        if (!keep[i]) continue;
+        const uint32_t bits = __float_as_uint(A.okp[(long)V[i] * kOkpFloats + 4]);
+        if ((bits & mask) == prefix) atomicAdd(&s_hist[(bits >> (8 * pass)) & 255], 1);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t cum = 0, rank = s_rank;
+        int d = 255;
+        for (; d > 0; --d) {
+          if (cum + (uint32_t)s_hist[d] >= rank) break;
+          cum += (uint32_t)s_hist[d];
+        }
+        s_rank = rank - cum;
+        s_prefix = prefix | ((uint32_t)d << (8 * pass));
+      }
+      mask |= 255u << (8 * pass);
+      __syncthreads();
+    }
+    const uint32_t thr = s_prefix;
+    for (int i = tid; i < n; i += kSelThreads)
+      if (keep[i] && __float_as_uint(A.okp[(long)V[i] * kOkpFloats + 4]) < thr) keep[i] = 0;
+    __syncthreads();
+  }
+  // ordered compaction: thread t owns [t * per, (t + 1) * per)
+  const int per = (n + kSelThreads - 1) / kSelThreads;
+  const int lo = min(tid * per, n), hi = min(lo + per, n);
+  int c = 0;
+  for (int i = lo; i < hi; ++i) c += keep[i];
+  s_scan[tid] = c;
+  __syncthreads();
+  for (int off = 1; off < kSelThreads; off <<= 1) {
+    const int v = tid >= off ? s_scan[tid - off] : 0;
+    __syncthreads();
+    s_scan[tid] += v;
+    __syncthreads();
+  }
+  int pos = s_scan[tid] - c;
+  for (int i = lo; i < hi; ++i)
+    if (keep[i]) A.sel[base + pos++] = V[i];
+  if (tid == kSelThreads - 1) A.sel_count[b] = s_scan[tid];
+}
+
+// ---- descriptors ---------------------------------------------------------------------
+struct DescArgs {
+  const float* G;
+  Octaves O;
+  const float* okp;
+  const uint32_t* sel;
+  const int32_t* sel_count;
+  int batch, cap_img;
+  vo_sift_keypoint* kp_out;   // (batch, cap_img)
+  float* desc_out;            // (batch, cap_img, 128)
+  int32_t* count_out;         // (batch)
+  ExpTab tab;
+};
+
+constexpr int kDescThreads = 256;
+constexpr int kMaxBatch = 256;
+
+__global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
+  __shared__ float s_mag[kGrid];
+  __shared__ float s_obin[kGrid];
+  __shared__ float s_h10[16 * 10];
+  __shared__ float s_raw[kDesc];
+  __shared__ int s_off[kMaxBatch + 1];
+  __shared__ float s_nrm;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int acc = 0;
+    for (int b = 0; b < A.batch; ++b) {
+      s_off[b] = acc;
+      acc += max(A.sel_count[b], 0);
+    }
+    s_off[A.batch] = acc;
+  }
+  if (blockIdx.x == 0 && tid < A.batch) A.count_out[tid] = A.sel_count[tid];
+  __syncthreads();
+  const int total = s_off[A.batch];
+  for (int g = blockIdx.x; g < total; g += gridDim.x) {
+    int b = 0;
+    while (s_off[b + 1] <= g) ++b;
+    const int pos = g - s_off[b];
+    const float* R = A.okp + (long)A.sel[(long)b * A.cap_img + pos] * kOkpFloats;
+    const float x2 = R[0], y2 = R[1], size2 = R[2], angle = R[3], response = R[4];
+    const int word = __float_as_int(R[5]);
+    const int o = word & 255, layer = (word >> 8) & 255;
+    const float s = 1.0f / (float)(1 << o);
+    const float ptx = x2 * s, pty = y2 * s, scl = (size2 * s) * 0.5f;
+    float ori = 360.f - angle;
+    if (fabsf(ori - 360.f) < kFltEps) ori = 0.f;
+    const float* img = level_ptr(A.G, A.O, b, o, layer);
+    const int rows = A.O.oh[o], cols = A.O.ow[o], pitch = A.O.op[o];
+    const int px = (int)rintf(ptx), py = (int)rintf(pty);
+    const float a_rad = ori * (float)(3.14159265358979323846 / 180);
+    const float cos0 = (float)cos((double)a_rad), sin0 = (float)sin((double)a_rad);
+    const float bins_per_rad = (float)kN / 360.f;
+    const float exp_scale = -1.f / (kD * kD * 0.5f);
+    const float hist_width = 3.f * scl;
+    int radius = (int)rintf(hist_width * 1.4142135623730951f * (float)(kD + 1) * 0.5f);
+    radius = min(radius, (int)sqrt((double)cols * cols + (double)rows * rows));
+    radius = min(radius, kMaxDescR);  // the host bounds sigma so that this never binds
+    const float cos_t = __fdiv_rn(cos0, hist_width), sin_t = __fdiv_rn(sin0, hist_width);
+    const int side = 2 * radius + 1, len = side * side;
+    // phase 1: the window's samples (only those inside the descriptor and the image are
+    // read back; phase 2 repeats the same float tests)
+    for (int k = tid; k < len; k += kDescThreads) {
+      const int i = k / side - radius, j = k % side - radius;
+      const float c_rot = (float)j * cos_t - (float)i * sin_t;
+      const float r_rot = (float)j * sin_t + (float)i * cos_t;
+      const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
+      const int r = py + i, c = px + j;
+      if (rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 && c < cols - 1) {
+        const float dx = img[(long)r * pitch + c + 1] - img[(long)r * pitch + c - 1];
+        const float dy = img[(long)(r - 1) * pitch + c] - img[(long)(r + 1) * pitch + c];
+        const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, A.tab.v);
+        const float Ori = fast_atan2_deg(dy, dx);
+        const float Mag = sqrt_rn(dx * dx + dy * dy);
+        s_obin[k] = (Ori - ori) * bins_per_rad;
+        s_mag[k] = Mag * w;
+      }
+    }
+    __syncthreads();
+    // phase 2: lane -> (cell q, orientation slot O); the cell (Rc, Cc) of the (d+2)^2 grid
+    // receives from samples with r0 in {Rc-2, Rc-1}, c0 in {Cc-2, Cc-1}
+    if (tid < 160) {
+      const int q = tid / 10, O = tid % 10;
+      const int Rc = q / 4 + 1, Cc = q % 4 + 1;
+      // bounding box of r_rot in [Rc-3.5, Rc-1.5], c_rot in [Cc-3.5, Cc-1.5] (units of
+      // hist_width), mapped back to window coordinates, one sample of margin
+      float imin = 1e30f, imax = -1e30f, jmin = 1e30f, jmax = -1e30f;
+      for (int cr = 0; cr < 2; ++cr)
+        for (int cc = 0; cc < 2; ++cc) {
+          const float u = hist_width * ((float)Rc - 3.5f + 2.0f * cr);
+          const float v = hist_width * ((float)Cc - 3.5f + 2.0f * cc);
+          const float ii = u * cos0 - v * sin0, jj = u * sin0 + v * cos0;
+          imin = fminf(imin, ii);
+          imax = fmaxf(imax, ii);
+          jmin = fminf(jmin, jj);
+          jmax = fmaxf(jmax, jj);
+        }
+      const int i0 = max(-radius, (int)floorf(imin) - 1), i1 = min(radius, (int)ceilf(imax) + 1);
+      const int j0 = max(-radius, (int)floorf(jmin) - 1), j1 = min(radius, (int)ceilf(jmax) + 1);
+      float acc = 0.0f;
+      for (int i = i0; i <= i1; ++i) {
+        const int r = py + i;
+        if (r <= 0 || r >= rows - 1) continue;
+        for (int j = j0; j <= j1; ++j) {
+          const int c = px + j;
+          const float c_rot = (float)j * cos_t - (float)i * sin_t;
+          const float r_rot = (float)j * sin_t + (float)i * cos_t;
+          const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
+          if (!(rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && c > 0 && c < cols - 1)) continue;
+          const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
+          const int dr = Rc - 1 - r0, dc = Cc - 1 - c0;
+          if ((unsigned)dr > 1u || (unsigned)dc > 1u) continue;
+          const int k = (i + radius) * side + (j + radius);
+          const float obin = s_obin[k], mag = s_mag[k];
+          int o0 = (int)floorf(obin);
+          const float ob = obin - (float)o0;
+          if (o0 < 0) o0 += kN;
+          if (o0 >= kN) o0 -= kN;
+          const int dO = O - o0;
+          if ((unsigned)dO > 1u) continue;
+          const float rb = rbin - (float)r0, cb = cbin - (float)c0;
+          const float v_r1 = mag * rb, v_r0 = mag - v_r1;
+          const float vr = dr ? v_r1 : v_r0;
+          const float v_c1 = vr * cb, v_c0 = vr - v_c1;
+          const float vc = dc ? v_c1 : v_c0;
+          const float v_o1 = vc * ob, v_o0 = vc - v_o1;
+          acc = acc + (dO ? v_o1 : v_o0);
+        }
+      }
+      s_h10[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < kDesc) {
+      const int q = tid / kN, k = tid % kN;
+      float v = s_h10[q * 10 + k];
+      if (k < 2) v = v + s_h10[q * 10 + k + kN];
+      s_raw[tid] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float n2 = 0.0f;
+      for (int k = 0; k < kDesc; ++k) n2 = n2 + s_raw[k] * s_raw[k];
+      const float thr = sqrt_rn(n2) * 0.2f;
+      n2 = 0.0f;
+      for (int k = 0; k < kDesc; ++k) {
+        const float v = fminf(s_raw[k], thr);
+        n2 = n2 + v * v;
+      }
+      s_nrm = thr;
+      s_h10[0] = __fdiv_rn(512.f, fmaxf(sqrt_rn(n2), kFltEps));
+    }
+    __syncthreads();
+    const long out = (long)b * A.cap_img + pos;
+    if (tid < kDesc) {
+      const float v = fminf(s_raw[tid], s_nrm) * s_h10[0];
+      A.desc_out[out * kDesc + tid] = fminf(fmaxf(rintf(v), 0.0f), 255.0f);
+    }
+    if (tid == 0) {
+      vo_sift_keypoint kp;
+      kp.x = x2 * 0.5f;
+      kp.y = y2 * 0.5f;
+      kp.size = size2 * 0.5f;
+      kp.angle = angle;
+      kp.response = response;
+      kp.octave = (word & ~255) | ((o - 1) & 255);  // first octave -1
+      kp.image = b;
+      kp.reserved = 0;
+      A.kp_out[out] = kp;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+ExpTab make_exp_tab() {
+  ExpTab t;
+  for (int j = 0; j < 64; ++j) t.v[j] = (float)(std::pow(2.0, j / 64.0) * kExpA0);
+  return t;
+}
+
+// Orientation, filtering and descriptors of the candidates sift_run left in the workspace.
+void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double sigma, int nfeatures, int cap_img,
+                   const float* cand_f, const int32_t* cand_i, const int32_t* cand_count, int cand_cap,
+                   const float* G, vo_sift_keypoint* d_kp, float* d_desc, int32_t* d_count) {
+  VO_REQUIRE(batch >= 1 && batch <= kMaxBatch, VO_ERR_ARG, "sift: batch %d outside 1..%d", batch, kMaxBatch);
+  VO_REQUIRE(cap_img >= 1 && cap_img <= kMaxCapImg, VO_ERR_ARG, "sift: capacity %d outside 1..%d", cap_img,
+             kMaxCapImg);
+  // largest descriptor window: scl <= sigma 2^((n_layers + 0.5) / n_layers)
+  const double scl_max = sigma * std::pow(2.0, (n_layers + 0.5) / n_layers);
+  const int r_max = (int)std::ceil(3.0 * scl_max * 1.4142135623730951 * (kD + 1) * 0.5) + 1;
+  VO_REQUIRE(r_max <= kMaxDescR, VO_ERR_ARG,
+             "sift: sigma %g with %d layers needs a %d-sample descriptor radius (max %d)", sigma, n_layers, r_max,
+             kMaxDescR);
+  std::vector<int64_t> lay(3 + 5 * kMaxOct);
+  const int nv = sift_layout(h, w, n_layers, lay.data(), (int)lay.size());
+  VO_REQUIRE(nv <= (int)lay.size(), VO_ERR_ARG, "sift: %dx%d has too many octaves", h, w);
+  Octaves O{};
+  const int n_oct = (int)lay[0];
+  O.g_img = lay[1];
+  O.n_layers = n_layers;
+  for (int o = 0; o < n_oct; ++o) {
+    O.oh[o] = (int)lay[3 + 5 * o];
+    O.ow[o] = (int)lay[4 + 5 * o];
+    O.op[o] = (int)lay[5 + 5 * o];
+    O.off[o] = lay[6 + 5 * o];
+  }
+  SiftWorkspace& ws = ctx->sift;
+  const size_t slots = (size_t)batch * cap_img;
+  ws.okp.reserve(slots * kOkpFloats * sizeof(float));
+  ws.keys.reserve(slots * 2 * sizeof(uint64_t));
+  ws.vals.reserve(slots * 3 * sizeof(uint32_t));
+  ws.segs.reserve((size_t)4 * batch * sizeof(int32_t));
+  float* okp = ws.okp.as<float>();
+  uint64_t* keys_in = ws.keys.as<uint64_t>();
+  uint64_t* keys_out = keys_in + slots;
+  uint32_t* vals_in = ws.vals.as<uint32_t>();
+  uint32_t* vals_out = vals_in + slots;
+  uint32_t* sel = vals_out + slots;
+  int32_t* img_count = ws.segs.as<int32_t>();
+  int32_t* seg_beg = img_count + batch;
+  int32_t* seg_end = seg_beg + batch;
+  int32_t* sel_count = seg_end + batch;
+  hipStream_t st = ctx->stream;
+  const ExpTab tab = make_exp_tab();
+
+  ctx->prof.begin(st, kKSiftOrient);
+  VO_HIP_CHECK(hipMemsetAsync(img_count, 0, batch * sizeof(int32_t), st));
+  OriArgs oa;
+  oa.G = G;
+  oa.O = O;
+  oa.cand_f = cand_f;
+  oa.cand_i = cand_i;
+  oa.cand_count = cand_count;
+  oa.cand_cap = cand_cap;
+  oa.cap_img = cap_img;
+  oa.okp = okp;
+  oa.img_count = img_count;
+  oa.tab = tab;
+  // persistent: 64-lane workgroups looping over the candidates (count is on the device)
+  const int ori_blocks = std::max(1, std::min(cand_cap, ctx->num_cus * 32));
+  hipLaunchKernelGGL(sift_orient_kernel, dim3(ori_blocks), dim3(64), 0, st, oa);
+  VO_HIP_CHECK(hipGetLastError());
+  ctx->prof.end(st);
+
+  ctx->prof.begin(st, kKSiftSelect);
+  hipLaunchKernelGGL(sift_keys_kernel, dim3(ceil_div((int64_t)slots, 256)), dim3(256), 0, st, okp, img_count, cap_img,
+                     batch, keys_in, vals_in, seg_beg, seg_end);
+  size_t tmp_bytes = 0;
+  VO_HIP_CHECK(rocprim::segmented_radix_sort_pairs(nullptr, tmp_bytes, keys_in, keys_out, vals_in, vals_out,
+                                                   (unsigned)slots, (unsigned)batch, seg_beg, seg_end, 0, 64, st));
+  ws.sort_tmp.reserve(tmp_bytes);
+  VO_HIP_CHECK(rocprim::segmented_radix_sort_pairs(ws.sort_tmp.ptr, tmp_bytes, keys_in, keys_out, vals_in,
+                                                   vals_out, (unsigned)slots, (unsigned)batch, seg_beg, seg_end, 0,
+                                                   64, st));
+  SelArgs sa;
+  sa.okp = okp;
+  sa.keys = keys_out;
+  sa.vals = vals_out;
+  sa.img_count = img_count;
+  sa.cand_count = cand_count;
+  sa.cand_cap = cand_cap;
+  sa.cap_img = cap_img;
+  sa.nfeatures = nfeatures;
+  sa.sel = sel;
+  sa.sel_count = sel_count;
+  hipLaunchKernelGGL(sift_select_kernel, dim3(batch), dim3(kSelThreads), 0, st, sa);
+  VO_HIP_CHECK(hipGetLastError());
+  ctx->prof.end(st);
+
+  ctx->prof.begin(st, kKSiftDesc);
+  DescArgs da;
+  da.G = G;
+  da.O = O;
+  da.okp = okp;
+  da.sel = sel;
+  da.sel_count = sel_count;
+  da.batch = batch;
+  da.cap_img = cap_img;
+  da.kp_out = d_kp;
+  da.desc_out = d_desc;
+  da.count_out = d_count;
+  da.tab = tab;
+  hipLaunchKernelGGL(sift_desc_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(kDescThreads), 0, st, da);
+  VO_HIP_CHECK(hipGetLastError());
+  ctx->prof.end(st);
+}
+
+}  // namespace vo

@@ -109,7 +109,8 @@ __global__ __launch_bounds__(256) void tri_kernel(TriArgs a) {
   const float u = (float)__dadd_rn(__dmul_rn(xn, a.fx), a.cx);
   const float v = (float)__dadd_rn(__dmul_rn(yn, a.fy), a.cy);
   const float du = __fsub_rn(u, q2.x), dv = __fsub_rn(v, q2.y);
-  const float err = __fsqrt_rn(__fadd_rn(__fmul_rn(du, du), __fmul_rn(dv, dv)));
+  // correctly rounded sqrtf (__fsqrt_rn is the approximate native sqrt in this HIP)
+  const float err = (float)sqrt((double)__fadd_rn(__fmul_rn(du, du), __fmul_rn(dv, dv)));
   a.mask[i] = (zc > a.min_depth && err < a.max_err) ? 1 : 0;
 }
 

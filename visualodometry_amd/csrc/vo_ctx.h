@@ -39,6 +39,13 @@ struct SiftWorkspace {
   DevBuf g, d;     // float pyramids (pitched, all octaves)
   DevBuf img;      // host-call staging: the uint8 image
   DevBuf kp;       // host-call staging: keypoints + count
+  DevBuf cand;     // detectAndCompute: refined extrema (float + int records, count)
+  DevBuf okp;      // oriented keypoints (batch, capacity, 8 floats)
+  DevBuf keys;     // uint64 sort keys in / out
+  DevBuf vals;     // uint32 record indices in / out, then the selection
+  DevBuf segs;     // int32 per-image counts, segment bounds, kept counts
+  DevBuf sort_tmp; // rocprim temporary storage
+  DevBuf out;      // host-call staging: keypoints, descriptors, count
 };
 
 class BAEngine;   // ba.hip
@@ -47,7 +54,8 @@ struct Comm;      // ba.hip (RCCL communicator)
 // Kernel ids of the event profiler (vo_profile_* in include/vo_hip.h).
 enum KernelId {
   kKBaLin = 0, kKBaReduce, kKBaSolve, kKMatchPack, kKMatchI8, kKMatchF32, kKMatchMerge,
-  kKTriangulate, kKPnpHyp, kKPnpScore, kKPnpFinal, kKSiftPyramid, kKSiftExtrema, kKCount
+  kKTriangulate, kKPnpHyp, kKPnpScore, kKPnpFinal, kKSiftPyramid, kKSiftExtrema, kKSiftOrient, kKSiftSelect,
+  kKSiftDesc, kKCount
 };
 
 // HIP-event timing of individual kernels on the context stream (off by default).
@@ -101,4 +109,8 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
               double sigma, int n_layers, int capacity, float* d_kpf, int32_t* d_kpi, int32_t* d_count,
               float** g_out, float** d_out, int64_t* layout);
 int sift_layout(int h, int w, int n_layers, int64_t* out, int n);
+// SIFT orientation, filtering and descriptors (sift_desc.hip) of sift_run's candidates.
+void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double sigma, int nfeatures, int cap_img,
+                   const float* cand_f, const int32_t* cand_i, const int32_t* cand_count, int cand_cap,
+                   const float* G, vo_sift_keypoint* d_kp, float* d_desc, int32_t* d_count);
 }  // namespace vo

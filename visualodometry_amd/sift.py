@@ -1,11 +1,15 @@
-"""SIFT keypoint detection on the MI355X (detection half).
+"""SIFT on the MI355X: ``cv2.SIFT_create(...).detectAndCompute``.
 
-:func:`detect` runs the scale space, the DoG extrema and ``adjustLocalExtrema`` of OpenCV's
-SIFT (reference ``cv2.SIFT_create(...).detectAndCompute`` at
-``src/modules/frontend.py:27-32,55``) in ``vo_sift_detect`` (``csrc/sift.hip``); the
-restatement it is checked against is ``oracle/sift_ref.py``.  Orientation assignment and
-descriptors are not part of it yet.  Fails loudly without the HIP library (no CPU
-fallback).
+Reference: ``src/modules/frontend.py:27-32`` creates the extractor, ``:55`` calls
+``detectAndCompute(gray, None)`` and ``:59-60`` keeps ``k.pt`` and the float32 descriptors.
+
+* :func:`detect_and_compute` / :class:`SIFT` (``SIFT_create``): the whole call in
+  ``vo_sift_detect_and_compute`` (``csrc/sift.hip`` + ``csrc/sift_desc.hip``): scale space,
+  extrema, orientation, removeDuplicatedSorted, retainBest(nfeatures), descriptors.
+* :func:`detect`: the refined extrema alone (``vo_sift_detect``), for parity.
+
+The restatement both are checked against is ``oracle/sift_ref.py``.  Fails loudly without
+the HIP library (no CPU fallback).
 """
 
 from __future__ import annotations
@@ -86,3 +90,101 @@ def detect_device(d_imgs: _lib.DeviceArray, contrast: float, edge: float, sigma:
                                              float(edge), float(sigma), int(n_layers), int(d_kpf.shape[0]),
                                              C.c_void_p(d_kpf.ptr), C.c_void_p(d_kpi.ptr), C.c_void_p(d_count.ptr)),
           "vo_sift_detect_batch_async")
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                     ("octave", "<i4"), ("image", "<i4"), ("reserved", "<i4")])  # vo_sift_keypoint
+
+
+def _kp_dict(kp: np.ndarray, desc: np.ndarray) -> dict:
+    return {"pt": np.stack([kp["x"], kp["y"]], 1).astype(np.float32).reshape(-1, 2),
+            "size": kp["size"].copy(), "angle": kp["angle"].copy(), "response": kp["response"].copy(),
+            "octave": kp["octave"].copy(), "descriptors": desc}
+
+
+def detect_and_compute(gray, nfeatures: int = 0, contrast: float = 0.04, edge: float = 10.0, sigma: float = 1.6,
+                       n_layers: int = 3, capacity: int = 1 << 15, ctx: _lib.Context | None = None) -> dict:
+    """``SIFT_create(nfeatures, n_layers, contrast, edge, sigma).detectAndCompute(gray, None)``
+    -> dict: pt (N, 2), size, angle, response, octave, descriptors (N, 128) float32, in the
+    order of ``oracle/sift_ref.detect_and_compute``."""
+    ctx = ctx or _lib.context()
+    img = np.ascontiguousarray(np.asarray(gray, dtype=np.uint8))
+    if img.ndim != 2:
+        raise ValueError("detect_and_compute: a single-channel (h, w) uint8 image is expected")
+    h, w = img.shape
+    kp = np.zeros(capacity, KP_DTYPE)
+    desc = np.zeros((capacity, 128), np.float32)
+    cnt = C.c_int32(0)
+    check(ctx.lib.vo_sift_detect_and_compute(ctx.handle, ptr(img, C.c_uint8), h, w, int(nfeatures), float(contrast),
+                                             float(edge), float(sigma), int(n_layers), int(capacity),
+                                             kp.ctypes.data_as(C.c_void_p), ptr(desc, C.c_float), C.byref(cnt)),
+          "vo_sift_detect_and_compute")
+    n = cnt.value
+    return _kp_dict(kp[:n], desc[:n])
+
+
+def detect_and_compute_device(d_imgs: _lib.DeviceArray, nfeatures: int, contrast: float, edge: float, sigma: float,
+                              n_layers: int, d_kp: _lib.DeviceArray, d_desc: _lib.DeviceArray,
+                              d_counts: _lib.DeviceArray, ctx: _lib.Context | None = None) -> None:
+    """A batch of (batch, h, w) uint8 images in HBM (``vo_sift_detect_and_compute_batch_async``):
+    d_kp (batch, capacity, 8) 32-byte keypoint records, d_desc (batch, capacity, 128) float32,
+    d_counts (batch,) int32; enqueued."""
+    ctx = ctx or d_imgs.ctx
+    b, h, w = d_imgs.shape
+    cap = int(d_kp.shape[1])
+    if d_kp.shape[0] != b or d_desc.shape[:2] != (b, cap) or d_counts.shape[0] != b:
+        raise ValueError("detect_and_compute_device: output shapes do not match the batch")
+    check(ctx.lib.vo_sift_detect_and_compute_batch_async(
+        ctx.handle, C.c_void_p(d_imgs.ptr), b, h, w, int(nfeatures), float(contrast), float(edge), float(sigma),
+        int(n_layers), cap, C.c_void_p(d_kp.ptr), C.c_void_p(d_desc.ptr), C.c_void_p(d_counts.ptr)),
+        "vo_sift_detect_and_compute_batch_async")
+
+
+def unpack_device_keypoints(raw: np.ndarray) -> np.ndarray:
+    """(…, 8) 32-bit words copied back from a device keypoint buffer -> KP_DTYPE records."""
+    return np.ascontiguousarray(raw).view(KP_DTYPE).reshape(raw.shape[:-1])
+
+
+class KeyPoint:
+    """The fields of ``cv2.KeyPoint`` the reference reads (``frontend.py:59``: ``k.pt``)."""
+
+    __slots__ = ("pt", "size", "angle", "response", "octave", "class_id")
+
+    def __init__(self, x, y, size, angle, response, octave):
+        self.pt = (float(x), float(y))
+        self.size = float(size)
+        self.angle = float(angle)
+        self.response = float(response)
+        self.octave = int(octave)
+        self.class_id = -1
+
+
+class SIFT:
+    """``cv2.SIFT`` as the reference uses it: ``SIFT_create(nfeatures=..., contrastThreshold=...,
+    edgeThreshold=..., sigma=...)`` then ``detectAndCompute(gray, None) -> (keypoints,
+    descriptors)`` (``frontend.py:27-32,55``); descriptors is None when nothing is found, as in
+    OpenCV's Python binding."""
+
+    def __init__(self, nfeatures: int = 0, nOctaveLayers: int = 3, contrastThreshold: float = 0.04,
+                 edgeThreshold: float = 10.0, sigma: float = 1.6, ctx: _lib.Context | None = None):
+        self.nfeatures = int(nfeatures)
+        self.n_layers = int(nOctaveLayers)
+        self.contrast = float(contrastThreshold)
+        self.edge = float(edgeThreshold)
+        self.sigma = float(sigma)
+        self._ctx = ctx
+
+    def detectAndCompute(self, image, mask=None, descriptors=None, useProvidedKeypoints=False):
+        if mask is not None or useProvidedKeypoints:
+            raise NotImplementedError("SIFT.detectAndCompute: masks and provided keypoints are not supported")
+        r = detect_and_compute(image, self.nfeatures, self.contrast, self.edge, self.sigma, self.n_layers,
+                               ctx=self._ctx or _lib.context())
+        kps = tuple(KeyPoint(p[0], p[1], s, a, q, o) for p, s, a, q, o in
+                    zip(r["pt"], r["size"], r["angle"], r["response"], r["octave"]))
+        return kps, (r["descriptors"] if len(kps) else None)
+
+
+def SIFT_create(nfeatures: int = 0, nOctaveLayers: int = 3, contrastThreshold: float = 0.04,
+                edgeThreshold: float = 10.0, sigma: float = 1.6, **kw) -> SIFT:
+    """``cv2.SIFT_create`` (keyword names as the reference passes them, ``frontend.py:27-32``)."""
+    return SIFT(nfeatures, nOctaveLayers, contrastThreshold, edgeThreshold, sigma, **kw)
