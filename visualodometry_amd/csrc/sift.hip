@@ -9,9 +9,11 @@
 // A batch of equally sized images is processed level by level (one launch per pyramid
 // level for the whole batch, grid.z = image):
 //   sift_upsample_kernel  uint8 -> float32 doubled image (INTER_LINEAR, exact)
-//   sift_blur_kernel      one Gaussian level: a 64 x 16 output tile, its (16 + 2r) x
+//   sift_blur_r_kernel<R> one Gaussian level for tap radius R <= 16 (sift_blur_kernel for
+//                         wider kernels): a 64 x 16 output tile, its (16 + 2r) x
 //                         (64 + 2r) input tile staged in LDS (BORDER_REFLECT_101), the row
-//                         pass for the tile's rows into LDS, the column pass, and the DoG
+//                         pass for the tile's rows into LDS, the column pass (4 outputs per
+//                         thread from registers in both passes), and the DoG
 //                         D_{i-1} = G_i - G_{i-1} written beside G_i (HBM-bound: 16 B/pixel)
 //   sift_down_kernel      next octave's level 0 = every other pixel of level nOctaveLayers
 //   sift_extrema_kernel   per octave: one thread per DoG pixel of levels 1..nOctaveLayers,
@@ -118,6 +120,102 @@ __global__ __launch_bounds__(256) void sift_blur_kernel(const float* __restrict_
       if (prev) dog[(long)blockIdx.z * dog_stride + (long)gy * pitch + gx] = s - prev[o];
     }
   }
+}
+
+// The same level for tap radius R known at compile time: staging with the reflected row
+// and column indices computed once per row / column (none for interior tiles), and 4
+// outputs per thread in both passes from registers (float4 LDS reads); every output is
+// still s = 0, s = s + k_j x_j left to right, so the result is bitwise the generic kernel's.
+template <int R>
+__global__ __launch_bounds__(256) void sift_blur_r_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                          const float* __restrict__ prev, float* __restrict__ dog,
+                                                          int h, int w, int pitch, long stride, long dog_stride,
+                                                          Taps T) {
+  constexpr int TW = kTileW + 2 * R, TWP = (TW + 3) & ~3, TH = kTileH + 2 * R, NX = 4 + 2 * R;
+  __shared__ float4 in4[TH * TWP / 4];
+  __shared__ float4 tmp4[TH * kTileW / 4];
+  float* in = reinterpret_cast<float*>(in4);
+  float* tmp = reinterpret_cast<float*>(tmp4);
+  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH;
+  const long base = (long)blockIdx.z * stride;
+  const float* S = src + base;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const bool interior = x0 - R >= 0 && x0 + kTileW + R <= w && y0 - R >= 0 && y0 + kTileH + R <= h;
+  int gx0 = x0 + tx - R, gx1 = x0 + tx + 64 - R;
+  if (!interior) {
+    gx0 = reflect101(gx0, w);
+    gx1 = reflect101(gx1, w);
+  }
+  for (int r = ty; r < TH; r += 4) {
+    const int gy = interior ? y0 + r - R : reflect101(y0 + r - R, h);
+    const float* row = S + (long)gy * pitch;
+    in[r * TWP + tx] = row[gx0];
+    if (tx + 64 < TW) in[r * TWP + tx + 64] = row[gx1];
+  }
+  __syncthreads();
+  float k[2 * R + 1];
+#pragma unroll
+  for (int j = 0; j <= 2 * R; ++j) k[j] = T.k[j];
+  // row pass: TH rows x 16 column quads
+  for (int t = threadIdx.x; t < TH * 16; t += 256) {
+    const int r = t >> 4, q = (t & 15) * 4;
+    const float4* p = in4 + (r * TWP + q) / 4;
+    float x[(NX + 3) & ~3];
+#pragma unroll
+    for (int m = 0; m < (NX + 3) / 4; ++m) {
+      const float4 v = p[m];
+      x[4 * m] = v.x;
+      x[4 * m + 1] = v.y;
+      x[4 * m + 2] = v.z;
+      x[4 * m + 3] = v.w;
+    }
+    float o[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float s = 0.0f;
+#pragma unroll
+      for (int j = 0; j <= 2 * R; ++j) s = s + k[j] * x[u + j];
+      o[u] = s;
+    }
+    tmp4[(r * kTileW + q) / 4] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+  __syncthreads();
+  // column pass: column tx, rows 4 ty .. 4 ty + 3
+  float x[NX];
+#pragma unroll
+  for (int m = 0; m < NX; ++m) x[m] = tmp[(4 * ty + m) * kTileW + tx];
+  const int gx = x0 + tx;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j <= 2 * R; ++j) s = s + k[j] * x[u + j];
+    const int gy = y0 + 4 * ty + u;
+    if (gx < w && gy < h) {
+      const long o = base + (long)gy * pitch + gx;
+      dst[o] = s;
+      if (prev) dog[(long)blockIdx.z * dog_stride + (long)gy * pitch + gx] = s - prev[o];
+    }
+  }
+}
+
+// One Gaussian level through the radius-specialised kernel when there is one.
+void launch_blur(dim3 grid, hipStream_t st, const float* src, float* dst, const float* prev, float* dog, int h,
+                 int w, int pitch, long stride, long dog_stride, const Taps& T) {
+#define VO_BLUR_CASE(RR)                                                                                       \
+  case RR:                                                                                                     \
+    hipLaunchKernelGGL(sift_blur_r_kernel<RR>, grid, dim3(256), 0, st, src, dst, prev, dog, h, w, pitch, stride, \
+                       dog_stride, T);                                                                         \
+    return;
+  switch (T.r) {
+    VO_BLUR_CASE(1) VO_BLUR_CASE(2) VO_BLUR_CASE(3) VO_BLUR_CASE(4) VO_BLUR_CASE(5) VO_BLUR_CASE(6)
+    VO_BLUR_CASE(7) VO_BLUR_CASE(8) VO_BLUR_CASE(9) VO_BLUR_CASE(10) VO_BLUR_CASE(11) VO_BLUR_CASE(12)
+    VO_BLUR_CASE(13) VO_BLUR_CASE(14) VO_BLUR_CASE(15) VO_BLUR_CASE(16)
+    default:
+      hipLaunchKernelGGL(sift_blur_kernel, grid, dim3(256), 0, st, src, dst, prev, dog, h, w, pitch, stride,
+                         dog_stride, T);
+  }
+#undef VO_BLUR_CASE
 }
 
 __global__ __launch_bounds__(256) void sift_down_kernel(const float* __restrict__ src, int src_pitch, long src_stride,
@@ -360,16 +458,16 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
     if (o == 0) {
       // the doubled image goes to level 1's slot, which its own blur overwrites later
       hipLaunchKernelGGL(sift_upsample_kernel, px, dim3(256), 0, st, d_img, h, w, h * w, Go + lvl, op, g.g_img);
-      hipLaunchKernelGGL(sift_blur_kernel, tiles, dim3(256), 0, st, Go + lvl, Go, (const float*)nullptr,
-                         (float*)nullptr, oh, ow, op, g.g_img, g.d_img, make_taps((double)sig_diff));
+      launch_blur(tiles, st, Go + lvl, Go, nullptr, nullptr, oh, ow, op, g.g_img, g.d_img,
+                  make_taps((double)sig_diff));
     } else {
       const long src = g.g_off[o - 1] + (long)n_layers * g.oh[o - 1] * g.op[o - 1];
       hipLaunchKernelGGL(sift_down_kernel, px, dim3(256), 0, st, G + src, g.op[o - 1], g.g_img, Go, oh, ow, op,
                          g.g_img);
     }
     for (int i = 1; i < n_layers + 3; ++i)
-      hipLaunchKernelGGL(sift_blur_kernel, tiles, dim3(256), 0, st, Go + (i - 1) * lvl, Go + i * lvl,
-                         Go + (i - 1) * lvl, Do + (i - 1) * lvl, oh, ow, op, g.g_img, g.d_img, make_taps(sig[i]));
+      launch_blur(tiles, st, Go + (i - 1) * lvl, Go + i * lvl, Go + (i - 1) * lvl, Do + (i - 1) * lvl, oh, ow, op,
+                  g.g_img, g.d_img, make_taps(sig[i]));
     VO_HIP_CHECK(hipGetLastError());
   }
   ctx->prof.end(st);

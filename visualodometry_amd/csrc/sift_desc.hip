@@ -21,13 +21,16 @@
 //                         (x, y, size, angle) dropped (removeDuplicatedSorted), the
 //                         nfeatures-th largest response found by a 4-pass radix select
 //                         (retainBest keeps every response >= it), ordered compaction
-//   sift_desc_kernel      one 256-thread workgroup per kept keypoint: phase 1 evaluates
-//                         the rotated window (gradient, fastAtan2, magnitude, exp32f) into
-//                         an LDS grid; phase 2 gives each of the 16 x 10 interior
-//                         (cell, orientation) bins a lane that walks the bounding box of
-//                         its cell's rotated footprint in sample order and adds its
-//                         trilinear share; phase 3 folds the circular orientation bins,
-//                         clips at 0.2 of the norm, renormalises to 512 and rounds.
+//   sift_desc_kernel      one 256-thread workgroup per kept keypoint, the rotated window in
+//                         blocks of 256 positions: each thread evaluates one sample
+//                         (gradient, fastAtan2, magnitude, exp32f, row and column
+//                         interpolation) and appends it to the stable LDS lists of the (up
+//                         to 4) interior cells it votes into (one ballot per cell and wave);
+//                         then wave w owns descriptor cell row w + 1, lanes 0..35 its
+//                         (column, orientation) bins, and each lane walks its cell's list in
+//                         window order adding its orientation share; finally the circular
+//                         orientation bins are folded, clipped at 0.2 of the norm,
+//                         renormalised to 512 and rounded.
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include <algorithm>
@@ -48,8 +51,6 @@ constexpr int kMaxOct = 16;
 constexpr int kOriBins = 36;
 constexpr int kOriChunk = 1024;
 constexpr int kD = 4, kN = 8, kDesc = kD * kD * kN;
-constexpr int kMaxDescR = 40;                   // LDS window (2R+1)^2 samples
-constexpr int kGrid = (2 * kMaxDescR + 1) * (2 * kMaxDescR + 1);
 constexpr int kOkpFloats = 8;                   // x, y, size, angle, response (doubled-image units), octave word
 constexpr float kFltEps = 1.1920928955078125e-07f;
 
@@ -78,8 +79,10 @@ struct OriArgs {
 };
 
 __global__ __launch_bounds__(64) void sift_orient_kernel(OriArgs A) {
-  __shared__ int s_bin[kOriChunk];
-  __shared__ float s_val[kOriChunk];
+  __shared__ int4 s_bin4[kOriChunk / 4];
+  __shared__ float4 s_val4[kOriChunk / 4];
+  int* s_bin = reinterpret_cast<int*>(s_bin4);
+  float* s_val = reinterpret_cast<float*>(s_val4);
   __shared__ float s_th[kOriBins + 4];
   __shared__ float s_h[kOriBins];
   const int lane = threadIdx.x;
@@ -122,8 +125,27 @@ __global__ __launch_bounds__(64) void sift_orient_kernel(OriArgs A) {
       __syncthreads();
       // lane b sums the samples of bin b in sample order (+0.0 elsewhere: an identity,
       // every partial sum is >= +0)
-      if (lane < kOriBins)
-        for (int t = 0; t < kn; ++t) acc = acc + (s_bin[t] == lane ? s_val[t] : 0.0f);
+      if (lane < kOriBins) {
+        // sixteen samples per LDS wait
+        int t = 0;
+        for (; t + 16 <= kn; t += 16) {
+          int4 bb[4];
+          float4 vv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            bb[u] = s_bin4[(t >> 2) + u];
+            vv[u] = s_val4[(t >> 2) + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            acc = acc + (bb[u].x == lane ? vv[u].x : 0.0f);
+            acc = acc + (bb[u].y == lane ? vv[u].y : 0.0f);
+            acc = acc + (bb[u].z == lane ? vv[u].z : 0.0f);
+            acc = acc + (bb[u].w == lane ? vv[u].w : 0.0f);
+          }
+        }
+        for (; t < kn; ++t) acc = acc + (s_bin[t] == lane ? s_val[t] : 0.0f);
+      }
       __syncthreads();
     }
     if (lane < kOriBins) s_th[lane + 2] = acc;
@@ -334,13 +356,17 @@ constexpr int kDescThreads = 256;
 constexpr int kMaxBatch = 256;
 
 __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
-  __shared__ float s_mag[kGrid];
-  __shared__ float s_obin[kGrid];
-  __shared__ float s_h10[16 * 10];
-  __shared__ float s_raw[kDesc];
+  // per 256-position block of the window: for each of the 16 interior cells, the samples
+  // that vote into it, in window order, as (obin, value after the row and column
+  // interpolation)
+  __shared__ float2 s_list[16][kDescThreads];
+  __shared__ int s_cnt[kDescThreads / 64][16];
+  __shared__ float s_h[16 * 9];
+  __shared__ float4 s_raw4[kDesc / 4];
   __shared__ int s_off[kMaxBatch + 1];
-  __shared__ float s_nrm;
-  const int tid = threadIdx.x;
+  __shared__ float s_scale[2];
+  float* s_raw = reinterpret_cast<float*>(s_raw4);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) {
     int acc = 0;
     for (int b = 0; b < A.batch; ++b) {
@@ -352,6 +378,11 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
   if (blockIdx.x == 0 && tid < A.batch) A.count_out[tid] = A.sel_count[tid];
   __syncthreads();
   const int total = s_off[A.batch];
+  // consumer ownership: wave w -> cell row Rc = w + 1 of the (d+2)^2 grid; lane < 36 ->
+  // cell column Cc = lane / 9 + 1 and orientation slot O = lane % 9 (slot 9 never receives:
+  // o0 + 1 <= n)
+  const int Rc = wave + 1, Cc = lane / 9 + 1, O = lane % 9;
+  const int my_cell = (Rc - 1) * 4 + (Cc - 1);
   for (int g = blockIdx.x; g < total; g += gridDim.x) {
     int b = 0;
     while (s_off[b + 1] <= g) ++b;
@@ -374,104 +405,126 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
     const float hist_width = 3.f * scl;
     int radius = (int)rintf(hist_width * 1.4142135623730951f * (float)(kD + 1) * 0.5f);
     radius = min(radius, (int)sqrt((double)cols * cols + (double)rows * rows));
-    radius = min(radius, kMaxDescR);  // the host bounds sigma so that this never binds
     const float cos_t = __fdiv_rn(cos0, hist_width), sin_t = __fdiv_rn(sin0, hist_width);
     const int side = 2 * radius + 1, len = side * side;
-    // phase 1: the window's samples (only those inside the descriptor and the image are
-    // read back; phase 2 repeats the same float tests)
-    for (int k = tid; k < len; k += kDescThreads) {
-      const int i = k / side - radius, j = k % side - radius;
-      const float c_rot = (float)j * cos_t - (float)i * sin_t;
-      const float r_rot = (float)j * sin_t + (float)i * cos_t;
-      const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
-      const int r = py + i, c = px + j;
-      if (rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 && c < cols - 1) {
-        const float dx = img[(long)r * pitch + c + 1] - img[(long)r * pitch + c - 1];
-        const float dy = img[(long)(r - 1) * pitch + c] - img[(long)(r + 1) * pitch + c];
-        const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, A.tab.v);
-        const float Ori = fast_atan2_deg(dy, dx);
-        const float Mag = sqrt_rn(dx * dx + dy * dy);
-        s_obin[k] = (Ori - ori) * bins_per_rad;
-        s_mag[k] = Mag * w;
-      }
-    }
-    __syncthreads();
-    // phase 2: lane -> (cell q, orientation slot O); the cell (Rc, Cc) of the (d+2)^2 grid
-    // receives from samples with r0 in {Rc-2, Rc-1}, c0 in {Cc-2, Cc-1}
-    if (tid < 160) {
-      const int q = tid / 10, O = tid % 10;
-      const int Rc = q / 4 + 1, Cc = q % 4 + 1;
-      // bounding box of r_rot in [Rc-3.5, Rc-1.5], c_rot in [Cc-3.5, Cc-1.5] (units of
-      // hist_width), mapped back to window coordinates, one sample of margin
-      float imin = 1e30f, imax = -1e30f, jmin = 1e30f, jmax = -1e30f;
-      for (int cr = 0; cr < 2; ++cr)
-        for (int cc = 0; cc < 2; ++cc) {
-          const float u = hist_width * ((float)Rc - 3.5f + 2.0f * cr);
-          const float v = hist_width * ((float)Cc - 3.5f + 2.0f * cc);
-          const float ii = u * cos0 - v * sin0, jj = u * sin0 + v * cos0;
-          imin = fminf(imin, ii);
-          imax = fmaxf(imax, ii);
-          jmin = fminf(jmin, jj);
-          jmax = fmaxf(jmax, jj);
+    float acc = 0.0f;
+    for (int k0 = 0; k0 < len; k0 += kDescThreads) {
+      const int k = k0 + tid;
+      bool valid = false;
+      int r0 = -9, c0 = -9;
+      float obin = 0.0f, v_r0 = 0.0f, v_r1 = 0.0f, cb = 0.0f;
+      if (k < len) {
+        const int i = k / side - radius, j = k % side - radius;
+        const float c_rot = (float)j * cos_t - (float)i * sin_t;
+        const float r_rot = (float)j * sin_t + (float)i * cos_t;
+        const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
+        const int r = py + i, c = px + j;
+        valid = rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 &&
+                c < cols - 1;
+        if (valid) {
+          const float dx = img[(long)r * pitch + c + 1] - img[(long)r * pitch + c - 1];
+          const float dy = img[(long)(r - 1) * pitch + c] - img[(long)(r + 1) * pitch + c];
+          const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, A.tab.v);
+          const float Ori = fast_atan2_deg(dy, dx);
+          const float Mag = sqrt_rn(dx * dx + dy * dy);
+          obin = (Ori - ori) * bins_per_rad;
+          const float mag = Mag * w;
+          r0 = (int)floorf(rbin);
+          c0 = (int)floorf(cbin);
+          const float rb = rbin - (float)r0;
+          cb = cbin - (float)c0;
+          v_r1 = mag * rb;
+          v_r0 = mag - v_r1;
         }
-      const int i0 = max(-radius, (int)floorf(imin) - 1), i1 = min(radius, (int)ceilf(imax) + 1);
-      const int j0 = max(-radius, (int)floorf(jmin) - 1), j1 = min(radius, (int)ceilf(jmax) + 1);
-      float acc = 0.0f;
-      for (int i = i0; i <= i1; ++i) {
-        const int r = py + i;
-        if (r <= 0 || r >= rows - 1) continue;
-        for (int j = j0; j <= j1; ++j) {
-          const int c = px + j;
-          const float c_rot = (float)j * cos_t - (float)i * sin_t;
-          const float r_rot = (float)j * sin_t + (float)i * cos_t;
-          const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
-          if (!(rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && c > 0 && c < cols - 1)) continue;
-          const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
-          const int dr = Rc - 1 - r0, dc = Cc - 1 - c0;
-          if ((unsigned)dr > 1u || (unsigned)dc > 1u) continue;
-          const int k = (i + radius) * side + (j + radius);
-          const float obin = s_obin[k], mag = s_mag[k];
-          int o0 = (int)floorf(obin);
-          const float ob = obin - (float)o0;
+      }
+      // stable per-cell lists: the sample votes into cells (r0 + 1 + dr, c0 + 1 + dc)
+      const uint64_t lt = (1ull << lane) - 1ull;
+      uint64_t bal[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int dr = q / 4 - r0, dc = q % 4 - c0;  // cell (q/4 + 1, q%4 + 1)
+        bal[q] = __ballot(valid && (unsigned)dr <= 1u && (unsigned)dc <= 1u);
+        if (lane == 0) s_cnt[wave][q] = __popcll(bal[q]);
+      }
+      __syncthreads();
+      if (valid) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int dr = q / 4 - r0, dc = q % 4 - c0;
+          if ((unsigned)dr <= 1u && (unsigned)dc <= 1u) {
+            int off = __popcll(bal[q] & lt);
+            for (int w = 0; w < wave; ++w) off += s_cnt[w][q];
+            const float vr = dr ? v_r1 : v_r0;
+            const float v_c1 = vr * cb, v_c0 = vr - v_c1;
+            s_list[q][off] = make_float2(obin, dc ? v_c1 : v_c0);
+          }
+        }
+      }
+      __syncthreads();
+      // the owner of (cell, O) adds its orientation share of each entry, in order (+0.0 when
+      // missed: an identity, every partial sum is >= +0)
+      if (lane < 36) {
+        const int n = s_cnt[0][my_cell] + s_cnt[1][my_cell] + s_cnt[2][my_cell] + s_cnt[3][my_cell];
+        const float2* L = s_list[my_cell];
+        auto step = [&](const float2 e) {
+          int o0 = (int)floorf(e.x);
+          const float ob = e.x - (float)o0;
           if (o0 < 0) o0 += kN;
           if (o0 >= kN) o0 -= kN;
           const int dO = O - o0;
-          if ((unsigned)dO > 1u) continue;
-          const float rb = rbin - (float)r0, cb = cbin - (float)c0;
-          const float v_r1 = mag * rb, v_r0 = mag - v_r1;
-          const float vr = dr ? v_r1 : v_r0;
-          const float v_c1 = vr * cb, v_c0 = vr - v_c1;
-          const float vc = dc ? v_c1 : v_c0;
-          const float v_o1 = vc * ob, v_o0 = vc - v_o1;
-          acc = acc + (dO ? v_o1 : v_o0);
+          const float v_o1 = e.y * ob, v_o0 = e.y - v_o1;
+          acc = acc + ((unsigned)dO <= 1u ? (dO ? v_o1 : v_o0) : 0.0f);
+        };
+        int t = 0;
+        for (; t + 4 <= n; t += 4) {
+          float2 e[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) e[u] = L[t + u];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) step(e[u]);
         }
+        for (; t < n; ++t) step(L[t]);
       }
-      s_h10[tid] = acc;
+      __syncthreads();
     }
+    if (lane < 36) s_h[((Rc - 1) * 4 + (Cc - 1)) * 9 + O] = acc;
     __syncthreads();
     if (tid < kDesc) {
       const int q = tid / kN, k = tid % kN;
-      float v = s_h10[q * 10 + k];
-      if (k < 2) v = v + s_h10[q * 10 + k + kN];
+      float v = s_h[q * 9 + k];
+      if (k == 0) v = v + s_h[q * 9 + kN];  // hist[idx] += hist[idx + n] (slot n + 1 is zero)
       s_raw[tid] = v;
     }
     __syncthreads();
     if (tid == 0) {
+      // the two norms in element order (OpenCV's scalar loops)
       float n2 = 0.0f;
-      for (int k = 0; k < kDesc; ++k) n2 = n2 + s_raw[k] * s_raw[k];
+#pragma unroll 8
+      for (int k = 0; k < kDesc / 4; ++k) {
+        const float4 v = s_raw4[k];
+        n2 = n2 + v.x * v.x;
+        n2 = n2 + v.y * v.y;
+        n2 = n2 + v.z * v.z;
+        n2 = n2 + v.w * v.w;
+      }
       const float thr = sqrt_rn(n2) * 0.2f;
       n2 = 0.0f;
-      for (int k = 0; k < kDesc; ++k) {
-        const float v = fminf(s_raw[k], thr);
-        n2 = n2 + v * v;
+#pragma unroll 8
+      for (int k = 0; k < kDesc / 4; ++k) {
+        const float4 v = s_raw4[k];
+        const float a = fminf(v.x, thr), bb = fminf(v.y, thr), c = fminf(v.z, thr), d = fminf(v.w, thr);
+        n2 = n2 + a * a;
+        n2 = n2 + bb * bb;
+        n2 = n2 + c * c;
+        n2 = n2 + d * d;
       }
-      s_nrm = thr;
-      s_h10[0] = __fdiv_rn(512.f, fmaxf(sqrt_rn(n2), kFltEps));
+      s_scale[0] = thr;
+      s_scale[1] = __fdiv_rn(512.f, fmaxf(sqrt_rn(n2), kFltEps));
     }
     __syncthreads();
     const long out = (long)b * A.cap_img + pos;
     if (tid < kDesc) {
-      const float v = fminf(s_raw[tid], s_nrm) * s_h10[0];
+      const float v = fminf(s_raw[tid], s_scale[0]) * s_scale[1];
       A.desc_out[out * kDesc + tid] = fminf(fmaxf(rintf(v), 0.0f), 255.0f);
     }
     if (tid == 0) {
@@ -505,12 +558,6 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   VO_REQUIRE(batch >= 1 && batch <= kMaxBatch, VO_ERR_ARG, "sift: batch %d outside 1..%d", batch, kMaxBatch);
   VO_REQUIRE(cap_img >= 1 && cap_img <= kMaxCapImg, VO_ERR_ARG, "sift: capacity %d outside 1..%d", cap_img,
              kMaxCapImg);
-  // largest descriptor window: scl <= sigma 2^((n_layers + 0.5) / n_layers)
-  const double scl_max = sigma * std::pow(2.0, (n_layers + 0.5) / n_layers);
-  const int r_max = (int)std::ceil(3.0 * scl_max * 1.4142135623730951 * (kD + 1) * 0.5) + 1;
-  VO_REQUIRE(r_max <= kMaxDescR, VO_ERR_ARG,
-             "sift: sigma %g with %d layers needs a %d-sample descriptor radius (max %d)", sigma, n_layers, r_max,
-             kMaxDescR);
   std::vector<int64_t> lay(3 + 5 * kMaxOct);
   const int nv = sift_layout(h, w, n_layers, lay.data(), (int)lay.size());
   VO_REQUIRE(nv <= (int)lay.size(), VO_ERR_ARG, "sift: %dx%d has too many octaves", h, w);
