@@ -1,5 +1,7 @@
 """Drop-in hooks on CPU: window assembly, write-back, method patching."""
 
+import types
+
 import numpy as np
 import pytest
 
@@ -120,6 +122,30 @@ def test_match_frames_routing():
     d = {"descriptors": np.zeros((1, 5, 128), np.float32)}
     with pytest.raises(_lib.VoError):  # the SIFT branch goes to the HIP library, never a CPU path
         patched(_Front("sift"), d, d)
+
+
+def test_frontend_init_swaps_in_the_gpu_sift():
+    class FrontSift:
+        def __init__(self, config):
+            self.conf = config
+            self.extractor = "cv2.SIFT"
+
+    patched = hooks._wrap_frontend_init(FrontSift.__init__)
+    cfg = types.SimpleNamespace(extractor_type="sift", sift_n_features=4000, sift_contrast_threshold=0.02,
+                                sift_edge_threshold=2.0,
+                                sift_sigma=1.6)
+    f = FrontSift.__new__(FrontSift)
+    patched(f, cfg)
+    from visualodometry_amd import sift
+
+    assert isinstance(f.extractor, sift.SIFT)
+    assert (f.extractor.nfeatures, f.extractor.contrast, f.extractor.edge, f.extractor.sigma) == (4000, 0.02, 2.0, 1.6)
+    f = FrontSift.__new__(FrontSift)
+    patched(f, types.SimpleNamespace(extractor_type="sift", sift_on_gpu=False))
+    assert f.extractor == "cv2.SIFT"
+    f = FrontSift.__new__(FrontSift)
+    patched(f, types.SimpleNamespace(extractor_type="superpoint"))
+    assert f.extractor == "cv2.SIFT"
 
 
 def test_install_is_idempotent():

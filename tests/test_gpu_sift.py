@@ -107,6 +107,15 @@ def test_detect_and_compute_kitti_size(ctx):
     _check_full(got, ref)
 
 
+def test_detect_and_compute_textured_kitti(ctx):
+    # ~7.8k keypoints: the nfeatures = 4000 cut of the reference's KITTI config binds
+    img = sift_scene(376, 1241, seed=200, texture=12.0)
+    got = sift.detect_and_compute(img, 4000, 0.02, 2.0, 1.6, ctx=ctx)
+    ref = S.detect_and_compute(img, 4000, 0.02, 2.0, 1.6)
+    assert len(ref["pt"]) >= 4000
+    _check_full(got, ref)
+
+
 def test_detect_and_compute_edge_cases(ctx):
     flat = np.full((64, 64), 128, np.uint8)
     r = sift.detect_and_compute(flat, ctx=ctx)

@@ -49,6 +49,7 @@ class VOConfig:
     ba_fixed: int = 2  # oldest keyframes held fixed (gauge)
     ba_iters: int = 10  # Gauss-Newton iterations per keyframe
     ba_lambda: float = 1.0  # fixed Levenberg damping (identical in oracle and kernel)
+    sift_on_gpu: bool = True  # SIFT detectAndCompute on the MI355X (frontend.py:27-32,55)
     match_on_gpu: bool = True  # SIFT matching on the MI355X (knn-2 + ratio test)
     triangulate_on_gpu: bool = True  # triangulate_points on the MI355X (DLT + filters)
     pnp_on_gpu: bool = True  # cv2.solvePnPRansac of the tracking step on the MI355X

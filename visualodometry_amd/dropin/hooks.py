@@ -4,6 +4,10 @@ Nothing of the reference is copied: :func:`install` patches methods of the
 reference's own classes and names of its modules once they are imported (cv2 etc.
 are the caller's environment):
 
+* ``FeatureFrontend.__init__`` (reference ``src/modules/frontend.py:10-34``): with the SIFT
+  extractor and ``cfg.sift_on_gpu`` (default on), ``self.extractor`` becomes
+  :func:`visualodometry_amd.sift.SIFT_create` with the same nfeatures / contrast / edge /
+  sigma, so ``process_image`` (``:51-75``) runs detectAndCompute on the MI355X.
 * ``FeatureFrontend.match_frames`` (reference ``src/modules/frontend.py:78-113``),
   SIFT branch -> :func:`visualodometry_amd.matcher.match_knn2_ratio`.  The
   LightGlue branch (``:80-84``) is left to the original method.
@@ -245,6 +249,20 @@ def _wrap_reset(orig):
 _PNP_ON_GPU = [True]  # set from the VO config at construction (cfg.pnp_on_gpu)
 
 
+def _wrap_frontend_init(orig):
+    from .. import sift
+
+    def __init__(self, config, *args, **kw):  # FeatureFrontend(config), frontend.py:10
+        orig(self, config, *args, **kw)
+        if getattr(config, "extractor_type", None) == "sift" and getattr(config, "sift_on_gpu", True):
+            self.extractor = sift.SIFT_create(nfeatures=config.sift_n_features,
+                                              contrastThreshold=config.sift_contrast_threshold,
+                                              edgeThreshold=config.sift_edge_threshold, sigma=config.sift_sigma)
+
+    __init__._vo_amd_wrapped = orig
+    return __init__
+
+
 def _wrap_match_frames(orig):
     from .. import matcher
 
@@ -305,6 +323,8 @@ def install(frontend_cls=None, vo_cls=None) -> None:
         f = getattr(mod, "triangulate_points", None) if mod is not None else None
         if f is not None and not hasattr(f, "_vo_amd_wrapped"):
             mod.triangulate_points = _wrap_triangulate(f)
+    if not hasattr(frontend_cls.__init__, "_vo_amd_wrapped"):
+        frontend_cls.__init__ = _wrap_frontend_init(frontend_cls.__init__)
     if not hasattr(frontend_cls.match_frames, "_vo_amd_wrapped"):
         frontend_cls.match_frames = _wrap_match_frames(frontend_cls.match_frames)
     if not hasattr(vo_cls._create_keyframe, "_vo_amd_wrapped"):

@@ -327,11 +327,14 @@ def pnp_case(n: int, seed: int, noise_px: float = 0.3, outlier_frac: float = 0.2
     return X32, uv.astype(np.float32), K, T_cw, out
 
 
-def sift_scene(h: int = 376, w: int = 1241, seed: int = 0, n_blobs: int = 400, n_boxes: int = 60) -> np.ndarray:
+def sift_scene(h: int = 376, w: int = 1241, seed: int = 0, n_blobs: int = 400, n_boxes: int = 60,
+               texture: float = 0.0) -> np.ndarray:
     """A uint8 grayscale image of KITTI's size (``image_0``, ``dataset_loader.py:63``) with
     SIFT-detectable structure: a smooth vertical gradient, Gaussian blobs of 2-10 px
     sigma (light and dark), axis-aligned boxes (edges and corners) and 2 gray levels of
-    noise."""
+    noise.  ``texture`` > 0 adds cubic value noise at 3, 6 and 12 px scales of that
+    amplitude (gray levels): at 12 a KITTI-size image has ~7.8k SIFT keypoints at the
+    reference's KITTI settings, so its ``nfeatures = 4000`` cut binds as on real frames."""
     rng = np.random.default_rng(seed)
     yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
     im = 70.0 + 60.0 * yy / h
@@ -347,4 +350,11 @@ def sift_scene(h: int = 376, w: int = 1241, seed: int = 0, n_blobs: int = 400, n
         g = np.exp(-((yy[y0:y1, x0:x1] - cy) ** 2 + (xx[y0:y1, x0:x1] - cx) ** 2) / (2 * s * s))
         im[y0:y1, x0:x1] += rng.choice([-1.0, 1.0]) * rng.uniform(40, 90) * g
     im += rng.normal(0, 2.0, im.shape)
+    if texture > 0:
+        from scipy.ndimage import zoom
+
+        trng = np.random.default_rng(seed + 99)
+        for sc in (3, 6, 12):
+            g = trng.normal(0, 1, (h // sc + 2, w // sc + 2))
+            im += texture * zoom(g, sc, order=3)[:h, :w]
     return np.clip(np.rint(im), 0, 255).astype(np.uint8)
