@@ -139,7 +139,7 @@ FP64_VECTOR_PEAK_TFLOPS = 78.6  # 256 CUs x 4 SIMDs x 32 FLOP/clk (4-cycle wave6
 TRI_FLOPS_PER_POINT = 2892      # DLT 32 + 5 Jacobi sweeps (typical; a wave stops once converged) x 6 pairs x ~92 + ~100
 
 
-def bench_triangulate(ctx, n: int = 1_000_000, calls: int = 20, warmup: int = 3):
+def bench_triangulate(ctx, n: int = 1_000_000, calls: int = 200, warmup: int = 3):
     """device-resident triangulation throughput (points/s)."""
     from visualodometry_amd import _lib, triangulate
     from visualodometry_amd.synthetic import triangulation_case
