@@ -17,9 +17,10 @@
 //                         D_{i-1} = G_i - G_{i-1} written beside G_i (HBM-bound: 16 B/pixel)
 //   sift_down_kernel      next octave's level 0 = every other pixel of level nOctaveLayers
 //   sift_extrema_kernel   per octave: one thread per DoG pixel of levels 1..nOctaveLayers,
-//                         the 26-neighbour test, then adjustLocalExtrema for the (rare)
-//                         candidates; accepted keypoints appended with an atomic counter
-//                         and put in (image, octave, level, row, column) order on the host.
+//                         the 26-neighbour test; extrema appended to a candidate list
+//   sift_refine_kernel    adjustLocalExtrema, one thread per candidate of every octave;
+//                         accepted keypoints appended with an atomic counter and put in
+//                         (image, octave, level, row, column) order on the host.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -227,15 +228,41 @@ __global__ __launch_bounds__(256) void sift_down_kernel(const float* __restrict_
       src[(long)blockIdx.z * src_stride + (long)(2 * y) * src_pitch + 2 * x];
 }
 
+constexpr int kMaxOctaves = 16;
+constexpr int kCandRegions = 64;  // candidate appends spread over this many counters
+
+// Per-octave DoG geometry of a batch (all octaves in one launch of the refinement).
+struct DogGeom {
+  const float* dog;                 // DoG pyramid base
+  long img_stride;                  // floats per image
+  long off[kMaxOctaves];            // octave's first DoG level
+  int h[kMaxOctaves], w[kMaxOctaves], pitch[kMaxOctaves];
+};
+
 struct ExtArgs {
   const float* dog;  // octave's DoG levels: level l of image b at dog + b * img_stride + l * lvl_stride
   long img_stride, lvl_stride;
-  int h, w, pitch, n_layers, octave, threshold, capacity;
+  int h, w, pitch, n_layers, octave, threshold;
+  uint64_t* cand;    // packed (image, octave, level, row, column) of the 26-neighbour extrema:
+  int cand_cap;      //   kCandRegions regions of cand_cap entries,
+  int32_t* cand_n;   //   each with its own append counter
+};
+
+struct RefArgs {
+  DogGeom G;
+  int n_layers, capacity;
   float contrast, edge, sigma;
+  const uint64_t* cand;  // kCandRegions x cand_cap
+  int cand_cap;
+  const int32_t* cand_n;  // kCandRegions counters
   float* kp_f;       // (capacity, kKpFloats)
   int32_t* kp_i;     // (capacity, kKpInts)
   int32_t* count;
 };
+
+__device__ __forceinline__ uint64_t pack_cand(int b, int o, int layer, int r, int c) {
+  return ((uint64_t)b << 48) | ((uint64_t)o << 44) | ((uint64_t)layer << 40) | ((uint64_t)r << 20) | (uint64_t)c;
+}
 
 __device__ __forceinline__ float at(const float* L, int pitch, int r, int c) { return L[(long)r * pitch + c]; }
 
@@ -256,33 +283,16 @@ __device__ __forceinline__ void solve3(const float (&a)[3][3], const float (&b)[
               b[0] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]));
 }
 
-__global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int r = blockIdx.y * 4 + (threadIdx.x >> 6);
-  const int lz = blockIdx.z % A.n_layers, b = blockIdx.z / A.n_layers;
-  const int layer0 = lz + 1;
-  if (c < kBorder || c >= A.w - kBorder || r < kBorder || r >= A.h - kBorder) return;
-  const float* D = A.dog + (long)b * A.img_stride;
-  const float* img = D + (long)layer0 * A.lvl_stride;
-  const float val = at(img, A.pitch, r, c);
-  if (!(fabsf(val) > (float)A.threshold)) return;
-  const float* prv = img - A.lvl_stride;
-  const float* nxt = img + A.lvl_stride;
-  bool is_max = val > 0, is_min = val < 0;
-#pragma unroll
-  for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-    for (int dx = -1; dx <= 1; ++dx) {
-      const float a = at(prv, A.pitch, r + dy, c + dx), n = at(nxt, A.pitch, r + dy, c + dx);
-      is_max = is_max && val >= a && val >= n;
-      is_min = is_min && val <= a && val <= n;
-      if (dy != 0 || dx != 0) {
-        const float s = at(img, A.pitch, r + dy, c + dx);
-        is_max = is_max && val >= s;
-        is_min = is_min && val <= s;
-      }
-    }
-  if (!is_max && !is_min) return;
+struct ExtView {
+  long lvl_stride;
+  int h, w, pitch, n_layers, octave, capacity;
+  float contrast, edge, sigma;
+  float* kp_f;
+  int32_t* kp_i;
+  int32_t* count;
+};
+
+__device__ __forceinline__ void refine_one(const ExtView& A, const float* D, int b, int layer0, int r, int c) {
   // adjustLocalExtrema (oracle/sift_ref.py adjust_local_extremum)
   const float img_scale = 1.0f / 255.0f;
   const float deriv_scale = img_scale * 0.5f, second = img_scale, cross = img_scale * 0.25f;
@@ -357,6 +367,87 @@ __global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
   Q[5] = cc;
   Q[6] = r;
   Q[7] = c;
+}
+
+// One thread per DoG pixel of levels 1..n_layers: the 26-neighbour test; extrema are
+// appended to the candidate list (refined by sift_refine_kernel, all octaves at once, so
+// the few candidates do not hold a whole wave each through the Newton steps).
+__global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int r = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int lz = blockIdx.z % A.n_layers, b = blockIdx.z / A.n_layers;
+  const int layer0 = lz + 1;
+  bool ext = false;
+  if (c >= kBorder && c < A.w - kBorder && r >= kBorder && r < A.h - kBorder) {
+    const float* D = A.dog + (long)b * A.img_stride;
+    const float* img = D + (long)layer0 * A.lvl_stride;
+    const float val = at(img, A.pitch, r, c);
+    if (fabsf(val) > (float)A.threshold) {
+      const float* prv = img - A.lvl_stride;
+      const float* nxt = img + A.lvl_stride;
+      bool is_max = val > 0, is_min = val < 0;
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const float a = at(prv, A.pitch, r + dy, c + dx), n = at(nxt, A.pitch, r + dy, c + dx);
+          is_max = is_max && val >= a && val >= n;
+          is_min = is_min && val <= a && val <= n;
+          if (dy != 0 || dx != 0) {
+            const float s = at(img, A.pitch, r + dy, c + dx);
+            is_max = is_max && val >= s;
+            is_min = is_min && val <= s;
+          }
+        }
+      ext = is_max || is_min;
+    }
+  }
+  // one append per wave (ballot + the lane's rank), on one of kCandRegions counters
+  const uint64_t bal = __ballot(ext);
+  if (bal == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)bal) - 1;
+  const int region = (int)((blockIdx.x + 7u * blockIdx.y + 13u * blockIdx.z + (threadIdx.x >> 6)) % kCandRegions);
+  int base = 0;
+  if (lane == leader) base = atomicAdd(A.cand_n + region, __popcll(bal));
+  base = __shfl(base, leader);
+  if (ext) {
+    const int slot = base + __popcll(bal & ((1ull << lane) - 1ull));
+    if (slot < A.cand_cap) A.cand[(long)region * A.cand_cap + slot] = pack_cand(b, A.octave, layer0, r, c);
+  }
+}
+
+// adjustLocalExtrema for every candidate of the batch, one thread each (grid-stride over
+// the device-side count); accepted keypoints appended with an atomic counter.
+__global__ __launch_bounds__(256) void sift_refine_kernel(RefArgs RA) {
+  const int region = blockIdx.y;
+  const int ncand = RA.cand_n[region];
+  if (ncand > RA.cand_cap) {  // candidates were dropped: poison the count (host raises)
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(RA.count, 1 << 30);
+    return;
+  }
+  const uint64_t* cand = RA.cand + (long)region * RA.cand_cap;
+  for (int ci = blockIdx.x * 256 + threadIdx.x; ci < ncand; ci += gridDim.x * 256) {
+    const uint64_t pc = cand[ci];
+    const int b = (int)(pc >> 48), o = (int)((pc >> 44) & 15), layer0 = (int)((pc >> 40) & 15);
+    const int r = (int)((pc >> 20) & 0xFFFFF), c = (int)(pc & 0xFFFFF);
+    ExtView A;
+    A.h = RA.G.h[o];
+    A.w = RA.G.w[o];
+    A.pitch = RA.G.pitch[o];
+    A.lvl_stride = (long)A.h * A.pitch;
+    A.n_layers = RA.n_layers;
+    A.octave = o;
+    A.capacity = RA.capacity;
+    A.contrast = RA.contrast;
+    A.edge = RA.edge;
+    A.sigma = RA.sigma;
+    A.kp_f = RA.kp_f;
+    A.kp_i = RA.kp_i;
+    A.count = RA.count;
+    const float* D = RA.G.dog + (long)b * RA.G.img_stride + RA.G.off[o];
+    refine_one(A, D, b, layer0, r, c);
+  }
 }
 
 Taps make_taps(double sigma) {
@@ -471,6 +562,17 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
     VO_HIP_CHECK(hipGetLastError());
   }
   ctx->prof.end(st);
+  // candidate lists of the 26-neighbour extrema (kCandRegions regions with their own
+  // counters): at most one per 9 pixels of a level, bounded here by a quarter of the
+  // candidate levels' pixels (overflow poisons the keypoint count)
+  int64_t cand_px = 0;
+  for (int o = 0; o < g.n_oct; ++o) cand_px += (int64_t)g.oh[o] * g.ow[o];
+  const int cand_cap = (int)std::min<int64_t>(((int64_t)batch * n_layers * cand_px / 4) / kCandRegions + 1024,
+                                              (int64_t)1 << 26);  // per region
+  ws.cand_ext.reserve((size_t)kCandRegions * cand_cap * sizeof(uint64_t) + kCandRegions * sizeof(int32_t));
+  uint64_t* cand = ws.cand_ext.as<uint64_t>();
+  int32_t* cand_n = reinterpret_cast<int32_t*>(cand + (size_t)kCandRegions * cand_cap);
+  VO_HIP_CHECK(hipMemsetAsync(cand_n, 0, kCandRegions * sizeof(int32_t), st));
   ctx->prof.begin(st, kKSiftExtrema);
   for (int o = 0; o < g.n_oct; ++o) {
     const int oh = g.oh[o], ow = g.ow[o];
@@ -485,15 +587,34 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
     A.n_layers = n_layers;
     A.octave = o;
     A.threshold = threshold;
-    A.capacity = capacity;
-    A.contrast = (float)contrast;
-    A.edge = (float)edge;
-    A.sigma = sf;
-    A.kp_f = d_kpf;
-    A.kp_i = d_kpi;
-    A.count = d_count;
+    A.cand = cand;
+    A.cand_cap = cand_cap;
+    A.cand_n = cand_n;
     hipLaunchKernelGGL(sift_extrema_kernel, dim3(ceil_div(ow, 64), ceil_div(oh, 4), batch * n_layers), dim3(256),
                        0, st, A);
+  }
+  if (capacity > 0 || d_kpf) {
+    RefArgs R{};
+    R.G.dog = Dg;
+    R.G.img_stride = g.d_img;
+    for (int o = 0; o < g.n_oct; ++o) {
+      R.G.off[o] = g.d_off[o];
+      R.G.h[o] = g.oh[o];
+      R.G.w[o] = g.ow[o];
+      R.G.pitch[o] = g.op[o];
+    }
+    R.n_layers = n_layers;
+    R.capacity = capacity;
+    R.contrast = (float)contrast;
+    R.edge = (float)edge;
+    R.sigma = sf;
+    R.cand = cand;
+    R.cand_cap = cand_cap;
+    R.cand_n = cand_n;
+    R.kp_f = d_kpf;
+    R.kp_i = d_kpi;
+    R.count = d_count;
+    hipLaunchKernelGGL(sift_refine_kernel, dim3(std::max(1, ctx->num_cus / 4), kCandRegions), dim3(256), 0, st, R);
   }
   ctx->prof.end(st);
   VO_HIP_CHECK(hipGetLastError());

@@ -23,12 +23,12 @@
 //                         (retainBest keeps every response >= it), ordered compaction
 //   sift_desc_kernel      one 256-thread workgroup per kept keypoint, the rotated window in
 //                         blocks of 256 positions: each thread evaluates one sample
-//                         (gradient, fastAtan2, magnitude, exp32f, row and column
-//                         interpolation) and appends it to the stable LDS lists of the (up
-//                         to 4) interior cells it votes into (one ballot per cell and wave);
-//                         then wave w owns descriptor cell row w + 1, lanes 0..35 its
-//                         (column, orientation) bins, and each lane walks its cell's list in
-//                         window order adding its orientation share; finally the circular
+//                         (gradient, fastAtan2, magnitude, exp32f, trilinear shares) and
+//                         appends it to the stable LDS lists of the (up to 4) interior
+//                         cells it votes into as (o0, share to o0, share to o0 + 1) (one
+//                         ballot per cell and wave); then wave w owns descriptor cell row
+//                         w + 1, lanes 0..35 its (column, orientation) bins, and each lane
+//                         walks its cell's list in window order adding its share; finally the circular
 //                         orientation bins are folded, clipped at 0.2 of the norm,
 //                         renormalised to 512 and rounded.
 #include <rocprim/device/device_segmented_radix_sort.hpp>
@@ -359,7 +359,8 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
   // per 256-position block of the window: for each of the 16 interior cells, the samples
   // that vote into it, in window order, as (obin, value after the row and column
   // interpolation)
-  __shared__ float2 s_list[16][kDescThreads];
+  __shared__ float2 s_list[16][kDescThreads];   // (v_o0, v_o1): the two orientation shares
+  __shared__ uint8_t s_o0[16][kDescThreads];     // the lower orientation bin o0 (wrapped)
   __shared__ int s_cnt[kDescThreads / 64][16];
   __shared__ float s_h[16 * 9];
   __shared__ float4 s_raw4[kDesc / 4];
@@ -412,7 +413,8 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
       const int k = k0 + tid;
       bool valid = false;
       int r0 = -9, c0 = -9;
-      float obin = 0.0f, v_r0 = 0.0f, v_r1 = 0.0f, cb = 0.0f;
+      float ob = 0.0f, v_r0 = 0.0f, v_r1 = 0.0f, cb = 0.0f;
+      int o0 = 0;
       if (k < len) {
         const int i = k / side - radius, j = k % side - radius;
         const float c_rot = (float)j * cos_t - (float)i * sin_t;
@@ -427,8 +429,12 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
           const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, A.tab.v);
           const float Ori = fast_atan2_deg(dy, dx);
           const float Mag = sqrt_rn(dx * dx + dy * dy);
-          obin = (Ori - ori) * bins_per_rad;
+          const float obin = (Ori - ori) * bins_per_rad;
           const float mag = Mag * w;
+          o0 = (int)floorf(obin);
+          ob = obin - (float)o0;
+          if (o0 < 0) o0 += kN;
+          if (o0 >= kN) o0 -= kN;
           r0 = (int)floorf(rbin);
           c0 = (int)floorf(cbin);
           const float rb = rbin - (float)r0;
@@ -456,7 +462,10 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
             for (int w = 0; w < wave; ++w) off += s_cnt[w][q];
             const float vr = dr ? v_r1 : v_r0;
             const float v_c1 = vr * cb, v_c0 = vr - v_c1;
-            s_list[q][off] = make_float2(obin, dc ? v_c1 : v_c0);
+            const float vc = dc ? v_c1 : v_c0;
+            const float v_o1 = vc * ob, v_o0 = vc - v_o1;
+            s_list[q][off] = make_float2(v_o0, v_o1);
+            s_o0[q][off] = (uint8_t)o0;
           }
         }
       }
@@ -466,24 +475,21 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
       if (lane < 36) {
         const int n = s_cnt[0][my_cell] + s_cnt[1][my_cell] + s_cnt[2][my_cell] + s_cnt[3][my_cell];
         const float2* L = s_list[my_cell];
-        auto step = [&](const float2 e) {
-          int o0 = (int)floorf(e.x);
-          const float ob = e.x - (float)o0;
-          if (o0 < 0) o0 += kN;
-          if (o0 >= kN) o0 -= kN;
+        const uint8_t* L0 = s_o0[my_cell];
+        auto step = [&](const float2 e, const int o0) {
           const int dO = O - o0;
-          const float v_o1 = e.y * ob, v_o0 = e.y - v_o1;
-          acc = acc + ((unsigned)dO <= 1u ? (dO ? v_o1 : v_o0) : 0.0f);
+          acc = acc + (dO == 0 ? e.x : (dO == 1 ? e.y : 0.0f));
         };
         int t = 0;
         for (; t + 4 <= n; t += 4) {
           float2 e[4];
+          const uint32_t o4 = *reinterpret_cast<const uint32_t*>(L0 + t);
 #pragma unroll
           for (int u = 0; u < 4; ++u) e[u] = L[t + u];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) step(e[u]);
+          for (int u = 0; u < 4; ++u) step(e[u], (o4 >> (8 * u)) & 255);
         }
-        for (; t < n; ++t) step(L[t]);
+        for (; t < n; ++t) step(L[t], L0[t]);
       }
       __syncthreads();
     }

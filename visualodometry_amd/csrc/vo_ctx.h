@@ -39,6 +39,7 @@ struct SiftWorkspace {
   DevBuf g, d;     // float pyramids (pitched, all octaves)
   DevBuf img;      // host-call staging: the uint8 image
   DevBuf kp;       // host-call staging: keypoints + count
+  DevBuf cand_ext; // packed 26-neighbour extrema awaiting refinement + their count
   DevBuf cand;     // detectAndCompute: refined extrema (float + int records, count)
   DevBuf okp;      // oriented keypoints (batch, capacity, 8 floats)
   DevBuf keys;     // uint64 sort keys in / out
