@@ -14,8 +14,8 @@
 //                         lane b < 36 sums the samples of bin b in sample order; [1 4 6 4 1]
 //                         smoothing, peaks >= 0.8 max appended per image with the
 //                         parabolic angle
-//   sift_keys_kernel      64-bit (x bits, y bits) sort keys per image region
-//   rocprim segmented radix sort (one segment per image): x asc, then y asc
+//   sift_keys_kernel      64-bit sort keys (image | x bits | y bits, 10 + 27 + 27 bits)
+//   rocprim radix sort of the whole batch at once: image, then x asc, then y asc
 //   sift_select_kernel    one workgroup per image: runs of equal (x, y) ordered by (size
 //                         desc, angle asc, response desc, octave desc), duplicates in
 //                         (x, y, size, angle) dropped (removeDuplicatedSorted), the
@@ -31,7 +31,7 @@
 //                         walks its cell's list in window order adding its share; finally the circular
 //                         orientation bins are folded, clipped at 0.2 of the norm,
 //                         renormalised to 512 and rounded.
-#include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -194,20 +194,20 @@ __global__ __launch_bounds__(64) void sift_orient_kernel(OriArgs A) {
 // ---- sort keys, segments -------------------------------------------------------------
 __global__ __launch_bounds__(256) void sift_keys_kernel(const float* __restrict__ okp, const int32_t* __restrict__ img_count,
                                                         int cap_img, int batch, uint64_t* __restrict__ keys,
-                                                        uint32_t* __restrict__ vals, int32_t* __restrict__ seg_beg,
-                                                        int32_t* __restrict__ seg_end) {
+                                                        uint32_t* __restrict__ vals) {
   const long g = (long)blockIdx.x * 256 + threadIdx.x;
   const int b = (int)(g / cap_img), s = (int)(g - (long)b * cap_img);
   if (b >= batch) return;
-  if (s == 0) {
-    seg_beg[b] = b * cap_img;
-    seg_end[b] = b * cap_img + min(img_count[b], cap_img);
-  }
-  if (s >= min(img_count[b], cap_img)) return;
-  const float* R = okp + g * kOkpFloats;
-  // x, y > 0 (>= 4.5 octave pixels): the float bit patterns order like the values
-  keys[g] = ((uint64_t)__float_as_uint(R[0]) << 32) | __float_as_uint(R[1]);
   vals[g] = (uint32_t)g;
+  if (s >= min(img_count[b], cap_img)) {
+    keys[g] = ~0ull;  // unused slot: after every image
+    return;
+  }
+  const float* R = okp + g * kOkpFloats;
+  // x, y in [4.5, 32768) doubled-image pixels: their float bits minus those of 2.0 fit in
+  // 27 bits and order like the values
+  const uint64_t xb = __float_as_uint(R[0]) - 0x40000000u, yb = __float_as_uint(R[1]) - 0x40000000u;
+  keys[g] = ((uint64_t)b << 54) | (xb << 27) | yb;
 }
 
 // ---- removeDuplicatedSorted + retainBest + ordered compaction ------------------------
@@ -242,13 +242,15 @@ __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
   const int b = blockIdx.x, tid = threadIdx.x;
   const long base = (long)b * A.cap_img;
   const int cnt = A.img_count[b];
+  long sbase = 0;  // this image's first element in the batch-wide sorted order
+  for (int q = 0; q < b; ++q) sbase += min(A.img_count[q], A.cap_img);
   if (*A.cand_count > A.cand_cap || cnt > A.cap_img) {
     if (tid == 0) A.sel_count[b] = -1;
     return;
   }
   const int n = cnt;
-  const uint64_t* K = A.keys + base;
-  uint32_t* V = A.vals + base;
+  const uint64_t* K = A.keys + sbase;
+  uint32_t* V = A.vals + sbase;
   // runs of equal (x, y): insertion sort by the rest of the comparator (runs are short)
   for (int i = tid; i < n; i += kSelThreads) {
     if (i + 1 < n && K[i + 1] == K[i] && (i == 0 || K[i - 1] != K[i])) {
@@ -564,6 +566,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   VO_REQUIRE(batch >= 1 && batch <= kMaxBatch, VO_ERR_ARG, "sift: batch %d outside 1..%d", batch, kMaxBatch);
   VO_REQUIRE(cap_img >= 1 && cap_img <= kMaxCapImg, VO_ERR_ARG, "sift: capacity %d outside 1..%d", cap_img,
              kMaxCapImg);
+  VO_REQUIRE(h <= 16383 && w <= 16383, VO_ERR_ARG, "sift: image %dx%d larger than 16383 pixels a side", h, w);
   std::vector<int64_t> lay(3 + 5 * kMaxOct);
   const int nv = sift_layout(h, w, n_layers, lay.data(), (int)lay.size());
   VO_REQUIRE(nv <= (int)lay.size(), VO_ERR_ARG, "sift: %dx%d has too many octaves", h, w);
@@ -590,9 +593,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   uint32_t* vals_out = vals_in + slots;
   uint32_t* sel = vals_out + slots;
   int32_t* img_count = ws.segs.as<int32_t>();
-  int32_t* seg_beg = img_count + batch;
-  int32_t* seg_end = seg_beg + batch;
-  int32_t* sel_count = seg_end + batch;
+  int32_t* sel_count = img_count + batch;
   hipStream_t st = ctx->stream;
   const ExpTab tab = make_exp_tab();
 
@@ -617,14 +618,17 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
 
   ctx->prof.begin(st, kKSiftSelect);
   hipLaunchKernelGGL(sift_keys_kernel, dim3(ceil_div((int64_t)slots, 256)), dim3(256), 0, st, okp, img_count, cap_img,
-                     batch, keys_in, vals_in, seg_beg, seg_end);
+                     batch, keys_in, vals_in);
+  // image bits 54.. (ceil(log2(batch + 1)) of them; unused slots are all ones)
+  int img_bits = 1;
+  while ((1 << img_bits) <= batch) ++img_bits;
+  const unsigned end_bit = 54u + (unsigned)img_bits;
   size_t tmp_bytes = 0;
-  VO_HIP_CHECK(rocprim::segmented_radix_sort_pairs(nullptr, tmp_bytes, keys_in, keys_out, vals_in, vals_out,
-                                                   (unsigned)slots, (unsigned)batch, seg_beg, seg_end, 0, 64, st));
+  VO_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, keys_in, keys_out, vals_in, vals_out, slots, 0u, end_bit,
+                                         st));
   ws.sort_tmp.reserve(tmp_bytes);
-  VO_HIP_CHECK(rocprim::segmented_radix_sort_pairs(ws.sort_tmp.ptr, tmp_bytes, keys_in, keys_out, vals_in,
-                                                   vals_out, (unsigned)slots, (unsigned)batch, seg_beg, seg_end, 0,
-                                                   64, st));
+  VO_HIP_CHECK(rocprim::radix_sort_pairs(ws.sort_tmp.ptr, tmp_bytes, keys_in, keys_out, vals_in, vals_out, slots, 0u,
+                                         end_bit, st));
   SelArgs sa;
   sa.okp = okp;
   sa.keys = keys_out;
