@@ -1529,7 +1529,13 @@ __global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
       const bool more = p + 1 < nside;
       tabs(tbase + (more ? p + 1 : p), nxt);
       if (gw == 0) {
+#ifdef VO_K3_LOOKAHEAD_PAIRS
         tasks(cur, 0, 3 * cur.npri, lane, 64, std::true_type{});
+#else
+        // the look-ahead items one row per lane (<= 42 rows: one round, half the chain of
+        // a row pair); the other wave keeps row pairs for the rest of the trailing window
+        tasks(cur, 0, 6 * cur.npri, lane, 64, std::false_type{});
+#endif
         mark(kS3Barrier);
         if (more) panel(nxt);
         mark(kS3Mid);
