@@ -200,7 +200,7 @@ PNP_FLOPS_PER_HYP = 68_000  # EPnP: 12x12 Jacobi SVD (431 pair checks x ~26 + 31
 PNP_FLOPS_PER_EVAL = 40     # scoring: R X + t, 1/z, pixel, float32 error (fp64 + fp32 ops) per point x hypothesis
 
 
-def bench_pnp(ctx, batch: int = 256, n: int = 1000, calls: int = 20, warmup: int = 3, thr: float = 1.0):
+def bench_pnp(ctx, batch: int = 1024, n: int = 1000, calls: int = 20, warmup: int = 3, thr: float = 1.0):
     """device-resident PnP-RANSAC throughput (frames/s), batched frames."""
     from oracle import pnp_ref
     from visualodometry_amd import _lib, pnp
