@@ -135,6 +135,67 @@ def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: 
     return res
 
 
+def bench_matcher_float(ctx, batch: int = 16, n: int = 2048, dim: int = 256, calls: int = 10, warmup: int = 2):
+    """BASELINE config 5's matcher: SuperPoint-like L2-normalised float32 descriptors (not
+    integer-valued, so the exact fp32 path: k-ordered fmaf chain), 2048 x
+    2048 x 256 per frame pair, knn2 + ratio 0.75, frame pairs resident in HBM."""
+    from oracle import match_ref
+    from visualodometry_amd import _lib, matcher
+    from visualodometry_amd.synthetic import superpoint_like_pair
+
+    pairs = [superpoint_like_pair(n, n, 2000 + b, dim=dim) for b in range(batch)]
+    a = _lib.DeviceArray.from_numpy(ctx, np.stack([q[0] for q in pairs]))
+    b = _lib.DeviceArray.from_numpy(ctx, np.stack([q[1] for q in pairs]))
+    out = _lib.DeviceArray(ctx, (batch, n), np.int32)
+    for _ in range(warmup):
+        matcher.match_batch_device(a, b, out=out, ctx=ctx)
+    matcher.synchronize(ctx)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        matcher.match_batch_device(a, b, out=out, ctx=ctx)
+    matcher.synchronize(ctx)
+    dt = time.perf_counter() - t0
+    _lib.profile_enable(ctx, True)
+    for _ in range(calls):
+        matcher.match_batch_device(a, b, out=out, ctx=ctx)
+    matcher.synchronize(ctx)
+    prof = _lib.profile_read(ctx)
+    _lib.profile_enable(ctx, False)
+    threads = min(16, os.cpu_count() or 1)
+    ref = match_ref.match_c(pairs[0][0], pairs[0][1], nthreads=threads)
+    got = out.numpy()[0]
+    kept = np.nonzero(got >= 0)[0]
+    assert np.array_equal(np.stack([kept, got[kept]], 1), ref), "float matcher parity guard failed"
+    kern = {k: round(v[0] / v[1] * 1e3, 2) for k, v in prof.items()}
+    ms_f, cnt_f = prof.get("match_i8", (0.0, 1))  # the sweep launch; it takes the fp32 path on device
+    avg_s = ms_f / max(cnt_f, 1) / 1e3
+    # fp32 VALU: a subtract and an FMA per (pair, k)
+    tfl = 3.0 * dim * batch * n * n / avg_s / 1e12 if avg_s > 0 else 0.0
+    res = {
+        "metric": "descriptor-match Mpairs/sec (float path)",
+        "value": batch * n * n * calls / dt / 1e6,
+        "unit": "Mpairs/s",
+        "dtype": "f32",
+        "config": {"workload": f"SuperPoint-like L2-normalised float32 {n} x {n} x {dim}, {batch} frame pairs "
+                               "per call, knn2 + ratio 0.75 (BASELINE config 5 matcher)", "calls": calls},
+        "kernel_us": kern,
+        "roofline": {"bound": "valu-fp32", "kernel": "match sweep, fp32 path", "achieved": tfl,
+                     "peak": FP32_VECTOR_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": tfl / FP32_VECTOR_PEAK_TFLOPS,
+                     "note": "3 flops (sub + fma) per pair and dimension / the sweep's HIP-event duration; "
+                             "exact k-ordered fmaf chain, so no MFMA"},
+    }
+    rows = 256
+    t0 = time.perf_counter()
+    match_ref.knn2_c(pairs[0][0][:rows], pairs[0][1], threads)
+    cdt = time.perf_counter() - t0
+    res["cpu_baseline"] = {"value": rows * n / cdt / 1e6, "unit": "Mpairs/s", "cores": threads, "kind": "port",
+                           "sample": f"oracle/match_ref.c knn2 on {rows} x {n} x {dim} of frame pair 0, "
+                                     f"{threads} host threads"}
+    return res
+
+
+FP32_VECTOR_PEAK_TFLOPS = 157.3  # 256 CUs x 4 SIMDs x 64 FLOP/clk (FMA, 16 lanes x 2, packed x2) x 2.4 GHz
 FP64_VECTOR_PEAK_TFLOPS = 78.6  # 256 CUs x 4 SIMDs x 32 FLOP/clk (4-cycle wave64 fp64 FMA) x 2.4 GHz
 TRI_FLOPS_PER_POINT = 2892      # DLT 32 + 5 Jacobi sweeps (typical; a wave stops once converged) x 6 pairs x ~92 + ~100
 
@@ -495,6 +556,7 @@ def main() -> int:
         line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
     if rank == 0 and world == 1 and not args.no_matcher:
         line["secondary"] = bench_matcher(ctx, traffic_all=traffic_all)
+        line["matcher_float"] = bench_matcher_float(ctx)
         line["triangulate"] = bench_triangulate(ctx)
         line["pnp"] = bench_pnp(ctx)
         line["sift"] = bench_sift(ctx)

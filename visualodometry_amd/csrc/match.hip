@@ -40,8 +40,9 @@ constexpr int kRowsPerWG = 256;     // 4 waves
 // v_lshl_add_u32 forms a key from the MFMA dot product.
 __host__ __device__ constexpr uint32_t max_off(int Dp) { return (uint32_t)Dp * 48896u + 1u; }
 constexpr int kCollide = 1 << 22;   // sqrtf(n) == sqrtf(n+1) needs n >= 2^22
-constexpr int kFloatTile = 64;      // float path: 64 x 64 pair tile per WG
-constexpr int kFloatKC = 32;        // float path k-chunk staged in LDS
+constexpr int kFloatTile = 64;      // float path: 64 rows x kFloatCols columns per WG tile
+constexpr int kFloatCols = 128;     //   (4 rows x 8 columns per thread)
+constexpr int kFloatKC = 16;        // float path: k-chunk staged in LDS
 
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r;
@@ -372,13 +373,16 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
 // the columns arrive in ascending j, so a candidate can only enter the top-2 if
 // d2 < d2(second): sqrtf is evaluated only then (exact filter, see header).
 __device__ __forceinline__ void sweep_f32(const MatchArgs& p, int rowbase) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
   const float* da = p.da;
   const float* db = p.db;
   const int n0 = p.n0, n1 = p.n1, dim = p.dim, n0_pad = p.n0_pad, split_w = p.split_w;
   const long a_bstride = p.a_bstride, b_bstride = p.b_bstride;
   uint4* partial = p.partial;
-  __shared__ float sa[kFloatKC][kFloatTile + 1];
-  __shared__ float sb[kFloatKC][kFloatTile + 1];
+  // k-major tiles (rows padded by 16 bytes): a thread reads its 4 rows and its 8 columns
+  // of one k as one and two 16-byte loads
+  __shared__ __attribute__((aligned(16))) float sa[kFloatKC][kFloatTile + 4];
+  __shared__ __attribute__((aligned(16))) float sb[kFloatKC][kFloatCols + 4];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int b = blockIdx.z, split = blockIdx.y, nsplit = gridDim.y;
   const float* A = da + b * a_bstride;
@@ -393,44 +397,53 @@ __device__ __forceinline__ void sweep_f32(const MatchArgs& p, int rowbase) {
   }
   const int c0 = split * split_w;
   const int c1 = min(c0 + split_w, n1);
-  for (int ct = c0; ct < c1; ct += kFloatTile) {
-    float acc[4][4];
+  for (int ct = c0; ct < c1; ct += kFloatCols) {
+    // acc[i][q] = the k-ordered fmaf chains of rows ty*4+i, columns tx*8+2q, tx*8+2q+1:
+    // packed fp32 (v_pk_add_f32 / v_pk_fma_f32 are the same IEEE operations per element)
+    f2 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc[i][c] = 0.0f;
+      for (int q = 0; q < 4; ++q) acc[i][q] = f2{0.0f, 0.0f};
     for (int k0 = 0; k0 < dim; k0 += kFloatKC) {
       __syncthreads();
       for (int e = threadIdx.x; e < kFloatKC * kFloatTile; e += 256) {
         const int rr = e / kFloatKC, kk = e % kFloatKC;
-        const int ga = rowbase + rr, gb = ct + rr, gk = k0 + kk;
+        const int ga = rowbase + rr, gk = k0 + kk;
         sa[kk][rr] = (ga < n0 && gk < dim) ? A[(long)ga * dim + gk] : 0.0f;
+      }
+      for (int e = threadIdx.x; e < kFloatKC * kFloatCols; e += 256) {
+        const int rr = e / kFloatKC, kk = e % kFloatKC;
+        const int gb = ct + rr, gk = k0 + kk;
         sb[kk][rr] = (gb < n1 && gk < dim) ? B[(long)gb * dim + gk] : 0.0f;
       }
       __syncthreads();
       const int kc = min(kFloatKC, dim - k0);
       for (int kk = 0; kk < kc; ++kk) {
-        float av[4], bv[4];
+        const float4 a4 = *reinterpret_cast<const float4*>(&sa[kk][ty * 4]);
+        const float4 bl = *reinterpret_cast<const float4*>(&sb[kk][tx * 8]);
+        const float4 bh = *reinterpret_cast<const float4*>(&sb[kk][tx * 8 + 4]);
+        const f2 bv[4] = {f2{bl.x, bl.y}, f2{bl.z, bl.w}, f2{bh.x, bh.y}, f2{bh.z, bh.w}};
+        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) av[i] = sa[kk][ty * 4 + i];
+        for (int i = 0; i < 4; ++i) {
+          const f2 a2 = f2{av[i], av[i]};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) bv[c] = sb[kk][tx + 16 * c];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float df = av[i] - bv[c];
-            acc[i][c] = __builtin_fmaf(df, df, acc[i][c]);
+          for (int q = 0; q < 4; ++q) {
+            const f2 df = a2 - bv[q];
+            acc[i][q] = __builtin_elementwise_fma(df, df, acc[i][q]);
           }
+        }
       }
     }
+    // this lane's columns in ascending j (strict '<' keeps the lower j on equal s)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int j = ct + tx + 16 * c;
+    for (int c = 0; c < 8; ++c) {
+      const int j = ct + tx * 8 + c;
       if (j >= c1) continue;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float d = acc[i][c];
+        const float d = (c & 1) ? acc[i][c >> 1].y : acc[i][c >> 1].x;
         if (d < d2nd[i]) {  // d2 >= d2(second) implies s >= s2: cannot enter
           const float s = sqrtf_rn(d);
           if (s < s1[i]) {
