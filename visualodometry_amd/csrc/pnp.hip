@@ -16,11 +16,12 @@
 //                     one-sided Jacobi SVDs, a 12x12 one among them, three beta
 //                     approximations with 5 Householder Gauss-Newton steps each), then
 //                     the Rodrigues round trip the model makes through (rvec, tvec);
-//   pnp_score_kernel  one workgroup per (frame, hypothesis): float32 reprojection error
+//   pnp_score_kernel  one workgroup per (frame, group of hypotheses): float32 reprojection error
 //                     of every point, inlier count;
 //   pnp_final_kernel  one workgroup per frame: RANSAC replay (best model, niters update),
 //                     inlier mask of the best model, Levenberg-Marquardt refinement on the
 //                     inliers (fixed-order block reductions), Rodrigues to rvec.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -36,6 +37,8 @@ namespace {
 using namespace pnpm;
 
 // ---------------------------------------------------------------- kernels
+constexpr int kScoreGroupMax = 128;  // hypotheses scored by one workgroup, at most
+
 struct PnpArgs {
   const float* X;          // (total, 3) object points, frames back to back
   const float* uv;         // (total, 2) image points
@@ -96,31 +99,38 @@ __global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a) {
   model[15] = ok ? 1.0 : 0.0;
 }
 
-__global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a) {
-  const int g = blockIdx.x;  // (frame, hypothesis)
-  const int f = g / a.H;
+__global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group) {
+  // one workgroup per (frame, group of `group` hypotheses): the frame's points stay in L1
+  // across its hypotheses; the host sizes groups so the grid still fills the chip
+  const int ngroups = (a.H + group - 1) / group;
+  const int f = blockIdx.x / ngroups, h0 = (blockIdx.x % ngroups) * group, h1 = min(h0 + group, a.H);
   const int o = a.off[f], n = a.off[f + 1] - o;
-  const double* model = a.models + (size_t)g * kModel;
-  __shared__ int s_count;
-  if (threadIdx.x == 0) s_count = 0;
+  __shared__ int s_count[kScoreGroupMax];
+  for (int h = threadIdx.x; h < h1 - h0; h += 256) s_count[h] = 0;
   __syncthreads();
-  if (model[15] != 0.0 && n > kPts) {
-    double R[9], t[3];
+  if (n > kPts) {
+    for (int h = h0; h < h1; ++h) {
+      const double* model = a.models + ((size_t)f * a.H + h) * kModel;  // uniform
+      if (model[15] == 0.0) continue;
+      double R[9], t[3];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) R[k] = model[k];
+      for (int k = 0; k < 9; ++k) R[k] = model[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) t[k] = model[9 + k];
-    int cnt = 0;
-    for (int i = threadIdx.x; i < n; i += 256) {
-      const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
-      float M[3];
-      load3(a.X, o + i, M);
-      cnt += is_inlier(R, t, M, q.x, q.y, a.K, a.thr2) ? 1 : 0;
+      for (int k = 0; k < 3; ++k) t[k] = model[9 + k];
+      int cnt = 0;
+      for (int i = threadIdx.x; i < n; i += 256) {
+        const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
+        float M[3];
+        load3(a.X, o + i, M);
+        cnt += is_inlier(R, t, M, q.x, q.y, a.K, a.thr2) ? 1 : 0;
+      }
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) cnt += __shfl_xor(cnt, m, 64);
+      if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_count[h - h0], cnt);
     }
-    if (cnt) atomicAdd(&s_count, cnt);
   }
   __syncthreads();
-  if (threadIdx.x == 0) a.counts[g] = s_count;
+  for (int h = threadIdx.x; h < h1 - h0; h += 256) a.counts[(size_t)f * a.H + h0 + h] = s_count[h];
 }
 
 // Sum of one double over a wave in a fixed order (butterfly).
@@ -340,7 +350,11 @@ void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* of
   ctx->prof.end(ctx->stream);
   VO_HIP_CHECK(hipGetLastError());
   ctx->prof.begin(ctx->stream, kKPnpScore);
-  hipLaunchKernelGGL(pnp_score_kernel, dim3(nh), dim3(256), 0, ctx->stream, a);
+  // hypotheses per scoring workgroup: one for small batches (single-frame latency), up to
+  // kScoreGroupMax while the grid keeps ~4 workgroups per CU
+  const int group = std::max(1, std::min({H, kScoreGroupMax, nh / std::max(1, 4 * ctx->num_cus)}));
+  const int ngroups = ceil_div(H, group);
+  hipLaunchKernelGGL(pnp_score_kernel, dim3(batch * ngroups), dim3(256), 0, ctx->stream, a, group);
   ctx->prof.end(ctx->stream);
   VO_HIP_CHECK(hipGetLastError());
   ctx->prof.begin(ctx->stream, kKPnpFinal);
