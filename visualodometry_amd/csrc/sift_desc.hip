@@ -445,23 +445,40 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
           v_r0 = mag - v_r1;
         }
       }
-      // stable per-cell lists: the sample votes into cells (r0 + 1 + dr, c0 + 1 + dc)
-      const uint64_t lt = (1ull << lane) - 1ull;
-      uint64_t bal[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int dr = q / 4 - r0, dc = q % 4 - c0;  // cell (q/4 + 1, q%4 + 1)
-        bal[q] = __ballot(valid && (unsigned)dr <= 1u && (unsigned)dc <= 1u);
-        if (lane == 0) s_cnt[wave][q] = __popcll(bal[q]);
-      }
-      __syncthreads();
+      // stable per-cell lists: the sample votes into interior cells q = (r0 + dr) * 4 + (c0 + dc),
+      // dr, dc in {0, 1} (cell row r0 + 1 + dr of the (d+2)^2 grid): its hit mask, one
+      // ballot per cell, the wave's count per cell stored by lane q, and the cell's offset
+      // of this wave (the counts of the waves before it) computed once by lane q
+      uint32_t hit = 0;
       if (valid) {
 #pragma unroll
+        for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+          for (int dc = 0; dc < 2; ++dc) {
+            const int rr = r0 + dr, cc = c0 + dc;
+            if ((unsigned)rr < 4u && (unsigned)cc < 4u) hit |= 1u << (rr * 4 + cc);
+          }
+      }
+      uint64_t bal[16];
+      int cntv = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        bal[q] = __ballot((hit >> q) & 1u);
+        cntv = lane == q ? __popcll(bal[q]) : cntv;
+      }
+      if (lane < 16) s_cnt[wave][lane] = cntv;
+      __syncthreads();
+      int basev = 0;
+      if (lane < 16)
+        for (int w = 0; w < wave; ++w) basev += s_cnt[w][lane];
+      if (hit) {
+#pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const int dr = q / 4 - r0, dc = q % 4 - c0;
-          if ((unsigned)dr <= 1u && (unsigned)dc <= 1u) {
-            int off = __popcll(bal[q] & lt);
-            for (int w = 0; w < wave; ++w) off += s_cnt[w][q];
+          if ((hit >> q) & 1u) {
+            const uint64_t m = bal[q];
+            const int off = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
+                            __builtin_amdgcn_readlane(basev, q);
+            const int dr = q / 4 - r0, dc = q % 4 - c0;
             const float vr = dr ? v_r1 : v_r0;
             const float v_c1 = vr * cb, v_c0 = vr - v_c1;
             const float vc = dc ? v_c1 : v_c0;
