@@ -1,7 +1,9 @@
 """Host emulation of sift_desc_kernel (csrc/sift_desc.hip) against the oracle.
 
-The kernel walks the rotated window in blocks of 256 positions; each valid sample is
-appended, in window order, to the LDS list of every interior descriptor cell it votes into
+The kernel compacts the window's valid positions in order and processes them 256 at a
+time (this emulation keeps blocks of 256 positions: the per-bin order, window order, is the
+same); each valid sample is appended, in window order, to the LDS list of every interior
+descriptor cell it votes into
 as (obin, value after the row and column interpolation); the lane owning (cell,
 orientation slot) then walks its cell's list adding its orientation share.  This test
 restates that block / list / owner walk in float32 numpy and checks that it reproduces

@@ -21,8 +21,10 @@
 //                         (x, y, size, angle) dropped (removeDuplicatedSorted), the
 //                         nfeatures-th largest response found by a 4-pass radix select
 //                         (retainBest keeps every response >= it), ordered compaction
-//   sift_desc_kernel      one 256-thread workgroup per kept keypoint, the rotated window in
-//                         blocks of 256 positions: each thread evaluates one sample
+//   sift_desc_kernel      one 256-thread workgroup per kept keypoint: the square window's
+//                         positions are classified by the cheap geometry test and the valid
+//                         ones compacted in order (about half lie outside the rotated
+//                         square); then, 256 valid samples at a time, each thread evaluates one sample
 //                         (gradient, fastAtan2, magnitude, exp32f, trilinear shares) and
 //                         appends it to the stable LDS lists of the (up to 4) interior
 //                         cells it votes into as (o0, share to o0, share to o0 + 1) (one
@@ -355,6 +357,7 @@ struct DescArgs {
 };
 
 constexpr int kDescThreads = 256;
+constexpr int kPosCap = 768;   // compacted window positions per pass (uint16: windows < 65536)
 constexpr int kMaxBatch = 256;
 
 __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
@@ -364,6 +367,8 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
   __shared__ float2 s_list[16][kDescThreads];   // (v_o0, v_o1): the two orientation shares
   __shared__ uint8_t s_o0[16][kDescThreads];     // the lower orientation bin o0 (wrapped)
   __shared__ int s_cnt[kDescThreads / 64][16];
+  __shared__ uint16_t s_pos[kPosCap];  // valid window positions of the current pass, in order
+  __shared__ int s_wc[kDescThreads / 64];
   __shared__ float s_h[16 * 9];
   __shared__ float4 s_raw4[kDesc / 4];
   __shared__ int s_off[kMaxBatch + 1];
@@ -411,106 +416,136 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
     const float cos_t = __fdiv_rn(cos0, hist_width), sin_t = __fdiv_rn(sin0, hist_width);
     const int side = 2 * radius + 1, len = side * side;
     float acc = 0.0f;
-    for (int k0 = 0; k0 < len; k0 += kDescThreads) {
-      const int k = k0 + tid;
-      bool valid = false;
-      int r0 = -9, c0 = -9;
-      float ob = 0.0f, v_r0 = 0.0f, v_r1 = 0.0f, cb = 0.0f;
-      int o0 = 0;
-      if (k < len) {
-        const int i = k / side - radius, j = k % side - radius;
-        const float c_rot = (float)j * cos_t - (float)i * sin_t;
-        const float r_rot = (float)j * sin_t + (float)i * cos_t;
-        const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
-        const int r = py + i, c = px + j;
-        valid = rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 &&
-                c < cols - 1;
+    // The window's positions, in order, are classified 256 at a time by the cheap geometry
+    // test and the valid ones compacted into s_pos (about half of the square window lies
+    // outside the rotated descriptor square); the sample work then runs on dense blocks.
+    int kk0 = 0;
+    while (kk0 < len) {
+      int n = 0;
+      while (kk0 < len && n + kDescThreads <= kPosCap) {
+        const int k = kk0 + tid;
+        bool v = false;
+        if (k < len) {
+          const int i = k / side - radius, j = k % side - radius;
+          const float c_rot = (float)j * cos_t - (float)i * sin_t;
+          const float r_rot = (float)j * sin_t + (float)i * cos_t;
+          const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
+          const int r = py + i, c = px + j;
+          v = rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 && c < cols - 1;
+        }
+        const uint64_t bal = __ballot(v);
+        if (lane == 0) s_wc[wave] = __popcll(bal);
+        __syncthreads();
+        int off = n, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kDescThreads / 64; ++w) {
+          off += w < wave ? s_wc[w] : 0;
+          tot += s_wc[w];
+        }
+        if (v) s_pos[off + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)k;
+        n += tot;
+        kk0 += kDescThreads;
+        __syncthreads();
+      }
+      for (int t0 = 0; t0 < n; t0 += kDescThreads) {
+        const bool valid = t0 + tid < n;
+        int r0 = -9, c0 = -9;
+        float ob = 0.0f, v_r0 = 0.0f, v_r1 = 0.0f, cb = 0.0f;
+        int o0 = 0;
+        {
+          if (valid) {
+            const int k = s_pos[t0 + tid];
+            const int i = k / side - radius, j = k % side - radius;
+            const float c_rot = (float)j * cos_t - (float)i * sin_t;
+            const float r_rot = (float)j * sin_t + (float)i * cos_t;
+            const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
+            const int r = py + i, c = px + j;
+            const float dx = img[(long)r * pitch + c + 1] - img[(long)r * pitch + c - 1];
+            const float dy = img[(long)(r - 1) * pitch + c] - img[(long)(r + 1) * pitch + c];
+            const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, A.tab.v);
+            const float Ori = fast_atan2_deg(dy, dx);
+            const float Mag = sqrt_rn(dx * dx + dy * dy);
+            const float obin = (Ori - ori) * bins_per_rad;
+            const float mag = Mag * w;
+            o0 = (int)floorf(obin);
+            ob = obin - (float)o0;
+            if (o0 < 0) o0 += kN;
+            if (o0 >= kN) o0 -= kN;
+            r0 = (int)floorf(rbin);
+            c0 = (int)floorf(cbin);
+            const float rb = rbin - (float)r0;
+            cb = cbin - (float)c0;
+            v_r1 = mag * rb;
+            v_r0 = mag - v_r1;
+          }
+        }
+        // stable per-cell lists: the sample votes into interior cells q = (r0 + dr) * 4 + (c0 + dc),
+        // dr, dc in {0, 1} (cell row r0 + 1 + dr of the (d+2)^2 grid): its hit mask, one
+        // ballot per cell, the wave's count per cell stored by lane q, and the cell's offset
+        // of this wave (the counts of the waves before it) computed once by lane q
+        uint32_t hit = 0;
         if (valid) {
-          const float dx = img[(long)r * pitch + c + 1] - img[(long)r * pitch + c - 1];
-          const float dy = img[(long)(r - 1) * pitch + c] - img[(long)(r + 1) * pitch + c];
-          const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, A.tab.v);
-          const float Ori = fast_atan2_deg(dy, dx);
-          const float Mag = sqrt_rn(dx * dx + dy * dy);
-          const float obin = (Ori - ori) * bins_per_rad;
-          const float mag = Mag * w;
-          o0 = (int)floorf(obin);
-          ob = obin - (float)o0;
-          if (o0 < 0) o0 += kN;
-          if (o0 >= kN) o0 -= kN;
-          r0 = (int)floorf(rbin);
-          c0 = (int)floorf(cbin);
-          const float rb = rbin - (float)r0;
-          cb = cbin - (float)c0;
-          v_r1 = mag * rb;
-          v_r0 = mag - v_r1;
+  #pragma unroll
+          for (int dr = 0; dr < 2; ++dr)
+  #pragma unroll
+            for (int dc = 0; dc < 2; ++dc) {
+              const int rr = r0 + dr, cc = c0 + dc;
+              if ((unsigned)rr < 4u && (unsigned)cc < 4u) hit |= 1u << (rr * 4 + cc);
+            }
         }
-      }
-      // stable per-cell lists: the sample votes into interior cells q = (r0 + dr) * 4 + (c0 + dc),
-      // dr, dc in {0, 1} (cell row r0 + 1 + dr of the (d+2)^2 grid): its hit mask, one
-      // ballot per cell, the wave's count per cell stored by lane q, and the cell's offset
-      // of this wave (the counts of the waves before it) computed once by lane q
-      uint32_t hit = 0;
-      if (valid) {
-#pragma unroll
-        for (int dr = 0; dr < 2; ++dr)
-#pragma unroll
-          for (int dc = 0; dc < 2; ++dc) {
-            const int rr = r0 + dr, cc = c0 + dc;
-            if ((unsigned)rr < 4u && (unsigned)cc < 4u) hit |= 1u << (rr * 4 + cc);
-          }
-      }
-      uint64_t bal[16];
-      int cntv = 0;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        bal[q] = __ballot((hit >> q) & 1u);
-        cntv = lane == q ? __popcll(bal[q]) : cntv;
-      }
-      if (lane < 16) s_cnt[wave][lane] = cntv;
-      __syncthreads();
-      int basev = 0;
-      if (lane < 16)
-        for (int w = 0; w < wave; ++w) basev += s_cnt[w][lane];
-      if (hit) {
-#pragma unroll
+        uint64_t bal[16];
+        int cntv = 0;
+  #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          if ((hit >> q) & 1u) {
-            const uint64_t m = bal[q];
-            const int off = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
-                            __builtin_amdgcn_readlane(basev, q);
-            const int dr = q / 4 - r0, dc = q % 4 - c0;
-            const float vr = dr ? v_r1 : v_r0;
-            const float v_c1 = vr * cb, v_c0 = vr - v_c1;
-            const float vc = dc ? v_c1 : v_c0;
-            const float v_o1 = vc * ob, v_o0 = vc - v_o1;
-            s_list[q][off] = make_float2(v_o0, v_o1);
-            s_o0[q][off] = (uint8_t)o0;
+          bal[q] = __ballot((hit >> q) & 1u);
+          cntv = lane == q ? __popcll(bal[q]) : cntv;
+        }
+        if (lane < 16) s_cnt[wave][lane] = cntv;
+        __syncthreads();
+        int basev = 0;
+        if (lane < 16)
+          for (int w = 0; w < wave; ++w) basev += s_cnt[w][lane];
+        if (hit) {
+  #pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            if ((hit >> q) & 1u) {
+              const uint64_t m = bal[q];
+              const int off = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
+                              __builtin_amdgcn_readlane(basev, q);
+              const int dr = q / 4 - r0, dc = q % 4 - c0;
+              const float vr = dr ? v_r1 : v_r0;
+              const float v_c1 = vr * cb, v_c0 = vr - v_c1;
+              const float vc = dc ? v_c1 : v_c0;
+              const float v_o1 = vc * ob, v_o0 = vc - v_o1;
+              s_list[q][off] = make_float2(v_o0, v_o1);
+              s_o0[q][off] = (uint8_t)o0;
+            }
           }
         }
-      }
-      __syncthreads();
-      // the owner of (cell, O) adds its orientation share of each entry, in order (+0.0 when
-      // missed: an identity, every partial sum is >= +0)
-      if (lane < 36) {
-        const int n = s_cnt[0][my_cell] + s_cnt[1][my_cell] + s_cnt[2][my_cell] + s_cnt[3][my_cell];
-        const float2* L = s_list[my_cell];
-        const uint8_t* L0 = s_o0[my_cell];
-        auto step = [&](const float2 e, const int o0) {
-          const int dO = O - o0;
-          acc = acc + (dO == 0 ? e.x : (dO == 1 ? e.y : 0.0f));
-        };
-        int t = 0;
-        for (; t + 4 <= n; t += 4) {
-          float2 e[4];
-          const uint32_t o4 = *reinterpret_cast<const uint32_t*>(L0 + t);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) e[u] = L[t + u];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) step(e[u], (o4 >> (8 * u)) & 255);
+        __syncthreads();
+        // the owner of (cell, O) adds its orientation share of each entry, in order (+0.0 when
+        // missed: an identity, every partial sum is >= +0)
+        if (lane < 36) {
+          const int nl = s_cnt[0][my_cell] + s_cnt[1][my_cell] + s_cnt[2][my_cell] + s_cnt[3][my_cell];
+          const float2* L = s_list[my_cell];
+          const uint8_t* L0 = s_o0[my_cell];
+          auto step = [&](const float2 e, const int o0) {
+            const int dO = O - o0;
+            acc = acc + (dO == 0 ? e.x : (dO == 1 ? e.y : 0.0f));
+          };
+          int t = 0;
+          for (; t + 4 <= nl; t += 4) {
+            float2 e[4];
+            const uint32_t o4 = *reinterpret_cast<const uint32_t*>(L0 + t);
+  #pragma unroll
+            for (int u = 0; u < 4; ++u) e[u] = L[t + u];
+  #pragma unroll
+            for (int u = 0; u < 4; ++u) step(e[u], (o4 >> (8 * u)) & 255);
+          }
+          for (; t < nl; ++t) step(L[t], L0[t]);
         }
-        for (; t < n; ++t) step(L[t], L0[t]);
+        __syncthreads();
       }
-      __syncthreads();
     }
     if (lane < 36) s_h[((Rc - 1) * 4 + (Cc - 1)) * 9 + O] = acc;
     __syncthreads();
@@ -584,6 +619,11 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   VO_REQUIRE(cap_img >= 1 && cap_img <= kMaxCapImg, VO_ERR_ARG, "sift: capacity %d outside 1..%d", cap_img,
              kMaxCapImg);
   VO_REQUIRE(h <= 16383 && w <= 16383, VO_ERR_ARG, "sift: image %dx%d larger than 16383 pixels a side", h, w);
+  // descriptor windows are indexed in 16 bits: (2 radius + 1)^2 < 65536, radius <= 127, with
+  // radius <= 3 scl sqrt2 (d + 1) / 2 + 1 and scl <= sigma 2^((n_layers + 0.5) / n_layers)
+  const double scl_max = sigma * std::pow(2.0, (n_layers + 0.5) / n_layers);
+  VO_REQUIRE(3.0 * scl_max * 1.4142135623730951 * (kD + 1) * 0.5 + 1.0 <= 127.0, VO_ERR_ARG,
+             "sift: sigma %g with %d layers gives descriptor windows over 255 samples a side", sigma, n_layers);
   std::vector<int64_t> lay(3 + 5 * kMaxOct);
   const int nv = sift_layout(h, w, n_layers, lay.data(), (int)lay.size());
   VO_REQUIRE(nv <= (int)lay.size(), VO_ERR_ARG, "sift: %dx%d has too many octaves", h, w);
