@@ -36,6 +36,11 @@ namespace {
 constexpr int kBorder = 5;        // SIFT_IMG_BORDER
 constexpr int kMaxInterp = 5;     // SIFT_MAX_INTERP_STEPS
 constexpr int kTileW = 64, kTileH = 16, kMaxR = 32;
+#ifndef VO_TILE_HR
+#define VO_TILE_HR 16
+#endif
+constexpr int kTileHR = VO_TILE_HR;  // tile height of the radius-specialised blur (16 or 32)
+constexpr int kRowsPT = kTileHR / 4;  // column-pass outputs per thread
 constexpr int kKpFloats = 8;      // x, y, size, response, xi, (pad) per keypoint
 constexpr int kKpInts = 8;        // image, octave word, candidate level, level, row, col, cand row, cand col
 
@@ -132,16 +137,18 @@ __global__ __launch_bounds__(256) void sift_blur_r_kernel(const float* __restric
                                                           const float* __restrict__ prev, float* __restrict__ dog,
                                                           int h, int w, int pitch, long stride, long dog_stride,
                                                           Taps T) {
-  constexpr int TW = kTileW + 2 * R, TWP = (TW + 3) & ~3, TH = kTileH + 2 * R, NX = 4 + 2 * R;
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  constexpr int TW = kTileW + 2 * R, TWP = (TW + 3) & ~3, TH = kTileHR + 2 * R;
+  constexpr int NXR = 4 + 2 * R, NXC = kRowsPT + 2 * R;
   __shared__ float4 in4[TH * TWP / 4];
   __shared__ float4 tmp4[TH * kTileW / 4];
   float* in = reinterpret_cast<float*>(in4);
   float* tmp = reinterpret_cast<float*>(tmp4);
-  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH;
+  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileHR;
   const long base = (long)blockIdx.z * stride;
   const float* S = src + base;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const bool interior = x0 - R >= 0 && x0 + kTileW + R <= w && y0 - R >= 0 && y0 + kTileH + R <= h;
+  const bool interior = x0 - R >= 0 && x0 + kTileW + R <= w && y0 - R >= 0 && y0 + kTileHR + R <= h;
   int gx0 = x0 + tx - R, gx1 = x0 + tx + 64 - R;
   if (!interior) {
     gx0 = reflect101(gx0, w);
@@ -157,45 +164,49 @@ __global__ __launch_bounds__(256) void sift_blur_r_kernel(const float* __restric
   float k[2 * R + 1];
 #pragma unroll
   for (int j = 0; j <= 2 * R; ++j) k[j] = T.k[j];
-  // row pass: TH rows x 16 column quads
+  // row pass: TH rows x 16 column quads; outputs in pairs as packed fp32 (v_pk_mul_f32 and
+  // v_pk_add_f32: per element the same IEEE multiply and add, no FMA)
   for (int t = threadIdx.x; t < TH * 16; t += 256) {
     const int r = t >> 4, q = (t & 15) * 4;
     const float4* p = in4 + (r * TWP + q) / 4;
-    float x[(NX + 3) & ~3];
+    float x[(NXR + 3) & ~3];
 #pragma unroll
-    for (int m = 0; m < (NX + 3) / 4; ++m) {
+    for (int m = 0; m < (NXR + 3) / 4; ++m) {
       const float4 v = p[m];
       x[4 * m] = v.x;
       x[4 * m + 1] = v.y;
       x[4 * m + 2] = v.z;
       x[4 * m + 3] = v.w;
     }
-    float o[4];
+    f2 s01 = f2{0.0f, 0.0f}, s23 = f2{0.0f, 0.0f};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      float s = 0.0f;
-#pragma unroll
-      for (int j = 0; j <= 2 * R; ++j) s = s + k[j] * x[u + j];
-      o[u] = s;
+    for (int j = 0; j <= 2 * R; ++j) {
+      const f2 kj = f2{k[j], k[j]};
+      s01 = s01 + kj * f2{x[j], x[j + 1]};
+      s23 = s23 + kj * f2{x[j + 2], x[j + 3]};
     }
-    tmp4[(r * kTileW + q) / 4] = make_float4(o[0], o[1], o[2], o[3]);
+    tmp4[(r * kTileW + q) / 4] = make_float4(s01.x, s01.y, s23.x, s23.y);
   }
   __syncthreads();
-  // column pass: column tx, rows 4 ty .. 4 ty + 3
-  float x[NX];
+  // column pass: column tx, rows kRowsPT ty .. kRowsPT (ty + 1) - 1, in pairs
+  float x[NXC];
 #pragma unroll
-  for (int m = 0; m < NX; ++m) x[m] = tmp[(4 * ty + m) * kTileW + tx];
+  for (int m = 0; m < NXC; ++m) x[m] = tmp[(kRowsPT * ty + m) * kTileW + tx];
   const int gx = x0 + tx;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    float s = 0.0f;
+  for (int u = 0; u < kRowsPT; u += 2) {
+    f2 s = f2{0.0f, 0.0f};
 #pragma unroll
-    for (int j = 0; j <= 2 * R; ++j) s = s + k[j] * x[u + j];
-    const int gy = y0 + 4 * ty + u;
-    if (gx < w && gy < h) {
-      const long o = base + (long)gy * pitch + gx;
-      dst[o] = s;
-      if (prev) dog[(long)blockIdx.z * dog_stride + (long)gy * pitch + gx] = s - prev[o];
+    for (int j = 0; j <= 2 * R; ++j) s = s + f2{k[j], k[j]} * f2{x[u + j], x[u + 1 + j]};
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int gy = y0 + kRowsPT * ty + u + e;
+      const float v = e ? s.y : s.x;
+      if (gx < w && gy < h) {
+        const long o = base + (long)gy * pitch + gx;
+        dst[o] = v;
+        if (prev) dog[(long)blockIdx.z * dog_stride + (long)gy * pitch + gx] = v - prev[o];
+      }
     }
   }
 }
@@ -203,10 +214,11 @@ __global__ __launch_bounds__(256) void sift_blur_r_kernel(const float* __restric
 // One Gaussian level through the radius-specialised kernel when there is one.
 void launch_blur(dim3 grid, hipStream_t st, const float* src, float* dst, const float* prev, float* dog, int h,
                  int w, int pitch, long stride, long dog_stride, const Taps& T) {
-#define VO_BLUR_CASE(RR)                                                                                       \
-  case RR:                                                                                                     \
-    hipLaunchKernelGGL(sift_blur_r_kernel<RR>, grid, dim3(256), 0, st, src, dst, prev, dog, h, w, pitch, stride, \
-                       dog_stride, T);                                                                         \
+  const dim3 gridr(grid.x, ceil_div(h, kTileHR), grid.z);
+#define VO_BLUR_CASE(RR)                                                                                        \
+  case RR:                                                                                                      \
+    hipLaunchKernelGGL(sift_blur_r_kernel<RR>, gridr, dim3(256), 0, st, src, dst, prev, dog, h, w, pitch, stride, \
+                       dog_stride, T);                                                                          \
     return;
   switch (T.r) {
     VO_BLUR_CASE(1) VO_BLUR_CASE(2) VO_BLUR_CASE(3) VO_BLUR_CASE(4) VO_BLUR_CASE(5) VO_BLUR_CASE(6)
@@ -230,6 +242,8 @@ __global__ __launch_bounds__(256) void sift_down_kernel(const float* __restrict_
 
 constexpr int kMaxOctaves = 16;
 constexpr int kCandRegions = 64;  // candidate appends spread over this many counters
+constexpr int kExtRun = 8;        // rows per thread of the extrema test
+constexpr int kCandStride = 64;   // ints between two candidate counters (own 256-byte line)
 
 // Per-octave DoG geometry of a batch (all octaves in one launch of the refinement).
 struct DogGeom {
@@ -373,47 +387,84 @@ __device__ __forceinline__ void refine_one(const ExtView& A, const float* D, int
 // appended to the candidate list (refined by sift_refine_kernel, all octaves at once, so
 // the few candidates do not hold a whole wave each through the Newton steps).
 __global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
+  // thread = one column and a run of kExtRun rows; the 3 x 3 x 3 neighbourhood slides down
+  // the run in registers (a ring of three rows per level, static slots after unrolling):
+  // 9 loads per pixel instead of 27
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int r = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int r0 = blockIdx.y * (4 * kExtRun) + (threadIdx.x >> 6) * kExtRun;
   const int lz = blockIdx.z % A.n_layers, b = blockIdx.z / A.n_layers;
   const int layer0 = lz + 1;
-  bool ext = false;
-  if (c >= kBorder && c < A.w - kBorder && r >= kBorder && r < A.h - kBorder) {
-    const float* D = A.dog + (long)b * A.img_stride;
-    const float* img = D + (long)layer0 * A.lvl_stride;
-    const float val = at(img, A.pitch, r, c);
-    if (fabsf(val) > (float)A.threshold) {
-      const float* prv = img - A.lvl_stride;
-      const float* nxt = img + A.lvl_stride;
+  const int rs = max(r0, kBorder), re = min(r0 + kExtRun, A.h - kBorder);
+  const bool colok = c >= kBorder && c < A.w - kBorder;
+  const int cc = colok ? c : kBorder;  // loads stay inside the image
+  const float* L1 = A.dog + (long)b * A.img_stride + (long)layer0 * A.lvl_stride;
+  const float* Lv[3] = {L1 - A.lvl_stride, L1, L1 + A.lvl_stride};
+  float W[3][3][3];  // [level][ring slot][column - 1]
+  auto ld = [&](int slot, int r) {
+    const long ro = (long)min(max(r, 0), A.h - 1) * A.pitch + cc;
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+      W[l][slot][0] = Lv[l][ro - 1];
+      W[l][slot][1] = Lv[l][ro];
+      W[l][slot][2] = Lv[l][ro + 1];
+    }
+  };
+  ld(0, r0 - 1);
+  ld(1, r0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ int s_off[4][kExtRun];
+  __shared__ int s_base;
+  uint64_t bal[kExtRun];
+#pragma unroll
+  for (int u = 0; u < kExtRun; ++u) {
+    const int r = r0 + u;
+    ld((u + 2) % 3, r + 1);
+    const int sl[3] = {u % 3, (u + 1) % 3, (u + 2) % 3};  // rows r - 1, r, r + 1
+    const float val = W[1][sl[1]][1];
+    bool ext = false;
+    if (colok && r >= rs && r < re && fabsf(val) > (float)A.threshold) {
       bool is_max = val > 0, is_min = val < 0;
 #pragma unroll
-      for (int dy = -1; dy <= 1; ++dy)
+      for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-          const float a = at(prv, A.pitch, r + dy, c + dx), n = at(nxt, A.pitch, r + dy, c + dx);
+        for (int dx = 0; dx < 3; ++dx) {
+          const float a = W[0][sl[dy]][dx], n = W[2][sl[dy]][dx];
           is_max = is_max && val >= a && val >= n;
           is_min = is_min && val <= a && val <= n;
-          if (dy != 0 || dx != 0) {
-            const float s = at(img, A.pitch, r + dy, c + dx);
-            is_max = is_max && val >= s;
-            is_min = is_min && val <= s;
+          if (dy != 1 || dx != 1) {
+            const float sv = W[1][sl[dy]][dx];
+            is_max = is_max && val >= sv;
+            is_min = is_min && val <= sv;
           }
         }
       ext = is_max || is_min;
     }
+    bal[u] = __ballot(ext);
+    if (lane == 0) s_off[wave][u] = __popcll(bal[u]);
   }
-  // one append per wave (ballot + the lane's rank), on one of kCandRegions counters
-  const uint64_t bal = __ballot(ext);
-  if (bal == 0) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((unsigned long long)bal) - 1;
-  const int region = (int)((blockIdx.x + 7u * blockIdx.y + 13u * blockIdx.z + (threadIdx.x >> 6)) % kCandRegions);
-  int base = 0;
-  if (lane == leader) base = atomicAdd(A.cand_n + region, __popcll(bal));
-  base = __shfl(base, leader);
-  if (ext) {
-    const int slot = base + __popcll(bal & ((1ull << lane) - 1ull));
-    if (slot < A.cand_cap) A.cand[(long)region * A.cand_cap + slot] = pack_cand(b, A.octave, layer0, r, c);
+  // the workgroup's candidates in (wave, row, lane) order: one atomic per workgroup, on one
+  // of kCandRegions counters (each on its own 256-byte line)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int q = 0; q < 4 * kExtRun; ++q) {
+      const int v = s_off[q / kExtRun][q % kExtRun];
+      s_off[q / kExtRun][q % kExtRun] = acc;
+      acc += v;
+    }
+    const int region = (int)((blockIdx.x + 7u * blockIdx.y + 13u * blockIdx.z) % kCandRegions);
+    s_base = acc ? atomicAdd(A.cand_n + region * kCandStride, acc) : 0;
+    s_off[0][0] = region;  // (offset 0 of the first group is always 0)
+  }
+  __syncthreads();
+  const int region = s_off[0][0], base = s_base;
+  const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int u = 0; u < kExtRun; ++u) {
+    if ((bal[u] >> lane) & 1ull) {
+      const int slot = base + (wave == 0 && u == 0 ? 0 : s_off[wave][u]) + __popcll(bal[u] & lt);
+      if (slot < A.cand_cap) A.cand[(long)region * A.cand_cap + slot] = pack_cand(b, A.octave, layer0, r0 + u, c);
+    }
   }
 }
 
@@ -421,7 +472,7 @@ __global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
 // the device-side count); accepted keypoints appended with an atomic counter.
 __global__ __launch_bounds__(256) void sift_refine_kernel(RefArgs RA) {
   const int region = blockIdx.y;
-  const int ncand = RA.cand_n[region];
+  const int ncand = RA.cand_n[region * kCandStride];
   if (ncand > RA.cand_cap) {  // candidates were dropped: poison the count (host raises)
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(RA.count, 1 << 30);
     return;
@@ -569,10 +620,11 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
   for (int o = 0; o < g.n_oct; ++o) cand_px += (int64_t)g.oh[o] * g.ow[o];
   const int cand_cap = (int)std::min<int64_t>(((int64_t)batch * n_layers * cand_px / 4) / kCandRegions + 1024,
                                               (int64_t)1 << 26);  // per region
-  ws.cand_ext.reserve((size_t)kCandRegions * cand_cap * sizeof(uint64_t) + kCandRegions * sizeof(int32_t));
+  ws.cand_ext.reserve((size_t)kCandRegions * cand_cap * sizeof(uint64_t) +
+                      (size_t)kCandRegions * kCandStride * sizeof(int32_t));
   uint64_t* cand = ws.cand_ext.as<uint64_t>();
   int32_t* cand_n = reinterpret_cast<int32_t*>(cand + (size_t)kCandRegions * cand_cap);
-  VO_HIP_CHECK(hipMemsetAsync(cand_n, 0, kCandRegions * sizeof(int32_t), st));
+  VO_HIP_CHECK(hipMemsetAsync(cand_n, 0, (size_t)kCandRegions * kCandStride * sizeof(int32_t), st));
   ctx->prof.begin(st, kKSiftExtrema);
   for (int o = 0; o < g.n_oct; ++o) {
     const int oh = g.oh[o], ow = g.ow[o];
@@ -590,8 +642,8 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
     A.cand = cand;
     A.cand_cap = cand_cap;
     A.cand_n = cand_n;
-    hipLaunchKernelGGL(sift_extrema_kernel, dim3(ceil_div(ow, 64), ceil_div(oh, 4), batch * n_layers), dim3(256),
-                       0, st, A);
+    hipLaunchKernelGGL(sift_extrema_kernel, dim3(ceil_div(ow, 64), ceil_div(oh, 4 * kExtRun), batch * n_layers),
+                       dim3(256), 0, st, A);
   }
   if (capacity > 0 || d_kpf) {
     RefArgs R{};
