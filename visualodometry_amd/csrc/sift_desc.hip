@@ -53,6 +53,7 @@ constexpr int kMaxOct = 16;
 constexpr int kOriBins = 36;
 constexpr int kOriChunk = 1024;
 constexpr int kD = 4, kN = 8, kDesc = kD * kD * kN;
+constexpr int kCountStride = 64;                // ints between per-image append counters (own 256-byte line)
 constexpr int kOkpFloats = 8;                   // x, y, size, angle, response (doubled-image units), octave word
 constexpr float kFltEps = 1.1920928955078125e-07f;
 
@@ -76,7 +77,7 @@ struct OriArgs {
   const int32_t* cand_count;
   int cand_cap, cap_img;
   float* okp;                 // (batch, cap_img, 8)
-  int32_t* img_count;         // (batch)
+  int32_t* img_count;         // (batch) at stride kCountStride
   ExpTab tab;
 };
 
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(64) void sift_orient_kernel(OriArgs A) {
         bin = bin < 0 ? (float)kOriBins + bin : (bin >= kOriBins ? bin - (float)kOriBins : bin);
         float angle = 360.f - (360.f / kOriBins) * bin;
         if (fabsf(angle - 360.f) < kFltEps) angle = 0.f;
-        const int slot = atomicAdd(A.img_count + b, 1);
+        const int slot = atomicAdd(A.img_count + b * kCountStride, 1);
         if (slot < A.cap_img) {
           float* R = A.okp + ((long)b * A.cap_img + slot) * kOkpFloats;
           R[0] = F[0];
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(256) void sift_keys_kernel(const float* __restrict_
   const int b = (int)(g / cap_img), s = (int)(g - (long)b * cap_img);
   if (b >= batch) return;
   vals[g] = (uint32_t)g;
-  if (s >= min(img_count[b], cap_img)) {
+  if (s >= min(img_count[b * kCountStride], cap_img)) {
     keys[g] = ~0ull;  // unused slot: after every image
     return;
   }
@@ -243,9 +244,9 @@ __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
   __shared__ uint32_t s_prefix, s_rank;
   const int b = blockIdx.x, tid = threadIdx.x;
   const long base = (long)b * A.cap_img;
-  const int cnt = A.img_count[b];
+  const int cnt = A.img_count[b * kCountStride];
   long sbase = 0;  // this image's first element in the batch-wide sorted order
-  for (int q = 0; q < b; ++q) sbase += min(A.img_count[q], A.cap_img);
+  for (int q = 0; q < b; ++q) sbase += min(A.img_count[q * kCountStride], A.cap_img);
   if (*A.cand_count > A.cand_cap || cnt > A.cap_img) {
     if (tid == 0) A.sel_count[b] = -1;
     return;
@@ -642,7 +643,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   ws.okp.reserve(slots * kOkpFloats * sizeof(float));
   ws.keys.reserve(slots * 2 * sizeof(uint64_t));
   ws.vals.reserve(slots * 3 * sizeof(uint32_t));
-  ws.segs.reserve((size_t)4 * batch * sizeof(int32_t));
+  ws.segs.reserve((size_t)(kCountStride + 1) * batch * sizeof(int32_t));
   float* okp = ws.okp.as<float>();
   uint64_t* keys_in = ws.keys.as<uint64_t>();
   uint64_t* keys_out = keys_in + slots;
@@ -650,12 +651,12 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   uint32_t* vals_out = vals_in + slots;
   uint32_t* sel = vals_out + slots;
   int32_t* img_count = ws.segs.as<int32_t>();
-  int32_t* sel_count = img_count + batch;
+  int32_t* sel_count = img_count + (size_t)batch * kCountStride;
   hipStream_t st = ctx->stream;
   const ExpTab tab = make_exp_tab();
 
   ctx->prof.begin(st, kKSiftOrient);
-  VO_HIP_CHECK(hipMemsetAsync(img_count, 0, batch * sizeof(int32_t), st));
+  VO_HIP_CHECK(hipMemsetAsync(img_count, 0, (size_t)batch * kCountStride * sizeof(int32_t), st));
   OriArgs oa;
   oa.G = G;
   oa.O = O;
