@@ -306,7 +306,9 @@ struct ExtView {
   int32_t* count;
 };
 
-__device__ __forceinline__ void refine_one(const ExtView& A, const float* D, int b, int layer0, int r, int c) {
+// adjustLocalExtrema of one candidate: true and the keypoint record (F, Q) when accepted.
+__device__ __forceinline__ bool refine_one(const ExtView& A, const float* D, int b, int layer0, int r, int c,
+                                           float (&F)[kKpFloats], int32_t (&Q)[kKpInts]) {
   // adjustLocalExtrema (oracle/sift_ref.py adjust_local_extremum)
   const float img_scale = 1.0f / 255.0f;
   const float deriv_scale = img_scale * 0.5f, second = img_scale, cross = img_scale * 0.25f;
@@ -336,14 +338,14 @@ __device__ __forceinline__ void refine_one(const ExtView& A, const float* D, int
     xc = -X[0];
     if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
     const float lim = (float)(2147483647 / 3);
-    if (fabsf(xi) > lim || fabsf(xr) > lim || fabsf(xc) > lim) return;
+    if (fabsf(xi) > lim || fabsf(xr) > lim || fabsf(xc) > lim) return false;
     cc += (int)rint(xc);
     rr += (int)rint(xr);
     layer += (int)rint(xi);
     if (layer < 1 || layer > A.n_layers || cc < kBorder || cc >= A.w - kBorder || rr < kBorder || rr >= A.h - kBorder)
-      return;
+      return false;
   }
-  if (i >= kMaxInterp) return;
+  if (i >= kMaxInterp) return false;
   const float* I = D + (long)layer * A.lvl_stride;
   const float* P = I - A.lvl_stride;
   const float* N = I + A.lvl_stride;
@@ -353,18 +355,15 @@ __device__ __forceinline__ void refine_one(const ExtView& A, const float* D, int
                        (at(N, p, rr, cc) - at(P, p, rr, cc)) * deriv_scale};
   const float t = (0.0f + dD[0] * xc + dD[1] * xr) + dD[2] * xi;
   const float contr = at(I, p, rr, cc) * img_scale + t * 0.5f;
-  if (fabsf(contr) * (float)A.n_layers < A.contrast) return;
+  if (fabsf(contr) * (float)A.n_layers < A.contrast) return false;
   const float v2 = at(I, p, rr, cc) * 2.0f;
   const float dxx = (at(I, p, rr, cc + 1) + at(I, p, rr, cc - 1) - v2) * second;
   const float dyy = (at(I, p, rr + 1, cc) + at(I, p, rr - 1, cc) - v2) * second;
   const float dxy = (at(I, p, rr + 1, cc + 1) - at(I, p, rr + 1, cc - 1) - at(I, p, rr - 1, cc + 1) +
                      at(I, p, rr - 1, cc - 1)) * cross;
   const float tr = dxx + dyy, det = dxx * dyy - dxy * dxy;
-  if (det <= 0.0f || tr * tr * A.edge >= (A.edge + 1.0f) * (A.edge + 1.0f) * det) return;
-  const int slot = atomicAdd(A.count, 1);
-  if (slot >= A.capacity) return;
+  if (det <= 0.0f || tr * tr * A.edge >= (A.edge + 1.0f) * (A.edge + 1.0f) * det) return false;
   const float scale = (float)(1 << A.octave);
-  float* F = A.kp_f + (long)slot * kKpFloats;
   F[0] = ((float)cc + xc) * scale;
   F[1] = ((float)rr + xr) * scale;
   // powf(2, e) as (float)exp2((double)e): correctly rounded on host and device alike
@@ -372,7 +371,6 @@ __device__ __forceinline__ void refine_one(const ExtView& A, const float* D, int
   F[3] = fabsf(contr);
   F[4] = xi;
   F[5] = F[6] = F[7] = 0.0f;
-  int32_t* Q = A.kp_i + (long)slot * kKpInts;
   Q[0] = b;
   Q[1] = A.octave + (layer << 8) + ((int)rint(((double)xi + 0.5) * 255) << 16);
   Q[2] = layer0;
@@ -381,6 +379,7 @@ __device__ __forceinline__ void refine_one(const ExtView& A, const float* D, int
   Q[5] = cc;
   Q[6] = r;
   Q[7] = c;
+  return true;
 }
 
 // One thread per DoG pixel of levels 1..n_layers: the 26-neighbour test; extrema are
@@ -478,26 +477,49 @@ __global__ __launch_bounds__(256) void sift_refine_kernel(RefArgs RA) {
     return;
   }
   const uint64_t* cand = RA.cand + (long)region * RA.cand_cap;
-  for (int ci = blockIdx.x * 256 + threadIdx.x; ci < ncand; ci += gridDim.x * 256) {
-    const uint64_t pc = cand[ci];
-    const int b = (int)(pc >> 48), o = (int)((pc >> 44) & 15), layer0 = (int)((pc >> 40) & 15);
-    const int r = (int)((pc >> 20) & 0xFFFFF), c = (int)(pc & 0xFFFFF);
-    ExtView A;
-    A.h = RA.G.h[o];
-    A.w = RA.G.w[o];
-    A.pitch = RA.G.pitch[o];
-    A.lvl_stride = (long)A.h * A.pitch;
-    A.n_layers = RA.n_layers;
-    A.octave = o;
-    A.capacity = RA.capacity;
-    A.contrast = RA.contrast;
-    A.edge = RA.edge;
-    A.sigma = RA.sigma;
-    A.kp_f = RA.kp_f;
-    A.kp_i = RA.kp_i;
-    A.count = RA.count;
-    const float* D = RA.G.dog + (long)b * RA.G.img_stride + RA.G.off[o];
-    refine_one(A, D, b, layer0, r, c);
+  const int lane = threadIdx.x & 63;
+  // wave-uniform loop: accepted keypoints are appended with one atomic per wave
+  for (int wbase = blockIdx.x * 256 + (int)(threadIdx.x & ~63u); wbase < ncand; wbase += gridDim.x * 256) {
+    const int ci = wbase + lane;
+    bool ok = false;
+    float F[kKpFloats];
+    int32_t Q[kKpInts];
+    if (ci < ncand) {
+      const uint64_t pc = cand[ci];
+      const int b = (int)(pc >> 48), o = (int)((pc >> 44) & 15), layer0 = (int)((pc >> 40) & 15);
+      const int r = (int)((pc >> 20) & 0xFFFFF), c = (int)(pc & 0xFFFFF);
+      ExtView A;
+      A.h = RA.G.h[o];
+      A.w = RA.G.w[o];
+      A.pitch = RA.G.pitch[o];
+      A.lvl_stride = (long)A.h * A.pitch;
+      A.n_layers = RA.n_layers;
+      A.octave = o;
+      A.capacity = RA.capacity;
+      A.contrast = RA.contrast;
+      A.edge = RA.edge;
+      A.sigma = RA.sigma;
+      A.kp_f = RA.kp_f;
+      A.kp_i = RA.kp_i;
+      A.count = RA.count;
+      const float* D = RA.G.dog + (long)b * RA.G.img_stride + RA.G.off[o];
+      ok = refine_one(A, D, b, layer0, r, c, F, Q);
+    }
+    const uint64_t bal = __ballot(ok);
+    if (bal == 0) continue;
+    const int leader = __ffsll((unsigned long long)bal) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(RA.count, __popcll(bal));
+    base = __shfl(base, leader);
+    if (ok) {
+      const int slot = base + __popcll(bal & ((1ull << lane) - 1ull));
+      if (slot < RA.capacity) {
+#pragma unroll
+        for (int e = 0; e < kKpFloats; ++e) RA.kp_f[(long)slot * kKpFloats + e] = F[e];
+#pragma unroll
+        for (int e = 0; e < kKpInts; ++e) RA.kp_i[(long)slot * kKpInts + e] = Q[e];
+      }
+    }
   }
 }
 
