@@ -47,9 +47,10 @@ constexpr float kAtP5 = (float)0.1555786518463281 * kRad2Deg;
 constexpr float kAtP7 = (float)-0.04432655554792128 * kRad2Deg;
 constexpr float kDblEpsF = (float)2.220446049250313e-16;
 
-// Correctly rounded sqrtf on host and device: the f64 sqrt is correctly rounded and
-// 53 >= 2 * 24 + 2, so rounding it to float is too.
-VO_HD float sqrt_rn(float x) { return (float)sqrt((double)x); }
+// Correctly rounded sqrtf on host and device. On gfx950 `sqrtf` is LLVM's correctly rounded
+// expansion (v_sqrt_f32, then the fma residuals of the neighbouring floats pick the result);
+// __fsqrt_rn is not (it maps to the native approximation unless OCML_BASIC_ROUNDED_OPERATIONS).
+VO_HD float sqrt_rn(float x) { return sqrtf(x); }
 
 struct ExpTab {
   float v[64];
