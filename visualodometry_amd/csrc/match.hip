@@ -46,12 +46,8 @@ constexpr int kFloatKC = 16;        // float path: k-chunk staged in LDS
 
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r;
-#ifdef VO_MED3_VOLATILE
-  asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-#else
   // not volatile: a pure function the scheduler may interleave with the MFMAs
   asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-#endif
   return r;
 }
 
@@ -259,20 +255,11 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
     Acc a;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) a.v[mt] = v4i{0, 0, 0, 0};
-#ifdef VO_MATCH_MT_INNER
-    // k-step outer, row tile inner: consecutive MFMAs are independent (no accumulator RAW)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        a.v[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], f.bf[ks], a.v[mt], 0, 0, 0);
-#else
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         a.v[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], f.bf[ks], a.v[mt], 0, 0, 0);
-#endif
     return a;
   };
   auto epi = [&](const Acc& a, uint32_t ccol) {
@@ -295,35 +282,12 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
     for (int ch = 0; ch < nchunk; ++ch) {
       const int buf = ch & 1, cb = c0 + 64 * ch;
       if (ch + 1 < nchunk) gload(cb + 64, g, gc);  // in flight during this chunk
-#ifdef VO_MATCH_PIPE
-      // software pipeline: the next tile's fragments and MFMAs are issued before this
-      // tile's epilogue, so the VALU top-2 work overlaps the matrix pipe
-      {
-        Frag f = frag(buf, 0);
-        Acc a = mm(f);
-        uint32_t ccur = f.cc;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (u < 3 && cb + 16 * (u + 1) < c1) {
-            const Frag fn = frag(buf, u + 1);
-            const Acc an = mm(fn);
-            epi(a, ccur);
-            a = an;
-            ccur = fn.cc;
-          } else {
-            epi(a, ccur);
-            break;
-          }
-        }
-      }
-#else
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (cb + 16 * u < c1) {
           const Frag f = frag(buf, u);
           epi(mm(f), f.cc);
         }
-#endif
       if (ch + 1 < nchunk) sstore(buf ^ 1, g, gc);
       __syncthreads();
     }
