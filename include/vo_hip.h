@@ -17,8 +17,9 @@
  *   vo_triangulate        <- triangulate_points, src/modules/frontend.py:115-148
  *   vo_pnp_ransac         <- cv2.solvePnPRansac in the tracking step,
  *                            src/modules/vo.py:135-141
- *   vo_sift_detect        <- the detection half of SIFT detectAndCompute,
- *                            src/modules/frontend.py:27-32,55
+ *   vo_sift_detect_and_compute <- cv2.SIFT_create(...).detectAndCompute,
+ *                            src/modules/frontend.py:27-32,55 (vo_sift_detect: its
+ *                            extrema stage, for parity)
  *   vo_ba_*               <- new: the reference has no BA (pyceres/pycolmap
  *                            are declared in pyproject.toml:11-12 but never
  *                            imported).  Insertion point: the keyframe hook
@@ -230,14 +231,15 @@ int vo_pnp_ransac_batch_async(vo_ctx* ctx, const float* d_objpts, const float* d
  * (iterations x 5 int32), for parity tests. */
 int vo_pnp_subsets(int count, int iterations, int32_t* out);
 
-/* ---- SIFT keypoint detection (detection half) -------- */
+/* ---- SIFT keypoint detection (the extrema stage) ----- */
 /* Replaces the keypoint detection of cv2.SIFT_create(nfeatures, contrastThreshold,
  * edgeThreshold, sigma).detectAndCompute(gray, None) (reference
  * src/modules/frontend.py:27-32,55): doubled base image, Gaussian / DoG pyramid of
  * n_layers + 3 levels per octave, 26-neighbour extrema of DoG levels 1..n_layers beyond a
  * 5-pixel border with |v| > floor(0.5 contrast / n_layers * 255), adjustLocalExtrema
- * (sub-pixel fit, contrast and edge tests).  Orientation assignment, the nfeatures cut
- * and descriptors are not included.  img: h x w uint8 row-major.
+ * (sub-pixel fit, contrast and edge tests): the refined extrema before orientation
+ * assignment (vo_sift_detect_and_compute below runs the whole call; this stage is exposed
+ * for parity tests).  img: h x w uint8 row-major.
  * Per keypoint, in (octave, candidate level, row, column) order:
  *   kp_f[8]: x, y (input-image pixels), size, response, xi, 0, 0, 0
  *   kp_i[8]: image, OpenCV's octave word (first octave -1), candidate level, level,

@@ -1,9 +1,9 @@
-"""CPU oracle for SIFT keypoint detection -- TEST INFRASTRUCTURE ONLY.
+"""CPU oracle for SIFT detectAndCompute -- TEST INFRASTRUCTURE ONLY.
 
 Imported by ``tests/`` and the ``cpu_baseline`` leg of ``bench.py``; never by the product
 path.
 
-Restates the detection half of ``cv2.SIFT_create(nfeatures, contrastThreshold,
+Restates ``cv2.SIFT_create(nfeatures, contrastThreshold,
 edgeThreshold, sigma).detectAndCompute(gray, None)`` as the reference calls it
 (``src/modules/frontend.py:27-32,55``; OpenCV 4.12 ``features2d/src/sift.dispatch.cpp`` and
 ``sift.simd.hpp``; cv2 is absent here, so this follows its published source):
@@ -36,8 +36,8 @@ FMA use depend on the CPU it runs on, so no order is "the" reference):
   ``getGaussianKernel(cvRound(8 sigma + 1) | 1, sigma, CV_32F)`` (:func:`gaussian_kernel`);
 * keypoints come out in (octave, level, row, column) order; OpenCV's order after its
   parallel gather, ``removeDuplicatedSorted`` and ``retainBest`` is implementation-defined.
-* Orientation assignment (which may duplicate a keypoint per histogram peak), the
-  ``nfeatures`` cut and the descriptors are not part of this row yet.
+* Orientation assignment, the keypoint filtering and the descriptors: see the section
+  further down (``detect_and_compute``).
 
 Parity pin: OpenCV cannot run here and the reference has no fixtures, so against OpenCV
 this is **parity unpinned**.  It is pinned by known answers (``tests/test_oracle_sift.py``):

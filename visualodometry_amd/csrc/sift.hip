@@ -1,6 +1,7 @@
 // SIFT keypoint detection (scale space, DoG, extrema, sub-pixel refinement) on gfx950.
 //
-// Replaces the detection half of cv2.SIFT_create(...).detectAndCompute(gray, None) at
+// The detection stage (scale space and refined extrema) of
+// cv2.SIFT_create(...).detectAndCompute(gray, None) at
 // reference src/modules/frontend.py:27-32,55 (OpenCV 4.12 sift.dispatch.cpp /
 // sift.simd.hpp), restated with its arithmetic in oracle/sift_ref.py; this file keeps that
 // operation order in float32 with FMA contraction off, so every pyramid level is bitwise
