@@ -182,6 +182,10 @@ int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
  * layout usable [11] its rows per side m [12] separator rows s [13] bottom rows. 
  * Returns the count written, or VO_ERR_ARG (vo_last_error() says why). */
 int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* out, int n);
+/* Host only: a 64-bit FNV-1a digest of every array of the static plan (chunks, segments,
+ * slab layout, pair and camera lists, profile, K3 step tables) for `prob`; it pins the plan
+ * (and so every kernel's summation order) across planner changes (tests/golden). */
+int vo_ba_plan_digest(const vo_ba_problem* prob, int target_segments, uint64_t* digest);
 
 /* ---- triangulation ----------------------------------- */
 /* Replaces triangulate_points (reference src/modules/frontend.py:115-148):

@@ -69,3 +69,19 @@ def test_csr_from_obs_pt_is_stable():
     order, ptr = csr_from_obs_pt(3, obs_pt)
     np.testing.assert_array_equal(order, [1, 3, 2, 0, 4, 5])
     np.testing.assert_array_equal(ptr, [0, 2, 3, 6])
+
+
+def test_plan_digests_pinned():
+    """The static BA plan (chunks, segments, slab layout, pair lists, profile, K3 tables)
+    is bitwise the one recorded in tests/golden/plan_digests.json: planner changes must
+    not move any kernel's summation order (tests/golden/make_plan_digests.py)."""
+    import json
+    import sys
+
+    from tests.conftest import ROOT
+
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import make_plan_digests
+
+    want = json.loads((ROOT / "tests" / "golden" / "plan_digests.json").read_text())
+    assert make_plan_digests.digests() == want

@@ -107,6 +107,18 @@ def plan_probe(K, point_ptr, obs_cam, obs_uv, n_poses: int, n_fixed: int = 2,
     return dict(zip(keys[:n], out[:n].tolist()))
 
 
+def plan_digest(K, point_ptr, obs_cam, obs_uv, n_poses: int, n_fixed: int = 2, target_segments: int = 512) -> int:
+    """Host-only 64-bit digest of the whole static plan (``vo_ba_plan_digest``): pins the
+    planner's output, and with it every kernel's summation order."""
+    point_ptr = np.ascontiguousarray(point_ptr, dtype=np.int32)
+    obs_cam = np.ascontiguousarray(obs_cam, dtype=np.int32)
+    obs_uv = np.ascontiguousarray(obs_uv, dtype=np.float32).reshape(-1, 2)
+    prob = _problem_struct(K, point_ptr, obs_cam, obs_uv, n_poses, n_fixed, 0.0)
+    d = C.c_uint64(0)
+    check(_lib.load().vo_ba_plan_digest(C.byref(prob), int(target_segments), C.byref(d)), "vo_ba_plan_digest")
+    return int(d.value)
+
+
 class BASession:
     """A BA problem resident on one device (structure + state in HBM).
 

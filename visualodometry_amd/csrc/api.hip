@@ -580,6 +580,20 @@ int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n) {
   return g != VO_OK ? g : k;
 }
 
+int vo_ba_plan_digest(const vo_ba_problem* prob, int target_segments, uint64_t* digest) {
+  return guarded([&] {
+    VO_REQUIRE(prob && digest, VO_ERR_ARG, "vo_ba_plan_digest: null argument");
+    std::vector<int32_t> zero(1, 0);
+    vo::BAPlan P;
+    std::string err = vo::build_plan(P, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed,
+                                     prob->n_points ? prob->point_ptr : zero.data(), prob->obs_cam,
+                                     prob->obs_uv, target_segments);
+    VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_plan_digest: %s", err.c_str());
+    vo::build_profile(P, vo::local_profile_first(P));
+    *digest = vo::plan_digest(P);
+  });
+}
+
 int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* out, int n) {
   int k = 0;
   int g = guarded([&] {

@@ -567,4 +567,29 @@ void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
   build_two_sided(P);
 }
 
+uint64_t plan_digest(const BAPlan& P) {
+  uint64_t h = 1469598103934665603ull;
+  auto bytes = [&](const void* p, size_t n) {
+    const unsigned char* c = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  };
+  auto vec = [&](const auto& v) {
+    const uint64_t n = v.size();
+    bytes(&n, sizeof n);
+    if (n) bytes(v.data(), n * sizeof(v[0]));
+  };
+  const int32_t sizes[6] = {P.n_poses, P.n_points, P.n_obs, P.n_fixed, P.n_free, P.n_te};
+  bytes(sizes, sizeof sizes);
+  vec(P.pt_perm); vec(P.obs_uv); vec(P.obs_cam); vec(P.obs_te); vec(P.te_cam); vec(P.te_pt); vec(P.te_obs);
+  vec(P.te_lcam); vec(P.pt_te); vec(P.chunk_obs); vec(P.chunk_te); vec(P.chunk_pt); vec(P.chunk_slot_base);
+  vec(P.chunk_cam_base); vec(P.chunk_hdr); vec(P.slab_pos); vec(P.cam_pos); vec(P.seg_hdr); vec(P.chunk_img);
+  vec(P.slot_ptr); vec(P.pair_list); vec(P.cam_ptr); vec(P.cam_list); vec(P.camo_ptr); vec(P.camo_list);
+  vec(P.seg_chunk); vec(P.seg_slot_off); vec(P.seg_cam_off); vec(P.slot_i); vec(P.slot_j); vec(P.segcam_f);
+  vec(P.segcam_diag); vec(P.seg_acam_off); vec(P.seg_acam); vec(P.obs_acam); vec(P.prof_first); vec(P.prof_off);
+  vec(P.prof_last); vec(P.prof_src_ptr); vec(P.prof_src); vec(P.prof_diag); vec(P.camb_ptr); vec(P.camb_src);
+  vec(P.solve_tab); vec(P.solve2_tab);
+  bytes(&P.solve2_layout, sizeof P.solve2_layout);
+  return h;
+}
+
 }  // namespace vo

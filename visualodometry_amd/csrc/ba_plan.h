@@ -158,5 +158,7 @@ std::string build_plan(BAPlan& plan, int n_poses, int n_points, int n_obs, int n
 std::vector<int32_t> local_profile_first(const BAPlan& plan);
 // Builds the profile and the K2 reduction index from a (possibly all-reduced) first[].
 void build_profile(BAPlan& plan, const std::vector<int32_t>& first);
+// 64-bit FNV-1a over every plan array in a fixed order (vo_ba_plan_digest).
+uint64_t plan_digest(const BAPlan& plan);
 
 }  // namespace vo
