@@ -69,7 +69,16 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     const int p = P.pt_perm[q];
     idx.resize(point_ptr[p + 1] - point_ptr[p]);
     std::iota(idx.begin(), idx.end(), point_ptr[p]);
-    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return obs_cam[a] < obs_cam[b]; });
+    // stable insertion sort by camera (tracks are short; no allocation per landmark)
+    for (size_t i = 1; i < idx.size(); ++i) {
+      const int32_t v = idx[i];
+      size_t j = i;
+      while (j > 0 && obs_cam[idx[j - 1]] > obs_cam[v]) {
+        idx[j] = idx[j - 1];
+        --j;
+      }
+      idx[j] = v;
+    }
     for (size_t k = 0; k < idx.size(); ++k) {
       const int o = idx[k];
       if (k == 0 || obs_cam[o] != obs_cam[idx[k - 1]]) {
@@ -108,6 +117,13 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     P.chunk_pt.push_back(q);
     c_obs = c_te = c_pts = c_pairs = 0;
   };
+  // membership of the open segment's cameras and camera pairs: stamp tables (stamp = the
+  // segment's number) when the free cameras are few, the linear searches otherwise
+  const int Nf = N - n_fixed;
+  const bool tables = Nf <= kPlanTableCams;
+  std::vector<int32_t> cam_stamp(tables ? N : 0, -1), fcam_stamp(tables ? std::max(Nf, 1) : 0, -1);
+  std::vector<int32_t> pair_stamp(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, -1);
+  auto seg_id = [&]() { return (int32_t)segs.size() - 1; };
   for (int q = 0; q < L; ++q) {
     const int t0 = P.pt_te[q], t1 = P.pt_te[q + 1];
     const int nob = P.te_obs[t1] - P.te_obs[t0], nte = t1 - t0;
@@ -128,16 +144,25 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     bool seg_fits = seg_open;
     if (seg_open) {
       Seg& s = segs.back();
+      const int32_t sid = seg_id();
       int ncams = (int)s.cams.size();
-      for (int c : cq) ncams += find_or_neg(s.cams, c) < 0;
       int nslots = (int)s.slots.size();
-      for (int a = 0; a < k; ++a)
-        for (int b = 0; b <= a; ++b) {
-          const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
-          nslots += std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end();
-        }
       int nacams = (int)s.acams.size();
-      for (int t = t0; t < t1; ++t) nacams += find_or_neg(s.acams, P.te_cam[t]) < 0;
+      if (tables) {
+        for (int c : cq) ncams += fcam_stamp[c] != sid;
+        for (int a = 0; a < k; ++a)
+          for (int b = 0; b <= a; ++b)
+            nslots += pair_stamp[(size_t)std::max(cq[a], cq[b]) * Nf + std::min(cq[a], cq[b])] != sid;
+        for (int t = t0; t < t1; ++t) nacams += cam_stamp[P.te_cam[t]] != sid;
+      } else {
+        for (int c : cq) ncams += find_or_neg(s.cams, c) < 0;
+        for (int a = 0; a < k; ++a)
+          for (int b = 0; b <= a; ++b) {
+            const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
+            nslots += std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end();
+          }
+        for (int t = t0; t < t1; ++t) nacams += find_or_neg(s.acams, P.te_cam[t]) < 0;
+      }
       seg_fits = ncams <= kSegCams && nslots <= kSegSlots && nacams <= kSegAllCams;
     }
     if (!seg_fits || (!chunk_fits && s_obs >= seg_obs_target)) {
@@ -149,15 +174,38 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       open_chunk(q);
     }
     Seg& s = segs.back();
-    for (int c : cq)
-      if (find_or_neg(s.cams, c) < 0) s.cams.push_back(c);
-    for (int t = t0; t < t1; ++t)
-      if (find_or_neg(s.acams, P.te_cam[t]) < 0) s.acams.push_back(P.te_cam[t]);
-    for (int a = 0; a < k; ++a)
-      for (int b = 0; b <= a; ++b) {
-        const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
-        if (std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end()) s.slots.push_back(pr);
-      }
+    const int32_t sid = seg_id();
+    if (tables) {
+      for (int c : cq)
+        if (fcam_stamp[c] != sid) {
+          fcam_stamp[c] = sid;
+          s.cams.push_back(c);
+        }
+      for (int t = t0; t < t1; ++t)
+        if (cam_stamp[P.te_cam[t]] != sid) {
+          cam_stamp[P.te_cam[t]] = sid;
+          s.acams.push_back(P.te_cam[t]);
+        }
+      for (int a = 0; a < k; ++a)
+        for (int b = 0; b <= a; ++b) {
+          const int32_t hi = std::max(cq[a], cq[b]), lo = std::min(cq[a], cq[b]);
+          int32_t& st = pair_stamp[(size_t)hi * Nf + lo];
+          if (st != sid) {
+            st = sid;
+            s.slots.push_back(std::make_pair(hi, lo));
+          }
+        }
+    } else {
+      for (int c : cq)
+        if (find_or_neg(s.cams, c) < 0) s.cams.push_back(c);
+      for (int t = t0; t < t1; ++t)
+        if (find_or_neg(s.acams, P.te_cam[t]) < 0) s.acams.push_back(P.te_cam[t]);
+      for (int a = 0; a < k; ++a)
+        for (int b = 0; b <= a; ++b) {
+          const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
+          if (std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end()) s.slots.push_back(pr);
+        }
+    }
     c_obs += nob;
     c_te += nte;
     c_pts += 1;
@@ -178,6 +226,13 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   P.obs_acam.assign(std::max(M, 1), 0);
   P.chunk_slot_base.assign(nchunks, 0);
   P.chunk_cam_base.assign(nchunks, 0);
+  // per-segment lookup tables (camera -> window index, camera pair -> slot) and reusable
+  // counting-sort buffers for the per-chunk lists
+  std::vector<int32_t> fcam_idx(tables ? std::max(Nf, 1) : 0, -1), acam_idx(tables ? N : 0, -1);
+  std::vector<int32_t> pair_slot(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, -1);
+  std::vector<int32_t> cnt, cnt2;
+  std::vector<uint16_t> pairs_tmp;
+  std::vector<int32_t> pairs_slot;
   for (size_t si = 0; si < segs.size(); ++si) {
     Seg& s = segs[si];
     std::sort(s.cams.begin(), s.cams.end());
@@ -189,16 +244,27 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       P.slot_j.push_back(pr.second);
     }
     std::sort(s.acams.begin(), s.acams.end());
+    if (tables) {
+      for (size_t i = 0; i < s.cams.size(); ++i) fcam_idx[s.cams[i]] = (int32_t)i;
+      for (size_t i = 0; i < s.acams.size(); ++i) acam_idx[s.acams[i]] = (int32_t)i;
+      for (size_t i = 0; i < s.slots.size(); ++i) pair_slot[(size_t)s.slots[i].first * Nf + s.slots[i].second] = (int32_t)i;
+    }
+    auto lcam_of = [&](int32_t c) {  // window index of free camera c
+      return tables ? fcam_idx[c] : (int32_t)(std::lower_bound(s.cams.begin(), s.cams.end(), c) - s.cams.begin());
+    };
+    auto slot_of = [&](const std::pair<int32_t, int32_t>& pr) {
+      return tables ? pair_slot[(size_t)pr.first * Nf + pr.second]
+                    : (int32_t)(std::lower_bound(s.slots.begin(), s.slots.end(), pr) - s.slots.begin());
+    };
     P.seg_acam.insert(P.seg_acam.end(), s.acams.begin(), s.acams.end());
     P.seg_acam_off.push_back((int32_t)P.seg_acam.size());
     for (int o = P.chunk_obs[ch0]; o < P.chunk_obs[ch1]; ++o)
-      P.obs_acam[o] = (uint8_t)(std::lower_bound(s.acams.begin(), s.acams.end(), P.obs_cam[o]) -
-                                s.acams.begin());
+      P.obs_acam[o] = (uint8_t)(tables ? acam_idx[P.obs_cam[o]]
+                                       : std::lower_bound(s.acams.begin(), s.acams.end(), P.obs_cam[o]) -
+                                             s.acams.begin());
     for (int c : s.cams) {
       P.segcam_f.push_back(c);
-      const auto d = std::make_pair(c, c);
-      P.segcam_diag.push_back(
-          (int32_t)(std::lower_bound(s.slots.begin(), s.slots.end(), d) - s.slots.begin()));
+      P.segcam_diag.push_back(slot_of(std::make_pair(c, c)));
     }
     P.seg_chunk.push_back(ch1);
     P.seg_slot_off.push_back((int32_t)P.slot_i.size());
@@ -207,49 +273,57 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     for (int ch = ch0; ch < ch1; ++ch) {
       const int te0 = P.chunk_te[ch];
       for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
-        if (P.te_cam[t] >= n_fixed) {
-          const int lc = (int)(std::lower_bound(s.cams.begin(), s.cams.end(), P.te_cam[t] - n_fixed) -
-                               s.cams.begin());
-          P.te_lcam[t] = (int16_t)lc;
-        }
-      // pair lists by slot
-      std::vector<std::vector<uint16_t>> lists(ns);
+        if (P.te_cam[t] >= n_fixed) P.te_lcam[t] = (int16_t)lcam_of(P.te_cam[t] - n_fixed);
+      // pair lists by slot: a stable counting sort of the (x, y) pairs in generation order
+      pairs_tmp.clear();
+      pairs_slot.clear();
       for (int q = P.chunk_pt[ch]; q < P.chunk_pt[ch + 1]; ++q) {
         for (int x = P.pt_te[q]; x < P.pt_te[q + 1]; ++x) {
           if (P.te_cam[x] < n_fixed) continue;
           for (int y = P.pt_te[q]; y <= x; ++y) {
             if (P.te_cam[y] < n_fixed) continue;
-            const auto pr = std::make_pair(P.te_cam[x] - n_fixed, P.te_cam[y] - n_fixed);
-            const int sl = (int)(std::lower_bound(s.slots.begin(), s.slots.end(), pr) - s.slots.begin());
-            lists[sl].push_back((uint16_t)((x - te0) | ((y - te0) << 8)));
+            pairs_slot.push_back(slot_of(std::make_pair(P.te_cam[x] - n_fixed, P.te_cam[y] - n_fixed)));
+            pairs_tmp.push_back((uint16_t)((x - te0) | ((y - te0) << 8)));
           }
         }
       }
+      cnt.assign(ns + 1, 0);
+      for (int32_t sl : pairs_slot) ++cnt[sl + 1];
+      for (int sl = 0; sl < ns; ++sl) cnt[sl + 1] += cnt[sl];
       P.chunk_slot_base[ch] = (int32_t)P.slot_ptr.size();
-      for (int sl = 0; sl < ns; ++sl) {
-        P.slot_ptr.push_back((int32_t)P.pair_list.size());
-        P.pair_list.insert(P.pair_list.end(), lists[sl].begin(), lists[sl].end());
-      }
-      P.slot_ptr.push_back((int32_t)P.pair_list.size());
-      // camera lists
-      std::vector<std::vector<uint8_t>> cl(nc);
+      const int32_t pbase = (int32_t)P.pair_list.size();
+      for (int sl = 0; sl < ns; ++sl) P.slot_ptr.push_back(pbase + cnt[sl]);
+      P.slot_ptr.push_back(pbase + cnt[ns]);
+      P.pair_list.resize(pbase + pairs_tmp.size());
+      for (size_t e = 0; e < pairs_tmp.size(); ++e) P.pair_list[pbase + cnt[pairs_slot[e]]++] = pairs_tmp[e];
+      // camera lists: track entries and observations by window camera, in order
+      cnt.assign(nc + 1, 0);
       for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
-        if (P.te_lcam[t] >= 0) cl[P.te_lcam[t]].push_back((uint8_t)(t - te0));
-      std::vector<std::vector<uint8_t>> co(nc);
+        if (P.te_lcam[t] >= 0) ++cnt[P.te_lcam[t] + 1];
+      cnt2.assign(nc + 1, 0);
       const int ob0 = P.chunk_obs[ch];
-      for (int o = ob0; o < P.chunk_obs[ch + 1]; ++o) {
-        const int t = P.obs_te[o];
-        if (P.te_lcam[t] >= 0) co[P.te_lcam[t]].push_back((uint8_t)(o - ob0));
+      for (int o = ob0; o < P.chunk_obs[ch + 1]; ++o)
+        if (P.te_lcam[P.obs_te[o]] >= 0) ++cnt2[P.te_lcam[P.obs_te[o]] + 1];
+      for (int c = 0; c < nc; ++c) {
+        cnt[c + 1] += cnt[c];
+        cnt2[c + 1] += cnt2[c];
       }
       P.chunk_cam_base[ch] = (int32_t)P.cam_ptr.size();
+      const int32_t cbase = (int32_t)P.cam_list.size(), obase = (int32_t)P.camo_list.size();
       for (int c = 0; c < nc; ++c) {
-        P.cam_ptr.push_back((int32_t)P.cam_list.size());
-        P.cam_list.insert(P.cam_list.end(), cl[c].begin(), cl[c].end());
-        P.camo_ptr.push_back((int32_t)P.camo_list.size());
-        P.camo_list.insert(P.camo_list.end(), co[c].begin(), co[c].end());
+        P.cam_ptr.push_back(cbase + cnt[c]);
+        P.camo_ptr.push_back(obase + cnt2[c]);
       }
-      P.cam_ptr.push_back((int32_t)P.cam_list.size());
-      P.camo_ptr.push_back((int32_t)P.camo_list.size());
+      P.cam_ptr.push_back(cbase + cnt[nc]);
+      P.camo_ptr.push_back(obase + cnt2[nc]);
+      P.cam_list.resize(cbase + cnt[nc]);
+      P.camo_list.resize(obase + cnt2[nc]);
+      for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
+        if (P.te_lcam[t] >= 0) P.cam_list[cbase + cnt[P.te_lcam[t]]++] = (uint8_t)(t - te0);
+      for (int o = ob0; o < P.chunk_obs[ch + 1]; ++o) {
+        const int lc = P.te_lcam[P.obs_te[o]];
+        if (lc >= 0) P.camo_list[obase + cnt2[lc]++] = (uint8_t)(o - ob0);
+      }
     }
   }
   if (P.pair_list.empty()) P.pair_list.push_back(0);  // keep device arrays non-empty

@@ -37,6 +37,7 @@ constexpr int kChunkHdr = 16;
 
 constexpr int kSegCams = 24;     // free (window) cameras of a segment
 constexpr int kSegAllCams = 16;  // all cameras its observations reference (poses staged in LDS)
+constexpr int kPlanTableCams = 512;  // planner: flat lookup tables up to this many free cameras
 
 // Per segment, kSegHdr ints: [0] nslots [1] slot offset [2] first window camera [3] window
 // cameras [4] cameras seen [5] first chunk [6] end chunk [7] spare | [8..15] cameras seen
