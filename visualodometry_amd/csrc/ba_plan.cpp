@@ -1,6 +1,8 @@
 // Host-side static planner for the BA Gauss-Newton step (see ba_plan.h).
 #include "ba_plan.h"
 
+#include <thread>
+
 #include <algorithm>
 #include <cstdio>
 #include <numeric>
@@ -353,39 +355,53 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       h[13] = P.camo_ptr[cb + nc];
     }
   }
-  // chunk LDS images
-  P.chunk_img.assign((size_t)std::max(nchunks, 1), ChunkImg());
-  for (size_t si = 0; si + 1 < P.seg_chunk.size(); ++si) {
-    const int ns = P.seg_slot_off[si + 1] - P.seg_slot_off[si];
-    const int nc = P.seg_cam_off[si + 1] - P.seg_cam_off[si];
-    const int cam0 = P.seg_cam_off[si];
-    for (int ch = P.seg_chunk[si]; ch < P.seg_chunk[si + 1]; ++ch) {
-      ChunkImg& g = P.chunk_img[ch];
-      const int32_t* h = &P.chunk_hdr[(size_t)ch * kChunkHdr];
-      const int ob0 = h[0], nob = h[1], te0 = h[2], nte = h[3], p0 = h[4], npt = h[5];
-      const int sb = h[6], cb = h[7], e0 = h[8], e1 = h[9], c0 = h[10], c1 = h[11], q0 = h[12], q1 = h[13];
-      for (int i = 0; i < nob; ++i) {
-        g.obs_te[i] = P.obs_te[ob0 + i] - te0;
-        g.uv[2 * i] = P.obs_uv[2 * (ob0 + i)];
-        g.uv[2 * i + 1] = P.obs_uv[2 * (ob0 + i) + 1];
-        g.acam[i] = P.obs_acam[ob0 + i];
+  // chunk LDS images: independent per chunk, built on a few host threads (segment ranges)
+  P.chunk_img.resize((size_t)std::max(nchunks, 1));
+  if (nchunks == 0) P.chunk_img[0] = ChunkImg();
+  auto build_imgs = [&P](size_t seg_a, size_t seg_b) {
+    for (size_t si = seg_a; si < seg_b; ++si) {
+      const int ns = P.seg_slot_off[si + 1] - P.seg_slot_off[si];
+      const int nc = P.seg_cam_off[si + 1] - P.seg_cam_off[si];
+      const int cam0 = P.seg_cam_off[si];
+      for (int ch = P.seg_chunk[si]; ch < P.seg_chunk[si + 1]; ++ch) {
+        ChunkImg& g = P.chunk_img[ch];
+        g = ChunkImg();
+        const int32_t* h = &P.chunk_hdr[(size_t)ch * kChunkHdr];
+        const int ob0 = h[0], nob = h[1], te0 = h[2], nte = h[3], p0 = h[4], npt = h[5];
+        const int sb = h[6], cb = h[7], e0 = h[8], e1 = h[9], c0 = h[10], c1 = h[11], q0 = h[12], q1 = h[13];
+        for (int i = 0; i < nob; ++i) {
+          g.obs_te[i] = P.obs_te[ob0 + i] - te0;
+          g.uv[2 * i] = P.obs_uv[2 * (ob0 + i)];
+          g.uv[2 * i + 1] = P.obs_uv[2 * (ob0 + i) + 1];
+          g.acam[i] = P.obs_acam[ob0 + i];
+        }
+        for (int i = 0; i <= nte; ++i) g.te_obs[i] = P.te_obs[te0 + i] - ob0;
+        for (int i = 0; i < nte; ++i) {
+          g.te_pt[i] = P.te_pt[te0 + i] - p0;
+          g.te_lcam[i] = P.te_lcam[te0 + i];
+        }
+        for (int i = 0; i <= npt; ++i) g.pt_te[i] = P.pt_te[p0 + i] - te0;
+        for (int i = 0; i <= ns; ++i) g.slotp[i] = P.slot_ptr[sb + i] - e0;
+        for (int i = 0; i < e1 - e0; ++i) g.pairs[i] = P.pair_list[e0 + i];
+        for (int i = 0; i <= nc; ++i) {
+          g.camp[i] = P.cam_ptr[cb + i] - c0;
+          g.camop[i] = P.camo_ptr[cb + i] - q0;
+        }
+        for (int i = 0; i < c1 - c0; ++i) g.caml[i] = P.cam_list[c0 + i];
+        for (int i = 0; i < q1 - q0; ++i) g.camol[i] = P.camo_list[q0 + i];
+        for (int i = 0; i < nc; ++i) g.dslot[i] = P.segcam_diag[cam0 + i];
       }
-      for (int i = 0; i <= nte; ++i) g.te_obs[i] = P.te_obs[te0 + i] - ob0;
-      for (int i = 0; i < nte; ++i) {
-        g.te_pt[i] = P.te_pt[te0 + i] - p0;
-        g.te_lcam[i] = P.te_lcam[te0 + i];
-      }
-      for (int i = 0; i <= npt; ++i) g.pt_te[i] = P.pt_te[p0 + i] - te0;
-      for (int i = 0; i <= ns; ++i) g.slotp[i] = P.slot_ptr[sb + i] - e0;
-      for (int i = 0; i < e1 - e0; ++i) g.pairs[i] = P.pair_list[e0 + i];
-      for (int i = 0; i <= nc; ++i) {
-        g.camp[i] = P.cam_ptr[cb + i] - c0;
-        g.camop[i] = P.camo_ptr[cb + i] - q0;
-      }
-      for (int i = 0; i < c1 - c0; ++i) g.caml[i] = P.cam_list[c0 + i];
-      for (int i = 0; i < q1 - q0; ++i) g.camol[i] = P.camo_list[q0 + i];
-      for (int i = 0; i < nc; ++i) g.dslot[i] = P.segcam_diag[cam0 + i];
     }
+  };
+  {
+    const size_t nseg_img = P.seg_chunk.size() - 1;
+    const int nthr = (int)std::min<size_t>(std::max(1u, std::min(8u, std::thread::hardware_concurrency())),
+                                            std::max<size_t>(1, nchunks / 128));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nthr; ++t)
+      pool.emplace_back(build_imgs, nseg_img * t / nthr, nseg_img * (t + 1) / nthr);
+    build_imgs(0, nseg_img / nthr);
+    for (auto& th : pool) th.join();
   }
   // segment headers (kSegHdr)
   const int nseg = (int)P.seg_chunk.size() - 1;
