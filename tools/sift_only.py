@@ -1,5 +1,6 @@
 """The SIFT bench line alone (bench.bench_sift) with per-kernel HIP-event averages; for
-quick GPU iterations on the SIFT kernels."""
+quick GPU iterations on the SIFT kernels.  --no-check skips the parity guard (timing-only
+diagnostic builds)."""
 import json
 import sys
 from pathlib import Path
@@ -9,6 +10,6 @@ import bench  # noqa: E402
 from visualodometry_amd import _lib  # noqa: E402
 
 ctx = _lib.context(0)
-r = bench.bench_sift(ctx)
+r = bench.bench_sift(ctx, check="--no-check" not in sys.argv)
 r.pop("cpu_baseline", None)
 print(json.dumps(r))

@@ -360,14 +360,17 @@ struct DescArgs {
 constexpr int kDescThreads = 256;
 constexpr int kPosCap = 768;   // compacted window positions per pass (uint16: windows < 65536)
 constexpr int kMaxBatch = 256;
+constexpr int kLists = 16 * 9;   // (interior cell, orientation slot 0..8) bins
+constexpr int kMskSlots = 26;    // 16 cell masks, a zero guard, 8 bin masks, a zero guard
 
 __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
-  // per 256-position block of the window: for each of the 16 interior cells, the samples
-  // that vote into it, in window order, as (obin, value after the row and column
-  // interpolation)
-  __shared__ float2 s_list[16][kDescThreads];   // (v_o0, v_o1): the two orientation shares
-  __shared__ uint8_t s_o0[16][kDescThreads];     // the lower orientation bin o0 (wrapped)
-  __shared__ int s_cnt[kDescThreads / 64][16];
+  // per 256-position block of the window: for each of the 144 (cell, orientation slot) bins,
+  // the terms it receives, in window order
+  __shared__ float s_pool[kDescThreads * 8];           // list terms: <= 4 cells x 2 slots per sample
+  __shared__ uint64_t s_msk[kDescThreads / 64][kMskSlots];
+  __shared__ int s_lc[kDescThreads / 64][kLists];      // per-wave entry counts
+  __shared__ int s_wb[kDescThreads / 64][kLists];      // per-wave write bases
+  __shared__ int s_lb[kLists], s_lt[kLists];           // list base and length
   __shared__ uint16_t s_pos[kPosCap];  // valid window positions of the current pass, in order
   __shared__ int s_wc[kDescThreads / 64];
   __shared__ float s_h[16 * 9];
@@ -387,11 +390,8 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
   if (blockIdx.x == 0 && tid < A.batch) A.count_out[tid] = A.sel_count[tid];
   __syncthreads();
   const int total = s_off[A.batch];
-  // consumer ownership: wave w -> cell row Rc = w + 1 of the (d+2)^2 grid; lane < 36 ->
-  // cell column Cc = lane / 9 + 1 and orientation slot O = lane % 9 (slot 9 never receives:
+  // list ownership: thread t < 144 sums bin t = cell * 9 + slot (slot 9 never receives:
   // o0 + 1 <= n)
-  const int Rc = wave + 1, Cc = lane / 9 + 1, O = lane % 9;
-  const int my_cell = (Rc - 1) * 4 + (Cc - 1);
   for (int g = blockIdx.x; g < total; g += gridDim.x) {
     int b = 0;
     while (s_off[b + 1] <= g) ++b;
@@ -461,11 +461,16 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
             const float r_rot = (float)j * sin_t + (float)i * cos_t;
             const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
             const int r = py + i, c = px + j;
+#ifdef VO_DESC_DIAG_NOSAMPLE  // timing-only diagnostic: no gathers, no transcendental math
+            const float w = 1.0f, Ori = (float)(k & 255), Mag = 1.0f;
+            (void)r; (void)c;
+#else
             const float dx = img[(long)r * pitch + c + 1] - img[(long)r * pitch + c - 1];
             const float dy = img[(long)(r - 1) * pitch + c] - img[(long)(r + 1) * pitch + c];
             const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, A.tab.v);
             const float Ori = fast_atan2_deg(dy, dx);
             const float Mag = sqrt_rn(dx * dx + dy * dy);
+#endif
             const float obin = (Ori - ori) * bins_per_rad;
             const float mag = Mag * w;
             o0 = (int)floorf(obin);
@@ -480,10 +485,12 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
             v_r0 = mag - v_r1;
           }
         }
-        // stable per-cell lists: the sample votes into interior cells q = (r0 + dr) * 4 + (c0 + dc),
-        // dr, dc in {0, 1} (cell row r0 + 1 + dr of the (d+2)^2 grid): its hit mask, one
-        // ballot per cell, the wave's count per cell stored by lane q, and the cell's offset
-        // of this wave (the counts of the waves before it) computed once by lane q
+        // (cell, slot) lists: the sample adds v_o0 to slot o0 and v_o1 to slot o0 + 1 of each
+        // interior cell q = (r0 + dr) * 4 + (c0 + dc) it votes into (dr, dc in {0, 1}; cell row
+        // r0 + 1 + dr of the (d+2)^2 grid).  List L = q * 9 + slot holds exactly the terms bin
+        // L receives from this block, in window order: a wave's entries are ranked by ballot
+        // (lanes are in window order), and a scan lays the waves' runs and the lists out in one
+        // pool.  The owner of L then sums a dense list.
         uint32_t hit = 0;
         if (valid) {
   #pragma unroll
@@ -494,61 +501,106 @@ __global__ __launch_bounds__(kDescThreads) void sift_desc_kernel(DescArgs A) {
               if ((unsigned)rr < 4u && (unsigned)cc < 4u) hit |= 1u << (rr * 4 + cc);
             }
         }
+        // the wave's masks: cells (s_msk[0..15]) and lower orientation bins (s_msk[17 + k]),
+        // with zero guards at 16 and 25 for the bins -1 and 8
         uint64_t bal[16];
-        int cntv = 0;
+        uint64_t mv = 0;
   #pragma unroll
         for (int q = 0; q < 16; ++q) {
           bal[q] = __ballot((hit >> q) & 1u);
-          cntv = lane == q ? __popcll(bal[q]) : cntv;
+          mv = lane == q ? bal[q] : mv;
         }
-        if (lane < 16) s_cnt[wave][lane] = cntv;
+  #pragma unroll
+        for (int k = 0; k < kN; ++k) {
+          const uint64_t ob_k = __ballot(hit != 0u && o0 == k);
+          mv = lane == 17 + k ? ob_k : mv;
+        }
+        if (lane < kMskSlots) s_msk[wave][lane] = mv;
         __syncthreads();
-        int basev = 0;
-        if (lane < 16)
-          for (int w = 0; w < wave; ++w) basev += s_cnt[w][lane];
+        // per-wave entry counts of the 144 lists: the wave's samples voting into cell q whose
+        // o0 is the slot or the slot - 1
+        for (int L = lane; L < kLists; L += 64) {
+          const int q = L / 9, sl = L - 9 * q;
+          s_lc[wave][L] = __popcll(s_msk[wave][q] & (s_msk[wave][17 + sl] | s_msk[wave][16 + sl]));
+        }
+        __syncthreads();
+        // wave 0 lays the lists out: lane l owns lists 3l .. 3l + 2 (l < 48)
+        if (wave == 0) {
+          int t3[3], sum = 0;
+  #pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            const int L = 3 * lane + u;
+            t3[u] = L < kLists ? s_lc[0][L] + s_lc[1][L] + s_lc[2][L] + s_lc[3][L] : 0;
+            sum += t3[u];
+          }
+          int incl = sum;
+  #pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+          }
+          int base = incl - sum;
+  #pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            const int L = 3 * lane + u;
+            if (L < kLists) {
+              s_lb[L] = base;
+              s_lt[L] = t3[u];
+              int wb = base;
+  #pragma unroll
+              for (int w = 0; w < kDescThreads / 64; ++w) {
+                s_wb[w][L] = wb;
+                wb += s_lc[w][L];
+              }
+            }
+            base += t3[u];
+          }
+        }
+        __syncthreads();
         if (hit) {
+          // samples of this wave feeding slot o0 (their o0 is o0 or o0 - 1) and slot o0 + 1
+          const uint64_t m_s0 = s_msk[wave][17 + o0] | s_msk[wave][16 + o0];
+          const uint64_t m_s1 = s_msk[wave][18 + o0] | s_msk[wave][17 + o0];
+          auto rank = [](uint64_t m) {
+            return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          };
   #pragma unroll
           for (int q = 0; q < 16; ++q) {
             if ((hit >> q) & 1u) {
-              const uint64_t m = bal[q];
-              const int off = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
-                              __builtin_amdgcn_readlane(basev, q);
               const int dr = q / 4 - r0, dc = q % 4 - c0;
               const float vr = dr ? v_r1 : v_r0;
               const float v_c1 = vr * cb, v_c0 = vr - v_c1;
               const float vc = dc ? v_c1 : v_c0;
               const float v_o1 = vc * ob, v_o0 = vc - v_o1;
-              s_list[q][off] = make_float2(v_o0, v_o1);
-              s_o0[q][off] = (uint8_t)o0;
+              const int L = q * 9 + o0;
+              s_pool[s_wb[wave][L] + rank(bal[q] & m_s0)] = v_o0;
+              s_pool[s_wb[wave][L + 1] + rank(bal[q] & m_s1)] = v_o1;
             }
           }
         }
         __syncthreads();
-        // the owner of (cell, O) adds its orientation share of each entry, in order (+0.0 when
-        // missed: an identity, every partial sum is >= +0)
-        if (lane < 36) {
-          const int nl = s_cnt[0][my_cell] + s_cnt[1][my_cell] + s_cnt[2][my_cell] + s_cnt[3][my_cell];
-          const float2* L = s_list[my_cell];
-          const uint8_t* L0 = s_o0[my_cell];
-          auto step = [&](const float2 e, const int o0) {
-            const int dO = O - o0;
-            acc = acc + (dO == 0 ? e.x : (dO == 1 ? e.y : 0.0f));
-          };
+        // the owner of list L adds its terms in order.  No barrier follows: the next block
+        // writes s_pool, s_lb and s_lt only after two barriers every owner must reach first.
+#ifdef VO_DESC_DIAG_NOCONSUME  // timing-only diagnostic: no list sums
+        if (tid < 0) {
+#else
+        if (tid < kLists) {
+#endif
+          const float* P = s_pool + s_lb[tid];
+          const int nl = s_lt[tid];
           int t = 0;
           for (; t + 4 <= nl; t += 4) {
-            float2 e[4];
-            const uint32_t o4 = *reinterpret_cast<const uint32_t*>(L0 + t);
+            float e[4];
   #pragma unroll
-            for (int u = 0; u < 4; ++u) e[u] = L[t + u];
+            for (int u = 0; u < 4; ++u) e[u] = P[t + u];
   #pragma unroll
-            for (int u = 0; u < 4; ++u) step(e[u], (o4 >> (8 * u)) & 255);
+            for (int u = 0; u < 4; ++u) acc = acc + e[u];
           }
-          for (; t < nl; ++t) step(L[t], L0[t]);
+          for (; t < nl; ++t) acc = acc + P[t];
         }
-        __syncthreads();
       }
     }
-    if (lane < 36) s_h[((Rc - 1) * 4 + (Cc - 1)) * 9 + O] = acc;
+    if (tid < kLists) s_h[tid] = acc;
     __syncthreads();
     if (tid < kDesc) {
       const int q = tid / kN, k = tid % kN;
