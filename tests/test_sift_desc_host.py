@@ -2,13 +2,13 @@
 
 The kernel compacts the window's valid positions in order and processes them 256 at a
 time (this emulation keeps blocks of 256 positions: the per-bin order, window order, is the
-same); each valid sample is appended, in window order, to the LDS list of every interior
-descriptor cell it votes into
-as (obin, value after the row and column interpolation); the lane owning (cell,
-orientation slot) then walks its cell's list adding its orientation share.  This test
-restates that block / list / owner walk in float32 numpy and checks that it reproduces
-``oracle.sift_ref.descriptor`` bit for bit (no sample missed, none counted twice, the
-per-bin order kept), on keypoints of every angle quadrant and scale.
+same).  Each valid sample appends, in window order, its two orientation shares to the list
+of each (interior cell, orientation slot) bin it votes into: v_o0 to slot o0 and v_o1 to
+slot o0 + 1, for every cell of its 2 x 2 row/column footprint.  The thread owning bin
+(cell, slot) then sums that list in order.  This test restates that block / bin-list / owner
+sum in float32 numpy and checks that it reproduces ``oracle.sift_ref.descriptor`` bit for
+bit (no sample missed, none counted twice, the per-bin order kept), on keypoints of every
+angle quadrant and scale.
 """
 
 import math
@@ -41,7 +41,7 @@ def emulate(img, x, y, ori, scl, d=4, n=8):
     side = 2 * radius + 1
     acc = np.zeros((16, 9), f)
     for k0 in range(0, side * side, 256):
-        lists = [[] for _ in range(16)]
+        lists = [[[] for _ in range(9)] for _ in range(16)]  # (cell, slot) bin lists
         for k in range(k0, min(k0 + 256, side * side)):
             i, j = k // side - radius, k % side - radius
             c_rot, r_rot, rbin, cbin = geom(i, j)
@@ -55,6 +55,10 @@ def emulate(img, x, y, ori, scl, d=4, n=8):
             Mag = S.magnitude(np.array([dx]), np.array([dy]))[0]
             obin = f(f(Ori - ori) * bins_per_rad)
             mag = f(Mag * w)
+            o0 = math.floor(obin)
+            ob = f(obin - f(o0))
+            o0 = o0 + n if o0 < 0 else o0
+            o0 = o0 - n if o0 >= n else o0
             r0, c0 = math.floor(rbin), math.floor(cbin)
             rb, cb = f(rbin - f(r0)), f(cbin - f(c0))
             v_r1 = f(mag * rb)
@@ -64,19 +68,15 @@ def emulate(img, x, y, ori, scl, d=4, n=8):
                 if dr in (0, 1) and dc in (0, 1):
                     vr = v_r1 if dr else v_r0
                     v_c1 = f(vr * cb)
-                    lists[q].append((obin, v_c1 if dc else f(vr - v_c1)))
+                    vc = v_c1 if dc else f(vr - v_c1)
+                    v_o1 = f(vc * ob)
+                    lists[q][o0].append(f(vc - v_o1))
+                    lists[q][o0 + 1].append(v_o1)
         for q in range(16):
             for O in range(9):
                 a = acc[q, O]
-                for obin, vc in lists[q]:
-                    o0 = math.floor(obin)
-                    ob = f(obin - f(o0))
-                    o0 = o0 + n if o0 < 0 else o0
-                    o0 = o0 - n if o0 >= n else o0
-                    dO = O - o0
-                    if dO in (0, 1):
-                        v_o1 = f(vc * ob)
-                        a = f(a + (v_o1 if dO else f(vc - v_o1)))
+                for v in lists[q][O]:
+                    a = f(a + v)
                 acc[q, O] = a
     h = acc
     raw = np.empty(128, f)
@@ -95,7 +95,7 @@ def emulate(img, x, y, ori, scl, d=4, n=8):
     return np.clip(np.rint((raw * nrm2).astype(f)), 0, 255).astype(f)
 
 
-def test_record_walk_matches_oracle():
+def test_bin_list_sums_match_oracle():
     img = S.gaussian_pyramid(sift_scene(120, 160, seed=4, n_blobs=30, n_boxes=8))[0][2]
     rng = np.random.default_rng(0)
     for t in range(8):

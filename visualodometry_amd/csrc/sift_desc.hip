@@ -357,10 +357,14 @@ struct DescArgs {
   ExpTab tab;
 };
 
-constexpr int kDescThreads = 256;
-constexpr int kPosCap = 768;   // compacted window positions per pass (uint16: windows < 65536)
+#ifndef VO_DESC_THREADS
+#define VO_DESC_THREADS 256
+#endif
+constexpr int kDescThreads = VO_DESC_THREADS;  // samples per block (one per thread)
+constexpr int kPosCap = 3 * kDescThreads;  // compacted window positions per pass (uint16: windows < 65536)
 constexpr int kMaxBatch = 256;
 constexpr int kLists = 16 * 9;   // (interior cell, orientation slot 0..8) bins
+constexpr int kOwn = (kLists + kDescThreads - 1) / kDescThreads;  // lists summed per thread
 constexpr int kMskSlots = 26;    // 16 cell masks, a zero guard, 8 bin masks, a zero guard
 // resident descriptor workgroups per CU: every phase of a block is a short latency chain
 // (barriers, LDS round trips), so throughput comes from workgroups overlapping (8: 2017 ->
@@ -370,7 +374,7 @@ constexpr int kMskSlots = 26;    // 16 cell masks, a zero guard, 8 bin masks, a 
 #endif
 constexpr int kDescWgPerCu = VO_DESC_WG_PER_CU;
 
-__global__ __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_eu(kDescWgPerCu)))
+__global__ __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_eu(kDescWgPerCu * kDescThreads / 256)))
 void sift_desc_kernel(DescArgs A) {
   // per 256-position block of the window: for each of the 144 (cell, orientation slot) bins,
   // the terms it receives, in window order
@@ -424,7 +428,9 @@ void sift_desc_kernel(DescArgs A) {
     radius = min(radius, (int)sqrt((double)cols * cols + (double)rows * rows));
     const float cos_t = __fdiv_rn(cos0, hist_width), sin_t = __fdiv_rn(sin0, hist_width);
     const int side = 2 * radius + 1, len = side * side;
-    float acc = 0.0f;
+    float acc[kOwn];  // the sums of lists tid + w * kDescThreads
+  #pragma unroll
+    for (int w = 0; w < kOwn; ++w) acc[w] = 0.0f;
     // The window's positions, in order, are classified 256 at a time by the cheap geometry
     // test and the valid ones compacted into s_pos (about half of the square window lies
     // outside the rotated descriptor square); the sample work then runs on dense blocks.
@@ -538,7 +544,10 @@ void sift_desc_kernel(DescArgs A) {
   #pragma unroll
           for (int u = 0; u < 3; ++u) {
             const int L = 3 * lane + u;
-            t3[u] = L < kLists ? s_lc[0][L] + s_lc[1][L] + s_lc[2][L] + s_lc[3][L] : 0;
+            int t = 0;
+  #pragma unroll
+            for (int w = 0; w < kDescThreads / 64; ++w) t += L < kLists ? s_lc[w][L] : 0;
+            t3[u] = t;
             sum += t3[u];
           }
           int incl = sum;
@@ -594,21 +603,31 @@ void sift_desc_kernel(DescArgs A) {
 #else
         if (tid < kLists) {
 #endif
-          const float* P = s_pool + s_lb[tid];
-          const int nl = s_lt[tid];
-          int t = 0;
-          for (; t + 4 <= nl; t += 4) {
-            float e[4];
   #pragma unroll
-            for (int u = 0; u < 4; ++u) e[u] = P[t + u];
+          for (int w = 0; w < kOwn; ++w) {
+            const int L = tid + w * kDescThreads;
+            if (L < kLists) {
+              const float* P = s_pool + s_lb[L];
+              const int nl = s_lt[L];
+              float a = acc[w];
+              int t = 0;
+              for (; t + 4 <= nl; t += 4) {
+                float e[4];
   #pragma unroll
-            for (int u = 0; u < 4; ++u) acc = acc + e[u];
+                for (int u = 0; u < 4; ++u) e[u] = P[t + u];
+  #pragma unroll
+                for (int u = 0; u < 4; ++u) a = a + e[u];
+              }
+              for (; t < nl; ++t) a = a + P[t];
+              acc[w] = a;
+            }
           }
-          for (; t < nl; ++t) acc = acc + P[t];
         }
       }
     }
-    if (tid < kLists) s_h[tid] = acc;
+  #pragma unroll
+    for (int w = 0; w < kOwn; ++w)
+      if (tid + w * kDescThreads < kLists) s_h[tid + w * kDescThreads] = acc[w];
     __syncthreads();
     if (tid < kDesc) {
       const int q = tid / kN, k = tid % kN;
