@@ -52,6 +52,7 @@ using namespace siftm;
 constexpr int kMaxOct = 16;
 constexpr int kOriBins = 36;
 constexpr int kOriChunk = 1024;
+constexpr int kOriPerLane = kOriChunk / 64;  // chunk samples per lane of the one-wave workgroup
 constexpr int kD = 4, kN = 8, kDesc = kD * kD * kN;
 constexpr int kCountStride = 64;                // ints between per-image append counters (own 256-byte line)
 constexpr int kOkpFloats = 8;                   // x, y, size, angle, response (doubled-image units), octave word
@@ -81,11 +82,17 @@ struct OriArgs {
   ExpTab tab;
 };
 
-__global__ __launch_bounds__(64) void sift_orient_kernel(OriArgs A) {
-  __shared__ int4 s_bin4[kOriChunk / 4];
-  __shared__ float4 s_val4[kOriChunk / 4];
-  int* s_bin = reinterpret_cast<int*>(s_bin4);
-  float* s_val = reinterpret_cast<float*>(s_val4);
+// resident one-wave workgroups per CU; the loop is persistent, so the grid must not exceed
+// what fits (a second, late half of the grid would double the wall time)
+#ifndef VO_ORI_WG_PER_CU
+#define VO_ORI_WG_PER_CU 24
+#endif
+constexpr int kOriWgPerCu = VO_ORI_WG_PER_CU;
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOriWgPerCu / 4)))
+void sift_orient_kernel(OriArgs A) {
+  __shared__ float s_val[kOriChunk];  // the chunk's terms grouped by bin, window order inside a bin
+  __shared__ int s_run[kOriBins], s_base[kOriBins];
   __shared__ float s_th[kOriBins + 4];
   __shared__ float s_h[kOriBins];
   const int lane = threadIdx.x;
@@ -106,12 +113,20 @@ __global__ __launch_bounds__(64) void sift_orient_kernel(OriArgs A) {
     float acc = 0.0f;
     for (int k0 = 0; k0 < len; k0 += kOriChunk) {
       const int kn = min(kOriChunk, len - k0);
-      for (int t = lane; t < kn; t += 64) {
+      // samples t = lane + 64 u of the chunk (window order = (u, lane)); each is ranked
+      // inside its bin by a stable counting sort: peers (same bin) from six bit ballots, the
+      // rank among earlier peers by mbcnt, the bin's running count in s_run
+      if (lane < kOriBins) s_run[lane] = 0;
+      float vv[kOriPerLane];
+      int bb[kOriPerLane], rk[kOriPerLane];
+#pragma unroll
+      for (int u = 0; u < kOriPerLane; ++u) {
+        const int t = lane + 64 * u;
         const int k = k0 + t, i = k / side - radius, j = k % side - radius;
         const int y = pr + i, x = pc + j;
         int bin = -1;
         float v = 0.0f;
-        if (y > 0 && y < rows - 1 && x > 0 && x < cols - 1) {
+        if (t < kn && y > 0 && y < rows - 1 && x > 0 && x < cols - 1) {
           const float dx = img[(long)y * pitch + x + 1] - img[(long)y * pitch + x - 1];
           const float dy = img[(long)(y - 1) * pitch + x] - img[(long)(y + 1) * pitch + x];
           const float w = exp32f((float)(i * i + j * j) * expf_scale, A.tab.v);
@@ -122,32 +137,44 @@ __global__ __launch_bounds__(64) void sift_orient_kernel(OriArgs A) {
           if (bin < 0) bin += kOriBins;
           v = w * mag;
         }
-        s_bin[t] = bin;
-        s_val[t] = v;
-      }
-      __syncthreads();
-      // lane b sums the samples of bin b in sample order (+0.0 elsewhere: an identity,
-      // every partial sum is >= +0)
-      if (lane < kOriBins) {
-        // sixteen samples per LDS wait
-        int t = 0;
-        for (; t + 16 <= kn; t += 16) {
-          int4 bb[4];
-          float4 vv[4];
+        const int key = bin < 0 ? 63 : bin;  // 63: no bin (outside the image or the chunk)
+        uint64_t peers = ~0ull;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            bb[u] = s_bin4[(t >> 2) + u];
-            vv[u] = s_val4[(t >> 2) + u];
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            acc = acc + (bb[u].x == lane ? vv[u].x : 0.0f);
-            acc = acc + (bb[u].y == lane ? vv[u].y : 0.0f);
-            acc = acc + (bb[u].z == lane ? vv[u].z : 0.0f);
-            acc = acc + (bb[u].w == lane ? vv[u].w : 0.0f);
-          }
+        for (int bit = 0; bit < 6; ++bit) {
+          const uint64_t m = __ballot((key >> bit) & 1);
+          peers &= ((key >> bit) & 1) ? m : ~m;
         }
-        for (; t < kn; ++t) acc = acc + (s_bin[t] == lane ? s_val[t] : 0.0f);
+        const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+        rk[u] = bin >= 0 ? s_run[bin] + r : 0;
+        // the last peer carries the group's count (one wave: LDS keeps its accesses in order)
+        if (bin >= 0 && (peers >> lane) == 1ull) s_run[bin] = rk[u] + 1;
+        bb[u] = bin;
+        vv[u] = v;
+      }
+      // bin b's list starts at the sum of the earlier bins' counts
+      int cnt = lane < kOriBins ? s_run[lane] : 0, incl = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      if (lane < kOriBins) s_base[lane] = incl - cnt;
+#pragma unroll
+      for (int u = 0; u < kOriPerLane; ++u)
+        if (bb[u] >= 0) s_val[s_base[bb[u]] + rk[u]] = vv[u];
+      __syncthreads();
+      // lane b sums bin b's samples in window order
+      if (lane < kOriBins) {
+        const float* P = s_val + (incl - cnt);
+        int t = 0;
+        for (; t + 4 <= cnt; t += 4) {
+          float e[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) e[u] = P[t + u];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc = acc + e[u];
+        }
+        for (; t < cnt; ++t) acc = acc + P[t];
       }
       __syncthreads();
     }
@@ -748,7 +775,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   oa.img_count = img_count;
   oa.tab = tab;
   // persistent: 64-lane workgroups looping over the candidates (count is on the device)
-  const int ori_blocks = std::max(1, std::min(cand_cap, ctx->num_cus * 32));
+  const int ori_blocks = std::max(1, std::min(cand_cap, ctx->num_cus * kOriWgPerCu));
   hipLaunchKernelGGL(sift_orient_kernel, dim3(ori_blocks), dim3(64), 0, st, oa);
   VO_HIP_CHECK(hipGetLastError());
   ctx->prof.end(st);
