@@ -461,9 +461,10 @@ void sift_desc_kernel(DescArgs A) {
     // The window's positions, in order, are classified 256 at a time by the cheap geometry
     // test and the valid ones compacted into s_pos (about half of the square window lies
     // outside the rotated descriptor square); the sample work then runs on dense blocks.
-    int kk0 = 0;
-    while (kk0 < len) {
-      int n = 0;
+    // While the window has positions left, only full blocks are processed and the remainder
+    // (< one block, ahead of every later position) is carried to the front of s_pos.
+    int kk0 = 0, n = 0;
+    while (kk0 < len || n > 0) {
       while (kk0 < len && n + kDescThreads <= kPosCap) {
         const int k = kk0 + tid;
         bool v = false;
@@ -489,8 +490,9 @@ void sift_desc_kernel(DescArgs A) {
         kk0 += kDescThreads;
         __syncthreads();
       }
-      for (int t0 = 0; t0 < n; t0 += kDescThreads) {
-        const bool valid = t0 + tid < n;
+      const int nproc = kk0 < len ? (n & ~(kDescThreads - 1)) : n;
+      for (int t0 = 0; t0 < nproc; t0 += kDescThreads) {
+        const bool valid = t0 + tid < nproc;
         int r0 = -9, c0 = -9;
         float ob = 0.0f, v_r0 = 0.0f, v_r1 = 0.0f, cb = 0.0f;
         int o0 = 0;
@@ -651,6 +653,14 @@ void sift_desc_kernel(DescArgs A) {
           }
         }
       }
+      const int rem = n - nproc;  // uniform
+      if (rem > 0) {
+        const uint16_t keep = tid < rem ? s_pos[nproc + tid] : (uint16_t)0;
+        __syncthreads();
+        if (tid < rem) s_pos[tid] = keep;
+        __syncthreads();
+      }
+      n = rem;
     }
   #pragma unroll
     for (int w = 0; w < kOwn; ++w)
