@@ -69,6 +69,18 @@ __device__ __forceinline__ const float* level_ptr(const float* G, const Octaves&
   return G + (long)b * O.g_img + O.off[o] + (long)layer * O.oh[o] * O.op[o];
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave in DPP (no LDS round trips): row_shr
+// 1/2/4/8 inside each 16-lane row, then row_bcast:15 and row_bcast:31 across rows (GFX9).
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
 // ---- orientation -------------------------------------------------------------------
 struct OriArgs {
   const float* G;
@@ -152,12 +164,7 @@ void sift_orient_kernel(OriArgs A) {
         vv[u] = v;
       }
       // bin b's list starts at the sum of the earlier bins' counts
-      int cnt = lane < kOriBins ? s_run[lane] : 0, incl = cnt;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-      }
+      const int cnt = lane < kOriBins ? s_run[lane] : 0, incl = wave_incl_scan(cnt);
       if (lane < kOriBins) s_base[lane] = incl - cnt;
 #pragma unroll
       for (int u = 0; u < kOriPerLane; ++u)
@@ -579,12 +586,7 @@ void sift_desc_kernel(DescArgs A) {
             t3[u] = t;
             sum += t3[u];
           }
-          int incl = sum;
-  #pragma unroll
-          for (int d = 1; d < 64; d <<= 1) {
-            const int y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
-          }
+          const int incl = wave_incl_scan(sum);
           int base = incl - sum;
   #pragma unroll
           for (int u = 0; u < 3; ++u) {
