@@ -395,7 +395,10 @@ struct DescArgs {
 #define VO_DESC_THREADS 256
 #endif
 constexpr int kDescThreads = VO_DESC_THREADS;  // samples per block (one per thread)
-constexpr int kPosCap = 3 * kDescThreads;  // compacted window positions per pass (uint16: windows < 65536)
+constexpr int kClassify = 2;  // window positions classified per thread and iteration
+// compacted window positions per pass (uint16: windows < 65536): a carried partial block plus
+// kClassify blocks always fit, and a pass ends with >= 2 full blocks
+constexpr int kPosCap = (kClassify + 2) * kDescThreads;
 constexpr int kMaxBatch = 256;
 constexpr int kLists = 16 * 9;   // (interior cell, orientation slot 0..8) bins
 constexpr int kOwn = (kLists + kDescThreads - 1) / kDescThreads;  // lists summed per thread
@@ -418,7 +421,7 @@ void sift_desc_kernel(DescArgs A) {
   __shared__ int s_wb[kDescThreads / 64][kLists];      // per-wave write bases
   __shared__ int s_lb[kLists], s_lt[kLists];           // list base and length
   __shared__ uint16_t s_pos[kPosCap];  // valid window positions of the current pass, in order
-  __shared__ int s_wc[kDescThreads / 64];
+  __shared__ int s_wc[kClassify][kDescThreads / 64];
   __shared__ float s_h[16 * 9];
   __shared__ float4 s_raw4[kDesc / 4];
   __shared__ int s_off[kMaxBatch + 1];
@@ -472,29 +475,40 @@ void sift_desc_kernel(DescArgs A) {
     // (< one block, ahead of every later position) is carried to the front of s_pos.
     int kk0 = 0, n = 0;
     while (kk0 < len || n > 0) {
-      while (kk0 < len && n + kDescThreads <= kPosCap) {
-        const int k = kk0 + tid;
-        bool v = false;
-        if (k < len) {
-          const int i = k / side - radius, j = k % side - radius;
-          const float c_rot = (float)j * cos_t - (float)i * sin_t;
-          const float r_rot = (float)j * sin_t + (float)i * cos_t;
-          const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
-          const int r = py + i, c = px + j;
-          v = rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 && c < cols - 1;
+      while (kk0 < len && n + kClassify * kDescThreads <= kPosCap) {
+        // kClassify * 256 positions per iteration, position kk0 + p * 256 + tid in slot p
+        bool v[kClassify];
+        uint64_t bal[kClassify];
+  #pragma unroll
+        for (int p = 0; p < kClassify; ++p) {
+          const int k = kk0 + p * kDescThreads + tid;
+          v[p] = false;
+          if (k < len) {
+            const int i = k / side - radius, j = k % side - radius;
+            const float c_rot = (float)j * cos_t - (float)i * sin_t;
+            const float r_rot = (float)j * sin_t + (float)i * cos_t;
+            const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
+            const int r = py + i, c = px + j;
+            v[p] = rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 && c < cols - 1;
+          }
+          bal[p] = __ballot(v[p]);
+          if (lane == 0) s_wc[p][wave] = __popcll(bal[p]);
         }
-        const uint64_t bal = __ballot(v);
-        if (lane == 0) s_wc[wave] = __popcll(bal);
         __syncthreads();
-        int off = n, tot = 0;
-#pragma unroll
-        for (int w = 0; w < kDescThreads / 64; ++w) {
-          off += w < wave ? s_wc[w] : 0;
-          tot += s_wc[w];
+        int base = n;
+  #pragma unroll
+        for (int p = 0; p < kClassify; ++p) {
+          int off = base, tot = 0;
+  #pragma unroll
+          for (int w = 0; w < kDescThreads / 64; ++w) {
+            off += w < wave ? s_wc[p][w] : 0;
+            tot += s_wc[p][w];
+          }
+          if (v[p]) s_pos[off + __popcll(bal[p] & ((1ull << lane) - 1ull))] = (uint16_t)(kk0 + p * kDescThreads + tid);
+          base += tot;
         }
-        if (v) s_pos[off + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)k;
-        n += tot;
-        kk0 += kDescThreads;
+        n = base;
+        kk0 += kClassify * kDescThreads;
         __syncthreads();
       }
       const int nproc = kk0 < len ? (n & ~(kDescThreads - 1)) : n;
