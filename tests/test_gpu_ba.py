@@ -65,12 +65,14 @@ def test_run_matches_c_oracle(ctx, cfg):
     assert _rel(dP, dPr) < REL
 
 
-def test_cfg4_global_solve_path(ctx):
-    """100 poses x 200k landmarks: the profile exceeds LDS -> global-memory solve."""
+def test_cfg4_matches_c_oracle(ctx):
+    """100 poses x 200k landmarks: the profile (225 KB) exceeds LDS; the banded K3 streams
+    it through its LDS rings."""
     p = make_ba_config("cfg4")
     s = _session(p, ctx)
     st = s.plan_stats()
     assert st["profile_blocks"] * 288 > 150 * 1024
+    assert st["band_solver"] == 1
     rc, costs = s.run(3)
     assert rc == _lib.VO_OK
     R = cref.BAProblemRef(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 1.0)
@@ -189,3 +191,63 @@ def test_sliding_window_api(ctx):
     np.testing.assert_allclose(res.cost_per_iter, cr, rtol=1e-8)
     assert _rel(res.poses_cw, st.poses_cw()) < REL
     assert _rel(res.points, st.X) < REL
+
+
+def _step_vs_oracle(ctx, p, lam=1.0):
+    s = _session(p, ctx, lam)
+    rc, S, b, dc, cost = s.gn_step()
+    assert rc == _lib.VO_OK
+    st = ba_ref.BAState.from_poses(p.poses_cw, p.points)
+    struct = ba_ref.BAStructure(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_fixed, p.n_poses)
+    ref = ba_ref.gn_step(st, struct, lam)
+    assert _rel(S, ref.system.S) < 1e-11
+    assert _rel(dc, ref.dc) < 1e-8
+    P, X = s.get_state()
+    assert _rel(P, ref.state.poses_cw()) < 1e-10
+    assert _rel(X, ref.state.X) < 1e-8
+    return s
+
+
+@pytest.mark.parametrize("n_poses,max_track", [(3, 2), (4, 2), (6, 8), (12, 3), (16, 8), (18, 8),
+                                               (23, 8), (40, 10), (61, 4)])
+def test_band_solver_shapes(ctx, n_poses, max_track):
+    """The banded K3 over one-sided (F < 2w + 2) and two-sided splits, odd and even F,
+    bandwidths 1..9: one GN step against the numpy oracle's dense Cholesky."""
+    p = make_ba_problem(n_poses, 40 * n_poses, 31 + n_poses, max_track=max_track)
+    s = _step_vs_oracle(ctx, p)
+    assert s.plan_stats()["band_solver"] == 1
+
+
+def _add_far_landmark(p, cams):
+    """One extra landmark seen by the given (far apart) cameras: a wide / non-monotone
+    profile row."""
+    from visualodometry_amd.synthetic import BAProblemData
+
+    X = p.points[:1] * 0.0 + np.array([[0.5, 0.2, 60.0]])
+    uv = []
+    for c in cams:
+        T = p.poses_cw[c]
+        pc = T[:3, :3] @ X[0] + T[:3, 3]
+        q = p.K @ pc
+        uv.append(q[:2] / q[2])
+    ptr = np.append(p.point_ptr, p.point_ptr[-1] + len(cams))
+    return BAProblemData(
+        **{**p.__dict__, "points": np.vstack([p.points, X]), "point_ptr": ptr,
+           "obs_cam": np.append(p.obs_cam, cams).astype(p.obs_cam.dtype),
+           "obs_uv": np.vstack([p.obs_uv, np.array(uv, dtype=p.obs_uv.dtype)])})
+
+
+def test_wide_profile_uses_profile_solver(ctx):
+    """A landmark linking keyframes 2 and 19 makes the bandwidth 17 > 9: the profile solver
+    (any envelope) takes the window."""
+    p = _add_far_landmark(make_ba_problem(20, 800, 41), [2, 19])
+    s = _step_vs_oracle(ctx, p)
+    assert s.plan_stats()["band_solver"] == 0
+
+
+def test_non_monotone_profile_band_solver(ctx):
+    """A landmark linking keyframes 2 and 11 of a short-track window: first[] is not
+    monotone and the bandwidth 9 still fits the banded K3 (zeros inside the band)."""
+    p = _add_far_landmark(make_ba_problem(12, 500, 43, max_track=3), [2, 11])
+    s = _step_vs_oracle(ctx, p)
+    assert s.plan_stats()["band_solver"] == 1

@@ -103,7 +103,7 @@ def plan_probe(K, point_ptr, obs_cam, obs_uv, n_poses: int, n_fixed: int = 2,
                                            ptr(out, C.c_int64), 14), "vo_ba_plan_probe")
     keys = ["chunks", "segments", "slab_blocks", "profile_blocks", "track_entries",
             "max_chunk_pairs", "max_segment_slots", "max_segment_cameras", "free_poses",
-            "max_row_span", "two_sided", "two_sided_m", "two_sided_s", "two_sided_nbot"]
+            "max_row_span", "band_solver", "band_top_rows", "band_separator_rows", "band_bottom_rows"]
     return dict(zip(keys[:n], out[:n].tolist()))
 
 
@@ -187,7 +187,7 @@ class BASession:
         out = np.zeros(8, dtype=np.int64)
         n = check(self.ctx.lib.vo_ba_plan_stats(self.ctx.handle, ptr(out, C.c_int64), 8), "stats")
         keys = ["chunks", "segments", "slab_blocks", "reduced_blocks", "profile_blocks",
-                "track_entries", "algorithmic_bytes_per_iter", "wide_landmarks"]
+                "track_entries", "algorithmic_bytes_per_iter", "band_solver"]
         return dict(zip(keys[:n], out[:n].tolist()))
 
 

@@ -5,6 +5,7 @@
 #include <cstring>
 #include <vector>
 
+#include "ba_band.h"
 #include "ba_plan.h"
 #include "vo_ctx.h"
 
@@ -619,10 +620,11 @@ int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* ou
     }
     int span = 0;
     for (int r = 0; r < P.n_free; ++r) span = std::max(span, r - P.prof_first[r]);
-    const vo::TwoSidedLayout& T = P.solve2_layout;
+    std::vector<int> first(P.prof_first.begin(), P.prof_first.end());
+    const vo::BandSplit T = vo::band_split(P.n_free, first);
     const int64_t v[14] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), P.n_prof_blocks(),
                            P.n_te, max_pairs, max_slots, max_cams, P.n_free, span,
-                           T.enabled, T.m, T.s, T.nbot};
+                           vo::band_supported(P.n_free, T.w, P.n_poses) ? 1 : 0, T.m, T.s, T.nb};
     k = std::min(n, 14);
     for (int i = 0; i < k; ++i) out[i] = v[i];
   });

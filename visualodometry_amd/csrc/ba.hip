@@ -40,10 +40,24 @@
 #include <string>
 #include <type_traits>
 
+#include "ba_band.h"
+#include "ba_math.h"
 #include "ba_plan.h"
 #include "vo_ctx.h"
 
 namespace vo {
+
+// Diagnostic build only (make EXTRA=-DVO_BA_STAMPS=1): per-phase s_memtime stamps of K1
+// and the profile K3.  The product build executes none.
+#ifndef VO_BA_STAMPS
+#define VO_BA_STAMPS 0
+#endif
+constexpr bool kBaStamps = VO_BA_STAMPS != 0;
+// Planner target: K1 segments per CU (profiles/r01_segment_sweep.md); a tuning build may
+// override it at compile time.
+#ifndef VO_BA_SEGMENTS_PER_CU
+#define VO_BA_SEGMENTS_PER_CU 4
+#endif
 
 #define VO_NCCL_CHECK(expr)                                                          \
   do {                                                                               \
@@ -125,7 +139,6 @@ namespace {
 constexpr int kLinThreads = 256;
 constexpr int kBsWindow = 10;  // K3 back substitution: register window of block rows
 constexpr double kPivotRelEps = 1e-12;  // == oracle/ba_ref.py PIVOT_REL_EPS
-constexpr double kExpTaylor = 1e-4;     // == oracle/ba_ref.py EXP_TAYLOR_THETA
 enum { kBacksub = 1, kAccum = 2 };
 
 struct LinArgs {
@@ -723,9 +736,13 @@ struct ReduceArgs {
   const double* slab;
   const double* slab_b;
   const double* slab_cost;
-  double* sys;  // nprof*36 + 6F + 1
+  double* sys;         // output: profile [S | b | cost] or the banded K3's column layout
+  const int* dst;      // per profile block: output offset of its 36 values (| kRedTranspose)
+  const int* rdst;     // per free camera: output offset of its 6 rhs values
+  long cost_off;       // output offset of the cost
   const int* status;
 };
+constexpr int kRedTranspose = 1 << 30;  // dst flag: store the block transposed
 
 // Sums slab rows k0 + part + j*stride (entry e of each, rows of W doubles), j = 0, 1, ...,
 // in fixed order with 4 independent loads in flight.  K1 wrote each block's window slots
@@ -769,7 +786,8 @@ __global__ __launch_bounds__(kRedThreads) void ba_reduce_kernel(ReduceArgs A) {
 #pragma unroll
       for (int q = 0; q < kRedSParts; ++q) acc += part[36 * q + tid];
       if (diag && tid % 7 == 0) acc += A.lambda;
-      A.sys[36l * blk + tid] = acc;
+      const int d = A.dst[blk];
+      A.sys[(d & ~kRedTranspose) + ((d & kRedTranspose) ? 6 * (tid % 6) + tid / 6 : tid)] = acc;
     }
     if (!diag) return;
     __syncthreads();
@@ -780,7 +798,7 @@ __global__ __launch_bounds__(kRedThreads) void ba_reduce_kernel(ReduceArgs A) {
     if (tid < 6) {
       double acc = 0.0;
       for (int q = 0; q < kRedBParts; ++q) acc += part[6 * q + tid];
-      A.sys[36l * A.nprof + 6 * f + tid] = acc;
+      A.sys[A.rdst[f] + tid] = acc;
     }
     return;
   }
@@ -793,7 +811,7 @@ __global__ __launch_bounds__(kRedThreads) void ba_reduce_kernel(ReduceArgs A) {
     if (tid < m) part[tid] += part[tid + m];
     __syncthreads();
   }
-  if (tid == 0) A.sys[36l * A.nprof + 6 * A.F] = part[0];
+  if (tid == 0) A.sys[A.cost_off] = part[0];
 }
 
 // K3: profile Cholesky solve S dc = b + pose update.
@@ -812,124 +830,7 @@ struct SolveArgs {
   unsigned long long* stamps;  // diagnostic build only
 };
 
-__device__ __forceinline__ void se3_exp_apply(const double* d, const double* T, double* out) {
-  const double r0 = d[0], r1 = d[1], r2 = d[2], p0 = d[3], p1 = d[4], p2 = d[5];
-  const double th2 = p0 * p0 + p1 * p1 + p2 * p2;
-  const double th = sqrt(th2);
-  double A, B, C;
-  if (th < kExpTaylor) {
-    A = 1.0 - th2 / 6.0;
-    B = 0.5 - th2 / 24.0;
-    C = 1.0 / 6.0 - th2 / 120.0;
-  } else {
-    double s, c;
-    sincos(th, &s, &c);
-    A = s / th;
-    B = (1.0 - c) / (th * th);
-    C = (th - s) / (th * th * th);
-  }
-  // P = [phi]x, P2 = P P
-  const double P[9] = {0, -p2, p1, p2, 0, -p0, -p1, p0, 0};
-  double P2[9];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      P2[3 * i + j] = P[3 * i] * P[j] + P[3 * i + 1] * P[3 + j] + P[3 * i + 2] * P[6 + j];
-  double Rd[9], V[9];
-#pragma unroll
-  for (int e = 0; e < 9; ++e) {
-    const double I = (e % 4 == 0) ? 1.0 : 0.0;
-    Rd[e] = I + A * P[e] + B * P2[e];
-    V[e] = I + B * P[e] + C * P2[e];
-  }
-  const double td0 = V[0] * r0 + V[1] * r1 + V[2] * r2;
-  const double td1 = V[3] * r0 + V[4] * r1 + V[5] * r2;
-  const double td2 = V[6] * r0 + V[7] * r1 + V[8] * r2;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      out[3 * i + j] = Rd[3 * i] * T[j] + Rd[3 * i + 1] * T[3 + j] + Rd[3 * i + 2] * T[6 + j];
-  }
-  out[9] = Rd[0] * T[9] + Rd[1] * T[10] + Rd[2] * T[11] + td0;
-  out[10] = Rd[3] * T[9] + Rd[4] * T[10] + Rd[5] * T[11] + td1;
-  out[11] = Rd[6] * T[9] + Rd[7] * T[10] + Rd[8] * T[11] + td2;
-}
 
-// ---- 6x6 block kernels in registers (packed lower storage, P(i,c) = i(i+1)/2 + c)
-#ifndef VO_CHOL_NEWTON
-#define VO_CHOL_NEWTON 1
-#endif
-constexpr bool kCholNewton = VO_CHOL_NEWTON != 0;
-__device__ __forceinline__ constexpr int P6(int i, int c) { return i * (i + 1) / 2 + c; }
-
-// In-place Cholesky a = L L^T; r = 1/diag(L) from v_rsq_f64 + one Newton step
-// (critical chain per column: rsq + 3 dependent ops instead of sqrt + divide; the
-// step takes the ~2^-23 estimate to ~1e-14 relative).
-// kDiag = false leaves a[P6(j, j)] unfactored: no solve reads L's diagonal (fwd6/bwd6
-// use r = 1/l_jj), only the stored factor does.
-template <bool kDiag = true>
-__device__ __forceinline__ bool chol6(double (&a)[21], double (&r)[6]) {
-  bool ok = true;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const double d = a[P6(j, j)];
-    ok = ok && d > 0.0;
-    const double dd = d > 0.0 ? d : 1.0;
-    double q = __builtin_amdgcn_rsq(dd);
-    if (kCholNewton) q = q * (1.5 - 0.5 * dd * q * q);
-    r[j] = q;
-    if (kDiag) a[P6(j, j)] = dd * q;
-#pragma unroll
-    for (int i = j + 1; i < 6; ++i) a[P6(i, j)] *= q;
-#pragma unroll
-    for (int i = j + 1; i < 6; ++i)
-#pragma unroll
-      for (int c = j + 1; c <= i; ++c) a[P6(i, c)] -= a[P6(i, j)] * a[P6(c, j)];
-  }
-  return ok;
-}
-
-// v <- L^-1 v (forward substitution); also solves x L^T = v for a row vector.
-__device__ __forceinline__ void fwd6(const double (&L)[21], const double (&r)[6], double (&v)[6]) {
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    double s = v[i];
-#pragma unroll
-    for (int m = 0; m < i; ++m) s -= L[P6(i, m)] * v[m];
-    v[i] = s * r[i];
-  }
-}
-
-// v <- L^-T v (back substitution).
-__device__ __forceinline__ void bwd6(const double (&L)[21], const double (&r)[6], double (&v)[6]) {
-#pragma unroll
-  for (int i = 5; i >= 0; --i) {
-    double s = v[i];
-#pragma unroll
-    for (int m = i + 1; m < 6; ++m) s -= L[P6(m, i)] * v[m];
-    v[i] = s * r[i];
-  }
-}
-
-// v[lane] for a register array without a runtime index (a runtime index would
-// put the whole array in scratch memory).
-template <int N>
-__device__ __forceinline__ double pick(const double (&v)[N], int lane) {
-  double out = 0.0;
-#pragma unroll
-  for (int e = 0; e < N; ++e) out = lane == e ? v[e] : out;
-  return out;
-}
-
-// Orders wave 0's own LDS (or, on the global path, memory) traffic between its
-// lanes: LDS ops of one wave complete in order; global stores need a fence.
-template <bool kLds>
-__device__ __forceinline__ void wave_sync() {
-  if (!kLds) __threadfence_block();
-  __builtin_amdgcn_wave_barrier();
-}
 
 // K3.  Right-looking 6x6-block Cholesky of the profile of S with the forward
 // substitution folded in, then back substitution and the pose update; one
@@ -1320,374 +1221,6 @@ __global__ __launch_bounds__(64 * NW) void ba_solve_kernel(SolveArgs A) {
     for (int k = 0; k < kS3Count; ++k) A.stamps[k] = st_acc[k];
 }
 
-// ---- K3, two-sided variant (BAPlan::solve2_tab, TwoSidedLayout) ---------------------
-__device__ __forceinline__ void ld6g(const double* p, double (&v)[6]) {
-  const double2* q = reinterpret_cast<const double2*>(p);
-  const double2 a0 = q[0], a1 = q[1], a2 = q[2];
-  v[0] = a0.x; v[1] = a0.y; v[2] = a1.x; v[3] = a1.y; v[4] = a2.x; v[5] = a2.y;
-}
-__device__ __forceinline__ void st6g(double* p, const double (&v)[6]) {
-  double2* q = reinterpret_cast<double2*>(p);
-  q[0] = make_double2(v[0], v[1]);
-  q[1] = make_double2(v[2], v[3]);
-  q[2] = make_double2(v[4], v[5]);
-}
-__device__ __forceinline__ double dot6g(const double (&u)[6], const double* w) {
-  const double2* q = reinterpret_cast<const double2*>(w);
-  const double2 a0 = q[0], a1 = q[1], a2 = q[2];
-  return u[0] * a0.x + u[1] * a0.y + u[2] * a1.x + u[3] * a1.y + u[4] * a2.x + u[5] * a2.y;
-}
-
-struct Solve2Args {
-  SolveArgs base;
-  TwoSidedLayout tl;
-  const int* tab;  // BAPlan::solve2_tab
-  long lds_kf, lds_y, lds_panel, lds_pose, lds_tab;
-  int stamp_thread;  // diagnostic build: the thread whose clock the stamps follow
-};
-
-// LDS image: [profile 36*nprof | shadow blocks 36*nshadow | per column 36 (L, 1/diag, y')
-// | y 6F + shadow rhs 6s | 4 private panels | poses | step table]
-SolveLds solve2_lds_layout(int nprof, int F, const TwoSidedLayout& T, int n_poses) {
-  SolveLds L;
-  L.prof = 0;
-  L.kf = 36ull * (nprof + T.nshadow);
-  L.y = L.kf + 36ull * F;
-  L.panel = L.y + 6ull * F + 6ull * T.s + ((6ull * F + 6ull * T.s) & 1);
-  L.pose = L.panel + 4ull * 36 * std::max(1, T.max_panel);
-  L.tab = L.pose + 12ull * n_poses;
-  L.total = L.tab * 8 + 4ull * std::max(1, T.len);
-  return L;
-}
-
-// One workgroup of four waves.  Phase p of the sides: waves 0-1 run top-down step p,
-// waves 2-3 bottom-up step m+p (each wave computes its step's whole panel into its own
-// panel copy, so the trailing update needs no barrier); one barrier per phase.  Then
-// the shadows are merged, the separator is factored by all four waves, and the back
-// substitution runs separator first, then top (wave 0) and bottom (wave 2) together.
-template <bool kStamp>
-__global__ __launch_bounds__(256) void ba_solve2_kernel(Solve2Args A2) {
-  const SolveArgs& A = A2.base;
-  const TwoSidedLayout& T = A2.tl;
-  unsigned long long st_t = 0, st_acc[kS3Count] = {};
-  auto mark = [&](int ph) {
-    if (kStamp && (int)threadIdx.x == A2.stamp_thread) {
-      const unsigned long long n = __builtin_amdgcn_s_memtime();
-      if (st_t) st_acc[ph] += n - st_t;
-      st_t = n;
-    }
-  };
-  mark(0);
-  extern __shared__ __attribute__((aligned(16))) double dyn[];
-  __shared__ int s_fail;
-  const int tid = threadIdx.x, F = A.F;
-  const int wave = tid >> 6, lane = tid & 63;
-  const bool prior_fail = A.status && *A.status;
-  double* Sm = dyn;
-  double* kf = dyn + A2.lds_kf;
-  double* y = dyn + A2.lds_y;
-  double* pose_l = dyn + A2.lds_pose;
-  int* tab = reinterpret_cast<int*>(dyn + A2.lds_tab);
-  const int* t_col = tab + T.col;
-  const int* t_mode = tab + T.mode;
-  const int* t_diag = tab + T.diag;
-  const int* t_sptr = tab + T.step_ptr;
-  const int* t_pblk = tab + T.panel_blk;
-  const int* t_py = tab + T.panel_y;
-  const int* t_iptr = tab + T.item_ptr;
-  const int* t_iblk = tab + T.item_blk;
-  const int* t_iq = tab + T.item_q;
-  const int* t_ipri = tab + T.item_pri;
-  const int* t_merge = tab + T.merge_main;
-  const int* t_cptr = tab + T.colb_ptr;
-  const int* t_colb = tab + T.colb;
-  const int* t_off = tab + T.off;
-  const int* t_first = tab + T.first;
-  const int m = T.m, s = T.s, nbot = T.nbot;
-  if (tid == 0) {
-    s_fail = prior_fail ? 1 : 0;
-    if (A.cost_out) *A.cost_out = A.sys[36l * A.nprof + 6l * F];
-  }
-  if (!prior_fail) {
-    copy_in<double2, 16>(reinterpret_cast<double2*>(Sm), reinterpret_cast<const double2*>(A.sys),
-                         18 * A.nprof, tid, 256);
-    copy_in<double, 4>(y, A.sys + 36l * A.nprof, 6 * F, tid, 256);
-    copy_in<int, 8>(tab, A2.tab, T.len, tid, 256);
-    for (int e = tid; e < 36 * T.nshadow; e += 256) Sm[36l * A.nprof + e] = 0.0;
-    for (int e = tid; e < 6 * s; e += 256) y[6 * F + e] = 0.0;
-  }
-  copy_in<double, 4>(pose_l, A.pose_cur, 12 * A.n_poses, tid, 256);
-  __syncthreads();
-  mark(kS3Setup);
-
-  bool bad = false;
-  // One elimination step t on a group of gnw waves (gw: this wave's index in it); roles
-  // (group-local): wY updates y, wK keeps (L, 1/diag, y') and the failure flag, wC
-  // writes the previous step's panel into the profile.
-  // kPairs: each trailing task covers rows {rp, rp+3} of one block (2-wave groups: one
-  // round of tasks over 128 lanes); otherwise one row per task.
-  // Per-step table entries (k, mode, panel range, item range, look-ahead items) and the
-  // panel wave's lane entries (its panel block and y row).
-  struct StepTab {
-    int k, md, p0, nb, i0, nit, npri, diag, pblk, pyi;
-  };
-  auto tabs = [&](int t, StepTab& s) {
-    s.k = t_col[t];
-    s.md = t_mode[t];
-    s.p0 = t_sptr[t];
-    s.nb = t_sptr[t + 1] - s.p0;
-    s.i0 = t_iptr[t];
-    s.nit = t_iptr[t + 1] - s.i0;
-    s.npri = t_ipri[t];
-    s.diag = t_diag[t];
-    const int qi = s.p0 + (lane < 6 * s.nb ? lane / 6 : 0);
-    s.pblk = s.nb > 0 ? t_pblk[qi] : 0;
-    s.pyi = s.nb > 0 ? t_py[qi] : 0;
-  };
-  // Panel of a step (one wave, one lane per panel row): factor the diagonal block, solve
-  // the panel rows, write them into the profile blocks they replace, update y.
-  auto panel = [&](const StepTab& st) {
-    const bool prow = lane < 6 * st.nb;
-    const int rr = lane % 6;
-    double L[21], r[6], yk[6], sv[6];
-    {
-      // lower triangle of the diagonal block: row i needs its first i + 1 entries
-      const double2* D = reinterpret_cast<const double2*>(Sm + 36l * st.diag);
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int c = 0; c <= i; c += 2) {
-          const double2 v = D[3 * i + c / 2];
-          L[P6(i, c)] = v.x;
-          if (c + 1 <= i) L[P6(i, c + 1)] = v.y;
-        }
-    }
-    ld6g(y + 6 * st.k, yk);
-    if (st.md == 0) {
-      ld6g(Sm + 36l * st.pblk + 6 * rr, sv);  // row rr of block (i, k)
-    } else {
-#pragma unroll
-      for (int c = 0; c < 6; ++c) sv[c] = Sm[36l * st.pblk + 6 * c + rr];  // column rr of block (k, j)
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const bool ok = chol6<false>(L, r);
-    fwd6(L, r, yk);
-    if (lane == 0) bad = bad || !ok || !isfinite(yk[0] + yk[1] + yk[2] + yk[3] + yk[4] + yk[5]);
-    fwd6(L, r, sv);
-    if (prow) {
-      // the panel row of L (bottom side: row of L~ in block (k, j)) replaces the block row
-      st6g(Sm + 36l * st.pblk + 6 * rr, sv);
-      y[st.pyi + rr] -= sv[0] * yk[0] + sv[1] * yk[1] + sv[2] * yk[2] + sv[3] * yk[3] +
-                        sv[4] * yk[4] + sv[5] * yk[5];
-    }
-  };
-  // Trailing tasks [ta, tb) of a step over nl lanes (this lane: li): rows rp (and rp + 3
-  // with kPairs) of the item's block -= (rows of panel block q & 0xffff) x (panel block
-  // q >> 16)^T, the panel blocks already holding L.
-  auto tasks = [&](const StepTab& st, int ta, int tb, int li, int nl, auto pairs_tag) {
-    constexpr bool kPairs = decltype(pairs_tag)::value;
-    constexpr int kPer = kPairs ? 3 : 6;
-    for (int t2 = ta + li; t2 < tb; t2 += nl) {
-      const int it = t2 / kPer, rp = t2 % kPer;
-      const int blk = t_iblk[st.i0 + it], q = t_iq[st.i0 + it];
-      double x0[6], x1[6], a0[6], a1[6], bq[6][6];
-      ld6g(Sm + 36l * blk + 6 * rp, x0);
-      if (kPairs) ld6g(Sm + 36l * blk + 6 * (rp + 3), x1);
-      ld6g(Sm + 36l * (q & 0xffff) + 6 * rp, a0);
-      if (kPairs) ld6g(Sm + 36l * (q & 0xffff) + 6 * (rp + 3), a1);
-      const double* B = Sm + 36l * (q >> 16);
-#pragma unroll
-      for (int c = 0; c < 6; ++c) ld6g(B + 6 * c, bq[c]);
-#pragma unroll
-      for (int c = 0; c < 6; ++c)
-#pragma unroll
-        for (int e = 0; e < 6; ++e) {
-          x0[c] = __builtin_fma(-a0[e], bq[c][e], x0[c]);
-          if (kPairs) x1[c] = __builtin_fma(-a1[e], bq[c][e], x1[c]);
-        }
-      st6g(Sm + 36l * blk + 6 * rp, x0);
-      if (kPairs) st6g(Sm + 36l * blk + 6 * (rp + 3), x1);
-    }
-  };
-
-  // Sides, with look-ahead: in phase p, wave A of a side (gw 0) applies the step's items
-  // on the next step's line and then factors that next step's panel, while wave B applies
-  // the remaining items; one barrier per phase.  Disjoint blocks: A writes the next
-  // line and panel, B the rest of the trailing window; both read the current panel.
-  const int g = wave >> 1, gw = wave & 1;
-  const int P = m > nbot ? m : nbot;
-  const int nside = g == 0 ? m : nbot, tbase = g == 0 ? 0 : m;
-  StepTab cur, nxt;
-  if (!prior_fail) {
-    tabs(tbase, cur);
-    if (gw == 0) panel(cur);
-  }
-  __syncthreads();
-  mark(kS3Factor);
-  for (int p = 0; p < P && !prior_fail; ++p) {
-    if (p < nside) {
-      const bool more = p + 1 < nside;
-      tabs(tbase + (more ? p + 1 : p), nxt);
-      if (gw == 0) {
-#ifdef VO_K3_LOOKAHEAD_PAIRS
-        tasks(cur, 0, 3 * cur.npri, lane, 64, std::true_type{});
-#else
-        // the look-ahead items one row per lane (<= 42 rows: one round, half the chain of
-        // a row pair); the other wave keeps row pairs for the rest of the trailing window
-        tasks(cur, 0, 6 * cur.npri, lane, 64, std::false_type{});
-#endif
-        mark(kS3Barrier);
-        if (more) panel(nxt);
-        mark(kS3Mid);
-      } else {
-        tasks(cur, 3 * cur.npri, 3 * cur.nit, lane, 64, std::true_type{});
-        mark(kS3Barrier);
-      }
-      cur = nxt;
-    }
-    __syncthreads();
-    mark(kS3Data);  // barrier wait
-  }
-  // merge the bottom side's separator contributions (fixed order)
-  if (!prior_fail) {
-    for (int e = tid; e < 36 * T.nshadow; e += 256) {
-      const int mb = t_merge[e / 36];
-      if (mb >= 0) Sm[36l * mb + e % 36] += Sm[36l * (A.nprof + e / 36) + e % 36];
-    }
-    for (int e = tid; e < 6 * s; e += 256) y[6 * m + e] += y[6 * F + e];
-  }
-  __syncthreads();
-  mark(kS3Panel);
-  // separator, same look-ahead: wave 0 the next line and panel, waves 1-3 the rest
-  if (!prior_fail && m + nbot < F) {
-    tabs(m + nbot, cur);
-    if (wave == 0) panel(cur);
-  }
-  __syncthreads();
-  for (int t = m + nbot; t < F && !prior_fail; ++t) {
-    const bool more = t + 1 < F;
-    tabs(more ? t + 1 : t, nxt);
-    if (wave == 0) {
-      tasks(cur, 0, 6 * cur.npri, lane, 64, std::false_type{});
-      if (more) panel(nxt);
-    } else {
-      tasks(cur, 6 * cur.npri, 6 * cur.nit, tid - 64, 192, std::false_type{});
-    }
-    cur = nxt;
-    __syncthreads();
-  }
-  if (bad) s_fail = 1;
-  __syncthreads();
-  // The factored columns for the back substitution, all at once (lane k): L_kk, 1/diag
-  // and y'_k = L_kk^-1 y_k recomputed from the final D_k and y_k, which no later step
-  // writes -- the same operations on the same values as in the elimination, so bitwise
-  // what it used.  (Stored there by one lane per step, the 17 writes queued every
-  // later LDS access of that wave.)
-  if (!prior_fail)
-    for (int k = tid; k < F; k += 256) {
-      double L[21], r[6], yk[6], dr[6];
-      const double* D = Sm + 36l * (t_off[k] + k - t_first[k]);  // block (k, k)
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        ld6g(D + 6 * i, dr);
-#pragma unroll
-        for (int c = 0; c <= i; ++c) L[P6(i, c)] = dr[c];
-      }
-      ld6g(y + 6 * k, yk);
-      chol6(L, r);
-      fwd6(L, r, yk);
-      double* kc = kf + 36l * k;
-#pragma unroll
-      for (int e = 0; e < 20; e += 2) reinterpret_cast<double2*>(kc)[e / 2] = make_double2(L[e], L[e + 1]);
-      reinterpret_cast<double2*>(kc)[10] = make_double2(L[20], 0.0);
-      st6g(kc + 24, r);
-      st6g(kc + 30, yk);
-    }
-  __syncthreads();
-  mark(kS3Trail);
-
-  // One wave's back substitution over k = kb, kb + dir, ... (!= ke): x_k = L_kk^-T y'_k,
-  // then y'_i -= B^T x_k for the rows coupled to k -- up: block (k, j), j in [first[k], k);
-  // down: block (i, k) from the column list.  Every load of a step (L_kk, y'_k, each
-  // coupled row's y' and B column) is issued at once, so a step costs one LDS round
-  // trip; x_k is stored by six lanes, one 8-byte store each.
-  auto bs_run = [&](int kb, int ke, int dir, bool up, bool down) {
-    for (int k = kb; k != ke; k += dir) {
-      const int fk = t_first[k], okk = t_off[k];
-      const int nup = up ? k - fk : 0;
-      const int cb = down ? t_cptr[k - m] : 0, ndn = down ? t_cptr[k - m + 1] - cb : 0;
-      const int nt = 6 * (nup + ndn);
-      double Lk[21], rk[6], x[6];
-      {
-        const double* o = kf + 36l * k;
-#pragma unroll
-        for (int e = 0; e < 20; e += 2) {
-          const double2 v = reinterpret_cast<const double2*>(o)[e / 2];
-          Lk[e] = v.x;
-          Lk[e + 1] = v.y;
-        }
-        Lk[20] = o[20];
-        ld6g(o + 24, rk);
-        ld6g(o + 30, x);
-      }
-      // this lane's coupled (row, column c) pairs: t = lane, lane + 64
-      double yv[2], col[2][6];
-      int yrow[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int tt = lane + 64 * h, tq = min(tt, max(nt - 1, 0)) / 6, cc = tt % 6;
-        int row, blk;
-        if (tq < nup) {
-          row = fk + tq;
-          blk = okk + tq;  // block (k, fk + tq)
-        } else {
-          const int q = cb + tq - nup;
-          row = t_colb[2 * q];
-          blk = t_colb[2 * q + 1];  // block (row, k)
-        }
-        yrow[h] = tt < nt ? row : -1;
-        yv[h] = kf[36l * row + 30 + cc];
-        const double* B = Sm + 36l * blk + cc;
-#pragma unroll
-        for (int rr = 0; rr < 6; ++rr) col[h][rr] = B[6 * rr];
-      }
-      bwd6(Lk, rk, x);
-      if (lane < 6) kf[36l * k + 30 + lane] = pick<6>(x, lane);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        if (yrow[h] >= 0)
-          kf[36l * yrow[h] + 30 + (lane + 64 * h) % 6] =
-              yv[h] - (col[h][0] * x[0] + col[h][1] * x[1] + col[h][2] * x[2] + col[h][3] * x[3] +
-                       col[h][4] * x[4] + col[h][5] * x[5]);
-      wave_sync<true>();
-    }
-  };
-  if (!s_fail && wave == 0) bs_run(m + s - 1, m - 1, -1, true, true);
-  __syncthreads();
-  // top rows descending (wave 0) and bottom rows ascending (wave 2) concurrently
-  if (!s_fail && wave == 0) bs_run(m - 1, -1, -1, true, false);
-  if (!s_fail && wave == 2) bs_run(m + s, F, 1, false, true);
-  __syncthreads();
-  mark(kS3Backsub);
-  const bool failed = s_fail != 0;
-  for (int e = tid; e < 6 * F; e += 256) A.dc[e] = failed ? 0.0 : kf[36l * (e / 6) + 30 + e % 6];
-  for (int c = tid; c < A.n_poses; c += 256) {
-    const double* Tp = pose_l + 12 * c;
-    double* out = A.pose_next + 12 * c;
-    if (failed || c < A.n_fixed) {
-      for (int e = 0; e < 12; ++e) out[e] = Tp[e];
-    } else {
-      const double* d6 = kf + 36l * (c - A.n_fixed) + 30;
-      double d[6];
-      for (int e = 0; e < 6; ++e) d[e] = d6[e];
-      se3_exp_apply(d, Tp, out);
-    }
-  }
-  if (tid == 0 && failed && !prior_fail) *A.status = A.iter_tag;
-  mark(kS3Tail);
-  if (kStamp && tid == A2.stamp_thread && A.stamps)
-    for (int k = 0; k < kS3Count; ++k) A.stamps[k] = st_acc[k];
-}
 
 template <class T>
 void upload(DevBuf& buf, const std::vector<T>& v, hipStream_t st) {
@@ -1782,7 +1315,6 @@ class BAEngine {
     upload(d_camo_ptr_, P.camo_ptr, st);
     upload(d_camo_list_, P.camo_list, st);
     upload(d_segcam_diag_, P.segcam_diag, st);
-    stamps_on_ = getenv("VO_BA_STAMPS") && atoi(getenv("VO_BA_STAMPS")) != 0;
     const int F = P.n_free;
     d_points_.reserve(std::max(1, P.n_points) * 24ull);
     d_pose_[0].reserve(P.n_poses * 96ull);
@@ -1791,8 +1323,6 @@ class BAEngine {
     d_slab_.reserve(std::max(1, P.n_slab_slots()) * 288ull);
     d_slab_b_.reserve(std::max<size_t>(1, P.segcam_f.size()) * 48ull);
     d_slab_cost_.reserve(std::max(1, P.n_segments()) * 8ull);
-    sys_len_ = 36ull * P.n_prof_blocks() + 6ull * F + 1;
-    d_sys_.reserve(sys_len_ * 8);
     d_linv_.reserve(std::max(1, F) * 288ull);
     d_status_.reserve(sizeof(int));
     VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
@@ -1808,34 +1338,51 @@ class BAEngine {
     }
     const size_t lds = solve_layout_.total;
     solve_lds_size_ = lds;
-    {  // two-sided K3 when its LDS image fits (profile + shadows in LDS)
-      const TwoSidedLayout& T2 = P.solve2_layout;
-      solve2_ = false;
-      if (T2.enabled && !getenv("VO_K3_V2")) {
-        solve2_layout_ = solve2_lds_layout(P.n_prof_blocks(), F, T2, P.n_poses);
-        if (solve2_layout_.total <= kSolveLdsMax) {
-          solve2_ = true;
-          upload(d_solve2_tab_, P.solve2_tab, st);
-          VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve2_kernel<false>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)solve2_layout_.total));
-          VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve2_kernel<true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)solve2_layout_.total));
+    {  // banded K3 when the block bandwidth and F fit it; the profile solver otherwise
+      std::vector<int> first(P.prof_first.begin(), P.prof_first.end());
+      band_ = band_split(F, first);
+      band_on_ = F > 0 && band_supported(F, band_.w, P.n_poses);
+      // K2's output layout: the profile [S | b | cost], or the banded K3's columns
+      const int nprof = P.n_prof_blocks();
+      red_dst_.assign(std::max(1, nprof), 0);
+      red_rdst_.assign(std::max(1, F), 0);
+      size_t pad = 0;
+      if (band_on_) {
+        const int w = band_.w, CS = band_col_stride(w), top = band_.m + band_.s;
+        const int base_b = top * CS;
+        for (int i = 0; i < F; ++i) {
+          for (int j = P.prof_first[i]; j <= i; ++j) {
+            const int b = P.prof_off[i] + j - P.prof_first[i];
+            red_dst_[b] = i < top ? j * CS + 36 * (i - j) : (base_b + (F - 1 - i) * CS + 36 * (i - j)) | kRedTranspose;
+          }
+          red_rdst_[i] = i < top ? i * CS + 36 * (w + 1) : base_b + (F - 1 - i) * CS + 36 * (w + 1);
         }
+        sys_len_ = (size_t)(F + band_.s) * CS + 1;
+        cost_off_ = (long)sys_len_ - 1;
+        pad = band_slot_stride(w);  // the ring loader's last LDS-DMA piece reads past the end
+        band_tab_ = band_tables(F, band_);
+        upload(d_band_tab_, band_tab_.tab, st);
+        band_lds_ = band_lds_bytes(F, w, P.n_poses);
+        band_set_attributes(band_lds_);
+        d_fac_.reserve(band_fac_doubles(F, w) * 8);
+      } else {
+        for (int b = 0; b < nprof; ++b) red_dst_[b] = 36 * b;
+        for (int f = 0; f < F; ++f) red_rdst_[f] = 36 * nprof + 6 * f;
+        sys_len_ = 36ull * nprof + 6ull * F + 1;
+        cost_off_ = (long)sys_len_ - 1;
       }
+      d_sys_.reserve((sys_len_ + pad) * 8);
+      // entries K2 never writes (outside the profile, the bottom side's separator) stay 0
+      VO_HIP_CHECK(hipMemsetAsync(d_sys_.ptr, 0, (sys_len_ + pad) * 8, st));
+      upload(d_red_dst_, red_dst_, st);
+      upload(d_red_rdst_, red_rdst_, st);
+      d_zero_.reserve(512);  // zero block (masked prefetches)
+      VO_HIP_CHECK(hipMemsetAsync(d_zero_.ptr, 0, 512, st));
     }
     {
-      const char* w = getenv("VO_K3_WAVES");
-      solve_waves_ = w ? atoi(w) : 4;
-      if (solve_waves_ != 1 && solve_waves_ != 2) solve_waves_ = 4;
       const int l = (int)lds;
-      set_solve_lds<true, false, 1>(l); set_solve_lds<true, true, 1>(l);
-      set_solve_lds<false, false, 1>(l); set_solve_lds<false, true, 1>(l);
-      set_solve_lds<true, false, 2>(l); set_solve_lds<true, true, 2>(l);
-      set_solve_lds<false, false, 2>(l); set_solve_lds<false, true, 2>(l);
-      set_solve_lds<true, false, 4>(l); set_solve_lds<true, true, 4>(l);
-      set_solve_lds<false, false, 4>(l); set_solve_lds<false, true, 4>(l);
+      set_solve_lds<true>(l);
+      set_solve_lds<false>(l);
     }
     VO_HIP_CHECK(hipStreamSynchronize(st));
     have_problem_ = true;
@@ -1922,22 +1469,26 @@ class BAEngine {
     VO_HIP_CHECK(hipStreamSynchronize(st));
     cur_ ^= 1;
     pending_ = true;
-    if (S_out) {
+    if (S_out) {  // K2's output layout (red_dst_) back to the dense symmetric S
       const int n = 6 * F;
       std::fill(S_out, S_out + (size_t)n * n, 0.0);
       for (int i = 0; i < F; ++i)
         for (int j = P.prof_first[i]; j <= i; ++j) {
-          const double* blk = sys.data() + 36ull * (P.prof_off[i] + j - P.prof_first[i]);
+          const int d = red_dst_[P.prof_off[i] + j - P.prof_first[i]];
+          const double* blk = sys.data() + (d & ~kRedTranspose);
+          const bool tr = d & kRedTranspose;
           for (int r = 0; r < 6; ++r)
             for (int c = 0; c < 6; ++c) {
-              S_out[(size_t)(6 * i + r) * n + 6 * j + c] = blk[6 * r + c];
-              S_out[(size_t)(6 * j + c) * n + 6 * i + r] = blk[6 * r + c];
+              const double v = blk[tr ? 6 * c + r : 6 * r + c];
+              S_out[(size_t)(6 * i + r) * n + 6 * j + c] = v;
+              S_out[(size_t)(6 * j + c) * n + 6 * i + r] = v;
             }
         }
     }
-    if (b_out) std::copy(sys.begin() + 36ull * P.n_prof_blocks(), sys.begin() + 36ull * P.n_prof_blocks() + 6 * F, b_out);
+    if (b_out)
+      for (int f = 0; f < F; ++f) std::copy(sys.begin() + red_rdst_[f], sys.begin() + red_rdst_[f] + 6, b_out + 6 * f);
     if (dc_out) std::copy(dc.begin(), dc.end(), dc_out);
-    if (cost_out) *cost_out = sys[sys_len_ - 1];
+    if (cost_out) *cost_out = sys[cost_off_];
     if (status) {
       VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
       VO_HIP_CHECK(hipStreamSynchronize(st));
@@ -1949,9 +1500,8 @@ class BAEngine {
 
   int stats(int64_t* out, int n) const {
     const BAPlan& P = plan_;
-    const int64_t wide = 0;
     const int64_t v[8] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), (int64_t)P.slot_i.size(),
-                          P.n_prof_blocks(), P.n_te, P.algorithmic_bytes_per_iter(), wide};
+                          P.n_prof_blocks(), P.n_te, P.algorithmic_bytes_per_iter(), band_on_ ? 1 : 0};
     const int k = std::min(n, 8);
     for (int i = 0; i < k; ++i) out[i] = v[i];
     return k;
@@ -1965,10 +1515,9 @@ class BAEngine {
 
   // Planner target of 4 segments per CU (K1's LDS footprint admits two resident
   // workgroups per CU; the planner's chunk packing leaves ~2.6 per CU at cfg3,
-  // measured best of 128..2048 -- profiles/r01_segment_sweep.md).  Overridable.
+  // measured best of 128..2048 -- profiles/r01_segment_sweep.md).
   static int segments_target(int num_cus) {
-    const char* e = getenv("VO_BA_SEGMENTS");
-    return e ? std::max(1, atoi(e)) : 4 * std::max(1, num_cus);
+    return VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
   }
 
   LinArgs lin_args() {
@@ -2072,6 +1621,9 @@ class BAEngine {
     R.slab_b = d_slab_b_.as<double>();
     R.slab_cost = d_slab_cost_.as<double>();
     R.sys = d_sys_.as<double>();
+    R.dst = d_red_dst_.as<int>();
+    R.rdst = d_red_rdst_.as<int>();
+    R.cost_off = cost_off_;
     R.status = d_status_.as<int>();
     ctx_->prof.begin(ctx_->stream, kKBaReduce);
     hipLaunchKernelGGL(ba_reduce_kernel, dim3(R.nprof + 1), dim3(kRedThreads), 0, ctx_->stream, R);
@@ -2081,41 +1633,48 @@ class BAEngine {
       ctx_->comm->allreduce(d_sys_.as<double>(), sys_len_, false, ctx_->stream);
   }
 
-  template <bool kL, bool kS>
-  void launch_solve_t(const SolveArgs& A) {
-    if (solve_waves_ == 1)
-      hipLaunchKernelGGL((ba_solve_kernel<kL, kS, 1>), dim3(1), dim3(64), solve_lds_size_, ctx_->stream, A);
-    else if (solve_waves_ == 2)
-      hipLaunchKernelGGL((ba_solve_kernel<kL, kS, 2>), dim3(1), dim3(128), solve_lds_size_, ctx_->stream, A);
-    else
-      hipLaunchKernelGGL((ba_solve_kernel<kL, kS, 4>), dim3(1), dim3(256), solve_lds_size_, ctx_->stream, A);
-  }
   void launch_solve(const SolveArgs& A) {
-    if (solve2_) {
-      Solve2Args A2;
-      A2.base = A;
-      A2.tl = plan_.solve2_layout;
-      A2.tab = d_solve2_tab_.as<int>();
-      A2.lds_kf = (long)solve2_layout_.kf;
-      A2.lds_y = (long)solve2_layout_.y;
-      A2.lds_panel = (long)solve2_layout_.panel;
-      A2.lds_pose = (long)solve2_layout_.pose;
-      A2.lds_tab = (long)solve2_layout_.tab;
-      A2.stamp_thread = 64 * std::min(3, std::max(0, getenv("VO_K3_STAMP_WAVE") ? atoi(getenv("VO_K3_STAMP_WAVE")) : 0));
-      if (stamps_on_)
-        hipLaunchKernelGGL((ba_solve2_kernel<true>), dim3(1), dim3(256), solve2_layout_.total, ctx_->stream, A2);
-      else
-        hipLaunchKernelGGL((ba_solve2_kernel<false>), dim3(1), dim3(256), solve2_layout_.total, ctx_->stream, A2);
+    if (band_on_) {
+      const BAPlan& P = plan_;
+      BandArgs B;
+      B.F = A.F;
+      B.w = band_.w;
+      B.m = band_.m;
+      B.nb = band_.nb;
+      B.s = band_.s;
+      B.nprof = A.nprof;
+      B.n_poses = A.n_poses;
+      B.n_fixed = A.n_fixed;
+      B.iter_tag = A.iter_tag;
+      B.cost_off = cost_off_;
+      B.merge = band_tab_.merge;
+      B.n_merge = band_tab_.n_merge;
+      B.tab = d_band_tab_.as<int>();
+      B.sys = A.sys;
+      B.zero = d_zero_.as<double>();
+      B.fac = d_fac_.as<double>();
+      B.cost_out = A.cost_out;
+      B.dc = A.dc;
+      B.pose_cur = A.pose_cur;
+      B.pose_next = A.pose_next;
+      B.status = A.status;
+      B.stamps = nullptr;
+      if (stamps_on_) {
+        d_stamps3_.reserve(8 * kBandStamps * 8);
+        B.stamps = d_stamps3_.as<unsigned long long>();
+      }
+      (void)P;
+      launch_band_solve(B, band_lds_, ctx_->stream);
       return;
     }
-    if (solve_lds_ && stamps_on_) launch_solve_t<true, true>(A);
-    else if (solve_lds_) launch_solve_t<true, false>(A);
-    else if (stamps_on_) launch_solve_t<false, true>(A);
-    else launch_solve_t<false, false>(A);
+    if (solve_lds_)
+      hipLaunchKernelGGL((ba_solve_kernel<true, kBaStamps, 4>), dim3(1), dim3(256), solve_lds_size_, ctx_->stream, A);
+    else
+      hipLaunchKernelGGL((ba_solve_kernel<false, kBaStamps, 4>), dim3(1), dim3(256), solve_lds_size_, ctx_->stream, A);
   }
-  template <bool kL, bool kS, int NW>
+  template <bool kL>
   static void set_solve_lds(int lds) {
-    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<kL, kS, NW>,
+    VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<kL, kBaStamps, 4>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   }
 
@@ -2174,6 +1733,7 @@ class BAEngine {
     R.nseg = std::max(1, plan_.n_segments());
     R.slab_cost = d_slab_cost_.as<double>();
     R.sys = d_cost_tmp();
+    R.cost_off = 0;
     R.status = d_status_.as<int>();
     hipLaunchKernelGGL(ba_reduce_kernel, dim3(1), dim3(kRedThreads), 0, ctx_->stream, R);
     VO_HIP_CHECK(hipGetLastError());
@@ -2201,10 +1761,13 @@ class BAEngine {
   int cur_ = 0;
   size_t sys_len_ = 0, solve_lds_size_ = 0;
   SolveLds solve_layout_{};
-  int solve_waves_ = 4;
-  bool solve2_ = false;
-  SolveLds solve2_layout_{};
-  DevBuf d_solve2_tab_;
+  BandSplit band_{};
+  bool band_on_ = false;
+  size_t band_lds_ = 0;
+  BandTables band_tab_;
+  DevBuf d_fac_, d_zero_, d_band_tab_, d_red_dst_, d_red_rdst_;
+  std::vector<int32_t> red_dst_, red_rdst_;  // K2 output offsets (host copies for gn_step)
+  long cost_off_ = 0;
   DevBuf d_solve_tab_;
   DevBuf d_obs_uv_, d_obs_cam_, d_obs_te_, d_te_cam_, d_te_pt_, d_te_obs_, d_te_lcam_, d_pt_te_;
   DevBuf d_chunk_obs_, d_chunk_te_, d_chunk_pt_, d_chunk_slot_base_, d_chunk_cam_base_, d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;
@@ -2215,7 +1778,7 @@ class BAEngine {
       d_prof_row_;
   DevBuf d_camb_ptr_, d_camb_src_, d_segcam_f_, d_stamps_, d_stamps3_;
   DevBuf d_camo_ptr_, d_camo_list_, d_segcam_diag_;
-  bool stamps_on_ = false;
+  static constexpr bool stamps_on_ = kBaStamps;
 
  public:
   // Diagnostic: per-phase cycle sums of the last K1 launch (VO_BA_STAMPS=1 builds).
@@ -2236,9 +1799,10 @@ class BAEngine {
       for (int g = 0; g < nseg; ++g) acc += h[(size_t)g * kPhCount + i];
       out[i] = acc;
     }
-    if (n >= kPhCount + kS3Count && d_stamps3_.ptr) {
-      VO_HIP_CHECK(hipMemcpy(out + kPhCount, d_stamps3_.ptr, kS3Count * 8, hipMemcpyDeviceToHost));
-      k += kS3Count;
+    const int n3 = band_on_ ? 8 * kBandStamps : (int)kS3Count;  // K3: banded or profile solver
+    if (n >= kPhCount + n3 && d_stamps3_.ptr) {
+      VO_HIP_CHECK(hipMemcpy(out + kPhCount, d_stamps3_.ptr, n3 * 8, hipMemcpyDeviceToHost));
+      k += n3;
     }
     return k;
   }

@@ -1,0 +1,66 @@
+// K3 for banded reduced camera systems (ba_band.hip), launched by the BA engine (ba.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <vector>
+
+namespace vo {
+
+// Widest block bandwidth (max_i i - first[i]) the banded solver takes: one chain wave
+// holds the panel of a block column, one lane per scalar row, (w + 1) * 6 <= 64.
+constexpr int kBandMaxW = 9;
+constexpr int kBandMaxF = 512;
+constexpr int kBandStamps = 32;  // diagnostic build: phase slots per wave
+
+// Split of the F free block rows: top rows [0, m) eliminated top-down, bottom rows
+// [F - nb, F) bottom-up, concurrently; the separator [m, m + s) (s = w) last, top-down.
+// One-sided (nb = s = 0, m = F) when F is too small for two sides.
+struct BandSplit {
+  int w = 0, m = 0, nb = 0, s = 0;
+};
+BandSplit band_split(int F, const std::vector<int>& first);
+
+// Merge pairs of one window structure (host-built, uploaded once): (destination, source)
+// LDS offsets (doubles) of the separator's blocks and rhs, top ring += bottom ring.
+struct BandTables {
+  std::vector<int> tab;
+  int merge = 0, n_merge = 0;
+};
+BandTables band_tables(int F, const BandSplit& b);
+
+// K2 writes the reduced camera system in the banded layout (ba.hip, red_dst_): per side,
+// column v = band_col_stride(w) doubles -- block (v + q, v) of the side's coordinates
+// row-major at 36 q (the bottom side's blocks transposed), the rhs of row v at 36 (w + 1),
+// 6 zero doubles; top columns [0, m + s), then bottom columns [0, nb + s), then the cost.
+struct BandArgs {
+  int F, w, m, nb, s;
+  int nprof, n_poses, n_fixed, iter_tag;
+  int merge, n_merge;     // merge pairs in tab (BandTables)
+  long cost_off;          // the cost in sys
+  const int* tab;
+  const double* sys;      // K2's banded layout (above), padded by one ring slot
+  const double* zero;     // 64 zero doubles: the source of masked prefetches
+  double* fac;            // factor records: F columns x band_col_stride(w) doubles
+  double* cost_out;       // if set: receives the cost of this linearisation (sys tail)
+  double* dc;             // 6F out
+  const double* pose_cur;
+  double* pose_next;
+  int* status;
+  unsigned long long* stamps;  // diagnostic build: 4 waves x kBandStamps phase cycles
+};
+
+// Doubles per ring slot / factor record: (w + 1) blocks of 36, the rhs row (6) and the
+// reciprocal diagonal (6).
+inline int band_col_stride(int w) { return 36 * (w + 1) + 12; }
+// Doubles per LDS ring slot: the column padded to whole 1 KiB LDS-DMA wave pieces.
+inline int band_slot_stride(int w) { return (band_col_stride(w) + 127) / 128 * 128; }
+size_t band_lds_bytes(int F, int w, int n_poses);
+size_t band_fac_doubles(int F, int w);
+// true if the window fits the kernel (lane budget, LDS budget)
+bool band_supported(int F, int w, int n_poses);
+void band_set_attributes(size_t lds);
+void launch_band_solve(const BandArgs& A, size_t lds, hipStream_t st);
+
+}  // namespace vo

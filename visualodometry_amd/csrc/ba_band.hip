@@ -1,0 +1,596 @@
+// K3 for banded reduced camera systems: S dc = b by a two-sided block Cholesky, then the
+// left se(3) pose update T <- exp(dc^) T.  Build-defined solve (the reference has no BA,
+// SURVEY.md §8 a9-a10); same arithmetic contract as oracle/ba_ref.py gn_step (dense
+// Cholesky of S, exp map of oracle/ba_ref.py se3_exp), checked to 1e-5 over whole runs.
+//
+// The window's reduced camera matrix is block banded: a landmark track spans at most
+// w + 1 consecutive keyframes, so block (i, j) is zero for i - j > w (w = 7 for the
+// BASELINE windows).  Rows are split into top [0, m), separator [m, m + w) and bottom
+// [m + w, F); the top is eliminated top-down and the bottom bottom-up (the same
+// algorithm on the block-reversed matrix) at the same time, then the separator, which
+// receives both sides' Schur updates, continues the top side.  The chain of dependent
+// block steps is max(m, nb) + w instead of F.
+//
+// One workgroup of eight waves (two per SIMD).  Per side:
+//   chain wave   holds the block column being factored in registers, one lane per
+//                scalar row (lane 6 g + r: row r of the block row = g mod (w + 1)).  Step
+//                k: the diagonal block's rows go through LDS to every lane, each lane
+//                factors it (chol6) and solves its own panel row, the panel goes to the
+//                LDS ring; after the workgroup barrier the lane loads its row of column
+//                k + 1 and applies step k's update to it.  Nothing else is on the chain.
+//   helper wave  after the barrier: the forward substitution of step k (y'_k = L_kk^-1
+//                y_k, y_i -= L_ik y'_k), the ring loader (column k + w + 2 from registers
+//                into the slot of column k - 1, column k + w + 3 issued), the factor
+//                record of column k to global memory and the rest of step k's trailing
+//                update (blocks (i, j), k + 2 <= j <= i <= k + w) in the ring.
+// Back substitution: each chain wave walks its rows upwards, x_k = L_kk^-T y'_k in
+// every lane, then lane (q, c) subtracts (L_{k,k-q}^T x_k)_c from its row k - q; the
+// next row goes through LDS.  Factor records come from global memory (L2) two steps
+// ahead.  The bottom side starts once the separator's x is known.
+//
+// LDS: two rings of w + 3 block columns (36 (w+1) + 12 doubles each: blocks, rhs row,
+// 1/diag), x (6F), the poses, the column source tables -- so the cfg4 window (F = 98,
+// a 225 KB profile) runs like cfg3.
+#include "ba_band.h"
+
+#include <algorithm>
+#include <climits>
+
+#include "ba_math.h"
+#include "vo_common.h"
+
+namespace vo {
+
+BandSplit band_split(int F, const std::vector<int>& first) {
+  BandSplit b;
+  int w = 0;
+  for (int i = 0; i < F; ++i) w = std::max(w, i - first[i]);
+  b.w = w;
+  if (F >= 2 * w + 2) {
+    b.s = w;
+    b.nb = (F - w) / 2;
+    b.m = F - w - b.nb;
+  } else {
+    b.m = F;
+  }
+  return b;
+}
+
+BandTables band_tables(int F, const BandSplit& b) {
+  const int w = b.w, R = w + 1, RC = w + 3, CS = band_slot_stride(w), m = b.m, sp = b.s;
+  BandTables T;
+  T.merge = 0;
+  for (int jj = 0; jj < sp; ++jj)
+    for (int qq = 0; qq < sp - jj; ++qq) {
+      const int j = m + jj, i = j + qq;
+      for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 6; ++c) {
+          T.tab.push_back((j % RC) * CS + 36 * qq + 6 * r + c);
+          T.tab.push_back(RC * CS + ((F - 1 - i) % RC) * CS + 36 * qq + 6 * c + r);
+        }
+    }
+  for (int d = 0; d < sp; ++d) {
+    const int i = m + d;
+    for (int r = 0; r < 6; ++r) {
+      T.tab.push_back((i % RC) * CS + 36 * R + r);
+      T.tab.push_back(RC * CS + ((F - 1 - i) % RC) * CS + 36 * R + r);
+    }
+  }
+  T.n_merge = (int)T.tab.size() / 2;
+  if (T.tab.empty()) T.tab.push_back(0);
+  return T;
+}
+
+size_t band_lds_bytes(int F, int w, int n_poses) {
+  const size_t CS = band_slot_stride(w), RC = w + 3;
+  return 8 * (2 * RC * CS + 6 * (size_t)F + 12 * (size_t)n_poses + 16);
+}
+
+size_t band_fac_doubles(int F, int w) { return (size_t)std::max(F, 1) * band_col_stride(w); }
+
+bool band_supported(int F, int w, int n_poses) {
+  return w >= 0 && w <= kBandMaxW && F <= kBandMaxF && band_lds_bytes(F, w, n_poses) <= 160 * 1024 - 64;
+}
+
+namespace {
+
+// chol6 (ba_math.h) without the per-pivot positivity test on the dependent chain: a
+// non-positive pivot gives a NaN / inf reciprocal (v_rsq_f64), which the caller detects
+// from r afterwards (the same "not SPD" outcome).  The diagonal of L is not stored.
+__device__ __forceinline__ void chol6_nochk(double (&a)[21], double (&r)[6]) {
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const double d = a[P6(j, j)];
+    double q = __builtin_amdgcn_rsq(d);
+    if (kCholNewton) q = q * (1.5 - 0.5 * d * q * q);
+    r[j] = q;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) a[P6(i, j)] *= q;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i)
+#pragma unroll
+      for (int c = j + 1; c <= i; ++c) a[P6(i, c)] -= a[P6(i, j)] * a[P6(c, j)];
+  }
+}
+
+constexpr int kBandWaves = 8;
+constexpr int kBandThreads = 64 * kBandWaves;
+constexpr int kLdRegs = 6;      // ring loader: elements per lane of one column
+constexpr int kTaskRounds = 2;  // trailing (block, row pair) tasks per lane
+constexpr int kProLoads = 8;    // prologue: 16-byte pieces per thread (columns 0 .. w + 1 of both sides)
+static_assert(36 * (kBandMaxW + 1) + 12 <= 64 * kLdRegs, "one column per loader wave");
+static_assert(3 * (kBandMaxW - 1) * kBandMaxW / 2 <= 64 * kTaskRounds, "trailing tasks per helper wave");
+static_assert(6 * (kBandMaxW + 1) <= 64, "one lane per panel row");
+static_assert(36 * (kBandMaxW + 1) + 12 <= 3 * 128, "at most three 1 KiB LDS-DMA pieces per column");
+static_assert((kBandMaxW + 2) * (36 * (kBandMaxW + 1) + 12) <= kProLoads * kBandThreads, "prologue");
+// Wave roles (wave = 2 * role + side; wave w runs on SIMD w mod 4, so each side's chain
+// shares its SIMD only with that side's loader, which mostly waits on memory).
+enum { kChain = 0, kTrail = 1, kLoad = 2, kFwd = 3 };
+
+// LDS writes of every wave complete, then the workgroup barrier.  Global loads and
+// stores stay in flight (__syncthreads would drain them: the ring loader's prefetch).
+__device__ __forceinline__ void band_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+#ifndef VO_BA_STAMPS
+#define VO_BA_STAMPS 0
+#endif
+// Diagnostic build only (EXTRA=-DVO_BA_STAMPS=1): lane 0 of each wave accumulates
+// s_memtime deltas per phase; the product build executes none.
+#if VO_BA_STAMPS
+#define BST(i)                                                    \
+  do {                                                            \
+    if (lane == 0) {                                              \
+      const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
+      st_acc[i] += n_ - st_t;                                     \
+      st_t = n_;                                                  \
+    }                                                             \
+  } while (0)
+// value x computed (and every LDS access retired) before the next stamp
+#define BSETTLE(x)                                                                        \
+  do {                                                                                    \
+    int d_;                                                                               \
+    asm volatile("s_waitcnt lgkmcnt(0)\n\tv_mov_b32 %0, %1" : "=v"(d_) : "v"(__double2loint(x))); \
+  } while (0)
+#else
+#define BST(i) \
+  do {         \
+  } while (0)
+#define BSETTLE(x) \
+  do {             \
+  } while (0)
+#endif
+
+// Loads below never feed a select or branch before their first real use: a value that
+// must be zero is loaded from the zero block (A.zero) instead, so the waitcnt pass can
+// leave every prefetch in flight.
+__global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  __shared__ int s_fail;
+#if VO_BA_STAMPS
+  unsigned long long st_acc[kBandStamps] = {}, st_t = __builtin_amdgcn_s_memtime();
+#endif
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // CS: doubles per column (K2 layout, factor record), CSP per ring slot (1 KiB pieces)
+  const int F = A.F, w = A.w, R = w + 1, CS = 36 * R + 12, CSP = (CS + 127) / 128 * 128, RC = w + 3;
+  const int m = A.m, nb = A.nb, sp = A.s;
+  const bool prior_fail = A.status && *A.status;
+  double* ringT = dyn;
+  double* ringB = ringT + RC * CSP;
+  double* xs = ringB + RC * CSP;
+  double* pose_l = xs + 6 * F;
+  double* bb = pose_l + 12 * A.n_poses;  // 2 x 8
+  const int ncolT = m + sp, ncolB = nb + sp;
+
+  const int side = wave & 1, role = wave >> 1;
+  const bool sbot = side == 1;
+  // this wave's side: ring (column v in slot v mod (w + 3)), back-substitution row
+  // broadcast, factor records (column v at v * CS, global), column sources, columns
+  // factored before the merge, columns loaded into the ring
+  double* const sring = sbot ? ringB : ringT;
+  double* const sbbuf = bb + 8 * side;
+  double* const sfac = sbot ? A.fac + (long)ncolT * CS : A.fac;
+  const double* const ssys = A.sys + (sbot ? (long)ncolT * CS : 0);  // this side's columns (K2)
+  const int sna = sbot ? nb : m, snload = sbot ? ncolB : ncolT;
+
+  if (tid == 0) {
+    s_fail = prior_fail ? 1 : 0;
+    if (A.cost_out) *A.cost_out = A.sys[A.cost_off];
+  }
+
+  // Ring prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every
+  // 16-byte load in flight, then the stores.
+  if (!prior_fail) {
+    const int nT = min(w + 2, ncolT) * CS / 2, nB = min(w + 2, ncolB) * CS / 2;  // double2 pieces
+    const double2* gT = reinterpret_cast<const double2*>(A.sys);
+    const double2* gB = reinterpret_cast<const double2*>(A.sys + (long)ncolT * CS);
+    double2 v[kProLoads];
+#pragma unroll
+    for (int u = 0; u < kProLoads; ++u) {
+      const int e = tid + u * kBandThreads;
+      v[u] = e < nT ? gT[e] : e < nT + nB ? gB[e - nT] : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < kProLoads; ++u) {
+      const int e = tid + u * kBandThreads;
+      const bool top = e < nT;
+      const int x = 2 * (top ? e : e - nT), col = x / CS;
+      if (e < nT + nB)
+        *reinterpret_cast<double2*>(dyn + (top ? 0 : RC * CSP) + col * CSP + x - col * CS) = v[u];
+    }
+  }
+
+  // ---- loader wave: column v by LDS-DMA, nDma 1 KiB wave pieces (16 bytes per lane)
+  const int nDma = CSP / 128;
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) const void gbl_void;
+  auto dma_col = [&](int v, double* slot) __attribute__((always_inline)) {
+    const double* src = ssys + (long)v * CS + 2 * lane;
+    for (int t = 0; t < nDma; ++t)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + 128 * t), (lds_void*)(slot + 128 * t), 16, 0, 0);
+  };
+  // every DMA but the last column's nDma pieces complete
+  auto dma_wait_prev = [&]() __attribute__((always_inline)) {
+    if (nDma == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if (nDma == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  };
+  // ---- trailing wave: task lane + 64 h = block (k + qi, k + qj), rows r and r + 3
+  // (blocks by qj, then qi): target column offset qj, offsets of the target row r, of
+  // L_{k+qi,k} row r, of L_{k+qj,k}
+  int tk_qj[kTaskRounds], tk_o[kTaskRounds], tk_a[kTaskRounds], tk_b[kTaskRounds];
+  {
+    const int nt = 3 * (w - 1) * w / 2;
+#pragma unroll
+    for (int h = 0; h < kTaskRounds; ++h) {
+      const int t = lane + 64 * h;
+      int qj = 0, qi = 0, r = 0;
+      if (t < nt) {
+        int b = t / 3;
+        r = t - 3 * b;
+        qj = 2;
+        while (b >= w - qj + 1) {
+          b -= w - qj + 1;
+          ++qj;
+        }
+        qi = qj + b;
+      }
+      tk_qj[h] = t < nt ? qj : -1;
+      tk_o[h] = 36 * (qi - qj) + 6 * r;
+      tk_a[h] = 36 * qi + 6 * r;
+      tk_b[h] = 36 * qj;
+    }
+  }
+  band_barrier();
+  BST(0);
+
+  // ---- chain wave: lane 6 g + sr holds row sr of block (k + q, k), q = (g - k) mod R
+  const bool act = role == kChain && lane < 6 * R;
+  const int g = lane / 6, sr = lane % 6;
+  int q = act ? g : 0;
+  double P[6] = {0, 0, 0, 0, 0, 0};
+  double L1[6][6];  // L_{k+1,k}, read at the end of step k's factor phase
+  bool bad = false;
+  if (act && !prior_fail && sna > 0) ld6g(sring + 36 * g + 6 * sr, P);  // column 0 (slot 0), block g
+
+  // Step k, before the barrier (column k in slot sk): factor the diagonal block, solve
+  // this lane's panel row, write the panel and 1/diag into the ring.
+  auto chain_pre = [&](int sk) __attribute__((always_inline)) {
+    double* col = sring + sk * CSP;
+    // the diagonal block's rows (group q == 0) to every lane through LDS
+    if (act && q == 0) st6g(col + 6 * sr, P);
+    wave_sync<true>();
+    double L[21], r[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int c = 0; c <= i; c += 2) {
+        const double2 v = reinterpret_cast<const double2*>(col + 6 * i)[c / 2];
+        L[P6(i, c)] = v.x;
+        if (c + 1 <= i) L[P6(i, c + 1)] = v.y;
+      }
+    BSETTLE(L[20]);
+    BST(17);
+    chol6_nochk(L, r);
+    bad = bad || !(isfinite(r[0] + r[1] + r[2] + r[3] + r[4] + r[5]));
+    BSETTLE(r[5]);
+    BST(18);
+    fwd6(L, r, P);  // x L_kk^T = row; on the diagonal group: row sr of L_kk
+    BSETTLE(P[5]);
+    BST(19);
+    if (act) st6g(col + 36 * q + 6 * sr, P);
+    if (act && q == 0) col[36 * R + 6 + sr] = pick<6>(r, sr);
+    wave_sync<true>();
+    // L_{k+1,k} for the update after the barrier: issued now, its latency under the wait
+    if (w >= 1)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) ld6g(col + 36 + 6 * c, L1[c]);
+  };
+  // Step k, after the barrier: this lane's row of column k + 1 (every earlier step's
+  // update applied by the trailing wave) minus L_{i,k} L_{k+1,k}^T.
+  auto chain_post = [&](int sk1) __attribute__((always_inline)) {
+    const int q1 = q == 0 ? w : q - 1;
+    double N[6];
+    ld6g(sring + sk1 * CSP + (act ? 36 * q1 + 6 * sr : 0), N);
+    BSETTLE(N[5]);
+    BST(22);
+    if (w >= 1 && q != 0)
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+        N[c] -= P[0] * L1[c][0] + P[1] * L1[c][1] + P[2] * L1[c][2] + P[3] * L1[c][3] + P[4] * L1[c][4] +
+                P[5] * L1[c][5];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) P[c] = act ? N[c] : 0.0;
+    q = q1;
+    BSETTLE(P[5]);
+    BST(23);
+  };
+  // Forward-substitution wave, step k: y'_k = L_kk^-1 y_k into the record, y_i -= L_ik
+  // y'_k for the rows below (lane 6 qf + rf, qf = 1..w), then the factor record of column
+  // k (blocks, y'_k, 1/diag) to global memory.
+  auto fwd_step = [&](int k, int sk) __attribute__((always_inline)) {
+    double* col = sring + sk * CSP;
+    double L[21], r[6], y[6], row[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int c = 0; c <= i; c += 2) {
+        const double2 v = reinterpret_cast<const double2*>(col + 6 * i)[c / 2];
+        L[P6(i, c)] = v.x;
+        if (c + 1 <= i) L[P6(i, c + 1)] = v.y;
+      }
+    ld6g(col + 36 * R + 6, r);
+    ld6g(col + 36 * R, y);
+    const int qf = lane / 6, rf = lane % 6;
+    const bool on = qf >= 1 && qf < R;
+    ld6g(col + (on ? 36 * qf + 6 * rf : 0), row);
+    fwd6(L, r, y);
+    bad = bad || !isfinite(y[0] + y[1] + y[2] + y[3] + y[4] + y[5]);
+    if (on) {
+      const int st = sk + qf < RC ? sk + qf : sk + qf - RC;
+      sring[st * CSP + 36 * R + rf] -=
+          row[0] * y[0] + row[1] * y[1] + row[2] * y[2] + row[3] * y[3] + row[4] * y[4] + row[5] * y[5];
+    }
+    if (lane < 6) col[36 * R + lane] = pick<6>(y, lane);
+    const double2* s2 = reinterpret_cast<const double2*>(col);
+    double2* d2 = reinterpret_cast<double2*>(sfac + (long)k * CS);
+    double2 v2[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) v2[t] = s2[min(lane + 64 * t, CS / 2 - 1)];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      if (lane + 64 * t < CS / 2) d2[lane + 64 * t] = v2[t];
+  };
+  // Trailing wave, step k: blocks (i, j), k + 2 <= j <= i <= k + w, minus L_ik L_jk^T.
+  auto trail_step = [&](int sk) __attribute__((always_inline)) {
+    const double* col = sring + sk * CSP;
+#pragma unroll
+    for (int h = 0; h < kTaskRounds; ++h) {
+      if (tk_qj[h] < 0) continue;
+      const int st = sk + tk_qj[h] < RC ? sk + tk_qj[h] : sk + tk_qj[h] - RC;
+      double* out = sring + st * CSP + tk_o[h];
+      double o0[6], o1[6], a0[6], a1[6], B[6][6];
+      ld6g(out, o0);
+      ld6g(out + 18, o1);
+      ld6g(col + tk_a[h], a0);
+      ld6g(col + tk_a[h] + 18, a1);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) ld6g(col + tk_b[h] + 6 * c, B[c]);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        o0[c] -= a0[0] * B[c][0] + a0[1] * B[c][1] + a0[2] * B[c][2] + a0[3] * B[c][3] + a0[4] * B[c][4] +
+                 a0[5] * B[c][5];
+        o1[c] -= a1[0] * B[c][0] + a1[1] * B[c][1] + a1[2] * B[c][2] + a1[3] * B[c][3] + a1[4] * B[c][4] +
+                 a1[5] * B[c][5];
+      }
+      st6g(out, o0);
+      st6g(out + 18, o1);
+    }
+  };
+  // Loader wave, step k (slot of column k - 1: skm): column k + w + 2 into the freed
+  // slot (first read at step k + 2), then the previous column's pieces retired.
+  auto load_step = [&](int k, int skm) __attribute__((always_inline)) {
+    if (k + w + 2 < snload) {
+      dma_col(k + w + 2, sring + skm * CSP);
+      BST(20);
+      dma_wait_prev();
+      BST(21);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+  auto side_step = [&](int p, int sk, int skm) __attribute__((always_inline)) {
+    if (role == kTrail) trail_step(sk);
+    else if (role == kFwd) fwd_step(p, sk);
+    else if (role == kLoad) load_step(p, skm);
+  };
+
+  if (!prior_fail) {
+    const int PA = max(m, nb);
+    int sk = 0, skm = RC - 1;
+    for (int p = 0; p < PA; ++p) {
+      const bool on = p < sna;
+      const int sk1 = sk + 1 == RC ? 0 : sk + 1;
+      if (role == kChain && on) chain_pre(sk);
+      BST(1);
+      band_barrier();
+      BST(2);
+      if (on) {
+        if (role == kChain) {
+          if (p + 1 < snload) chain_post(sk1);
+        } else {
+          side_step(p, sk, skm);
+        }
+      }
+      BST(3);
+      skm = sk;
+      sk = sk1;
+    }
+    if (sp > 0) {
+      // both sides' state of the separator into the rings, the bottom's contributions
+      // merged into the top's (fixed order), then the top continues through the separator
+      if (act) st6g(sring + (sna % RC) * CSP + 36 * q + 6 * sr, P);
+      __syncthreads();
+      for (int e = tid; e < A.n_merge; e += kBandThreads) {
+        const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
+        dyn[d.x] += dyn[d.y];
+      }
+      __syncthreads();
+      if (act && side == 0) ld6g(ringT + (m % RC) * CSP + 36 * q + 6 * sr, P);
+      BST(4);
+      int sk = m % RC, skm = sk == 0 ? RC - 1 : sk - 1;
+      for (int p = m; p < m + sp; ++p) {
+        const int sk1 = sk + 1 == RC ? 0 : sk + 1;
+        if (role == kChain && side == 0) chain_pre(sk);
+        BST(5);
+        band_barrier();
+        BST(6);
+        if (side == 0) {
+          if (role == kChain) {
+            if (p + 1 < ncolT) chain_post(sk1);
+          } else {
+            side_step(p, sk, skm);
+          }
+        }
+        BST(7);
+        skm = sk;
+        sk = sk1;
+      }
+    }
+  }
+  if (lane == 0 && bad) s_fail = 1;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // factor records written
+  BST(8);
+  __syncthreads();
+  BST(9);
+  const bool failed = s_fail != 0;
+
+  // ---- back substitution L^T x = y' (chain waves); loader waves stage the poses
+  if (role == kLoad)
+    for (int e = tid - 64 * kLoad * 2; e < 12 * A.n_poses; e += 128) pose_l[e] = A.pose_cur[e];
+  double Yb = 0.0;
+  struct BsOps {
+    double L[21], r[6], Lc[6], yin;
+  };
+  int qb = 0;  // this lane's window row at the current step k is k - qb
+  auto bs_init = [&](int khi, int kp) __attribute__((always_inline)) {
+    qb = act ? ((khi - g) % R + R) % R : 0;
+    if (act) {
+      const int i = khi - qb;
+      const bool on = i >= 0 && i < kp;
+      Yb = *(on ? sfac + (long)i * CS + 36 * R + sr : A.zero);
+      if (qb == 0) sbbuf[sr] = Yb;
+    }
+    wave_sync<true>();
+  };
+  // operands of step k for a lane at window position qk (rows >= kp are pseudo steps:
+  // x given by the other side): L_kk, 1/diag (uniform, clamped record); column sr of
+  // L_{k,k-qk}; the y' of the row entering the window (k - w - 1) for the lane leaving it.
+  auto bs_fetch = [&](int k, int qk, int kp, BsOps& o) __attribute__((always_inline)) {
+    const int kk = max(min(k, kp - 1), 0);
+    const double* rec = sfac + (long)kk * CS;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int c = 0; c <= i; c += 2) {
+        const double2 v = reinterpret_cast<const double2*>(rec + 6 * i)[c / 2];
+        o.L[P6(i, c)] = v.x;
+        if (c + 1 <= i) o.L[P6(i, c + 1)] = v.y;
+      }
+    ld6g(rec + 36 * R + 6, o.r);
+    const int i = k - qk;
+    const bool on = act && qk >= 1 && i >= 0 && i < kp;
+    const double* rc = on ? sfac + (long)i * CS + 36 * qk + sr : A.zero;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) o.Lc[c] = rc[6 * c];
+    const int ie = k - R;
+    const bool on2 = act && qk == 0 && ie >= 0 && ie < kp;
+    o.yin = *(on2 ? sfac + (long)ie * CS + 36 * R + sr : A.zero);
+  };
+  auto bs_step = [&](int k, int kp, const BsOps& o) __attribute__((always_inline)) {
+    double x[6];
+    const int G = sbot ? F - 1 - k : k;
+    if (k >= kp) {
+      ld6g(xs + 6 * G, x);
+    } else {
+      ld6g(sbbuf, x);
+      bwd6(o.L, o.r, x);
+      if (lane < 6) xs[6 * G + lane] = pick<6>(x, lane);
+    }
+    if (act && qb >= 1)
+      Yb -= o.Lc[0] * x[0] + o.Lc[1] * x[1] + o.Lc[2] * x[2] + o.Lc[3] * x[3] + o.Lc[4] * x[4] + o.Lc[5] * x[5];
+    if (act && qb == 1) sbbuf[sr] = Yb;
+    if (act && qb == 0) Yb = o.yin;
+    qb = qb == 0 ? w : qb - 1;
+    wave_sync<true>();
+  };
+  auto dec = [&](int x) __attribute__((always_inline)) { return x == 0 ? w : x - 1; };
+  auto bs_run = [&](int khi, int klo, int kp) __attribute__((always_inline)) {
+    BsOps o0, o1;
+    int qa = dec(dec(qb)), qc = dec(qa);  // window positions of steps khi - 2, khi - 3
+    bs_fetch(khi, qb, kp, o0);
+    bs_fetch(khi - 1, dec(qb), kp, o1);
+    int k = khi;
+    for (; k - 1 >= klo; k -= 2) {
+      bs_step(k, kp, o0);
+      bs_fetch(k - 2, qa, kp, o0);
+      BST(26);
+      bs_step(k - 1, kp, o1);
+      bs_fetch(k - 3, qc, kp, o1);
+      BST(26);
+      qa = dec(dec(qa));
+      qc = dec(dec(qc));
+    }
+    if (k >= klo) bs_step(k, kp, o0);
+  };
+  if (!failed) {
+    if (role == kChain && side == 0 && sp > 0) {
+      bs_init(m + sp - 1, INT_MAX);
+      bs_run(m + sp - 1, m, INT_MAX);
+    }
+    BST(10);
+    __syncthreads();  // separator x in LDS
+    BST(11);
+    if (role == kChain && side == 0 && m > 0) {
+      if (sp == 0) bs_init(m - 1, INT_MAX);
+      bs_run(m - 1, 0, INT_MAX);
+    }
+    if (role == kChain && side == 1 && nb > 0) {
+      bs_init(nb + sp - 1, nb);
+      bs_run(nb + sp - 1, 0, nb);
+    }
+  }
+  BST(12);
+  __syncthreads();
+  BST(13);
+
+  for (int e = tid; e < 6 * F; e += kBandThreads) A.dc[e] = failed ? 0.0 : xs[e];
+  for (int c = tid; c < A.n_poses; c += kBandThreads) {
+    const double* T = pose_l + 12 * c;
+    double* out = A.pose_next + 12l * c;
+    if (failed || c < A.n_fixed) {
+      for (int e = 0; e < 12; ++e) out[e] = T[e];
+    } else {
+      double d[6];
+      for (int e = 0; e < 6; ++e) d[e] = xs[6 * (c - A.n_fixed) + e];
+      se3_exp_apply(d, T, out);
+    }
+  }
+  if (tid == 0 && failed && !prior_fail) *A.status = A.iter_tag;
+  BST(14);
+#if VO_BA_STAMPS
+  if (lane == 0 && A.stamps)
+    for (int i = 0; i < kBandStamps; ++i) A.stamps[kBandStamps * wave + i] = st_acc[i];
+#endif
+}
+
+}  // namespace
+
+void band_set_attributes(size_t lds) {
+  VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_band_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+}
+
+void launch_band_solve(const BandArgs& A, size_t lds, hipStream_t st) {
+  hipLaunchKernelGGL(ba_band_kernel, dim3(1), dim3(kBandThreads), lds, st, A);
+}
+
+}  // namespace vo

@@ -425,148 +425,6 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   return "";
 }
 
-// Two-sided K3 tables (see TwoSidedLayout); leaves solve2_layout.enabled = 0 when the
-// profile is not monotone or too small to profit.
-static void build_two_sided(BAPlan& P) {
-  const int F = P.n_free;
-  const std::vector<int32_t>& first = P.prof_first;
-  TwoSidedLayout& L = P.solve2_layout;
-  L = TwoSidedLayout();
-  P.solve2_tab.assign(1, 0);
-  int w = 0;
-  for (int i = 0; i < F; ++i) {
-    if (i > 0 && first[i] < first[i - 1]) return;  // not monotone
-    w = std::max(w, i - first[i]);
-  }
-  const int s = std::max(1, w);
-  const int m = (F - s) / 2, nbot = F - m - s;
-  if (m < 4 || nbot < 4) return;
-  auto blk = [&](int i, int j) { return P.prof_off[i] + (j - first[i]); };
-  auto in_sep = [&](int i) { return i >= m && i < m + s; };
-  const int nprof = P.n_prof_blocks();
-  auto shadow = [&](int a, int b) { return nprof + (a - m) * (a - m + 1) / 2 + (b - m); };
-  std::vector<int32_t> col, mode, diag, sptr{0}, pblk, py, iptr{0}, iblk, iq, ipri;
-  int maxnb = 0;
-  // item_q: the two panel blocks (profile indices) whose rows form the update of the
-  // item's block: (rows of block lo16) x (block hi16)^T
-  // Items of one step, those of the look-ahead line first (ipri of them): the blocks of
-  // the next step's column (top / separator: b == lk) or row (bottom: a == lk), which the
-  // panel wave updates before it factors that next step.
-  auto add_items = [&](const std::vector<int>& rows, const std::vector<int32_t>& pb, bool bottom,
-                       int lk) {
-    const int nb = (int)rows.size();
-    int npri = 0;
-    for (int pass = 0; pass < 2; ++pass)
-      for (int q1 = 0; q1 < nb; ++q1)
-        for (int q2 = 0; q2 <= q1; ++q2) {
-          const int a = rows[q1], b = rows[q2];  // a >= b (rows ascending)
-          const bool pri = bottom ? a == lk : b == lk;
-          if (pri != (pass == 0)) continue;
-          npri += pri;
-          iblk.push_back(bottom && in_sep(a) && in_sep(b) ? shadow(a, b) : blk(a, b));
-          iq.push_back(pb[q1] | (pb[q2] << 16));
-        }
-    iptr.push_back((int32_t)iblk.size());
-    ipri.push_back(npri);
-  };
-  // top steps (top-down, panels may include separator rows)
-  for (int k = 0; k < m; ++k) {
-    std::vector<int> rows;
-    for (int i = k + 1; i <= P.prof_last[k]; ++i)
-      if (first[i] <= k) rows.push_back(i);
-    col.push_back(k);
-    mode.push_back(0);
-    diag.push_back(blk(k, k));
-    std::vector<int32_t> pb;
-    for (int i : rows) {
-      pb.push_back(blk(i, k));
-      pblk.push_back(blk(i, k));
-      py.push_back(6 * i);
-    }
-    sptr.push_back((int32_t)pblk.size());
-    maxnb = std::max(maxnb, (int)rows.size());
-    add_items(rows, pb, false, k + 1);
-  }
-  // bottom steps (bottom-up: row k's blocks (k, j), j in [first[k], k))
-  for (int k = F - 1; k >= m + s; --k) {
-    std::vector<int> rows;
-    for (int j = first[k]; j < k; ++j) rows.push_back(j);
-    col.push_back(k);
-    mode.push_back(1);
-    diag.push_back(blk(k, k));
-    std::vector<int32_t> pb;
-    for (int j : rows) {
-      pb.push_back(blk(k, j));
-      pblk.push_back(blk(k, j));
-      py.push_back(in_sep(j) ? 6 * F + 6 * (j - m) : 6 * j);
-    }
-    sptr.push_back((int32_t)pblk.size());
-    maxnb = std::max(maxnb, (int)rows.size());
-    add_items(rows, pb, true, k - 1);
-  }
-  // separator steps (top-down within the separator)
-  for (int k = m; k < m + s; ++k) {
-    std::vector<int> rows;
-    for (int i = k + 1; i < m + s; ++i)
-      if (first[i] <= k) rows.push_back(i);
-    col.push_back(k);
-    mode.push_back(0);
-    diag.push_back(blk(k, k));
-    std::vector<int32_t> pb;
-    for (int i : rows) {
-      pb.push_back(blk(i, k));
-      pblk.push_back(blk(i, k));
-      py.push_back(6 * i);
-    }
-    sptr.push_back((int32_t)pblk.size());
-    maxnb = std::max(maxnb, (int)rows.size());
-    add_items(rows, pb, false, k + 1);
-  }
-  std::vector<int32_t> merge;
-  for (int a = m; a < m + s; ++a)
-    for (int b = m; b <= a; ++b) merge.push_back(first[a] <= b ? blk(a, b) : -1);
-  // column lists for the bottom back substitution: k >= m, bottom rows i > k
-  std::vector<int32_t> cptr{0}, cl;
-  for (int k = m; k < F; ++k) {
-    for (int i = std::max(k + 1, m + s); i < F; ++i)
-      if (first[i] <= k) {
-        cl.push_back(i);
-        cl.push_back(blk(i, k));
-      }
-    cptr.push_back((int32_t)(cl.size() / 2));
-  }
-  std::vector<int32_t>& T = P.solve2_tab;
-  T.clear();
-  auto put = [&](int& o, const std::vector<int32_t>& v) {
-    o = (int)T.size();
-    T.insert(T.end(), v.begin(), v.end());
-  };
-  std::vector<int32_t> offv(P.prof_off.begin(), P.prof_off.begin() + F);
-  put(L.col, col);
-  put(L.mode, mode);
-  put(L.diag, diag);
-  put(L.step_ptr, sptr);
-  put(L.panel_blk, pblk);
-  put(L.panel_y, py);
-  put(L.item_ptr, iptr);
-  put(L.item_blk, iblk);
-  put(L.item_q, iq);
-  put(L.item_pri, ipri);
-  put(L.merge_main, merge);
-  put(L.colb_ptr, cptr);
-  put(L.colb, cl);
-  put(L.off, offv);
-  put(L.first, first);
-  L.len = (int)T.size();
-  L.m = m;
-  L.s = s;
-  L.nbot = nbot;
-  L.nshadow = s * (s + 1) / 2;
-  L.max_panel = maxnb;
-  // one lane per panel row of the panel wave; item_q packs two 16-bit block indices
-  L.enabled = maxnb <= 10 && nprof + L.nshadow < 65536 ? 1 : 0;
-}
-
 std::vector<int32_t> local_profile_first(const BAPlan& P) {
   std::vector<int32_t> first(P.n_free);
   for (int i = 0; i < P.n_free; ++i) first[i] = i;
@@ -654,7 +512,6 @@ void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
   L.len = (int)T.size();
   L.max_panel = maxnb;
   if (T.empty()) T.push_back(0);
-  build_two_sided(P);
 }
 
 uint64_t plan_digest(const BAPlan& P) {
@@ -677,8 +534,7 @@ uint64_t plan_digest(const BAPlan& P) {
   vec(P.seg_chunk); vec(P.seg_slot_off); vec(P.seg_cam_off); vec(P.slot_i); vec(P.slot_j); vec(P.segcam_f);
   vec(P.segcam_diag); vec(P.seg_acam_off); vec(P.seg_acam); vec(P.obs_acam); vec(P.prof_first); vec(P.prof_off);
   vec(P.prof_last); vec(P.prof_src_ptr); vec(P.prof_src); vec(P.prof_diag); vec(P.camb_ptr); vec(P.camb_src);
-  vec(P.solve_tab); vec(P.solve2_tab);
-  bytes(&P.solve2_layout, sizeof P.solve2_layout);
+  vec(P.solve_tab);
   return h;
 }
 

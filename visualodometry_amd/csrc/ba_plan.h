@@ -73,26 +73,6 @@ struct SolveTableLayout {
   int max_panel = 0;  // most panel blocks in one column
 };
 
-// Two-sided ("twisted") K3 plan, used when the profile is monotone (first[] non
-// decreasing) and wide enough.  With w = max(i - first[i]) and a separator
-// [m, m+s), s = w, the top columns 0..m-1 are eliminated top-down and the bottom
-// rows F-1..m+s bottom-up (row panels: L~_{j,k} = (C_k^-1 S_{k,j})^T, stored in
-// block (k, j) as rows of L~_{j,k}) concurrently; the two sides meet only in the
-// separator-separator blocks and separator rhs, which the bottom side accumulates
-// in shadow copies (blocks nprof + sh, rhs 6F + 6(j - m)) merged before the
-// separator is factored top-down.  Steps are numbered: top 0..m-1, bottom
-// m..m+nbot-1 (rows F-1 down to m+s), separator after that.
-struct TwoSidedLayout {
-  int enabled = 0, m = 0, s = 0, nbot = 0, nshadow = 0;
-  int col = 0, mode = 0, diag = 0, step_ptr = 0, panel_blk = 0, panel_y = 0, item_ptr = 0,
-      item_blk = 0, item_q = 0;
-  int item_pri = 0;             // per step: leading items on the look-ahead line
-  int merge_main = 0;           // per shadow block: its profile block, -1 if none
-  int colb_ptr = 0, colb = 0;   // per k >= m: (bottom row i > k, block (i, k)) pairs
-  int off = 0, first = 0, len = 0;
-  int max_panel = 0;
-};
-
 struct BAPlan {
   int n_poses = 0, n_points = 0, n_obs = 0, n_fixed = 0, n_free = 0, n_te = 0;
   // internal order -> caller order
@@ -140,8 +120,6 @@ struct BAPlan {
   // plus diag[k] (profile block (k, k)), off[k], first[k].
   std::vector<int32_t> solve_tab;
   SolveTableLayout solve_layout;
-  std::vector<int32_t> solve2_tab;
-  TwoSidedLayout solve2_layout;
 
   int n_chunks() const { return (int)chunk_obs.size() - 1; }
   int n_segments() const { return (int)seg_chunk.size() - 1; }
