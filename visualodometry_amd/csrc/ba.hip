@@ -1360,11 +1360,11 @@ class BAEngine {
         sys_len_ = (size_t)(F + band_.s) * CS + 1;
         cost_off_ = (long)sys_len_ - 1;
         pad = band_slot_stride(w);  // the ring loader's last LDS-DMA piece reads past the end
-        band_tab_ = band_tables(F, band_);
+        band_lds_ = band_lds_layout(F, band_, P.n_poses);
+        band_tab_ = band_tables(F, band_, band_lds_);
         upload(d_band_tab_, band_tab_.tab, st);
-        band_lds_ = band_lds_bytes(F, w, P.n_poses);
         band_set_attributes(band_lds_);
-        d_fac_.reserve(band_fac_doubles(F, w) * 8);
+        if (!band_lds_.full) d_fac_.reserve(band_fac_doubles(F, w) * 8);
       } else {
         for (int b = 0; b < nprof; ++b) red_dst_[b] = 36 * b;
         for (int f = 0; f < F; ++f) red_rdst_[f] = 36 * nprof + 6 * f;
@@ -1652,7 +1652,7 @@ class BAEngine {
       B.tab = d_band_tab_.as<int>();
       B.sys = A.sys;
       B.zero = d_zero_.as<double>();
-      B.fac = d_fac_.as<double>();
+      B.fac = band_lds_.full ? nullptr : d_fac_.as<double>();
       B.cost_out = A.cost_out;
       B.dc = A.dc;
       B.pose_cur = A.pose_cur;
@@ -1763,7 +1763,7 @@ class BAEngine {
   SolveLds solve_layout_{};
   BandSplit band_{};
   bool band_on_ = false;
-  size_t band_lds_ = 0;
+  BandLds band_lds_;
   BandTables band_tab_;
   DevBuf d_fac_, d_zero_, d_band_tab_, d_red_dst_, d_red_rdst_;
   std::vector<int32_t> red_dst_, red_rdst_;  // K2 output offsets (host copies for gn_step)

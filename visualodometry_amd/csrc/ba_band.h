@@ -12,7 +12,8 @@ namespace vo {
 // holds the panel of a block column, one lane per scalar row, (w + 1) * 6 <= 64.
 constexpr int kBandMaxW = 9;
 constexpr int kBandMaxF = 512;
-constexpr int kBandStamps = 32;  // diagnostic build: phase slots per wave
+constexpr int kBandStamps = 32;
+constexpr size_t kBandLdsMax = 160 * 1024 - 1024;  // static LDS: flags, zero block  // dynamic LDS of the one workgroup  // diagnostic build: phase slots per wave
 
 // Split of the F free block rows: top rows [0, m) eliminated top-down, bottom rows
 // [F - nb, F) bottom-up, concurrently; the separator [m, m + s) (s = w) last, top-down.
@@ -28,7 +29,18 @@ struct BandTables {
   std::vector<int> tab;
   int merge = 0, n_merge = 0;
 };
-BandTables band_tables(int F, const BandSplit& b);
+// LDS layout of the two column stores.  Ring mode: w + 3 slots per side, each padded to
+// whole 1 KiB LDS-DMA pieces; factor records go to global memory.  Full mode (when it
+// fits): every column of a side in its own slot at the K2 stride, so the factor stays
+// in LDS for the back substitution (a DMA's last piece spills into the next slot, or into
+// the 1 KiB pad after the side, with the K2 values of the following column).
+struct BandLds {
+  bool full = false;
+  int rc = 0, ss = 0, pad = 0;  // slots per side, doubles per slot, doubles after each side
+  size_t bytes = 0;
+};
+BandLds band_lds_layout(int F, const BandSplit& b, int n_poses);
+BandTables band_tables(int F, const BandSplit& b, const BandLds& L);
 
 // K2 writes the reduced camera system in the banded layout (ba.hip, red_dst_): per side,
 // column v = band_col_stride(w) doubles -- block (v + q, v) of the side's coordinates
@@ -56,11 +68,10 @@ struct BandArgs {
 inline int band_col_stride(int w) { return 36 * (w + 1) + 12; }
 // Doubles per LDS ring slot: the column padded to whole 1 KiB LDS-DMA wave pieces.
 inline int band_slot_stride(int w) { return (band_col_stride(w) + 127) / 128 * 128; }
-size_t band_lds_bytes(int F, int w, int n_poses);
 size_t band_fac_doubles(int F, int w);
 // true if the window fits the kernel (lane budget, LDS budget)
 bool band_supported(int F, int w, int n_poses);
-void band_set_attributes(size_t lds);
-void launch_band_solve(const BandArgs& A, size_t lds, hipStream_t st);
+void band_set_attributes(const BandLds& L);
+void launch_band_solve(const BandArgs& A, const BandLds& L, hipStream_t st);
 
 }  // namespace vo

@@ -56,8 +56,30 @@ BandSplit band_split(int F, const std::vector<int>& first) {
   return b;
 }
 
-BandTables band_tables(int F, const BandSplit& b) {
-  const int w = b.w, R = w + 1, RC = w + 3, CS = band_slot_stride(w), m = b.m, sp = b.s;
+static size_t band_lds_total(const BandLds& L, int F, int n_poses) {
+  return 8 * (2 * ((size_t)L.rc * L.ss + L.pad) + 6 * (size_t)F + 12 * (size_t)n_poses + (L.full ? 104 : 0));
+}
+
+BandLds band_lds_layout(int F, const BandSplit& b, int n_poses) {
+  BandLds L;
+  const int CS = band_col_stride(b.w);
+  L.full = true;
+  L.rc = std::max(b.m + b.s, b.nb + b.s);
+  L.ss = CS;
+  L.pad = 128;
+  L.bytes = band_lds_total(L, F, n_poses);
+  if (L.bytes <= kBandLdsMax) return L;
+  L.full = false;
+  L.rc = b.w + 3;
+  L.ss = band_slot_stride(b.w);
+  L.pad = 0;
+  L.bytes = band_lds_total(L, F, n_poses);
+  return L;
+}
+
+BandTables band_tables(int F, const BandSplit& b, const BandLds& L) {
+  const int w = b.w, R = w + 1, RC = L.rc, SS = L.ss, m = b.m, sp = b.s;
+  const int offB = RC * SS + L.pad;
   BandTables T;
   T.merge = 0;
   for (int jj = 0; jj < sp; ++jj)
@@ -65,15 +87,15 @@ BandTables band_tables(int F, const BandSplit& b) {
       const int j = m + jj, i = j + qq;
       for (int r = 0; r < 6; ++r)
         for (int c = 0; c < 6; ++c) {
-          T.tab.push_back((j % RC) * CS + 36 * qq + 6 * r + c);
-          T.tab.push_back(RC * CS + ((F - 1 - i) % RC) * CS + 36 * qq + 6 * c + r);
+          T.tab.push_back((j % RC) * SS + 36 * qq + 6 * r + c);
+          T.tab.push_back(offB + ((F - 1 - i) % RC) * SS + 36 * qq + 6 * c + r);
         }
     }
   for (int d = 0; d < sp; ++d) {
     const int i = m + d;
     for (int r = 0; r < 6; ++r) {
-      T.tab.push_back((i % RC) * CS + 36 * R + r);
-      T.tab.push_back(RC * CS + ((F - 1 - i) % RC) * CS + 36 * R + r);
+      T.tab.push_back((i % RC) * SS + 36 * R + r);
+      T.tab.push_back(offB + ((F - 1 - i) % RC) * SS + 36 * R + r);
     }
   }
   T.n_merge = (int)T.tab.size() / 2;
@@ -81,15 +103,14 @@ BandTables band_tables(int F, const BandSplit& b) {
   return T;
 }
 
-size_t band_lds_bytes(int F, int w, int n_poses) {
-  const size_t CS = band_slot_stride(w), RC = w + 3;
-  return 8 * (2 * RC * CS + 6 * (size_t)F + 12 * (size_t)n_poses + 16);
-}
-
 size_t band_fac_doubles(int F, int w) { return (size_t)std::max(F, 1) * band_col_stride(w); }
 
 bool band_supported(int F, int w, int n_poses) {
-  return w >= 0 && w <= kBandMaxW && F <= kBandMaxF && band_lds_bytes(F, w, n_poses) <= 160 * 1024 - 64;
+  if (w < 0 || w > kBandMaxW || F > kBandMaxF) return false;
+  BandSplit b;
+  b.w = w;
+  b.m = F;  // the ring layout's size does not depend on the split
+  return band_lds_layout(F, b, n_poses).bytes <= kBandLdsMax;
 }
 
 namespace {
@@ -151,7 +172,21 @@ __device__ __forceinline__ void band_barrier() { asm volatile("s_waitcnt lgkmcnt
     int d_;                                                                               \
     asm volatile("s_waitcnt lgkmcnt(0)\n\tv_mov_b32 %0, %1" : "=v"(d_) : "v"(__double2loint(x))); \
   } while (0)
+#if VO_BA_STAMPS >= 2  // fine stamps: each one drains the wave's LDS queue (s_memtime)
+#define BSTF(i) BST(i)
 #else
+#define BSTF(i) \
+  do {          \
+  } while (0)
+#undef BSETTLE
+#define BSETTLE(x) \
+  do {             \
+  } while (0)
+#endif
+#else
+#define BSTF(i) \
+  do {          \
+  } while (0)
 #define BST(i) \
   do {         \
   } while (0)
@@ -163,35 +198,43 @@ __device__ __forceinline__ void band_barrier() { asm volatile("s_waitcnt lgkmcnt
 // Loads below never feed a select or branch before their first real use: a value that
 // must be zero is loaded from the zero block (A.zero) instead, so the waitcnt pass can
 // leave every prefetch in flight.
+template <bool kFull>
 __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int s_fail;
+  __shared__ __attribute__((aligned(16))) double s_zero[40];   // full mode's zero block
+  __shared__ __attribute__((aligned(16))) double s_dummy[64];  // full mode: masked stores
 #if VO_BA_STAMPS
   unsigned long long st_acc[kBandStamps] = {}, st_t = __builtin_amdgcn_s_memtime();
 #endif
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  // CS: doubles per column (K2 layout, factor record), CSP per ring slot (1 KiB pieces)
-  const int F = A.F, w = A.w, R = w + 1, CS = 36 * R + 12, CSP = (CS + 127) / 128 * 128, RC = w + 3;
+  // CS: doubles per column (K2 layout, factor record; full mode: SS == CS); SS per slot (ring mode: whole 1 KiB
+  // pieces), RC slots per side (band_lds_layout)
+  const int F = A.F, w = A.w, R = w + 1, CS = 36 * R + 12, CSP = (CS + 127) / 128 * 128;
   const int m = A.m, nb = A.nb, sp = A.s;
+  const int ncolT = m + sp, ncolB = nb + sp;
+  const int SS = kFull ? CS : CSP, RC = kFull ? max(ncolT, ncolB) : w + 3, SPAD = kFull ? 128 : 0;
   const bool prior_fail = A.status && *A.status;
   double* ringT = dyn;
-  double* ringB = ringT + RC * CSP;
-  double* xs = ringB + RC * CSP;
-  double* pose_l = xs + 6 * F;
-  double* bb = pose_l + 12 * A.n_poses;  // 2 x 8
-  const int ncolT = m + sp, ncolB = nb + sp;
+  double* ringB = ringT + RC * SS + SPAD;
+  double* zs = ringB + RC * SS + SPAD;  // back substitution: z (6F)
+  double* pose_l = zs + 6 * F;
+  // full mode: a zero block (masked loads) and a dummy row (masked stores), dyn offsets
+  const int ZOFF = (int)(pose_l - dyn) + 12 * A.n_poses, DOFF = ZOFF + 40;
 
   const int side = wave & 1, role = wave >> 1;
   const bool sbot = side == 1;
-  // this wave's side: ring (column v in slot v mod (w + 3)), back-substitution row
-  // broadcast, factor records (column v at v * CS, global), column sources, columns
+  // this wave's side: ring (column v in slot v mod RC), factor records (column v at v *
+  // CS: global memory, or the full-mode slots themselves), column sources, columns
   // factored before the merge, columns loaded into the ring
   double* const sring = sbot ? ringB : ringT;
-  double* const sbbuf = bb + 8 * side;
-  double* const sfac = sbot ? A.fac + (long)ncolT * CS : A.fac;
+  const double* const recT = kFull ? ringT : A.fac;  // the top side's records
+  const double* const sfac = kFull ? sring : sbot ? A.fac + (long)ncolT * CS : A.fac;
   const double* const ssys = A.sys + (sbot ? (long)ncolT * CS : 0);  // this side's columns (K2)
   const int sna = sbot ? nb : m, snload = sbot ? ncolB : ncolT;
 
+  if (tid < 40) s_zero[tid] = 0.0;
+  if (kFull && tid < 40) dyn[ZOFF + tid] = 0.0;
   if (tid == 0) {
     s_fail = prior_fail ? 1 : 0;
     if (A.cost_out) *A.cost_out = A.sys[A.cost_off];
@@ -215,7 +258,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       const bool top = e < nT;
       const int x = 2 * (top ? e : e - nT), col = x / CS;
       if (e < nT + nB)
-        *reinterpret_cast<double2*>(dyn + (top ? 0 : RC * CSP) + col * CSP + x - col * CS) = v[u];
+        *reinterpret_cast<double2*>((top ? ringT : ringB) + col * SS + x - col * CS) = v[u];
     }
   }
 
@@ -275,7 +318,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // Step k, before the barrier (column k in slot sk): factor the diagonal block, solve
   // this lane's panel row, write the panel and 1/diag into the ring.
   auto chain_pre = [&](int sk) __attribute__((always_inline)) {
-    double* col = sring + sk * CSP;
+    double* col = sring + sk * SS;
     // the diagonal block's rows (group q == 0) to every lane through LDS
     if (act && q == 0) st6g(col + 6 * sr, P);
     wave_sync<true>();
@@ -289,14 +332,14 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
         if (c + 1 <= i) L[P6(i, c + 1)] = v.y;
       }
     BSETTLE(L[20]);
-    BST(17);
+    BSTF(17);
     chol6_nochk(L, r);
     bad = bad || !(isfinite(r[0] + r[1] + r[2] + r[3] + r[4] + r[5]));
     BSETTLE(r[5]);
-    BST(18);
+    BSTF(18);
     fwd6(L, r, P);  // x L_kk^T = row; on the diagonal group: row sr of L_kk
     BSETTLE(P[5]);
-    BST(19);
+    BSTF(19);
     if (act) st6g(col + 36 * q + 6 * sr, P);
     if (act && q == 0) col[36 * R + 6 + sr] = pick<6>(r, sr);
     wave_sync<true>();
@@ -310,9 +353,9 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   auto chain_post = [&](int sk1) __attribute__((always_inline)) {
     const int q1 = q == 0 ? w : q - 1;
     double N[6];
-    ld6g(sring + sk1 * CSP + (act ? 36 * q1 + 6 * sr : 0), N);
+    ld6g(sring + sk1 * SS + (act ? 36 * q1 + 6 * sr : 0), N);
     BSETTLE(N[5]);
-    BST(22);
+    BSTF(22);
     if (w >= 1 && q != 0)
 #pragma unroll
       for (int c = 0; c < 6; ++c)
@@ -322,13 +365,13 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     for (int c = 0; c < 6; ++c) P[c] = act ? N[c] : 0.0;
     q = q1;
     BSETTLE(P[5]);
-    BST(23);
+    BSTF(23);
   };
   // Forward-substitution wave, step k: y'_k = L_kk^-1 y_k into the record, y_i -= L_ik
   // y'_k for the rows below (lane 6 qf + rf, qf = 1..w), then the factor record of column
   // k (blocks, y'_k, 1/diag) to global memory.
   auto fwd_step = [&](int k, int sk) __attribute__((always_inline)) {
-    double* col = sring + sk * CSP;
+    double* col = sring + sk * SS;
     double L[21], r[6], y[6], row[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -347,12 +390,13 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     bad = bad || !isfinite(y[0] + y[1] + y[2] + y[3] + y[4] + y[5]);
     if (on) {
       const int st = sk + qf < RC ? sk + qf : sk + qf - RC;
-      sring[st * CSP + 36 * R + rf] -=
+      sring[st * SS + 36 * R + rf] -=
           row[0] * y[0] + row[1] * y[1] + row[2] * y[2] + row[3] * y[3] + row[4] * y[4] + row[5] * y[5];
     }
     if (lane < 6) col[36 * R + lane] = pick<6>(y, lane);
+    if (kFull) return;  // the record stays in its slot
     const double2* s2 = reinterpret_cast<const double2*>(col);
-    double2* d2 = reinterpret_cast<double2*>(sfac + (long)k * CS);
+    double2* d2 = reinterpret_cast<double2*>(const_cast<double*>(sfac) + (long)k * CS);
     double2 v2[3];
 #pragma unroll
     for (int t = 0; t < 3; ++t) v2[t] = s2[min(lane + 64 * t, CS / 2 - 1)];
@@ -362,12 +406,12 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   };
   // Trailing wave, step k: blocks (i, j), k + 2 <= j <= i <= k + w, minus L_ik L_jk^T.
   auto trail_step = [&](int sk) __attribute__((always_inline)) {
-    const double* col = sring + sk * CSP;
+    const double* col = sring + sk * SS;
 #pragma unroll
     for (int h = 0; h < kTaskRounds; ++h) {
       if (tk_qj[h] < 0) continue;
       const int st = sk + tk_qj[h] < RC ? sk + tk_qj[h] : sk + tk_qj[h] - RC;
-      double* out = sring + st * CSP + tk_o[h];
+      double* out = sring + st * SS + tk_o[h];
       double o0[6], o1[6], a0[6], a1[6], B[6][6];
       ld6g(out, o0);
       ld6g(out + 18, o1);
@@ -387,13 +431,14 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     }
   };
   // Loader wave, step k (slot of column k - 1: skm): column k + w + 2 into the freed
-  // slot (first read at step k + 2), then the previous column's pieces retired.
+  // slot (full mode: its own slot; first read at step k + 2), then the previous column's
+  // pieces retired.
   auto load_step = [&](int k, int skm) __attribute__((always_inline)) {
     if (k + w + 2 < snload) {
-      dma_col(k + w + 2, sring + skm * CSP);
-      BST(20);
+      dma_col(k + w + 2, sring + (kFull ? k + w + 2 : skm) * SS);
+      BSTF(20);
       dma_wait_prev();
-      BST(21);
+      BSTF(21);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -428,14 +473,14 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     if (sp > 0) {
       // both sides' state of the separator into the rings, the bottom's contributions
       // merged into the top's (fixed order), then the top continues through the separator
-      if (act) st6g(sring + (sna % RC) * CSP + 36 * q + 6 * sr, P);
+      if (act) st6g(sring + (sna % RC) * SS + 36 * q + 6 * sr, P);
       __syncthreads();
       for (int e = tid; e < A.n_merge; e += kBandThreads) {
         const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
         dyn[d.x] += dyn[d.y];
       }
       __syncthreads();
-      if (act && side == 0) ld6g(ringT + (m % RC) * CSP + 36 * q + 6 * sr, P);
+      if (act && side == 0) ld6g(ringT + (m % RC) * SS + 36 * q + 6 * sr, P);
       BST(4);
       int sk = m % RC, skm = sk == 0 ? RC - 1 : sk - 1;
       for (int p = m; p < m + sp; ++p) {
@@ -464,30 +509,76 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   BST(9);
   const bool failed = s_fail != 0;
 
-  // ---- back substitution L^T x = y' (chain waves); loader waves stage the poses
+  // ---- back substitution L^T x = y'.  z_k = y'_k - sum_{q=1..w} L_{k+q,k}^T x_{k+q} runs
+  // down the chain; x_k = L_kk^-T z_k is taken off it: x_k's share of the lane's row
+  // j = k - q is g . z_k with g = L_kk^-1 (column sr of L_{k,j}), formed from operands
+  // fetched two steps ahead.  A chain step is the readlane broadcast of z_k from the
+  // lanes holding it plus 6 FMAs; every x_k is formed in parallel at the end from z (LDS)
+  // and the factor records.  Loader waves stage the poses meanwhile.
   if (role == kLoad)
     for (int e = tid - 64 * kLoad * 2; e < 12 * A.n_poses; e += 128) pose_l[e] = A.pose_cur[e];
+  // Full mode: every block L_{k,i} (k - w <= i < k) is replaced by G = L_kk^-1 L_{k,i}
+  // first, one block per thread (the records are in LDS); the chain then reads g as is.
+  if (kFull && !failed) {
+    const int nT = ncolT * w, nAll = (ncolT + ncolB) * w;
+    for (int e = tid; e < nAll; e += kBandThreads) {
+      const bool eb = e >= nT;
+      const int e2 = eb ? e - nT : e, k = e2 / w, qq = e2 - k * w + 1, i = k - qq;
+      if (i < 0 || (eb && i >= nb)) continue;
+      double* fs = eb ? ringB : ringT;
+      // L_kk: this side's record, or (the bottom side's separator rows) the top's
+      const double* rec = (eb && k >= nb) ? ringT + (long)(F - 1 - k) * CS : fs + (long)k * CS;
+      double L[21], r[6], Bk[6][6];
+#pragma unroll
+      for (int ii = 0; ii < 6; ++ii)
+#pragma unroll
+        for (int c = 0; c <= ii; c += 2) {
+          const double2 v = reinterpret_cast<const double2*>(rec + 6 * ii)[c / 2];
+          L[P6(ii, c)] = v.x;
+          if (c + 1 <= ii) L[P6(ii, c + 1)] = v.y;
+        }
+      ld6g(rec + 36 * R + 6, r);
+      double* blk = fs + (long)i * CS + 36 * qq;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) ld6g(blk + 6 * c, Bk[c]);
+#pragma unroll
+      for (int s2 = 0; s2 < 6; ++s2) {
+        double gv[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) gv[c] = Bk[c][s2];
+        fwd6(L, r, gv);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) Bk[c][s2] = gv[c];
+      }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) st6g(blk + 6 * c, Bk[c]);
+    }
+    __syncthreads();
+  }
+  BST(16);
+  // masked operands come from a zero block in the records' address space (LDS loads stay
+  // ds_read, not flat)
+  const double* const zsrc = kFull ? s_zero : A.zero;
   double Yb = 0.0;
-  struct BsOps {
-    double L[21], r[6], Lc[6], yin;
-  };
   int qb = 0;  // this lane's window row at the current step k is k - qb
   auto bs_init = [&](int khi, int kp) __attribute__((always_inline)) {
     qb = act ? ((khi - g) % R + R) % R : 0;
     if (act) {
       const int i = khi - qb;
       const bool on = i >= 0 && i < kp;
-      Yb = *(on ? sfac + (long)i * CS + 36 * R + sr : A.zero);
-      if (qb == 0) sbbuf[sr] = Yb;
+      Yb = *(on ? sfac + (long)i * CS + 36 * R + sr : zsrc);
     }
-    wave_sync<true>();
   };
-  // operands of step k for a lane at window position qk (rows >= kp are pseudo steps:
-  // x given by the other side): L_kk, 1/diag (uniform, clamped record); column sr of
-  // L_{k,k-qk}; the y' of the row entering the window (k - w - 1) for the lane leaving it.
+  struct BsOps {
+    double L[21], r[6], Lc[6], yin;
+  };
+  // operands of step k for a lane at window position qk: L_kk and 1/diag (this side's
+  // record k, clamped; for the bottom side's separator rows k >= kp, the top's record
+  // F - 1 - k), column sr of L_{k,k-qk} (zero unless the lane's row is live), and the y'
+  // of the row entering the window (k - w - 1) for the lane leaving it.
   auto bs_fetch = [&](int k, int qk, int kp, BsOps& o) __attribute__((always_inline)) {
-    const int kk = max(min(k, kp - 1), 0);
-    const double* rec = sfac + (long)kk * CS;
+    if (!kFull) {  // full mode: g precomputed in place of the block
+    const double* rec = k >= kp ? recT + (long)(F - 1 - k) * CS : sfac + (long)max(k, 0) * CS;
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
@@ -497,31 +588,32 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
         if (c + 1 <= i) o.L[P6(i, c + 1)] = v.y;
       }
     ld6g(rec + 36 * R + 6, o.r);
+    }
     const int i = k - qk;
     const bool on = act && qk >= 1 && i >= 0 && i < kp;
-    const double* rc = on ? sfac + (long)i * CS + 36 * qk + sr : A.zero;
+    const double* rc = on ? sfac + (long)i * CS + 36 * qk + sr : zsrc;
 #pragma unroll
     for (int c = 0; c < 6; ++c) o.Lc[c] = rc[6 * c];
     const int ie = k - R;
     const bool on2 = act && qk == 0 && ie >= 0 && ie < kp;
-    o.yin = *(on2 ? sfac + (long)ie * CS + 36 * R + sr : A.zero);
+    o.yin = *(on2 ? sfac + (long)ie * CS + 36 * R + sr : zsrc);
   };
-  auto bs_step = [&](int k, int kp, const BsOps& o) __attribute__((always_inline)) {
-    double x[6];
+  auto bs_step = [&](int k, int kp, int g0, BsOps& o) __attribute__((always_inline)) {
+    if (!kFull) fwd6(o.L, o.r, o.Lc);  // g, independent of z_k
+    double z[6];
     const int G = sbot ? F - 1 - k : k;
     if (k >= kp) {
-      ld6g(xs + 6 * G, x);
+      ld6g(zs + 6 * G, z);  // the separator's z (top side)
     } else {
-      ld6g(sbbuf, x);
-      bwd6(o.L, o.r, x);
-      if (lane < 6) xs[6 * G + lane] = pick<6>(x, lane);
+      const int l0 = __builtin_amdgcn_readfirstlane(6 * g0);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) z[c] = readlane_d(Yb, l0 + c);
+      if (act && qb == 0) zs[6 * G + sr] = Yb;
     }
     if (act && qb >= 1)
-      Yb -= o.Lc[0] * x[0] + o.Lc[1] * x[1] + o.Lc[2] * x[2] + o.Lc[3] * x[3] + o.Lc[4] * x[4] + o.Lc[5] * x[5];
-    if (act && qb == 1) sbbuf[sr] = Yb;
+      Yb -= o.Lc[0] * z[0] + o.Lc[1] * z[1] + o.Lc[2] * z[2] + o.Lc[3] * z[3] + o.Lc[4] * z[4] + o.Lc[5] * z[5];
     if (act && qb == 0) Yb = o.yin;
     qb = qb == 0 ? w : qb - 1;
-    wave_sync<true>();
   };
   auto dec = [&](int x) __attribute__((always_inline)) { return x == 0 ? w : x - 1; };
   auto bs_run = [&](int khi, int klo, int kp) __attribute__((always_inline)) {
@@ -529,49 +621,121 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     int qa = dec(dec(qb)), qc = dec(qa);  // window positions of steps khi - 2, khi - 3
     bs_fetch(khi, qb, kp, o0);
     bs_fetch(khi - 1, dec(qb), kp, o1);
+    int g0 = khi % R;  // the group at window position 0 (holding z_k) at step k
     int k = khi;
     for (; k - 1 >= klo; k -= 2) {
-      bs_step(k, kp, o0);
+      bs_step(k, kp, g0, o0);
       bs_fetch(k - 2, qa, kp, o0);
-      BST(26);
-      bs_step(k - 1, kp, o1);
+      g0 = dec(g0);
+      bs_step(k - 1, kp, g0, o1);
       bs_fetch(k - 3, qc, kp, o1);
-      BST(26);
+      g0 = dec(g0);
+      BSTF(26);
       qa = dec(dec(qa));
       qc = dec(dec(qc));
     }
-    if (k >= klo) bs_step(k, kp, o0);
+    if (k >= klo) bs_step(k, kp, g0, o0);
+  };
+  // Full mode: the same steps with LDS operands and no divergent code.  A lane's row j =
+  // k - qb stays fixed while it crosses the window, so its g address is its row's record
+  // plus 36 per step; z_k goes through LDS (the qb == 0 lanes store it, every lane reads
+  // it back: the store is the one zs needs anyway).
+  auto bs_run_full = [&](int khi, int klo, int kp) __attribute__((always_inline)) {
+    // offsets into dyn; selects kept opaque so that they stay v_cndmask, not branches
+    const int sbase = (int)(sring - dyn);
+    int qf = qb, kf = khi;
+    int pf = sbase + (khi - qb) * CS + 36 * qb + sr;  // g of the step being fetched (if live)
+    auto fetch = [&](double (&gv)[6], double& yin) __attribute__((always_inline)) {
+      const int jf = kf - qf;
+      const bool on = act & (qf >= 1) & (jf >= 0) & (jf < kp);
+      int og = on ? pf : ZOFF;
+      asm volatile("" : "+v"(og));
+      const double* pg = dyn + og;
+      gv[0] = pg[0]; gv[1] = pg[6]; gv[2] = pg[12]; gv[3] = pg[18]; gv[4] = pg[24]; gv[5] = pg[30];
+      int oy = kf - R >= 0 ? sbase + (kf - R) * CS + 36 * R + sr : ZOFF;
+      asm volatile("" : "+v"(oy));
+      yin = dyn[oy];
+      --kf;
+      const bool wrap = qf == 0;
+      qf = wrap ? w : qf - 1;
+      pf = wrap ? pf - R * CS + 36 * w : pf - 36;
+    };
+    int zk = (int)(zs - dyn) + 6 * (sbot ? F - 1 - khi : khi);  // z_k of the current step
+    const int dz = sbot ? 6 : -6;
+    auto step = [&](int k, const double (&gv)[6], double yin) __attribute__((always_inline)) {
+      int ow = ((k < kp) & act & (qb == 0)) ? zk + sr : DOFF + lane;
+      asm volatile("" : "+v"(ow));
+      dyn[ow] = Yb;
+      double z[6];
+      ld6g(dyn + zk, z);
+      double d = gv[0] * z[0] + gv[1] * z[1] + gv[2] * z[2] + gv[3] * z[3] + gv[4] * z[4] + gv[5] * z[5];
+      asm volatile("" : "+v"(d));
+      Yb = qb == 0 ? yin : Yb - d;
+      qb = qb == 0 ? w : qb - 1;
+      zk += dz;
+    };
+    double gA[6], gB[6], yA, yB;
+    fetch(gA, yA);
+    fetch(gB, yB);
+    int k = khi;
+    for (; k - 1 >= klo; k -= 2) {
+      step(k, gA, yA);
+      fetch(gA, yA);
+      step(k - 1, gB, yB);
+      fetch(gB, yB);
+    }
+    if (k >= klo) step(k, gA, yA);
+  };
+  auto bs_go = [&](int khi, int klo, int kp) __attribute__((always_inline)) {
+    if constexpr (kFull) bs_run_full(khi, klo, kp);
+    else bs_run(khi, klo, kp);
   };
   if (!failed) {
     if (role == kChain && side == 0 && sp > 0) {
       bs_init(m + sp - 1, INT_MAX);
-      bs_run(m + sp - 1, m, INT_MAX);
+      bs_go(m + sp - 1, m, INT_MAX);
     }
     BST(10);
-    __syncthreads();  // separator x in LDS
+    __syncthreads();  // the separator's z in LDS
     BST(11);
     if (role == kChain && side == 0 && m > 0) {
       if (sp == 0) bs_init(m - 1, INT_MAX);
-      bs_run(m - 1, 0, INT_MAX);
+      bs_go(m - 1, 0, INT_MAX);
     }
     if (role == kChain && side == 1 && nb > 0) {
       bs_init(nb + sp - 1, nb);
-      bs_run(nb + sp - 1, 0, nb);
+      bs_go(nb + sp - 1, 0, nb);
     }
   }
   BST(12);
   __syncthreads();
   BST(13);
 
-  for (int e = tid; e < 6 * F; e += kBandThreads) A.dc[e] = failed ? 0.0 : xs[e];
+  // x_k = L_kk^-T z_k for every row at once, then the pose update
+  const double* const recB = kFull ? ringB : A.fac + (long)ncolT * CS;
   for (int c = tid; c < A.n_poses; c += kBandThreads) {
     const double* T = pose_l + 12 * c;
     double* out = A.pose_next + 12l * c;
     if (failed || c < A.n_fixed) {
       for (int e = 0; e < 12; ++e) out[e] = T[e];
+      if (c >= A.n_fixed)
+        for (int e = 0; e < 6; ++e) A.dc[6 * (c - A.n_fixed) + e] = 0.0;
     } else {
-      double d[6];
-      for (int e = 0; e < 6; ++e) d[e] = xs[6 * (c - A.n_fixed) + e];
+      const int G = c - A.n_fixed;
+      const double* rec = G < ncolT ? recT + (long)G * CS : recB + (long)(F - 1 - G) * CS;
+      double L[21], r[6], d[6];
+#pragma unroll
+      for (int ii = 0; ii < 6; ++ii)
+#pragma unroll
+        for (int cc = 0; cc <= ii; cc += 2) {
+          const double2 v = reinterpret_cast<const double2*>(rec + 6 * ii)[cc / 2];
+          L[P6(ii, cc)] = v.x;
+          if (cc + 1 <= ii) L[P6(ii, cc + 1)] = v.y;
+        }
+      ld6g(rec + 36 * R + 6, r);
+      ld6g(zs + 6 * G, d);
+      bwd6(L, r, d);
+      st6g(A.dc + 6 * G, d);
       se3_exp_apply(d, T, out);
     }
   }
@@ -585,12 +749,16 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
 
 }  // namespace
 
-void band_set_attributes(size_t lds) {
-  VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_band_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+void band_set_attributes(const BandLds& L) {
+  const void* f = L.full ? (const void*)ba_band_kernel<true> : (const void*)ba_band_kernel<false>;
+  VO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.bytes));
 }
 
-void launch_band_solve(const BandArgs& A, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL(ba_band_kernel, dim3(1), dim3(kBandThreads), lds, st, A);
+void launch_band_solve(const BandArgs& A, const BandLds& L, hipStream_t st) {
+  if (L.full)
+    hipLaunchKernelGGL(ba_band_kernel<true>, dim3(1), dim3(kBandThreads), L.bytes, st, A);
+  else
+    hipLaunchKernelGGL(ba_band_kernel<false>, dim3(1), dim3(kBandThreads), L.bytes, st, A);
 }
 
 }  // namespace vo

@@ -128,6 +128,13 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// fp64 value of lane l (wave-uniform l): two v_readlane_b32
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
 // ---- 6-double rows (16-byte aligned) ---------------------------------------------
 __device__ __forceinline__ void ld6g(const double* p, double (&v)[6]) {
   const double2* q = reinterpret_cast<const double2*>(p);
