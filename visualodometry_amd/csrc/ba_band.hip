@@ -57,7 +57,7 @@ BandSplit band_split(int F, const std::vector<int>& first) {
 }
 
 static size_t band_lds_total(const BandLds& L, int F, int n_poses) {
-  return 8 * (2 * ((size_t)L.rc * L.ss + L.pad) + 6 * (size_t)F + 12 * (size_t)n_poses + (L.full ? 104 : 0));
+  return 8 * (2 * ((size_t)L.rc * L.ss + L.pad) + 6 * (size_t)F + 12 * (size_t)n_poses + 104);
 }
 
 BandLds band_lds_layout(int F, const BandSplit& b, int n_poses) {
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   double* ringB = ringT + RC * SS + SPAD;
   double* zs = ringB + RC * SS + SPAD;  // back substitution: z (6F)
   double* pose_l = zs + 6 * F;
-  // full mode: a zero block (masked loads) and a dummy row (masked stores), dyn offsets
+  // a zero block (masked loads) and a dummy row (masked stores), dyn offsets
   const int ZOFF = (int)(pose_l - dyn) + 12 * A.n_poses, DOFF = ZOFF + 40;
 
   const int side = wave & 1, role = wave >> 1;
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   const int sna = sbot ? nb : m, snload = sbot ? ncolB : ncolT;
 
   if (tid < 40) s_zero[tid] = 0.0;
-  if (kFull && tid < 40) dyn[ZOFF + tid] = 0.0;
+  if (tid < 40) dyn[ZOFF + tid] = 0.0;
   if (tid == 0) {
     s_fail = prior_fail ? 1 : 0;
     if (A.cost_out) *A.cost_out = A.sys[A.cost_off];
@@ -319,8 +319,14 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // this lane's panel row, write the panel and 1/diag into the ring.
   auto chain_pre = [&](int sk) __attribute__((always_inline)) {
     double* col = sring + sk * SS;
-    // the diagonal block's rows (group q == 0) to every lane through LDS
-    if (act && q == 0) st6g(col + 6 * sr, P);
+    const int ocol = (int)(col - dyn);
+    // the diagonal block's rows (group q == 0) to every lane through LDS (other lanes
+    // store to the dummy row: no divergent code on the chain)
+    {
+      int o = (act & (q == 0)) ? ocol + 6 * sr : DOFF;
+      asm volatile("" : "+v"(o));
+      st6g(dyn + o, P);
+    }
     wave_sync<true>();
     double L[21], r[6];
 #pragma unroll
@@ -334,14 +340,19 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     BSETTLE(L[20]);
     BSTF(17);
     chol6_nochk(L, r);
-    bad = bad || !(isfinite(r[0] + r[1] + r[2] + r[3] + r[4] + r[5]));
+    bad = bad | !(isfinite(r[0] + r[1] + r[2] + r[3] + r[4] + r[5]));
     BSETTLE(r[5]);
     BSTF(18);
     fwd6(L, r, P);  // x L_kk^T = row; on the diagonal group: row sr of L_kk
     BSETTLE(P[5]);
     BSTF(19);
-    if (act) st6g(col + 36 * q + 6 * sr, P);
-    if (act && q == 0) col[36 * R + 6 + sr] = pick<6>(r, sr);
+    {
+      int o = act ? ocol + 36 * q + 6 * sr : DOFF;
+      int o2 = (act & (q == 0)) ? ocol + 36 * R + 6 + sr : DOFF + 8;
+      asm volatile("" : "+v"(o), "+v"(o2));
+      st6g(dyn + o, P);
+      dyn[o2] = pick<6>(r, sr);
+    }
     wave_sync<true>();
     // L_{k+1,k} for the update after the barrier: issued now, its latency under the wait
     if (w >= 1)
@@ -353,16 +364,23 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   auto chain_post = [&](int sk1) __attribute__((always_inline)) {
     const int q1 = q == 0 ? w : q - 1;
     double N[6];
-    ld6g(sring + sk1 * SS + (act ? 36 * q1 + 6 * sr : 0), N);
+    int o = act ? (int)(sring - dyn) + sk1 * SS + 36 * q1 + 6 * sr : ZOFF;
+    asm volatile("" : "+v"(o));
+    ld6g(dyn + o, N);
     BSETTLE(N[5]);
     BSTF(22);
-    if (w >= 1 && q != 0)
+    if (w >= 1) {
+      const bool upd = q != 0;
 #pragma unroll
-      for (int c = 0; c < 6; ++c)
-        N[c] -= P[0] * L1[c][0] + P[1] * L1[c][1] + P[2] * L1[c][2] + P[3] * L1[c][3] + P[4] * L1[c][4] +
-                P[5] * L1[c][5];
+      for (int c = 0; c < 6; ++c) {
+        double u = N[c] - (P[0] * L1[c][0] + P[1] * L1[c][1] + P[2] * L1[c][2] + P[3] * L1[c][3] +
+                           P[4] * L1[c][4] + P[5] * L1[c][5]);
+        asm volatile("" : "+v"(u));
+        N[c] = upd ? u : N[c];
+      }
+    }
 #pragma unroll
-    for (int c = 0; c < 6; ++c) P[c] = act ? N[c] : 0.0;
+    for (int c = 0; c < 6; ++c) P[c] = N[c];  // non-chain lanes load the zero block
     q = q1;
     BSETTLE(P[5]);
     BSTF(23);
@@ -384,16 +402,18 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     ld6g(col + 36 * R + 6, r);
     ld6g(col + 36 * R, y);
     const int qf = lane / 6, rf = lane % 6;
-    const bool on = qf >= 1 && qf < R;
+    const bool on = (qf >= 1) & (qf < R) & (k + qf < snload);  // rows past the side: none
     ld6g(col + (on ? 36 * qf + 6 * rf : 0), row);
     fwd6(L, r, y);
-    bad = bad || !isfinite(y[0] + y[1] + y[2] + y[3] + y[4] + y[5]);
-    if (on) {
+    bad = bad | !isfinite(y[0] + y[1] + y[2] + y[3] + y[4] + y[5]);
+    {
       const int st = sk + qf < RC ? sk + qf : sk + qf - RC;
-      sring[st * SS + 36 * R + rf] -=
-          row[0] * y[0] + row[1] * y[1] + row[2] * y[2] + row[3] * y[3] + row[4] * y[4] + row[5] * y[5];
+      int o = on ? (int)(sring - dyn) + st * SS + 36 * R + rf : DOFF + lane;
+      int o2 = lane < 6 ? (int)(col - dyn) + 36 * R + lane : DOFF + lane;
+      asm volatile("" : "+v"(o), "+v"(o2));
+      dyn[o] -= row[0] * y[0] + row[1] * y[1] + row[2] * y[2] + row[3] * y[3] + row[4] * y[4] + row[5] * y[5];
+      dyn[o2] = pick<6>(y, lane);
     }
-    if (lane < 6) col[36 * R + lane] = pick<6>(y, lane);
     if (kFull) return;  // the record stays in its slot
     const double2* s2 = reinterpret_cast<const double2*>(col);
     double2* d2 = reinterpret_cast<double2*>(const_cast<double*>(sfac) + (long)k * CS);
@@ -405,11 +425,11 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       if (lane + 64 * t < CS / 2) d2[lane + 64 * t] = v2[t];
   };
   // Trailing wave, step k: blocks (i, j), k + 2 <= j <= i <= k + w, minus L_ik L_jk^T.
-  auto trail_step = [&](int sk) __attribute__((always_inline)) {
+  auto trail_step = [&](int k, int sk) __attribute__((always_inline)) {
     const double* col = sring + sk * SS;
 #pragma unroll
     for (int h = 0; h < kTaskRounds; ++h) {
-      if (tk_qj[h] < 0) continue;
+      if (tk_qj[h] < 0 || k + tk_qj[h] >= snload) continue;  // no column past the side
       const int st = sk + tk_qj[h] < RC ? sk + tk_qj[h] : sk + tk_qj[h] - RC;
       double* out = sring + st * SS + tk_o[h];
       double o0[6], o1[6], a0[6], a1[6], B[6][6];
@@ -444,9 +464,48 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     }
   };
   auto side_step = [&](int p, int sk, int skm) __attribute__((always_inline)) {
-    if (role == kTrail) trail_step(sk);
+    if (role == kTrail) trail_step(p, sk);
     else if (role == kFwd) fwd_step(p, sk);
     else if (role == kLoad) load_step(p, skm);
+  };
+
+  // Full mode: every block L_{k,i} (k - w <= i < k) is replaced by G = L_kk^-1 L_{k,i}
+  // before the back substitution (one block per thread; L_kk from this side's record, or
+  // for the bottom side's separator rows from the top's).  Item lists: set 0 = the rows
+  // final after phase A (top rows < m, then bottom rows < nb; done by the idle bottom
+  // waves during the separator phase), set 1 = the separator rows (top rows m .. m + s,
+  // then the bottom side's pseudo rows nb .. nb + s).
+  auto g_item = [&](int set, int e) __attribute__((always_inline)) {
+    const int nt = (set == 0 ? m : sp) * w;
+    const bool eb = e >= nt;
+    const int e2 = eb ? e - nt : e, k = e2 / w + (set == 0 ? 0 : eb ? nb : m), qq = e2 % w + 1, i = k - qq;
+    if (i < 0 || (eb && i >= nb)) return;
+    double* fs = eb ? ringB : ringT;
+    const double* rec = (eb && k >= nb) ? ringT + (long)(F - 1 - k) * CS : fs + (long)k * CS;
+    double L[21], r[6], Bk[6][6];
+#pragma unroll
+    for (int ii = 0; ii < 6; ++ii)
+#pragma unroll
+      for (int c = 0; c <= ii; c += 2) {
+        const double2 v = reinterpret_cast<const double2*>(rec + 6 * ii)[c / 2];
+        L[P6(ii, c)] = v.x;
+        if (c + 1 <= ii) L[P6(ii, c + 1)] = v.y;
+      }
+    ld6g(rec + 36 * R + 6, r);
+    double* blk = fs + (long)i * CS + 36 * qq;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) ld6g(blk + 6 * c, Bk[c]);
+#pragma unroll
+    for (int s2 = 0; s2 < 6; ++s2) {
+      double gv[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) gv[c] = Bk[c][s2];
+      fwd6(L, r, gv);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) Bk[c][s2] = gv[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 6; ++c) st6g(blk + 6 * c, Bk[c]);
   };
 
   if (!prior_fail) {
@@ -495,6 +554,10 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
           } else {
             side_step(p, sk, skm);
           }
+        } else if (kFull) {
+          const int n0 = (m + nb) * w, chunk = (n0 + sp - 1) / sp, t = p - m;
+          const int e1 = min(n0, (t + 1) * chunk);
+          for (int e = t * chunk + 64 * role + lane; e < e1; e += 256) g_item(0, e);
         }
         BST(7);
         skm = sk;
@@ -517,42 +580,11 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // and the factor records.  Loader waves stage the poses meanwhile.
   if (role == kLoad)
     for (int e = tid - 64 * kLoad * 2; e < 12 * A.n_poses; e += 128) pose_l[e] = A.pose_cur[e];
-  // Full mode: every block L_{k,i} (k - w <= i < k) is replaced by G = L_kk^-1 L_{k,i}
-  // first, one block per thread (the records are in LDS); the chain then reads g as is.
+  // Full mode, the rest of the G blocks (rows the separator phase finalised: the top's
+  // separator rows and the bottom side's pseudo rows), then the back substitution.
   if (kFull && !failed) {
-    const int nT = ncolT * w, nAll = (ncolT + ncolB) * w;
-    for (int e = tid; e < nAll; e += kBandThreads) {
-      const bool eb = e >= nT;
-      const int e2 = eb ? e - nT : e, k = e2 / w, qq = e2 - k * w + 1, i = k - qq;
-      if (i < 0 || (eb && i >= nb)) continue;
-      double* fs = eb ? ringB : ringT;
-      // L_kk: this side's record, or (the bottom side's separator rows) the top's
-      const double* rec = (eb && k >= nb) ? ringT + (long)(F - 1 - k) * CS : fs + (long)k * CS;
-      double L[21], r[6], Bk[6][6];
-#pragma unroll
-      for (int ii = 0; ii < 6; ++ii)
-#pragma unroll
-        for (int c = 0; c <= ii; c += 2) {
-          const double2 v = reinterpret_cast<const double2*>(rec + 6 * ii)[c / 2];
-          L[P6(ii, c)] = v.x;
-          if (c + 1 <= ii) L[P6(ii, c + 1)] = v.y;
-        }
-      ld6g(rec + 36 * R + 6, r);
-      double* blk = fs + (long)i * CS + 36 * qq;
-#pragma unroll
-      for (int c = 0; c < 6; ++c) ld6g(blk + 6 * c, Bk[c]);
-#pragma unroll
-      for (int s2 = 0; s2 < 6; ++s2) {
-        double gv[6];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) gv[c] = Bk[c][s2];
-        fwd6(L, r, gv);
-#pragma unroll
-        for (int c = 0; c < 6; ++c) Bk[c][s2] = gv[c];
-      }
-#pragma unroll
-      for (int c = 0; c < 6; ++c) st6g(blk + 6 * c, Bk[c]);
-    }
+    const int nR = sp > 0 ? 2 * sp * w : m * w;  // one-sided windows: every top row here
+    for (int e = tid; e < nR; e += kBandThreads) g_item(sp > 0 ? 1 : 0, e);
     __syncthreads();
   }
   BST(16);
