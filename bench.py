@@ -51,10 +51,28 @@ def ba_kernel_bytes(kind: str, n_poses: int, n_points: int, n_obs: int, n_free: 
     return 0.0
 
 
+def host_cores():
+    """Host cores this process may use: its CPU affinity, capped by a cgroup CPU quota
+    (on the GPU box the job's share of a larger machine).  Returns (threads, note)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    threads = min(n, quota) if quota else n
+    note = f"{threads} threads = every core this job may use (affinity {n}"
+    note += f", cgroup quota {quota}" if quota else ""
+    note += f"; os.cpu_count() {os.cpu_count()})"
+    return threads, note
+
+
 def cpu_baseline_ba(p, lam: float, budget_s: float = 3.0):
     from oracle import cref
 
-    threads = min(16, os.cpu_count() or 1)
+    threads, note = host_cores()
     R = cref.BAProblemRef(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, lam)
     poses, pts = p.poses_cw, p.points
     ok, poses, pts, *_ = R.step(poses, pts, threads, want_system=False)  # warm-up
@@ -67,7 +85,7 @@ def cpu_baseline_ba(p, lam: float, budget_s: float = 3.0):
             break
     return {"value": n / dt, "unit": "GN-iters/s", "cores": threads, "kind": "port",
             "sample": f"oracle/ba_ref.c (OpenMP, dense Schur + dense Cholesky) on the same cfg3 "
-                      f"window: {n} GN iterations in {dt:.2f} s on {threads} host threads"}
+                      f"window: {n} GN iterations in {dt:.2f} s; {note}"}
 
 
 def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: int = 3, traffic_all=None):
@@ -123,15 +141,14 @@ def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: 
     # CPU baseline: C oracle on a bounded sample of query rows
     from oracle import cref
 
-    threads = min(16, os.cpu_count() or 1)
+    threads, note = host_cores()
     rows = 1000
     t0 = time.perf_counter()
     cref.knn2(pairs[0][0][:rows], pairs[0][1], threads)
     cdt = time.perf_counter() - t0
     res["cpu_baseline"] = {"value": rows * n / cdt / 1e6, "unit": "Mpairs/s", "cores": threads,
                            "kind": "port",
-                           "sample": f"oracle/match_ref.c knn2 on {rows} x {n} x 128 of frame pair 0, "
-                                     f"{threads} host threads"}
+                           "sample": f"oracle/match_ref.c knn2 on {rows} x {n} x 128 of frame pair 0; {note}"}
     return res
 
 
@@ -161,7 +178,7 @@ def bench_matcher_float(ctx, batch: int = 16, n: int = 2048, dim: int = 256, cal
     matcher.synchronize(ctx)
     prof = _lib.profile_read(ctx)
     _lib.profile_enable(ctx, False)
-    threads = min(16, os.cpu_count() or 1)
+    threads, note = host_cores()
     ref = match_ref.match_c(pairs[0][0], pairs[0][1], nthreads=threads)
     got = out.numpy()[0]
     kept = np.nonzero(got >= 0)[0]
@@ -190,8 +207,7 @@ def bench_matcher_float(ctx, batch: int = 16, n: int = 2048, dim: int = 256, cal
     match_ref.knn2_c(pairs[0][0][:rows], pairs[0][1], threads)
     cdt = time.perf_counter() - t0
     res["cpu_baseline"] = {"value": rows * n / cdt / 1e6, "unit": "Mpairs/s", "cores": threads, "kind": "port",
-                           "sample": f"oracle/match_ref.c knn2 on {rows} x {n} x {dim} of frame pair 0, "
-                                     f"{threads} host threads"}
+                           "sample": f"oracle/match_ref.c knn2 on {rows} x {n} x {dim} of frame pair 0; {note}"}
     return res
 
 

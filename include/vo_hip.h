@@ -120,27 +120,32 @@ typedef struct {
 
 /* Uploads the observation structure and builds the static execution plan
  * (landmark chunks, per-workgroup camera-pair windows, reduced-system profile).
- * Replaces any previous problem in this context. */
-int vo_ba_setup(vo_ctx* ctx, const vo_ba_problem* prob);
+ * Replaces any previous problem in this context.  *session_out receives the id of
+ * this problem (unique in the process); every later vo_ba_* call on it passes that
+ * id and fails with VO_ERR_STATE once another vo_ba_setup on the context has replaced
+ * the problem (whose sizes the caller's buffers no longer match).  With a
+ * communicator (vo_comm_init) every rank reaches the same verdict: a shard that
+ * fails its checks on one rank is VO_ERR_ARG on all ranks. */
+int vo_ba_setup(vo_ctx* ctx, const vo_ba_problem* prob, uint64_t* session_out);
 /* poses: (n_poses, 12) float64 = R_cw row-major (9) then t_cw (3);
- * points: (n_points, 3) float64. */
-int vo_ba_set_state(vo_ctx* ctx, const double* poses, const double* points);
-int vo_ba_get_state(vo_ctx* ctx, double* poses, double* points);
+ * points: (n_points, 3) float64 -- the sizes of the session's problem. */
+int vo_ba_set_state(vo_ctx* ctx, uint64_t session, const double* poses, const double* points);
+int vo_ba_get_state(vo_ctx* ctx, uint64_t session, double* poses, double* points);
 /* Runs `iters` pure Gauss-Newton iterations (every step accepted) on the
  * device-resident state.  cost_out (iters+1 doubles, may be NULL): sum of
  * squared residuals before each iteration and after the last one.
  * Returns VO_ERR_NOT_SPD (state left at the last good iterate) if the reduced
  * camera system is not positive definite. */
-int vo_ba_run(vo_ctx* ctx, int iters, double* cost_out);
+int vo_ba_run(vo_ctx* ctx, uint64_t session, int iters, double* cost_out);
 /* Same, enqueued on the context stream with no host synchronisation and no
  * cost read-back (for timing).  Errors surface at the next synchronous call. */
-int vo_ba_run_async(vo_ctx* ctx, int iters);
+int vo_ba_run_async(vo_ctx* ctx, uint64_t session, int iters);
 /* One GN iteration with the intermediate quantities exported (parity tests):
  * S_out: dense (6F, 6F) float64 reduced camera matrix with F = n_poses-n_fixed
  * (may be NULL), b_out: (6F), dc_out: (6F) pose update (may be NULL),
  * cost_out: 1 double.  The state is advanced by the step. */
-int vo_ba_gn_step(vo_ctx* ctx, double* S_out, double* b_out, double* dc_out,
-                     double* cost_out);
+int vo_ba_gn_step(vo_ctx* ctx, uint64_t session, double* S_out, double* b_out, double* dc_out,
+                  double* cost_out);
 /* One-call convenience: setup + set_state + run + get_state. */
 int vo_ba_solve(vo_ctx* ctx, const vo_ba_problem* prob, double* poses, double* points,
                 int iters, double* cost_out);

@@ -10,6 +10,7 @@ import pytest
 
 from oracle import ba_ref, cref
 from visualodometry_amd import _lib
+from visualodometry_amd._lib import VoError
 from visualodometry_amd.ba import BASession, BAWindow, SlidingWindowBA
 from visualodometry_amd.synthetic import make_ba_config, make_ba_problem
 
@@ -251,3 +252,25 @@ def test_non_monotone_profile_band_solver(ctx):
     p = _add_far_landmark(make_ba_problem(12, 500, 43, max_track=3), [2, 11])
     s = _step_vs_oracle(ctx, p)
     assert s.plan_stats()["band_solver"] == 1
+
+
+def test_two_sessions_on_one_context(ctx):
+    """A second setup on the same context replaces the first problem: the first
+    session's calls fail with VO_ERR_STATE instead of reading the other problem's sizes
+    (ADVICE r1)."""
+    p2 = make_ba_config("cfg2")
+    small = make_ba_problem(6, 80, 5)
+    s1 = _session(small, ctx)
+    s2 = _session(p2, ctx)
+    for call in (lambda: s1.get_state(), lambda: s1.run(1), lambda: s1.gn_step(),
+                 lambda: s1.set_state(small.poses_cw, small.points), lambda: s1.run_async(1)):
+        with pytest.raises(VoError) as e:
+            call()
+        assert e.value.code == _lib.VO_ERR_STATE
+    rc, costs = s2.run(2)  # the current session is unaffected
+    assert rc == _lib.VO_OK and np.all(np.isfinite(costs))
+    s1b = _session(small, ctx)  # a fresh setup of the first problem works again
+    rc, _ = s1b.run(1)
+    assert rc == _lib.VO_OK
+    with pytest.raises(VoError):
+        s2.get_state()

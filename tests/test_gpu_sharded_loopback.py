@@ -87,3 +87,33 @@ def test_loopback_one_rank_is_neutral():
     np.testing.assert_array_equal(res[0][3], c0)
     np.testing.assert_array_equal(res[0][4], P0)
     np.testing.assert_array_equal(res[0][5], X0)
+
+
+def test_one_invalid_shard_fails_every_rank():
+    """Only rank 1's shard is invalid (an observation of a camera outside the window):
+    every rank's vo_ba_setup fails with VO_ERR_ARG -- none is left waiting in a
+    collective."""
+    p = make_ba_config("cfg2")
+    nranks = 2
+    codes = [None] * nranks
+
+    def worker(r):
+        ctx = _lib.Context(0)
+        _lib.comm_init_loopback(ctx, nranks, r, b"vo-loopback-invalid")
+        (_p0, _p1), ptr, cam, uv, _pts = shard(p.point_ptr, p.obs_cam, p.obs_uv, p.points, nranks, r)
+        cam = cam.copy()
+        if r == 1:
+            cam[0] = p.n_poses + 3
+        try:
+            BASession(p.K, ptr, cam, uv, p.n_poses, p.n_fixed, 1.0, ctx)
+            codes[r] = 0
+        except _lib.VoError as e:
+            codes[r] = e.code
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a rank is stuck in a collective"
+    assert codes == [_lib.VO_ERR_ARG] * nranks

@@ -72,12 +72,12 @@ SIGNATURES = {
     "vo_match_knn2_ratio": (_I, [_P, _PF, _I, _PF, _I, _I, _D, _PI32, _PI32]),
     "vo_match_knn2": (_I, [_P, _PF, _I, _PF, _I, _I, _PI32, _PF]),
     "vo_match_batch_async": (_I, [_P, _P, _P, _I, _I, _I, _I, _D, _P]),
-    "vo_ba_setup": (_I, [_P, C.POINTER(BAProblemC)]),
-    "vo_ba_set_state": (_I, [_P, _PD, _PD]),
-    "vo_ba_get_state": (_I, [_P, _PD, _PD]),
-    "vo_ba_run": (_I, [_P, _I, _PD]),
-    "vo_ba_run_async": (_I, [_P, _I]),
-    "vo_ba_gn_step": (_I, [_P, _PD, _PD, _PD, _PD]),
+    "vo_ba_setup": (_I, [_P, C.POINTER(BAProblemC), C.POINTER(C.c_uint64)]),
+    "vo_ba_set_state": (_I, [_P, C.c_uint64, _PD, _PD]),
+    "vo_ba_get_state": (_I, [_P, C.c_uint64, _PD, _PD]),
+    "vo_ba_run": (_I, [_P, C.c_uint64, _I, _PD]),
+    "vo_ba_run_async": (_I, [_P, C.c_uint64, _I]),
+    "vo_ba_gn_step": (_I, [_P, C.c_uint64, _PD, _PD, _PD, _PD]),
     "vo_ba_solve": (_I, [_P, C.POINTER(BAProblemC), _PD, _PD, _I, _PD]),
     "vo_ba_plan_stats": (_I, [_P, _PI64, _I]),
     "vo_ba_debug_stamps": (_I, [_P, C.POINTER(C.c_uint64), _I]),

@@ -139,33 +139,39 @@ class BASession:
         prob = _problem_struct(K, self.point_ptr, self.obs_cam, self.obs_uv, self.n_poses,
                                self.n_fixed, lam)
         self._prob = prob
-        check(self.ctx.lib.vo_ba_setup(self.ctx.handle, C.byref(prob)), "vo_ba_setup")
+        sid = C.c_uint64(0)
+        check(self.ctx.lib.vo_ba_setup(self.ctx.handle, C.byref(prob), C.byref(sid)), "vo_ba_setup")
+        # the problem's id on this context: a later setup on the same context (another
+        # session) makes every call below fail with VO_ERR_STATE instead of misreading
+        self.session = int(sid.value)
 
     def set_state(self, poses_cw: np.ndarray, points: np.ndarray) -> None:
         rt = np.ascontiguousarray(poses_to_rt(poses_cw))
         pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
         if rt.shape[0] != self.n_poses or pts.shape[0] != self.n_points:
             raise ValueError("state shape does not match the problem")
-        check(self.ctx.lib.vo_ba_set_state(self.ctx.handle, ptr(rt, C.c_double), ptr(pts, C.c_double)),
+        check(self.ctx.lib.vo_ba_set_state(self.ctx.handle, self.session, ptr(rt, C.c_double),
+                                           ptr(pts, C.c_double)),
               "vo_ba_set_state")
 
     def get_state(self):
         rt = np.empty((self.n_poses, 12))
         pts = np.empty((self.n_points, 3))
-        check(self.ctx.lib.vo_ba_get_state(self.ctx.handle, ptr(rt, C.c_double), ptr(pts, C.c_double)),
+        check(self.ctx.lib.vo_ba_get_state(self.ctx.handle, self.session, ptr(rt, C.c_double),
+                                           ptr(pts, C.c_double)),
               "vo_ba_get_state")
         return rt_to_poses(rt), pts
 
     def run(self, iters: int):
         """``iters`` GN iterations; returns (status_code, costs[iters+1])."""
         costs = np.empty(iters + 1)
-        rc = self.ctx.lib.vo_ba_run(self.ctx.handle, int(iters), ptr(costs, C.c_double))
+        rc = self.ctx.lib.vo_ba_run(self.ctx.handle, self.session, int(iters), ptr(costs, C.c_double))
         if rc not in (_lib.VO_OK, _lib.VO_ERR_NOT_SPD):
             check(rc, "vo_ba_run")
         return rc, costs
 
     def run_async(self, iters: int) -> None:
-        check(self.ctx.lib.vo_ba_run_async(self.ctx.handle, int(iters)), "vo_ba_run_async")
+        check(self.ctx.lib.vo_ba_run_async(self.ctx.handle, self.session, int(iters)), "vo_ba_run_async")
 
     def synchronize(self) -> None:
         check(self.ctx.lib.vo_synchronize(self.ctx.handle), "vo_synchronize")
@@ -177,7 +183,7 @@ class BASession:
         b = np.empty(6 * F)
         dc = np.empty(6 * F)
         cost = np.empty(1)
-        rc = self.ctx.lib.vo_ba_gn_step(self.ctx.handle, ptr(S, C.c_double), ptr(b, C.c_double),
+        rc = self.ctx.lib.vo_ba_gn_step(self.ctx.handle, self.session, ptr(S, C.c_double), ptr(b, C.c_double),
                                            ptr(dc, C.c_double), ptr(cost, C.c_double))
         if rc not in (_lib.VO_OK, _lib.VO_ERR_NOT_SPD):
             check(rc, "vo_ba_gn_step")

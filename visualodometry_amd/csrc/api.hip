@@ -66,7 +66,8 @@ Profiler::~Profiler() {
 }
 
 // ba.hip
-void ba_setup(vo_ctx*, const vo_ba_problem*);
+uint64_t ba_setup(vo_ctx*, const vo_ba_problem*);
+void ba_check_session(vo_ctx*, uint64_t);
 void ba_set_state(vo_ctx*, const double*, const double*);
 void ba_get_state(vo_ctx*, double*, double*);
 int ba_run(vo_ctx*, int, double*, bool);
@@ -484,49 +485,57 @@ int vo_match_batch_async(vo_ctx* ctx, const float* d_des0, const float* d_des1, 
   });
 }
 
-int vo_ba_setup(vo_ctx* ctx, const vo_ba_problem* prob) {
+int vo_ba_setup(vo_ctx* ctx, const vo_ba_problem* prob, uint64_t* session_out) {
   return guarded([&] {
     vo::bind(ctx);
-    vo::ba_setup(ctx, prob);
+    VO_REQUIRE(session_out, VO_ERR_ARG, "vo_ba_setup: null session_out");
+    *session_out = 0;
+    *session_out = vo::ba_setup(ctx, prob);
   });
 }
 
-int vo_ba_set_state(vo_ctx* ctx, const double* poses, const double* points) {
+int vo_ba_set_state(vo_ctx* ctx, uint64_t session, const double* poses, const double* points) {
   return guarded([&] {
     vo::bind(ctx);
     VO_REQUIRE(poses && points, VO_ERR_ARG, "vo_ba_set_state: null arrays");
+    vo::ba_check_session(ctx, session);
     vo::ba_set_state(ctx, poses, points);
   });
 }
 
-int vo_ba_get_state(vo_ctx* ctx, double* poses, double* points) {
+int vo_ba_get_state(vo_ctx* ctx, uint64_t session, double* poses, double* points) {
   return guarded([&] {
     vo::bind(ctx);
     VO_REQUIRE(poses && points, VO_ERR_ARG, "vo_ba_get_state: null arrays");
+    vo::ba_check_session(ctx, session);
     vo::ba_get_state(ctx, poses, points);
   });
 }
 
-int vo_ba_run(vo_ctx* ctx, int iters, double* cost_out) {
+int vo_ba_run(vo_ctx* ctx, uint64_t session, int iters, double* cost_out) {
   int rc = VO_OK;
   int g = guarded([&] {
     vo::bind(ctx);
+    vo::ba_check_session(ctx, session);
     rc = vo::ba_run(ctx, iters, cost_out, true);
   });
   return g != VO_OK ? g : rc;
 }
 
-int vo_ba_run_async(vo_ctx* ctx, int iters) {
+int vo_ba_run_async(vo_ctx* ctx, uint64_t session, int iters) {
   return guarded([&] {
     vo::bind(ctx);
+    vo::ba_check_session(ctx, session);
     vo::ba_run(ctx, iters, nullptr, false);
   });
 }
 
-int vo_ba_gn_step(vo_ctx* ctx, double* S_out, double* b_out, double* dc_out, double* cost_out) {
+int vo_ba_gn_step(vo_ctx* ctx, uint64_t session, double* S_out, double* b_out, double* dc_out,
+                  double* cost_out) {
   int rc = VO_OK;
   int g = guarded([&] {
     vo::bind(ctx);
+    vo::ba_check_session(ctx, session);
     rc = vo::ba_gn_step(ctx, S_out, b_out, dc_out, cost_out);
   });
   return g != VO_OK ? g : rc;
@@ -534,13 +543,14 @@ int vo_ba_gn_step(vo_ctx* ctx, double* S_out, double* b_out, double* dc_out, dou
 
 int vo_ba_solve(vo_ctx* ctx, const vo_ba_problem* prob, double* poses, double* points, int iters,
                 double* cost_out) {
-  int rc = vo_ba_setup(ctx, prob);
+  uint64_t s = 0;
+  int rc = vo_ba_setup(ctx, prob, &s);
   if (rc) return rc;
-  rc = vo_ba_set_state(ctx, poses, points);
+  rc = vo_ba_set_state(ctx, s, poses, points);
   if (rc) return rc;
-  const int run_rc = vo_ba_run(ctx, iters, cost_out);
+  const int run_rc = vo_ba_run(ctx, s, iters, cost_out);
   if (run_rc && run_rc != VO_ERR_NOT_SPD) return run_rc;
-  rc = vo_ba_get_state(ctx, poses, points);
+  rc = vo_ba_get_state(ctx, s, poses, points);
   return rc ? rc : run_rc;
 }
 

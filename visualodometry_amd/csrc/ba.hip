@@ -31,6 +31,7 @@
 #include <cmath>
 #include <cstring>
 #include <type_traits>
+#include <atomic>
 #include <vector>
 
 #include <condition_variable>
@@ -1231,26 +1232,45 @@ void upload(DevBuf& buf, const std::vector<T>& v, hipStream_t st) {
 
 constexpr size_t kSolveLdsMax = 160 * 1024 - 64;  // gfx950: 160 KiB per workgroup (+ s_fail)
 
+std::atomic<uint64_t> g_ba_sessions{0};  // session ids, unique in the process
+
 }  // namespace
 
 class BAEngine {
  public:
   explicit BAEngine(vo_ctx* ctx) : ctx_(ctx) {}
 
-  void setup(const vo_ba_problem* prob) {
-    VO_REQUIRE(prob, VO_ERR_ARG, "vo_ba_setup: null problem");
-    VO_REQUIRE(prob->n_poses >= 1 && prob->n_points >= 0 && prob->n_obs >= 0, VO_ERR_ARG,
-               "vo_ba_setup: bad sizes");
-    VO_REQUIRE(prob->lambda >= 0.0, VO_ERR_ARG, "vo_ba_setup: lambda must be >= 0");
-    VO_REQUIRE((prob->n_points == 0 || prob->point_ptr) && (prob->n_obs == 0 || (prob->obs_cam && prob->obs_uv)),
-               VO_ERR_ARG, "vo_ba_setup: null arrays");
-    const int target = segments_target(ctx_->num_cus);
-    std::vector<int32_t> zero_ptr(1, 0);
-    const int32_t* pp = prob->n_points ? prob->point_ptr : zero_ptr.data();
-    if (prob->n_points == 0)
-      VO_REQUIRE(prob->n_obs == 0, VO_ERR_ARG, "vo_ba_setup: observations without points");
-    std::string err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs,
-                                 prob->n_fixed, pp, prob->obs_cam, prob->obs_uv, target);
+  // Returns the new session id.  Every argument and plan check completes before any
+  // collective: with a communicator, all ranks then agree (min all-reduce of [ok, F, -F])
+  // and fail together, so one rank's bad shard is an error everywhere, not a hang.
+  uint64_t setup(const vo_ba_problem* prob) {
+    have_problem_ = false;
+    have_state_ = false;
+    std::string err;
+    if (!prob) err = "null problem";
+    else if (!(prob->n_poses >= 1 && prob->n_points >= 0 && prob->n_obs >= 0)) err = "bad sizes";
+    else if (!(prob->lambda >= 0.0)) err = "lambda must be >= 0";
+    else if (!((prob->n_points == 0 || prob->point_ptr) && (prob->n_obs == 0 || (prob->obs_cam && prob->obs_uv))))
+      err = "null arrays";
+    else if (prob->n_points == 0 && prob->n_obs != 0) err = "observations without points";
+    if (err.empty()) {
+      const int target = segments_target(ctx_->num_cus);
+      std::vector<int32_t> zero_ptr(1, 0);
+      const int32_t* pp = prob->n_points ? prob->point_ptr : zero_ptr.data();
+      err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
+                       prob->obs_uv, target);
+    }
+    if (ctx_->comm && ctx_->comm->nranks > 1) {
+      const int32_t F = err.empty() ? plan_.n_free : 0;
+      std::vector<int32_t> agree = {err.empty() ? 1 : 0, F, -F};
+      DevBuf tmp;
+      upload(tmp, agree, ctx_->stream);
+      ctx_->comm->allreduce(tmp.as<int32_t>(), agree.size(), true, ctx_->stream);
+      VO_HIP_CHECK(hipMemcpyAsync(agree.data(), tmp.ptr, agree.size() * 4, hipMemcpyDeviceToHost, ctx_->stream));
+      VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
+      if (err.empty() && agree[0] == 0) err = "another rank's shard failed its checks";
+      if (err.empty() && agree[1] != -agree[2]) err = "ranks disagree on the number of free poses";
+    }
     VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_setup: %s", err.c_str());
     std::vector<int32_t> first = local_profile_first(plan_);
     if (ctx_->comm && ctx_->comm->nranks > 1 && !first.empty()) {
@@ -1389,6 +1409,16 @@ class BAEngine {
     have_state_ = false;
     pending_ = false;
     cur_ = 0;
+    session_ = ++g_ba_sessions;
+    return session_;
+  }
+
+  // The caller's session must be the engine's current problem (VO_ERR_STATE otherwise):
+  // a later vo_ba_setup on the same context replaces it, and its sizes with it.
+  void check_session(uint64_t s) const {
+    VO_REQUIRE(have_problem_ && s == session_, VO_ERR_STATE,
+               "BA session %llu is not this context's current problem (%llu): another vo_ba_setup replaced it",
+               (unsigned long long)s, (unsigned long long)session_);
   }
 
   void set_state(const double* poses, const double* points) {
@@ -1758,6 +1788,7 @@ class BAEngine {
   BAPlan plan_;
   vo_ba_problem prob_{};
   bool have_problem_ = false, have_state_ = false, pending_ = false, solve_lds_ = false;
+  uint64_t session_ = 0;
   int cur_ = 0;
   size_t sys_len_ = 0, solve_lds_size_ = 0;
   SolveLds solve_layout_{};
@@ -1817,7 +1848,8 @@ BAEngine* ba_engine(vo_ctx* ctx) {
   if (!ctx->ba) ctx->ba.reset(new BAEngine(ctx));
   return ctx->ba.get();
 }
-void ba_setup(vo_ctx* ctx, const vo_ba_problem* p) { ba_engine(ctx)->setup(p); }
+uint64_t ba_setup(vo_ctx* ctx, const vo_ba_problem* p) { return ba_engine(ctx)->setup(p); }
+void ba_check_session(vo_ctx* ctx, uint64_t s) { ba_engine(ctx)->check_session(s); }
 void ba_set_state(vo_ctx* ctx, const double* poses, const double* pts) {
   ba_engine(ctx)->set_state(poses, pts);
 }

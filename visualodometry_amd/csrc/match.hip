@@ -22,6 +22,10 @@
 // chain sum((a_k - b_k)^2) in fp32 and keys are (sqrtf(d2), j) directly.
 #include "vo_ctx.h"
 
+#ifndef VO_MATCH_WGS_PER_CU
+#define VO_MATCH_WGS_PER_CU 2
+#endif
+
 namespace vo {
 namespace {
 
@@ -577,12 +581,10 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
   const int n0_pad = ceil_div(n0, kRowsPerWG) * kRowsPerWG;
   const int n1_pad = ceil_div(std::max(n1, 1), 16) * 16;
 
-  // split the train columns so the grid fills the chip (w | 4096, w >= 64)
+  // split the train columns so the grid fills the chip (w | 4096, w >= 64); the split
+  // count does not change any result (splits merge on exact (d^2, j) keys)
   const int row_wgs = n0_pad / kRowsPerWG;
-  static const int wgs_per_cu = [] {
-    const char* e = getenv("VO_MATCH_WGS_PER_CU");
-    return e ? std::max(1, atoi(e)) : 2;
-  }();
+  constexpr int wgs_per_cu = VO_MATCH_WGS_PER_CU;  // tuning builds: EXTRA=-DVO_MATCH_WGS_PER_CU=n
   const int want = std::max(1, ceil_div(wgs_per_cu * ctx->num_cus, (int64_t)row_wgs * batch));
   int w = pow2_floor(std::max(1, n1_pad / want));
   w = std::max(256, std::min(4096, w));
