@@ -139,3 +139,26 @@ def test_ate_is_similarity_invariant():
 def test_trajectory_xz_layout():
     tr = [np.array([1.0, 2.0, 3.0]), np.array([4.0, 5.0, 6.0])]  # vo.trajectory entries
     np.testing.assert_array_equal(trajectory_xz(tr), [[1.0, 3.0], [4.0, 6.0]])  # GT cols 3, 11
+
+
+def test_items_values_keys_vectorised_equal_dict():
+    """items()/values()/keys() come from one vectorised pass and equal the
+    dict they replace, in id order, with float32 coordinates."""
+    import time
+
+    rng = np.random.default_rng(3)
+    store, ref = MapStore(), {}
+    for pid in range(25000):
+        x = rng.normal(size=3).astype(np.float32)
+        store[pid] = x
+        ref[pid] = x
+    store.prune_below(5000)
+    for pid in range(5000):
+        del ref[pid]
+    assert store.keys() == list(ref.keys())
+    for (k, v), (rk, rv) in zip(store.items(), ref.items()):
+        assert k == rk and np.array_equal(v, rv) and v.dtype == np.float32
+    assert all(np.array_equal(a, b) for a, b in zip(store.values(), ref.values()))
+    t0 = time.perf_counter()
+    n = sum(1 for _ in store.items())
+    assert n == 20000 and time.perf_counter() - t0 < 0.5

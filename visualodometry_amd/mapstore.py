@@ -83,6 +83,18 @@ class MapStore(MutableMapping):
     def __len__(self) -> int:
         return self._n
 
+    # one vectorised pass instead of MutableMapping's per-key __getitem__ (the reference's
+    # per-frame ``for pid, pt in self.map_points.items()``, vo.py:349, over up to 20k points)
+    def keys(self):
+        return self.arrays()[0].tolist()
+
+    def values(self):
+        return list(self.arrays()[1])
+
+    def items(self):
+        ids, xyz = self.arrays()
+        return list(zip(ids.tolist(), xyz))
+
     # --- vectorised access
     def contains(self, ids) -> np.ndarray:
         ids = np.asarray(ids, dtype=np.int64)
