@@ -207,7 +207,8 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
 #if VO_BA_STAMPS
   unsigned long long st_acc[kBandStamps] = {}, st_t = __builtin_amdgcn_s_memtime();
 #endif
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // wave (so role and side) is wave-uniform: readfirstlane lets the compiler branch on SGPRs
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   // CS: doubles per column (K2 layout, factor record; full mode: SS == CS); SS per slot (ring mode: whole 1 KiB
   // pieces), RC slots per side (band_lds_layout)
   const int F = A.F, w = A.w, R = w + 1, CS = 36 * R + 12, CSP = (CS + 127) / 128 * 128;
