@@ -102,6 +102,19 @@ int vo_match_knn2(vo_ctx* ctx, const float* des0, int n0, const float* des1, int
 int vo_match_batch_async(vo_ctx* ctx, const float* d_des0, const float* d_des1,
                          int batch, int n0, int n1, int dim, double ratio,
                          int32_t* d_best);
+/* Descriptor-kind hint for this context's later matcher calls (results never depend on
+ * it; the device checks every call's values either way):
+ *   VO_DESC_AUTO (0, default) launches both paths' kernels; a call runs the one its
+ *     values need (a device-side flag) -- SIFT integers on the int8 MFMA sweep, other
+ *     floats on the bf16 MFMA shortlist + exact re-rank;
+ *   VO_DESC_SIFT (1): OpenCV SIFT integers expected (FeatureFrontend with the SIFT
+ *     extractor, frontend.py:25-34): the float shortlist is not launched, and a call
+ *     whose values are not 0..255 integers takes the exact fp32 sweep instead;
+ *   VO_DESC_FLOAT (2): SuperPoint-like floats expected (same kernels as AUTO). */
+#define VO_DESC_AUTO 0
+#define VO_DESC_SIFT 1
+#define VO_DESC_FLOAT 2
+int vo_match_hint(vo_ctx* ctx, int kind);
 
 /* ---- sliding-window bundle adjustment ------------------------------------ */
 typedef struct {

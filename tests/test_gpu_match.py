@@ -64,6 +64,41 @@ def test_superpoint_2048(ctx):
     _check_knn2(d0, d1, ctx, oracle="c")
 
 
+@pytest.mark.parametrize("dim", [32, 100, 192, 256])
+def test_float_shortlist_dims(ctx, dim):
+    """bf16 MFMA shortlist + exact re-rank (match_bf16.hip) at every K padding."""
+    d0, d1 = superpoint_like_pair(333, 517, 30 + dim, dim=dim)
+    _check_knn2(d0, d1, ctx, oracle="c")
+
+
+def test_float_shortlist_unnormalised(ctx):
+    """Non-integer descriptors with large norms: the candidate bound scales with them."""
+    rng = np.random.default_rng(31)
+    d0 = (rng.standard_normal((400, 128)) * 50 + 100).astype(np.float32)
+    d1 = np.concatenate([d0[:200] + rng.standard_normal((200, 128)).astype(np.float32),
+                         (rng.standard_normal((300, 128)) * 50 + 100).astype(np.float32)])
+    _check_knn2(d0, d1, ctx, oracle="c")
+
+
+def test_float_shortlist_overflow_rescans_exactly(ctx):
+    """Hundreds of train rows within the bf16 error of each other: more than 32
+    candidates per query, so those rows take the exact full re-scan."""
+    rng = np.random.default_rng(32)
+    base = rng.standard_normal((1, 256)).astype(np.float32)
+    d1 = np.concatenate([base + 1e-4 * rng.standard_normal((300, 256)).astype(np.float32),
+                         rng.standard_normal((200, 256)).astype(np.float32)])
+    d0 = np.concatenate([base + 1e-4 * rng.standard_normal((20, 256)).astype(np.float32),
+                         rng.standard_normal((50, 256)).astype(np.float32)])
+    _check_knn2(d0, d1, ctx, oracle="c")
+
+
+def test_float_shortlist_exact_ties(ctx):
+    """Duplicate float train rows: equal exact distances keep the lower train index."""
+    d0, d1 = superpoint_like_pair(200, 100, 33)
+    d1 = np.concatenate([d1, d1, d1[::-1]])
+    _check_knn2(d0, d1, ctx, oracle="c")
+
+
 def test_ties_keep_lower_train_index(ctx):
     rng = np.random.default_rng(0)
     base = rng.integers(0, 256, (8, 128)).astype(np.float32)

@@ -72,6 +72,7 @@ SIGNATURES = {
     "vo_match_knn2_ratio": (_I, [_P, _PF, _I, _PF, _I, _I, _D, _PI32, _PI32]),
     "vo_match_knn2": (_I, [_P, _PF, _I, _PF, _I, _I, _PI32, _PF]),
     "vo_match_batch_async": (_I, [_P, _P, _P, _I, _I, _I, _I, _D, _P]),
+    "vo_match_hint": (_I, [_P, _I]),
     "vo_ba_setup": (_I, [_P, C.POINTER(BAProblemC), C.POINTER(C.c_uint64)]),
     "vo_ba_set_state": (_I, [_P, C.c_uint64, _PD, _PD]),
     "vo_ba_get_state": (_I, [_P, C.c_uint64, _PD, _PD]),

@@ -485,6 +485,15 @@ int vo_match_batch_async(vo_ctx* ctx, const float* d_des0, const float* d_des1, 
   });
 }
 
+int vo_match_hint(vo_ctx* ctx, int kind) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(kind == VO_DESC_AUTO || kind == VO_DESC_SIFT || kind == VO_DESC_FLOAT, VO_ERR_ARG,
+               "vo_match_hint: unknown kind %d", kind);
+    ctx->match.kind_hint = kind;
+  });
+}
+
 int vo_ba_setup(vo_ctx* ctx, const vo_ba_problem* prob, uint64_t* session_out) {
   return guarded([&] {
     vo::bind(ctx);

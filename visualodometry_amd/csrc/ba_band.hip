@@ -203,7 +203,6 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int s_fail;
   __shared__ __attribute__((aligned(16))) double s_zero[40];   // full mode's zero block
-  __shared__ __attribute__((aligned(16))) double s_dummy[64];  // full mode: masked stores
 #if VO_BA_STAMPS
   unsigned long long st_acc[kBandStamps] = {}, st_t = __builtin_amdgcn_s_memtime();
 #endif

@@ -20,7 +20,7 @@
 //
 // Float path (any other values, e.g. SuperPoint): d2 is the k-ordered fmaf
 // chain sum((a_k - b_k)^2) in fp32 and keys are (sqrtf(d2), j) directly.
-#include "vo_ctx.h"
+#include "match_short.h"
 
 #ifndef VO_MATCH_WGS_PER_CU
 #define VO_MATCH_WGS_PER_CU 2
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void pack_kernel(PackSide sa, PackSide sb, int
   const float* src = P.des + b * P.in_bstride + (long)row * dim;
   int8_t* dst = P.q8 + b * P.q_bstride + (long)row * Dp;
   int acc = 0;
-  bool bad = false;
+  bool bad = false, nonfinite = false;
   for (int e = sub * 4; e < Dp; e += 64) {
     float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     if (live_row) {
@@ -137,6 +137,7 @@ __global__ __launch_bounds__(256) void pack_kernel(PackSide sa, PackSide sb, int
       const bool live = live_row && e + u < dim;
       const bool ok = (v[u] == rintf(v[u])) && v[u] >= 0.0f && v[u] <= 255.0f;
       bad |= live && !ok;
+      nonfinite |= live && !isfinite(v[u]);
       q[u] = live && ok ? (int)v[u] - 128 : 0;
       acc += q[u] * q[u];
     }
@@ -146,7 +147,8 @@ __global__ __launch_bounds__(256) void pack_kernel(PackSide sa, PackSide sb, int
   }
 #pragma unroll
   for (int m = 1; m < 16; m <<= 1) acc += __shfl_xor(acc, m, 64);
-  if (__any(bad) && (threadIdx.x & 63) == 0) *flag = gen;  // every writer stores the same value
+  if (__any(bad) && (threadIdx.x & 63) == 0) flag[0] = gen;  // every writer stores the same value
+  if (__any(nonfinite) && (threadIdx.x & 63) == 0) flag[1] = gen;  // the exact sweep handles it
   if (sub == 0) {
     P.norms[b * (long)P.n_pad + row] = acc;
     if (is_b) {
@@ -169,6 +171,7 @@ struct MatchArgs {
   const float* da;
   const float* db;
   int n0, n1, dim, Dp, n0_pad, n1_pad, split_w, force_f32;
+  int short_ok;  // float calls take the bf16 shortlist (match_bf16.hip) unless non-finite
   long qa_bstride, qb_bstride, a_bstride, b_bstride;
   uint4* partial;
   const uint32_t* flag;
@@ -442,7 +445,8 @@ __device__ __forceinline__ void sweep_f32(const MatchArgs& p, int rowbase) {
 // Merge of the nsplit partials, one thread per query row (256-row workgroups), then
 // the exact near-tie rescan (rare; a whole wave per flagged row) and the ratio test.
 __global__ __launch_bounds__(256) void merge_kernel(MatchArgs p, int nsplit) {
-  const bool fpath = p.force_f32 || *p.flag == p.gen;  // uniform
+  const bool fpath = p.force_f32 || p.flag[0] == p.gen;  // uniform
+  if (fpath && p.short_ok && p.flag[1] != p.gen) return;  // frerank_kernel writes the outputs
   const int b = blockIdx.y, lane = threadIdx.x & 63;
   const int row = blockIdx.x * kRowsPerWG + threadIdx.x;
   uint64_t k1 = ~0ull, k2 = ~0ull;
@@ -506,10 +510,10 @@ __global__ __launch_bounds__(256) void merge_kernel(MatchArgs p, int nsplit) {
 
 template <int KS>
 __global__ __launch_bounds__(256) void match_kernel(MatchArgs p) {
-  const bool fpath = p.force_f32 || *p.flag == p.gen;  // uniform
+  const bool fpath = p.force_f32 || p.flag[0] == p.gen;  // uniform
   if (!fpath) {
     sweep_i8<KS>(p);
-  } else {
+  } else if (!p.short_ok || p.flag[1] == p.gen) {  // the exact fp32 sweep
 #pragma unroll 1
     for (int t = 0; t < kRowsPerWG / kFloatTile; ++t)
       sweep_f32(p, blockIdx.x * kRowsPerWG + t * kFloatTile);
@@ -590,11 +594,11 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
   w = std::max(256, std::min(4096, w));
   const int nsplit = std::max(1, ceil_div(n1_pad, w));
 
-  ws.flag.reserve(sizeof(uint32_t));
+  ws.flag.reserve(2 * sizeof(uint32_t));
   ws.partial.reserve((size_t)batch * nsplit * n0_pad * sizeof(uint4));
   // generation tag of this call (see pack_kernel); 0 is the reset value of the flag
   if (++ws.gen == 0 || ws.flag_fresh) {
-    VO_HIP_CHECK(hipMemsetAsync(ws.flag.ptr, 0, sizeof(uint32_t), st));
+    VO_HIP_CHECK(hipMemsetAsync(ws.flag.ptr, 0, 2 * sizeof(uint32_t), st));
     ws.gen = 1;
     ws.flag_fresh = false;
   }
@@ -611,6 +615,9 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
   a.n1_pad = n1_pad;
   a.split_w = w;
   a.force_f32 = int_ok ? 0 : 1;
+  // dim <= 256: the shortlist's A fragments fit in VGPRs; a SIFT hint leaves it unlaunched
+  // (float values then take the exact sweep)
+  a.short_ok = int_ok && ws.kind_hint != VO_DESC_SIFT ? 1 : 0;
   a.a_bstride = (long)n0 * dim;
   a.b_bstride = (long)n1 * dim;
   a.partial = ws.partial.as<uint4>();
@@ -660,6 +667,42 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
     default: hipLaunchKernelGGL(match_kernel<4>, grid, dim3(256), 0, st, a); break;
   }
   ctx->prof.end(st);
+  if (a.short_ok) {  // float calls: bf16 MFMA shortlist + exact re-rank (match_bf16.hip)
+    ShortArgs s{};
+    s.da = d_des0;
+    s.db = d_des1;
+    s.n0 = n0;
+    s.n1 = n1;
+    s.dim = dim;
+    s.Dp = short_Dp(dim);
+    s.n0_pad = n0_pad;
+    s.n1_pad = n1_pad;
+    s.split_w = w;
+    s.nsplit = nsplit;
+    s.a_bstride = a.a_bstride;
+    s.b_bstride = a.b_bstride;
+    s.flag = flag;
+    s.gen = ws.gen;
+    s.ratio = ratio;
+    s.best = d_best;
+    s.idx2 = d_idx2;
+    s.dist2 = d_dist2;
+    ws.hbf.reserve((size_t)batch * (n0_pad + n1_pad) * s.Dp * 2);
+    s.ha = ws.hbf.as<__bf16>();
+    s.hb = s.ha + (size_t)batch * n0_pad * s.Dp;
+    ws.fnorm.reserve((size_t)batch * (n0_pad + n1_pad) * sizeof(float));
+    s.nbq = ws.fnorm.as<float>();
+    s.ra = s.nbq + (size_t)batch * n1_pad;
+    if (ws.bmax.bytes < (size_t)batch * sizeof(uint32_t)) {
+      ws.bmax.reserve((size_t)batch * sizeof(uint32_t));
+      VO_HIP_CHECK(hipMemsetAsync(ws.bmax.ptr, 0, ws.bmax.bytes, st));
+    }
+    s.bmax = ws.bmax.as<uint32_t>();
+    s.part = reinterpret_cast<float2*>(a.partial);  // (batch, nsplit, n0_pad) float2 fits the uint4 partials
+    ws.cand.reserve((size_t)batch * (n0_pad / 16) * 4 * (n1_pad / 16) * sizeof(uint64_t));
+    s.mask = ws.cand.as<uint64_t>();
+    short_launch(ctx, s, batch);
+  }
   ctx->prof.begin(st, kKMatchMerge);
   hipLaunchKernelGGL(merge_kernel, dim3(row_wgs, batch), dim3(256), 0, st, a, nsplit);
   ctx->prof.end(st);

@@ -1,0 +1,450 @@
+// Float-descriptor matcher (SuperPoint-like, BASELINE config 5) on the matrix cores:
+// a bf16 MFMA shortlist followed by an exact fp32 re-rank, bit-exact against
+// oracle/match_ref.c (k-ordered fmaf chain, keys (sqrtf(d2), j), OpenCV's tie rule).
+// Replaces the same cv2.BFMatcher(NORM_L2).knnMatch(k=2) + ratio loop as the integer
+// path (reference src/modules/frontend.py:86-111; the LightGlue branch :80-84 is what
+// config 5 swaps for brute force).
+//
+// Why a shortlist is exact.  Let D_j be the exact squared distance of query a to train
+// row b_j, F_j the fp32 fmaf chain the oracle computes, and A_j the shortlist value
+// |b'_j|^2 - 2 a'.b'_j + |a'|^2 with a', b' the bf16 (round to nearest even, unit
+// roundoff 2^-8) images, products exact in fp32 and sums in fp32 (the row constant
+// |a'|^2 is dropped: it does not change a row's ranking).  Then
+//   |A_j - D_j| <= 2^-8 (|a| + |b_j|)^2 (2 + 2^-8) + (n + 4) 2^-24 (|a| + |b_j|)^2,
+//   |F_j - D_j| <= (n + 4) 2^-24 (|a| + |b_j|)^2                     (n = dim <= 256),
+// so |A_j - F_j| <= E = c (|a| + max_j |b_j|)^2 with c = 1.25 (2^-7 + 4e-5) (a 25 %
+// margin).  With m2 the second smallest A of the row, the second smallest F is at most
+// m2 + E, and every j whose F does not exceed it has A_j <= m2 + 2E.  So the candidate set
+// {j : A_j <= m2 + 2E} holds every pair the exact top-2 can take (ties included), and
+// ranking the candidates by their exact fp32 chains reproduces the oracle.  Candidates
+// are recorded as bit masks (one ballot per row group and 16-column tile), so the set is
+// complete whatever its size, and the re-rank is deterministic.
+//
+// Kernels (one call, every launch exits at once unless the call's descriptors took the
+// float path -- pack_kernel's device-side flag -- and are finite, dim <= 256):
+//   fpack   bf16 images of both sides, |b'|^2 per train row (+inf for padding), |a| and
+//           max |b| (the bound)
+//   fsweep<1>  v_mfma_f32_16x16x32_bf16 sweep, top-2 of A per (row, split)
+//   fsweep<2>  the same sweep again: every A <= m2 + 2E marked in the row's tile masks
+//   frerank    one workgroup per 16 query rows: exact fmaf chains of the pooled candidates, top-2 by
+//              (sqrtf(d2), j), ratio test (the merge_kernel outputs)
+#include "match_short.h"
+
+namespace vo {
+
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+constexpr int kShortRowsPerWG = 128;  // 4 waves x 32 query rows (two 16-row M tiles)
+constexpr float kShortC = 1.25f * (0.0078125f + 4e-5f);
+
+namespace {
+
+__device__ __forceinline__ bool short_active(const ShortArgs& p) {
+  return p.flag[0] == p.gen && p.flag[1] != p.gen;  // uniform
+}
+
+__device__ __forceinline__ float med3_f32(float a, float b, float c) {
+  float r;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// ---- bf16 images, norms ------------------------------------------------------------
+// 16 threads per row, 8 consecutive elements per thread and step.  Rows past n are
+// written as zeros (train padding rows get |b'|^2 = +inf: never a candidate).
+__global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int v4) {
+  if (!short_active(p)) return;
+  const bool is_b = (int)blockIdx.x >= a_wgs;
+  const int b = blockIdx.y;
+  const int n = is_b ? p.n1 : p.n0, n_pad = is_b ? p.n1_pad : p.n0_pad;
+  const int row = (((int)blockIdx.x - (is_b ? a_wgs : 0)) * 256 + (int)threadIdx.x) >> 4;
+  const int sub = threadIdx.x & 15;
+  const bool in = row < n_pad;  // every thread reaches the workgroup reduction below
+  const bool live = row < n;
+  const float* src = (is_b ? p.db + b * p.b_bstride : p.da + b * p.a_bstride) + (long)row * p.dim;
+  __bf16* dst = (is_b ? p.hb + (long)b * p.n1_pad * p.Dp : p.ha + (long)b * p.n0_pad * p.Dp) + (long)row * p.Dp;
+  float q2 = 0.0f, x2 = 0.0f;
+  for (int e = sub * 8; in && e < p.Dp; e += 128) {
+    v8bf h;
+    float vv[8];
+    if (v4 && live && e + 8 <= p.dim) {
+      const float4 x0 = *reinterpret_cast<const float4*>(src + e);
+      const float4 x1 = *reinterpret_cast<const float4*>(src + e + 4);
+      vv[0] = x0.x; vv[1] = x0.y; vv[2] = x0.z; vv[3] = x0.w;
+      vv[4] = x1.x; vv[5] = x1.y; vv[6] = x1.z; vv[7] = x1.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) vv[u] = (live && e + u < p.dim) ? src[e + u] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float v = vv[u];
+      const __bf16 hv = (__bf16)v;
+      const float hf = (float)hv;
+      h[u] = hv;
+      q2 = fmaf(hf, hf, q2);
+      x2 = fmaf(v, v, x2);
+    }
+    *reinterpret_cast<v8bf*>(dst + e) = h;
+  }
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) {
+    q2 += __shfl_xor(q2, m, 64);
+    x2 += __shfl_xor(x2, m, 64);
+  }
+  // norms rounded up by a few ulps: the bound only needs upper estimates
+  const float r = sqrtf(x2) * 1.0001f;
+  if (sub == 0 && in) {
+    if (is_b) p.nbq[(long)b * p.n1_pad + row] = live ? q2 : __builtin_huge_valf();
+    else p.ra[(long)b * p.n0_pad + row] = r;
+  }
+  if (!is_b) return;
+  // max |b| of the workgroup's 16 rows, then one atomic per workgroup (not per row: same-
+  // address atomics serialise)
+  uint32_t m = live ? __float_as_uint(r) : 0u;
+#pragma unroll
+  for (int k = 16; k < 64; k <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, k, 64));
+  __shared__ uint32_t wmax[4];
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+    if (m) atomicMax(p.bmax + b, m);
+  }
+}
+
+// ---- bf16 MFMA sweep ---------------------------------------------------------------
+// Grid (n0_pad / 128, nsplit, batch).  Wave w holds the A fragments of query rows
+// rowbase .. rowbase + 31 in VGPRs; train columns arrive in 64-column chunks staged in
+// LDS (one global fetch per workgroup, double-buffered, rows padded by 16 bytes).  A
+// 16-column tile: B fragments from LDS, KS MFMAs per M tile, then per (row, column)
+// A' = |b'|^2 - 2 a'.b' and PASS 1: running top-2 (v_min_f32 + v_med3_f32), PASS 2: the
+// candidate test.
+template <int PASS, int KS>
+__global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
+  if (!short_active(p)) return;
+  constexpr int Dp = 32 * KS;
+  constexpr int kRow = Dp + 8;  // bf16 elements per LDS row
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int b = blockIdx.z, split = blockIdx.y, nsplit = p.nsplit;
+  const int rowbase = blockIdx.x * kShortRowsPerWG + wave * 32;
+  const __bf16* A = p.ha + (long)b * p.n0_pad * Dp;
+  const __bf16* B = p.hb + (long)b * p.n1_pad * Dp;
+  const float* nbq = p.nbq + (long)b * p.n1_pad;
+
+  v8bf af[2][KS];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      af[mt][ks] = *reinterpret_cast<const v8bf*>(A + (long)(rowbase + 16 * mt + (lane & 15)) * Dp + 32 * ks +
+                                                  8 * (lane >> 4));
+
+  // this lane's rows: 16 mt + 4 (lane >> 4) + r
+  float m1[2][4], m2[2][4], thr[2][4];
+  if (PASS == 1) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m1[mt][r] = m2[mt][r] = __builtin_huge_valf();
+    // clear this workgroup's candidate masks: 8 row blocks x 4 x the split's tiles
+    const int T = p.n1_pad / 16, t0 = split * p.split_w / 16, nt = min(p.split_w / 16, T - t0);
+    for (int e = tid; e < 32 * nt; e += 256) {
+      const int rb = e / (4 * nt), rr = (e / nt) % 4, t = e % nt;
+      p.mask[(((long)b * (p.n0_pad / 16) + blockIdx.x * 8 + rb) * 4 + rr) * T + t0 + t] = 0ull;
+    }
+  } else {
+    const float bm = __uint_as_float(p.bmax[b]);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rowbase + 16 * mt + 4 * (lane >> 4) + r;
+        float a1 = __builtin_huge_valf(), a2 = __builtin_huge_valf();
+        for (int s = 0; s < nsplit; ++s) {
+          const float2 q = p.part[((long)b * nsplit + s) * p.n0_pad + row];
+          a2 = med3_f32(a1, q.x, fminf(a2, q.y));
+          a1 = fminf(a1, q.x);
+        }
+        const float ra = p.ra[(long)b * p.n0_pad + row] + bm;
+        // +inf when the row has < 2 columns; padding rows take nothing
+        thr[mt][r] = row < p.n0 ? a2 + 2.0f * kShortC * ra * ra : -__builtin_huge_valf();
+      }
+  }
+
+  const int c0 = split * p.split_w;
+  const int c1 = min(c0 + p.split_w, p.n1_pad);
+  __shared__ __attribute__((aligned(16))) __bf16 sB[2][64 * kRow];
+  __shared__ float sN[2][64];
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  auto gload = [&](int cbase, v4i (&g)[KS], float& gn) {
+    const int col = min(cbase + (tid >> 2), c1 - 1);
+    const __bf16* src = B + (long)col * Dp + (tid & 3) * 8 * KS;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) g[ks] = *reinterpret_cast<const v4i*>(src + 8 * ks);
+    gn = nbq[min(cbase + (tid & 63), c1 - 1)];
+  };
+  auto sstore = [&](int buf, const v4i (&g)[KS], float gn) {
+    __bf16* dst = &sB[buf][(tid >> 2) * kRow + (tid & 3) * 8 * KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<v4i*>(dst + 8 * ks) = g[ks];
+    if (tid < 64) sN[buf][tid] = gn;
+  };
+  if (c0 < c1) {
+    const int nchunk = (c1 - c0 + 63) / 64;
+    v4i g[KS];
+    float gn;
+    gload(c0, g, gn);
+    sstore(0, g, gn);
+    __syncthreads();
+    for (int ch = 0; ch < nchunk; ++ch) {
+      const int buf = ch & 1, cb = c0 + 64 * ch;
+      if (ch + 1 < nchunk) gload(cb + 64, g, gn);
+      // the chunk's four 16-column tiles x two M tiles: eight independent accumulators,
+      // k-step outer, so consecutive MFMAs never wait on each other
+      v4f acc[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) acc[u][mt] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        v8bf bf[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          bf[u] = *reinterpret_cast<const v8bf*>(&sB[buf][(16 * u + (lane & 15)) * kRow + 8 * (lane >> 4) + 32 * ks]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+            acc[u][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt][ks], bf[u], acc[u][mt], 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (cb + 16 * u >= c1) continue;  // uniform
+        const float nc = sN[buf][16 * u + (lane & 15)];
+        const int col = cb + 16 * u + (lane & 15);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = fmaf(-2.0f, acc[u][mt][r], nc);
+            if (PASS == 1) {
+              m2[mt][r] = med3_f32(m1[mt][r], m2[mt][r], v);
+              m1[mt][r] = fminf(m1[mt][r], v);
+            } else {
+              // one ballot per (M tile, r): rows 16 mt + 4 g + r (g = lane >> 4) x the tile's
+              // 16 columns; stored only when a bit is set (rare)
+              const uint64_t hit = __ballot(v <= thr[mt][r] && col < p.n1);
+              if (hit && lane == 0)
+                p.mask[(((long)b * (p.n0_pad / 16) + (rowbase >> 4) + mt) * 4 + r) * (p.n1_pad / 16) +
+                       (cb >> 4) + u] = hit;
+            }
+          }
+      }
+      if (ch + 1 < nchunk) sstore(buf ^ 1, g, gn);
+      __syncthreads();
+    }
+  }
+  if (PASS == 1) {
+    // top-2 over the 16 lanes of a row (one DPP row): second = med3(a1, b1, min(a2, b2))
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float M1 = m1[mt][r], M2 = m2[mt][r];
+#define VO_TOP2_STEP(CTRL)                                                                             \
+  {                                                                                                    \
+    const float b1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(M1), CTRL, 0xF, 0xF, false)); \
+    const float b2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(M2), CTRL, 0xF, 0xF, false)); \
+    M2 = med3_f32(M1, b1, fminf(M2, b2));                                                              \
+    M1 = fminf(M1, b1);                                                                                \
+  }
+        VO_TOP2_STEP(0x121)
+        VO_TOP2_STEP(0x122)
+        VO_TOP2_STEP(0x124)
+        VO_TOP2_STEP(0x128)
+#undef VO_TOP2_STEP
+        if ((lane & 15) == 0) {
+          const int row = rowbase + 16 * mt + 4 * (lane >> 4) + r;
+          p.part[((long)b * nsplit + split) * p.n0_pad + row] = make_float2(M1, M2);
+        }
+      }
+  }
+}
+
+// ---- exact re-rank -----------------------------------------------------------------
+__device__ __forceinline__ float sqrtf_rn2(float x) { return (float)sqrt((double)x); }
+
+__device__ __forceinline__ uint64_t key64s(uint32_t d, uint32_t j) { return ((uint64_t)d << 32) | j; }
+
+__device__ __forceinline__ void merge2s(uint64_t& a1, uint64_t& a2, uint64_t b1, uint64_t b2) {
+  const uint64_t lo = a1 < b1 ? a1 : b1;
+  const uint64_t hi = a1 < b1 ? b1 : a1;
+  const uint64_t m = a2 < b2 ? a2 : b2;
+  a1 = lo;
+  a2 = hi < m ? hi : m;
+}
+
+// One workgroup per block of 16 query rows (the rows one set of candidate masks covers).
+// The block's candidates (row, column) are pooled into one LDS list, so every lane of
+// every wave has a candidate: thread c loads candidate c's train row (two halves of 32
+// float4, all in flight) and runs the exact k-ordered fmaf chain against its query row
+// (staged in LDS), keys (sqrtf(d2), j) go to LDS, and thread r merges row r's keys.  The
+// candidate set is complete (masks have no capacity); a block with more than kPool
+// candidates takes its rows one at a time through the same code.
+constexpr int kPool = 1024;
+constexpr int kQStr = 260;  // floats per staged query row
+
+__device__ __forceinline__ float chain_regs(const float* x, const float* y, int dim) {
+  // the oracle's distance: sum over k ascending of fmaf(x_k - y_k, x_k - y_k, acc); the
+  // train row y (global) arrives 128 elements at a time, every load in flight first
+  float acc = 0.0f;
+  for (int h = 0; h < dim; h += 128) {
+    float4 yr[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t)
+      yr[t] = h + 4 * t < dim ? *reinterpret_cast<const float4*>(y + h + 4 * t) : make_float4(0, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 32; ++t) {
+      if (h + 4 * t >= dim) break;
+      const float4 xv = *reinterpret_cast<const float4*>(x + h + 4 * t);
+      float d = xv.x - yr[t].x;
+      acc = fmaf(d, d, acc);
+      d = xv.y - yr[t].y;
+      acc = fmaf(d, d, acc);
+      d = xv.z - yr[t].z;
+      acc = fmaf(d, d, acc);
+      d = xv.w - yr[t].w;
+      acc = fmaf(d, d, acc);
+    }
+  }
+  return acc;
+}
+
+__device__ __forceinline__ float chain_scalar(const float* x, const float* y, int dim) {
+  float acc = 0.0f;
+  for (int k = 0; k < dim; ++k) {
+    const float d = x[k] - y[k];
+    acc = fmaf(d, d, acc);
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4) {
+  if (!short_active(p)) return;
+  const int b = blockIdx.y, R = blockIdx.x, tid = threadIdx.x;
+  if (R == 0 && tid == 0) p.bmax[b] = 0u;  // fsweep<2> is done with it
+  __shared__ __attribute__((aligned(16))) float sq[16 * kQStr];
+  __shared__ int slist[kPool];      // row_local << 16 | column tile bit position (see below)
+  __shared__ int scol[kPool];
+  __shared__ uint64_t skey[kPool];
+  __shared__ int sscan[256];
+  const int row0 = 16 * R;
+  for (int e = tid; e < 16 * p.dim; e += 256) {
+    const int rl = e / p.dim, k = e - rl * p.dim;
+    sq[rl * kQStr + k] = row0 + rl < p.n0 ? p.da[b * p.a_bstride + (long)(row0 + rl) * p.dim + k] : 0.0f;
+  }
+  const int T = p.n1_pad / 16;
+  const uint64_t* mblk = p.mask + ((long)b * (p.n0_pad / 16) + R) * 4 * T;  // (r, t) entries
+  const float* B = p.db + b * p.b_bstride;
+  // this thread's mask entries: e = tid, tid + 256, ... of the 4 T entries (r, t)
+  int cnt = 0;
+  for (int e = tid; e < 4 * T; e += 256) cnt += __popcll(mblk[e]);
+  // workgroup exclusive prefix of the counts
+  sscan[tid] = cnt;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {
+    const int v = tid >= d ? sscan[tid - d] : 0;
+    __syncthreads();
+    sscan[tid] += v;
+    __syncthreads();
+  }
+  const int total = sscan[255];
+  int pos = sscan[tid] - cnt;
+  const bool pooled = total <= kPool;
+  if (pooled) {
+    for (int e = tid; e < 4 * T; e += 256) {
+      const int r = e / T, t = e - r * T;
+      for (uint64_t m = mblk[e]; m; m &= m - 1) {
+        const int bit = __builtin_ctzll(m), g = bit >> 4;
+        slist[pos] = 4 * g + r;  // row_local = 4 g + r
+        scol[pos] = 16 * t + (bit & 15);
+        ++pos;
+      }
+    }
+  }
+  __syncthreads();
+  uint64_t k1 = ~0ull, k2 = ~0ull;
+  if (pooled) {
+    for (int c = tid; c < total; c += 256) {
+      const int rl = slist[c], j = scol[c];
+      const float* y = B + (long)j * p.dim;
+      const float d = v4 ? chain_regs(sq + rl * kQStr, y, p.dim) : chain_scalar(sq + rl * kQStr, y, p.dim);
+      skey[c] = key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)j);
+    }
+    __syncthreads();
+    if (tid < 16)
+      for (int c = 0; c < total; ++c)
+        if (slist[c] == tid) merge2s(k1, k2, skey[c], ~0ull);
+  } else if (tid < 16) {  // rare: thread r walks row r's candidates itself
+    const int g = tid >> 2, r = tid & 3;
+    for (int t = 0; t < T; ++t)
+      for (uint32_t m = (uint32_t)(mblk[r * T + t] >> (16 * g)) & 0xFFFFu; m; m &= m - 1) {
+        const int j = 16 * t + __builtin_ctz(m);
+        const float d = chain_scalar(sq + tid * kQStr, B + (long)j * p.dim, p.dim);
+        merge2s(k1, k2, key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)j), ~0ull);
+      }
+  }
+  const int row = row0 + tid;
+  if (tid >= 16 || row >= p.n0) return;
+  const float s1 = k1 == ~0ull ? __builtin_huge_valf() : __uint_as_float((uint32_t)(k1 >> 32));
+  const float s2 = k2 == ~0ull ? __builtin_huge_valf() : __uint_as_float((uint32_t)(k2 >> 32));
+  const int j1 = k1 == ~0ull ? -1 : (int)(uint32_t)k1;
+  const int j2 = k2 == ~0ull ? -1 : (int)(uint32_t)k2;
+  const long o = (long)b * p.n0 + row;
+  if (p.best) p.best[o] = (j2 >= 0 && (double)s1 < p.ratio * (double)s2) ? j1 : -1;
+  if (p.idx2) {
+    p.idx2[2 * o] = j1;
+    p.idx2[2 * o + 1] = j2;
+    p.dist2[2 * o] = j1 >= 0 ? s1 : 3.402823466e+38f;
+    p.dist2[2 * o + 1] = j2 >= 0 ? s2 : 3.402823466e+38f;
+  }
+}
+
+}  // namespace
+
+void short_launch(vo_ctx* ctx, ShortArgs& a, int batch) {
+  hipStream_t st = ctx->stream;
+  const int a_wgs = (int)ceil_div((int64_t)a.n0_pad * 16, 256);
+  const int b_wgs = (int)ceil_div((int64_t)a.n1_pad * 16, 256);
+  ctx->prof.begin(st, kKMatchPack);
+  const int v4 = a.dim % 4 == 0 && (uintptr_t)a.da % 16 == 0 && (uintptr_t)a.db % 16 == 0;
+  hipLaunchKernelGGL(fpack_kernel, dim3(a_wgs + b_wgs, batch), dim3(256), 0, st, a, a_wgs, v4);
+  ctx->prof.end(st);
+  const dim3 grid(a.n0_pad / kShortRowsPerWG, a.nsplit, batch);
+  ctx->prof.begin(st, kKMatchF32);
+  switch (a.Dp / 32) {
+#define VO_SWEEPS(KS)                                                                \
+  case KS:                                                                           \
+    hipLaunchKernelGGL((fsweep_kernel<1, KS>), grid, dim3(256), 0, st, a);           \
+    hipLaunchKernelGGL((fsweep_kernel<2, KS>), grid, dim3(256), 0, st, a);           \
+    break;
+    VO_SWEEPS(1)
+    VO_SWEEPS(2)
+    VO_SWEEPS(3)
+    VO_SWEEPS(4)
+    VO_SWEEPS(5)
+    VO_SWEEPS(6)
+    VO_SWEEPS(7)
+    VO_SWEEPS(8)
+#undef VO_SWEEPS
+  }
+  ctx->prof.end(st);
+  ctx->prof.begin(st, kKMatchMerge);
+  hipLaunchKernelGGL(frerank_kernel, dim3(a.n0_pad / 16, batch), dim3(256), 0, st, a, v4);
+  ctx->prof.end(st);
+}
+
+}  // namespace vo

@@ -1,0 +1,33 @@
+// Float-descriptor shortlist matcher (match_bf16.hip), launched by match_run (match.hip).
+#pragma once
+
+#include "vo_ctx.h"
+
+namespace vo {
+
+struct ShortArgs {
+  const float* da;
+  const float* db;
+  __bf16* ha;           // (batch, n0_pad, Dp) bf16 query image
+  __bf16* hb;           // (batch, n1_pad, Dp) bf16 train image
+  float* nbq;           // (batch, n1_pad) |b'|^2, +inf for padding columns
+  float* ra;            // (batch, n0_pad) |a|
+  uint32_t* bmax;       // (batch) max |b| (float bits); zero between calls
+  float2* part;         // (batch, nsplit, n0_pad) top-2 of A per split
+  uint64_t* mask;       // candidate bits: (batch, n0_pad / 16, 4, n1_pad / 16) -- entry (R, r, t)
+                        // bit 16 g + c = row 16 R + 4 g + r, column 16 t + c (fsweep<2>)
+  int n0, n1, dim, Dp, n0_pad, n1_pad, split_w, nsplit;
+  long a_bstride, b_bstride;
+  const uint32_t* flag;  // [0] == gen: not SIFT integers; [1] == gen: a non-finite value
+  uint32_t gen;
+  double ratio;
+  int32_t* best;
+  int32_t* idx2;
+  float* dist2;
+};
+
+// bf16 K padding of the shortlist (a multiple of 32, at most 256 for dim <= 256)
+inline int short_Dp(int dim) { return (dim + 31) / 32 * 32; }
+void short_launch(vo_ctx* ctx, ShortArgs& a, int batch);
+
+}  // namespace vo

@@ -19,7 +19,12 @@ struct MatchWorkspace {
   DevBuf pairs;     // int32 (n0, 2) compacted pairs + count
   DevBuf flag;      // uint32: == gen when this call's descriptors are not 0..255 integers
   DevBuf tri;       // triangulation staging: pts1, pts2, pts3d, mask
+  DevBuf hbf;       // float path: bf16 images of both sides (match_bf16.hip)
+  DevBuf fnorm;     // float path: |b'|^2 per train row, |a| per query row
+  DevBuf bmax;      // float path: max |b| per batch entry (zero between calls)
+  DevBuf cand;      // float path: candidate lists + counts
   uint32_t gen = 0;         // generation tag of the current call
+  int kind_hint = 0;        // VO_DESC_* (vo_match_hint)
   bool flag_fresh = true;   // flag not yet zeroed
 };
 

@@ -99,6 +99,17 @@ def match_batch_device(des0: _lib.DeviceArray, des1: _lib.DeviceArray, ratio: fl
     return out
 
 
+DESC_AUTO, DESC_SIFT, DESC_FLOAT = 0, 1, 2  # vo_match_hint kinds (include/vo_hip.h)
+
+
+def set_descriptor_kind(kind: int, ctx: _lib.Context | None = None) -> None:
+    """``vo_match_hint``: which descriptors later calls on ``ctx`` expect (results never
+    depend on it).  ``DESC_SIFT`` leaves the float shortlist unlaunched (the drop-in sets it
+    for the reference's SIFT extractor); ``DESC_AUTO`` launches both paths' kernels."""
+    ctx = ctx or _lib.context()
+    check(ctx.lib.vo_match_hint(ctx.handle, int(kind)), "vo_match_hint")
+
+
 def synchronize(ctx: _lib.Context | None = None) -> None:
     ctx = ctx or _lib.context()
     check(ctx.lib.vo_synchronize(ctx.handle), "vo_synchronize")
