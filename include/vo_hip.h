@@ -295,9 +295,11 @@ typedef struct vo_sift_keypoint {
  * nfeatures-th largest), and calcSIFTDescriptor (4 x 4 x 8, clipped at 0.2, scaled to 512,
  * saturate_cast<uchar>, stored as float).  Keypoints come out in removeDuplicatedSorted's
  * order (x asc, y asc, size desc, angle asc, response desc, octave desc); OpenCV's order
- * after retainBest is implementation-defined.  capacity bounds the
- * oriented keypoints considered (before the nfeatures cut) and the output; *count = the
- * number written; VO_ERR_ARG when a capacity overflowed.  Host buffers:
+ * after retainBest is implementation-defined.  capacity is the size of
+ * the output buffers; the oriented keypoints considered before the nfeatures cut start at
+ * that capacity and the call retries with 4x more (up to 131072 per image) when they
+ * overflow, as OpenCV has no such cap.  *count = the number written; VO_ERR_ARG when more
+ * than 131072 oriented keypoints or more than capacity output keypoints.  Host buffers:
  * kps[capacity], desc[capacity x 128]. */
 int vo_sift_detect_and_compute(vo_ctx* ctx, const uint8_t* img, int h, int w, int nfeatures, double contrast,
                                double edge, double sigma, int n_layers, int capacity, vo_sift_keypoint* kps,

@@ -58,10 +58,10 @@ def _sharded(p, nranks, iters, lam, group):
     return out
 
 
-@pytest.mark.parametrize("cfg,nranks", [("cfg2", 2), ("cfg2", 3), ("cfg3", 2)])
+@pytest.mark.parametrize("cfg,nranks", [("cfg2", 2), ("cfg2", 3), ("cfg3", 2), ("cfg4", 2), ("cfg4", 4)])
 def test_sharded_matches_unsharded(cfg, nranks):
     p = make_ba_config(cfg)
-    iters, lam = 5, 1.0
+    iters, lam = (3 if cfg == "cfg4" else 5), 1.0  # cfg4 = BASELINE config 4, 100 x 200k
     rc0, c0, P0, X0 = _unsharded(p, iters, lam)
     res = _sharded(p, nranks, iters, lam, f"vo-loopback-{cfg}-{nranks}".encode())
     # every rank solved the same reduced system: identical poses and cost trajectories

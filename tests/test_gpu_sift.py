@@ -116,6 +116,19 @@ def test_detect_and_compute_textured_kitti(ctx):
     _check_full(got, ref)
 
 
+def test_detect_and_compute_low_contrast_capacity_retry(ctx):
+    """The malaga / parking SIFT settings (contrast 0.01, edge 2, nfeatures 3000,
+    config.py:80-85,92-96) on a textured 480 x 640 image, with a working capacity far below
+    the oriented keypoint count: the call grows it (4x per overflow) instead of failing
+    (ADVICE r1), and the result equals the oracle and the large-capacity call."""
+    img = sift_scene(480, 640, seed=201, texture=14.0)
+    ref = S.detect_and_compute(img, 3000, 0.01, 2.0, 1.6)
+    assert len(ref["pt"]) >= 3000
+    got = sift.detect_and_compute(img, 3000, 0.01, 2.0, 1.6, capacity=3072, ctx=ctx)
+    _check_full(got, ref)
+    _check_full(sift.detect_and_compute(img, 3000, 0.01, 2.0, 1.6, ctx=ctx), ref)
+
+
 def test_detect_and_compute_edge_cases(ctx):
     flat = np.full((64, 64), 128, np.uint8)
     r = sift.detect_and_compute(flat, ctx=ctx)

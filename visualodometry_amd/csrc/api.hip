@@ -429,17 +429,28 @@ int vo_sift_detect_and_compute(vo_ctx* ctx, const uint8_t* img, int h, int w, in
     vo::SiftWorkspace& ws = ctx->sift;
     const size_t nimg = (size_t)h * w;
     ws.img.reserve(nimg);
-    ws.out.reserve((size_t)capacity * (sizeof(vo_sift_keypoint) + 128 * sizeof(float)) + 64);
-    vo_sift_keypoint* dK = ws.out.as<vo_sift_keypoint>();
-    float* dD = reinterpret_cast<float*>(dK + capacity);
-    int32_t* dC = reinterpret_cast<int32_t*>(dD + (size_t)capacity * 128);
     hipStream_t s = ctx->stream;
     VO_HIP_CHECK(hipMemcpyAsync(ws.img.ptr, img, nimg, hipMemcpyHostToDevice, s));
-    sift_full(ctx, ws.img.as<uint8_t>(), 1, h, w, nfeatures, contrast, edge, sigma, n_layers, capacity, dK, dD, dC);
-    int32_t n = 0;
-    VO_HIP_CHECK(hipMemcpyAsync(&n, dC, 4, hipMemcpyDeviceToHost, s));
-    VO_HIP_CHECK(hipStreamSynchronize(s));
-    VO_REQUIRE(n >= 0, VO_ERR_ARG, "vo_sift_detect_and_compute: more than capacity=%d keypoints", capacity);
+    // The working capacity (oriented keypoints before duplicate removal and retainBest)
+    // starts at the caller's and grows 4x per overflow up to the kernel limit (OpenCV has
+    // no cap); only the final keypoints must fit the caller's buffers.
+    int cap = std::min(capacity, vo::sift_max_capacity()), n = -1;
+    vo_sift_keypoint* dK = nullptr;
+    float* dD = nullptr;
+    for (;;) {
+      ws.out.reserve((size_t)cap * (sizeof(vo_sift_keypoint) + 128 * sizeof(float)) + 64);
+      dK = ws.out.as<vo_sift_keypoint>();
+      dD = reinterpret_cast<float*>(dK + cap);
+      int32_t* dC = reinterpret_cast<int32_t*>(dD + (size_t)cap * 128);
+      sift_full(ctx, ws.img.as<uint8_t>(), 1, h, w, nfeatures, contrast, edge, sigma, n_layers, cap, dK, dD, dC);
+      VO_HIP_CHECK(hipMemcpyAsync(&n, dC, 4, hipMemcpyDeviceToHost, s));
+      VO_HIP_CHECK(hipStreamSynchronize(s));
+      if (n >= 0 || cap >= vo::sift_max_capacity()) break;
+      cap = (int)std::min<int64_t>(4ll * cap, vo::sift_max_capacity());
+    }
+    VO_REQUIRE(n >= 0, VO_ERR_ARG, "vo_sift_detect_and_compute: more than %d keypoints in one image", cap);
+    VO_REQUIRE(n <= capacity, VO_ERR_ARG, "vo_sift_detect_and_compute: %d keypoints exceed capacity=%d", n,
+               capacity);
     *count = n;
     if (n == 0) return;
     VO_HIP_CHECK(hipMemcpyAsync(kps, dK, (size_t)n * sizeof(vo_sift_keypoint), hipMemcpyDeviceToHost, s));

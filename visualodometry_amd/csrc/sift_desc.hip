@@ -268,7 +268,7 @@ __device__ __forceinline__ bool kp_less2(const float* a, const float* b) {
 }
 
 constexpr int kSelThreads = 1024;
-constexpr int kMaxCapImg = 32768;
+constexpr int kMaxCapImg = 131072;  // keep[] in LDS: 128 KiB of the select kernel's 160
 
 __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
   __shared__ uint8_t keep[kMaxCapImg];
@@ -745,6 +745,8 @@ ExpTab make_exp_tab() {
 }
 
 // Orientation, filtering and descriptors of the candidates sift_run left in the workspace.
+int sift_max_capacity() { return kMaxCapImg; }
+
 void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double sigma, int nfeatures, int cap_img,
                    const float* cand_f, const int32_t* cand_i, const int32_t* cand_count, int cand_cap,
                    const float* G, vo_sift_keypoint* d_kp, float* d_desc, int32_t* d_count) {

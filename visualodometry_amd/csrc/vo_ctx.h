@@ -116,6 +116,7 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
               float** g_out, float** d_out, int64_t* layout);
 int sift_layout(int h, int w, int n_layers, int64_t* out, int n);
 // SIFT orientation, filtering and descriptors (sift_desc.hip) of sift_run's candidates.
+int sift_max_capacity();  // largest per-image keypoint capacity of sift_describe
 void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double sigma, int nfeatures, int cap_img,
                    const float* cand_f, const int32_t* cand_i, const int32_t* cand_count, int cand_cap,
                    const float* G, vo_sift_keypoint* d_kp, float* d_desc, int32_t* d_count);
