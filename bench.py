@@ -156,7 +156,8 @@ def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: 
     return res
 
 
-def bench_matcher_float(ctx, batch: int = 16, n: int = 2048, dim: int = 256, calls: int = 10, warmup: int = 2):
+def bench_matcher_float(ctx, batch: int = 16, n: int = 2048, dim: int = 256, calls: int = 10, warmup: int = 2,
+                        traffic_all=None):
     """BASELINE config 5's matcher: SuperPoint-like L2-normalised float32 descriptors (not
     integer-valued: the bf16 MFMA shortlist + exact fp32 re-rank, bit-exact with the
     k-ordered fmaf chain), 2048 x 2048 x 256 per frame pair, knn2 + ratio
@@ -204,6 +205,7 @@ def bench_matcher_float(ctx, batch: int = 16, n: int = 2048, dim: int = 256, cal
         "kernel_us": kern,
         "roofline": {"bound": "mfma", "kernel": "match_f32 (fsweep<1> + fsweep<2>, bf16 MFMA)", "achieved": tfl,
                      "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tfl / BF16_MFMA_PEAK_TFLOPS,
+                     "traffic": (traffic_all or {}).get("match_f32"),
                      "note": "2 sweeps x 2 flops per pair and dimension / their summed HIP-event duration; the "
                              "exact fp32 re-rank of the shortlisted candidates is in kernel_us.match_merge"},
     }
@@ -580,7 +582,7 @@ def main() -> int:
         line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
     if rank == 0 and world == 1 and not args.no_matcher:
         line["secondary"] = bench_matcher(ctx, traffic_all=traffic_all)
-        line["matcher_float"] = bench_matcher_float(ctx)
+        line["matcher_float"] = bench_matcher_float(ctx, traffic_all=traffic_all)
         line["triangulate"] = bench_triangulate(ctx)
         line["pnp"] = bench_pnp(ctx)
         line["sift"] = bench_sift(ctx)
