@@ -192,6 +192,13 @@ int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n);
 int vo_profile_enable(vo_ctx* ctx, int on);
 int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
 
+/* Host only: groups observations by landmark (the CSR that vo_ba_problem takes) from a
+ * per-observation landmark index, as the keyframe window holds it (reference
+ * src/modules/vo.py:252-288 builds the BA problem from the map's observation lists):
+ * point_ptr (n_points + 1) and order (n_obs, stable: observations of one landmark keep the
+ * caller's order), so that obs_cam[order] / obs_uv[order] are the problem's arrays.
+ * VO_ERR_ARG if an index is out of range. */
+int vo_ba_group_by_point(int n_points, int n_obs, const int32_t* obs_pt, int32_t* order, int32_t* point_ptr);
 /* Host-only: builds the static plan of `prob` without a device (planner tests,
  * capacity checks).  Fills up to n int64 values: [0] chunks [1] segments
  * [2] slab blocks [3] profile blocks [4] track entries [5] max pairs in a chunk

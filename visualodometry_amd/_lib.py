@@ -82,6 +82,7 @@ SIGNATURES = {
     "vo_ba_solve": (_I, [_P, C.POINTER(BAProblemC), _PD, _PD, _I, _PD]),
     "vo_ba_plan_stats": (_I, [_P, _PI64, _I]),
     "vo_ba_debug_stamps": (_I, [_P, C.POINTER(C.c_uint64), _I]),
+    "vo_ba_group_by_point": (_I, [_I, _I, _PI32, _PI32, _PI32]),
     "vo_ba_plan_probe": (_I, [C.POINTER(BAProblemC), _I, _PI64, _I]),
     "vo_ba_plan_digest": (_I, [C.POINTER(BAProblemC), _I, C.POINTER(C.c_uint64)]),
     "vo_profile_enable": (_I, [_P, _I]),

@@ -66,14 +66,33 @@ def rt_to_poses(rt: np.ndarray) -> np.ndarray:
 
 
 def csr_from_obs_pt(n_points: int, obs_pt: np.ndarray):
-    """Stable grouping of observations by landmark -> (order, point_ptr)."""
-    obs_pt = np.asarray(obs_pt, dtype=np.int64)
-    if obs_pt.size and (obs_pt.min() < 0 or obs_pt.max() >= n_points):
+    """Stable grouping of observations by landmark -> (order, point_ptr)
+    (``vo_ba_group_by_point``: one counting sort on the host)."""
+    obs_pt = np.ascontiguousarray(obs_pt, dtype=np.int32).reshape(-1)
+    order = np.empty(obs_pt.size, dtype=np.int32)
+    ptr_ = np.empty(int(n_points) + 1, dtype=np.int32)
+    rc = _lib.load().vo_ba_group_by_point(int(n_points), obs_pt.size, ptr(obs_pt, C.c_int32),
+                                          ptr(order, C.c_int32), ptr(ptr_, C.c_int32))
+    if rc != _lib.VO_OK:
         raise ValueError("obs_pt out of range")
-    order = np.argsort(obs_pt, kind="stable")
-    ptr_ = np.zeros(n_points + 1, dtype=np.int32)
-    ptr_[1:] = np.cumsum(np.bincount(obs_pt, minlength=n_points))
     return order, ptr_
+
+
+def group_window(n_points: int, window: "BAWindow"):
+    """The window's observations grouped by landmark -> (point_ptr, obs_cam, obs_uv).
+    Windows built landmark by landmark (dropin/hooks.py ``KeyframeWindow.build``) are
+    already grouped: their arrays pass through unchanged; others are reordered by
+    ``csr_from_obs_pt``."""
+    obs_pt = np.asarray(window.obs_pt)
+    obs_cam = np.asarray(window.obs_cam)
+    obs_uv = np.asarray(window.obs_uv, dtype=np.float32).reshape(-1, 2)
+    n = obs_pt.size
+    if n and obs_pt[0] >= 0 and obs_pt[-1] < n_points and bool(np.all(obs_pt[1:] >= obs_pt[:-1])):
+        point_ptr = np.zeros(n_points + 1, np.int32)
+        np.cumsum(np.bincount(obs_pt, minlength=n_points), out=point_ptr[1:])
+        return point_ptr, obs_cam, obs_uv
+    order, point_ptr = csr_from_obs_pt(n_points, obs_pt)
+    return point_ptr, obs_cam[order], obs_uv[order]
 
 
 def _problem_struct(K, point_ptr, obs_cam, obs_uv, n_poses, n_fixed, lam):
@@ -219,9 +238,7 @@ class SlidingWindowBA:
         if poses.shape[0] == 0 or pts.shape[0] == 0 or np.asarray(window.obs_cam).size == 0 \
                 or poses.shape[0] <= n_fixed:
             return BAResult(poses.copy(), pts.copy(), np.zeros(0), "skipped", "empty window")
-        order, point_ptr = csr_from_obs_pt(pts.shape[0], window.obs_pt)
-        obs_cam = np.asarray(window.obs_cam)[order]
-        obs_uv = np.asarray(window.obs_uv, dtype=np.float32).reshape(-1, 2)[order]
+        point_ptr, obs_cam, obs_uv = group_window(pts.shape[0], window)
         ctx = _lib.context(self.device)
         try:
             sess = BASession(self.K, point_ptr, obs_cam, obs_uv, poses.shape[0], n_fixed, self.lam, ctx)

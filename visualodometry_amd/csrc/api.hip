@@ -625,6 +625,22 @@ int vo_ba_plan_digest(const vo_ba_problem* prob, int target_segments, uint64_t* 
   });
 }
 
+int vo_ba_group_by_point(int n_points, int n_obs, const int32_t* obs_pt, int32_t* order, int32_t* point_ptr) {
+  return guarded([&] {
+    VO_REQUIRE(n_points >= 0 && n_obs >= 0, VO_ERR_ARG, "vo_ba_group_by_point: bad sizes");
+    VO_REQUIRE(point_ptr && (n_obs == 0 || (obs_pt && order)), VO_ERR_ARG, "vo_ba_group_by_point: null argument");
+    std::fill(point_ptr, point_ptr + n_points + 1, 0);
+    for (int o = 0; o < n_obs; ++o) {
+      VO_REQUIRE(obs_pt[o] >= 0 && obs_pt[o] < n_points, VO_ERR_ARG, "vo_ba_group_by_point: obs_pt[%d]=%d out of range",
+                 o, obs_pt[o]);
+      ++point_ptr[obs_pt[o] + 1];
+    }
+    for (int p = 0; p < n_points; ++p) point_ptr[p + 1] += point_ptr[p];
+    std::vector<int32_t> next(point_ptr, point_ptr + std::max(n_points, 1));
+    for (int o = 0; o < n_obs; ++o) order[next[obs_pt[o]]++] = o;  // stable: caller order within a landmark
+  });
+}
+
 int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* out, int n) {
   int k = 0;
   int g = guarded([&] {
@@ -637,8 +653,7 @@ int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* ou
     VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_plan_probe: %s", err.c_str());
     vo::build_profile(P, vo::local_profile_first(P));
     int64_t max_pairs = 0, max_slots = 0, max_cams = 0;
-    for (int c = 0; c < P.n_chunks(); ++c) {
-      int s = 0;
+    for (int c = 0, s = 0; c < P.n_chunks(); ++c) {
       while (s + 1 < P.n_segments() + 1 && P.seg_chunk[s + 1] <= c) ++s;
       const int ns = P.seg_slot_off[s + 1] - P.seg_slot_off[s];
       const int b = P.chunk_slot_base[c];

@@ -145,37 +145,11 @@ enum { kBacksub = 1, kAccum = 2 };
 struct LinArgs {
   int n_fixed;
   double fx, fy, cx, cy, lambda;
-  const float2* obs_uv;
-  const int* obs_cam;
-  const int* obs_te;
-  const int* te_cam;
-  const int* te_pt;
-  const int* te_obs;
-  const int16_t* te_lcam;
-  const int* pt_te;
-  const int* chunk_obs;
-  const int* chunk_te;
-  const int* chunk_pt;
-  const int* chunk_slot_base;
-  const int* chunk_cam_base;
   const int4* chunk_hdr;  // kChunkHdr ints per chunk (BAPlan::chunk_hdr)
   const ChunkImg* chunk_img;  // BAPlan::chunk_img
   const int* slab_pos;        // BAPlan::slab_pos (window slot -> slab row)
   const int* cam_pos;         // BAPlan::cam_pos (window camera -> rhs slab row)
   const int* seg_hdr;     // kSegHdr ints per segment (BAPlan::seg_hdr)
-  const int* seg_acam_off;
-  const int* seg_acam;
-  const uint8_t* obs_acam;
-  const int* slot_ptr;
-  const uint16_t* pair_list;
-  const int* cam_ptr;
-  const uint8_t* cam_list;
-  const int* camo_ptr;
-  const uint8_t* camo_list;
-  const int* segcam_diag;
-  const int* seg_chunk;
-  const int* seg_slot_off;
-  const int* seg_cam_off;
   double* points;
   double* slab;
   double* slab_b;
@@ -183,7 +157,6 @@ struct LinArgs {
   const double* pose_old;  // linearisation of the pending step (back-substitution)
   const double* pose_new;  // current linearisation point
   const double* dc;        // pending pose update (6 per free camera)
-  const int* segcam_f;     // free camera of each segment window camera
   const int* status;
   unsigned long long* stamps;  // diagnostic build only: per segment phase cycles
 };
@@ -729,11 +702,9 @@ struct ReduceArgs {
   int nprof, F, nseg;
   double lambda;
   const int* prof_src_ptr;
-  const int* prof_src;
   const uint8_t* prof_diag;
   const int* prof_diag_cam;  // free camera of each profile block (its block row)
   const int* camb_ptr;
-  const int* camb_src;
   const double* slab;
   const double* slab_b;
   const double* slab_cost;
@@ -1223,8 +1194,8 @@ __global__ __launch_bounds__(64 * NW) void ba_solve_kernel(SolveArgs A) {
 }
 
 
-template <class T>
-void upload(DevBuf& buf, const std::vector<T>& v, hipStream_t st) {
+template <class T, class A>
+void upload(DevBuf& buf, const std::vector<T, A>& v, hipStream_t st) {
   buf.reserve(std::max<size_t>(v.size(), 1) * sizeof(T));
   if (!v.empty())
     VO_HIP_CHECK(hipMemcpyAsync(buf.ptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
@@ -1244,6 +1215,9 @@ class BAEngine {
   // collective: with a communicator, all ranks then agree (min all-reduce of [ok, F, -F])
   // and fail together, so one rank's bad shard is an error everywhere, not a hang.
   uint64_t setup(const vo_ba_problem* prob) {
+#ifdef VO_PLAN_TIMING
+    auto t_ = std::chrono::steady_clock::now();
+#endif
     have_problem_ = false;
     have_state_ = false;
     std::string err;
@@ -1272,6 +1246,7 @@ class BAEngine {
       if (err.empty() && agree[1] != -agree[2]) err = "ranks disagree on the number of free poses";
     }
     VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_setup: %s", err.c_str());
+    PLAN_T("setup: plan");
     std::vector<int32_t> first = local_profile_first(plan_);
     if (ctx_->comm && ctx_->comm->nranks > 1 && !first.empty()) {
       DevBuf tmp;
@@ -1282,6 +1257,7 @@ class BAEngine {
       VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
     }
     build_profile(plan_, first);
+    PLAN_T("setup: profile");
     prob_ = *prob;
     prob_.point_ptr = nullptr;
     prob_.obs_cam = nullptr;
@@ -1289,39 +1265,12 @@ class BAEngine {
 
     hipStream_t st = ctx_->stream;
     const BAPlan& P = plan_;
-    upload(d_obs_uv_, P.obs_uv, st);
-    upload(d_obs_cam_, P.obs_cam, st);
-    upload(d_obs_te_, P.obs_te, st);
-    upload(d_te_cam_, P.te_cam, st);
-    upload(d_te_pt_, P.te_pt, st);
-    upload(d_te_obs_, P.te_obs, st);
-    upload(d_te_lcam_, P.te_lcam, st);
-    upload(d_pt_te_, P.pt_te, st);
-    upload(d_chunk_obs_, P.chunk_obs, st);
-    upload(d_chunk_te_, P.chunk_te, st);
-    upload(d_chunk_pt_, P.chunk_pt, st);
-    upload(d_chunk_slot_base_, P.chunk_slot_base, st);
-    upload(d_chunk_cam_base_, P.chunk_cam_base, st);
     upload(d_chunk_hdr_, P.chunk_hdr, st);
     upload(d_chunk_img_, P.chunk_img, st);
     upload(d_slab_pos_, P.slab_pos, st);
     upload(d_cam_pos_, P.cam_pos, st);
     upload(d_seg_hdr_, P.seg_hdr, st);
-    upload(d_seg_acam_off_, P.seg_acam_off, st);
-    upload(d_seg_acam_, P.seg_acam, st);
-    upload(d_obs_acam_, P.obs_acam, st);
-    upload(d_slot_ptr_, P.slot_ptr, st);
-    upload(d_pair_list_, P.pair_list, st);
-    upload(d_cam_ptr_, P.cam_ptr, st);
-    upload(d_cam_list_, P.cam_list, st);
-    upload(d_seg_chunk_, P.seg_chunk, st);
-    upload(d_seg_slot_off_, P.seg_slot_off, st);
-    upload(d_seg_cam_off_, P.seg_cam_off, st);
-    upload(d_prof_first_, P.prof_first, st);
-    upload(d_prof_off_, P.prof_off, st);
-    upload(d_prof_last_, P.prof_last, st);
     upload(d_prof_src_ptr_, P.prof_src_ptr, st);
-    upload(d_prof_src_, P.prof_src, st);
     upload(d_prof_diag_, P.prof_diag, st);
     {
       std::vector<int32_t> row(std::max(1, P.n_prof_blocks()), 0);
@@ -1330,11 +1279,7 @@ class BAEngine {
       upload(d_prof_row_, row, st);
     }
     upload(d_camb_ptr_, P.camb_ptr, st);
-    upload(d_camb_src_, P.camb_src, st);
-    upload(d_segcam_f_, P.segcam_f, st);
-    upload(d_camo_ptr_, P.camo_ptr, st);
-    upload(d_camo_list_, P.camo_list, st);
-    upload(d_segcam_diag_, P.segcam_diag, st);
+    PLAN_T("setup: uploads");
     const int F = P.n_free;
     d_points_.reserve(std::max(1, P.n_points) * 24ull);
     d_pose_[0].reserve(P.n_poses * 96ull);
@@ -1356,6 +1301,7 @@ class BAEngine {
                  "vo_ba_setup: %d free poses / panel of %d blocks exceed the solver's LDS budget", F,
                  TL.max_panel);
     }
+    PLAN_T("setup: bufs");
     const size_t lds = solve_layout_.total;
     solve_lds_size_ = lds;
     {  // banded K3 when the block bandwidth and F fit it; the profile solver otherwise
@@ -1399,12 +1345,15 @@ class BAEngine {
       d_zero_.reserve(512);  // zero block (masked prefetches)
       VO_HIP_CHECK(hipMemsetAsync(d_zero_.ptr, 0, 512, st));
     }
+    PLAN_T("setup: band");
     {
       const int l = (int)lds;
       set_solve_lds<true>(l);
       set_solve_lds<false>(l);
     }
+    PLAN_T("setup: attrs");
     VO_HIP_CHECK(hipStreamSynchronize(st));
+    PLAN_T("setup: sync");
     have_problem_ = true;
     have_state_ = false;
     pending_ = false;
@@ -1556,37 +1505,11 @@ class BAEngine {
     A.n_fixed = P.n_fixed;
     A.fx = prob_.fx; A.fy = prob_.fy; A.cx = prob_.cx; A.cy = prob_.cy;
     A.lambda = prob_.lambda;
-    A.obs_uv = d_obs_uv_.as<float2>();
-    A.obs_cam = d_obs_cam_.as<int>();
-    A.obs_te = d_obs_te_.as<int>();
-    A.te_cam = d_te_cam_.as<int>();
-    A.te_pt = d_te_pt_.as<int>();
-    A.te_obs = d_te_obs_.as<int>();
-    A.te_lcam = d_te_lcam_.as<int16_t>();
-    A.pt_te = d_pt_te_.as<int>();
-    A.chunk_obs = d_chunk_obs_.as<int>();
-    A.chunk_te = d_chunk_te_.as<int>();
-    A.chunk_pt = d_chunk_pt_.as<int>();
-    A.chunk_slot_base = d_chunk_slot_base_.as<int>();
-    A.chunk_cam_base = d_chunk_cam_base_.as<int>();
     A.chunk_hdr = d_chunk_hdr_.as<int4>();
     A.chunk_img = d_chunk_img_.as<ChunkImg>();
     A.slab_pos = d_slab_pos_.as<int>();
     A.cam_pos = d_cam_pos_.as<int>();
     A.seg_hdr = d_seg_hdr_.as<int>();
-    A.seg_acam_off = d_seg_acam_off_.as<int>();
-    A.seg_acam = d_seg_acam_.as<int>();
-    A.obs_acam = d_obs_acam_.as<uint8_t>();
-    A.slot_ptr = d_slot_ptr_.as<int>();
-    A.pair_list = d_pair_list_.as<uint16_t>();
-    A.cam_ptr = d_cam_ptr_.as<int>();
-    A.cam_list = d_cam_list_.as<uint8_t>();
-    A.camo_ptr = d_camo_ptr_.as<int>();
-    A.camo_list = d_camo_list_.as<uint8_t>();
-    A.segcam_diag = d_segcam_diag_.as<int>();
-    A.seg_chunk = d_seg_chunk_.as<int>();
-    A.seg_slot_off = d_seg_slot_off_.as<int>();
-    A.seg_cam_off = d_seg_cam_off_.as<int>();
     A.points = d_points_.as<double>();
     A.slab = d_slab_.as<double>();
     A.slab_b = d_slab_b_.as<double>();
@@ -1594,7 +1517,6 @@ class BAEngine {
     A.pose_old = d_pose_[cur_ ^ 1].as<double>();
     A.pose_new = d_pose_[cur_].as<double>();
     A.dc = d_dc_.as<double>();
-    A.segcam_f = d_segcam_f_.as<int>();
     A.status = d_status_.as<int>();
     A.stamps = nullptr;
     return A;
@@ -1642,11 +1564,9 @@ class BAEngine {
     // systems of the landmark shards are all-reduced
     R.lambda = (ctx_->comm && ctx_->comm->rank > 0) ? 0.0 : prob_.lambda;
     R.prof_src_ptr = d_prof_src_ptr_.as<int>();
-    R.prof_src = d_prof_src_.as<int>();
     R.prof_diag = d_prof_diag_.as<uint8_t>();
     R.prof_diag_cam = d_prof_row_.as<int>();
     R.camb_ptr = d_camb_ptr_.as<int>();
-    R.camb_src = d_camb_src_.as<int>();
     R.slab = d_slab_.as<double>();
     R.slab_b = d_slab_b_.as<double>();
     R.slab_cost = d_slab_cost_.as<double>();
@@ -1800,15 +1720,8 @@ class BAEngine {
   std::vector<int32_t> red_dst_, red_rdst_;  // K2 output offsets (host copies for gn_step)
   long cost_off_ = 0;
   DevBuf d_solve_tab_;
-  DevBuf d_obs_uv_, d_obs_cam_, d_obs_te_, d_te_cam_, d_te_pt_, d_te_obs_, d_te_lcam_, d_pt_te_;
-  DevBuf d_chunk_obs_, d_chunk_te_, d_chunk_pt_, d_chunk_slot_base_, d_chunk_cam_base_, d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;
-  DevBuf d_seg_acam_off_, d_seg_acam_, d_obs_acam_;
-  DevBuf d_slot_ptr_, d_pair_list_, d_cam_ptr_, d_cam_list_;
-  DevBuf d_seg_chunk_, d_seg_slot_off_, d_seg_cam_off_;
-  DevBuf d_prof_first_, d_prof_off_, d_prof_last_, d_prof_src_ptr_, d_prof_src_, d_prof_diag_,
-      d_prof_row_;
-  DevBuf d_camb_ptr_, d_camb_src_, d_segcam_f_, d_stamps_, d_stamps3_;
-  DevBuf d_camo_ptr_, d_camo_list_, d_segcam_diag_;
+  DevBuf d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;  // K1's plan (the chunk images hold every list)
+  DevBuf d_prof_src_ptr_, d_prof_diag_, d_prof_row_, d_camb_ptr_, d_stamps_, d_stamps3_;
   static constexpr bool stamps_on_ = kBaStamps;
 
  public:

@@ -155,6 +155,14 @@ __device__ __forceinline__ void band_barrier() { asm volatile("s_waitcnt lgkmcnt
 #ifndef VO_BA_STAMPS
 #define VO_BA_STAMPS 0
 #endif
+// Tuning builds (EXTRA=-D...): VO_BA_DBCAST 0 broadcasts the diagonal block through LDS
+// instead of readlane; VO_BA_EXP != 0 disables one helper role (timing only, results wrong).
+#ifndef VO_BA_DBCAST
+#define VO_BA_DBCAST 0
+#endif
+#ifndef VO_BA_EXP
+#define VO_BA_EXP 0
+#endif
 // Diagnostic build only (EXTRA=-DVO_BA_STAMPS=1): lane 0 of each wave accumulates
 // s_memtime deltas per phase; the product build executes none.
 #if VO_BA_STAMPS
@@ -317,9 +325,21 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
 
   // Step k, before the barrier (column k in slot sk): factor the diagonal block, solve
   // this lane's panel row, write the panel and 1/diag into the ring.
-  auto chain_pre = [&](int sk) __attribute__((always_inline)) {
+  auto chain_pre = [&](int k, int sk) __attribute__((always_inline)) {
     double* col = sring + sk * SS;
     const int ocol = (int)(col - dyn);
+    double L[21], r[6];
+#if VO_BA_DBCAST
+    // the diagonal block's rows (group q == 0: lanes 6 (k mod R) + i) to every lane by
+    // readlane (uniform lane index): no LDS round trip on the chain
+    {
+      const int dl = 6 * (k % R);
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int c = 0; c <= i; ++c) L[P6(i, c)] = readlane_d(P[c], dl + i);
+    }
+#else
     // the diagonal block's rows (group q == 0) to every lane through LDS (other lanes
     // store to the dummy row: no divergent code on the chain)
     {
@@ -328,7 +348,6 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       st6g(dyn + o, P);
     }
     wave_sync<true>();
-    double L[21], r[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
@@ -337,6 +356,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
         L[P6(i, c)] = v.x;
         if (c + 1 <= i) L[P6(i, c + 1)] = v.y;
       }
+#endif
     BSETTLE(L[20]);
     BSTF(17);
     chol6_nochk(L, r);
@@ -463,10 +483,11 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   };
+  // VO_BA_EXP: 1 no trail, 2 no fwd, 3 no loader
   auto side_step = [&](int p, int sk, int skm) __attribute__((always_inline)) {
-    if (role == kTrail) trail_step(p, sk);
-    else if (role == kFwd) fwd_step(p, sk);
-    else if (role == kLoad) load_step(p, skm);
+    if (role == kTrail) { if (VO_BA_EXP != 1) trail_step(p, sk); }
+    else if (role == kFwd) { if (VO_BA_EXP != 2) fwd_step(p, sk); }
+    else if (role == kLoad) { if (VO_BA_EXP != 3) load_step(p, skm); }
   };
 
   // Full mode: every block L_{k,i} (k - w <= i < k) is replaced by G = L_kk^-1 L_{k,i}
@@ -514,7 +535,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     for (int p = 0; p < PA; ++p) {
       const bool on = p < sna;
       const int sk1 = sk + 1 == RC ? 0 : sk + 1;
-      if (role == kChain && on) chain_pre(sk);
+      if (role == kChain && on) chain_pre(p, sk);
       BST(1);
       band_barrier();
       BST(2);
@@ -544,7 +565,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       int sk = m % RC, skm = sk == 0 ? RC - 1 : sk - 1;
       for (int p = m; p < m + sp; ++p) {
         const int sk1 = sk + 1 == RC ? 0 : sk + 1;
-        if (role == kChain && side == 0) chain_pre(sk);
+        if (role == kChain && side == 0) chain_pre(p, sk);
         BST(5);
         band_barrier();
         BST(6);

@@ -1,6 +1,9 @@
 // Host-side static planner for the BA Gauss-Newton step (see ba_plan.h).
 #include "ba_plan.h"
 
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 
 #include <algorithm>
@@ -34,9 +37,144 @@ int64_t BAPlan::algorithmic_bytes_per_iter() const {
          2 * F6 * F6 * 8 + F6 * 8 * 2;
 }
 
+namespace {
+
+// fn(t) for t = 0 .. n - 1 on n host threads (t = 0 on the caller).  Every use writes
+// disjoint, precomputed ranges, so the plan never depends on the thread count or timing.
+// Workers persist across plans (thread creation would cost more than a small phase); a
+// caller that finds the pool busy (another context planning) starts its own threads.
+class PlanPool {
+ public:
+  static PlanPool& get() {
+    static PlanPool pool;
+    return pool;
+  }
+  template <class Fn>
+  void run(int n, Fn&& fn) {
+    std::unique_lock<std::mutex> busy(use_, std::try_to_lock);
+    if (!busy.owns_lock() || n - 1 > (int)workers_.size()) {
+      std::vector<std::thread> pool;
+      for (int t = 1; t < n; ++t) pool.emplace_back([&fn, t] { fn(t); });
+      fn(0);
+      for (auto& th : pool) th.join();
+      return;
+    }
+    std::function<void(int)> job = [&fn](int t) { fn(t); };
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &job;
+      active_ = n - 1;
+      pending_ = n - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+  ~PlanPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& th : workers_) th.join();
+  }
+
+ private:
+  PlanPool() {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    for (unsigned t = 1; t < std::min(hw, 8u); ++t) workers_.emplace_back([this, t] { loop((int)t); });
+  }
+  void loop(int t) {
+    long seen = 0;
+    for (;;) {
+      std::function<void(int)>* job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        if (t > active_) continue;  // not needed this round
+        job = job_;
+      }
+      (*job)(t);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex use_, mu_;
+  std::condition_variable cv_, done_;
+  std::function<void(int)>* job_ = nullptr;
+  int active_ = 0, pending_ = 0;
+  long gen_ = 0;
+  bool stop_ = false;
+};
+
+template <class Fn>
+void run_parallel(int n, Fn&& fn) {
+  if (n <= 1) return fn(0);
+  PlanPool::get().run(n, fn);
+}
+
+int plan_threads(int64_t work) {
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  return (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::min(hw, 8u), work / 2048 + 1}));
+}
+
+// Landmark ranges packed independently (a segment boundary at every range start): a
+// fixed function of the landmark count, never of the host, so the plan is the same on
+// every machine.
+#ifndef VO_PLAN_PARTS
+#define VO_PLAN_PARTS 8
+#endif
+constexpr int kPlanParts = VO_PLAN_PARTS;
+int plan_parts(int L) { return std::max(1, std::min(kPlanParts, L / 2048)); }
+
+struct PlanSeg {
+  int chunk0;                               // first chunk (global index after the merge)
+  std::vector<int32_t> cams, acams;         // free / all cameras (unsorted while growing)
+  std::vector<std::pair<int32_t, int32_t>> slots;
+};
+
+// one landmark range's greedy packing: chunks (first landmark, pair count, free track
+// entries, free observations) and segments (first chunk, local index)
+struct PlanPart {
+  std::vector<int32_t> chunk_q, chunk_pairs, chunk_fte, chunk_fobs;
+  std::vector<PlanSeg> segs;
+  int err_q = -1;
+  std::string err;
+};
+
+}  // namespace
+
+void BAPlan::reset() {
+  n_poses = n_points = n_obs = n_fixed = n_free = n_te = 0;
+  for (auto* v : {&pt_perm, &obs_cam, &obs_te, &te_cam, &te_pt, &te_obs, &pt_te, &chunk_obs, &chunk_te,
+                  &chunk_pt, &chunk_slot_base, &chunk_cam_base, &chunk_hdr, &slab_pos, &cam_pos, &seg_hdr,
+                  &slot_ptr, &cam_ptr, &camo_ptr, &seg_chunk, &seg_slot_off, &seg_cam_off, &slot_i, &slot_j,
+                  &segcam_f, &segcam_diag, &seg_acam_off, &seg_acam, &prof_first, &prof_off, &prof_last,
+                  &prof_src_ptr, &prof_src, &camb_ptr, &camb_src, &solve_tab})
+    v->clear();
+  obs_uv.clear();
+  te_lcam.clear();
+  chunk_img.clear();
+  pair_list.clear();
+  cam_list.clear();
+  camo_list.clear();
+  obs_acam.clear();
+  prof_diag.clear();
+  solve_layout = SolveTableLayout();
+}
+
 std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_t* point_ptr,
                        const int32_t* obs_cam, const float* obs_uv, int target_segments) {
-  P = BAPlan();
+#ifdef VO_PLAN_TIMING
+  auto t_ = std::chrono::steady_clock::now();
+#endif
+  P.reset();
   if (N < 1 || L < 0 || M < 0) return fmt("bad sizes n_poses=%ld n_points=%ld n_obs=%ld", N, L, M);
   if (N > 32767) return fmt("n_poses=%ld exceeds the 32767 camera ids of a segment header", N);
   if (n_fixed < 0 || n_fixed > N) return fmt("bad n_fixed=%ld (n_poses=%ld)", n_fixed, N);
@@ -51,324 +189,404 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   P.n_obs = M;
   P.n_fixed = n_fixed;
   P.n_free = N - n_fixed;
+  const int nthr = plan_threads(M);
 
-  // landmarks ordered by first camera: keeps each workgroup's camera window narrow
-  std::vector<int32_t> first(L, N);
-  for (int p = 0; p < L; ++p)
-    for (int o = point_ptr[p]; o < point_ptr[p + 1]; ++o) first[p] = std::min(first[p], obs_cam[o]);
-  P.pt_perm.resize(L);
-  std::iota(P.pt_perm.begin(), P.pt_perm.end(), 0);
-  std::stable_sort(P.pt_perm.begin(), P.pt_perm.end(),
-                   [&](int a, int b) { return first[a] < first[b]; });
-
-  // observations grouped by (landmark, camera) -> track entries
-  P.obs_uv.reserve(2 * (size_t)M);
-  P.obs_cam.reserve(M);
-  P.obs_te.reserve(M);
-  P.pt_te.assign(1, 0);
-  std::vector<int32_t> idx;
-  for (int q = 0; q < L; ++q) {
-    const int p = P.pt_perm[q];
-    idx.resize(point_ptr[p + 1] - point_ptr[p]);
-    std::iota(idx.begin(), idx.end(), point_ptr[p]);
-    // stable insertion sort by camera (tracks are short; no allocation per landmark)
-    for (size_t i = 1; i < idx.size(); ++i) {
-      const int32_t v = idx[i];
-      size_t j = i;
-      while (j > 0 && obs_cam[idx[j - 1]] > obs_cam[v]) {
-        idx[j] = idx[j - 1];
-        --j;
-      }
-      idx[j] = v;
+  // landmarks ordered by first camera (stable counting sort; no observation: last), which
+  // keeps each workgroup's camera window narrow
+  {
+    std::vector<int32_t> first(L), cnt(N + 2, 0);
+    for (int p = 0; p < L; ++p) {
+      int f = N;
+      for (int o = point_ptr[p]; o < point_ptr[p + 1]; ++o) f = std::min(f, (int)obs_cam[o]);
+      first[p] = f;
+      ++cnt[f + 1];
     }
-    for (size_t k = 0; k < idx.size(); ++k) {
-      const int o = idx[k];
-      if (k == 0 || obs_cam[o] != obs_cam[idx[k - 1]]) {
-        P.te_cam.push_back(obs_cam[o]);
-        P.te_pt.push_back(q);
-        P.te_obs.push_back((int32_t)P.obs_cam.size());
-      }
-      P.obs_uv.push_back(obs_uv[2 * o]);
-      P.obs_uv.push_back(obs_uv[2 * o + 1]);
-      P.obs_cam.push_back(obs_cam[o]);
-      P.obs_te.push_back((int32_t)P.te_cam.size() - 1);
-    }
-    P.pt_te.push_back((int32_t)P.te_cam.size());
+    for (int c = 0; c <= N; ++c) cnt[c + 1] += cnt[c];
+    P.pt_perm.resize(L);
+    for (int p = 0; p < L; ++p) P.pt_perm[cnt[first[p]]++] = p;
   }
-  P.n_te = (int)P.te_cam.size();
-  P.te_obs.push_back(M);
-  P.te_lcam.assign(P.n_te, -1);
+  PLAN_T("order");
 
-  // ---- chunks and segments
+  // observations grouped by (landmark, camera) -> track entries.  Pass A sorts each
+  // landmark's observations by camera (stable) into its slot and counts its track
+  // entries; pass B writes every array at the prefix offsets.
+  std::vector<int32_t> ob_start(L + 1), sorted(std::max(M, 1)), te_start(L + 1);
+  ob_start[0] = 0;
+  for (int q = 0; q < L; ++q) ob_start[q + 1] = ob_start[q] + point_ptr[P.pt_perm[q] + 1] - point_ptr[P.pt_perm[q]];
+  auto qrange = [&](int t, int n) { return std::make_pair((int)((int64_t)L * t / n), (int)((int64_t)L * (t + 1) / n)); };
+  run_parallel(nthr, [&](int t) {
+    const auto [qa, qb] = qrange(t, nthr);
+    for (int q = qa; q < qb; ++q) {
+      const int p = P.pt_perm[q], n = point_ptr[p + 1] - point_ptr[p];
+      int32_t* idx = &sorted[ob_start[q]];
+      for (int i = 0; i < n; ++i) {  // stable insertion sort by camera (tracks are short)
+        const int32_t v = point_ptr[p] + i;
+        int j = i;
+        while (j > 0 && obs_cam[idx[j - 1]] > obs_cam[v]) {
+          idx[j] = idx[j - 1];
+          --j;
+        }
+        idx[j] = v;
+      }
+      int nte = 0;
+      for (int k = 0; k < n; ++k) nte += k == 0 || obs_cam[idx[k]] != obs_cam[idx[k - 1]];
+      te_start[q + 1] = nte;
+    }
+  });
+  te_start[0] = 0;
+  for (int q = 0; q < L; ++q) te_start[q + 1] += te_start[q];
+  P.n_te = te_start[L];
+  P.obs_uv.resize(2 * (size_t)M);
+  P.obs_cam.resize(M);
+  P.obs_te.resize(M);
+  P.te_cam.resize(P.n_te);
+  P.te_pt.resize(P.n_te);
+  P.te_obs.resize(P.n_te + 1);
+  P.pt_te.resize(L + 1);
+  run_parallel(nthr, [&](int t) {
+    const auto [qa, qb] = qrange(t, nthr);
+    for (int q = qa; q < qb; ++q) {
+      int te = te_start[q] - 1;
+      P.pt_te[q] = te_start[q];
+      for (int pos = ob_start[q]; pos < ob_start[q + 1]; ++pos) {
+        const int o = sorted[pos];
+        if (pos == ob_start[q] || obs_cam[o] != obs_cam[sorted[pos - 1]]) {
+          ++te;
+          P.te_cam[te] = obs_cam[o];
+          P.te_pt[te] = q;
+          P.te_obs[te] = pos;
+        }
+        P.obs_uv[2 * (size_t)pos] = obs_uv[2 * (size_t)o];
+        P.obs_uv[2 * (size_t)pos + 1] = obs_uv[2 * (size_t)o + 1];
+        P.obs_cam[pos] = obs_cam[o];
+        P.obs_te[pos] = te;
+      }
+    }
+  });
+  P.pt_te[L] = P.n_te;
+  P.te_obs[P.n_te] = M;
+  P.te_lcam.assign(P.n_te, -1);
+  PLAN_T("track entries");
+
+  // ---- chunks and segments: each landmark range packed greedily on its own thread
   const int nseg_target = std::max(1, target_segments);
   const int64_t seg_obs_target = std::max<int64_t>(1, (M + nseg_target - 1) / nseg_target);
-  struct Seg {
-    int chunk0;
-    std::vector<int32_t> cams;                   // free cameras (unsorted while growing)
-    std::vector<int32_t> acams;                  // all cameras (unsorted while growing)
-    std::vector<std::pair<int32_t, int32_t>> slots;
-  };
-  std::vector<Seg> segs;
-  std::vector<int32_t> cq;
-  int c_obs = 0, c_te = 0, c_pts = 0, c_pairs = 0;
-  int64_t s_obs = 0;
-  bool seg_open = false;
-  auto open_chunk = [&](int q) {
-    P.chunk_obs.push_back(P.te_obs[P.pt_te[q]]);
-    P.chunk_te.push_back(P.pt_te[q]);
-    P.chunk_pt.push_back(q);
-    c_obs = c_te = c_pts = c_pairs = 0;
-  };
-  // membership of the open segment's cameras and camera pairs: stamp tables (stamp = the
-  // segment's number) when the free cameras are few, the linear searches otherwise
   const int Nf = N - n_fixed;
   const bool tables = Nf <= kPlanTableCams;
-  std::vector<int32_t> cam_stamp(tables ? N : 0, -1), fcam_stamp(tables ? std::max(Nf, 1) : 0, -1);
-  std::vector<int32_t> pair_stamp(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, -1);
-  auto seg_id = [&]() { return (int32_t)segs.size() - 1; };
-  for (int q = 0; q < L; ++q) {
-    const int t0 = P.pt_te[q], t1 = P.pt_te[q + 1];
-    const int nob = P.te_obs[t1] - P.te_obs[t0], nte = t1 - t0;
-    cq.clear();
-    for (int t = t0; t < t1; ++t)
-      if (P.te_cam[t] >= n_fixed) cq.push_back(P.te_cam[t] - n_fixed);
-    if (t1 - t0 > kSegAllCams)
-      return fmt("landmark %ld is too wide (%ld cameras); limit: %ld cameras per landmark", P.pt_perm[q],
-                 t1 - t0, (long)kSegAllCams);
-    const int k = (int)cq.size();
-    if (nob > kChunkObs || nte > kChunkTe || k > kSegCams || k * (k + 1) / 2 > kSegSlots)
-      return fmt("landmark %ld is too wide (%ld observations, %ld free cameras); "
-                 "limits: 64 observations, 10 free cameras per landmark",
-                 P.pt_perm[q], nob, k);
-    const int npairs = k * (k + 1) / 2;
-    bool chunk_fits = seg_open && c_obs + nob <= kChunkObs && c_te + nte <= kChunkTe &&
-                      c_pts + 1 <= kChunkPts && c_pairs + npairs <= kChunkPairs;
-    bool seg_fits = seg_open;
-    if (seg_open) {
-      Seg& s = segs.back();
-      const int32_t sid = seg_id();
-      int ncams = (int)s.cams.size();
-      int nslots = (int)s.slots.size();
-      int nacams = (int)s.acams.size();
+  const int nparts = plan_parts(L);
+  std::vector<PlanPart> parts(nparts);
+  auto pack = [&](int pi) {
+    PlanPart& R = parts[pi];
+    const int qa = (int)((int64_t)L * pi / nparts), qb = (int)((int64_t)L * (pi + 1) / nparts);
+    // membership of the open segment's cameras and camera pairs: stamp tables (stamp = the
+    // segment's local number) when the free cameras are few, the linear searches otherwise
+    std::vector<int32_t> cam_stamp(tables ? N : 0, -1), fcam_stamp(tables ? std::max(Nf, 1) : 0, -1);
+    std::vector<int32_t> pair_stamp(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, -1);
+    std::vector<int32_t> cq;
+    int c_obs = 0, c_te = 0, c_pts = 0, c_pairs = 0;
+    int64_t s_obs = 0;
+    bool seg_open = false;
+    auto open_chunk = [&](int q) {
+      R.chunk_q.push_back(q);
+      R.chunk_pairs.push_back(0);
+      R.chunk_fte.push_back(0);
+      R.chunk_fobs.push_back(0);
+      c_obs = c_te = c_pts = c_pairs = 0;
+    };
+    for (int q = qa; q < qb; ++q) {
+      const int t0 = P.pt_te[q], t1 = P.pt_te[q + 1];
+      const int nob = P.te_obs[t1] - P.te_obs[t0], nte = t1 - t0;
+      cq.clear();
+      int fobs = 0;
+      for (int t = t0; t < t1; ++t)
+        if (P.te_cam[t] >= n_fixed) {
+          cq.push_back(P.te_cam[t] - n_fixed);
+          fobs += P.te_obs[t + 1] - P.te_obs[t];
+        }
+      if (t1 - t0 > kSegAllCams) {
+        R.err_q = q;
+        R.err = fmt("landmark %ld is too wide (%ld cameras); limit: %ld cameras per landmark", P.pt_perm[q], t1 - t0,
+                    (long)kSegAllCams);
+        return;
+      }
+      const int k = (int)cq.size();
+      if (nob > kChunkObs || nte > kChunkTe || k > kSegCams || k * (k + 1) / 2 > kSegSlots) {
+        R.err_q = q;
+        R.err = fmt("landmark %ld is too wide (%ld observations, %ld free cameras); "
+                    "limits: 64 observations, 10 free cameras per landmark",
+                    P.pt_perm[q], nob, k);
+        return;
+      }
+      const int npairs = k * (k + 1) / 2;
+      const bool chunk_fits = seg_open && c_obs + nob <= kChunkObs && c_te + nte <= kChunkTe &&
+                              c_pts + 1 <= kChunkPts && c_pairs + npairs <= kChunkPairs;
+      bool seg_fits = seg_open;
+      if (seg_open) {
+        PlanSeg& s = R.segs.back();
+        const int32_t sid = (int32_t)R.segs.size() - 1;
+        int ncams = (int)s.cams.size(), nslots = (int)s.slots.size(), nacams = (int)s.acams.size();
+        if (tables) {
+          for (int c : cq) ncams += fcam_stamp[c] != sid;
+          for (int a = 0; a < k; ++a)
+            for (int b = 0; b <= a; ++b)
+              nslots += pair_stamp[(size_t)std::max(cq[a], cq[b]) * Nf + std::min(cq[a], cq[b])] != sid;
+          for (int t = t0; t < t1; ++t) nacams += cam_stamp[P.te_cam[t]] != sid;
+        } else {
+          for (int c : cq) ncams += find_or_neg(s.cams, c) < 0;
+          for (int a = 0; a < k; ++a)
+            for (int b = 0; b <= a; ++b) {
+              const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
+              nslots += std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end();
+            }
+          for (int t = t0; t < t1; ++t) nacams += find_or_neg(s.acams, P.te_cam[t]) < 0;
+        }
+        seg_fits = ncams <= kSegCams && nslots <= kSegSlots && nacams <= kSegAllCams;
+      }
+      if (!seg_fits || (!chunk_fits && s_obs >= seg_obs_target)) {
+        R.segs.push_back(PlanSeg{(int)R.chunk_q.size(), {}, {}, {}});
+        seg_open = true;
+        s_obs = 0;
+        open_chunk(q);
+      } else if (!chunk_fits) {
+        open_chunk(q);
+      }
+      PlanSeg& s = R.segs.back();
+      const int32_t sid = (int32_t)R.segs.size() - 1;
       if (tables) {
-        for (int c : cq) ncams += fcam_stamp[c] != sid;
+        for (int c : cq)
+          if (fcam_stamp[c] != sid) {
+            fcam_stamp[c] = sid;
+            s.cams.push_back(c);
+          }
+        for (int t = t0; t < t1; ++t)
+          if (cam_stamp[P.te_cam[t]] != sid) {
+            cam_stamp[P.te_cam[t]] = sid;
+            s.acams.push_back(P.te_cam[t]);
+          }
         for (int a = 0; a < k; ++a)
-          for (int b = 0; b <= a; ++b)
-            nslots += pair_stamp[(size_t)std::max(cq[a], cq[b]) * Nf + std::min(cq[a], cq[b])] != sid;
-        for (int t = t0; t < t1; ++t) nacams += cam_stamp[P.te_cam[t]] != sid;
+          for (int b = 0; b <= a; ++b) {
+            const int32_t hi = std::max(cq[a], cq[b]), lo = std::min(cq[a], cq[b]);
+            int32_t& st = pair_stamp[(size_t)hi * Nf + lo];
+            if (st != sid) {
+              st = sid;
+              s.slots.push_back(std::make_pair(hi, lo));
+            }
+          }
       } else {
-        for (int c : cq) ncams += find_or_neg(s.cams, c) < 0;
+        for (int c : cq)
+          if (find_or_neg(s.cams, c) < 0) s.cams.push_back(c);
+        for (int t = t0; t < t1; ++t)
+          if (find_or_neg(s.acams, P.te_cam[t]) < 0) s.acams.push_back(P.te_cam[t]);
         for (int a = 0; a < k; ++a)
           for (int b = 0; b <= a; ++b) {
             const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
-            nslots += std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end();
+            if (std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end()) s.slots.push_back(pr);
           }
-        for (int t = t0; t < t1; ++t) nacams += find_or_neg(s.acams, P.te_cam[t]) < 0;
       }
-      seg_fits = ncams <= kSegCams && nslots <= kSegSlots && nacams <= kSegAllCams;
+      c_obs += nob;
+      c_te += nte;
+      c_pts += 1;
+      c_pairs += npairs;
+      s_obs += nob;
+      R.chunk_pairs.back() += npairs;
+      R.chunk_fte.back() += k;
+      R.chunk_fobs.back() += fobs;
     }
-    if (!seg_fits || (!chunk_fits && s_obs >= seg_obs_target)) {
-      segs.push_back(Seg{(int)P.chunk_obs.size(), {}, {}, {}});
-      seg_open = true;
-      s_obs = 0;
-      open_chunk(q);
-    } else if (!chunk_fits) {
-      open_chunk(q);
+  };
+  run_parallel(std::min(nparts, nthr), [&](int t) {
+    const int nt = std::min(nparts, nthr);
+    for (int pi = t; pi < nparts; pi += nt) pack(pi);
+  });
+  for (const PlanPart& R : parts)  // the first error in landmark order
+    if (R.err_q >= 0) return R.err;
+  // merge the ranges: chunks and segments in landmark order
+  std::vector<PlanSeg> segs;
+  std::vector<int32_t> ch_pairs, ch_fte, ch_fobs;
+  for (PlanPart& R : parts) {
+    const int base = (int)P.chunk_pt.size();
+    for (size_t c = 0; c < R.chunk_q.size(); ++c) {
+      const int q = R.chunk_q[c];
+      P.chunk_obs.push_back(P.te_obs[P.pt_te[q]]);
+      P.chunk_te.push_back(P.pt_te[q]);
+      P.chunk_pt.push_back(q);
     }
-    Seg& s = segs.back();
-    const int32_t sid = seg_id();
-    if (tables) {
-      for (int c : cq)
-        if (fcam_stamp[c] != sid) {
-          fcam_stamp[c] = sid;
-          s.cams.push_back(c);
-        }
-      for (int t = t0; t < t1; ++t)
-        if (cam_stamp[P.te_cam[t]] != sid) {
-          cam_stamp[P.te_cam[t]] = sid;
-          s.acams.push_back(P.te_cam[t]);
-        }
-      for (int a = 0; a < k; ++a)
-        for (int b = 0; b <= a; ++b) {
-          const int32_t hi = std::max(cq[a], cq[b]), lo = std::min(cq[a], cq[b]);
-          int32_t& st = pair_stamp[(size_t)hi * Nf + lo];
-          if (st != sid) {
-            st = sid;
-            s.slots.push_back(std::make_pair(hi, lo));
-          }
-        }
-    } else {
-      for (int c : cq)
-        if (find_or_neg(s.cams, c) < 0) s.cams.push_back(c);
-      for (int t = t0; t < t1; ++t)
-        if (find_or_neg(s.acams, P.te_cam[t]) < 0) s.acams.push_back(P.te_cam[t]);
-      for (int a = 0; a < k; ++a)
-        for (int b = 0; b <= a; ++b) {
-          const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
-          if (std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end()) s.slots.push_back(pr);
-        }
+    ch_pairs.insert(ch_pairs.end(), R.chunk_pairs.begin(), R.chunk_pairs.end());
+    ch_fte.insert(ch_fte.end(), R.chunk_fte.begin(), R.chunk_fte.end());
+    ch_fobs.insert(ch_fobs.end(), R.chunk_fobs.begin(), R.chunk_fobs.end());
+    for (PlanSeg& s : R.segs) {
+      s.chunk0 += base;
+      segs.push_back(std::move(s));
     }
-    c_obs += nob;
-    c_te += nte;
-    c_pts += 1;
-    c_pairs += npairs;
-    s_obs += nob;
   }
   P.chunk_obs.push_back(M);
   P.chunk_te.push_back(P.n_te);
   P.chunk_pt.push_back(L);
+  PLAN_T("segments");
 
-  // ---- per segment: sorted windows, slab offsets, per chunk pair and camera lists
+  // ---- per segment: sorted windows, slab offsets, per chunk pair and camera lists,
+  // chunk headers and LDS images, segment headers.  Offsets first (prefix sums over
+  // segments and chunks), then segment ranges filled in parallel.
   const int nchunks = (int)P.chunk_obs.size() - 1;
-  P.seg_chunk.assign(1, 0);
-  P.seg_slot_off.assign(1, 0);
-  P.seg_cam_off.assign(1, 0);
-  P.seg_acam_off.assign(1, 0);
-  P.seg_acam.clear();
+  const int nseg = (int)segs.size();
+  std::vector<int32_t> seg_of(std::max(nchunks, 1), 0);
+  P.seg_chunk.resize(nseg + 1);
+  P.seg_slot_off.resize(nseg + 1);
+  P.seg_cam_off.resize(nseg + 1);
+  P.seg_acam_off.resize(nseg + 1);
+  P.seg_chunk[0] = P.seg_slot_off[0] = P.seg_cam_off[0] = P.seg_acam_off[0] = 0;
+  for (int si = 0; si < nseg; ++si) {
+    const PlanSeg& s = segs[si];
+    const int ch1 = si + 1 < nseg ? segs[si + 1].chunk0 : nchunks;
+    for (int ch = s.chunk0; ch < ch1; ++ch) seg_of[ch] = si;
+    P.seg_chunk[si + 1] = ch1;
+    P.seg_slot_off[si + 1] = P.seg_slot_off[si] + (int)s.slots.size();
+    P.seg_cam_off[si + 1] = P.seg_cam_off[si] + (int)s.cams.size();
+    P.seg_acam_off[si + 1] = P.seg_acam_off[si] + (int)s.acams.size();
+  }
+  // per chunk: its slot_ptr / cam_ptr rows and its pair / camera list ranges
+  std::vector<int32_t> pair_base(nchunks + 1), cl_base(nchunks + 1), col_base(nchunks + 1);
+  P.chunk_slot_base.resize(nchunks);
+  P.chunk_cam_base.resize(nchunks);
+  {
+    int32_t sb = 0, cb = 0;
+    pair_base[0] = cl_base[0] = col_base[0] = 0;
+    for (int ch = 0; ch < nchunks; ++ch) {
+      const PlanSeg& s = segs[seg_of[ch]];
+      P.chunk_slot_base[ch] = sb;
+      P.chunk_cam_base[ch] = cb;
+      sb += (int)s.slots.size() + 1;
+      cb += (int)s.cams.size() + 1;
+      pair_base[ch + 1] = pair_base[ch] + ch_pairs[ch];
+      cl_base[ch + 1] = cl_base[ch] + ch_fte[ch];
+      col_base[ch + 1] = col_base[ch] + ch_fobs[ch];
+    }
+    P.slot_ptr.resize(sb);
+    P.cam_ptr.resize(cb);
+    P.camo_ptr.resize(cb);
+  }
+  P.slot_i.resize(P.seg_slot_off[nseg]);
+  P.slot_j.resize(P.seg_slot_off[nseg]);
+  P.segcam_f.resize(P.seg_cam_off[nseg]);
+  P.segcam_diag.resize(P.seg_cam_off[nseg]);
+  P.seg_acam.resize(P.seg_acam_off[nseg]);
   P.obs_acam.assign(std::max(M, 1), 0);
-  P.chunk_slot_base.assign(nchunks, 0);
-  P.chunk_cam_base.assign(nchunks, 0);
-  // per-segment lookup tables (camera -> window index, camera pair -> slot) and reusable
-  // counting-sort buffers for the per-chunk lists
-  std::vector<int32_t> fcam_idx(tables ? std::max(Nf, 1) : 0, -1), acam_idx(tables ? N : 0, -1);
-  std::vector<int32_t> pair_slot(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, -1);
-  std::vector<int32_t> cnt, cnt2;
-  std::vector<uint16_t> pairs_tmp;
-  std::vector<int32_t> pairs_slot;
-  for (size_t si = 0; si < segs.size(); ++si) {
-    Seg& s = segs[si];
-    std::sort(s.cams.begin(), s.cams.end());
-    std::sort(s.slots.begin(), s.slots.end());
-    const int ch0 = s.chunk0;
-    const int ch1 = si + 1 < segs.size() ? segs[si + 1].chunk0 : nchunks;
-    for (auto& pr : s.slots) {
-      P.slot_i.push_back(pr.first);
-      P.slot_j.push_back(pr.second);
-    }
-    std::sort(s.acams.begin(), s.acams.end());
-    if (tables) {
-      for (size_t i = 0; i < s.cams.size(); ++i) fcam_idx[s.cams[i]] = (int32_t)i;
-      for (size_t i = 0; i < s.acams.size(); ++i) acam_idx[s.acams[i]] = (int32_t)i;
-      for (size_t i = 0; i < s.slots.size(); ++i) pair_slot[(size_t)s.slots[i].first * Nf + s.slots[i].second] = (int32_t)i;
-    }
-    auto lcam_of = [&](int32_t c) {  // window index of free camera c
-      return tables ? fcam_idx[c] : (int32_t)(std::lower_bound(s.cams.begin(), s.cams.end(), c) - s.cams.begin());
-    };
-    auto slot_of = [&](const std::pair<int32_t, int32_t>& pr) {
-      return tables ? pair_slot[(size_t)pr.first * Nf + pr.second]
-                    : (int32_t)(std::lower_bound(s.slots.begin(), s.slots.end(), pr) - s.slots.begin());
-    };
-    P.seg_acam.insert(P.seg_acam.end(), s.acams.begin(), s.acams.end());
-    P.seg_acam_off.push_back((int32_t)P.seg_acam.size());
-    for (int o = P.chunk_obs[ch0]; o < P.chunk_obs[ch1]; ++o)
-      P.obs_acam[o] = (uint8_t)(tables ? acam_idx[P.obs_cam[o]]
-                                       : std::lower_bound(s.acams.begin(), s.acams.end(), P.obs_cam[o]) -
-                                             s.acams.begin());
-    for (int c : s.cams) {
-      P.segcam_f.push_back(c);
-      P.segcam_diag.push_back(slot_of(std::make_pair(c, c)));
-    }
-    P.seg_chunk.push_back(ch1);
-    P.seg_slot_off.push_back((int32_t)P.slot_i.size());
-    P.seg_cam_off.push_back((int32_t)P.segcam_f.size());
-    const int ns = (int)s.slots.size(), nc = (int)s.cams.size();
-    for (int ch = ch0; ch < ch1; ++ch) {
-      const int te0 = P.chunk_te[ch];
-      for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
-        if (P.te_cam[t] >= n_fixed) P.te_lcam[t] = (int16_t)lcam_of(P.te_cam[t] - n_fixed);
-      // pair lists by slot: a stable counting sort of the (x, y) pairs in generation order
-      pairs_tmp.clear();
-      pairs_slot.clear();
-      for (int q = P.chunk_pt[ch]; q < P.chunk_pt[ch + 1]; ++q) {
-        for (int x = P.pt_te[q]; x < P.pt_te[q + 1]; ++x) {
-          if (P.te_cam[x] < n_fixed) continue;
-          for (int y = P.pt_te[q]; y <= x; ++y) {
-            if (P.te_cam[y] < n_fixed) continue;
-            pairs_slot.push_back(slot_of(std::make_pair(P.te_cam[x] - n_fixed, P.te_cam[y] - n_fixed)));
-            pairs_tmp.push_back((uint16_t)((x - te0) | ((y - te0) << 8)));
-          }
-        }
-      }
-      cnt.assign(ns + 1, 0);
-      for (int32_t sl : pairs_slot) ++cnt[sl + 1];
-      for (int sl = 0; sl < ns; ++sl) cnt[sl + 1] += cnt[sl];
-      P.chunk_slot_base[ch] = (int32_t)P.slot_ptr.size();
-      const int32_t pbase = (int32_t)P.pair_list.size();
-      for (int sl = 0; sl < ns; ++sl) P.slot_ptr.push_back(pbase + cnt[sl]);
-      P.slot_ptr.push_back(pbase + cnt[ns]);
-      P.pair_list.resize(pbase + pairs_tmp.size());
-      for (size_t e = 0; e < pairs_tmp.size(); ++e) P.pair_list[pbase + cnt[pairs_slot[e]]++] = pairs_tmp[e];
-      // camera lists: track entries and observations by window camera, in order
-      cnt.assign(nc + 1, 0);
-      for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
-        if (P.te_lcam[t] >= 0) ++cnt[P.te_lcam[t] + 1];
-      cnt2.assign(nc + 1, 0);
-      const int ob0 = P.chunk_obs[ch];
-      for (int o = ob0; o < P.chunk_obs[ch + 1]; ++o)
-        if (P.te_lcam[P.obs_te[o]] >= 0) ++cnt2[P.te_lcam[P.obs_te[o]] + 1];
-      for (int c = 0; c < nc; ++c) {
-        cnt[c + 1] += cnt[c];
-        cnt2[c + 1] += cnt2[c];
-      }
-      P.chunk_cam_base[ch] = (int32_t)P.cam_ptr.size();
-      const int32_t cbase = (int32_t)P.cam_list.size(), obase = (int32_t)P.camo_list.size();
-      for (int c = 0; c < nc; ++c) {
-        P.cam_ptr.push_back(cbase + cnt[c]);
-        P.camo_ptr.push_back(obase + cnt2[c]);
-      }
-      P.cam_ptr.push_back(cbase + cnt[nc]);
-      P.camo_ptr.push_back(obase + cnt2[nc]);
-      P.cam_list.resize(cbase + cnt[nc]);
-      P.camo_list.resize(obase + cnt2[nc]);
-      for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
-        if (P.te_lcam[t] >= 0) P.cam_list[cbase + cnt[P.te_lcam[t]]++] = (uint8_t)(t - te0);
-      for (int o = ob0; o < P.chunk_obs[ch + 1]; ++o) {
-        const int lc = P.te_lcam[P.obs_te[o]];
-        if (lc >= 0) P.camo_list[obase + cnt2[lc]++] = (uint8_t)(o - ob0);
-      }
-    }
-  }
-  if (P.pair_list.empty()) P.pair_list.push_back(0);  // keep device arrays non-empty
-  if (P.cam_list.empty()) P.cam_list.push_back(0);
-  if (P.camo_list.empty()) P.camo_list.push_back(0);
-  // chunk headers: ob0 nob te0 nte p0 npt sb cb e0 e1 c0 c1 q0 q1 (+2 spare)
+  P.pair_list.resize(pair_base[nchunks]);
+  P.cam_list.resize(cl_base[nchunks]);
+  P.camo_list.resize(col_base[nchunks]);
   P.chunk_hdr.assign((size_t)std::max(nchunks, 1) * kChunkHdr, 0);
-  for (size_t si = 0; si + 1 < P.seg_chunk.size(); ++si) {
-    const int ns = P.seg_slot_off[si + 1] - P.seg_slot_off[si];
-    const int nc = P.seg_cam_off[si + 1] - P.seg_cam_off[si];
-    for (int ch = P.seg_chunk[si]; ch < P.seg_chunk[si + 1]; ++ch) {
-      int32_t* h = &P.chunk_hdr[(size_t)ch * kChunkHdr];
-      const int sb = P.chunk_slot_base[ch], cb = P.chunk_cam_base[ch];
-      h[0] = P.chunk_obs[ch];
-      h[1] = P.chunk_obs[ch + 1] - P.chunk_obs[ch];
-      h[2] = P.chunk_te[ch];
-      h[3] = P.chunk_te[ch + 1] - P.chunk_te[ch];
-      h[4] = P.chunk_pt[ch];
-      h[5] = P.chunk_pt[ch + 1] - P.chunk_pt[ch];
-      h[6] = sb;
-      h[7] = cb;
-      h[8] = P.slot_ptr[sb];
-      h[9] = P.slot_ptr[sb + ns];
-      h[10] = P.cam_ptr[cb];
-      h[11] = P.cam_ptr[cb + nc];
-      h[12] = P.camo_ptr[cb];
-      h[13] = P.camo_ptr[cb + nc];
-    }
-  }
-  // chunk LDS images: independent per chunk, built on a few host threads (segment ranges)
   P.chunk_img.resize((size_t)std::max(nchunks, 1));
   if (nchunks == 0) P.chunk_img[0] = ChunkImg();
-  auto build_imgs = [&P](size_t seg_a, size_t seg_b) {
-    for (size_t si = seg_a; si < seg_b; ++si) {
-      const int ns = P.seg_slot_off[si + 1] - P.seg_slot_off[si];
-      const int nc = P.seg_cam_off[si + 1] - P.seg_cam_off[si];
-      const int cam0 = P.seg_cam_off[si];
-      for (int ch = P.seg_chunk[si]; ch < P.seg_chunk[si + 1]; ++ch) {
+  P.seg_hdr.assign((size_t)std::max(nseg, 1) * kSegHdr, 0);
+  auto fill = [&](int sa, int sbnd) {
+    // per-thread lookup tables (camera -> window index, camera pair -> slot) and counting-sort buffers
+    std::vector<int32_t> fcam_idx(tables ? std::max(Nf, 1) : 0, -1), acam_idx(tables ? N : 0, -1);
+    std::vector<int32_t> pair_slot(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, -1);
+    std::vector<int32_t> cnt, cnt2, pairs_slot;
+    std::vector<uint16_t> pairs_tmp;
+    for (int si = sa; si < sbnd; ++si) {
+      PlanSeg& s = segs[si];
+      std::sort(s.cams.begin(), s.cams.end());
+      std::sort(s.slots.begin(), s.slots.end());
+      std::sort(s.acams.begin(), s.acams.end());
+      const int ch0 = P.seg_chunk[si], ch1 = P.seg_chunk[si + 1];
+      const int so = P.seg_slot_off[si], co = P.seg_cam_off[si];
+      for (size_t i = 0; i < s.slots.size(); ++i) {
+        P.slot_i[so + i] = s.slots[i].first;
+        P.slot_j[so + i] = s.slots[i].second;
+      }
+      if (tables) {
+        for (size_t i = 0; i < s.cams.size(); ++i) fcam_idx[s.cams[i]] = (int32_t)i;
+        for (size_t i = 0; i < s.acams.size(); ++i) acam_idx[s.acams[i]] = (int32_t)i;
+        for (size_t i = 0; i < s.slots.size(); ++i) pair_slot[(size_t)s.slots[i].first * Nf + s.slots[i].second] = (int32_t)i;
+      }
+      auto lcam_of = [&](int32_t c) {  // window index of free camera c
+        return tables ? fcam_idx[c] : (int32_t)(std::lower_bound(s.cams.begin(), s.cams.end(), c) - s.cams.begin());
+      };
+      auto slot_of = [&](const std::pair<int32_t, int32_t>& pr) {
+        return tables ? pair_slot[(size_t)pr.first * Nf + pr.second]
+                      : (int32_t)(std::lower_bound(s.slots.begin(), s.slots.end(), pr) - s.slots.begin());
+      };
+      std::copy(s.acams.begin(), s.acams.end(), P.seg_acam.begin() + P.seg_acam_off[si]);
+      for (int o = P.chunk_obs[ch0]; o < P.chunk_obs[ch1]; ++o)
+        P.obs_acam[o] = (uint8_t)(tables ? acam_idx[P.obs_cam[o]]
+                                         : std::lower_bound(s.acams.begin(), s.acams.end(), P.obs_cam[o]) -
+                                               s.acams.begin());
+      for (size_t i = 0; i < s.cams.size(); ++i) {
+        P.segcam_f[co + i] = s.cams[i];
+        P.segcam_diag[co + i] = slot_of(std::make_pair(s.cams[i], s.cams[i]));
+      }
+      const int ns = (int)s.slots.size(), nc = (int)s.cams.size();
+      for (int ch = ch0; ch < ch1; ++ch) {
+        const int te0 = P.chunk_te[ch];
+        for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
+          if (P.te_cam[t] >= n_fixed) P.te_lcam[t] = (int16_t)lcam_of(P.te_cam[t] - n_fixed);
+        // pair lists by slot: a stable counting sort of the (x, y) pairs in generation order
+        pairs_tmp.clear();
+        pairs_slot.clear();
+        for (int q = P.chunk_pt[ch]; q < P.chunk_pt[ch + 1]; ++q) {
+          for (int x = P.pt_te[q]; x < P.pt_te[q + 1]; ++x) {
+            if (P.te_cam[x] < n_fixed) continue;
+            for (int y = P.pt_te[q]; y <= x; ++y) {
+              if (P.te_cam[y] < n_fixed) continue;
+              pairs_slot.push_back(slot_of(std::make_pair(P.te_cam[x] - n_fixed, P.te_cam[y] - n_fixed)));
+              pairs_tmp.push_back((uint16_t)((x - te0) | ((y - te0) << 8)));
+            }
+          }
+        }
+        cnt.assign(ns + 1, 0);
+        for (int32_t sl : pairs_slot) ++cnt[sl + 1];
+        for (int sl = 0; sl < ns; ++sl) cnt[sl + 1] += cnt[sl];
+        const int32_t pbase = pair_base[ch];
+        int32_t* sp = &P.slot_ptr[P.chunk_slot_base[ch]];
+        for (int sl = 0; sl <= ns; ++sl) sp[sl] = pbase + cnt[sl];
+        for (size_t e = 0; e < pairs_tmp.size(); ++e) P.pair_list[pbase + cnt[pairs_slot[e]]++] = pairs_tmp[e];
+        // camera lists: track entries and observations by window camera, in order
+        cnt.assign(nc + 1, 0);
+        for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
+          if (P.te_lcam[t] >= 0) ++cnt[P.te_lcam[t] + 1];
+        cnt2.assign(nc + 1, 0);
+        const int ob0 = P.chunk_obs[ch];
+        for (int o = ob0; o < P.chunk_obs[ch + 1]; ++o)
+          if (P.te_lcam[P.obs_te[o]] >= 0) ++cnt2[P.te_lcam[P.obs_te[o]] + 1];
+        for (int c = 0; c < nc; ++c) {
+          cnt[c + 1] += cnt[c];
+          cnt2[c + 1] += cnt2[c];
+        }
+        const int32_t cbase = cl_base[ch], obase = col_base[ch];
+        int32_t* cp = &P.cam_ptr[P.chunk_cam_base[ch]];
+        int32_t* op = &P.camo_ptr[P.chunk_cam_base[ch]];
+        for (int c = 0; c <= nc; ++c) {
+          cp[c] = cbase + cnt[c];
+          op[c] = obase + cnt2[c];
+        }
+        for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
+          if (P.te_lcam[t] >= 0) P.cam_list[cbase + cnt[P.te_lcam[t]]++] = (uint8_t)(t - te0);
+        for (int o = ob0; o < P.chunk_obs[ch + 1]; ++o) {
+          const int lc = P.te_lcam[P.obs_te[o]];
+          if (lc >= 0) P.camo_list[obase + cnt2[lc]++] = (uint8_t)(o - ob0);
+        }
+        // chunk header: ob0 nob te0 nte p0 npt sb cb e0 e1 c0 c1 q0 q1 (+2 spare)
+        int32_t* h = &P.chunk_hdr[(size_t)ch * kChunkHdr];
+        const int sb = P.chunk_slot_base[ch], cb = P.chunk_cam_base[ch];
+        h[0] = ob0;
+        h[1] = P.chunk_obs[ch + 1] - ob0;
+        h[2] = te0;
+        h[3] = P.chunk_te[ch + 1] - te0;
+        h[4] = P.chunk_pt[ch];
+        h[5] = P.chunk_pt[ch + 1] - P.chunk_pt[ch];
+        h[6] = sb;
+        h[7] = cb;
+        h[8] = P.slot_ptr[sb];
+        h[9] = P.slot_ptr[sb + ns];
+        h[10] = P.cam_ptr[cb];
+        h[11] = P.cam_ptr[cb + nc];
+        h[12] = P.camo_ptr[cb];
+        h[13] = P.camo_ptr[cb + nc];
+        // the chunk's LDS image (chunk-relative offsets, unused entries zero)
         ChunkImg& g = P.chunk_img[ch];
         g = ChunkImg();
-        const int32_t* h = &P.chunk_hdr[(size_t)ch * kChunkHdr];
-        const int ob0 = h[0], nob = h[1], te0 = h[2], nte = h[3], p0 = h[4], npt = h[5];
-        const int sb = h[6], cb = h[7], e0 = h[8], e1 = h[9], c0 = h[10], c1 = h[11], q0 = h[12], q1 = h[13];
+        const int nob = h[1], nte = h[3], p0 = h[4], npt = h[5];
+        const int e0 = h[8], e1 = h[9], c0 = h[10], c1 = h[11], q0 = h[12], q1 = h[13];
         for (int i = 0; i < nob; ++i) {
           g.obs_te[i] = P.obs_te[ob0 + i] - te0;
           g.uv[2 * i] = P.obs_uv[2 * (ob0 + i)];
@@ -389,39 +607,37 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         }
         for (int i = 0; i < c1 - c0; ++i) g.caml[i] = P.cam_list[c0 + i];
         for (int i = 0; i < q1 - q0; ++i) g.camol[i] = P.camo_list[q0 + i];
-        for (int i = 0; i < nc; ++i) g.dslot[i] = P.segcam_diag[cam0 + i];
+        for (int i = 0; i < nc; ++i) g.dslot[i] = P.segcam_diag[co + i];
+      }
+      // segment header (kSegHdr)
+      int32_t* h = &P.seg_hdr[(size_t)si * kSegHdr];
+      h[0] = ns;
+      h[1] = so;
+      h[2] = co;
+      h[3] = nc;
+      h[4] = (int)s.acams.size();
+      h[5] = ch0;
+      h[6] = ch1;
+      int16_t* h16 = reinterpret_cast<int16_t*>(h);
+      for (int i = 0; i < h[4]; ++i) h16[16 + i] = (int16_t)s.acams[i];
+      for (int i = 0; i < nc; ++i) h16[32 + i] = (int16_t)s.cams[i];
+      if (ch1 > ch0) std::copy(&P.chunk_hdr[(size_t)ch0 * kChunkHdr], &P.chunk_hdr[(size_t)(ch0 + 1) * kChunkHdr], h + 32);
+      if (tables) {  // clear this segment's table entries for the next one
+        for (int32_t c : s.cams) fcam_idx[c] = -1;
+        for (int32_t c : s.acams) acam_idx[c] = -1;
+        for (const auto& pr : s.slots) pair_slot[(size_t)pr.first * Nf + pr.second] = -1;
       }
     }
   };
   {
-    const size_t nseg_img = P.seg_chunk.size() - 1;
-    const int nthr = (int)std::min<size_t>(std::max(1u, std::min(8u, std::thread::hardware_concurrency())),
-                                            std::max<size_t>(1, nchunks / 128));
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nthr; ++t)
-      pool.emplace_back(build_imgs, nseg_img * t / nthr, nseg_img * (t + 1) / nthr);
-    build_imgs(0, nseg_img / nthr);
-    for (auto& th : pool) th.join();
+    const int nt = std::max(1, std::min(nthr, nseg));
+    run_parallel(nt, [&](int t) { fill((int)((int64_t)nseg * t / nt), (int)((int64_t)nseg * (t + 1) / nt)); });
   }
-  // segment headers (kSegHdr)
-  const int nseg = (int)P.seg_chunk.size() - 1;
-  P.seg_hdr.assign((size_t)std::max(nseg, 1) * kSegHdr, 0);
-  for (int si = 0; si < nseg; ++si) {
-    int32_t* h = &P.seg_hdr[(size_t)si * kSegHdr];
-    h[0] = P.seg_slot_off[si + 1] - P.seg_slot_off[si];
-    h[1] = P.seg_slot_off[si];
-    h[2] = P.seg_cam_off[si];
-    h[3] = P.seg_cam_off[si + 1] - P.seg_cam_off[si];
-    h[4] = P.seg_acam_off[si + 1] - P.seg_acam_off[si];
-    h[5] = P.seg_chunk[si];
-    h[6] = P.seg_chunk[si + 1];
-    int16_t* h16 = reinterpret_cast<int16_t*>(h);
-    for (int i = 0; i < h[4]; ++i) h16[16 + i] = (int16_t)P.seg_acam[P.seg_acam_off[si] + i];
-    for (int i = 0; i < h[3]; ++i) h16[32 + i] = (int16_t)P.segcam_f[P.seg_cam_off[si] + i];
-    if (h[6] > h[5])
-      std::copy(&P.chunk_hdr[(size_t)h[5] * kChunkHdr], &P.chunk_hdr[(size_t)(h[5] + 1) * kChunkHdr], h + 32);
-  }
+  if (P.pair_list.empty()) P.pair_list.push_back(0);  // keep device arrays non-empty
+  if (P.cam_list.empty()) P.cam_list.push_back(0);
+  if (P.camo_list.empty()) P.camo_list.push_back(0);
   if (P.segcam_diag.empty()) P.segcam_diag.push_back(0);
+  PLAN_T("lists+images");
   return "";
 }
 

@@ -20,8 +20,25 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
+#include <utility>
 #include <string>
 #include <vector>
+// Diagnostic build only (EXTRA=-DVO_PLAN_TIMING): host setup section times to stderr.
+#include <cstdio>
+#ifdef VO_PLAN_TIMING
+#include <chrono>
+#define PLAN_T(name)                                                                                          \
+  do {                                                                                                        \
+    const auto n_ = std::chrono::steady_clock::now();                                                         \
+    std::fprintf(stderr, "  %-14s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(n_ - t_).count()); \
+    t_ = n_;                                                                                                  \
+  } while (0)
+#else
+#define PLAN_T(name) \
+  do {               \
+  } while (0)
+#endif
 
 namespace vo {
 
@@ -67,6 +84,27 @@ struct alignas(16) ChunkImg {
 };
 static_assert(sizeof(ChunkImg) % 16 == 0, "16-byte staging granules");
 
+// Allocator whose resize() default-initialises (leaves a trivial type unwritten): the
+// planner writes every chunk image in full, on its worker threads.
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = DefaultInitAlloc<U>;
+  };
+  DefaultInitAlloc() = default;
+  template <class U>
+  DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... Args>
+  void construct(U* p, Args&&... args) {
+    ::new (static_cast<void*>(p)) U(std::forward<Args>(args)...);
+  }
+};
+
 struct SolveTableLayout {
   int diag = 0, off = 0, first = 0, step_ptr = 0, panel_i = 0, panel_blk = 0, item_ptr = 0,
       item_blk = 0, item_q = 0, len = 0;
@@ -95,7 +133,7 @@ struct BAPlan {
   // (the inverse of camb_src); K1 writes there so K2 reads contiguous rows
   std::vector<int32_t> slab_pos, cam_pos;
   std::vector<int32_t> seg_hdr;  // kSegHdr ints per segment
-  std::vector<ChunkImg> chunk_img;
+  std::vector<ChunkImg, DefaultInitAlloc<ChunkImg>> chunk_img;
   std::vector<int32_t> slot_ptr;   // per chunk: nslots(seg)+1 offsets into pair_list
   std::vector<uint16_t> pair_list; // (te_x_local | te_y_local << 8)
   std::vector<int32_t> cam_ptr;    // per chunk: ncams(seg)+1 offsets into cam_list
@@ -121,6 +159,7 @@ struct BAPlan {
   std::vector<int32_t> solve_tab;
   SolveTableLayout solve_layout;
 
+  void reset();  // empty every array, keep its capacity (a session's next window reuses it)
   int n_chunks() const { return (int)chunk_obs.size() - 1; }
   int n_segments() const { return (int)seg_chunk.size() - 1; }
   int n_slab_slots() const { return (int)slot_i.size(); }
