@@ -192,18 +192,37 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   const int nthr = plan_threads(M);
 
   // landmarks ordered by first camera (stable counting sort; no observation: last), which
-  // keeps each workgroup's camera window narrow
+  // keeps each workgroup's camera window narrow.  Per-thread histograms over landmark
+  // ranges, offsets in (camera, range) order, then each range scatters its landmarks.
   {
-    std::vector<int32_t> first(L), cnt(N + 2, 0);
-    for (int p = 0; p < L; ++p) {
-      int f = N;
-      for (int o = point_ptr[p]; o < point_ptr[p + 1]; ++o) f = std::min(f, (int)obs_cam[o]);
-      first[p] = f;
-      ++cnt[f + 1];
-    }
-    for (int c = 0; c <= N; ++c) cnt[c + 1] += cnt[c];
+    std::vector<int32_t> first(L);
+    const int nt = std::max(1, std::min(nthr, L / 1024 + 1));
+    std::vector<int32_t> hist((size_t)nt * (N + 1), 0);
+    auto lrange = [&](int t) { return std::make_pair((int)((int64_t)L * t / nt), (int)((int64_t)L * (t + 1) / nt)); };
+    run_parallel(nt, [&](int t) {
+      const auto [pa, pb] = lrange(t);
+      int32_t* h = &hist[(size_t)t * (N + 1)];
+      for (int p = pa; p < pb; ++p) {
+        int f = N;
+        for (int o = point_ptr[p]; o < point_ptr[p + 1]; ++o) f = std::min(f, (int)obs_cam[o]);
+        first[p] = f;
+        ++h[f];
+      }
+    });
+    int32_t off = 0;
+    for (int c = 0; c <= N; ++c)
+      for (int t = 0; t < nt; ++t) {
+        int32_t& h = hist[(size_t)t * (N + 1) + c];
+        const int32_t n = h;
+        h = off;
+        off += n;
+      }
     P.pt_perm.resize(L);
-    for (int p = 0; p < L; ++p) P.pt_perm[cnt[first[p]]++] = p;
+    run_parallel(nt, [&](int t) {
+      const auto [pa, pb] = lrange(t);
+      int32_t* h = &hist[(size_t)t * (N + 1)];
+      for (int p = pa; p < pb; ++p) P.pt_perm[h[first[p]]++] = p;
+    });
   }
   PLAN_T("order");
 
@@ -661,27 +680,39 @@ void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
   const int nb = P.prof_off[F];
   P.prof_diag.assign(nb, 0);
   for (int i = 0; i < F; ++i) P.prof_diag[P.prof_off[i] + (i - first[i])] = 1;
-  std::vector<std::vector<int32_t>> src(nb);
-  for (size_t s = 0; s < P.slot_i.size(); ++s)
-    src[P.prof_off[P.slot_i[s]] + (P.slot_j[s] - first[P.slot_i[s]])].push_back((int32_t)s);
-  P.prof_src_ptr.assign(1, 0);
-  P.prof_src.clear();
-  for (int b = 0; b < nb; ++b) {
-    P.prof_src.insert(P.prof_src.end(), src[b].begin(), src[b].end());
-    P.prof_src_ptr.push_back((int32_t)P.prof_src.size());
+  // per profile block its slab slots, per free camera its rhs entries: stable counting
+  // sorts (slots / entries in plan order within a block), and the inverse positions
+  const size_t nslot = P.slot_i.size(), nent = P.segcam_f.size();
+  std::vector<int32_t> sblk(nslot);
+  P.prof_src_ptr.assign(nb + 1, 0);
+  for (size_t s = 0; s < nslot; ++s) {
+    sblk[s] = P.prof_off[P.slot_i[s]] + (P.slot_j[s] - first[P.slot_i[s]]);
+    ++P.prof_src_ptr[sblk[s] + 1];
   }
-  std::vector<std::vector<int32_t>> cb(F);
-  for (size_t e = 0; e < P.segcam_f.size(); ++e) cb[P.segcam_f[e]].push_back((int32_t)e);
-  P.camb_ptr.assign(1, 0);
-  P.camb_src.clear();
-  for (int f = 0; f < F; ++f) {
-    P.camb_src.insert(P.camb_src.end(), cb[f].begin(), cb[f].end());
-    P.camb_ptr.push_back((int32_t)P.camb_src.size());
+  for (int b = 0; b < nb; ++b) P.prof_src_ptr[b + 1] += P.prof_src_ptr[b];
+  P.prof_src.resize(nslot);
+  P.slab_pos.assign(std::max<size_t>(nslot, 1), 0);
+  {
+    std::vector<int32_t> next(P.prof_src_ptr.begin(), P.prof_src_ptr.end() - 1);
+    for (size_t s = 0; s < nslot; ++s) {
+      const int32_t k = next[sblk[s]]++;
+      P.prof_src[k] = (int32_t)s;
+      P.slab_pos[s] = k;
+    }
   }
-  P.slab_pos.assign(std::max<size_t>(P.slot_i.size(), 1), 0);
-  for (size_t k = 0; k < P.prof_src.size(); ++k) P.slab_pos[P.prof_src[k]] = (int32_t)k;
-  P.cam_pos.assign(std::max<size_t>(P.segcam_f.size(), 1), 0);
-  for (size_t k = 0; k < P.camb_src.size(); ++k) P.cam_pos[P.camb_src[k]] = (int32_t)k;
+  P.camb_ptr.assign(F + 1, 0);
+  for (size_t e = 0; e < nent; ++e) ++P.camb_ptr[P.segcam_f[e] + 1];
+  for (int f = 0; f < F; ++f) P.camb_ptr[f + 1] += P.camb_ptr[f];
+  P.camb_src.resize(nent);
+  P.cam_pos.assign(std::max<size_t>(nent, 1), 0);
+  {
+    std::vector<int32_t> next(P.camb_ptr.begin(), P.camb_ptr.end() - 1);
+    for (size_t e = 0; e < nent; ++e) {
+      const int32_t k = next[P.segcam_f[e]]++;
+      P.camb_src[k] = (int32_t)e;
+      P.cam_pos[e] = k;
+    }
+  }
   if (P.prof_src.empty()) P.prof_src.push_back(0);
   if (P.camb_src.empty()) P.camb_src.push_back(0);
 
