@@ -123,7 +123,8 @@ __device__ __forceinline__ void chol6_nochk(double (&a)[21], double (&r)[6]) {
   for (int j = 0; j < 6; ++j) {
     const double d = a[P6(j, j)];
     double q = __builtin_amdgcn_rsq(d);
-    if (kCholNewton) q = q * (1.5 - 0.5 * d * q * q);
+    // one Newton step, q + (q / 2)(1 - d q^2): three dependent operations on the chain
+    if (kCholNewton) q = __builtin_fma(0.5 * q, __builtin_fma(-(d * q), q, 1.0), q);
     r[j] = q;
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) a[P6(i, j)] *= q;
@@ -248,6 +249,8 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     if (A.cost_out) *A.cost_out = A.sys[A.cost_off];
   }
 
+  // the poses for the tail's update, staged now (their load latency under the prologue's)
+  for (int e = tid; e < 12 * A.n_poses; e += kBandThreads) pose_l[e] = A.pose_cur[e];
   // Ring prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every
   // 16-byte load in flight, then the stores.
   if (!prior_fail) {
@@ -491,19 +494,21 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   };
 
   // Full mode: every block L_{k,i} (k - w <= i < k) is replaced by G = L_kk^-1 L_{k,i}
-  // before the back substitution (one block per thread; L_kk from this side's record, or
-  // for the bottom side's separator rows from the top's).  Item lists: set 0 = the rows
-  // final after phase A (top rows < m, then bottom rows < nb; done by the idle bottom
-  // waves during the separator phase), set 1 = the separator rows (top rows m .. m + s,
-  // then the bottom side's pseudo rows nb .. nb + s).
+  // before the back substitution, one block column per thread (L_kk from this side's
+  // record, or for the bottom side's separator rows from the top's).  Item e = 6 b + s2:
+  // column s2 of block b of the lists: set 0 = the rows final after phase A (top rows < m,
+  // then bottom rows < nb; done by the idle bottom waves during the separator phase),
+  // set 1 = the separator rows (top rows m .. m + s, then the bottom side's pseudo rows
+  // nb .. nb + s).
   auto g_item = [&](int set, int e) __attribute__((always_inline)) {
+    const int bi = e / 6, s2 = e - 6 * bi;
     const int nt = (set == 0 ? m : sp) * w;
-    const bool eb = e >= nt;
-    const int e2 = eb ? e - nt : e, k = e2 / w + (set == 0 ? 0 : eb ? nb : m), qq = e2 % w + 1, i = k - qq;
+    const bool eb = bi >= nt;
+    const int e2 = eb ? bi - nt : bi, k = e2 / w + (set == 0 ? 0 : eb ? nb : m), qq = e2 % w + 1, i = k - qq;
     if (i < 0 || (eb && i >= nb)) return;
     double* fs = eb ? ringB : ringT;
     const double* rec = (eb && k >= nb) ? ringT + (long)(F - 1 - k) * CS : fs + (long)k * CS;
-    double L[21], r[6], Bk[6][6];
+    double L[21], r[6], gv[6];
 #pragma unroll
     for (int ii = 0; ii < 6; ++ii)
 #pragma unroll
@@ -513,20 +518,12 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
         if (c + 1 <= ii) L[P6(ii, c + 1)] = v.y;
       }
     ld6g(rec + 36 * R + 6, r);
-    double* blk = fs + (long)i * CS + 36 * qq;
+    double* col = fs + (long)i * CS + 36 * qq + s2;
 #pragma unroll
-    for (int c = 0; c < 6; ++c) ld6g(blk + 6 * c, Bk[c]);
+    for (int c = 0; c < 6; ++c) gv[c] = col[6 * c];
+    fwd6(L, r, gv);
 #pragma unroll
-    for (int s2 = 0; s2 < 6; ++s2) {
-      double gv[6];
-#pragma unroll
-      for (int c = 0; c < 6; ++c) gv[c] = Bk[c][s2];
-      fwd6(L, r, gv);
-#pragma unroll
-      for (int c = 0; c < 6; ++c) Bk[c][s2] = gv[c];
-    }
-#pragma unroll
-    for (int c = 0; c < 6; ++c) st6g(blk + 6 * c, Bk[c]);
+    for (int c = 0; c < 6; ++c) col[6 * c] = gv[c];
   };
 
   if (!prior_fail) {
@@ -576,7 +573,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
             side_step(p, sk, skm);
           }
         } else if (kFull) {
-          const int n0 = (m + nb) * w, chunk = (n0 + sp - 1) / sp, t = p - m;
+          const int n0 = 6 * (m + nb) * w, chunk = (n0 + sp - 1) / sp, t = p - m;
           const int e1 = min(n0, (t + 1) * chunk);
           for (int e = t * chunk + 64 * role + lane; e < e1; e += 256) g_item(0, e);
         }
@@ -598,13 +595,11 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // j = k - q is g . z_k with g = L_kk^-1 (column sr of L_{k,j}), formed from operands
   // fetched two steps ahead.  A chain step is the readlane broadcast of z_k from the
   // lanes holding it plus 6 FMAs; every x_k is formed in parallel at the end from z (LDS)
-  // and the factor records.  Loader waves stage the poses meanwhile.
-  if (role == kLoad)
-    for (int e = tid - 64 * kLoad * 2; e < 12 * A.n_poses; e += 128) pose_l[e] = A.pose_cur[e];
+  // and the factor records.
   // Full mode, the rest of the G blocks (rows the separator phase finalised: the top's
   // separator rows and the bottom side's pseudo rows), then the back substitution.
   if (kFull && !failed) {
-    const int nR = sp > 0 ? 2 * sp * w : m * w;  // one-sided windows: every top row here
+    const int nR = 6 * (sp > 0 ? 2 * sp * w : m * w);  // one-sided windows: every top row here
     for (int e = tid; e < nR; e += kBandThreads) g_item(sp > 0 ? 1 : 0, e);
     __syncthreads();
   }
@@ -727,10 +722,31 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       qb = qb == 0 ? w : qb - 1;
       zk += dz;
     };
+    int k = khi;
+    // pseudo steps (the bottom side's separator rows, k >= kp): z_k is the top side's,
+    // already in zs, so nothing is stored and each z is fetched one step ahead: the steps
+    // are independent subtractions instead of LDS round trips
+    if (k >= kp && k >= klo) {
+      double zc[6];
+      ld6g(dyn + zk, zc);
+      for (; k >= kp && k >= klo; --k) {
+        double gv[6], yin, zn[6];
+        fetch(gv, yin);
+        int on = k - 1 >= kp ? zk + dz : zk;
+        asm volatile("" : "+v"(on));
+        ld6g(dyn + on, zn);
+        double d = gv[0] * zc[0] + gv[1] * zc[1] + gv[2] * zc[2] + gv[3] * zc[3] + gv[4] * zc[4] + gv[5] * zc[5];
+        asm volatile("" : "+v"(d));
+        Yb = qb == 0 ? yin : Yb - d;
+        qb = qb == 0 ? w : qb - 1;
+        zk += dz;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) zc[c] = zn[c];
+      }
+    }
     double gA[6], gB[6], yA, yB;
     fetch(gA, yA);
     fetch(gB, yB);
-    int k = khi;
     for (; k - 1 >= klo; k -= 2) {
       step(k, gA, yA);
       fetch(gA, yA);

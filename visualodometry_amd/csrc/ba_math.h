@@ -21,9 +21,10 @@ __device__ __forceinline__ void se3_exp_apply(const double* d, const double* T, 
   } else {
     double s, c;
     sincos(th, &s, &c);
-    A = s / th;
-    B = (1.0 - c) / (th * th);
-    C = (th - s) / (th * th * th);
+    const double it = 1.0 / th, it2 = it * it;  // one division on the tail's chain
+    A = s * it;
+    B = (1.0 - c) * it2;
+    C = (th - s) * (it2 * it);
   }
   // P = [phi]x, P2 = P P
   const double P[9] = {0, -p2, p1, p2, 0, -p0, -p1, p0, 0};
