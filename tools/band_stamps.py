@@ -23,7 +23,7 @@ from visualodometry_amd.synthetic import make_ba_config  # noqa: E402
 NK1 = 16  # K1 phase slots precede the K3 stamps
 PH = ["prologue", "A: pre", "A: barrier", "A: post/helper", "merge", "B: pre", "B: barrier", "B: post/helper",
       "vmcnt drain", "sync", "BS1", "BS1 sync", "BS2", "BS2 sync", "tail", "-",
-      "G pass", "c: D bcast", "c: chol6", "c: fwd6", "ld: dma issue", "ld: dma wait", "c: post loads", "c: post fma", "-", "-", "bs: 2 steps"]
+      "G pass", "c: D bcast", "c: chol6", "c: fwd6", "ld: dma issue", "ld: dma wait", "c: post loads", "c: post fma", "f: loads", "f: fwd6", "bs: 2 steps", "f: rmw"]
 WAVES = ["T chain", "B chain", "T trail", "B trail", "T load", "B load", "T fwd", "B fwd"]
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg3"

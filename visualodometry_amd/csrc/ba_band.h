@@ -29,7 +29,7 @@ struct BandTables {
   std::vector<int> tab;
   int merge = 0, n_merge = 0;
 };
-// LDS layout of the two column stores.  Ring mode: w + 3 slots per side, each padded to
+// LDS layout of the two column stores.  Ring mode: w + 4 slots per side, each padded to
 // whole 1 KiB LDS-DMA pieces; factor records go to global memory.  Full mode (when it
 // fits): every column of a side in its own slot at the K2 stride, so the factor stays
 // in LDS for the back substitution (a DMA's last piece spills into the next slot, or into

@@ -11,26 +11,23 @@
 // receives both sides' Schur updates, continues the top side.  The chain of dependent
 // block steps is max(m, nb) + w instead of F.
 //
-// One workgroup of eight waves (two per SIMD).  Per side:
-//   chain wave   holds the block column being factored in registers, one lane per
-//                scalar row (lane 6 g + r: row r of the block row = g mod (w + 1)).  Step
-//                k: the diagonal block's rows go through LDS to every lane, each lane
-//                factors it (chol6) and solves its own panel row, the panel goes to the
-//                LDS ring; after the workgroup barrier the lane loads its row of column
-//                k + 1 and applies step k's update to it.  Nothing else is on the chain.
-//   helper wave  after the barrier: the forward substitution of step k (y'_k = L_kk^-1
-//                y_k, y_i -= L_ik y'_k), the ring loader (column k + w + 2 from registers
-//                into the slot of column k - 1, column k + w + 3 issued), the factor
-//                record of column k to global memory and the rest of step k's trailing
-//                update (blocks (i, j), k + 2 <= j <= i <= k + w) in the ring.
-// Back substitution: each chain wave walks its rows upwards, x_k = L_kk^-T y'_k in
-// every lane, then lane (q, c) subtracts (L_{k,k-q}^T x_k)_c from its row k - q; the
-// next row goes through LDS.  Factor records come from global memory (L2) two steps
-// ahead.  The bottom side starts once the separator's x is known.
+// One workgroup of eight waves (two per SIMD), four roles per side:
+//   chain   holds the block column being factored in registers, one lane per scalar row
+//           (lane 6 g + r: row r of block row g).  Step k: the diagonal block's rows go
+//           through LDS to every lane, each lane factors it (chol6) and solves its own panel
+//           row, the panel goes to LDS; after the workgroup barrier the lane loads its row
+//           of column k + 1 and applies step k's update to it.
+//   trail   after the barrier: the rest of step k's trailing update (blocks (i, j),
+//           k + 2 <= j <= i <= k + w); ring mode: then column k - 1's factor record to
+//           global memory.
+//   fwd     the forward substitution of step k (y'_k = L_kk^-1 y_k, y_i -= L_ik y'_k).
+//   loader  column k + w + 2 by LDS-DMA (ring mode: into the slot of column k - 2).
+// Back substitution as a z recurrence (z_k = y'_k - sum_q L_{k+q,k}^T x_{k+q}); x_k =
+// L_kk^-T z_k for every row at the end (see the back-substitution section below).
 //
-// LDS: two rings of w + 3 block columns (36 (w+1) + 12 doubles each: blocks, rhs row,
-// 1/diag), x (6F), the poses, the column source tables -- so the cfg4 window (F = 98,
-// a 225 KB profile) runs like cfg3.
+// LDS: full mode (the cfg3 window) keeps every column of both sides; ring mode (cfg4:
+// F = 98, a 225 KB profile) keeps w + 4 column slots per side and writes the factor
+// records to global memory.  Plus z (6F), the poses and the merge table.
 #include "ba_band.h"
 
 #include <algorithm>
@@ -70,7 +67,7 @@ BandLds band_lds_layout(int F, const BandSplit& b, int n_poses) {
   L.bytes = band_lds_total(L, F, n_poses);
   if (L.bytes <= kBandLdsMax) return L;
   L.full = false;
-  L.rc = b.w + 3;
+  L.rc = b.w + 4;
   L.ss = band_slot_stride(b.w);
   L.pad = 0;
   L.bytes = band_lds_total(L, F, n_poses);
@@ -222,7 +219,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   const int F = A.F, w = A.w, R = w + 1, CS = 36 * R + 12, CSP = (CS + 127) / 128 * 128;
   const int m = A.m, nb = A.nb, sp = A.s;
   const int ncolT = m + sp, ncolB = nb + sp;
-  const int SS = kFull ? CS : CSP, RC = kFull ? max(ncolT, ncolB) : w + 3, SPAD = kFull ? 128 : 0;
+  const int SS = kFull ? CS : CSP, RC = kFull ? max(ncolT, ncolB) : w + 4, SPAD = kFull ? 128 : 0;
   const bool prior_fail = A.status && *A.status;
   double* ringT = dyn;
   double* ringB = ringT + RC * SS + SPAD;
@@ -427,8 +424,12 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     const int qf = lane / 6, rf = lane % 6;
     const bool on = (qf >= 1) & (qf < R) & (k + qf < snload);  // rows past the side: none
     ld6g(col + (on ? 36 * qf + 6 * rf : 0), row);
+    BSETTLE(row[5]);
+    BSTF(24);
     fwd6(L, r, y);
     bad = bad | !isfinite(y[0] + y[1] + y[2] + y[3] + y[4] + y[5]);
+    BSETTLE(y[5]);
+    BSTF(25);
     {
       const int st = sk + qf < RC ? sk + qf : sk + qf - RC;
       int o = on ? (int)(sring - dyn) + st * SS + 36 * R + rf : DOFF + lane;
@@ -437,15 +438,36 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       dyn[o] -= row[0] * y[0] + row[1] * y[1] + row[2] * y[2] + row[3] * y[3] + row[4] * y[4] + row[5] * y[5];
       dyn[o2] = pick<6>(y, lane);
     }
-    if (kFull) return;  // the record stays in its slot
-    const double2* s2 = reinterpret_cast<const double2*>(col);
-    double2* d2 = reinterpret_cast<double2*>(const_cast<double*>(sfac) + (long)k * CS);
-    double2 v2[3];
+    BSETTLE(y[0]);
+    BSTF(27);
+  };
+  // Ring mode: the factor record of column kc (blocks, y', 1/diag; in slot sc) to global
+  // memory, by the trailing wave one step after its forward substitution (the fwd wave is
+  // the ring's slowest role otherwise).  The ring has w + 4 slots, so the loader refills
+  // column kc's slot only a step later, after the barrier that retires these reads.
+  // The three 16-byte pieces per lane go out in one asm block: issued together from three
+  // register tuples (compiled stores would share one tuple and wait for each other), after
+  // all of the wave's LDS work of the step; they complete under the next barrier and the
+  // vmcnt(0) drain after the elimination covers them.
+  typedef __attribute__((ext_vector_type(4))) int i32x4;
+  auto rec_load = [&](int sc, i32x4 (&v2)[3]) __attribute__((always_inline)) {
+    const i32x4* s2 = reinterpret_cast<const i32x4*>(sring + sc * SS);
 #pragma unroll
     for (int t = 0; t < 3; ++t) v2[t] = s2[min(lane + 64 * t, CS / 2 - 1)];
-#pragma unroll
-    for (int t = 0; t < 3; ++t)
-      if (lane + 64 * t < CS / 2) d2[lane + 64 * t] = v2[t];
+  };
+  auto rec_store = [&](int kc, const i32x4 (&v2)[3]) __attribute__((always_inline)) {
+    i32x4* d2 = reinterpret_cast<i32x4*>(const_cast<double*>(sfac) + (long)kc * CS);
+    const bool t2 = lane + 128 < CS / 2;
+    i32x4* a0 = d2 + lane;
+    i32x4* a1 = d2 + lane + 64;
+    i32x4* a2 = d2 + (t2 ? lane + 128 : lane);  // masked lanes rewrite their first piece
+    const i32x4 v2b = t2 ? v2[2] : v2[0];
+    asm volatile(
+        "global_store_dwordx4 %0, %3, off\n\t"
+        "global_store_dwordx4 %1, %4, off\n\t"
+        "global_store_dwordx4 %2, %5, off" ::"v"(a0),
+        "v"(a1), "v"(a2), "v"(v2[0]), "v"(v2[1]), "v"(v2b)
+        : "memory");
   };
   // Trailing wave, step k: blocks (i, j), k + 2 <= j <= i <= k + w, minus L_ik L_jk^T.
   auto trail_step = [&](int k, int sk) __attribute__((always_inline)) {
@@ -473,12 +495,12 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       st6g(out + 18, o1);
     }
   };
-  // Loader wave, step k (slot of column k - 1: skm): column k + w + 2 into the freed
-  // slot (full mode: its own slot; first read at step k + 2), then the previous column's
-  // pieces retired.
-  auto load_step = [&](int k, int skm) __attribute__((always_inline)) {
+  // Loader wave, step k: column k + w + 2 into its slot (ring mode: column c in slot
+  // c mod (w + 4), i.e. column k - 2's, whose record the trailing wave copied a step ago;
+  // first read at step k + 2), then the previous column's pieces retired.
+  auto load_step = [&](int k) __attribute__((always_inline)) {
     if (k + w + 2 < snload) {
-      dma_col(k + w + 2, sring + (kFull ? k + w + 2 : skm) * SS);
+      dma_col(k + w + 2, sring + (kFull ? k + w + 2 : (k + w + 2) % RC) * SS);
       BSTF(20);
       dma_wait_prev();
       BSTF(21);
@@ -488,9 +510,18 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   };
   // VO_BA_EXP: 1 no trail, 2 no fwd, 3 no loader
   auto side_step = [&](int p, int sk, int skm) __attribute__((always_inline)) {
-    if (role == kTrail) { if (VO_BA_EXP != 1) trail_step(p, sk); }
-    else if (role == kFwd) { if (VO_BA_EXP != 2) fwd_step(p, sk); }
-    else if (role == kLoad) { if (VO_BA_EXP != 3) load_step(p, skm); }
+    if (role == kTrail) {
+      // ring mode: column p - 1's record read first (its latency under the trailing
+      // update), stored to global memory last
+      i32x4 v2[3];
+      if (!kFull && p >= 1) rec_load(skm, v2);
+      if (VO_BA_EXP != 1) trail_step(p, sk);
+      if (!kFull && p >= 1) rec_store(p - 1, v2);
+    } else if (role == kFwd) {
+      if (VO_BA_EXP != 2) fwd_step(p, sk);
+    } else if (role == kLoad) {
+      if (VO_BA_EXP != 3) load_step(p);
+    }
   };
 
   // Full mode: every block L_{k,i} (k - w <= i < k) is replaced by G = L_kk^-1 L_{k,i}
@@ -583,6 +614,15 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       }
     }
   }
+  if (!kFull && !prior_fail) {  // each side's last record (no later step copies it)
+    band_barrier();
+    const int last = sbot ? nb - 1 : ncolT - 1;
+    if (role == kTrail && last >= 0) {
+      i32x4 v2[3];
+      rec_load(last % RC, v2);
+      rec_store(last, v2);
+    }
+  }
   if (lane == 0 && bad) s_fail = 1;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // factor records written
   BST(8);
@@ -650,13 +690,28 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     if (!kFull) fwd6(o.L, o.r, o.Lc);  // g, independent of z_k
     double z[6];
     const int G = sbot ? F - 1 - k : k;
+    // z's LDS accesses in asm: a compiled LDS access here would first wait for every
+    // outstanding global load (LDS-DMA shares the counter), i.e. for the prefetched operands
+    // of the next two steps
     if (k >= kp) {
-      ld6g(zs + 6 * G, z);  // the separator's z (top side)
+      const uint32_t a = (uint32_t)(uintptr_t)(zs + 6 * G);  // the separator's z (top side)
+      asm volatile(
+          "ds_read_b128 %0, %3\n\t"
+          "ds_read_b128 %1, %3 offset:16\n\t"
+          "ds_read_b128 %2, %3 offset:32\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=v"(*reinterpret_cast<double2*>(&z[0])), "=v"(*reinterpret_cast<double2*>(&z[2])),
+            "=v"(*reinterpret_cast<double2*>(&z[4]))
+          : "v"(a)
+          : "memory");
     } else {
       const int l0 = __builtin_amdgcn_readfirstlane(6 * g0);
 #pragma unroll
       for (int c = 0; c < 6; ++c) z[c] = readlane_d(Yb, l0 + c);
-      if (act && qb == 0) zs[6 * G + sr] = Yb;
+      if (act && qb == 0) {
+        const uint32_t a = (uint32_t)(uintptr_t)(zs + 6 * G + sr);
+        asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(Yb) : "memory");
+      }
     }
     if (act && qb >= 1)
       Yb -= o.Lc[0] * z[0] + o.Lc[1] * z[1] + o.Lc[2] * z[2] + o.Lc[3] * z[3] + o.Lc[4] * z[4] + o.Lc[5] * z[5];
@@ -765,6 +820,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       bs_go(m + sp - 1, m, INT_MAX);
     }
     BST(10);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm z stores retired
     __syncthreads();  // the separator's z in LDS
     BST(11);
     if (role == kChain && side == 0 && m > 0) {
@@ -777,6 +833,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     }
   }
   BST(12);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
   BST(13);
 
