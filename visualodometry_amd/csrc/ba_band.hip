@@ -424,20 +424,20 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     const int qf = lane / 6, rf = lane % 6;
     const bool on = (qf >= 1) & (qf < R) & (k + qf < snload);  // rows past the side: none
     ld6g(col + (on ? 36 * qf + 6 * rf : 0), row);
+    // the rhs entry this lane updates, read with the other operands (its latency under fwd6)
+    const int st = sk + qf < RC ? sk + qf : sk + qf - RC;
+    int o = on ? (int)(sring - dyn) + st * SS + 36 * R + rf : DOFF + lane;
+    int o2 = lane < 6 ? (int)(col - dyn) + 36 * R + lane : DOFF + lane;
+    asm volatile("" : "+v"(o), "+v"(o2));
+    const double yo = dyn[o];
     BSETTLE(row[5]);
     BSTF(24);
     fwd6(L, r, y);
     bad = bad | !isfinite(y[0] + y[1] + y[2] + y[3] + y[4] + y[5]);
     BSETTLE(y[5]);
     BSTF(25);
-    {
-      const int st = sk + qf < RC ? sk + qf : sk + qf - RC;
-      int o = on ? (int)(sring - dyn) + st * SS + 36 * R + rf : DOFF + lane;
-      int o2 = lane < 6 ? (int)(col - dyn) + 36 * R + lane : DOFF + lane;
-      asm volatile("" : "+v"(o), "+v"(o2));
-      dyn[o] -= row[0] * y[0] + row[1] * y[1] + row[2] * y[2] + row[3] * y[3] + row[4] * y[4] + row[5] * y[5];
-      dyn[o2] = pick<6>(y, lane);
-    }
+    dyn[o] = yo - (row[0] * y[0] + row[1] * y[1] + row[2] * y[2] + row[3] * y[3] + row[4] * y[4] + row[5] * y[5]);
+    dyn[o2] = pick<6>(y, lane);
     BSETTLE(y[0]);
     BSTF(27);
   };
