@@ -510,24 +510,47 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
   double cost = 0.0;
   st.count(kPhSlots, nslots);
   st.count(kPhCams, ncams);
+  // staging of a chunk: one 16-byte load of its image and of its landmark positions
+  // (state) per thread, issued one chunk ahead (the next chunk's landmarks are disjoint from
+  // the ones this chunk's back substitution writes); headers are read two chunks ahead
+  constexpr int kImgVec = (int)(sizeof(ChunkImg) / 16);
+  static_assert(kImgVec <= kLinThreads && 3 * kChunkPts <= kLinThreads, "one staging element per thread");
+  const int i0 = tid;
+  auto stage_img = [&](int c) { return reinterpret_cast<const uint4*>(A.chunk_img + c)[min(tid, kImgVec - 1)]; };
+  auto stage_x = [&](const int4& hp) { return A.points[3l * hp.x + min(i0, max(3 * hp.y - 1, 0))]; };
+  uint4 v_img = stage_img(ch0);
+  double v_x = stage_x(h1);
+  int4 n0, n1, n2, n3;  // the next chunk's header
+  {
+    const int chn = min(ch0 + 1, ch1 - 1);
+    n0 = A.chunk_hdr[4l * chn];
+    n1 = A.chunk_hdr[4l * chn + 1];
+    n2 = A.chunk_hdr[4l * chn + 2];
+    n3 = A.chunk_hdr[4l * chn + 3];
+  }
   for (int ch = ch0; ch < ch1; ++ch) {
-    // this chunk's header is in registers (segment header, or prefetched one chunk
-    // ahead); every list load of the chunk is in flight at once
-    const int chn = min(ch + 1, ch1 - 1);
-    const int4 n0 = A.chunk_hdr[4l * chn], n1 = A.chunk_hdr[4l * chn + 1], n2 = A.chunk_hdr[4l * chn + 2],
-               n3 = A.chunk_hdr[4l * chn + 3];
+    const int chn = min(ch + 1, ch1 - 1), chn2 = min(ch + 2, ch1 - 1);
+    const int4 m0 = A.chunk_hdr[4l * chn2], m1 = A.chunk_hdr[4l * chn2 + 1], m2 = A.chunk_hdr[4l * chn2 + 2],
+               m3 = A.chunk_hdr[4l * chn2 + 3];
+    const uint4 w_img = stage_img(chn);
+    const double w_x = stage_x(n1);
     const int nob = h0.y, nte = h0.w, p0 = h1.x, npt = h1.y, e0 = h2.x, e1 = h2.y;
     st.count(kPhObs, nob);
     st.count(kPhTe, nte);
     st.count(kPhPts, npt);
     st.count(kPhPairs, e1 - e0);
-    // staging: one 16-byte load of the chunk image and the chunk's landmark positions
-    // (state), both issued before the previous chunk is released
-    constexpr int kImgVec = (int)(sizeof(ChunkImg) / 16);
-    static_assert(kImgVec <= kLinThreads && 3 * kChunkPts <= kLinThreads, "one staging element per thread");
-    const uint4 v_img = reinterpret_cast<const uint4*>(A.chunk_img + ch)[min(tid, kImgVec - 1)];
-    const int i0 = tid;
-    const double v_x = A.points[3l * p0 + min(i0, max(3 * npt - 1, 0))];
+    auto rotate = [&]() {
+      h0 = n0;
+      h1 = n1;
+      h2 = n2;
+      h3 = n3;
+      n0 = m0;
+      n1 = m1;
+      n2 = m2;
+      n3 = m3;
+      v_img = w_img;
+      v_x = w_x;
+    };
     __syncthreads();  // previous chunk fully consumed
     if (tid < kImgVec) reinterpret_cast<uint4*>(&S.img)[tid] = v_img;
     if (i0 < 3 * npt) (&S.X[0][0])[i0] = v_x;
@@ -542,10 +565,7 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
 
     if (!(MODE & kAccum)) {
       lin_obs(S, A, S.pose_n, nob, cost);  // cost at the updated state
-      h0 = n0;
-      h1 = n1;
-      h2 = n2;
-      h3 = n3;
+      rotate();
       continue;
     }
     lin_obs(S, A, S.pose_n, nob, cost);
@@ -674,10 +694,7 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
       }
     }
     st.mark(kPhSchurU);
-    h0 = n0;
-    h1 = n1;
-    h2 = n2;
-    h3 = n3;
+    rotate();
   }
   __syncthreads();
   if (MODE & kAccum) {  // window slots to their profile-major slab rows (K2 reads them in order)
