@@ -85,3 +85,45 @@ def test_plan_digests_pinned():
 
     want = json.loads((ROOT / "tests" / "golden" / "plan_digests.json").read_text())
     assert make_plan_digests.digests() == want
+
+
+def test_plan_digest_independent_of_concurrent_planners():
+    """Plans built by several host threads at once (one takes the persistent planner pool,
+    the others start their own threads: ba_plan.cpp PlanPool) are the same plan as one
+    built alone -- the parallel planner writes disjoint, precomputed ranges only."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from visualodometry_amd.ba import plan_digest
+
+    p = make_ba_config("cfg3")
+    alone = plan_digest(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 1024)
+    with ThreadPoolExecutor(4) as ex:
+        got = list(ex.map(lambda _: plan_digest(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 1024),
+                          range(8)))
+    assert got == [alone] * 8
+
+
+def test_csr_from_obs_pt_rejects_out_of_range():
+    with pytest.raises(ValueError):
+        csr_from_obs_pt(3, np.array([0, 3]))
+    with pytest.raises(ValueError):
+        csr_from_obs_pt(3, np.array([-1, 0]))
+
+
+def test_group_window_passes_grouped_windows_through():
+    """Windows built landmark by landmark keep their arrays; others are reordered stably."""
+    from visualodometry_amd.ba import BAWindow, group_window
+
+    obs_pt = np.array([0, 0, 1, 2, 2, 2])
+    cam = np.arange(6, dtype=np.int32)
+    uv = np.arange(12, dtype=np.float32).reshape(6, 2)
+    w = BAWindow(np.zeros((3, 4, 4)), np.zeros((3, 3)), uv, cam, obs_pt, 1)
+    ptr_, cam2, uv2 = group_window(3, w)
+    np.testing.assert_array_equal(ptr_, [0, 2, 3, 6])
+    assert cam2 is w.obs_cam or np.shares_memory(cam2, w.obs_cam)
+    perm = np.array([3, 0, 5, 2, 1, 4])
+    w2 = BAWindow(np.zeros((3, 4, 4)), np.zeros((3, 3)), uv[perm], cam[perm], obs_pt[perm], 1)
+    ptr2, cam3, uv3 = group_window(3, w2)
+    np.testing.assert_array_equal(ptr2, [0, 2, 3, 6])
+    np.testing.assert_array_equal(cam3, [0, 1, 2, 3, 5, 4])  # stable within a landmark
+    np.testing.assert_array_equal(uv3, uv[[0, 1, 2, 3, 5, 4]])
