@@ -96,33 +96,61 @@ static void se3_apply(const double d[6], const double* T, double* out) {
   }
 }
 
-/* Dense lower Cholesky in place + solve; returns 0 if S is not positive definite. */
+/* Lower Cholesky in place + solve; returns 0 if S is not positive definite.  The
+ * arithmetic is the dense algorithm's, term for term; entries outside the envelope of S
+ * (left of each row's first nonzero, which the factor keeps) are exact zeros, and the
+ * loops skip them, so the result is bitwise the dense one at O(n bw^2) instead of O(n^3)
+ * (the CPU baseline then pays for the arithmetic S needs, not for zeros). */
 static int chol_solve(double* S, int n, double* x, int nthreads) {
-  for (int k = 0; k < n; ++k) {
+  (void)nthreads;
+  int* first = (int*)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  int* last = (int*)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  for (int i = 0; i < n; ++i) {
+    int f = i;
+    for (int j = 0; j < i; ++j)
+      if (S[(int64_t)i * n + j] != 0.0) {
+        f = j;
+        break;
+      }
+    first[i] = f;
+    last[i] = i;
+  }
+  for (int i = 0; i < n; ++i)
+    for (int k = first[i]; k < i; ++k)
+      if (last[k] < i) last[k] = i;
+  int ok = 1;
+  for (int k = 0; k < n && ok; ++k) {
     const double d = S[(int64_t)k * n + k];
-    if (!(d > 0.0)) return 0;
+    if (!(d > 0.0)) {
+      ok = 0;
+      break;
+    }
     const double l = sqrt(d), il = 1.0 / l;
     S[(int64_t)k * n + k] = l;
-    for (int i = k + 1; i < n; ++i) S[(int64_t)i * n + k] *= il;
-#pragma omp parallel for schedule(static) num_threads(nthreads) if (n - k > 64)
-    for (int i = k + 1; i < n; ++i) {
+    for (int i = k + 1; i <= last[k]; ++i) S[(int64_t)i * n + k] *= il;
+    for (int i = k + 1; i <= last[k]; ++i) {
+      if (first[i] > k) continue;  /* l_ik == 0 */
       const double lik = S[(int64_t)i * n + k];
       double* row = S + (int64_t)i * n;
-      const double* colk = S;
-      for (int j = k + 1; j <= i; ++j) row[j] -= lik * colk[(int64_t)j * n + k];
+      for (int j = k + 1; j <= i; ++j)
+        if (first[j] <= k) row[j] -= lik * S[(int64_t)j * n + k];
     }
   }
-  for (int i = 0; i < n; ++i) {
-    double s = x[i];
-    for (int m = 0; m < i; ++m) s -= S[(int64_t)i * n + m] * x[m];
-    x[i] = s / S[(int64_t)i * n + i];
+  if (ok) {
+    for (int i = 0; i < n; ++i) {
+      double s = x[i];
+      for (int m = first[i]; m < i; ++m) s -= S[(int64_t)i * n + m] * x[m];
+      x[i] = s / S[(int64_t)i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      double s = x[i];
+      for (int m = i + 1; m <= last[i]; ++m) s -= S[(int64_t)m * n + i] * x[m];
+      x[i] = s / S[(int64_t)i * n + i];
+    }
   }
-  for (int i = n - 1; i >= 0; --i) {
-    double s = x[i];
-    for (int m = i + 1; m < n; ++m) s -= S[(int64_t)m * n + i] * x[m];
-    x[i] = s / S[(int64_t)i * n + i];
-  }
-  return 1;
+  free(first);
+  free(last);
+  return ok;
 }
 
 typedef struct {
@@ -206,8 +234,11 @@ int oracle_ba_step(int N, int L, int n_fixed, double fx, double fy, double cx, d
   double* S = part[0].S;
   double* b = part[0].b;
   double cost = part[0].cost;
+  /* thread partials summed in thread order per entry (entries in parallel) */
+#pragma omp parallel for schedule(static) num_threads(nt)
+  for (int64_t e = 0; e < (int64_t)n * n; ++e)
+    for (int t = 1; t < nt; ++t) S[e] += part[t].S[e];
   for (int t = 1; t < nt; ++t) {
-    for (int64_t e = 0; e < (int64_t)n * n; ++e) S[e] += part[t].S[e];
     for (int e = 0; e < n; ++e) b[e] += part[t].b[e];
     cost += part[t].cost;
   }
