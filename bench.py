@@ -85,7 +85,7 @@ def cpu_baseline_ba(p, lam: float, budget_s: float = 3.0):
         if dt >= budget_s or n >= 2000:
             break
     return {"value": n / dt, "unit": "GN-iters/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ba_ref.c (OpenMP, dense Schur + dense Cholesky) on the same cfg3 "
+            "sample": f"oracle/ba_ref.c (OpenMP Schur accumulation into a dense S, Cholesky over its envelope) on the same cfg3 "
                       f"window: {n} GN iterations in {dt:.2f} s; {note}"}
 
 
