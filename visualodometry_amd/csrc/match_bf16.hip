@@ -337,7 +337,7 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4) {
   const int b = blockIdx.y, R = blockIdx.x, tid = threadIdx.x;
   if (R == 0 && tid == 0) p.bmax[b] = 0u;  // fsweep<2> is done with it
   __shared__ __attribute__((aligned(16))) float sq[16 * kQStr];
-  __shared__ int slist[kPool];      // row_local << 16 | column tile bit position (see below)
+  __shared__ __attribute__((aligned(8))) int slist[kPool];  // row_local << 16 | column tile bit position (see below)
   __shared__ int scol[kPool];
   __shared__ uint64_t skey[kPool];
   __shared__ int sscan[256];
@@ -385,9 +385,21 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4) {
       skey[c] = key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)j);
     }
     __syncthreads();
-    if (tid < 16)
-      for (int c = 0; c < total; ++c)
-        if (slist[c] == tid) merge2s(k1, k2, skey[c], ~0ull);
+    // row r's keys merged by 16 threads (r + 16 part, every 16th pooled candidate), then
+    // their 16 partial top-2s by thread r (keys are unique: the order does not matter)
+    {
+      const int r = tid & 15, part = tid >> 4;
+      uint64_t a1 = ~0ull, a2 = ~0ull;
+      for (int c = part; c < total; c += 16)
+        if (slist[c] == r) merge2s(a1, a2, skey[c], ~0ull);
+      __syncthreads();  // skey / scol are free now: partials in their place
+      skey[tid] = a1;
+      reinterpret_cast<uint64_t*>(slist)[tid] = a2;
+      __syncthreads();
+      if (tid < 16)
+        for (int q = 0; q < 16; ++q)
+          merge2s(k1, k2, skey[tid + 16 * q], reinterpret_cast<const uint64_t*>(slist)[tid + 16 * q]);
+    }
   } else if (tid < 16) {  // rare: thread r walks row r's candidates itself
     const int g = tid >> 2, r = tid & 3;
     for (int t = 0; t < T; ++t)
