@@ -342,9 +342,26 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4) {
   __shared__ uint64_t skey[kPool];
   __shared__ int sscan[256];
   const int row0 = 16 * R;
-  for (int e = tid; e < 16 * p.dim; e += 256) {
-    const int rl = e / p.dim, k = e - rl * p.dim;
-    sq[rl * kQStr + k] = row0 + rl < p.n0 ? p.da[b * p.a_bstride + (long)(row0 + rl) * p.dim + k] : 0.0f;
+  if (v4) {  // the block's 16 query rows as float4s, every load in flight before the stores
+    const int nv = p.dim / 4, nall = 16 * nv;  // dim <= 256: at most 4 per thread
+    float4 tq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u, rl = e / max(nv, 1), k4 = e - rl * nv;
+      tq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < nall && row0 + rl < p.n0)
+        tq[u] = reinterpret_cast<const float4*>(p.da + b * p.a_bstride + (long)(row0 + rl) * p.dim)[k4];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u, rl = e / max(nv, 1), k4 = e - rl * nv;
+      if (e < nall) *reinterpret_cast<float4*>(sq + rl * kQStr + 4 * k4) = tq[u];
+    }
+  } else {
+    for (int e = tid; e < 16 * p.dim; e += 256) {
+      const int rl = e / p.dim, k = e - rl * p.dim;
+      sq[rl * kQStr + k] = row0 + rl < p.n0 ? p.da[b * p.a_bstride + (long)(row0 + rl) * p.dim + k] : 0.0f;
+    }
   }
   const int T = p.n1_pad / 16;
   const uint64_t* mblk = p.mask + ((long)b * (p.n0_pad / 16) + R) * 4 * T;  // (r, t) entries
