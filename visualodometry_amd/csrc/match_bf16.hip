@@ -296,18 +296,22 @@ __device__ __forceinline__ void merge2s(uint64_t& a1, uint64_t& a2, uint64_t b1,
 // candidates takes its rows one at a time through the same code.
 constexpr int kPool = 1024;
 constexpr int kQStr = 260;  // floats per staged query row
+#ifndef VO_CHAIN_SPAN
+#define VO_CHAIN_SPAN 128
+#endif
+constexpr int kChainSpan = VO_CHAIN_SPAN;  // train-row elements loaded before their chain
 
 __device__ __forceinline__ float chain_regs(const float* x, const float* y, int dim) {
   // the oracle's distance: sum over k ascending of fmaf(x_k - y_k, x_k - y_k, acc); the
-  // train row y (global) arrives 128 elements at a time, every load in flight first
+  // train row y (global) arrives kChainSpan elements at a time, every load in flight first
   float acc = 0.0f;
-  for (int h = 0; h < dim; h += 128) {
-    float4 yr[32];
+  for (int h = 0; h < dim; h += kChainSpan) {
+    float4 yr[kChainSpan / 4];
 #pragma unroll
-    for (int t = 0; t < 32; ++t)
+    for (int t = 0; t < kChainSpan / 4; ++t)
       yr[t] = h + 4 * t < dim ? *reinterpret_cast<const float4*>(y + h + 4 * t) : make_float4(0, 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < 32; ++t) {
+    for (int t = 0; t < kChainSpan / 4; ++t) {
       if (h + 4 * t >= dim) break;
       const float4 xv = *reinterpret_cast<const float4*>(x + h + 4 * t);
       float d = xv.x - yr[t].x;
