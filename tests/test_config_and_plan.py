@@ -127,3 +127,25 @@ def test_group_window_passes_grouped_windows_through():
     np.testing.assert_array_equal(ptr2, [0, 2, 3, 6])
     np.testing.assert_array_equal(cam3, [0, 1, 2, 3, 5, 4])  # stable within a landmark
     np.testing.assert_array_equal(uv3, uv[[0, 1, 2, 3, 5, 4]])
+
+
+def test_plan_in_forked_child():
+    """A child forked after the planner pool started (its threads do not survive fork)
+    still plans, and gets the same plan."""
+    import os
+    import signal
+
+    from visualodometry_amd.ba import plan_digest
+
+    p = make_ba_config("cfg2")
+    d0 = plan_digest(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 1024)
+    pid = os.fork()
+    if pid == 0:  # child: exit status says whether it matched; an alarm ends a hang
+        signal.alarm(60)
+        try:
+            d1 = plan_digest(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 1024)
+            os._exit(0 if d1 == d0 else 3)
+        except BaseException:
+            os._exit(4)
+    _, status = os.waitpid(pid, 0)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0

@@ -6,6 +6,8 @@
 #include <mutex>
 #include <thread>
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <numeric>
@@ -51,6 +53,14 @@ class PlanPool {
   }
   template <class Fn>
   void run(int n, Fn&& fn) {
+    // a forked child inherits the pool object but not its threads: it plans on its own
+    if (getpid() != owner_) {
+      std::vector<std::thread> pool;
+      for (int t = 1; t < n; ++t) pool.emplace_back([&fn, t] { fn(t); });
+      fn(0);
+      for (auto& th : pool) th.join();
+      return;
+    }
     std::unique_lock<std::mutex> busy(use_, std::try_to_lock);
     if (!busy.owns_lock() || n - 1 > (int)workers_.size()) {
       std::vector<std::thread> pool;
@@ -83,7 +93,7 @@ class PlanPool {
   }
 
  private:
-  PlanPool() {
+  PlanPool() : owner_(getpid()) {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     for (unsigned t = 1; t < std::min(hw, 8u); ++t) workers_.emplace_back([this, t] { loop((int)t); });
   }
@@ -104,6 +114,7 @@ class PlanPool {
       if (--pending_ == 0) done_.notify_one();
     }
   }
+  pid_t owner_;
   std::vector<std::thread> workers_;
   std::mutex use_, mu_;
   std::condition_variable cv_, done_;
