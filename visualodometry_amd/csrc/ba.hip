@@ -134,6 +134,20 @@ void Comm::allreduce(T* dbuf, size_t n, bool is_min, hipStream_t st) {
   VO_HIP_CHECK(hipStreamSynchronize(st));
 }
 
+void* plan_host_alloc(size_t bytes, bool pinned) {
+  void* p = nullptr;
+  if (pinned) {
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 64), hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+    return p;
+  }
+  return ::operator new(std::max<size_t>(bytes, 64), std::align_val_t(64));
+}
+
+void plan_host_free(void* p, bool pinned) noexcept {
+  if (!p) return;
+  if (pinned) (void)hipHostFree(p);
+  else ::operator delete(p, std::align_val_t(64));
+}
 
 namespace {
 
@@ -1235,6 +1249,9 @@ class BAEngine {
 #ifdef VO_PLAN_TIMING
     auto t_ = std::chrono::steady_clock::now();
 #endif
+    // the previous setup's chunk-image DMA may still read the page-locked images the
+    // planner is about to rewrite (a setup that failed after its upload returns unsynced)
+    VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
     have_problem_ = false;
     have_state_ = false;
     std::string err;
@@ -1263,6 +1280,9 @@ class BAEngine {
       if (err.empty() && agree[1] != -agree[2]) err = "ranks disagree on the number of free poses";
     }
     VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_setup: %s", err.c_str());
+    // the largest plan array first: from page-locked memory the copy runs while the host
+    // builds the profile and the K3 tables
+    upload(d_chunk_img_, plan_.chunk_img, ctx_->stream);
     PLAN_T("setup: plan");
     std::vector<int32_t> first = local_profile_first(plan_);
     if (ctx_->comm && ctx_->comm->nranks > 1 && !first.empty()) {
@@ -1283,7 +1303,6 @@ class BAEngine {
     hipStream_t st = ctx_->stream;
     const BAPlan& P = plan_;
     upload(d_chunk_hdr_, P.chunk_hdr, st);
-    upload(d_chunk_img_, P.chunk_img, st);
     upload(d_slab_pos_, P.slab_pos, st);
     upload(d_cam_pos_, P.cam_pos, st);
     upload(d_seg_hdr_, P.seg_hdr, st);
@@ -1722,7 +1741,7 @@ class BAEngine {
   }
 
   vo_ctx* ctx_;
-  BAPlan plan_;
+  BAPlan plan_{true};  // page-locked chunk images (async upload)
   vo_ba_problem prob_{};
   bool have_problem_ = false, have_state_ = false, pending_ = false, solve_lds_ = false;
   uint64_t session_ = 0;

@@ -21,6 +21,8 @@
 
 #include <cstdint>
 #include <memory>
+#include <new>
+#include <type_traits>
 #include <utility>
 #include <string>
 #include <vector>
@@ -84,17 +86,28 @@ struct alignas(16) ChunkImg {
 };
 static_assert(sizeof(ChunkImg) % 16 == 0, "16-byte staging granules");
 
-// Allocator whose resize() default-initialises (leaves a trivial type unwritten): the
-// planner writes every chunk image in full, on its worker threads.
+// Host memory of the chunk images (defined in ba.hip): page-locked (hipHostMalloc) for the
+// BA engine's plan, so vo_ba_setup's upload of the largest plan array is an asynchronous
+// DMA that overlaps the rest of setup; ordinary heap memory for the plans the digest and
+// probe entry points build (they run on hosts without a GPU).  Throws std::bad_alloc.
+void* plan_host_alloc(size_t bytes, bool pinned);
+void plan_host_free(void* p, bool pinned) noexcept;
+
+// Allocator of the chunk images: resize() default-initialises (leaves a trivial type
+// unwritten; the planner writes every image in full, on its worker threads), and the
+// memory kind is part of the allocator's state.
 template <class T>
-struct DefaultInitAlloc : std::allocator<T> {
+struct PlanHostAlloc {
+  using value_type = T;
+  using propagate_on_container_move_assignment = std::true_type;
+  using propagate_on_container_swap = std::true_type;
+  bool pinned = false;
+  PlanHostAlloc() = default;
+  explicit PlanHostAlloc(bool p) noexcept : pinned(p) {}
   template <class U>
-  struct rebind {
-    using other = DefaultInitAlloc<U>;
-  };
-  DefaultInitAlloc() = default;
-  template <class U>
-  DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+  PlanHostAlloc(const PlanHostAlloc<U>& o) noexcept : pinned(o.pinned) {}
+  T* allocate(size_t n) { return static_cast<T*>(plan_host_alloc(n * sizeof(T), pinned)); }
+  void deallocate(T* p, size_t) noexcept { plan_host_free(p, pinned); }
   template <class U>
   void construct(U* p) noexcept {
     ::new (static_cast<void*>(p)) U;
@@ -103,6 +116,8 @@ struct DefaultInitAlloc : std::allocator<T> {
   void construct(U* p, Args&&... args) {
     ::new (static_cast<void*>(p)) U(std::forward<Args>(args)...);
   }
+  friend bool operator==(const PlanHostAlloc& a, const PlanHostAlloc& b) { return a.pinned == b.pinned; }
+  friend bool operator!=(const PlanHostAlloc& a, const PlanHostAlloc& b) { return a.pinned != b.pinned; }
 };
 
 struct SolveTableLayout {
@@ -133,7 +148,7 @@ struct BAPlan {
   // (the inverse of camb_src); K1 writes there so K2 reads contiguous rows
   std::vector<int32_t> slab_pos, cam_pos;
   std::vector<int32_t> seg_hdr;  // kSegHdr ints per segment
-  std::vector<ChunkImg, DefaultInitAlloc<ChunkImg>> chunk_img;
+  std::vector<ChunkImg, PlanHostAlloc<ChunkImg>> chunk_img;
   std::vector<int32_t> slot_ptr;   // per chunk: nslots(seg)+1 offsets into pair_list
   std::vector<uint16_t> pair_list; // (te_x_local | te_y_local << 8)
   std::vector<int32_t> cam_ptr;    // per chunk: ncams(seg)+1 offsets into cam_list
@@ -159,6 +174,8 @@ struct BAPlan {
   std::vector<int32_t> solve_tab;
   SolveTableLayout solve_layout;
 
+  BAPlan() = default;
+  explicit BAPlan(bool pinned_images) : chunk_img(PlanHostAlloc<ChunkImg>(pinned_images)) {}
   void reset();  // empty every array, keep its capacity (a session's next window reuses it)
   int n_chunks() const { return (int)chunk_obs.size() - 1; }
   int n_segments() const { return (int)seg_chunk.size() - 1; }

@@ -25,6 +25,14 @@
 #ifndef VO_MATCH_WGS_PER_CU
 #define VO_MATCH_WGS_PER_CU 2
 #endif
+// Tuning builds only (EXTRA=-D...): columns per LDS-staged B chunk (64 or 128) and
+// s_setprio around each tile's MFMA issue.
+#ifndef VO_MATCH_CHUNK
+#define VO_MATCH_CHUNK 64
+#endif
+#ifndef VO_MATCH_PRIO
+#define VO_MATCH_PRIO 0
+#endif
 
 namespace vo {
 namespace {
@@ -35,6 +43,9 @@ constexpr int kKStep = 64;          // K of v_mfma_i32_16x16x64_i8
 constexpr int kMaxDpInt = 256;      // int path keeps A fragments in registers
 constexpr int kRowsPerWave = 64;    // 4 M-tiles of 16 rows
 constexpr int kRowsPerWG = 256;     // 4 waves
+constexpr int kMatchChunk = VO_MATCH_CHUNK;
+constexpr bool kMatchPrio = VO_MATCH_PRIO != 0;
+static_assert(kMatchChunk == 64 || kMatchChunk == 128, "B chunk of 64 or 128 columns");
 // Key range: |a'|^2 <= Dp * 128^2 and d2 - |a'|^2 = sum(b'^2 - 2 a'b') <= Dp * 48896, so
 // d2 - |a'|^2 lies in [-Dp * 16384, Dp * 48896]: 24 key bits + 8 column-tile bits.
 // int8 path keys are kept in max form: ((2 a'.b' - |b'|^2 + off) << 8) | (255 - tile)
@@ -224,21 +235,29 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
   // per workgroup instead of one per wave): 4 threads per column, rows padded to
   // Dp + 16 bytes so a wave's 16-lane ds_read_b128 groups hit distinct banks.
   constexpr int kRow = Dp + 16;
-  __shared__ __attribute__((aligned(16))) int8_t sB[2][64 * kRow];
-  __shared__ uint32_t sC[2][64];
+  constexpr int kCols = kMatchChunk;  // columns per staged chunk
+  constexpr int kNH = kCols / 64;     // 64-column pieces per thread
+  __shared__ __attribute__((aligned(16))) int8_t sB[2][kCols * kRow];
+  __shared__ uint32_t sC[2][kCols];
   const int tid = threadIdx.x;
-  auto gload = [&](int cbase, v4i (&g)[KS], uint32_t& gc) {
-    const int col = min(cbase + (tid >> 2), c1 - 1);  // clamped, unconditional
-    const int8_t* src = B + (long)col * Dp + (tid & 3) * 16 * KS;
+  auto gload = [&](int cbase, v4i (&g)[kNH][KS], uint32_t& gc) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) g[ks] = *reinterpret_cast<const v4i*>(src + 16 * ks);
-    gc = cc[min(cbase + (tid & 63), c1 - 1)];
+    for (int h = 0; h < kNH; ++h) {
+      const int col = min(cbase + 64 * h + (tid >> 2), c1 - 1);  // clamped, unconditional
+      const int8_t* src = B + (long)col * Dp + (tid & 3) * 16 * KS;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) g[h][ks] = *reinterpret_cast<const v4i*>(src + 16 * ks);
+    }
+    gc = cc[min(cbase + (tid & (kCols - 1)), c1 - 1)];
   };
-  auto sstore = [&](int buf, const v4i (&g)[KS], uint32_t gc) {
-    int8_t* dst = &sB[buf][(tid >> 2) * kRow + (tid & 3) * 16 * KS];
+  auto sstore = [&](int buf, const v4i (&g)[kNH][KS], uint32_t gc) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<v4i*>(dst + 16 * ks) = g[ks];
-    if (tid < 64) sC[buf][tid] = gc;
+    for (int h = 0; h < kNH; ++h) {
+      int8_t* dst = &sB[buf][(64 * h + (tid >> 2)) * kRow + (tid & 3) * 16 * KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<v4i*>(dst + 16 * ks) = g[h][ks];
+    }
+    if (tid < kCols) sC[buf][tid] = gc;
   };
   // One 16-column tile: its B fragments and column constants from LDS (frag), the
   // four row tiles' MFMAs into separate accumulators (mm), then the top-2 update
@@ -262,11 +281,13 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
     Acc a;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) a.v[mt] = v4i{0, 0, 0, 0};
+    if (kMatchPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         a.v[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], f.bf[ks], a.v[mt], 0, 0, 0);
+    if (kMatchPrio) __builtin_amdgcn_s_setprio(0);
     return a;
   };
   auto epi = [&](const Acc& a, uint32_t ccol) {
@@ -280,17 +301,17 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
       }
   };
   if (c0 < c1) {  // uniform over the workgroup (split bounds)
-    const int nchunk = (c1 - c0 + 63) / 64;
-    v4i g[KS];
+    const int nchunk = (c1 - c0 + kCols - 1) / kCols;
+    v4i g[kNH][KS];
     uint32_t gc;
     gload(c0, g, gc);
     sstore(0, g, gc);
     __syncthreads();
     for (int ch = 0; ch < nchunk; ++ch) {
-      const int buf = ch & 1, cb = c0 + 64 * ch;
-      if (ch + 1 < nchunk) gload(cb + 64, g, gc);  // in flight during this chunk
+      const int buf = ch & 1, cb = c0 + kCols * ch;
+      if (ch + 1 < nchunk) gload(cb + kCols, g, gc);  // in flight during this chunk
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < kCols / 16; ++u)
         if (cb + 16 * u < c1) {
           const Frag f = frag(buf, u);
           epi(mm(f), f.cc);
