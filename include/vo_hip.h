@@ -197,6 +197,9 @@ int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
  * src/modules/vo.py:252-288 builds the BA problem from the map's observation lists):
  * point_ptr (n_points + 1) and order (n_obs, stable: observations of one landmark keep the
  * caller's order), so that obs_cam[order] / obs_uv[order] are the problem's arrays.
+ * With order == NULL it only checks that the observations are already grouped
+ * (nondecreasing obs_pt, one pass) and fills point_ptr: returns 1 when they are not
+ * (point_ptr then unspecified; call again with an order array).
  * VO_ERR_ARG if an index is out of range. */
 int vo_ba_group_by_point(int n_points, int n_obs, const int32_t* obs_pt, int32_t* order, int32_t* point_ptr);
 /* Host-only: builds the static plan of `prob` without a device (planner tests,

@@ -129,6 +129,37 @@ def test_group_window_passes_grouped_windows_through():
     np.testing.assert_array_equal(uv3, uv[[0, 1, 2, 3, 5, 4]])
 
 
+def test_group_by_point_grouped_check():
+    """vo_ba_group_by_point with order == NULL: point_ptr of an already grouped window
+    (empty landmarks included), 1 for an ungrouped one, VO_ERR_ARG out of range."""
+    import ctypes as C
+
+    from visualodometry_amd import _lib
+    from visualodometry_amd._lib import ptr
+
+    lib = _lib.load()
+
+    def call(n_points, obs_pt):
+        x = np.ascontiguousarray(obs_pt, dtype=np.int32)
+        pp = np.full(n_points + 1, -7, dtype=np.int32)
+        return lib.vo_ba_group_by_point(n_points, x.size, ptr(x, C.c_int32), None, ptr(pp, C.c_int32)), pp
+
+    rc, pp = call(6, [1, 1, 3, 3, 3])
+    assert rc == _lib.VO_OK
+    np.testing.assert_array_equal(pp, [0, 0, 2, 2, 5, 5, 5])
+    rc, pp = call(3, [])
+    assert rc == _lib.VO_OK
+    np.testing.assert_array_equal(pp, [0, 0, 0, 0])
+    assert call(3, [0, 2, 1])[0] == 1
+    assert call(3, [0, 3])[0] == _lib.VO_ERR_ARG
+    assert call(3, [-1, 0])[0] == _lib.VO_ERR_ARG
+    rng = np.random.default_rng(3)
+    obs_pt = np.sort(rng.integers(0, 500, 4000))
+    rc, pp = call(500, obs_pt)
+    assert rc == _lib.VO_OK
+    np.testing.assert_array_equal(pp[1:], np.cumsum(np.bincount(obs_pt, minlength=500)))
+
+
 def test_plan_in_forked_child():
     """A child forked after the planner pool started (its threads do not survive fork)
     still plans, and gets the same plan."""

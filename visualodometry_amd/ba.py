@@ -83,14 +83,17 @@ def group_window(n_points: int, window: "BAWindow"):
     Windows built landmark by landmark (dropin/hooks.py ``KeyframeWindow.build``) are
     already grouped: their arrays pass through unchanged; others are reordered by
     ``csr_from_obs_pt``."""
-    obs_pt = np.asarray(window.obs_pt)
+    obs_pt = np.ascontiguousarray(window.obs_pt, dtype=np.int32).reshape(-1)
     obs_cam = np.asarray(window.obs_cam)
     obs_uv = np.asarray(window.obs_uv, dtype=np.float32).reshape(-1, 2)
-    n = obs_pt.size
-    if n and obs_pt[0] >= 0 and obs_pt[-1] < n_points and bool(np.all(obs_pt[1:] >= obs_pt[:-1])):
-        point_ptr = np.zeros(n_points + 1, np.int32)
-        np.cumsum(np.bincount(obs_pt, minlength=n_points), out=point_ptr[1:])
+    point_ptr = np.empty(int(n_points) + 1, dtype=np.int32)
+    # order == NULL: one pass that checks the grouping and fills point_ptr
+    rc = _lib.load().vo_ba_group_by_point(int(n_points), obs_pt.size, ptr(obs_pt, C.c_int32), None,
+                                          ptr(point_ptr, C.c_int32))
+    if rc == _lib.VO_OK:
         return point_ptr, obs_cam, obs_uv
+    if rc != 1:
+        raise ValueError("obs_pt out of range")
     order, point_ptr = csr_from_obs_pt(n_points, obs_pt)
     return point_ptr, obs_cam[order], obs_uv[order]
 

@@ -626,9 +626,30 @@ int vo_ba_plan_digest(const vo_ba_problem* prob, int target_segments, uint64_t* 
 }
 
 int vo_ba_group_by_point(int n_points, int n_obs, const int32_t* obs_pt, int32_t* order, int32_t* point_ptr) {
-  return guarded([&] {
+  int grouped = 1;
+  const int rc = guarded([&] {
     VO_REQUIRE(n_points >= 0 && n_obs >= 0, VO_ERR_ARG, "vo_ba_group_by_point: bad sizes");
-    VO_REQUIRE(point_ptr && (n_obs == 0 || (obs_pt && order)), VO_ERR_ARG, "vo_ba_group_by_point: null argument");
+    VO_REQUIRE(point_ptr && (n_obs == 0 || obs_pt), VO_ERR_ARG, "vo_ba_group_by_point: null argument");
+    if (!order) {  // already grouped (nondecreasing obs_pt)?  then only point_ptr
+      const int32_t* __restrict op = obs_pt;
+      int32_t* __restrict pp = point_ptr;
+      unsigned out_of_range = 0, descending = 0;  // branch-free scans
+      for (int o = 0; o < n_obs; ++o) out_of_range |= (unsigned)op[o] >= (unsigned)n_points;
+      for (int o = 1; o < n_obs; ++o) descending |= op[o] < op[o - 1];
+      if (out_of_range) {
+        int o = 0;
+        while ((unsigned)op[o] < (unsigned)n_points) ++o;
+        VO_REQUIRE(false, VO_ERR_ARG, "vo_ba_group_by_point: obs_pt[%d]=%d out of range", o, op[o]);
+      }
+      if (descending) {
+        grouped = 0;
+        return;
+      }
+      std::fill(pp, pp + n_points + 1, 0);
+      for (int o = 0; o < n_obs; ++o) ++pp[op[o] + 1];
+      for (int p = 0; p < n_points; ++p) pp[p + 1] += pp[p];
+      return;
+    }
     std::fill(point_ptr, point_ptr + n_points + 1, 0);
     for (int o = 0; o < n_obs; ++o) {
       VO_REQUIRE(obs_pt[o] >= 0 && obs_pt[o] < n_points, VO_ERR_ARG, "vo_ba_group_by_point: obs_pt[%d]=%d out of range",
@@ -639,6 +660,7 @@ int vo_ba_group_by_point(int n_points, int n_obs, const int32_t* obs_pt, int32_t
     std::vector<int32_t> next(point_ptr, point_ptr + std::max(n_points, 1));
     for (int o = 0; o < n_obs; ++o) order[next[obs_pt[o]]++] = o;  // stable: caller order within a landmark
   });
+  return rc == VO_OK && !grouped ? 1 : rc;
 }
 
 int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* out, int n) {
