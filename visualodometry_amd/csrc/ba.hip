@@ -1410,12 +1410,15 @@ class BAEngine {
     VO_REQUIRE(have_problem_, VO_ERR_STATE, "vo_ba_set_state before vo_ba_setup");
     const BAPlan& P = plan_;
     hipStream_t st = ctx_->stream;
-    VO_HIP_CHECK(hipMemcpyAsync(d_pose_[0].ptr, poses, P.n_poses * 96ull, hipMemcpyHostToDevice, st));
-    std::vector<double> pts(3ull * P.n_points);
+    // points gathered into internal order in the page-locked staging buffer, poses behind them
+    const size_t np = 3ull * P.n_points;
+    h_state_.reserve((np + 12ull * P.n_poses) * 8);
+    double* pts = h_state_.as<double>();
     for (int q = 0; q < P.n_points; ++q)
       for (int e = 0; e < 3; ++e) pts[3ull * q + e] = points[3ull * P.pt_perm[q] + e];
-    if (P.n_points)
-      VO_HIP_CHECK(hipMemcpyAsync(d_points_.ptr, pts.data(), pts.size() * 8, hipMemcpyHostToDevice, st));
+    std::memcpy(pts + np, poses, P.n_poses * 96ull);
+    VO_HIP_CHECK(hipMemcpyAsync(d_pose_[0].ptr, pts + np, P.n_poses * 96ull, hipMemcpyHostToDevice, st));
+    if (P.n_points) VO_HIP_CHECK(hipMemcpyAsync(d_points_.ptr, pts, np * 8, hipMemcpyHostToDevice, st));
     VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
     VO_HIP_CHECK(hipStreamSynchronize(st));
     cur_ = 0;
@@ -1428,11 +1431,13 @@ class BAEngine {
     finalize();
     const BAPlan& P = plan_;
     hipStream_t st = ctx_->stream;
-    std::vector<double> pts(3ull * P.n_points);
-    VO_HIP_CHECK(hipMemcpyAsync(poses, d_pose_[cur_].ptr, P.n_poses * 96ull, hipMemcpyDeviceToHost, st));
-    if (P.n_points)
-      VO_HIP_CHECK(hipMemcpyAsync(pts.data(), d_points_.ptr, pts.size() * 8, hipMemcpyDeviceToHost, st));
+    const size_t np = 3ull * P.n_points;
+    h_state_.reserve((np + 12ull * P.n_poses) * 8);
+    double* pts = h_state_.as<double>();
+    VO_HIP_CHECK(hipMemcpyAsync(pts + np, d_pose_[cur_].ptr, P.n_poses * 96ull, hipMemcpyDeviceToHost, st));
+    if (P.n_points) VO_HIP_CHECK(hipMemcpyAsync(pts, d_points_.ptr, np * 8, hipMemcpyDeviceToHost, st));
     VO_HIP_CHECK(hipStreamSynchronize(st));
+    std::memcpy(poses, pts + np, P.n_poses * 96ull);
     for (int q = 0; q < P.n_points; ++q)
       for (int e = 0; e < 3; ++e) points[3ull * P.pt_perm[q] + e] = pts[3ull * q + e];
   }
@@ -1756,6 +1761,7 @@ class BAEngine {
   std::vector<int32_t> red_dst_, red_rdst_;  // K2 output offsets (host copies for gn_step)
   long cost_off_ = 0;
   DevBuf d_solve_tab_;
+  HostBuf h_state_;  // page-locked staging of set_state / get_state
   DevBuf d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;  // K1's plan (the chunk images hold every list)
   DevBuf d_prof_src_ptr_, d_prof_diag_, d_prof_row_, d_camb_ptr_, d_stamps_, d_stamps3_;
   static constexpr bool stamps_on_ = kBaStamps;

@@ -61,6 +61,27 @@ struct DevBuf {
   ~DevBuf() { release(); }
 };
 
+// Page-locked host staging buffer that grows on demand (asynchronous DMA, no page faults).
+struct HostBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  void reserve(size_t n) {
+    if (n <= bytes) return;
+    if (ptr) VO_HIP_CHECK(hipHostFree(ptr));
+    ptr = nullptr;
+    bytes = 0;
+    VO_HIP_CHECK(hipHostMalloc(&ptr, n ? n : 16, hipHostMallocDefault));
+    bytes = n;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(ptr);
+  }
+  ~HostBuf() {
+    if (ptr) (void)hipHostFree(ptr);
+  }
+};
+
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 // Runs `fn`, converting vo::Error into the status code (message already set).
