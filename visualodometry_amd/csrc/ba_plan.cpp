@@ -1,6 +1,8 @@
 // Host-side static planner for the BA Gauss-Newton step (see ba_plan.h).
 #include "ba_plan.h"
 
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -45,6 +47,22 @@ namespace {
 // disjoint, precomputed ranges, so the plan never depends on the thread count or timing.
 // Workers persist across plans (thread creation would cost more than a small phase); a
 // caller that finds the pool busy (another context planning) starts its own threads.
+// Tuning builds only (EXTRA=-DVO_PLAN_SPIN_US=n): a worker that finished a phase, and the
+// caller waiting for one, poll for up to n microseconds before sleeping on the condition
+// variable (consecutive phases are tens of microseconds apart).
+#ifndef VO_PLAN_SPIN_US
+#define VO_PLAN_SPIN_US 0
+#endif
+constexpr int kPlanSpinUs = VO_PLAN_SPIN_US;
+
+template <class Pred>
+void spin_until(Pred&& done) {
+  if (kPlanSpinUs <= 0) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!done() && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(kPlanSpinUs)) {
+  }
+}
+
 class PlanPool {
  public:
   static PlanPool& get() {
@@ -79,6 +97,7 @@ class PlanPool {
     }
     cv_.notify_all();
     fn(0);
+    spin_until([&] { return pending_.load(std::memory_order_acquire) == 0; });
     std::unique_lock<std::mutex> lk(mu_);
     done_.wait(lk, [&] { return pending_ == 0; });
     job_ = nullptr;
@@ -101,6 +120,7 @@ class PlanPool {
     long seen = 0;
     for (;;) {
       std::function<void(int)>* job;
+      spin_until([&] { return gen_.load(std::memory_order_acquire) != seen; });
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
@@ -119,8 +139,9 @@ class PlanPool {
   std::mutex use_, mu_;
   std::condition_variable cv_, done_;
   std::function<void(int)>* job_ = nullptr;
-  int active_ = 0, pending_ = 0;
-  long gen_ = 0;
+  int active_ = 0;
+  std::atomic<int> pending_{0};  // written under mu_; atomic for the optional spin
+  std::atomic<long> gen_{0};
   bool stop_ = false;
 };
 
