@@ -1241,6 +1241,12 @@ std::atomic<uint64_t> g_ba_sessions{0};  // session ids, unique in the process
 class BAEngine {
  public:
   explicit BAEngine(vo_ctx* ctx) : ctx_(ctx) {}
+  ~BAEngine() {
+    if (h_state_ev_) {
+      (void)hipEventSynchronize(h_state_ev_);
+      (void)hipEventDestroy(h_state_ev_);
+    }
+  }
 
   // Returns the new session id.  Every argument and plan check completes before any
   // collective: with a communicator, all ranks then agree (min all-reduce of [ok, F, -F])
@@ -1388,8 +1394,9 @@ class BAEngine {
       set_solve_lds<false>(l);
     }
     PLAN_T("setup: attrs");
-    VO_HIP_CHECK(hipStreamSynchronize(st));
-    PLAN_T("setup: sync");
+    // no sync: everything above is stream-ordered before the first iteration, pageable
+    // sources are staged when their copy is issued, and the page-locked chunk images are
+    // only rewritten after the sync at the top of the next setup
     have_problem_ = true;
     have_state_ = false;
     pending_ = false;
@@ -1412,6 +1419,8 @@ class BAEngine {
     hipStream_t st = ctx_->stream;
     // points gathered into internal order in the page-locked staging buffer, poses behind them
     const size_t np = 3ull * P.n_points;
+    if (h_state_busy_) VO_HIP_CHECK(hipEventSynchronize(h_state_ev_));  // previous set_state's DMA
+    h_state_busy_ = false;
     h_state_.reserve((np + 12ull * P.n_poses) * 8);
     double* pts = h_state_.as<double>();
     for (int q = 0; q < P.n_points; ++q)
@@ -1419,8 +1428,11 @@ class BAEngine {
     std::memcpy(pts + np, poses, P.n_poses * 96ull);
     VO_HIP_CHECK(hipMemcpyAsync(d_pose_[0].ptr, pts + np, P.n_poses * 96ull, hipMemcpyHostToDevice, st));
     if (P.n_points) VO_HIP_CHECK(hipMemcpyAsync(d_points_.ptr, pts, np * 8, hipMemcpyHostToDevice, st));
+    // not synchronised here: the next writer of the staging buffer waits for this event
+    if (!h_state_ev_) VO_HIP_CHECK(hipEventCreateWithFlags(&h_state_ev_, hipEventDisableTiming));
+    VO_HIP_CHECK(hipEventRecord(h_state_ev_, st));
+    h_state_busy_ = true;
     VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
-    VO_HIP_CHECK(hipStreamSynchronize(st));
     cur_ = 0;
     pending_ = false;
     have_state_ = true;
@@ -1432,6 +1444,8 @@ class BAEngine {
     const BAPlan& P = plan_;
     hipStream_t st = ctx_->stream;
     const size_t np = 3ull * P.n_points;
+    if (h_state_busy_) VO_HIP_CHECK(hipEventSynchronize(h_state_ev_));  // before reserve() may free it
+    h_state_busy_ = false;
     h_state_.reserve((np + 12ull * P.n_poses) * 8);
     double* pts = h_state_.as<double>();
     VO_HIP_CHECK(hipMemcpyAsync(pts + np, d_pose_[cur_].ptr, P.n_poses * 96ull, hipMemcpyDeviceToHost, st));
@@ -1762,6 +1776,8 @@ class BAEngine {
   long cost_off_ = 0;
   DevBuf d_solve_tab_;
   HostBuf h_state_;  // page-locked staging of set_state / get_state
+  hipEvent_t h_state_ev_ = nullptr;  // set_state's upload from h_state_ done
+  bool h_state_busy_ = false;
   DevBuf d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;  // K1's plan (the chunk images hold every list)
   DevBuf d_prof_src_ptr_, d_prof_diag_, d_prof_row_, d_camb_ptr_, d_stamps_, d_stamps3_;
   static constexpr bool stamps_on_ = kBaStamps;
