@@ -334,11 +334,7 @@ int vo_comm_unique_id(char out[128]);
  * all-reduces the partial reduced camera system (S, b, cost) before the
  * redundant dense pose solve, so all ranks hold identical poses. */
 int vo_comm_init(vo_ctx* ctx, int nranks, int rank, const char id[128]);
-/* Test stand-in for vo_comm_init: nranks contexts of ONE process (any devices, one host
- * thread each) join the in-process group named by the 128-byte id; all-reduces go
- * through host memory in rank order.  Exercises the sharded path where RCCL cannot
- * (RCCL refuses two ranks on one device).  Not a transport for production. */
-int vo_comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128]);
+/* (The test-only loopback communicator is declared in vo_hip_testing.h.) */
 
 #ifdef __cplusplus
 }

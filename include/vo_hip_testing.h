@@ -1,0 +1,21 @@
+/* Test-only entry points of libvo_hip.so.  Not part of the product surface (vo_hip.h):
+ * nothing in src/main.py's path calls them; the parity tests (tests/) do. */
+#ifndef VO_HIP_TESTING_H
+#define VO_HIP_TESTING_H
+
+#include "vo_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Test stand-in for vo_comm_init: nranks contexts of ONE process (any devices, one host
+ * thread each) join the in-process group named by the 128-byte id; all-reduces go
+ * through host memory in rank order.  Exercises the sharded path where RCCL cannot
+ * (RCCL refuses two ranks on one device).  Not a transport for production. */
+int vo_comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VO_HIP_TESTING_H */

@@ -1,4 +1,4 @@
-"""The C-ABI library builds, loads and exports every symbol include/vo_hip.h declares (no GPU)."""
+"""The C-ABI library builds, loads and exports every symbol include/*.h declares (no GPU)."""
 
 import re
 
@@ -8,8 +8,9 @@ import pytest
 from visualodometry_amd import _lib
 
 
-def header_functions():
-    text = _lib.HEADER.read_text()
+def header_functions(path=None):
+    paths = [path] if path else [_lib.HEADER, _lib.TEST_HEADER]
+    text = "".join(p.read_text() for p in paths)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(vo_[a-z0-9_]+)\s*\(", text)))
 
@@ -27,6 +28,12 @@ def test_every_declared_function_is_exported_and_bound():
         assert hasattr(lib, n), f"{n} not exported by libvo_hip.so"
         assert n in _lib.SIGNATURES, f"{n} has no ctypes signature in _lib.py"
     assert set(_lib.SIGNATURES) <= set(names)
+
+
+def test_product_header_has_no_test_entry_points():
+    """The loopback communicator is test-only: declared in vo_hip_testing.h, not vo_hip.h."""
+    assert "vo_comm_init_loopback" not in header_functions(_lib.HEADER)
+    assert header_functions(_lib.TEST_HEADER) == ["vo_comm_init_loopback"]
 
 
 def test_no_device_fails_loudly(monkeypatch):

@@ -58,7 +58,8 @@ def _sharded(p, nranks, iters, lam, group):
     return out
 
 
-@pytest.mark.parametrize("cfg,nranks", [("cfg2", 2), ("cfg2", 3), ("cfg3", 2), ("cfg4", 2), ("cfg4", 4)])
+@pytest.mark.parametrize("cfg,nranks", [("cfg2", 2), ("cfg2", 3), ("cfg3", 2), ("cfg3", 4), ("cfg3", 8),
+                                        ("cfg4", 2), ("cfg4", 4), ("cfg4", 8)])
 def test_sharded_matches_unsharded(cfg, nranks):
     p = make_ba_config(cfg)
     iters, lam = (3 if cfg == "cfg4" else 5), 1.0  # cfg4 = BASELINE config 4, 100 x 200k

@@ -155,7 +155,8 @@ def test_items_values_keys_vectorised_equal_dict():
     store.prune_below(5000)
     for pid in range(5000):
         del ref[pid]
-    assert store.keys() == list(ref.keys())
+    assert list(store.keys()) == list(ref.keys())
+    assert 5000 in store.keys() and 4999 not in store.keys()  # KeysView containment (__contains__)
     for (k, v), (rk, rv) in zip(store.items(), ref.items()):
         assert k == rk and np.array_equal(v, rv) and v.dtype == np.float32
     assert all(np.array_equal(a, b) for a, b in zip(store.values(), ref.values()))

@@ -15,6 +15,8 @@ from pathlib import Path
 # VO_LIB_PATH selects an alternative build of the same library (tuning experiments)
 LIB_PATH = Path(os.environ.get("VO_LIB_PATH") or Path(__file__).resolve().parent / "lib" / "libvo_hip.so")
 HEADER = Path(__file__).resolve().parents[1] / "include" / "vo_hip.h"
+# test-only entry points (the loopback communicator), outside the product header
+TEST_HEADER = HEADER.with_name("vo_hip_testing.h")
 
 VO_OK = 0
 VO_ERR_ARG = -1

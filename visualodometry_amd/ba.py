@@ -65,10 +65,22 @@ def rt_to_poses(rt: np.ndarray) -> np.ndarray:
     return T
 
 
+def _as_index32(obs_pt) -> np.ndarray:
+    """obs_pt as contiguous int32, checked in its own (wider) type first: an int64 index of
+    2^31 or more, or a large negative one, must not wrap into [0, n_points)."""
+    a = np.asarray(obs_pt).reshape(-1)
+    if a.dtype != np.int32 and a.size:
+        if not np.issubdtype(a.dtype, np.integer):
+            raise ValueError("obs_pt must be integer")
+        if int(a.min()) < 0 or int(a.max()) > np.iinfo(np.int32).max:
+            raise ValueError("obs_pt out of range")
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
 def csr_from_obs_pt(n_points: int, obs_pt: np.ndarray):
     """Stable grouping of observations by landmark -> (order, point_ptr)
     (``vo_ba_group_by_point``: one counting sort on the host)."""
-    obs_pt = np.ascontiguousarray(obs_pt, dtype=np.int32).reshape(-1)
+    obs_pt = _as_index32(obs_pt)
     order = np.empty(obs_pt.size, dtype=np.int32)
     ptr_ = np.empty(int(n_points) + 1, dtype=np.int32)
     rc = _lib.load().vo_ba_group_by_point(int(n_points), obs_pt.size, ptr(obs_pt, C.c_int32),
@@ -83,7 +95,7 @@ def group_window(n_points: int, window: "BAWindow"):
     Windows built landmark by landmark (dropin/hooks.py ``KeyframeWindow.build``) are
     already grouped: their arrays pass through unchanged; others are reordered by
     ``csr_from_obs_pt``."""
-    obs_pt = np.ascontiguousarray(window.obs_pt, dtype=np.int32).reshape(-1)
+    obs_pt = _as_index32(window.obs_pt)
     obs_cam = np.asarray(window.obs_cam)
     obs_uv = np.asarray(window.obs_uv, dtype=np.float32).reshape(-1, 2)
     point_ptr = np.empty(int(n_points) + 1, dtype=np.int32)

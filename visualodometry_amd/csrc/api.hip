@@ -8,6 +8,7 @@
 #include "ba_band.h"
 #include "ba_plan.h"
 #include "vo_ctx.h"
+#include "../../include/vo_hip_testing.h"
 
 namespace vo {
 
@@ -709,6 +710,7 @@ int vo_comm_init(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
   });
 }
 
+// test-only (include/vo_hip_testing.h)
 int vo_comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
   return guarded([&] {
     vo::bind(ctx);

@@ -4,6 +4,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -69,25 +70,36 @@ class PlanPool {
     static PlanPool pool;
     return pool;
   }
+  // Exceptions (bad_alloc in a phase) never escape a thread: each call of fn is caught,
+  // the first exception is kept, every thread finishes the phase, then the caller rethrows
+  // it (guarded() maps it to an error code).
   template <class Fn>
   void run(int n, Fn&& fn) {
+    std::exception_ptr first;
+    std::mutex emu;
+    auto safe = [&](int t) {
+      try {
+        fn(t);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(emu);
+        if (!first) first = std::current_exception();
+      }
+    };
     // a forked child inherits the pool object but not its threads: it plans on its own
-    if (getpid() != owner_) {
+    std::unique_lock<std::mutex> busy(use_, std::defer_lock);
+    if (getpid() != owner_ || !busy.try_lock() || n - 1 > (int)workers_.size()) {
       std::vector<std::thread> pool;
-      for (int t = 1; t < n; ++t) pool.emplace_back([&fn, t] { fn(t); });
-      fn(0);
+      try {
+        for (int t = 1; t < n; ++t) pool.emplace_back([&safe, t] { safe(t); });
+      } catch (...) {  // thread creation failed: the rest of the phase on this thread
+        for (int t = (int)pool.size() + 1; t < n; ++t) safe(t);
+      }
+      safe(0);
       for (auto& th : pool) th.join();
+      if (first) std::rethrow_exception(first);
       return;
     }
-    std::unique_lock<std::mutex> busy(use_, std::try_to_lock);
-    if (!busy.owns_lock() || n - 1 > (int)workers_.size()) {
-      std::vector<std::thread> pool;
-      for (int t = 1; t < n; ++t) pool.emplace_back([&fn, t] { fn(t); });
-      fn(0);
-      for (auto& th : pool) th.join();
-      return;
-    }
-    std::function<void(int)> job = [&fn](int t) { fn(t); };
+    std::function<void(int)> job = [&safe](int t) { safe(t); };
     {
       std::lock_guard<std::mutex> lk(mu_);
       job_ = &job;
@@ -96,11 +108,14 @@ class PlanPool {
       ++gen_;
     }
     cv_.notify_all();
-    fn(0);
+    safe(0);
     spin_until([&] { return pending_.load(std::memory_order_acquire) == 0; });
-    std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [&] { return pending_ == 0; });
-    job_ = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      done_.wait(lk, [&] { return pending_ == 0; });
+      job_ = nullptr;
+    }
+    if (first) std::rethrow_exception(first);
   }
   ~PlanPool() {
     {

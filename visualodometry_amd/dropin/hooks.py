@@ -268,10 +268,10 @@ def _wrap_match_frames(orig):
 
     def match_frames(self, feats0, feats1):
         if getattr(self.conf, "extractor_type", None) == "sift" and getattr(self.conf, "match_on_gpu", True):
-            if not getattr(self, "_vo_amd_hinted", False):  # SIFT integers: the int8 path only
-                matcher.set_descriptor_kind(matcher.DESC_SIFT)
-                self._vo_amd_hinted = True
-            return matcher.match_knn2_ratio(feats0["descriptors"], feats1["descriptors"])
+            # SIFT integers: the int8 path only, hinted for this call (the context's own hint,
+            # which other users of the context may rely on, is restored afterwards)
+            return matcher.match_knn2_ratio(feats0["descriptors"], feats1["descriptors"],
+                                            kind=matcher.DESC_SIFT)
         return orig(self, feats0, feats1)
 
     match_frames._vo_amd_wrapped = orig

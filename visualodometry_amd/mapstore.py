@@ -84,10 +84,8 @@ class MapStore(MutableMapping):
         return self._n
 
     # one vectorised pass instead of MutableMapping's per-key __getitem__ (the reference's
-    # per-frame ``for pid, pt in self.map_points.items()``, vo.py:349, over up to 20k points)
-    def keys(self):
-        return self.arrays()[0].tolist()
-
+    # per-frame ``for pid, pt in self.map_points.items()``, vo.py:349, over up to 20k points);
+    # keys() stays Mapping's KeysView (O(1) containment through __contains__, set operations)
     def values(self):
         return list(self.arrays()[1])
 

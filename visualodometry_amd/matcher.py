@@ -31,8 +31,12 @@ def _as_des(d) -> np.ndarray:
     return np.ascontiguousarray(d, dtype=np.float32)
 
 
-def match_knn2_ratio(des0, des1, ratio: float = RATIO_THRESH, ctx: _lib.Context | None = None) -> np.ndarray:
-    """Ratio-test matches as an ``int64`` array ``(M, 2)`` of (query, train), ascending query."""
+def match_knn2_ratio(des0, des1, ratio: float = RATIO_THRESH, ctx: _lib.Context | None = None,
+                     kind: int | None = None) -> np.ndarray:
+    """Ratio-test matches as an ``int64`` array ``(M, 2)`` of (query, train), ascending query.
+
+    ``kind`` (``DESC_SIFT`` / ``DESC_FLOAT``) is a hint for this call only: the context's own
+    hint (:func:`set_descriptor_kind`) is restored afterwards.  Results never depend on it."""
     a, b = _as_des(des0), _as_des(des1)
     if a.shape[0] == 0 or b.shape[0] == 0:  # frontend.py:97-98
         return np.empty((0, 2), dtype=np.int64)
@@ -41,13 +45,21 @@ def match_knn2_ratio(des0, des1, ratio: float = RATIO_THRESH, ctx: _lib.Context 
     ctx = ctx or _lib.context()
     out = np.empty((a.shape[0], 2), dtype=np.int32)
     cnt = np.zeros(1, dtype=np.int32)
-    check(
-        ctx.lib.vo_match_knn2_ratio(
-            ctx.handle, ptr(a, C.c_float), a.shape[0], ptr(b, C.c_float), b.shape[0], a.shape[1],
-            float(ratio), ptr(out, C.c_int32), ptr(cnt, C.c_int32),
-        ),
-        "vo_match_knn2_ratio",
-    )
+    prior = getattr(ctx, "desc_kind", DESC_AUTO)
+    scoped = kind is not None and kind != prior
+    if scoped:
+        check(ctx.lib.vo_match_hint(ctx.handle, int(kind)), "vo_match_hint")
+    try:
+        check(
+            ctx.lib.vo_match_knn2_ratio(
+                ctx.handle, ptr(a, C.c_float), a.shape[0], ptr(b, C.c_float), b.shape[0], a.shape[1],
+                float(ratio), ptr(out, C.c_int32), ptr(cnt, C.c_int32),
+            ),
+            "vo_match_knn2_ratio",
+        )
+    finally:
+        if scoped:
+            check(ctx.lib.vo_match_hint(ctx.handle, int(prior)), "vo_match_hint")
     return out[: int(cnt[0])].astype(np.int64)
 
 
@@ -108,6 +120,7 @@ def set_descriptor_kind(kind: int, ctx: _lib.Context | None = None) -> None:
     for the reference's SIFT extractor); ``DESC_AUTO`` launches both paths' kernels."""
     ctx = ctx or _lib.context()
     check(ctx.lib.vo_match_hint(ctx.handle, int(kind)), "vo_match_hint")
+    ctx.desc_kind = int(kind)  # restored by match_knn2_ratio after a per-call hint
 
 
 def synchronize(ctx: _lib.Context | None = None) -> None:
