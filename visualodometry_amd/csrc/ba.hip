@@ -208,7 +208,7 @@ __device__ __forceinline__ void lin_obs(LinShared& S, const LinArgs& A, const do
     const double x = T[0] * X0 + T[1] * X1 + T[2] * X2 + T[9];
     const double y = T[3] * X0 + T[4] * X1 + T[5] * X2 + T[10];
     const double z = T[6] * X0 + T[7] * X1 + T[8] * X2 + T[11];
-    const double iz = 1.0 / z;
+    const double iz = rcp_nr(z);
     const float2 m = reinterpret_cast<const float2*>(S.img.uv)[o];
     const double r0 = A.fx * x * iz + A.cx - (double)m.x;
     const double r1 = A.fy * y * iz + A.cy - (double)m.y;
@@ -259,18 +259,19 @@ __device__ __forceinline__ bool point_block(const LinShared& S, const LinArgs& A
     }
   }
   v00 += A.lambda; v11 += A.lambda; v22 += A.lambda;
+  // pivots by v_rsq_f64 + one Newton step (~1e-14 relative) instead of IEEE sqrt and five
+  // divisions: the same pivot tests on the same values, no division on the chain
   const double eps = kPivotRelEps * (v00 + v11 + v22);
   bool ok = v00 > eps;
-  const double l00 = sqrt(ok ? v00 : 1.0);
-  const double l10 = v01 / l00, l20 = v02 / l00;
+  const double i00 = rsq_nr(ok ? v00 : 1.0);
+  const double l10 = v01 * i00, l20 = v02 * i00;
   const double d1 = v11 - l10 * l10;
   ok = ok && d1 > eps;
-  const double l11 = sqrt(ok ? d1 : 1.0);
-  const double l21 = (v12 - l20 * l10) / l11;
+  const double i11 = rsq_nr(ok ? d1 : 1.0);
+  const double l21 = (v12 - l20 * l10) * i11;
   const double d2 = v22 - l20 * l20 - l21 * l21;
   ok = ok && d2 > eps;
-  const double l22 = sqrt(ok ? d2 : 1.0);
-  const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+  const double i22 = rsq_nr(ok ? d2 : 1.0);
   l[0] = i00; l[1] = l10; l[2] = i11; l[3] = l20; l[4] = l21; l[5] = i22;
   h[0] = g0 * i00;
   h[1] = (g1 - l10 * h[0]) * i11;
@@ -382,7 +383,7 @@ __device__ __forceinline__ void chunk_backsub(LinShared& S, const LinArgs& A, in
     const double x = T[0] * X0 + T[1] * X1 + T[2] * X2 + T[9];
     const double y = T[3] * X0 + T[4] * X1 + T[5] * X2 + T[10];
     const double z = T[6] * X0 + T[7] * X1 + T[8] * X2 + T[11];
-    const double iz = 1.0 / z;
+    const double iz = rcp_nr(z);
     const float2 m = reinterpret_cast<const float2*>(S.img.uv)[o];
     double r0 = A.fx * x * iz + A.cx - (double)m.x;
     double r1 = A.fy * y * iz + A.cy - (double)m.y;

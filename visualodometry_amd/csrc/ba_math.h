@@ -111,6 +111,19 @@ __device__ __forceinline__ void bwd6(const double (&L)[21], const double (&r)[6]
   }
 }
 
+// 1/sqrt(d) and 1/z without the IEEE sqrt / division sequences: v_rsq_f64 (v_rcp_f64) is
+// good to ~2^-23 relative; one Newton step for rsq (~1e-14, as chol6) and two for rcp
+// (~1 ulp) -- a short dependent chain on the kernels' latency-bound paths.
+__device__ __forceinline__ double rsq_nr(double d) {
+  const double q = __builtin_amdgcn_rsq(d);
+  return __builtin_fma(0.5 * q, __builtin_fma(-(d * q), q, 1.0), q);
+}
+__device__ __forceinline__ double rcp_nr(double z) {
+  double r = __builtin_amdgcn_rcp(z);
+  r = __builtin_fma(r, __builtin_fma(-z, r, 1.0), r);
+  return __builtin_fma(r, __builtin_fma(-z, r, 1.0), r);
+}
+
 // v[lane] for a register array without a runtime index (a runtime index would
 // put the whole array in scratch memory).
 template <int N>
