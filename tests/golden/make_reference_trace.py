@@ -26,6 +26,16 @@ path on the GPU box (the reference itself never travels).
 
     python tests/golden/make_reference_trace.py            # both runs, compare, write the npz
     python tests/golden/make_reference_trace.py --check    # both runs, compare with the npz
+    python tests/golden/make_reference_trace.py --long     # the long drive (below)
+
+``--long`` drives the same three runs over a 1300-frame drive (``SCENE_LONG``), long enough
+for the BA hook's ``KeyframeWindow`` to reach its full 50 keyframes (``vo.py:252-288``,
+``_prune_map``'s 20 000 cap at ``vo.py:35-47`` binding), and writes
+``tests/golden/reference_trace_long.npz``: the three trajectories (reference, drop-in,
+drop-in with BA), the keyframe-window sizes of every BA call, and two windows with the C
+oracle's solutions (the last full-size window and a mid-size one).  ``tests/test_ate.py``
+computes the ATE of each trajectory on the drive's ground truth;
+``tests/test_gpu_reference_trace.py`` replays the two windows through the HIP path.
 """
 
 from __future__ import annotations
@@ -44,9 +54,13 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[2]
 REF_SRC = Path("/root/reference/src")
-OUT = ROOT / "tests" / "golden" / "reference_trace.npz"
-SCENE = dict(n_frames=60, n_landmarks=9000, seed=7, max_features=1400, n_distractors=80, noise_px=0.25, speed=1.2)
-MAX_TRI, MAX_PNP, MAX_WIN = 4, 6, 2  # calls kept in the fixture
+LONG = os.environ.get("VO_TRACE_LONG") == "1"
+OUT = ROOT / "tests" / "golden" / ("reference_trace_long.npz" if LONG else "reference_trace.npz")
+# the long drive keeps the short one's landmark density along a 5x longer corridor
+SCENE = (dict(n_frames=1300, n_landmarks=104000, seed=11, max_features=1400, n_distractors=80, noise_px=0.25,
+              speed=1.2) if LONG else
+         dict(n_frames=60, n_landmarks=9000, seed=7, max_features=1400, n_distractors=80, noise_px=0.25, speed=1.2))
+MAX_TRI, MAX_PNP, MAX_WIN = (0, 0, 2) if LONG else (4, 6, 2)  # calls kept in the fixture
 
 
 class _Any:
@@ -245,7 +259,7 @@ def run_dropin(out_path: str, ba: bool = False) -> None:
     from oracle import match_ref, triangulate_ref
     from visualodometry_amd import matcher, pnp, sift, triangulate
 
-    matcher.match_knn2_ratio = lambda d0, d1, ratio=0.75, ctx=None: match_ref.match_int(
+    matcher.match_knn2_ratio = lambda d0, d1, ratio=0.75, ctx=None, **kw: match_ref.match_int(
         matcher._as_des(d0), matcher._as_des(d1), ratio)
     triangulate.triangulate_points = lambda T1, T2, p1, p2, K, cfg, ctx=None: triangulate_ref.triangulate_points(
         T1, T2, p1, p2, K, cfg.min_depth, cfg.max_reproj_err)
@@ -308,10 +322,22 @@ def _save_run(path, rec, n_map, cfg) -> None:
             out[f"tri{i}_{k}"] = np.asarray(v)
     out["n_tri"] = np.int64(min(len(rec["tri"]), MAX_TRI))
     out["n_tri_calls"] = np.int64(len(rec["tri"]))
-    for i, t in enumerate(rec.get("win", [])[:MAX_WIN]):
+    wins = rec.get("win", [])
+    out["win_sizes"] = np.array([[t["poses"].shape[0], t["points"].shape[0], t["obs_uv"].shape[0]] for t in wins],
+                                np.int64).reshape(-1, 3)
+    if LONG and wins:
+        # the last window of the largest size, and the window closest to half that size
+        n = out["win_sizes"][:, 0]
+        full = int(np.flatnonzero(n == n.max())[-1])
+        mid = int(np.argmin(np.abs(n - n.max() / 2)))
+        wins = [wins[full], wins[mid]]
+        out["win_index"] = np.array([full, mid], np.int64)
+    if LONG:
+        out["matches"] = np.zeros((0, 2), np.int16)  # the long fixture keeps trajectories and windows only
+    for i, t in enumerate(wins[:MAX_WIN]):
         for k, v in t.items():
             out[f"win{i}_{k}"] = np.asarray(v)
-    out["n_win"] = np.int64(min(len(rec.get("win", [])), MAX_WIN))
+    out["n_win"] = np.int64(min(len(wins), MAX_WIN))
     out["n_win_calls"] = np.int64(len(rec.get("win", [])))
     for i, t in enumerate(rec["pnp"][:MAX_PNP]):
         for k, v in t.items():
@@ -324,11 +350,15 @@ def _save_run(path, rec, n_map, cfg) -> None:
 
 
 def _run(mode: str, path: str) -> None:
-    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", PYTHONPATH=str(ROOT))
-    r = subprocess.run([sys.executable, __file__, f"--{mode}", path], env=env, capture_output=True, text=True,
-                       timeout=900)
-    if r.returncode != 0:
-        raise SystemExit(f"{mode} run failed:\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}")
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", PYTHONPATH=str(ROOT), VO_TRACE_LONG="1" if LONG else "0")
+    return subprocess.Popen([sys.executable, __file__, f"--{mode}", path], env=env, stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True)
+
+
+def _wait(mode: str, proc) -> None:
+    out, err = proc.communicate(timeout=3600)
+    if proc.returncode != 0:
+        raise SystemExit(f"{mode} run failed:\n{out[-3000:]}\n{err[-3000:]}")
 
 
 def compare(a: dict, b: dict) -> list[str]:
@@ -341,6 +371,11 @@ def compare(a: dict, b: dict) -> list[str]:
 
 
 def main() -> None:
+    if "--long" in sys.argv and not LONG:  # re-read the module constants in long mode
+        os.environ["VO_TRACE_LONG"] = "1"
+        sys.argv.remove("--long")
+        r = subprocess.run([sys.executable, __file__] + sys.argv[1:], env=dict(os.environ))
+        raise SystemExit(r.returncode)
     if not REF_SRC.exists():
         raise SystemExit(f"{REF_SRC} is absent: the fixtures are generated in the build container")
     if len(sys.argv) > 2 and sys.argv[1] in ("--reference", "--dropin", "--dropin_ba"):
@@ -353,9 +388,9 @@ def main() -> None:
     check = "--check" in sys.argv
     with tempfile.TemporaryDirectory() as td:
         pr, pd, pb = (os.path.join(td, f"{n}.npz") for n in ("ref", "dropin", "dropin_ba"))
-        _run("reference", pr)
-        _run("dropin", pd)
-        _run("dropin_ba", pb)
+        runs = [(m, _run(m, p)) for m, p in (("reference", pr), ("dropin", pd), ("dropin_ba", pb))]  # in parallel
+        for m, proc in runs:
+            _wait(m, proc)
         a, b, c = dict(np.load(pr)), dict(np.load(pd)), dict(np.load(pb))
         diff = compare(a, b)
         ref_quirk = int((a["match_ndim"] == 1).sum())
@@ -369,6 +404,8 @@ def main() -> None:
         for k, v in c.items():
             if k.startswith("win") or k in ("n_win", "n_win_calls"):
                 a[k] = v
+        if LONG:
+            print("BA window sizes (poses, landmarks, observations):", c["win_sizes"].tolist())
         a["T_wc_ba"] = c["T_wc"]
         a["T_wc_dropin"] = b["T_wc"]
         if check:

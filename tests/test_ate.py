@@ -1,0 +1,87 @@
+"""The ``north_star`` trajectory criterion on the data that exists here (CPU).
+
+``north_star`` asks for "KITTI-05 ATE within 1 % of the CPU reference".  KITTI is absent, so
+the criterion runs on the synthetic drives of ``tests/vo_trace_scene.py`` that
+``tests/golden/make_reference_trace.py`` drove through the reference's own, unmodified
+``VisualOdometry`` (the short 60-frame drive and the 1300-frame one whose BA windows reach the
+hook's 50-keyframe cap).  Each fixture holds three trajectories of the same drive:
+
+* ``T_wc``: the reference's ``VisualOdometry`` exactly as written;
+* ``T_wc_dropin``: the reference's ``src/main.py`` unchanged through the drop-in hooks;
+* ``T_wc_ba``: the same with the sliding-window BA hook on (``VO_AMD_BA=1``), its windows
+  solved by the C oracle -- the HIP ``SlidingWindowBA`` reproduces those solutions to 1e-5
+  on the GPU (``tests/test_gpu_reference_trace.py``).
+
+ATE is computed as the reference's evaluation would see it: camera positions ``T_wc[:3, 3]``
+on the ground-truth layout the reference loads (``dataset_loader.py:60``:
+``poses[:, [3, 11]]``, the x and z translation), after a similarity alignment (monocular VO
+has no metric scale; ``mapstore.ate``).
+"""
+
+import json
+
+import numpy as np
+import pytest
+
+from oracle import cref
+from tests.conftest import GOLDEN
+from tests.vo_trace_scene import TraceScene
+from visualodometry_amd import ba as ba_mod
+from visualodometry_amd.mapstore import ate
+
+FIXTURES = ["reference_trace.npz", "reference_trace_long.npz"]
+
+
+@pytest.fixture(scope="module", params=FIXTURES)
+def drive(request):
+    g = dict(np.load(GOLDEN / request.param))
+    scene = TraceScene(**json.loads(str(g["scene"])))
+    gt = np.stack([T[:3, 3] for T in scene.T_wc])[:, [0, 2]]  # poses[:, [3, 11]]
+    return request.param, g, gt
+
+
+def _ate(g, key, gt):
+    est = g[key][:, :3, 3][:, [0, 2]]
+    assert est.shape == gt.shape
+    return ate(est, gt)["rmse"]
+
+
+def test_dropin_ate_equals_reference(drive):
+    _, g, gt = drive
+    np.testing.assert_array_equal(g["T_wc_dropin"], g["T_wc"])
+    assert _ate(g, "T_wc_dropin", gt) == _ate(g, "T_wc", gt)
+
+
+def test_ba_ate_within_one_percent_of_reference(drive):
+    """north_star: ATE within 1 % of the reference's (or better).  The BA hook lowers it."""
+    name, g, gt = drive
+    ref, with_ba = _ate(g, "T_wc", gt), _ate(g, "T_wc_ba", gt)
+    print(f"{name}: ATE rmse reference {ref:.4f}, drop-in with BA {with_ba:.4f} ({with_ba / ref:.3f}x)")
+    assert with_ba <= 1.01 * ref
+
+
+def test_long_drive_reaches_the_full_window():
+    """The BA hook's window reaches its 50 keyframes (``ba_window``) and the map its 20 000
+    point cap (``vo.py:35-47``) inside the reference's own loop; the fixture's first window is
+    the last full one."""
+    g = dict(np.load(GOLDEN / "reference_trace_long.npz"))
+    sizes = g["win_sizes"]
+    assert sizes[:, 0].max() == 50
+    assert sizes[:, 1].max() <= 20000 and sizes[:, 1].max() >= 19000
+    full, mid = (int(i) for i in g["win_index"])
+    assert g["win0_poses"].shape[0] == 50 and sizes[full, 0] == 50
+    assert 0 < g["win1_poses"].shape[0] < 50 and tuple(sizes[mid]) == (
+        g["win1_poses"].shape[0], g["win1_points"].shape[0], g["win1_obs_uv"].shape[0])
+
+
+def test_long_drive_mid_window_matches_c_oracle():
+    """The recorded mid-size window solution is the C oracle's (fixture integrity)."""
+    g = dict(np.load(GOLDEN / "reference_trace_long.npz"))
+    w = {k[len("win1_"):]: v for k, v in g.items() if k.startswith("win1_")}
+    order, ptr = ba_mod.csr_from_obs_pt(w["points"].shape[0], w["obs_pt"])
+    R = cref.BAProblemRef(g["K"], ptr, w["obs_cam"][order], w["obs_uv"][order], w["poses"].shape[0],
+                          int(w["n_fixed"]), float(w["lam"]))
+    _, P, X, costs = R.solve(w["poses"], w["points"], int(w["iters"]))
+    np.testing.assert_array_equal(costs, w["costs"])
+    np.testing.assert_array_equal(P, w["P"])
+    np.testing.assert_array_equal(X, w["X"])

@@ -100,3 +100,25 @@ def test_keyframe_window_ba_replay(trace):
         dP, dPr = res.poses_cw - w["poses"], w["P"] - w["poses"]
         assert np.abs(dP - dPr).max() <= REL * max(np.abs(dPr).max(), 1e-12)
         assert np.abs(res.points - w["X"]).max() <= REL * np.abs(w["X"]).max()
+
+
+@pytest.fixture(scope="module")
+def long_trace():
+    return dict(np.load(GOLDEN / "reference_trace_long.npz"))
+
+
+@pytest.mark.parametrize("i", [0, 1], ids=["full_window", "mid_window"])
+def test_long_drive_window_ba_replay(long_trace, i):
+    """The north-star window size assembled by the reference's own classes: the 1300-frame
+    drive's last 50-keyframe window (``_create_keyframe``, ``vo.py:252-288``, with
+    ``_prune_map``'s cap, ``vo.py:35-47``) and a mid-size one, replayed through the HIP
+    ``SlidingWindowBA`` against the C oracle's solution recorded with them."""
+    g = long_trace
+    w = _call(g, "win", i)
+    res = SlidingWindowBA(g["K"], iters=int(w["iters"]), lam=float(w["lam"])).optimize(
+        BAWindow(w["poses"], w["points"], w["obs_uv"], w["obs_cam"], w["obs_pt"], int(w["n_fixed"])))
+    assert res.status == "ok", res.message
+    np.testing.assert_allclose(res.cost_per_iter, w["costs"], rtol=REL)
+    dP, dPr = res.poses_cw - w["poses"], w["P"] - w["poses"]
+    assert np.abs(dP - dPr).max() <= REL * max(np.abs(dPr).max(), 1e-12)
+    assert np.abs(res.points - w["X"]).max() <= REL * np.abs(w["X"]).max()
