@@ -214,3 +214,25 @@ def test_duplicate_train_rows_across_lanes_tiles_and_splits(ctx):
     d1 = base[rng.permutation(np.repeat(np.arange(500), 8))]
     d0 = np.concatenate([base[:300], rng.integers(0, 256, (700, 128)).astype(np.float32)])
     _check_knn2(d0, d1, ctx)
+
+
+def test_float_hint_skips_int_pack_and_stays_exact(ctx):
+    """Under the float hint no int8 pack (and no integer check) runs: the bf16 shortlist + exact
+    re-rank must still reproduce the integer oracle on SIFT bytes (the fp32 chains of squared
+    byte differences are exact) and the fp32 oracle on floats, and a non-finite value must still
+    reach the exact sweep (fpack flags it) -- same outputs as without the hint."""
+    d0, d1 = sift_like_pair(2048, 2048, 21)
+    f0, f1 = superpoint_like_pair(1024, 1500, 22)
+    n0, n1 = f0.copy(), f1.copy()
+    n0[5, 7] = np.nan
+    n1[9, 3] = np.inf
+    auto = [matcher.match_knn2(n0, n1, ctx=ctx)]
+    matcher.set_descriptor_kind(matcher.DESC_FLOAT, ctx)
+    try:
+        _check_knn2(d0, d1, ctx)
+        _check_knn2(f0, f1, ctx, oracle="c")
+        hinted = matcher.match_knn2(n0, n1, ctx=ctx)
+    finally:
+        matcher.set_descriptor_kind(matcher.DESC_AUTO, ctx)
+    np.testing.assert_array_equal(hinted[0], auto[0][0])
+    np.testing.assert_array_equal(hinted[1].view(np.uint32), auto[0][1].view(np.uint32))

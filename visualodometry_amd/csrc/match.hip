@@ -635,9 +635,13 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
   a.n0_pad = n0_pad;
   a.n1_pad = n1_pad;
   a.split_w = w;
-  a.force_f32 = int_ok ? 0 : 1;
   // dim <= 256: the shortlist's A fragments fit in VGPRs; a SIFT hint leaves it unlaunched
-  // (float values then take the exact sweep)
+  // (float values then take the exact sweep).  A float hint skips the int8 pack and its
+  // integer check: the shortlist is exact for any finite values, SIFT integers included (their
+  // fp32 chains of <= 256 squared byte differences stay below 2^24, so F = the integer d^2 and
+  // the (sqrtf, j) keys order as the integer path's), and fpack flags non-finite values itself.
+  const bool float_hint = int_ok && ws.kind_hint == VO_DESC_FLOAT;
+  a.force_f32 = int_ok && !float_hint ? 0 : 1;
   a.short_ok = int_ok && ws.kind_hint != VO_DESC_SIFT ? 1 : 0;
   a.a_bstride = (long)n0 * dim;
   a.b_bstride = (long)n1 * dim;
@@ -655,7 +659,7 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
     VO_HIP_CHECK(hipGetLastError());
     return;
   }
-  if (int_ok) {
+  if (int_ok && !float_hint) {
     a.qa_bstride = (long)n0_pad * Dp;
     a.qb_bstride = (long)n1_pad * Dp;
     ws.q8.reserve((size_t)batch * (a.qa_bstride + a.qb_bstride));
@@ -679,15 +683,20 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
                        Dp, vec4, flag, ws.gen);
     ctx->prof.end(st);
   }
-  dim3 grid(row_wgs, nsplit, batch);
-  ctx->prof.begin(st, kKMatchI8);
-  switch (int_ok ? Dp / kKStep : 1) {
-    case 1: hipLaunchKernelGGL(match_kernel<1>, grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(match_kernel<2>, grid, dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(match_kernel<3>, grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL(match_kernel<4>, grid, dim3(256), 0, st, a); break;
-  }
-  ctx->prof.end(st);
+  auto sweep = [&]() {  // int8 sweep, or the exact fp32 sweep (float calls the shortlist cannot take)
+    dim3 grid(row_wgs, nsplit, batch);
+    ctx->prof.begin(st, kKMatchI8);
+    switch (int_ok ? Dp / kKStep : 1) {
+      case 1: hipLaunchKernelGGL(match_kernel<1>, grid, dim3(256), 0, st, a); break;
+      case 2: hipLaunchKernelGGL(match_kernel<2>, grid, dim3(256), 0, st, a); break;
+      case 3: hipLaunchKernelGGL(match_kernel<3>, grid, dim3(256), 0, st, a); break;
+      default: hipLaunchKernelGGL(match_kernel<4>, grid, dim3(256), 0, st, a); break;
+    }
+    ctx->prof.end(st);
+  };
+  // under the float hint fpack raises the non-finite flag, so the sweep that serves such
+  // calls is enqueued after it
+  if (!float_hint) sweep();
   if (a.short_ok) {  // float calls: bf16 MFMA shortlist + exact re-rank (match_bf16.hip)
     ShortArgs s{};
     s.da = d_des0;
@@ -704,6 +713,7 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
     s.b_bstride = a.b_bstride;
     s.flag = flag;
     s.gen = ws.gen;
+    s.forced = float_hint ? 1 : 0;
     s.ratio = ratio;
     s.best = d_best;
     s.idx2 = d_idx2;
@@ -724,6 +734,7 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
     s.mask = ws.cand.as<uint64_t>();
     short_launch(ctx, s, batch);
   }
+  if (float_hint) sweep();
   ctx->prof.begin(st, kKMatchMerge);
   hipLaunchKernelGGL(merge_kernel, dim3(row_wgs, batch), dim3(256), 0, st, a, nsplit);
   ctx->prof.end(st);

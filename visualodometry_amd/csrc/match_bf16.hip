@@ -41,7 +41,7 @@ constexpr float kShortC = 1.25f * (0.0078125f + 4e-5f);
 namespace {
 
 __device__ __forceinline__ bool short_active(const ShortArgs& p) {
-  return p.flag[0] == p.gen && p.flag[1] != p.gen;  // uniform
+  return (p.forced || p.flag[0] == p.gen) && p.flag[1] != p.gen;  // uniform
 }
 
 __device__ __forceinline__ float med3_f32(float a, float b, float c) {
@@ -54,7 +54,7 @@ __device__ __forceinline__ float med3_f32(float a, float b, float c) {
 // 16 threads per row, 8 consecutive elements per thread and step.  Rows past n are
 // written as zeros (train padding rows get |b'|^2 = +inf: never a candidate).
 __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int v4) {
-  if (!short_active(p)) return;
+  if (!p.forced && !short_active(p)) return;
   const bool is_b = (int)blockIdx.x >= a_wgs;
   const int b = blockIdx.y;
   const int n = is_b ? p.n1 : p.n0, n_pad = is_b ? p.n1_pad : p.n0_pad;
@@ -65,6 +65,7 @@ __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int 
   const float* src = (is_b ? p.db + b * p.b_bstride : p.da + b * p.a_bstride) + (long)row * p.dim;
   __bf16* dst = (is_b ? p.hb + (long)b * p.n1_pad * p.Dp : p.ha + (long)b * p.n0_pad * p.Dp) + (long)row * p.Dp;
   float q2 = 0.0f, x2 = 0.0f;
+  bool nonfinite = false;
   for (int e = sub * 8; in && e < p.Dp; e += 128) {
     v8bf h;
     float vv[8];
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int 
       h[u] = hv;
       q2 = fmaf(hf, hf, q2);
       x2 = fmaf(v, v, x2);
+      nonfinite |= !isfinite(v);  // padding is 0
     }
     *reinterpret_cast<v8bf*>(dst + e) = h;
   }
@@ -93,6 +95,8 @@ __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int 
     q2 += __shfl_xor(q2, m, 64);
     x2 += __shfl_xor(x2, m, 64);
   }
+  // float hint (no int8 pack): a non-finite value sends the call to the exact fp32 sweep
+  if (p.forced && __any(nonfinite) && (threadIdx.x & 63) == 0) const_cast<uint32_t*>(p.flag)[1] = p.gen;
   // norms rounded up by a few ulps: the bound only needs upper estimates
   const float r = sqrtf(x2) * 1.0001f;
   if (sub == 0 && in) {
@@ -327,6 +331,70 @@ __device__ __forceinline__ float chain_regs(const float* x, const float* y, int 
   return acc;
 }
 
+// Exact chains of the wave's (up to) 64 candidates, candidate c0 + lane, with the train rows
+// staged through LDS: a span of kRerankSpan elements of 8 rows per load instruction (8
+// lanes x 16 bytes per row: 8 x 128 contiguous bytes, not 64 rows' scattered 16 bytes), every
+// load of a span in flight, then each lane continues its own k-ordered fmaf chain from its
+// row's staged span and its query row (LDS).  Rows are padded by 16 bytes so the per-lane row
+// reads spread over the banks.  Returns lane's d2 (garbage for c0 + lane >= total).
+constexpr int kRerankSpan = 32;                 // floats per span (8 float4 per row)
+constexpr int kSpanF4 = kRerankSpan / 4, kSpanRows = 64 / kSpanF4;  // per load instruction
+constexpr int kRerankRowStr = kRerankSpan + 4;  // floats per staged row
+__device__ __forceinline__ float chain_staged(const float* __restrict__ B, const float* sq, const int* slist,
+                                              const int* scol, float* sbuf, int c0, int total, int dim) {
+  const int lane = threadIdx.x & 63;
+  const int c = min(c0 + lane, total - 1);
+  const float* x = sq + slist[c] * kQStr;
+  // loader role: instruction t stages rows kSpanRows t + lane / kSpanF4, float4 lane % kSpanF4
+  int jrow[kSpanF4];
+#pragma unroll
+  for (int t = 0; t < kSpanF4; ++t) jrow[t] = scol[min(c0 + kSpanRows * t + lane / kSpanF4, total - 1)];
+  // three spans in flight: span h's loads were issued two spans earlier
+  auto fetch = [&](int h, float4 (&v)[kSpanF4]) __attribute__((always_inline)) {
+    const int k4 = h / 4 + lane % kSpanF4;
+    const bool in = 4 * k4 < dim;
+#pragma unroll
+    for (int t = 0; t < kSpanF4; ++t)
+      v[t] = in ? reinterpret_cast<const float4*>(B + (long)jrow[t] * dim)[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto consume = [&](int h, const float4 (&v)[kSpanF4], float& acc) __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();  // every lane's reads of the previous span are done (in-order LDS)
+#pragma unroll
+    for (int t = 0; t < kSpanF4; ++t)
+      *reinterpret_cast<float4*>(sbuf + (kSpanRows * t + lane / kSpanF4) * kRerankRowStr + 4 * (lane % kSpanF4)) = v[t];
+    __builtin_amdgcn_wave_barrier();
+    const float* y = sbuf + lane * kRerankRowStr;
+    const int n = min(kRerankSpan, dim - h);
+    for (int k = 0; k < n; k += 4) {
+      const float4 xv = *reinterpret_cast<const float4*>(x + h + k);
+      const float4 yv = *reinterpret_cast<const float4*>(y + k);
+      float d = xv.x - yv.x;
+      acc = fmaf(d, d, acc);
+      d = xv.y - yv.y;
+      acc = fmaf(d, d, acc);
+      d = xv.z - yv.z;
+      acc = fmaf(d, d, acc);
+      d = xv.w - yv.w;
+      acc = fmaf(d, d, acc);
+    }
+  };
+  float acc = 0.0f;
+  float4 v0[kSpanF4], v1[kSpanF4], v2[kSpanF4];
+  fetch(0, v0);
+  if (kRerankSpan < dim) fetch(kRerankSpan, v1);
+  for (int h = 0; h < dim; h += 3 * kRerankSpan) {
+    if (h + 2 * kRerankSpan < dim) fetch(h + 2 * kRerankSpan, v2);
+    consume(h, v0, acc);
+    if (h + kRerankSpan >= dim) break;
+    if (h + 3 * kRerankSpan < dim) fetch(h + 3 * kRerankSpan, v0);
+    consume(h + kRerankSpan, v1, acc);
+    if (h + 2 * kRerankSpan >= dim) break;
+    if (h + 4 * kRerankSpan < dim) fetch(h + 4 * kRerankSpan, v1);
+    consume(h + 2 * kRerankSpan, v2, acc);
+  }
+  return acc;
+}
+
 __device__ __forceinline__ float chain_scalar(const float* x, const float* y, int dim) {
   float acc = 0.0f;
   for (int k = 0; k < dim; ++k) {
@@ -336,15 +404,22 @@ __device__ __forceinline__ float chain_scalar(const float* x, const float* y, in
   return acc;
 }
 
-__global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4) {
+// Grid: 8 * ceil(nR * batch / 8) workgroups, remapped XCD-major (workgroup L runs on XCD L mod
+// 8 by round-robin dispatch): XCD x takes the contiguous items [x per, (x + 1) per) of the
+// (pair, 16-row block) list, so the blocks of one frame pair share one L2 and its train rows
+// (2 MB at 2048 x 256) are fetched from the fabric once per XCD instead of by every XCD.
+__global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int nR, int nitems) {
   if (!short_active(p)) return;
-  const int b = blockIdx.y, R = blockIdx.x, tid = threadIdx.x;
+  const int per = (nitems + 7) / 8, L = blockIdx.x, item = (L & 7) * per + (L >> 3);
+  if (item >= nitems) return;
+  const int b = item / nR, R = item - b * nR, tid = threadIdx.x;
   if (R == 0 && tid == 0) p.bmax[b] = 0u;  // fsweep<2> is done with it
   __shared__ __attribute__((aligned(16))) float sq[16 * kQStr];
   __shared__ __attribute__((aligned(8))) int slist[kPool];  // row_local << 16 | column tile bit position (see below)
   __shared__ int scol[kPool];
   __shared__ uint64_t skey[kPool];
   __shared__ int sscan[256];
+  __shared__ __attribute__((aligned(16))) float sbuf[4][64 * kRerankRowStr];  // per-wave row staging
   const int row0 = 16 * R;
   if (v4) {  // the block's 16 query rows as float4s, every load in flight before the stores
     const int nv = p.dim / 4, nall = 16 * nv;  // dim <= 256: at most 4 per thread
@@ -399,11 +474,23 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4) {
   __syncthreads();
   uint64_t k1 = ~0ull, k2 = ~0ull;
   if (pooled) {
-    for (int c = tid; c < total; c += 256) {
-      const int rl = slist[c], j = scol[c];
-      const float* y = B + (long)j * p.dim;
-      const float d = v4 ? chain_regs(sq + rl * kQStr, y, p.dim) : chain_scalar(sq + rl * kQStr, y, p.dim);
-      skey[c] = key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)j);
+    if (v4) {
+      // wave w takes candidates 64 (w + 4 q) + lane (the loop bound is wave-uniform)
+      const int wv = tid >> 6;
+      for (int c0 = 64 * wv; c0 < total; c0 += 256) {
+#ifndef VO_RERANK_EXP
+#define VO_RERANK_EXP 0
+#endif
+        const float d = VO_RERANK_EXP == 1 ? 0.0f : chain_staged(B, sq, slist, scol, sbuf[wv], c0, total, p.dim);
+        const int c = c0 + (tid & 63);
+        if (c < total) skey[c] = key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)scol[c]);
+      }
+    } else {
+      for (int c = tid; c < total; c += 256) {
+        const int rl = slist[c], j = scol[c];
+        const float d = chain_scalar(sq + rl * kQStr, B + (long)j * p.dim, p.dim);
+        skey[c] = key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)j);
+      }
     }
     __syncthreads();
     // row r's keys merged by 16 threads (r + 16 part, every 16th pooled candidate), then
@@ -476,7 +563,8 @@ void short_launch(vo_ctx* ctx, ShortArgs& a, int batch) {
   }
   ctx->prof.end(st);
   ctx->prof.begin(st, kKMatchMerge);
-  hipLaunchKernelGGL(frerank_kernel, dim3(a.n0_pad / 16, batch), dim3(256), 0, st, a, v4);
+  const int nR = a.n0_pad / 16, nitems = nR * batch;
+  hipLaunchKernelGGL(frerank_kernel, dim3(8 * ((nitems + 7) / 8)), dim3(256), 0, st, a, v4, nR, nitems);
   ctx->prof.end(st);
 }
 

@@ -20,6 +20,7 @@ struct ShortArgs {
   long a_bstride, b_bstride;
   const uint32_t* flag;  // [0] == gen: not SIFT integers; [1] == gen: a non-finite value
   uint32_t gen;
+  int forced;            // float hint: no int8 pack ran; fpack itself flags non-finite values
   double ratio;
   int32_t* best;
   int32_t* idx2;
