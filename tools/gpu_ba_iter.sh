@@ -9,4 +9,5 @@ timeout -k 10 200 python bench.py --no-matcher --no-cpu-baseline > $OUT/bench_cf
 timeout -k 10 200 python bench.py --no-matcher --no-cpu-baseline --config cfg4 --steps 50 --warmup 5 > $OUT/bench_cfg4.json 2> $OUT/bench_cfg4.err
 VO_LIB_PATH=$PWD/visualodometry_amd/lib/libvo_hip_stamps.so timeout -k 10 120 python tools/ba_phase_stamps.py cfg3 > $OUT/k1st.txt 2>&1
 VO_LIB_PATH=$PWD/visualodometry_amd/lib/libvo_hip_stamps.so timeout -k 10 120 python tools/band_stamps.py cfg3 > $OUT/st1.txt 2>&1
+VO_LIB_PATH=$PWD/visualodometry_amd/lib/libvo_hip_stamps.so timeout -k 10 120 python tools/band_stamps.py cfg4 > $OUT/st4.txt 2>&1
 echo done

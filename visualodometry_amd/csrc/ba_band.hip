@@ -705,13 +705,22 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
           : "v"(a)
           : "memory");
     } else {
-      const int l0 = __builtin_amdgcn_readfirstlane(6 * g0);
-#pragma unroll
-      for (int c = 0; c < 6; ++c) z[c] = readlane_d(Yb, l0 + c);
-      if (act && qb == 0) {
-        const uint32_t a = (uint32_t)(uintptr_t)(zs + 6 * G + sr);
-        asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(Yb) : "memory");
-      }
+      // z_k to every lane through LDS (the lanes holding it store it, the others to the dummy
+      // row; LDS ops of one wave complete in order): one round trip instead of 12 v_readlanes
+      // and their SGPR hazards (~17 cycles per dword measured)
+      (void)g0;
+      const uint32_t aw = (uint32_t)(uintptr_t)((act && qb == 0) ? zs + 6 * G + sr : dyn + DOFF + lane);
+      const uint32_t ar = (uint32_t)(uintptr_t)(zs + 6 * G);
+      asm volatile(
+          "ds_write_b64 %3, %4\n\t"
+          "ds_read_b128 %0, %5\n\t"
+          "ds_read_b128 %1, %5 offset:16\n\t"
+          "ds_read_b128 %2, %5 offset:32\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(*reinterpret_cast<double2*>(&z[0])), "=&v"(*reinterpret_cast<double2*>(&z[2])),
+            "=&v"(*reinterpret_cast<double2*>(&z[4]))
+          : "v"(aw), "v"(Yb), "v"(ar)
+          : "memory");
     }
     if (act && qb >= 1)
       Yb -= o.Lc[0] * z[0] + o.Lc[1] * z[1] + o.Lc[2] * z[2] + o.Lc[3] * z[3] + o.Lc[4] * z[4] + o.Lc[5] * z[5];
