@@ -207,7 +207,7 @@ def bench_matcher_float(ctx, batch: int = 16, n: int = 2048, dim: int = 256, cal
                      "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tfl / BF16_MFMA_PEAK_TFLOPS,
                      "traffic": (traffic_all or {}).get("match_f32"),
                      "note": "2 sweeps x 2 flops per pair and dimension / their summed HIP-event duration; the "
-                             "exact fp32 re-rank of the shortlisted candidates is in kernel_us.match_merge"},
+                             "exact fp32 re-rank of the shortlisted candidates is kernel_us.match_rerank"},
     }
     rows = 256
     t0 = time.perf_counter()

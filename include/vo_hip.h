@@ -187,8 +187,9 @@ int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n);
  *      8 pnp_hyp, 9 pnp_score, 10 pnp_final, 11 sift_pyramid (all upsample, blur
  *      and downsample launches of one call), 12 sift_extrema (all octaves),
  *      13 sift_orient, 14 sift_select (sort keys, segmented sort, duplicate removal,
- *      retainBest, compaction), 15 sift_desc. */
-#define VO_PROFILE_KERNELS 16
+ *      retainBest, compaction), 15 sift_desc, 16 match_rerank (the float path's exact
+ *      re-rank; before it had an id of its own it was timed under match_merge). */
+#define VO_PROFILE_KERNELS 17
 int vo_profile_enable(vo_ctx* ctx, int on);
 int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
 

@@ -20,4 +20,8 @@ timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $ROOT/$OUT/${TAG}_write -o run -
 python tools/pmc_traffic.py $OUT/${TAG}_fetch/run_counter_collection.csv \
   $OUT/${TAG}_write/run_counter_collection.csv -o $OUT/traffic.json > /dev/null
 timeout -k 10 600 python bench.py --traffic-json $OUT/traffic.json > $OUT/bench_final.json 2> $OUT/bench_final.err
+timeout -k 10 300 python tools/shard_projection.py cfg3 > $OUT/shard_projection_cfg3.json 2> $OUT/shard_projection_cfg3.err
+timeout -k 10 300 python tools/shard_projection.py cfg4 > $OUT/shard_projection_cfg4.json 2> $OUT/shard_projection_cfg4.err
+timeout -k 10 300 python tools/host_call_latency.py > $OUT/host_latency.json 2> $OUT/host_latency.err
+timeout -k 10 300 python bench.py --config cfg4 --no-matcher --no-cpu-baseline --steps 50 --warmup 5 > $OUT/bench_cfg4.json 2> $OUT/bench_cfg4.err
 echo done

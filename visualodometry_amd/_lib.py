@@ -225,7 +225,7 @@ class DeviceArray:
 
 KERNEL_NAMES = ["ba_lin", "ba_reduce", "ba_solve", "match_pack", "match_i8", "match_f32",
                 "match_merge", "triangulate", "pnp_hyp", "pnp_score", "pnp_final", "sift_pyramid",
-                "sift_extrema", "sift_orient", "sift_select", "sift_desc"]
+                "sift_extrema", "sift_orient", "sift_select", "sift_desc", "match_rerank"]
 
 
 def profile_enable(ctx: "Context", on: bool = True) -> None:

@@ -47,6 +47,8 @@ void Profiler::end(hipStream_t st) {
   VO_HIP_CHECK(hipEventRecord(recs.back().stop, st));
 }
 
+static_assert(kKCount == VO_PROFILE_KERNELS, "profiler ids match include/vo_hip.h");
+
 void Profiler::read(double* ms, int64_t* counts) {
   for (int k = 0; k < kKCount; ++k) {
     ms[k] = 0.0;

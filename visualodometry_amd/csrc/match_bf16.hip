@@ -331,6 +331,11 @@ __device__ __forceinline__ float chain_regs(const float* x, const float* y, int 
   return acc;
 }
 
+// Timing-only builds (EXTRA=-DVO_RERANK_EXP=n, results wrong): 1 no chains, 2 chains without
+// the train-row loads, 3 the loads without the chains.
+#ifndef VO_RERANK_EXP
+#define VO_RERANK_EXP 0
+#endif
 // Exact chains of the wave's (up to) 64 candidates, candidate c0 + lane, with the train rows
 // staged through LDS: a span of kRerankSpan elements of 8 rows per load instruction (8
 // lanes x 16 bytes per row: 8 x 128 contiguous bytes, not 64 rows' scattered 16 bytes), every
@@ -355,7 +360,8 @@ __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const
     const bool in = 4 * k4 < dim;
 #pragma unroll
     for (int t = 0; t < kSpanF4; ++t)
-      v[t] = in ? reinterpret_cast<const float4*>(B + (long)jrow[t] * dim)[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[t] = in && VO_RERANK_EXP != 2 ? reinterpret_cast<const float4*>(B + (long)jrow[t] * dim)[k4]
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   auto consume = [&](int h, const float4 (&v)[kSpanF4], float& acc) __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();  // every lane's reads of the previous span are done (in-order LDS)
@@ -379,6 +385,15 @@ __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const
     }
   };
   float acc = 0.0f;
+  if (VO_RERANK_EXP == 3) {  // timing only: the loads, no staging or chain
+    float4 v[kSpanF4];
+    for (int h = 0; h < dim; h += kRerankSpan) {
+      fetch(h, v);
+#pragma unroll
+      for (int t = 0; t < kSpanF4; ++t) acc += v[t].x;
+    }
+    return acc;
+  }
   float4 v0[kSpanF4], v1[kSpanF4], v2[kSpanF4];
   fetch(0, v0);
   if (kRerankSpan < dim) fetch(kRerankSpan, v1);
@@ -478,9 +493,6 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
       // wave w takes candidates 64 (w + 4 q) + lane (the loop bound is wave-uniform)
       const int wv = tid >> 6;
       for (int c0 = 64 * wv; c0 < total; c0 += 256) {
-#ifndef VO_RERANK_EXP
-#define VO_RERANK_EXP 0
-#endif
         const float d = VO_RERANK_EXP == 1 ? 0.0f : chain_staged(B, sq, slist, scol, sbuf[wv], c0, total, p.dim);
         const int c = c0 + (tid & 63);
         if (c < total) skey[c] = key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)scol[c]);
@@ -562,7 +574,7 @@ void short_launch(vo_ctx* ctx, ShortArgs& a, int batch) {
 #undef VO_SWEEPS
   }
   ctx->prof.end(st);
-  ctx->prof.begin(st, kKMatchMerge);
+  ctx->prof.begin(st, kKMatchRerank);
   const int nR = a.n0_pad / 16, nitems = nR * batch;
   hipLaunchKernelGGL(frerank_kernel, dim3(8 * ((nitems + 7) / 8)), dim3(256), 0, st, a, v4, nR, nitems);
   ctx->prof.end(st);

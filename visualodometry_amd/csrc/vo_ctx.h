@@ -61,7 +61,7 @@ struct Comm;      // ba.hip (RCCL communicator)
 enum KernelId {
   kKBaLin = 0, kKBaReduce, kKBaSolve, kKMatchPack, kKMatchI8, kKMatchF32, kKMatchMerge,
   kKTriangulate, kKPnpHyp, kKPnpScore, kKPnpFinal, kKSiftPyramid, kKSiftExtrema, kKSiftOrient, kKSiftSelect,
-  kKSiftDesc, kKCount
+  kKSiftDesc, kKMatchRerank, kKCount
 };
 
 // HIP-event timing of individual kernels on the context stream (off by default).
