@@ -298,7 +298,7 @@ __device__ __forceinline__ void merge2s(uint64_t& a1, uint64_t& a2, uint64_t b1,
 // (staged in LDS), keys (sqrtf(d2), j) go to LDS, and thread r merges row r's keys.  The
 // candidate set is complete (masks have no capacity); a block with more than kPool
 // candidates takes its rows one at a time through the same code.
-constexpr int kPool = 1024;
+constexpr int kPool = 512;
 constexpr int kQStr = 260;  // floats per staged query row
 #ifndef VO_CHAIN_SPAN
 #define VO_CHAIN_SPAN 128
@@ -337,12 +337,12 @@ __device__ __forceinline__ float chain_regs(const float* x, const float* y, int 
 #define VO_RERANK_EXP 0
 #endif
 // Exact chains of the wave's (up to) 64 candidates, candidate c0 + lane, with the train rows
-// staged through LDS: a span of kRerankSpan elements of 8 rows per load instruction (8
-// lanes x 16 bytes per row: 8 x 128 contiguous bytes, not 64 rows' scattered 16 bytes), every
+// staged through LDS: a span of kRerankSpan elements of 16 rows per load instruction (4
+// lanes x 16 bytes per row: 16 x 64 contiguous bytes, not 64 rows' scattered 16 bytes), every
 // load of a span in flight, then each lane continues its own k-ordered fmaf chain from its
 // row's staged span and its query row (LDS).  Rows are padded by 16 bytes so the per-lane row
 // reads spread over the banks.  Returns lane's d2 (garbage for c0 + lane >= total).
-constexpr int kRerankSpan = 32;                 // floats per span (8 float4 per row)
+constexpr int kRerankSpan = 16;                 // floats per span (4 float4 per row)
 constexpr int kSpanF4 = kRerankSpan / 4, kSpanRows = 64 / kSpanF4;  // per load instruction
 constexpr int kRerankRowStr = kRerankSpan + 4;  // floats per staged row
 __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const float* sq, const int* slist,
