@@ -716,15 +716,18 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
     for (int e = tid; e < nslots * 36; e += kLinThreads) A.slab[36l * S.spos[e / 36] + e % 36] = S.win[e];
     for (int e = tid; e < ncams * 6; e += kLinThreads) A.slab_b[6l * S.cpos[e / 6] + e % 6] = S.bwin[e];
   }
-  static_assert(kChunkTe * 18 >= kLinThreads, "cost reduction scratch");
+  // segment cost: a fixed xor butterfly inside each wave, then the four wave sums in order
+  // (deterministic; one barrier instead of a nine-barrier LDS tree)
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) cost += __shfl_xor(cost, m, 64);
   double* red = &S.Z[0][0];  // Z is dead after the last chunk: reuse it for the cost
-  red[tid] = cost;
+  if ((tid & 63) == 0) red[tid >> 6] = cost;
   __syncthreads();
-  for (int w = kLinThreads / 2; w > 0; w >>= 1) {
-    if (tid < w) red[tid] += red[tid + w];
-    __syncthreads();
+  if (tid == 0) {
+    double c = 0.0;
+    for (int w = 0; w < kLinThreads / 64; ++w) c += red[w];
+    A.slab_cost[seg] = c;
   }
-  if (tid == 0) A.slab_cost[seg] = red[0];
   st.mark(kPhWrite);
   st.flush(A.stamps);
 }
