@@ -729,7 +729,9 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
       VO_HIP_CHECK(hipMemsetAsync(ws.bmax.ptr, 0, ws.bmax.bytes, st));
     }
     s.bmax = ws.bmax.as<uint32_t>();
-    s.part = reinterpret_cast<float2*>(a.partial);  // (batch, nsplit, n0_pad) float2 fits the uint4 partials
+    // (batch, nsplit_f, n0_pad) float2; short_launch picks nsplit_f <= ceil(n1_pad / 64)
+    ws.fpart.reserve((size_t)batch * ceil_div(n1_pad, 64) * n0_pad * sizeof(float2));
+    s.part = ws.fpart.as<float2>();
     ws.cand.reserve((size_t)batch * (n0_pad / 16) * 4 * (n1_pad / 16) * sizeof(uint64_t));
     s.mask = ws.cand.as<uint64_t>();
     short_launch(ctx, s, batch);

@@ -547,8 +547,23 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
 
 }  // namespace
 
+#ifndef VO_FSWEEP_WGS_PER_CU
+#define VO_FSWEEP_WGS_PER_CU 2  // tuning builds: EXTRA=-DVO_FSWEEP_WGS_PER_CU=n
+#endif
+
 void short_launch(vo_ctx* ctx, ShortArgs& a, int batch) {
   hipStream_t st = ctx->stream;
+  {
+    // the sweeps' own column split: a workgroup loads 64 KB of A fragments (128 rows x 256
+    // bf16) before its first MFMA, so it should sweep as many columns as the grid allows --
+    // about VO_FSWEEP_WGS_PER_CU workgroups per CU, one round (splits are multiples of 64
+    // columns, the staging chunk; the split never changes a result)
+    const int64_t row_blocks = (int64_t)(a.n0_pad / kShortRowsPerWG) * batch;
+    const int want = (int)std::max<int64_t>(1, ceil_div((int64_t)VO_FSWEEP_WGS_PER_CU * ctx->num_cus, row_blocks));
+    const int w = std::max(64, ((a.n1_pad + want - 1) / want + 63) / 64 * 64);
+    a.split_w = w;
+    a.nsplit = (a.n1_pad + w - 1) / w;
+  }
   const int a_wgs = (int)ceil_div((int64_t)a.n0_pad * 16, 256);
   const int b_wgs = (int)ceil_div((int64_t)a.n1_pad * 16, 256);
   ctx->prof.begin(st, kKMatchPack);

@@ -21,6 +21,7 @@ struct MatchWorkspace {
   DevBuf tri;       // triangulation staging: pts1, pts2, pts3d, mask
   DevBuf hbf;       // float path: bf16 images of both sides (match_bf16.hip)
   DevBuf fnorm;     // float path: |b'|^2 per train row, |a| per query row
+  DevBuf fpart;     // float path: top-2 of A per (split, row), the sweeps' own split
   DevBuf bmax;      // float path: max |b| per batch entry (zero between calls)
   DevBuf cand;      // float path: candidate lists + counts
   uint32_t gen = 0;         // generation tag of the current call
