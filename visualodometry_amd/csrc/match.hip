@@ -732,8 +732,8 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
     // (batch, nsplit_f, n0_pad) float2; short_launch picks nsplit_f <= ceil(n1_pad / 64)
     ws.fpart.reserve((size_t)batch * ceil_div(n1_pad, 64) * n0_pad * sizeof(float2));
     s.part = ws.fpart.as<float2>();
-    ws.cand.reserve((size_t)batch * (n0_pad / 16) * 4 * (n1_pad / 16) * sizeof(uint64_t));
-    s.mask = ws.cand.as<uint64_t>();
+    ws.cand.reserve((size_t)batch * (n0_pad / 32) * ceil_div(n1_pad, 64) * 64 * sizeof(uint32_t));
+    s.mask = ws.cand.as<uint32_t>();
     short_launch(ctx, s, batch);
   }
   if (float_hint) sweep();

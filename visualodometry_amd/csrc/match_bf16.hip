@@ -17,7 +17,7 @@
 // m2 + E, and every j whose F does not exceed it has A_j <= m2 + 2E.  So the candidate set
 // {j : A_j <= m2 + 2E} holds every pair the exact top-2 can take (ties included), and
 // ranking the candidates by their exact fp32 chains reproduces the oracle.  Candidates
-// are recorded as bit masks (one ballot per row group and 16-column tile), so the set is
+// are recorded as bit masks (one 32-bit word per lane and 64-column chunk), so the set is
 // complete whatever its size, and the re-rank is deterministic.
 //
 // Kernels (one call, every launch exits at once unless the call's descriptors took the
@@ -25,7 +25,7 @@
 //   fpack   bf16 images of both sides, |b'|^2 per train row (+inf for padding), |a| and
 //           max |b| (the bound)
 //   fsweep<1>  v_mfma_f32_16x16x32_bf16 sweep, top-2 of A per (row, split)
-//   fsweep<2>  the same sweep again: every A <= m2 + 2E marked in the row's tile masks
+//   fsweep<2>  the same sweep again: every A <= m2 + 2E marked in its lane's chunk word
 //   frerank    one workgroup per 16 query rows: exact fmaf chains of the pooled candidates, top-2 by
 //              (sqrtf(d2), j), ratio test (the merge_kernel outputs)
 #include "match_short.h"
@@ -35,13 +35,22 @@ namespace vo {
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
-constexpr int kShortRowsPerWG = 128;  // 4 waves x 32 query rows (two 16-row M tiles)
+constexpr int kShortMT = 2;                      // 16-row M tiles per wave (4: 256 VGPRs + AGPRs, one wave per SIMD, 180 us for both sweeps against 133)
+constexpr int kShortRowsPerWG = 64 * kShortMT;  // 4 waves x 16 kShortMT query rows
 constexpr float kShortC = 1.25f * (0.0078125f + 4e-5f);
 
 namespace {
 
 __device__ __forceinline__ bool short_active(const ShortArgs& p) {
   return (p.forced || p.flag[0] == p.gen) && p.flag[1] != p.gen;  // uniform
+}
+
+// Candidate masks of fsweep<2>: per (frame pair, 32-row wave group, 64-column chunk) one
+// 32-bit word per lane; bit 8 u + 4 mt + r = row 32 rg + 16 mt + 4 (lane >> 4) + r, column
+// 64 ch + 16 u + (lane & 15).  Index of the chunk's first word:
+static_assert(kShortMT == 2, "32 candidate bits per lane and chunk: 4 tiles x 2 M tiles x 4 rows");
+__device__ __forceinline__ long short_mask_word(const ShortArgs& p, int b, int rg, int ch) {
+  return (((long)b * (p.n0_pad / 32) + rg) * ((p.n1_pad + 63) / 64) + ch) * 64;
 }
 
 __device__ __forceinline__ float med3_f32(float a, float b, float c) {
@@ -119,8 +128,9 @@ __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int 
 }
 
 // ---- bf16 MFMA sweep ---------------------------------------------------------------
-// Grid (n0_pad / 128, nsplit, batch).  Wave w holds the A fragments of query rows
-// rowbase .. rowbase + 31 in VGPRs; train columns arrive in 64-column chunks staged in
+// Grid (n0_pad / kShortRowsPerWG, nsplit, batch).  Wave w holds the A fragments of query rows
+// rowbase .. rowbase + 16 kShortMT - 1 (kShortMT M tiles: every B fragment read from LDS feeds
+// kShortMT MFMAs) in VGPRs; train columns arrive in 64-column chunks staged in
 // LDS (one global fetch per workgroup, double-buffered, rows padded by 16 bytes).  A
 // 16-column tile: B fragments from LDS, KS MFMAs per M tile, then per (row, column)
 // A' = |b'|^2 - 2 a'.b' and PASS 1: running top-2 (v_min_f32 + v_med3_f32), PASS 2: the
@@ -132,36 +142,30 @@ __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
   constexpr int kRow = Dp + 8;  // bf16 elements per LDS row
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int b = blockIdx.z, split = blockIdx.y, nsplit = p.nsplit;
-  const int rowbase = blockIdx.x * kShortRowsPerWG + wave * 32;
+  const int rowbase = blockIdx.x * kShortRowsPerWG + wave * 16 * kShortMT;
   const __bf16* A = p.ha + (long)b * p.n0_pad * Dp;
   const __bf16* B = p.hb + (long)b * p.n1_pad * Dp;
   const float* nbq = p.nbq + (long)b * p.n1_pad;
 
-  v8bf af[2][KS];
+  v8bf af[kShortMT][KS];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < kShortMT; ++mt)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
       af[mt][ks] = *reinterpret_cast<const v8bf*>(A + (long)(rowbase + 16 * mt + (lane & 15)) * Dp + 32 * ks +
                                                   8 * (lane >> 4));
 
   // this lane's rows: 16 mt + 4 (lane >> 4) + r
-  float m1[2][4], m2[2][4], thr[2][4];
+  float m1[kShortMT][4], m2[kShortMT][4], thr[kShortMT][4];
   if (PASS == 1) {
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < kShortMT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) m1[mt][r] = m2[mt][r] = __builtin_huge_valf();
-    // clear this workgroup's candidate masks: 8 row blocks x 4 x the split's tiles
-    const int T = p.n1_pad / 16, t0 = split * p.split_w / 16, nt = min(p.split_w / 16, T - t0);
-    for (int e = tid; e < 32 * nt; e += 256) {
-      const int rb = e / (4 * nt), rr = (e / nt) % 4, t = e % nt;
-      p.mask[(((long)b * (p.n0_pad / 16) + blockIdx.x * 8 + rb) * 4 + rr) * T + t0 + t] = 0ull;
-    }
   } else {
     const float bm = __uint_as_float(p.bmax[b]);
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < kShortMT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rowbase + 16 * mt + 4 * (lane >> 4) + r;
@@ -205,13 +209,14 @@ __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
     for (int ch = 0; ch < nchunk; ++ch) {
       const int buf = ch & 1, cb = c0 + 64 * ch;
       if (ch + 1 < nchunk) gload(cb + 64, g, gn);
-      // the chunk's four 16-column tiles x two M tiles: eight independent accumulators,
+      uint32_t bits = 0;  // PASS 2: this lane's candidates of the chunk, bit 8 u + 4 mt + r
+      // the chunk's four 16-column tiles x four M tiles: sixteen independent accumulators,
       // k-step outer, so consecutive MFMAs never wait on each other
-      v4f acc[4][2];
+      v4f acc[4][kShortMT];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) acc[u][mt] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int mt = 0; mt < kShortMT; ++mt) acc[u][mt] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         v8bf bf[4];
@@ -221,7 +226,7 @@ __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-          for (int mt = 0; mt < 2; ++mt)
+          for (int mt = 0; mt < kShortMT; ++mt)
             acc[u][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt][ks], bf[u], acc[u][mt], 0, 0, 0);
       }
 #pragma unroll
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
         const float nc = sN[buf][16 * u + (lane & 15)];
         const int col = cb + 16 * u + (lane & 15);
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < kShortMT; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float v = fmaf(-2.0f, acc[u][mt][r], nc);
@@ -238,15 +243,13 @@ __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
               m2[mt][r] = med3_f32(m1[mt][r], m2[mt][r], v);
               m1[mt][r] = fminf(m1[mt][r], v);
             } else {
-              // one ballot per (M tile, r): rows 16 mt + 4 g + r (g = lane >> 4) x the tile's
-              // 16 columns; stored only when a bit is set (rare)
-              const uint64_t hit = __ballot(v <= thr[mt][r] && col < p.n1);
-              if (hit && lane == 0)
-                p.mask[(((long)b * (p.n0_pad / 16) + (rowbase >> 4) + mt) * 4 + r) * (p.n1_pad / 16) +
-                       (cb >> 4) + u] = hit;
+              // row 16 mt + 4 g + r (g = lane >> 4), column cb + 16 u + (lane & 15)
+              bits |= (v <= thr[mt][r] && col < p.n1) ? 1u << (8 * u + 4 * mt + r) : 0u;
             }
           }
       }
+      // one word per lane and chunk, every chunk: no ballot, no branch, nothing to clear
+      if (PASS == 2) p.mask[short_mask_word(p, b, rowbase >> 5, cb >> 6) + lane] = bits;
       if (ch + 1 < nchunk) sstore(buf ^ 1, g, gn);
       __syncthreads();
     }
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
   if (PASS == 1) {
     // top-2 over the 16 lanes of a row (one DPP row): second = med3(a1, b1, min(a2, b2))
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < kShortMT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float M1 = m1[mt][r], M2 = m2[mt][r];
@@ -457,12 +460,14 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
       sq[rl * kQStr + k] = row0 + rl < p.n0 ? p.da[b * p.a_bstride + (long)(row0 + rl) * p.dim + k] : 0.0f;
     }
   }
-  const int T = p.n1_pad / 16;
-  const uint64_t* mblk = p.mask + ((long)b * (p.n0_pad / 16) + R) * 4 * T;  // (r, t) entries
+  // the block's 16 rows are M tile mt = R & 1 of wave row group R >> 1: in each of its
+  // nch x 64 words, bits 8 u + 4 mt + r
+  const int nch = (p.n1_pad + 63) / 64, nw = 64 * nch;
+  const uint32_t* mblk = p.mask + short_mask_word(p, b, R >> 1, 0);
+  const uint32_t msel = 0x0F0F0F0Fu << (4 * (R & 1));
   const float* B = p.db + b * p.b_bstride;
-  // this thread's mask entries: e = tid, tid + 256, ... of the 4 T entries (r, t)
   int cnt = 0;
-  for (int e = tid; e < 4 * T; e += 256) cnt += __popcll(mblk[e]);
+  for (int e = tid; e < nw; e += 256) cnt += __popc(mblk[e] & msel);
   // workgroup exclusive prefix of the counts
   sscan[tid] = cnt;
   __syncthreads();
@@ -476,12 +481,12 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
   int pos = sscan[tid] - cnt;
   const bool pooled = total <= kPool;
   if (pooled) {
-    for (int e = tid; e < 4 * T; e += 256) {
-      const int r = e / T, t = e - r * T;
-      for (uint64_t m = mblk[e]; m; m &= m - 1) {
-        const int bit = __builtin_ctzll(m), g = bit >> 4;
-        slist[pos] = 4 * g + r;  // row_local = 4 g + r
-        scol[pos] = 16 * t + (bit & 15);
+    for (int e = tid; e < nw; e += 256) {
+      const int ch = e >> 6, ln = e & 63;
+      for (uint32_t m = mblk[e] & msel; m; m &= m - 1) {
+        const int bit = __builtin_ctz(m);
+        slist[pos] = 4 * (ln >> 4) + (bit & 3);  // row_local = 4 g + r
+        scol[pos] = 64 * ch + 16 * (bit >> 3) + (ln & 15);
         ++pos;
       }
     }
@@ -520,14 +525,17 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
         for (int q = 0; q < 16; ++q)
           merge2s(k1, k2, skey[tid + 16 * q], reinterpret_cast<const uint64_t*>(slist)[tid + 16 * q]);
     }
-  } else if (tid < 16) {  // rare: thread r walks row r's candidates itself
+  } else if (tid < 16) {  // rare: thread rl walks row rl's candidates itself
     const int g = tid >> 2, r = tid & 3;
-    for (int t = 0; t < T; ++t)
-      for (uint32_t m = (uint32_t)(mblk[r * T + t] >> (16 * g)) & 0xFFFFu; m; m &= m - 1) {
-        const int j = 16 * t + __builtin_ctz(m);
-        const float d = chain_scalar(sq + tid * kQStr, B + (long)j * p.dim, p.dim);
-        merge2s(k1, k2, key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)j), ~0ull);
-      }
+    for (int e = 16 * g; e < nw; e += (e & 15) == 15 ? 49 : 1) {  // the 16 lanes of group g of every chunk
+      const int ch = e >> 6, ln = e & 63;
+      for (int u = 0; u < 4; ++u)
+        if ((mblk[e] >> (8 * u + 4 * (R & 1) + r)) & 1u) {
+          const int j = 64 * ch + 16 * u + (ln & 15);
+          const float d = chain_scalar(sq + tid * kQStr, B + (long)j * p.dim, p.dim);
+          merge2s(k1, k2, key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)j), ~0ull);
+        }
+    }
   }
   const int row = row0 + tid;
   if (tid >= 16 || row >= p.n0) return;

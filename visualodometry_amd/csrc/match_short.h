@@ -14,8 +14,8 @@ struct ShortArgs {
   float* ra;            // (batch, n0_pad) |a|
   uint32_t* bmax;       // (batch) max |b| (float bits); zero between calls
   float2* part;         // (batch, nsplit, n0_pad) top-2 of A per split
-  uint64_t* mask;       // candidate bits: (batch, n0_pad / 16, 4, n1_pad / 16) -- entry (R, r, t)
-                        // bit 16 g + c = row 16 R + 4 g + r, column 16 t + c (fsweep<2>)
+  uint32_t* mask;       // candidate bits (fsweep<2>): (batch, n0_pad / 32, ceil(n1_pad / 64), 64 lanes)
+                        // words, see short_mask_word in match_bf16.hip
   int n0, n1, dim, Dp, n0_pad, n1_pad, split_w, nsplit;
   long a_bstride, b_bstride;
   const uint32_t* flag;  // [0] == gen: not SIFT integers; [1] == gen: a non-finite value
