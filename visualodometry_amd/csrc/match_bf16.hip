@@ -466,30 +466,50 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
   const uint32_t* mblk = p.mask + short_mask_word(p, b, R >> 1, 0);
   const uint32_t msel = 0x0F0F0F0Fu << (4 * (R & 1));
   const float* B = p.db + b * p.b_bstride;
+  // this thread's words (e = tid + 256 i), kept for the list pass: up to 8 (n1 <= 2048);
+  // wider train sets re-read the rest
+  constexpr int kWordRegs = 8;
+  uint32_t wr[kWordRegs];
   int cnt = 0;
-  for (int e = tid; e < nw; e += 256) cnt += __popc(mblk[e] & msel);
-  // workgroup exclusive prefix of the counts
-  sscan[tid] = cnt;
-  __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {
-    const int v = tid >= d ? sscan[tid - d] : 0;
-    __syncthreads();
-    sscan[tid] += v;
-    __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kWordRegs; ++i) {
+    const int e = tid + 256 * i;
+    wr[i] = e < nw ? mblk[e] & msel : 0u;
+    cnt += __popc(wr[i]);
   }
-  const int total = sscan[255];
-  int pos = sscan[tid] - cnt;
+  for (int e = tid + 256 * kWordRegs; e < nw; e += 256) cnt += __popc(mblk[e] & msel);
+  // workgroup exclusive prefix of the counts: inclusive scan inside each wave (fixed shuffle
+  // pattern), the four wave totals through LDS, one barrier
+  const int lane = tid & 63, wv = tid >> 6;
+  int incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(incl, d, 64);
+    incl += lane >= d ? v : 0;
+  }
+  if (lane == 63) sscan[wv] = incl;
+  __syncthreads();
+  int wbase = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    wbase += w < wv ? sscan[w] : 0;
+    total += sscan[w];
+  }
+  int pos = wbase + incl - cnt;
   const bool pooled = total <= kPool;
   if (pooled) {
-    for (int e = tid; e < nw; e += 256) {
+    auto emit = [&](int e, uint32_t m) {
       const int ch = e >> 6, ln = e & 63;
-      for (uint32_t m = mblk[e] & msel; m; m &= m - 1) {
+      for (; m; m &= m - 1) {
         const int bit = __builtin_ctz(m);
         slist[pos] = 4 * (ln >> 4) + (bit & 3);  // row_local = 4 g + r
         scol[pos] = 64 * ch + 16 * (bit >> 3) + (ln & 15);
         ++pos;
       }
-    }
+    };
+#pragma unroll
+    for (int i = 0; i < kWordRegs; ++i) emit(tid + 256 * i, wr[i]);
+    for (int e = tid + 256 * kWordRegs; e < nw; e += 256) emit(e, mblk[e] & msel);
   }
   __syncthreads();
   uint64_t k1 = ~0ull, k2 = ~0ull;
