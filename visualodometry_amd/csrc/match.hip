@@ -724,8 +724,8 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
     ws.fnorm.reserve((size_t)batch * (n0_pad + n1_pad) * sizeof(float));
     s.nbq = ws.fnorm.as<float>();
     s.ra = s.nbq + (size_t)batch * n1_pad;
-    if (ws.bmax.bytes < (size_t)batch * sizeof(uint32_t)) {
-      ws.bmax.reserve((size_t)batch * sizeof(uint32_t));
+    if (ws.bmax.bytes < (size_t)batch * kBmaxStride * sizeof(uint32_t)) {
+      ws.bmax.reserve((size_t)batch * kBmaxStride * sizeof(uint32_t));
       VO_HIP_CHECK(hipMemsetAsync(ws.bmax.ptr, 0, ws.bmax.bytes, st));
     }
     s.bmax = ws.bmax.as<uint32_t>();

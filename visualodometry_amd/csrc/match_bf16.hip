@@ -60,6 +60,11 @@ __device__ __forceinline__ float med3_f32(float a, float b, float c) {
 }
 
 // ---- bf16 images, norms ------------------------------------------------------------
+// Timing-only builds (EXTRA=-DVO_FPACK_EXP=n, results wrong): 1 no max-|b| atomic, 2 no bf16
+// stores, 3 every thread loads the same 64 bytes.
+#ifndef VO_FPACK_EXP
+#define VO_FPACK_EXP 0
+#endif
 // 16 threads per row, 8 consecutive elements per thread and step.  Rows past n are
 // written as zeros (train padding rows get |b'|^2 = +inf: never a candidate).
 __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int v4) {
@@ -75,6 +80,46 @@ __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int 
   __bf16* dst = (is_b ? p.hb + (long)b * p.n1_pad * p.Dp : p.ha + (long)b * p.n0_pad * p.Dp) + (long)row * p.Dp;
   float q2 = 0.0f, x2 = 0.0f;
   bool nonfinite = false;
+  if (v4 && p.dim == p.Dp && n > 0) {
+    // fast path (16-byte rows, dim a multiple of 32): a thread's <= two groups of 8 elements
+    // (k = 8 sub and 8 sub + 128), all four float4 loads issued first from a clamped row
+    // (dead rows read row n - 1 and convert zeros), no per-element guard
+    const float* s0 = (is_b ? p.db + b * p.b_bstride : p.da + b * p.a_bstride) + (long)min(row, n - 1) * p.dim;
+    const int k0 = 8 * sub, k1 = k0 + 128;
+    const bool g0 = in && k0 < p.Dp, g1 = in && k1 < p.Dp;
+    const float4* q = reinterpret_cast<const float4*>(VO_FPACK_EXP == 3 ? (const float*)p.nbq : s0);
+    const float4 x0 = q[min(k0, p.Dp - 8) / 4], x1 = q[min(k0, p.Dp - 8) / 4 + 1];
+    const float4 x2v = q[min(k1, p.Dp - 8) / 4], x3 = q[min(k1, p.Dp - 8) / 4 + 1];
+    const float vv[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
+                          x2v.x, x2v.y, x2v.z, x2v.w, x3.x, x3.y, x3.z, x3.w};
+#pragma unroll
+    for (int gi = 0; gi < 2; ++gi) {
+      const bool use = (gi == 0 ? g0 : g1) && live;
+      v8bf h;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float v = use ? vv[8 * gi + u] : 0.0f;
+        const __bf16 hv = (__bf16)v;
+        const float hf = (float)hv;
+        h[u] = hv;
+        q2 = fmaf(hf, hf, q2);
+        x2 = fmaf(v, v, x2);
+        nonfinite |= !isfinite(v);
+      }
+      if ((gi == 0 ? g0 : g1) && VO_FPACK_EXP != 2) *reinterpret_cast<v8bf*>(dst + (gi == 0 ? k0 : k1)) = h;
+    }
+    // the row's 16 lanes: quad_perm xor 1, xor 2, then row_half_mirror and row_mirror (every
+    // lane ends with the row sum; a fixed order, inside the bound's summation allowance)
+    auto rsum = [](float v) __attribute__((always_inline)) {
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+      return v;
+    };
+    q2 = rsum(q2);
+    x2 = rsum(x2);
+  } else {
   for (int e = sub * 8; in && e < p.Dp; e += 128) {
     v8bf h;
     float vv[8];
@@ -104,6 +149,7 @@ __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int 
     q2 += __shfl_xor(q2, m, 64);
     x2 += __shfl_xor(x2, m, 64);
   }
+  }
   // float hint (no int8 pack): a non-finite value sends the call to the exact fp32 sweep
   if (p.forced && __any(nonfinite) && (threadIdx.x & 63) == 0) const_cast<uint32_t*>(p.flag)[1] = p.gen;
   // norms rounded up by a few ulps: the bound only needs upper estimates
@@ -123,7 +169,7 @@ __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int 
   __syncthreads();
   if (threadIdx.x == 0) {
     m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-    if (m) atomicMax(p.bmax + b, m);
+    if (m && VO_FPACK_EXP != 1) atomicMax(p.bmax + kBmaxStride * b, m);
   }
 }
 
@@ -163,7 +209,7 @@ __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) m1[mt][r] = m2[mt][r] = __builtin_huge_valf();
   } else {
-    const float bm = __uint_as_float(p.bmax[b]);
+    const float bm = __uint_as_float(p.bmax[kBmaxStride * b]);
 #pragma unroll
     for (int mt = 0; mt < kShortMT; ++mt)
 #pragma unroll
@@ -431,7 +477,7 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
   const int per = (nitems + 7) / 8, L = blockIdx.x, item = (L & 7) * per + (L >> 3);
   if (item >= nitems) return;
   const int b = item / nR, R = item - b * nR, tid = threadIdx.x;
-  if (R == 0 && tid == 0) p.bmax[b] = 0u;  // fsweep<2> is done with it
+  if (R == 0 && tid == 0) p.bmax[kBmaxStride * b] = 0u;  // fsweep<2> is done with it
   __shared__ __attribute__((aligned(16))) float sq[16 * kQStr];
   __shared__ __attribute__((aligned(8))) int slist[kPool];  // row_local << 16 | column tile bit position (see below)
   __shared__ int scol[kPool];
