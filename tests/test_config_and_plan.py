@@ -180,3 +180,27 @@ def test_plan_in_forked_child():
             os._exit(4)
     _, status = os.waitpid(pid, 0)
     assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0
+
+
+def test_plan_input_errors_report_the_first_violation():
+    """The planner's argument checks (run inside its first parallel pass) name the lowest
+    non-monotone landmark offset, else the lowest out-of-range camera, whatever the thread
+    split: the messages a serial scan gives."""
+    from visualodometry_amd._lib import VoError
+    from visualodometry_amd.ba import plan_digest
+
+    p = make_ba_config("cfg3")  # 20k landmarks: the first pass runs on several threads
+    ptr0, cam0 = p.point_ptr.copy(), p.obs_cam.copy()
+
+    def err(point_ptr, obs_cam):
+        with pytest.raises(VoError) as e:
+            plan_digest(p.K, point_ptr, obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 1024)
+        return str(e.value)
+
+    cam = cam0.copy()
+    cam[[70000, 9000, 50000]] = [p.n_poses, -1, 99]
+    assert "obs_cam[9000]=-1 out of range" in err(ptr0, cam)
+    ptr = ptr0.copy()
+    ptr[[17001, 4001]] = ptr[[17001, 4001]] + 10**6  # breaks monotonicity at 17001 and 4001
+    assert "point_ptr not monotone at 4001" in err(ptr, cam)
+    assert "point_ptr not monotone at 4001" in err(ptr, cam0)

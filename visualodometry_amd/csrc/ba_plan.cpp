@@ -9,10 +9,13 @@
 #include <mutex>
 #include <thread>
 
+#include <sched.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <numeric>
 
 namespace vo {
@@ -43,6 +46,30 @@ int64_t BAPlan::algorithmic_bytes_per_iter() const {
 }
 
 namespace {
+
+// Host threads the planner may use: the CPU affinity, capped by a cgroup v2 CPU quota (a
+// GPU box's container sees every CPU of the machine but is granted a share of them) and by
+// kPlanMaxThreads.  The plan itself never depends on it.
+#ifndef VO_PLAN_MAX_THREADS
+#define VO_PLAN_MAX_THREADS 16
+#endif
+constexpr int kPlanMaxThreads = VO_PLAN_MAX_THREADS;
+int host_threads() {
+  static const int n = [] {
+    long c = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) c = std::max(1, CPU_COUNT(&set));
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char quota[32] = {0};
+      long period = 0;
+      if (std::fscanf(f, "%31s %ld", quota, &period) == 2 && std::strcmp(quota, "max") != 0 && period > 0)
+        c = std::min(c, std::max(1L, (std::atol(quota) + period - 1) / period));
+      std::fclose(f);
+    }
+    return (int)std::min<long>(c, kPlanMaxThreads);
+  }();
+  return n;
+}
 
 // fn(t) for t = 0 .. n - 1 on n host threads (t = 0 on the caller).  Every use writes
 // disjoint, precomputed ranges, so the plan never depends on the thread count or timing.
@@ -128,8 +155,7 @@ class PlanPool {
 
  private:
   PlanPool() : owner_(getpid()) {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    for (unsigned t = 1; t < std::min(hw, 8u); ++t) workers_.emplace_back([this, t] { loop((int)t); });
+    for (int t = 1; t < host_threads(); ++t) workers_.emplace_back([this, t] { loop(t); });
   }
   void loop(int t) {
     long seen = 0;
@@ -167,18 +193,17 @@ void run_parallel(int n, Fn&& fn) {
 }
 
 int plan_threads(int64_t work) {
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  return (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::min(hw, 8u), work / 2048 + 1}));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), work / 2048 + 1));
 }
 
 // Landmark ranges packed independently (a segment boundary at every range start): a
 // fixed function of the landmark count, never of the host, so the plan is the same on
 // every machine.
 #ifndef VO_PLAN_PARTS
-#define VO_PLAN_PARTS 8
+#define VO_PLAN_PARTS 16
 #endif
 constexpr int kPlanParts = VO_PLAN_PARTS;
-int plan_parts(int L) { return std::max(1, std::min(kPlanParts, L / 2048)); }
+int plan_parts(int L) { return std::max(1, std::min(kPlanParts, L / 1024)); }
 
 struct PlanSeg {
   int chunk0;                               // first chunk (global index after the merge)
@@ -199,11 +224,12 @@ struct PlanPart {
 
 void BAPlan::reset() {
   n_poses = n_points = n_obs = n_fixed = n_free = n_te = 0;
-  for (auto* v : {&pt_perm, &obs_cam, &obs_te, &te_cam, &te_pt, &te_obs, &pt_te, &chunk_obs, &chunk_te,
-                  &chunk_pt, &chunk_slot_base, &chunk_cam_base, &chunk_hdr, &slab_pos, &cam_pos, &seg_hdr,
-                  &slot_ptr, &cam_ptr, &camo_ptr, &seg_chunk, &seg_slot_off, &seg_cam_off, &slot_i, &slot_j,
-                  &segcam_f, &segcam_diag, &seg_acam_off, &seg_acam, &prof_first, &prof_off, &prof_last,
-                  &prof_src_ptr, &prof_src, &camb_ptr, &camb_src, &solve_tab})
+  for (auto* v : {&pt_perm, &obs_cam, &obs_te, &te_cam, &te_pt, &te_obs, &pt_te, &slot_ptr, &cam_ptr, &camo_ptr,
+                  &slot_i, &slot_j, &segcam_f, &segcam_diag})
+    v->clear();
+  for (auto* v : {&chunk_obs, &chunk_te, &chunk_pt, &chunk_slot_base, &chunk_cam_base, &chunk_hdr, &slab_pos,
+                  &cam_pos, &seg_hdr, &seg_chunk, &seg_slot_off, &seg_cam_off, &seg_acam_off, &seg_acam,
+                  &prof_first, &prof_off, &prof_last, &prof_src_ptr, &prof_src, &camb_ptr, &camb_src, &solve_tab})
     v->clear();
   obs_uv.clear();
   te_lcam.clear();
@@ -226,10 +252,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   if (N > 32767) return fmt("n_poses=%ld exceeds the 32767 camera ids of a segment header", N);
   if (n_fixed < 0 || n_fixed > N) return fmt("bad n_fixed=%ld (n_poses=%ld)", n_fixed, N);
   if (point_ptr[0] != 0 || point_ptr[L] != M) return "point_ptr must start at 0 and end at n_obs";
-  for (int p = 0; p < L; ++p)
-    if (point_ptr[p + 1] < point_ptr[p]) return fmt("point_ptr not monotone at %ld", p);
-  for (int o = 0; o < M; ++o)
-    if (obs_cam[o] < 0 || obs_cam[o] >= N) return fmt("obs_cam[%ld]=%ld out of range", o, obs_cam[o]);
+  // point_ptr monotone and obs_cam in range: checked by the first parallel pass below
 
   P.n_poses = N;
   P.n_points = L;
@@ -238,6 +261,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   P.n_free = N - n_fixed;
   const int nthr = plan_threads(M);
 
+  PlanArr<int32_t> ob_start(L + 1), sorted(std::max(M, 1)), te_start(L + 1);
   // landmarks ordered by first camera (stable counting sort; no observation: last), which
   // keeps each workgroup's camera window narrow.  Per-thread histograms over landmark
   // ranges, offsets in (camera, range) order, then each range scatters its landmarks.
@@ -245,9 +269,22 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     std::vector<int32_t> first(L);
     const int nt = std::max(1, std::min(nthr, L / 1024 + 1));
     std::vector<int32_t> hist((size_t)nt * (N + 1), 0);
+    std::vector<int32_t> bad_ptr(nt, -1), bad_obs(nt, -1);  // first violation of each range
     auto lrange = [&](int t) { return std::make_pair((int)((int64_t)L * t / nt), (int)((int64_t)L * (t + 1) / nt)); };
     run_parallel(nt, [&](int t) {
       const auto [pa, pb] = lrange(t);
+      for (int p = pa; p < pb; ++p)
+        if (point_ptr[p + 1] < point_ptr[p]) {
+          bad_ptr[t] = p;
+          return;
+        }
+      // locally monotone but outside [0, M]: another range is not monotone (reported there)
+      if (point_ptr[pa] < 0 || point_ptr[pb] > M) return;
+      for (int o = point_ptr[pa]; o < point_ptr[pb]; ++o)
+        if (obs_cam[o] < 0 || obs_cam[o] >= N) {
+          bad_obs[t] = o;
+          return;
+        }
       int32_t* h = &hist[(size_t)t * (N + 1)];
       for (int p = pa; p < pb; ++p) {
         int f = N;
@@ -256,6 +293,10 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         ++h[f];
       }
     });
+    for (int t = 0; t < nt; ++t)  // the lowest violation, as a serial scan would find it
+      if (bad_ptr[t] >= 0) return fmt("point_ptr not monotone at %ld", bad_ptr[t]);
+    for (int t = 0; t < nt; ++t)
+      if (bad_obs[t] >= 0) return fmt("obs_cam[%ld]=%ld out of range", bad_obs[t], obs_cam[bad_obs[t]]);
     int32_t off = 0;
     for (int c = 0; c <= N; ++c)
       for (int t = 0; t < nt; ++t) {
@@ -268,7 +309,11 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     run_parallel(nt, [&](int t) {
       const auto [pa, pb] = lrange(t);
       int32_t* h = &hist[(size_t)t * (N + 1)];
-      for (int p = pa; p < pb; ++p) P.pt_perm[h[first[p]]++] = p;
+      for (int p = pa; p < pb; ++p) {
+        const int32_t q = h[first[p]]++;
+        P.pt_perm[q] = p;
+        ob_start[q + 1] = point_ptr[p + 1] - point_ptr[p];  // the prefix sum follows
+      }
     });
   }
   PLAN_T("order");
@@ -276,9 +321,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   // observations grouped by (landmark, camera) -> track entries.  Pass A sorts each
   // landmark's observations by camera (stable) into its slot and counts its track
   // entries; pass B writes every array at the prefix offsets.
-  std::vector<int32_t> ob_start(L + 1), sorted(std::max(M, 1)), te_start(L + 1);
   ob_start[0] = 0;
-  for (int q = 0; q < L; ++q) ob_start[q + 1] = ob_start[q] + point_ptr[P.pt_perm[q] + 1] - point_ptr[P.pt_perm[q]];
+  for (int q = 0; q < L; ++q) ob_start[q + 1] += ob_start[q];
   auto qrange = [&](int t, int n) { return std::make_pair((int)((int64_t)L * t / n), (int)((int64_t)L * (t + 1) / n)); };
   run_parallel(nthr, [&](int t) {
     const auto [qa, qb] = qrange(t, nthr);
@@ -547,8 +591,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     // per-thread lookup tables (camera -> window index, camera pair -> slot) and counting-sort buffers
     std::vector<int32_t> fcam_idx(tables ? std::max(Nf, 1) : 0, -1), acam_idx(tables ? N : 0, -1);
     std::vector<int32_t> pair_slot(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, -1);
-    std::vector<int32_t> cnt, cnt2, pairs_slot;
-    std::vector<uint16_t> pairs_tmp;
+    int32_t cnt[std::max(kSegSlots, kSegCams) + 1], cnt2[kSegCams + 1], pslot[kChunkPairs];
+    uint16_t ptmp[kChunkPairs];
     for (int si = sa; si < sbnd; ++si) {
       PlanSeg& s = segs[si];
       std::sort(s.cams.begin(), s.cams.end());
@@ -587,30 +631,34 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
           if (P.te_cam[t] >= n_fixed) P.te_lcam[t] = (int16_t)lcam_of(P.te_cam[t] - n_fixed);
         // pair lists by slot: a stable counting sort of the (x, y) pairs in generation order
-        pairs_tmp.clear();
-        pairs_slot.clear();
+        // (a landmark's track entries are sorted by camera, so (cam x, cam y) is (hi, lo))
+        int npair = 0;
+        std::fill(cnt, cnt + ns + 1, 0);
         for (int q = P.chunk_pt[ch]; q < P.chunk_pt[ch + 1]; ++q) {
-          for (int x = P.pt_te[q]; x < P.pt_te[q + 1]; ++x) {
-            if (P.te_cam[x] < n_fixed) continue;
-            for (int y = P.pt_te[q]; y <= x; ++y) {
-              if (P.te_cam[y] < n_fixed) continue;
-              pairs_slot.push_back(slot_of(std::make_pair(P.te_cam[x] - n_fixed, P.te_cam[y] - n_fixed)));
-              pairs_tmp.push_back((uint16_t)((x - te0) | ((y - te0) << 8)));
+          const int ta = P.pt_te[q], tb = P.pt_te[q + 1];
+          for (int x = ta; x < tb; ++x) {
+            const int32_t cx = P.te_cam[x] - n_fixed;
+            if (cx < 0) continue;
+            for (int y = ta; y <= x; ++y) {
+              const int32_t cy = P.te_cam[y] - n_fixed;
+              if (cy < 0) continue;
+              const int32_t sl = slot_of(std::make_pair(cx, cy));
+              pslot[npair] = sl;
+              ptmp[npair++] = (uint16_t)((x - te0) | ((y - te0) << 8));
+              ++cnt[sl + 1];
             }
           }
         }
-        cnt.assign(ns + 1, 0);
-        for (int32_t sl : pairs_slot) ++cnt[sl + 1];
         for (int sl = 0; sl < ns; ++sl) cnt[sl + 1] += cnt[sl];
         const int32_t pbase = pair_base[ch];
         int32_t* sp = &P.slot_ptr[P.chunk_slot_base[ch]];
         for (int sl = 0; sl <= ns; ++sl) sp[sl] = pbase + cnt[sl];
-        for (size_t e = 0; e < pairs_tmp.size(); ++e) P.pair_list[pbase + cnt[pairs_slot[e]]++] = pairs_tmp[e];
+        for (int e = 0; e < npair; ++e) P.pair_list[pbase + cnt[pslot[e]]++] = ptmp[e];
         // camera lists: track entries and observations by window camera, in order
-        cnt.assign(nc + 1, 0);
+        std::fill(cnt, cnt + nc + 1, 0);
+        std::fill(cnt2, cnt2 + nc + 1, 0);
         for (int t = te0; t < P.chunk_te[ch + 1]; ++t)
           if (P.te_lcam[t] >= 0) ++cnt[P.te_lcam[t] + 1];
-        cnt2.assign(nc + 1, 0);
         const int ob0 = P.chunk_obs[ch];
         for (int o = ob0; o < P.chunk_obs[ch + 1]; ++o)
           if (P.te_lcam[P.obs_te[o]] >= 0) ++cnt2[P.te_lcam[P.obs_te[o]] + 1];

@@ -120,6 +120,30 @@ struct PlanHostAlloc {
   friend bool operator!=(const PlanHostAlloc& a, const PlanHostAlloc& b) { return a.pinned != b.pinned; }
 };
 
+// Allocator whose resize() leaves trivial elements unwritten, for the plan arrays the planner
+// writes in full on its worker threads (a value-initialising resize would zero them serially
+// first).  Every element of such an array is written before it is read, uploaded or digested.
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = DefaultInitAlloc<U>;
+  };
+  DefaultInitAlloc() = default;
+  template <class U>
+  DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... Args>
+  void construct(U* p, Args&&... args) {
+    ::new (static_cast<void*>(p)) U(std::forward<Args>(args)...);
+  }
+};
+template <class T>
+using PlanArr = std::vector<T, DefaultInitAlloc<T>>;
+
 struct SolveTableLayout {
   int diag = 0, off = 0, first = 0, step_ptr = 0, panel_i = 0, panel_blk = 0, item_ptr = 0,
       item_blk = 0, item_q = 0, len = 0;
@@ -129,14 +153,14 @@ struct SolveTableLayout {
 struct BAPlan {
   int n_poses = 0, n_points = 0, n_obs = 0, n_fixed = 0, n_free = 0, n_te = 0;
   // internal order -> caller order
-  std::vector<int32_t> pt_perm;   // internal point q -> caller point index
+  PlanArr<int32_t> pt_perm;   // internal point q -> caller point index
   // observations in internal order (points by first camera, then camera)
-  std::vector<float> obs_uv;      // 2 per obs
-  std::vector<int32_t> obs_cam, obs_te;
+  PlanArr<float> obs_uv;      // 2 per obs
+  PlanArr<int32_t> obs_cam, obs_te;
   // track entries
-  std::vector<int32_t> te_cam, te_pt, te_obs;  // te_obs: n_te+1
+  PlanArr<int32_t> te_cam, te_pt, te_obs;  // te_obs: n_te+1
   std::vector<int16_t> te_lcam;                // segment-local free camera, -1 if fixed
-  std::vector<int32_t> pt_te;                  // n_points+1
+  PlanArr<int32_t> pt_te;                  // n_points+1
   // chunks
   std::vector<int32_t> chunk_obs, chunk_te, chunk_pt;  // n_chunks+1
   std::vector<int32_t> chunk_slot_base, chunk_cam_base;  // index into slot_ptr / cam_ptr
@@ -149,17 +173,17 @@ struct BAPlan {
   std::vector<int32_t> slab_pos, cam_pos;
   std::vector<int32_t> seg_hdr;  // kSegHdr ints per segment
   std::vector<ChunkImg, PlanHostAlloc<ChunkImg>> chunk_img;
-  std::vector<int32_t> slot_ptr;   // per chunk: nslots(seg)+1 offsets into pair_list
-  std::vector<uint16_t> pair_list; // (te_x_local | te_y_local << 8)
-  std::vector<int32_t> cam_ptr;    // per chunk: ncams(seg)+1 offsets into cam_list
-  std::vector<uint8_t> cam_list;   // te local index
-  std::vector<int32_t> camo_ptr;   // same indexing as cam_ptr: offsets into camo_list
-  std::vector<uint8_t> camo_list;  // observation local index (U = Jc^T Jc of the camera)
+  PlanArr<int32_t> slot_ptr;   // per chunk: nslots(seg)+1 offsets into pair_list
+  PlanArr<uint16_t> pair_list; // (te_x_local | te_y_local << 8)
+  PlanArr<int32_t> cam_ptr;    // per chunk: ncams(seg)+1 offsets into cam_list
+  PlanArr<uint8_t> cam_list;   // te local index
+  PlanArr<int32_t> camo_ptr;   // same indexing as cam_ptr: offsets into camo_list
+  PlanArr<uint8_t> camo_list;  // observation local index (U = Jc^T Jc of the camera)
   // segments
   std::vector<int32_t> seg_chunk, seg_slot_off, seg_cam_off;  // n_seg+1
-  std::vector<int32_t> slot_i, slot_j;   // per slab slot: global free-camera block (i >= j)
-  std::vector<int32_t> segcam_f;         // per slab b entry: free camera
-  std::vector<int32_t> segcam_diag;      // per slab b entry: its diagonal slot within the segment
+  PlanArr<int32_t> slot_i, slot_j;   // per slab slot: global free-camera block (i >= j)
+  PlanArr<int32_t> segcam_f;         // per slab b entry: free camera
+  PlanArr<int32_t> segcam_diag;      // per slab b entry: its diagonal slot within the segment
   std::vector<int32_t> seg_acam_off, seg_acam;  // per segment: every camera its observations see
   std::vector<uint8_t> obs_acam;                // per observation: index into its segment's seg_acam
   // profile of S (block rows over free cameras)
