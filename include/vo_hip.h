@@ -317,7 +317,9 @@ int vo_sift_detect_and_compute(vo_ctx* ctx, const uint8_t* img, int h, int w, in
                                float* desc, int32_t* count);
 /* Batch of equally sized images in HBM (d_imgs: batch x h x w uint8).  Per image b:
  * d_kps[b * capacity + i], d_desc[(b * capacity + i) * 128], i < d_counts[b]
- * (d_counts[b] = -1 when a capacity overflowed).  Enqueued on the context stream. */
+ * (d_counts[b] < 0 when a capacity overflowed: -d_counts[b] is the working capacity that
+ * image asked for, a lower bound when an earlier stage was cut short).  Enqueued on the
+ * context stream. */
 int vo_sift_detect_and_compute_batch_async(vo_ctx* ctx, const uint8_t* d_imgs, int batch, int h, int w,
                                            int nfeatures, double contrast, double edge, double sigma,
                                            int n_layers, int capacity, vo_sift_keypoint* d_kps, float* d_desc,

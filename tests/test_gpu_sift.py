@@ -119,14 +119,28 @@ def test_detect_and_compute_textured_kitti(ctx):
 def test_detect_and_compute_low_contrast_capacity_retry(ctx):
     """The malaga / parking SIFT settings (contrast 0.01, edge 2, nfeatures 3000,
     config.py:80-85,92-96) on a textured 480 x 640 image, with a working capacity far below
-    the oriented keypoint count: the call grows it (4x per overflow) instead of failing
-    (ADVICE r1), and the result equals the oracle and the large-capacity call."""
+    the oriented keypoint count: the call grows it instead of failing, to the
+    capacity the overflowing pass reported, and the result equals the oracle and
+    the large-capacity call.  The batch entry point reports that capacity as -count."""
     img = sift_scene(480, 640, seed=201, texture=14.0)
     ref = S.detect_and_compute(img, 3000, 0.01, 2.0, 1.6)
     assert len(ref["pt"]) >= 3000
     got = sift.detect_and_compute(img, 3000, 0.01, 2.0, 1.6, capacity=3072, ctx=ctx)
     _check_full(got, ref)
     _check_full(sift.detect_and_compute(img, 3000, 0.01, 2.0, 1.6, ctx=ctx), ref)
+    d_img = _lib.DeviceArray.from_numpy(ctx, img[None])
+    d_cnt = _lib.DeviceArray(ctx, (1,), np.int32)
+    caps = [3072]
+    while True:  # the reported capacity is taken as is: one retry, two when a guess fell short
+        d_kp = _lib.DeviceArray(ctx, (1, caps[-1], 8), np.int32)
+        d_desc = _lib.DeviceArray(ctx, (1, caps[-1], 128), np.float32)
+        sift.detect_and_compute_device(d_img, 3000, 0.01, 2.0, 1.6, 3, d_kp, d_desc, d_cnt, ctx=ctx)
+        n = int(d_cnt.numpy()[0])
+        if n >= 0:
+            break
+        assert -n > caps[-1] and len(caps) < 3, caps
+        caps.append(-n)
+    assert len(caps) >= 2 and n == len(ref["pt"]), caps
 
 
 def test_detect_and_compute_edge_cases(ctx):

@@ -435,8 +435,9 @@ int vo_sift_detect_and_compute(vo_ctx* ctx, const uint8_t* img, int h, int w, in
     hipStream_t s = ctx->stream;
     VO_HIP_CHECK(hipMemcpyAsync(ws.img.ptr, img, nimg, hipMemcpyHostToDevice, s));
     // The working capacity (oriented keypoints before duplicate removal and retainBest)
-    // starts at the caller's and grows 4x per overflow up to the kernel limit (OpenCV has
-    // no cap); only the final keypoints must fit the caller's buffers.
+    // starts at the caller's; an overflowing pass reports the capacity it needed (-n) and the
+    // next pass takes that (at least twice the last, at most the kernel limit: OpenCV has no
+    // cap); only the final keypoints must fit the caller's buffers.
     int cap = std::min(capacity, vo::sift_max_capacity()), n = -1;
     vo_sift_keypoint* dK = nullptr;
     float* dD = nullptr;
@@ -449,7 +450,7 @@ int vo_sift_detect_and_compute(vo_ctx* ctx, const uint8_t* img, int h, int w, in
       VO_HIP_CHECK(hipMemcpyAsync(&n, dC, 4, hipMemcpyDeviceToHost, s));
       VO_HIP_CHECK(hipStreamSynchronize(s));
       if (n >= 0 || cap >= vo::sift_max_capacity()) break;
-      cap = (int)std::min<int64_t>(4ll * cap, vo::sift_max_capacity());
+      cap = (int)std::min<int64_t>(std::max<int64_t>(-(int64_t)n, 2ll * cap), vo::sift_max_capacity());
     }
     VO_REQUIRE(n >= 0, VO_ERR_ARG, "vo_sift_detect_and_compute: more than %d keypoints in one image", cap);
     VO_REQUIRE(n <= capacity, VO_ERR_ARG, "vo_sift_detect_and_compute: %d keypoints exceed capacity=%d", n,

@@ -256,7 +256,7 @@ struct SelArgs {
   const int32_t* cand_count;
   int cand_cap, cap_img, nfeatures;
   uint32_t* sel;         // (batch, cap_img) record indices in output order
-  int32_t* sel_count;    // (batch): kept, or -1 when a capacity overflowed
+  int32_t* sel_count;    // (batch): kept, or -(the capacity needed) when one overflowed
 };
 
 __device__ __forceinline__ bool kp_less2(const float* a, const float* b) {
@@ -282,7 +282,14 @@ __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
   long sbase = 0;  // this image's first element in the batch-wide sorted order
   for (int q = 0; q < b; ++q) sbase += min(A.img_count[q * kCountStride], A.cap_img);
   if (*A.cand_count > A.cand_cap || cnt > A.cap_img) {
-    if (tid == 0) A.sel_count[b] = -1;
+    // the counters kept counting past their capacities: report the per-image working
+    // capacity they ask for, so the host retries at that size instead of growing step by
+    // step.  With every candidate kept, cnt is exact; when candidates were dropped, cnt only
+    // counts the oriented keypoints of the kept ones, so ask for two per candidate (a second
+    // orientation peak is common, more are rare; a short guess costs one more pass).
+    const long ncand = *A.cand_count;
+    const long need = ncand > A.cand_cap ? max((long)cnt, 2 * ((ncand + gridDim.x - 1) / gridDim.x)) : (long)cnt;
+    if (tid == 0) A.sel_count[b] = -(int)min(max(need, 1l), (long)INT32_MAX);
     return;
   }
   const int n = cnt;
