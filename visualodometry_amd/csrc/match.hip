@@ -694,8 +694,8 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
     }
     ctx->prof.end(st);
   };
-  // under the float hint fpack raises the non-finite flag, so the sweep that serves such
-  // calls is enqueued after it
+  // under the float hint no exact sweep or merge is launched: fpack raises the non-finite
+  // flag and frerank_kernel then answers the call by an exact scan itself
   if (!float_hint) sweep();
   if (a.short_ok) {  // float calls: bf16 MFMA shortlist + exact re-rank (match_bf16.hip)
     ShortArgs s{};
@@ -736,10 +736,11 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
     s.mask = ws.cand.as<uint32_t>();
     short_launch(ctx, s, batch);
   }
-  if (float_hint) sweep();
-  ctx->prof.begin(st, kKMatchMerge);
-  hipLaunchKernelGGL(merge_kernel, dim3(row_wgs, batch), dim3(256), 0, st, a, nsplit);
-  ctx->prof.end(st);
+  if (!float_hint) {
+    ctx->prof.begin(st, kKMatchMerge);
+    hipLaunchKernelGGL(merge_kernel, dim3(row_wgs, batch), dim3(256), 0, st, a, nsplit);
+    ctx->prof.end(st);
+  }
   VO_HIP_CHECK(hipGetLastError());
 }
 

@@ -459,6 +459,10 @@ __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const
   return acc;
 }
 
+__device__ __forceinline__ const float* B_row(const ShortArgs& p, int b, int j) {
+  return p.db + b * p.b_bstride + (long)j * p.dim;
+}
+
 __device__ __forceinline__ float chain_scalar(const float* x, const float* y, int dim) {
   float acc = 0.0f;
   for (int k = 0; k < dim; ++k) {
@@ -472,8 +476,11 @@ __device__ __forceinline__ float chain_scalar(const float* x, const float* y, in
 // 8 by round-robin dispatch): XCD x takes the contiguous items [x per, (x + 1) per) of the
 // (pair, 16-row block) list, so the blocks of one frame pair share one L2 and its train rows
 // (2 MB at 2048 x 256) are fetched from the fabric once per XCD instead of by every XCD.
+// Under the float hint no exact sweep is launched: a call with non-finite values (fpack's
+// flag) is answered here by an exact scan of every train row instead (rare; see below).
 __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int nR, int nitems) {
-  if (!short_active(p)) return;
+  const bool exact_scan = p.forced && p.flag[1] == p.gen;  // uniform
+  if (!exact_scan && !short_active(p)) return;
   const int per = (nitems + 7) / 8, L = blockIdx.x, item = (L & 7) * per + (L >> 3);
   if (item >= nitems) return;
   const int b = item / nR, R = item - b * nR, tid = threadIdx.x;
@@ -506,6 +513,27 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
       sq[rl * kQStr + k] = row0 + rl < p.n0 ? p.da[b * p.a_bstride + (long)(row0 + rl) * p.dim + k] : 0.0f;
     }
   }
+  uint64_t k1 = ~0ull, k2 = ~0ull;
+  if (exact_scan) {
+    // the exact fp32 sweep's answer (match.hip sweep_f32 + merge_kernel): the two smallest
+    // (sqrtf(d2), j) keys over the train rows whose k-ordered fmaf chain d2 is finite (a NaN or
+    // +inf d2 never enters a top-2 there).  Thread (r, part) scans rows part, part + 16, ...
+    // for query row r; the 16 partial top-2s of a row merge as below.
+    __syncthreads();
+    const int r = tid & 15, part = tid >> 4;
+    uint64_t a1 = ~0ull, a2 = ~0ull;
+    if (row0 + r < p.n0)
+      for (int j = part; j < p.n1; j += 16) {
+        const float d = chain_scalar(sq + r * kQStr, B_row(p, b, j), p.dim);
+        if (d < __builtin_huge_valf()) merge2s(a1, a2, key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)j), ~0ull);
+      }
+    static_assert(kPool >= 512, "the partial top-2s fit the key pool");
+    skey[tid] = a1;
+    skey[256 + tid] = a2;
+    __syncthreads();
+    if (tid < 16)
+      for (int q = 0; q < 16; ++q) merge2s(k1, k2, skey[tid + 16 * q], skey[256 + tid + 16 * q]);
+  } else {
   // the block's 16 rows are M tile mt = R & 1 of wave row group R >> 1: in each of its
   // nch x 64 words, bits 8 u + 4 mt + r
   const int nch = (p.n1_pad + 63) / 64, nw = 64 * nch;
@@ -558,7 +586,6 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
     for (int e = tid + 256 * kWordRegs; e < nw; e += 256) emit(e, mblk[e] & msel);
   }
   __syncthreads();
-  uint64_t k1 = ~0ull, k2 = ~0ull;
   if (pooled) {
     if (v4) {
       // wave w takes candidates 64 (w + 4 q) + lane (the loop bound is wave-uniform)
@@ -602,6 +629,7 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
           merge2s(k1, k2, key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)j), ~0ull);
         }
     }
+  }
   }
   const int row = row0 + tid;
   if (tid >= 16 || row >= p.n0) return;
