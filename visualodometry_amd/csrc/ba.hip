@@ -54,10 +54,10 @@ namespace vo {
 #define VO_BA_STAMPS 0
 #endif
 constexpr bool kBaStamps = VO_BA_STAMPS != 0;
-// Planner target: K1 segments per CU (profiles/r01_segment_sweep.md); a tuning build may
-// override it at compile time.
+// Planner target: K1 segments per CU = K1's residency (three workgroups per CU), so the
+// whole launch is one round; a tuning build may override it at compile time.
 #ifndef VO_BA_SEGMENTS_PER_CU
-#define VO_BA_SEGMENTS_PER_CU 4
+#define VO_BA_SEGMENTS_PER_CU 3
 #endif
 
 #define VO_NCCL_CHECK(expr)                                                          \
@@ -1551,9 +1551,11 @@ class BAEngine {
     VO_REQUIRE(have_state_, VO_ERR_STATE, "BA: no state set");
   }
 
-  // Planner target of 4 segments per CU (K1's LDS footprint admits two resident
-  // workgroups per CU; the planner's chunk packing leaves ~2.6 per CU at cfg3,
-  // measured best of 128..2048 -- profiles/r01_segment_sweep.md).
+  // Planner target of one K1 round: as many segments as resident workgroups (three per CU,
+  // K1's __launch_bounds__ and LDS image).  A segment's time is about its chunk count times
+  // the per-chunk latency, so one round of longer segments beats two rounds of shorter ones
+  // (cfg4: 766 segments instead of 985; the cfg3 plan packs 678 either way).  Round 1's
+  // sweep (profiles/r01_segment_sweep.md) predates the three-per-CU K1.
   static int segments_target(int num_cus) {
     return VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
   }
