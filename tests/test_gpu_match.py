@@ -227,12 +227,32 @@ def test_float_hint_skips_int_pack_and_stays_exact(ctx):
     n0[5, 7] = np.nan
     n1[9, 3] = np.inf
     auto = [matcher.match_knn2(n0, n1, ctx=ctx)]
+    _check_knn2(n0, n1, ctx, oracle="c")  # the exact sweep (inside merge_kernel) vs the C oracle
     matcher.set_descriptor_kind(matcher.DESC_FLOAT, ctx)
     try:
         _check_knn2(d0, d1, ctx)
         _check_knn2(f0, f1, ctx, oracle="c")
         hinted = matcher.match_knn2(n0, n1, ctx=ctx)
+        _check_knn2(n0, n1, ctx, oracle="c")  # the re-rank kernel's exact scan vs the C oracle
     finally:
         matcher.set_descriptor_kind(matcher.DESC_AUTO, ctx)
     np.testing.assert_array_equal(hinted[0], auto[0][0])
     np.testing.assert_array_equal(hinted[1].view(np.uint32), auto[0][1].view(np.uint32))
+
+
+def test_sift_hint_with_float_values_takes_the_exact_sweep(ctx):
+    """Under the SIFT hint no shortlist is launched: float (and non-finite) values that reach the
+    int8 launch are answered by the exact fp32 sweep inside merge_kernel, bit-exact vs the C
+    oracle; SIFT bytes keep the int8 path."""
+    f0, f1 = superpoint_like_pair(700, 900, 23)
+    n0, n1 = f0.copy(), f1.copy()
+    n0[11, 2] = -np.inf
+    n1[4, 0] = np.nan
+    s0, s1 = sift_like_pair(600, 800, 24)
+    matcher.set_descriptor_kind(matcher.DESC_SIFT, ctx)
+    try:
+        _check_knn2(f0, f1, ctx, oracle="c")
+        _check_knn2(n0, n1, ctx, oracle="c")
+        _check_knn2(s0, s1, ctx)
+    finally:
+        matcher.set_descriptor_kind(matcher.DESC_AUTO, ctx)

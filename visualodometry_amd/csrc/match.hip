@@ -23,12 +23,12 @@
 #include "match_short.h"
 
 #ifndef VO_MATCH_WGS_PER_CU
-#define VO_MATCH_WGS_PER_CU 2
+#define VO_MATCH_WGS_PER_CU (VO_MATCH_MT == 2 ? 1 : 2)
 #endif
 // Tuning builds only (EXTRA=-D...): columns per LDS-staged B chunk (64 or 128) and
 // s_setprio around each tile's MFMA issue.
 #ifndef VO_MATCH_CHUNK
-#define VO_MATCH_CHUNK 64
+#define VO_MATCH_CHUNK (VO_MATCH_MT == 2 ? 128 : 64)
 #endif
 #ifndef VO_MATCH_PRIO
 #define VO_MATCH_PRIO 0
@@ -41,8 +41,16 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int kKStep = 64;          // K of v_mfma_i32_16x16x64_i8
 constexpr int kMaxDpInt = 256;      // int path keeps A fragments in registers
-constexpr int kRowsPerWave = 64;    // 4 M-tiles of 16 rows
-constexpr int kRowsPerWG = 256;     // 4 waves
+// M tiles of 16 query rows per wave (tuning builds: EXTRA=-DVO_MATCH_MT=2 gives 32-row waves,
+// eight per workgroup, 128-column B chunks)
+#ifndef VO_MATCH_MT
+#define VO_MATCH_MT 2
+#endif
+constexpr int kMT = VO_MATCH_MT;
+static_assert(kMT == 2 || kMT == 4, "two or four M tiles per wave");
+constexpr int kRowsPerWave = 16 * kMT;
+constexpr int kRowsPerWG = 256;     // 4 or 8 waves
+constexpr int kMatchThreads = 64 * kRowsPerWG / kRowsPerWave;
 constexpr int kMatchChunk = VO_MATCH_CHUNK;
 constexpr bool kMatchPrio = VO_MATCH_PRIO != 0;
 static_assert(kMatchChunk == 64 || kMatchChunk == 128, "B chunk of 64 or 128 columns");
@@ -183,6 +191,7 @@ struct MatchArgs {
   const float* db;
   int n0, n1, dim, Dp, n0_pad, n1_pad, split_w, force_f32;
   int short_ok;  // float calls take the bf16 shortlist (match_bf16.hip) unless non-finite
+  int exact_in_merge;  // int8 launch: merge_kernel runs the exact fp32 sweep for float values
   long qa_bstride, qb_bstride, a_bstride, b_bstride;
   uint4* partial;
   const uint32_t* flag;
@@ -215,17 +224,17 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
   const int8_t* B = qb + b * qb_bstride;
   const uint32_t* cc = colconst + b * (long)n1_pad;
 
-  v4i afrag[4][KS];
+  v4i afrag[kMT][KS];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  for (int mt = 0; mt < kMT; ++mt)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
       afrag[mt][ks] = *reinterpret_cast<const v4i*>(
           A + (long)(rowbase + mt * 16 + (lane & 15)) * Dp + ks * kKStep + 16 * (lane >> 4));
 
-  uint32_t m1[4][4], m2[4][4];
+  uint32_t m1[kMT][4], m2[kMT][4];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  for (int mt = 0; mt < kMT; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) m1[mt][r] = m2[mt][r] = 0u;
 
@@ -235,15 +244,17 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
   // per workgroup instead of one per wave): 4 threads per column, rows padded to
   // Dp + 16 bytes so a wave's 16-lane ds_read_b128 groups hit distinct banks.
   constexpr int kRow = Dp + 16;
-  constexpr int kCols = kMatchChunk;  // columns per staged chunk
-  constexpr int kNH = kCols / 64;     // 64-column pieces per thread
+  constexpr int kCols = kMatchChunk;           // columns per staged chunk
+  constexpr int kPieceCols = kMatchThreads / 4;  // columns one staging round covers
+  constexpr int kNH = kCols / kPieceCols;       // staging rounds per chunk
+  static_assert(kNH >= 1 && kCols % kPieceCols == 0, "B chunk staging");
   __shared__ __attribute__((aligned(16))) int8_t sB[2][kCols * kRow];
   __shared__ uint32_t sC[2][kCols];
   const int tid = threadIdx.x;
   auto gload = [&](int cbase, v4i (&g)[kNH][KS], uint32_t& gc) {
 #pragma unroll
     for (int h = 0; h < kNH; ++h) {
-      const int col = min(cbase + 64 * h + (tid >> 2), c1 - 1);  // clamped, unconditional
+      const int col = min(cbase + kPieceCols * h + (tid >> 2), c1 - 1);  // clamped, unconditional
       const int8_t* src = B + (long)col * Dp + (tid & 3) * 16 * KS;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) g[h][ks] = *reinterpret_cast<const v4i*>(src + 16 * ks);
@@ -253,7 +264,7 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
   auto sstore = [&](int buf, const v4i (&g)[kNH][KS], uint32_t gc) {
 #pragma unroll
     for (int h = 0; h < kNH; ++h) {
-      int8_t* dst = &sB[buf][(64 * h + (tid >> 2)) * kRow + (tid & 3) * 16 * KS];
+      int8_t* dst = &sB[buf][(kPieceCols * h + (tid >> 2)) * kRow + (tid & 3) * 16 * KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<v4i*>(dst + 16 * ks) = g[h][ks];
     }
@@ -267,7 +278,7 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
     uint32_t cc;
   };
   struct Acc {
-    v4i v[4];
+    v4i v[kMT];
   };
   auto frag = [&](int buf, int u) {
     Frag f;
@@ -280,10 +291,10 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
   auto mm = [&](const Frag& f) {
     Acc a;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) a.v[mt] = v4i{0, 0, 0, 0};
+    for (int mt = 0; mt < kMT; ++mt) a.v[mt] = v4i{0, 0, 0, 0};
     if (kMatchPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < kMT; ++mt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         a.v[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], f.bf[ks], a.v[mt], 0, 0, 0);
@@ -292,7 +303,7 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
   };
   auto epi = [&](const Acc& a, uint32_t ccol) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < kMT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint32_t p = ((uint32_t)a.v[mt][r] << 9) + ccol;
@@ -328,7 +339,7 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
   const int jblock = c0 & ~4095;
   const int gshift = lane & 48;  // this lane's 16-lane group in a ballot mask
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
+  for (int mt = 0; mt < kMT; ++mt) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const uint32_t a1 = m1[mt][r], a2 = m2[mt][r];
@@ -364,11 +375,12 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
 // tx + 16c.  Each pair's d2 is the fmaf chain over k in ascending order.  Per thread
 // the columns arrive in ascending j, so a candidate can only enter the top-2 if
 // d2 < d2(second): sqrtf is evaluated only then (exact filter, see header).
-__device__ __forceinline__ void sweep_f32(const MatchArgs& p, int rowbase) {
+__device__ __forceinline__ void sweep_f32(const MatchArgs& p, int rowbase, int b, int split, int nsplit, int c0,
+                                          int c1) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   const float* da = p.da;
   const float* db = p.db;
-  const int n0 = p.n0, n1 = p.n1, dim = p.dim, n0_pad = p.n0_pad, split_w = p.split_w;
+  const int n0 = p.n0, dim = p.dim, n0_pad = p.n0_pad;
   const long a_bstride = p.a_bstride, b_bstride = p.b_bstride;
   uint4* partial = p.partial;
   // k-major tiles (rows padded by 16 bytes): a thread reads its 4 rows and its 8 columns
@@ -376,7 +388,6 @@ __device__ __forceinline__ void sweep_f32(const MatchArgs& p, int rowbase) {
   __shared__ __attribute__((aligned(16))) float sa[kFloatKC][kFloatTile + 4];
   __shared__ __attribute__((aligned(16))) float sb[kFloatKC][kFloatCols + 4];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int b = blockIdx.z, split = blockIdx.y, nsplit = gridDim.y;
   const float* A = da + b * a_bstride;
   const float* B = db + b * b_bstride;
 
@@ -387,8 +398,6 @@ __device__ __forceinline__ void sweep_f32(const MatchArgs& p, int rowbase) {
     s1[i] = s2[i] = d1st[i] = d2nd[i] = __builtin_huge_valf();
     j1[i] = j2[i] = -1;
   }
-  const int c0 = split * split_w;
-  const int c1 = min(c0 + split_w, n1);
   for (int ct = c0; ct < c1; ct += kFloatCols) {
     // acc[i][q] = the k-ordered fmaf chains of rows ty*4+i, columns tx*8+2q, tx*8+2q+1:
     // packed fp32 (v_pk_add_f32 / v_pk_fma_f32 are the same IEEE operations per element)
@@ -407,7 +416,7 @@ __device__ __forceinline__ void sweep_f32(const MatchArgs& p, int rowbase) {
       for (int e = threadIdx.x; e < kFloatKC * kFloatCols; e += 256) {
         const int rr = e / kFloatKC, kk = e % kFloatKC;
         const int gb = ct + rr, gk = k0 + kk;
-        sb[kk][rr] = (gb < n1 && gk < dim) ? B[(long)gb * dim + gk] : 0.0f;
+        sb[kk][rr] = (gb < c1 && gk < dim) ? B[(long)gb * dim + gk] : 0.0f;
       }
       __syncthreads();
       const int kc = min(kFloatKC, dim - k0);
@@ -470,6 +479,16 @@ __global__ __launch_bounds__(256) void merge_kernel(MatchArgs p, int nsplit) {
   if (fpath && p.short_ok && p.flag[1] != p.gen) return;  // frerank_kernel writes the outputs
   const int b = blockIdx.y, lane = threadIdx.x & 63;
   const int row = blockIdx.x * kRowsPerWG + threadIdx.x;
+  if (fpath && p.exact_in_merge) {
+    // an int8-path launch whose values turned out not SIFT integers (or not finite): the
+    // exact fp32 sweep of this block's rows over every train column here, as split 0 of 1
+    // (rare; the int8 kernel keeps its registers to itself)
+#pragma unroll 1
+    for (int t = 0; t < kRowsPerWG / kFloatTile; ++t)
+      sweep_f32(p, blockIdx.x * kRowsPerWG + t * kFloatTile, b, 0, 1, 0, p.n1);
+    __syncthreads();  // the partials of this block's rows, written by this workgroup
+    nsplit = 1;
+  }
   uint64_t k1 = ~0ull, k2 = ~0ull;
   for (int s = 0; s < nsplit; ++s) {
     const uint4 q = p.partial[((long)b * nsplit + s) * p.n0_pad + row];
@@ -529,16 +548,21 @@ __global__ __launch_bounds__(256) void merge_kernel(MatchArgs p, int nsplit) {
   }
 }
 
+// The int8 sweep only: a call whose values are not SIFT integers (decided on the device by
+// pack_kernel) takes the exact fp32 sweep inside merge_kernel, so this kernel's registers and
+// LDS are its own, not the maximum of both paths'.
 template <int KS>
-__global__ __launch_bounds__(256) void match_kernel(MatchArgs p) {
+__global__ __launch_bounds__(kMatchThreads) void match_kernel(MatchArgs p) {
   const bool fpath = p.force_f32 || p.flag[0] == p.gen;  // uniform
-  if (!fpath) {
-    sweep_i8<KS>(p);
-  } else if (!p.short_ok || p.flag[1] == p.gen) {  // the exact fp32 sweep
+  if (!fpath) sweep_i8<KS>(p);
+}
+
+// descriptors wider than the int8 kernel takes (Dp > 256): the exact fp32 sweep is the path
+__global__ __launch_bounds__(256) void match_f32_kernel(MatchArgs p) {
+  const int c0 = blockIdx.y * p.split_w, c1 = min(c0 + p.split_w, p.n1);
 #pragma unroll 1
-    for (int t = 0; t < kRowsPerWG / kFloatTile; ++t)
-      sweep_f32(p, blockIdx.x * kRowsPerWG + t * kFloatTile);
-  }
+  for (int t = 0; t < kRowsPerWG / kFloatTile; ++t)
+    sweep_f32(p, blockIdx.x * kRowsPerWG + t * kFloatTile, blockIdx.z, blockIdx.y, gridDim.y, c0, c1);
 }
 
 // n1 == 0: no query has a neighbour
@@ -643,6 +667,7 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
   const bool float_hint = int_ok && ws.kind_hint == VO_DESC_FLOAT;
   a.force_f32 = int_ok && !float_hint ? 0 : 1;
   a.short_ok = int_ok && ws.kind_hint != VO_DESC_SIFT ? 1 : 0;
+  a.exact_in_merge = int_ok ? 1 : 0;
   a.a_bstride = (long)n0 * dim;
   a.b_bstride = (long)n1 * dim;
   a.partial = ws.partial.as<uint4>();
@@ -683,16 +708,22 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
                        Dp, vec4, flag, ws.gen);
     ctx->prof.end(st);
   }
-  auto sweep = [&]() {  // int8 sweep, or the exact fp32 sweep (float calls the shortlist cannot take)
+  auto sweep = [&]() {  // int8 sweep, and the exact fp32 sweep (float calls the shortlist cannot take)
     dim3 grid(row_wgs, nsplit, batch);
-    ctx->prof.begin(st, kKMatchI8);
-    switch (int_ok ? Dp / kKStep : 1) {
-      case 1: hipLaunchKernelGGL(match_kernel<1>, grid, dim3(256), 0, st, a); break;
-      case 2: hipLaunchKernelGGL(match_kernel<2>, grid, dim3(256), 0, st, a); break;
-      case 3: hipLaunchKernelGGL(match_kernel<3>, grid, dim3(256), 0, st, a); break;
-      default: hipLaunchKernelGGL(match_kernel<4>, grid, dim3(256), 0, st, a); break;
+    if (int_ok) {
+      ctx->prof.begin(st, kKMatchI8);
+      switch (Dp / kKStep) {
+        case 1: hipLaunchKernelGGL(match_kernel<1>, grid, dim3(kMatchThreads), 0, st, a); break;
+        case 2: hipLaunchKernelGGL(match_kernel<2>, grid, dim3(kMatchThreads), 0, st, a); break;
+        case 3: hipLaunchKernelGGL(match_kernel<3>, grid, dim3(kMatchThreads), 0, st, a); break;
+        default: hipLaunchKernelGGL(match_kernel<4>, grid, dim3(kMatchThreads), 0, st, a); break;
+      }
+      ctx->prof.end(st);
+    } else {
+      ctx->prof.begin(st, kKMatchF32);
+      hipLaunchKernelGGL(match_f32_kernel, grid, dim3(256), 0, st, a);
+      ctx->prof.end(st);
     }
-    ctx->prof.end(st);
   };
   // under the float hint no exact sweep or merge is launched: fpack raises the non-finite
   // flag and frerank_kernel then answers the call by an exact scan itself
