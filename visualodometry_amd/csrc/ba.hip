@@ -736,33 +736,35 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
 struct ReduceArgs {
   int nprof, F, nseg;
   double lambda;
-  const int* prof_src_ptr;
-  const uint8_t* prof_diag;
-  const int* prof_diag_cam;  // free camera of each profile block (its block row)
-  const int* camb_ptr;
+  // per profile block, host-built (BAEngine::setup) so that one load level gives every
+  // address: slab rows [x, y); on a diagonal block its camera's rhs slab entries [z, w)
+  // (z < 0 otherwise)
+  const int4* meta;
+  // per profile block: output offset of its 36 values (| kRedTranspose), of its rhs (diagonal)
+  const int2* out;
   const double* slab;
   const double* slab_b;
   const double* slab_cost;
   double* sys;         // output: profile [S | b | cost] or the banded K3's column layout
-  const int* dst;      // per profile block: output offset of its 36 values (| kRedTranspose)
-  const int* rdst;     // per free camera: output offset of its 6 rhs values
   long cost_off;       // output offset of the cost
   const int* status;
 };
 constexpr int kRedTranspose = 1 << 30;  // dst flag: store the block transposed
 
 // Sums slab rows k0 + part + j*stride (entry e of each, rows of W doubles), j = 0, 1, ...,
-// in fixed order with 4 independent loads in flight.  K1 wrote each block's window slots
+// in fixed order with 8 independent loads in flight.  K1 wrote each block's window slots
 // to consecutive rows in prof_src order, so this is the former gather, bit for bit.
 template <int W>
 __device__ __forceinline__ double sum_rows(const double* __restrict__ slab, int k0, int k1, int part,
                                            int stride, int e) {
   double acc = 0.0;
   int k = k0 + part;
-  for (; k + 3 * stride < k1; k += 4 * stride) {
-    const double v0 = slab[(long)W * k + e], v1 = slab[(long)W * (k + stride) + e];
-    const double v2 = slab[(long)W * (k + 2 * stride) + e], v3 = slab[(long)W * (k + 3 * stride) + e];
-    acc = (((acc + v0) + v1) + v2) + v3;
+  for (; k + 7 * stride < k1; k += 8 * stride) {
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = slab[(long)W * (k + i * stride) + e];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += v[i];
   }
   for (; k < k1; k += stride) acc += slab[(long)W * k + e];
   return acc;
@@ -777,48 +779,49 @@ constexpr int kRedBParts = kRedThreads / 6;   // partial sums per rhs entry
 
 // One workgroup per profile block: 7 strided partial sums per S entry and, on a
 // diagonal block, 42 per rhs entry of that camera, combined in fixed order (the
-// result is bitwise reproducible).  The last workgroup sums the cost.
+// result is bitwise reproducible).  The last workgroup sums the cost.  Every load of a
+// workgroup is issued before the status test (a failed earlier step: nothing is written).
 __global__ __launch_bounds__(kRedThreads) void ba_reduce_kernel(ReduceArgs A) {
-  if (A.status && *A.status) return;
-  __shared__ double part[kRedBParts * 6 > kRedSParts * 36 ? kRedBParts * 6 : kRedSParts * 36];
+  __shared__ double part[kRedSParts * 36], partb[kRedBParts * 6];
   const int blk = blockIdx.x, tid = threadIdx.x;
   if (blk < A.nprof) {
-    const bool diag = A.prof_diag[blk];
-    const int k0 = A.prof_src_ptr[blk], k1 = A.prof_src_ptr[blk + 1];
-    if (tid < kRedSParts * 36)
-      part[tid] = sum_rows<36>(A.slab, k0, k1, tid / 36, kRedSParts, tid % 36);
+    const int4 m = A.meta[blk];
+    const int2 o = A.out[blk];
+    const int failed = A.status ? *A.status : 0;
+    const bool diag = m.z >= 0;
+    double ps = 0.0, pb = 0.0;
+    if (tid < kRedSParts * 36) ps = sum_rows<36>(A.slab, m.x, m.y, tid / 36, kRedSParts, tid % 36);
+    if (diag && tid < kRedBParts * 6) pb = sum_rows<6>(A.slab_b, m.z, m.w, tid / 6, kRedBParts, tid % 6);
+    if (failed) return;  // uniform
+    if (tid < kRedSParts * 36) part[tid] = ps;
+    if (tid < kRedBParts * 6) partb[tid] = pb;
     __syncthreads();
     if (tid < 36) {
       double acc = 0.0;
 #pragma unroll
       for (int q = 0; q < kRedSParts; ++q) acc += part[36 * q + tid];
       if (diag && tid % 7 == 0) acc += A.lambda;
-      const int d = A.dst[blk];
-      A.sys[(d & ~kRedTranspose) + ((d & kRedTranspose) ? 6 * (tid % 6) + tid / 6 : tid)] = acc;
-    }
-    if (!diag) return;
-    __syncthreads();
-    const int f = A.prof_diag_cam[blk];
-    if (tid < kRedBParts * 6)
-      part[tid] = sum_rows<6>(A.slab_b, A.camb_ptr[f], A.camb_ptr[f + 1], tid / 6, kRedBParts, tid % 6);
-    __syncthreads();
-    if (tid < 6) {
+      A.sys[(o.x & ~kRedTranspose) + ((o.x & kRedTranspose) ? 6 * (tid % 6) + tid / 6 : tid)] = acc;
+    } else if (diag && tid >= 64 && tid < 70) {  // another wave: the rhs sum beside the S sum
+      const int e = tid - 64;
       double acc = 0.0;
-      for (int q = 0; q < kRedBParts; ++q) acc += part[6 * q + tid];
-      A.sys[A.rdst[f] + tid] = acc;
+      for (int q = 0; q < kRedBParts; ++q) acc += partb[6 * q + e];
+      A.sys[o.y + e] = acc;
     }
     return;
   }
   // cost: fixed-order lane-strided partial sums, then a fixed tree over the 256 lanes
   double c = 0.0;
   for (int s = tid; s < A.nseg; s += kRedThreads) c += A.slab_cost[s];
-  part[tid] = c;
+  if (A.status && *A.status) return;
+  __shared__ double cpart[kRedThreads];
+  cpart[tid] = c;
   __syncthreads();
   for (int m = kRedThreads / 2; m > 0; m >>= 1) {
-    if (tid < m) part[tid] += part[tid + m];
+    if (tid < m) cpart[tid] += cpart[tid + m];
     __syncthreads();
   }
-  if (tid == 0) A.sys[A.cost_off] = part[0];
+  if (tid == 0) A.sys[A.cost_off] = cpart[0];
 }
 
 // K3: profile Cholesky solve S dc = b + pose update.
@@ -1316,15 +1319,6 @@ class BAEngine {
     upload(d_slab_pos_, P.slab_pos, st);
     upload(d_cam_pos_, P.cam_pos, st);
     upload(d_seg_hdr_, P.seg_hdr, st);
-    upload(d_prof_src_ptr_, P.prof_src_ptr, st);
-    upload(d_prof_diag_, P.prof_diag, st);
-    {
-      std::vector<int32_t> row(std::max(1, P.n_prof_blocks()), 0);
-      for (int i = 0; i < P.n_free; ++i)
-        for (int b = P.prof_off[i]; b < P.prof_off[i + 1]; ++b) row[b] = i;
-      upload(d_prof_row_, row, st);
-    }
-    upload(d_camb_ptr_, P.camb_ptr, st);
     PLAN_T("setup: uploads");
     const int F = P.n_free;
     d_points_.reserve(std::max(1, P.n_points) * 24ull);
@@ -1386,8 +1380,18 @@ class BAEngine {
       d_sys_.reserve((sys_len_ + pad) * 8);
       // entries K2 never writes (outside the profile, the bottom side's separator) stay 0
       VO_HIP_CHECK(hipMemsetAsync(d_sys_.ptr, 0, (sys_len_ + pad) * 8, st));
-      upload(d_red_dst_, red_dst_, st);
-      upload(d_red_rdst_, red_rdst_, st);
+      // K2's per-block table: slab rows, the diagonal blocks' rhs entries, output offsets
+      std::vector<int4> meta(std::max(1, nprof), int4{0, 0, -1, -1});
+      std::vector<int2> out(std::max(1, nprof), int2{0, 0});
+      for (int i = 0; i < F; ++i)
+        for (int b = P.prof_off[i]; b < P.prof_off[i + 1]; ++b) {
+          const bool diag = P.prof_diag[b] != 0;
+          meta[b] = int4{P.prof_src_ptr[b], P.prof_src_ptr[b + 1], diag ? P.camb_ptr[i] : -1,
+                         diag ? P.camb_ptr[i + 1] : -1};
+          out[b] = int2{red_dst_[b], diag ? red_rdst_[i] : 0};
+        }
+      upload(d_red_meta_, meta, st);
+      upload(d_red_out_, out, st);
       d_zero_.reserve(512);  // zero block (masked prefetches)
       VO_HIP_CHECK(hipMemsetAsync(d_zero_.ptr, 0, 512, st));
     }
@@ -1624,16 +1628,12 @@ class BAEngine {
     // damping on the camera diagonal: added once -- by rank 0 only when the partial
     // systems of the landmark shards are all-reduced
     R.lambda = (ctx_->comm && ctx_->comm->rank > 0) ? 0.0 : prob_.lambda;
-    R.prof_src_ptr = d_prof_src_ptr_.as<int>();
-    R.prof_diag = d_prof_diag_.as<uint8_t>();
-    R.prof_diag_cam = d_prof_row_.as<int>();
-    R.camb_ptr = d_camb_ptr_.as<int>();
+    R.meta = d_red_meta_.as<int4>();
+    R.out = d_red_out_.as<int2>();
     R.slab = d_slab_.as<double>();
     R.slab_b = d_slab_b_.as<double>();
     R.slab_cost = d_slab_cost_.as<double>();
     R.sys = d_sys_.as<double>();
-    R.dst = d_red_dst_.as<int>();
-    R.rdst = d_red_rdst_.as<int>();
     R.cost_off = cost_off_;
     R.status = d_status_.as<int>();
     ctx_->prof.begin(ctx_->stream, kKBaReduce);
@@ -1777,7 +1777,7 @@ class BAEngine {
   bool band_on_ = false;
   BandLds band_lds_;
   BandTables band_tab_;
-  DevBuf d_fac_, d_zero_, d_band_tab_, d_red_dst_, d_red_rdst_;
+  DevBuf d_fac_, d_zero_, d_band_tab_, d_red_meta_, d_red_out_;
   std::vector<int32_t> red_dst_, red_rdst_;  // K2 output offsets (host copies for gn_step)
   long cost_off_ = 0;
   DevBuf d_solve_tab_;
@@ -1785,7 +1785,7 @@ class BAEngine {
   hipEvent_t h_state_ev_ = nullptr;  // set_state's upload from h_state_ done
   bool h_state_busy_ = false;
   DevBuf d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;  // K1's plan (the chunk images hold every list)
-  DevBuf d_prof_src_ptr_, d_prof_diag_, d_prof_row_, d_camb_ptr_, d_stamps_, d_stamps3_;
+  DevBuf d_stamps_, d_stamps3_;
   static constexpr bool stamps_on_ = kBaStamps;
 
  public:
