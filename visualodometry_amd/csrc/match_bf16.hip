@@ -185,7 +185,10 @@ template <int PASS, int KS>
 __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
   if (!short_active(p)) return;
   constexpr int Dp = 32 * KS;
-  constexpr int kRow = Dp + 8;  // bf16 elements per LDS row
+  // bf16 elements per LDS row: Dp + 16 (32 bytes) puts each of gfx950's ds_read_b128 16-lane
+  // groups ({0-3,12-15,20-27}, ...) on 16 distinct 16-byte slots for the fragment reads below
+  // (lane l: row l & 15, slot l >> 4); Dp + 8 was 2-way in every group
+  constexpr int kRow = Dp + 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int b = blockIdx.z, split = blockIdx.y, nsplit = p.nsplit;
   const int rowbase = blockIdx.x * kShortRowsPerWG + wave * 16 * kShortMT;
