@@ -185,10 +185,18 @@ template <int PASS, int KS>
 __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
   if (!short_active(p)) return;
   constexpr int Dp = 32 * KS;
-  // bf16 elements per LDS row: Dp + 16 (32 bytes) puts each of gfx950's ds_read_b128 16-lane
-  // groups ({0-3,12-15,20-27}, ...) on 16 distinct 16-byte slots for the fragment reads below
-  // (lane l: row l & 15, slot l >> 4); Dp + 8 was 2-way in every group
-  constexpr int kRow = Dp + 16;
+  // B chunk image in LDS: rows of Dp + 32 bf16 (Dp / 8 + 4 16-byte slots), slot s of row r
+  // stored at slot s ^ ((2 r) & (Dp / 8 - 1)) (power-of-two Dp / 8).  The staging thread t
+  // moves slots t & 3, (t & 3) + 4, ... of row t >> 2 (so four lanes load 64 contiguous bytes
+  // of a row), and with this stride and swizzle both gfx950 access patterns are bank-conflict
+  // free: the ds_write_b128 staging (8 x 8 contiguous lanes, banks (a/4) mod 32) and the
+  // fragment reads (ds_read_b128, 16-lane groups {0-3,12-15,20-27}, ..., banks (a/4) mod 64;
+  // lane l: row l & 15, slot l >> 4).  Round 2's Dp + 8 rows with 128 contiguous bytes per
+  // thread were 4-way on every staging store and 2-way on every fragment read.
+  constexpr int kRow = Dp + 32;
+  constexpr int kNS = Dp / 8;
+  constexpr int kSwz = (kNS & (kNS - 1)) == 0 ? kNS - 1 : 0;
+  auto swz = [](int row, int slot) { return slot ^ ((2 * row) & kSwz); };
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int b = blockIdx.z, split = blockIdx.y, nsplit = p.nsplit;
   const int rowbase = blockIdx.x * kShortRowsPerWG + wave * 16 * kShortMT;
@@ -237,15 +245,16 @@ __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
   typedef int v4i __attribute__((ext_vector_type(4)));
   auto gload = [&](int cbase, v4i (&g)[KS], float& gn) {
     const int col = min(cbase + (tid >> 2), c1 - 1);
-    const __bf16* src = B + (long)col * Dp + (tid & 3) * 8 * KS;
+    const __bf16* src = B + (long)col * Dp + 8 * (tid & 3);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) g[ks] = *reinterpret_cast<const v4i*>(src + 8 * ks);
+    for (int ks = 0; ks < KS; ++ks) g[ks] = *reinterpret_cast<const v4i*>(src + 32 * ks);  // slot (t & 3) + 4 ks
     gn = nbq[min(cbase + (tid & 63), c1 - 1)];
   };
   auto sstore = [&](int buf, const v4i (&g)[KS], float gn) {
-    __bf16* dst = &sB[buf][(tid >> 2) * kRow + (tid & 3) * 8 * KS];
+    const int row = tid >> 2;
+    __bf16* dst = &sB[buf][row * kRow];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<v4i*>(dst + 8 * ks) = g[ks];
+    for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<v4i*>(dst + 8 * swz(row, (tid & 3) + 4 * ks)) = g[ks];
     if (tid < 64) sN[buf][tid] = gn;
   };
   if (c0 < c1) {
@@ -271,7 +280,8 @@ __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
         v8bf bf[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          bf[u] = *reinterpret_cast<const v8bf*>(&sB[buf][(16 * u + (lane & 15)) * kRow + 8 * (lane >> 4) + 32 * ks]);
+          bf[u] = *reinterpret_cast<const v8bf*>(
+              &sB[buf][(16 * u + (lane & 15)) * kRow + 8 * swz(lane & 15, (lane >> 4) + 4 * ks)]);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
