@@ -406,7 +406,13 @@ __device__ __forceinline__ float chain_regs(const float* x, const float* y, int 
 // reads spread over the banks.  Returns lane's d2 (garbage for c0 + lane >= total).
 constexpr int kRerankSpan = 16;                 // floats per span (4 float4 per row)
 constexpr int kSpanF4 = kRerankSpan / 4, kSpanRows = 64 / kSpanF4;  // per load instruction
-constexpr int kRerankRowStr = kRerankSpan + 4;  // floats per staged row
+// Staged rows of kRerankSpan floats (4 16-byte slots), slot s of row r stored at s ^ ((r >> 2) & 3):
+// conflict-free on gfx950 both for the staging ds_write_b128 (8 x 8 contiguous lanes, four per
+// row) and for each lane reading its own row (ds_read_b128 16-lane groups {0-3,12-15,20-27},
+// ...); the former 16-byte row padding was 2-way on every staging store
+constexpr int kRerankRowStr = kRerankSpan;
+static_assert(kRerankSpan == 16, "the slot swizzle assumes 4 slots per staged row");
+__device__ __forceinline__ int rr_slot(int row, int slot) { return slot ^ ((row >> 2) & 3); }
 __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const float* sq, const int* slist,
                                               const int* scol, float* sbuf, int c0, int total, int dim) {
   const int lane = threadIdx.x & 63;
@@ -428,14 +434,16 @@ __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const
   auto consume = [&](int h, const float4 (&v)[kSpanF4], float& acc) __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();  // every lane's reads of the previous span are done (in-order LDS)
 #pragma unroll
-    for (int t = 0; t < kSpanF4; ++t)
-      *reinterpret_cast<float4*>(sbuf + (kSpanRows * t + lane / kSpanF4) * kRerankRowStr + 4 * (lane % kSpanF4)) = v[t];
+    for (int t = 0; t < kSpanF4; ++t) {
+      const int row = kSpanRows * t + lane / kSpanF4;
+      *reinterpret_cast<float4*>(sbuf + row * kRerankRowStr + 4 * rr_slot(row, lane % kSpanF4)) = v[t];
+    }
     __builtin_amdgcn_wave_barrier();
     const float* y = sbuf + lane * kRerankRowStr;
     const int n = min(kRerankSpan, dim - h);
     for (int k = 0; k < n; k += 4) {
       const float4 xv = *reinterpret_cast<const float4*>(x + h + k);
-      const float4 yv = *reinterpret_cast<const float4*>(y + k);
+      const float4 yv = *reinterpret_cast<const float4*>(y + 4 * rr_slot(lane, k / 4));
       float d = xv.x - yv.x;
       acc = fmaf(d, d, acc);
       d = xv.y - yv.y;
