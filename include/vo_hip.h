@@ -110,7 +110,10 @@ int vo_match_batch_async(vo_ctx* ctx, const float* d_des0, const float* d_des1,
  *   VO_DESC_SIFT (1): OpenCV SIFT integers expected (FeatureFrontend with the SIFT
  *     extractor, frontend.py:25-34): the float shortlist is not launched, and a call
  *     whose values are not 0..255 integers takes the exact fp32 sweep instead;
- *   VO_DESC_FLOAT (2): SuperPoint-like floats expected (same kernels as AUTO). */
+ *   VO_DESC_FLOAT (2): SuperPoint-like floats expected: no int8 pack, integer check, int8
+ *     sweep or merge is launched; every call takes the bf16 shortlist + exact re-rank (exact
+ *     for SIFT integers too), and a call with a non-finite value is answered by the re-rank
+ *     kernel's exact scan (the exact fp32 sweep's result). */
 #define VO_DESC_AUTO 0
 #define VO_DESC_SIFT 1
 #define VO_DESC_FLOAT 2
