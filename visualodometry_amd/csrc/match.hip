@@ -33,6 +33,11 @@
 #ifndef VO_MATCH_PRIO
 #define VO_MATCH_PRIO 0
 #endif
+// Timing-only builds (results wrong): 1 replaces the top-2 epilogue by one op per pair,
+// 2 skips the MFMAs (the epilogue runs on the B fragments)
+#ifndef VO_MATCH_EXP
+#define VO_MATCH_EXP 0
+#endif
 
 namespace vo {
 namespace {
@@ -71,6 +76,12 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
   uint32_t r;
   // not volatile: a pure function the scheduler may interleave with the MFMAs
   asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+__device__ __forceinline__ uint32_t max3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_max3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
 
@@ -324,7 +335,8 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
     for (int mt = 0; mt < kMT; ++mt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        a.v[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], f.bf[ks], a.v[mt], 0, 0, 0);
+        a.v[mt] = VO_MATCH_EXP == 2 ? a.v[mt] + f.bf[ks] + afrag[mt][ks]
+                                    : __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], f.bf[ks], a.v[mt], 0, 0, 0);
     if (kMatchPrio) __builtin_amdgcn_s_setprio(0);
     return a;
   };
@@ -333,9 +345,27 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
     for (int mt = 0; mt < kMT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        if (VO_MATCH_EXP == 1) {  // timing only: one op per pair instead of the top-2 update
+          m1[mt][r] ^= (uint32_t)a.v[mt][r];
+          continue;
+        }
         const uint32_t p = ((uint32_t)a.v[mt][r] << 9) + ccol;
         m2[mt][r] = med3_u32(m1[mt][r], m2[mt][r], p);
         m1[mt][r] = max(m1[mt][r], p);
+      }
+  };
+  // two keys p, q of one (row, lane) at once (keys are unique, larger = better): the new best
+  // is max3(m1, p, q) and the new second max(m2, med3(m1, p, q)) (m2 <= m1, so m2 can only be
+  // second by beating the middle of the three)
+  auto epi2 = [&](const Acc& a, uint32_t ca, const Acc& b, uint32_t cbk) {
+#pragma unroll
+    for (int mt = 0; mt < kMT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t p = ((uint32_t)a.v[mt][r] << 9) + ca;
+        const uint32_t q = ((uint32_t)b.v[mt][r] << 9) + cbk;
+        m2[mt][r] = max(m2[mt][r], med3_u32(m1[mt][r], p, q));
+        m1[mt][r] = max3_u32(m1[mt][r], p, q);
       }
   };
   if (c0 < c1) {  // uniform over the workgroup (split bounds)
@@ -348,12 +378,18 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
     for (int ch = 0; ch < nchunk; ++ch) {
       const int buf = ch & 1, cb = c0 + kCols * ch;
       if (ch + 1 < nchunk) gload(cb + kCols, g, gc);  // in flight during this chunk
+      // tiles in pairs: the two tiles' keys enter the top-2 together (epi2: 5 VALU ops for
+      // two pairs of the same (row, lane) instead of 6); a lone last tile takes epi
 #pragma unroll
-      for (int u = 0; u < kCols / 16; ++u)
-        if (cb + 16 * u < c1) {
+      for (int u = 0; u < kCols / 16; u += 2) {
+        if (cb + 16 * (u + 1) < c1) {
+          const Frag f0 = frag(buf, u), f1 = frag(buf, u + 1);
+          epi2(mm(f0), f0.cc, mm(f1), f1.cc);
+        } else if (cb + 16 * u < c1) {
           const Frag f = frag(buf, u);
           epi(mm(f), f.cc);
         }
+      }
       if (ch + 1 < nchunk) sstore(buf ^ 1, g, gc);
       __syncthreads();
     }
