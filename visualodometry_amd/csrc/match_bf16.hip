@@ -425,6 +425,13 @@ __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const
   // three spans in flight: span h's loads were issued two spans earlier
   auto fetch = [&](int h, float4 (&v)[kSpanF4]) __attribute__((always_inline)) {
     const int k4 = h / 4 + lane % kSpanF4;
+    if (h + kRerankSpan <= dim) {  // a whole span (uniform): unconditional loads
+#pragma unroll
+      for (int t = 0; t < kSpanF4; ++t)
+        v[t] = VO_RERANK_EXP != 2 ? reinterpret_cast<const float4*>(B + (long)jrow[t] * dim)[k4]
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      return;
+    }
     const bool in = 4 * k4 < dim;
 #pragma unroll
     for (int t = 0; t < kSpanF4; ++t)
@@ -440,10 +447,7 @@ __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const
     }
     __builtin_amdgcn_wave_barrier();
     const float* y = sbuf + lane * kRerankRowStr;
-    const int n = min(kRerankSpan, dim - h);
-    for (int k = 0; k < n; k += 4) {
-      const float4 xv = *reinterpret_cast<const float4*>(x + h + k);
-      const float4 yv = *reinterpret_cast<const float4*>(y + 4 * rr_slot(lane, k / 4));
+    auto step4 = [&](const float4& xv, const float4& yv) __attribute__((always_inline)) {
       float d = xv.x - yv.x;
       acc = fmaf(d, d, acc);
       d = xv.y - yv.y;
@@ -452,6 +456,20 @@ __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const
       acc = fmaf(d, d, acc);
       d = xv.w - yv.w;
       acc = fmaf(d, d, acc);
+    };
+    if (h + kRerankSpan <= dim) {  // a whole span (uniform): all eight LDS reads in flight at once
+      float4 xv[kSpanF4], yv[kSpanF4];
+#pragma unroll
+      for (int q = 0; q < kSpanF4; ++q) {
+        xv[q] = *reinterpret_cast<const float4*>(x + h + 4 * q);
+        yv[q] = *reinterpret_cast<const float4*>(y + 4 * rr_slot(lane, q));
+      }
+#pragma unroll
+      for (int q = 0; q < kSpanF4; ++q) step4(xv[q], yv[q]);
+    } else {
+      const int n = dim - h;
+      for (int k = 0; k < n; k += 4)
+        step4(*reinterpret_cast<const float4*>(x + h + k), *reinterpret_cast<const float4*>(y + 4 * rr_slot(lane, k / 4)));
     }
   };
   float acc = 0.0f;
