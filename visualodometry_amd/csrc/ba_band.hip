@@ -249,8 +249,10 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // the poses for the tail's update, staged now (their load latency under the prologue's)
   for (int e = tid; e < 12 * A.n_poses; e += kBandThreads) pose_l[e] = A.pose_cur[e];
   // Ring prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every
-  // 16-byte load in flight, then the stores.
-  if (!prior_fail) {
+  // 16-byte load in flight, then the stores.  The loads do not wait for the status word
+  // (one global round trip less on the launch's path); a failed earlier solve only skips
+  // the stores.
+  {
     const int nT = min(w + 2, ncolT) * CS / 2, nB = min(w + 2, ncolB) * CS / 2;  // double2 pieces
     const double2* gT = reinterpret_cast<const double2*>(A.sys);
     const double2* gB = reinterpret_cast<const double2*>(A.sys + (long)ncolT * CS);
@@ -260,6 +262,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       const int e = tid + u * kBandThreads;
       v[u] = e < nT ? gT[e] : e < nT + nB ? gB[e - nT] : make_double2(0.0, 0.0);
     }
+    if (!prior_fail)
 #pragma unroll
     for (int u = 0; u < kProLoads; ++u) {
       const int e = tid + u * kBandThreads;
