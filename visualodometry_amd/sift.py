@@ -112,15 +112,17 @@ def detect_and_compute(gray, nfeatures: int = 0, contrast: float = 0.04, edge: f
     if img.ndim != 2:
         raise ValueError("detect_and_compute: a single-channel (h, w) uint8 image is expected")
     h, w = img.shape
-    kp = np.zeros(capacity, KP_DTYPE)
-    desc = np.zeros((capacity, 128), np.float32)
+    # unzeroed outputs (the call writes the first `count` entries; a zeroed 17 MB pair cost
+    # milliseconds per call once the allocator serves it from the heap), compact copies returned
+    kp = np.empty(capacity, KP_DTYPE)
+    desc = np.empty((capacity, 128), np.float32)
     cnt = C.c_int32(0)
     check(ctx.lib.vo_sift_detect_and_compute(ctx.handle, ptr(img, C.c_uint8), h, w, int(nfeatures), float(contrast),
                                              float(edge), float(sigma), int(n_layers), int(capacity),
                                              kp.ctypes.data_as(C.c_void_p), ptr(desc, C.c_float), C.byref(cnt)),
           "vo_sift_detect_and_compute")
     n = cnt.value
-    return _kp_dict(kp[:n], desc[:n])
+    return _kp_dict(kp[:n], desc[:n].copy())
 
 
 def detect_and_compute_device(d_imgs: _lib.DeviceArray, nfeatures: int, contrast: float, edge: float, sigma: float,
@@ -159,6 +161,26 @@ class KeyPoint:
         self.class_id = -1
 
 
+def _keypoints(r: dict) -> tuple:
+    """KeyPoint objects of a detect_and_compute result: the fields converted to Python floats /
+    ints in bulk (``tolist``), then the slots set directly (no per-field ``float()`` calls)."""
+    pts = r["pt"].astype(np.float64)
+    out = []
+    new, append = KeyPoint.__new__, out.append
+    for pt, size, angle, response, octave in zip(zip(pts[:, 0].tolist(), pts[:, 1].tolist()), r["size"].tolist(),
+                                                  r["angle"].tolist(), r["response"].tolist(),
+                                                  r["octave"].tolist()):
+        k = new(KeyPoint)
+        k.pt = pt
+        k.size = size
+        k.angle = angle
+        k.response = response
+        k.octave = octave
+        k.class_id = -1
+        append(k)
+    return tuple(out)
+
+
 class SIFT:
     """``cv2.SIFT`` as the reference uses it: ``SIFT_create(nfeatures=..., contrastThreshold=...,
     edgeThreshold=..., sigma=...)`` then ``detectAndCompute(gray, None) -> (keypoints,
@@ -179,9 +201,7 @@ class SIFT:
             raise NotImplementedError("SIFT.detectAndCompute: masks and provided keypoints are not supported")
         r = detect_and_compute(image, self.nfeatures, self.contrast, self.edge, self.sigma, self.n_layers,
                                ctx=self._ctx or _lib.context())
-        kps = tuple(KeyPoint(p[0], p[1], s, a, q, o) for p, s, a, q, o in
-                    zip(r["pt"], r["size"], r["angle"], r["response"], r["octave"]))
-        return kps, (r["descriptors"] if len(kps) else None)
+        return _keypoints(r), (r["descriptors"] if len(r["size"]) else None)
 
 
 def SIFT_create(nfeatures: int = 0, nOctaveLayers: int = 3, contrastThreshold: float = 0.04,
