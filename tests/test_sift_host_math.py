@@ -52,3 +52,23 @@ def test_orientation_hist_host_build_matches_oracle(exe, tmp_path):
             np.testing.assert_array_equal(H[q], h)
             checked += 1
     assert checked > 100
+
+
+def test_keypoint_objects_carry_the_record_fields():
+    """detectAndCompute's bulk KeyPoint builder (sift._keypoints) gives the same Python values
+    and types as the per-keypoint cv2-style constructor, for every field the reference reads."""
+    from visualodometry_amd.sift import KP_DTYPE, KeyPoint, _keypoints, _kp_dict
+    rng = np.random.default_rng(5)
+    kp = np.zeros(257, KP_DTYPE)
+    for f in ("x", "y", "size", "angle", "response"):
+        kp[f] = rng.random(kp.size, dtype=np.float32) * 1000
+    kp["octave"] = rng.integers(-(1 << 20), 1 << 20, kp.size)
+    r = _kp_dict(kp, np.zeros((kp.size, 128), np.float32))
+    got = _keypoints(r)
+    assert isinstance(got, tuple) and len(got) == kp.size
+    for k, rec in zip(got, kp):
+        ref = KeyPoint(rec["x"], rec["y"], rec["size"], rec["angle"], rec["response"], rec["octave"])
+        for f in ("pt", "size", "angle", "response", "octave", "class_id"):
+            assert getattr(k, f) == getattr(ref, f) and type(getattr(k, f)) is type(getattr(ref, f)), f
+        assert type(k.pt[0]) is float and type(k.pt[1]) is float
+    assert _keypoints(_kp_dict(kp[:0], np.zeros((0, 128), np.float32))) == ()
