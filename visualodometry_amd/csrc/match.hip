@@ -21,6 +21,7 @@
 // Float path (any other values, e.g. SuperPoint): d2 is the k-ordered fmaf
 // chain sum((a_k - b_k)^2) in fp32 and keys are (sqrtf(d2), j) directly.
 #include "match_short.h"
+#include <type_traits>
 
 #ifndef VO_MATCH_WGS_PER_CU
 #define VO_MATCH_WGS_PER_CU (VO_MATCH_MT == 2 ? 1 : 2)
@@ -375,14 +376,17 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
     gload(c0, g, gc);
     sstore(0, g, gc);
     __syncthreads();
-    for (int ch = 0; ch < nchunk; ++ch) {
+    // One chunk: its tiles in pairs, the two tiles' keys entering the top-2 together (epi2:
+    // 5 VALU ops for two pairs of the same (row, lane) instead of 6); a lone last tile takes
+    // epi.  Whole chunks (every tile in range) run as a loop of their own with no bounds
+    // branch: the per-tile branches' joins made the compiler copy the 16 top-2 registers
+    // of each tile pair (16 v_mov per 40 VALU ops of the epilogue).
+    auto chunk = [&](int ch, auto whole) __attribute__((always_inline)) {
       const int buf = ch & 1, cb = c0 + kCols * ch;
       if (ch + 1 < nchunk) gload(cb + kCols, g, gc);  // in flight during this chunk
-      // tiles in pairs: the two tiles' keys enter the top-2 together (epi2: 5 VALU ops for
-      // two pairs of the same (row, lane) instead of 6); a lone last tile takes epi
 #pragma unroll
       for (int u = 0; u < kCols / 16; u += 2) {
-        if (cb + 16 * (u + 1) < c1) {
+        if (decltype(whole)::value || cb + 16 * (u + 1) < c1) {
           const Frag f0 = frag(buf, u), f1 = frag(buf, u + 1);
           epi2(mm(f0), f0.cc, mm(f1), f1.cc);
         } else if (cb + 16 * u < c1) {
@@ -392,7 +396,11 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
       }
       if (ch + 1 < nchunk) sstore(buf ^ 1, g, gc);
       __syncthreads();
-    }
+    };
+    const int nwhole = (c1 - c0) / kCols;
+    int ch = 0;
+    for (; ch < nwhole; ++ch) chunk(ch, std::true_type{});
+    for (; ch < nchunk; ++ch) chunk(ch, std::false_type{});
   }
 
   // Merge the 16 lanes that share each row (one DPP row) on the u32 keys: within a
