@@ -1,0 +1,14 @@
+"""The PnP bench line alone (bench.bench_pnp) with per-kernel HIP-event averages, for A/B runs of
+library builds (VO_LIB_PATH)."""
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import bench  # noqa: E402
+from visualodometry_amd import _lib  # noqa: E402
+
+ctx = _lib.context(0)
+r = bench.bench_pnp(ctx)
+r.pop("cpu_baseline", None)
+print(json.dumps({"value": r["value"], "kernel_us": r["kernel_us"]}))

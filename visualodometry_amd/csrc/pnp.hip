@@ -38,6 +38,7 @@ using namespace pnpm;
 
 // ---------------------------------------------------------------- kernels
 constexpr int kScoreGroupMax = 128;  // hypotheses scored by one workgroup, at most
+constexpr int kScoreRegPts = 4;      // points per thread held in registers (frames up to 1024 points)
 
 struct PnpArgs {
   const float* X;          // (total, 3) object points, frames back to back
@@ -108,7 +109,53 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group) {
   __shared__ int s_count[kScoreGroupMax];
   for (int h = threadIdx.x; h < h1 - h0; h += 256) s_count[h] = 0;
   __syncthreads();
-  if (n > kPts) {
+  if (n > kPts && n <= kScoreRegPts * 256) {
+    // the thread's points in registers for all the group's hypotheses, two hypotheses per
+    // pass (independent chains through the f64 division); per point the same arithmetic
+    float P[kScoreRegPts][5];
+#pragma unroll
+    for (int u = 0; u < kScoreRegPts; ++u) {
+      const int i = min((int)threadIdx.x + 256 * u, n - 1);
+      const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
+      float M[3];
+      load3(a.X, o + i, M);
+      P[u][0] = M[0];
+      P[u][1] = M[1];
+      P[u][2] = M[2];
+      P[u][3] = q.x;
+      P[u][4] = q.y;
+    }
+    auto score = [&](const double* model) __attribute__((always_inline)) {
+      double R[9], t[3];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) R[k] = model[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) t[k] = model[9 + k];
+      int cnt = 0;
+#pragma unroll
+      for (int u = 0; u < kScoreRegPts; ++u) {
+        const float M[3] = {P[u][0], P[u][1], P[u][2]};
+        cnt += ((int)threadIdx.x + 256 * u < n && is_inlier(R, t, M, P[u][3], P[u][4], a.K, a.thr2)) ? 1 : 0;
+      }
+      return cnt;
+    };
+    for (int h = h0; h < h1; h += 2) {
+      const double* m0 = a.models + ((size_t)f * a.H + h) * kModel;  // uniform
+      const double* m1 = a.models + ((size_t)f * a.H + min(h + 1, h1 - 1)) * kModel;
+      const bool on0 = m0[15] != 0.0, on1 = h + 1 < h1 && m1[15] != 0.0;
+      int c0 = on0 ? score(m0) : 0;
+      int c1 = on1 ? score(m1) : 0;
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        c0 += __shfl_xor(c0, m, 64);
+        c1 += __shfl_xor(c1, m, 64);
+      }
+      if ((threadIdx.x & 63) == 0) {
+        if (c0) atomicAdd(&s_count[h - h0], c0);
+        if (c1) atomicAdd(&s_count[h + 1 - h0], c1);
+      }
+    }
+  } else if (n > kPts) {
     for (int h = h0; h < h1; ++h) {
       const double* model = a.models + ((size_t)f * a.H + h) * kModel;  // uniform
       if (model[15] == 0.0) continue;
