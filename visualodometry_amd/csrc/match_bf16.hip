@@ -59,6 +59,15 @@ __device__ __forceinline__ float med3_f32(float a, float b, float c) {
   return r;
 }
 
+// IEEE minNum without fminf's operand canonicalisation (the compiler quiets a loop-carried
+// operand with v_max_f32 x, x, x before every v_min_f32): the running minima here come from
+// v_min / v_med3 and the keys from v_fma, never signalling NaNs, so the result is the same
+__device__ __forceinline__ float min_f32(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // ---- bf16 images, norms ------------------------------------------------------------
 // Timing-only builds (EXTRA=-DVO_FPACK_EXP=n, results wrong): 1 no max-|b| atomic, 2 no bf16
 // stores, 3 every thread loads the same 64 bytes.
@@ -300,7 +309,7 @@ __global__ __launch_bounds__(256) void fsweep_kernel(ShortArgs p) {
             const float v = fmaf(-2.0f, acc[u][mt][r], nc);
             if (PASS == 1) {
               m2[mt][r] = med3_f32(m1[mt][r], m2[mt][r], v);
-              m1[mt][r] = fminf(m1[mt][r], v);
+              m1[mt][r] = min_f32(m1[mt][r], v);
             } else {
               // row 16 mt + 4 g + r (g = lane >> 4), column cb + 16 u + (lane & 15)
               bits |= (v <= thr[mt][r] && col < p.n1) ? 1u << (8 * u + 4 * mt + r) : 0u;
