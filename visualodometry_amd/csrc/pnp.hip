@@ -216,7 +216,7 @@ __device__ __forceinline__ void lm_reduce(double (&acc)[kNe], double* red, doubl
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void pnp_final_kernel(PnpArgs a) {
+__global__ __launch_bounds__(256, 2) void pnp_final_kernel(PnpArgs a) {  // two per CU: <= 256 VGPRs
   const int f = blockIdx.x;
   const int o = a.off[f], n = a.off[f + 1] - o;
   __shared__ int s_best, s_count, s_go;
