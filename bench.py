@@ -534,6 +534,8 @@ def main() -> int:
         if best is None or ms > prof[best][0]:
             best = k
     nbytes = ba_kernel_bytes(best, p.n_poses, p1 - p0, int(ptr[-1]), n_free, stats["profile_blocks"])
+    if best == "ba_solve" and "ba_reduce" not in prof:  # K2 fused into K3's launch (one rank)
+        nbytes += ba_kernel_bytes("ba_reduce", p.n_poses, p1 - p0, int(ptr[-1]), n_free, stats["profile_blocks"])
     avg_s = prof[best][0] / prof[best][1] / 1e3
     achieved = nbytes / avg_s / 1e9
     traffic_all = {}

@@ -46,6 +46,10 @@
 #include "ba_plan.h"
 #include "vo_ctx.h"
 
+#ifndef VO_BA_FUSE
+#define VO_BA_FUSE 1  // tuning build: 0 launches K2 on its own
+#endif
+
 namespace vo {
 
 // Diagnostic build only (make EXTRA=-DVO_BA_STAMPS=1): per-phase s_memtime stamps of K1
@@ -732,50 +736,8 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
   st.flush(A.stamps);
 }
 
-// K2: fixed-order reduction of the slabs into [S profile | b | cost].
-struct ReduceArgs {
-  int nprof, F, nseg;
-  double lambda;
-  // per profile block, host-built (BAEngine::setup) so that one load level gives every
-  // address: slab rows [x, y); on a diagonal block its camera's rhs slab entries [z, w)
-  // (z < 0 otherwise)
-  const int4* meta;
-  // per profile block: output offset of its 36 values (| kRedTranspose), of its rhs (diagonal)
-  const int2* out;
-  const double* slab;
-  const double* slab_b;
-  const double* slab_cost;
-  double* sys;         // output: profile [S | b | cost] or the banded K3's column layout
-  long cost_off;       // output offset of the cost
-  const int* status;
-};
-constexpr int kRedTranspose = 1 << 30;  // dst flag: store the block transposed
-
-// Sums slab rows k0 + part + j*stride (entry e of each, rows of W doubles), j = 0, 1, ...,
-// in fixed order with 8 independent loads in flight.  K1 wrote each block's window slots
-// to consecutive rows in prof_src order, so this is the former gather, bit for bit.
-template <int W>
-__device__ __forceinline__ double sum_rows(const double* __restrict__ slab, int k0, int k1, int part,
-                                           int stride, int e) {
-  double acc = 0.0;
-  int k = k0 + part;
-  for (; k + 7 * stride < k1; k += 8 * stride) {
-    double v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = slab[(long)W * (k + i * stride) + e];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc += v[i];
-  }
-  for (; k < k1; k += stride) acc += slab[(long)W * k + e];
-  return acc;
-}
-
-#ifndef VO_RED_THREADS
-#define VO_RED_THREADS 256
-#endif
-constexpr int kRedThreads = VO_RED_THREADS;
-constexpr int kRedSParts = kRedThreads / 36;  // partial sums per S block entry
-constexpr int kRedBParts = kRedThreads / 6;   // partial sums per rhs entry
+// K2: fixed-order reduction of the slabs into [S profile | b | cost] (ReduceArgs, sum_rows:
+// ba_reduce.h).
 
 // One workgroup per profile block: 7 strided partial sums per S entry and, on a
 // diagonal block, 42 per rhs entry of that camera, combined in fixed order (the
@@ -812,7 +774,15 @@ __global__ __launch_bounds__(kRedThreads) void ba_reduce_kernel(ReduceArgs A) {
   }
   // cost: fixed-order lane-strided partial sums, then a fixed tree over the 256 lanes
   double c = 0.0;
-  for (int s = tid; s < A.nseg; s += kRedThreads) c += A.slab_cost[s];
+  if (A.nseg > 0) {  // lane-strided, in order, every load of a batch in flight (sum_rows)
+    for (int s = tid; s < A.nseg; s += 4 * kRedThreads) {
+      double v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = A.slab_cost[min(s + i * kRedThreads, A.nseg - 1)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) c += s + i * kRedThreads < A.nseg ? v[i] : 0.0;
+    }
+  }
   if (A.status && *A.status) return;
   __shared__ double cpart[kRedThreads];
   cpart[tid] = c;
@@ -1392,6 +1362,11 @@ class BAEngine {
         }
       upload(d_red_meta_, meta, st);
       upload(d_red_out_, out, st);
+      // K2 fused into the banded K3's launch when every workgroup of it fits one round at
+      // one per CU (the solver's LDS): cfg3's 356 blocks make 178 reducers + the solver
+      fuse_ok_ = VO_BA_FUSE && band_on_ && band_fused_workgroups(nprof) + 1 <= kFusedMaxWorkgroups;
+      d_red_count_.reserve(256);
+      VO_HIP_CHECK(hipMemsetAsync(d_red_count_.ptr, 0, 256, st));
       d_zero_.reserve(512);  // zero block (masked prefetches)
       VO_HIP_CHECK(hipMemsetAsync(d_zero_.ptr, 0, 512, st));
     }
@@ -1441,6 +1416,7 @@ class BAEngine {
     VO_HIP_CHECK(hipEventRecord(h_state_ev_, st));
     h_state_busy_ = true;
     VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
+    if (fuse_ok_) VO_HIP_CHECK(hipMemsetAsync(d_red_count_.ptr, 0, 256, st));  // after a timed-out solve
     cur_ = 0;
     pending_ = false;
     have_state_ = true;
@@ -1502,8 +1478,11 @@ class BAEngine {
     enqueue_lin(pending_ ? (kBacksub | kAccum) : kAccum);
     enqueue_reduce();
     std::vector<double> sys(sys_len_);
-    VO_HIP_CHECK(hipMemcpyAsync(sys.data(), d_sys_.ptr, sys_len_ * 8, hipMemcpyDeviceToHost, st));
+    // the reduced system as K2 wrote it: before the solve (the profile solver factors it in
+    // place), or after the fused K2 + K3 launch (the banded K3 only reads it)
+    if (!fused()) VO_HIP_CHECK(hipMemcpyAsync(sys.data(), d_sys_.ptr, sys_len_ * 8, hipMemcpyDeviceToHost, st));
     enqueue_solve(1);
+    if (fused()) VO_HIP_CHECK(hipMemcpyAsync(sys.data(), d_sys_.ptr, sys_len_ * 8, hipMemcpyDeviceToHost, st));
     std::vector<double> dc(6ull * F);
     int status = 0;
     if (F) VO_HIP_CHECK(hipMemcpyAsync(dc.data(), d_dc_.ptr, dc.size() * 8, hipMemcpyDeviceToHost, st));
@@ -1619,7 +1598,10 @@ class BAEngine {
     VO_HIP_CHECK(hipGetLastError());
   }
 
-  void enqueue_reduce() {
+  // K2 runs inside the banded K3's launch (one rank: no all-reduce between them)
+  bool fused() const { return fuse_ok_ && !(ctx_->comm && ctx_->comm->nranks > 1); }
+
+  ReduceArgs reduce_args() const {
     const BAPlan& P = plan_;
     ReduceArgs R;
     R.nprof = P.n_prof_blocks();
@@ -1636,6 +1618,12 @@ class BAEngine {
     R.sys = d_sys_.as<double>();
     R.cost_off = cost_off_;
     R.status = d_status_.as<int>();
+    return R;
+  }
+
+  void enqueue_reduce() {
+    if (fused()) return;  // K3's reducer workgroups do it
+    const ReduceArgs R = reduce_args();
     ctx_->prof.begin(ctx_->stream, kKBaReduce);
     hipLaunchKernelGGL(ba_reduce_kernel, dim3(R.nprof + 1), dim3(kRedThreads), 0, ctx_->stream, R);
     ctx_->prof.end(ctx_->stream);
@@ -1670,6 +1658,9 @@ class BAEngine {
       B.pose_next = A.pose_next;
       B.status = A.status;
       B.stamps = nullptr;
+      B.nred = fused() ? band_fused_workgroups(A.nprof) : 0;
+      B.red_count = d_red_count_.as<unsigned>();
+      B.red = reduce_args();
       if (stamps_on_) {
         d_stamps3_.reserve(8 * kBandStamps * 8);
         B.stamps = d_stamps3_.as<unsigned long long>();
@@ -1775,9 +1766,11 @@ class BAEngine {
   SolveLds solve_layout_{};
   BandSplit band_{};
   bool band_on_ = false;
+  bool fuse_ok_ = false;  // K2 fused into K3's launch (see fused())
+  static constexpr int kFusedMaxWorkgroups = 256;  // one round at one workgroup per CU (MI355X)
   BandLds band_lds_;
   BandTables band_tab_;
-  DevBuf d_fac_, d_zero_, d_band_tab_, d_red_meta_, d_red_out_;
+  DevBuf d_fac_, d_zero_, d_band_tab_, d_red_meta_, d_red_out_, d_red_count_;
   std::vector<int32_t> red_dst_, red_rdst_;  // K2 output offsets (host copies for gn_step)
   long cost_off_ = 0;
   DevBuf d_solve_tab_;

@@ -6,6 +6,8 @@
 #include <cstddef>
 #include <vector>
 
+#include "ba_reduce.h"
+
 namespace vo {
 
 // Widest block bandwidth (max_i i - first[i]) the banded solver takes: one chain wave
@@ -61,7 +63,18 @@ struct BandArgs {
   double* pose_next;
   int* status;
   unsigned long long* stamps;  // diagnostic build: 4 waves x kBandStamps phase cycles
+  // Fused K2 (nred > 0, one rank): workgroups 1..nred of the launch reduce the slabs into sys
+  // (two profile blocks each, the cost in the item after the last block: K2's sums bit for
+  // bit), store them write-through (sc1) and count themselves in red_count; workgroup 0, the
+  // solver, reads sys only after red_count reached nred and its agent-scope acquire, and
+  // takes nred back off the counter (zero between launches).
+  int nred;
+  unsigned* red_count;
+  ReduceArgs red;
 };
+// Reducer workgroups of a fused launch: items (profile blocks + the cost) per workgroup.
+constexpr int kBandRedItems = 2;
+inline int band_fused_workgroups(int nprof) { return (nprof + 1 + kBandRedItems - 1) / kBandRedItems; }
 
 // Doubles per ring slot / factor record: (w + 1) blocks of 36, the rhs row (6) and the
 // reciprocal diagonal (6).

@@ -201,6 +201,104 @@ __device__ __forceinline__ void band_barrier() { asm volatile("s_waitcnt lgkmcnt
   } while (0)
 #endif
 
+// ---- fused K2: the reducer workgroups (BandArgs::nred).  Each 256-thread half of a
+// workgroup runs ba_reduce_kernel's work for one item (a profile block, or the cost after
+// the last block) with K2's partition and order, so sys gets the same bits as from K2.  The
+// outputs go write-through (sc1: the solver reads them on another CU, maybe another XCD),
+// every storing wave drains them, and one lane counts the workgroup in red_count after the
+// workgroup barrier (MI355X_MICROARCH.md, hand-off rows: sc1 stores + vmcnt(0) + barrier +
+// one agent-scope atomic add; the solver polls relaxed, then one agent-scope acquire).
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+constexpr int kRedScr = kRedSParts * 36 + kRedBParts * 6 + kRedThreads;  // LDS doubles per half
+
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void band_reduce_wg(const BandArgs& B, int r, double* scr) {
+  static_assert(kRedThreads * kBandRedItems == 512, "two K2 items per 512-thread workgroup");
+  const ReduceArgs& A = B.red;
+  const int tid = threadIdx.x, h = tid / kRedThreads, t = tid % kRedThreads;
+  const int blk = kBandRedItems * r + h;
+  double* part = scr + h * kRedScr;
+  double* partb = part + kRedSParts * 36;
+  double* cpart = partb + kRedBParts * 6;
+  const bool isblk = blk < A.nprof, iscost = blk == A.nprof;
+  int4 m = make_int4(0, 0, -1, 0);
+  int2 o = make_int2(0, 0);
+  double ps = 0.0, pb = 0.0, c = 0.0;
+  if (isblk) {
+    m = A.meta[blk];
+    o = A.out[blk];
+    if (t < kRedSParts * 36) ps = sum_rows<36>(A.slab, m.x, m.y, t / 36, kRedSParts, t % 36);
+    if (m.z >= 0 && t < kRedBParts * 6) pb = sum_rows<6>(A.slab_b, m.z, m.w, t / 6, kRedBParts, t % 6);
+  } else if (iscost && A.nseg > 0) {
+    for (int s = t; s < A.nseg; s += 4 * kRedThreads) {
+      double v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = A.slab_cost[min(s + i * kRedThreads, A.nseg - 1)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) c += s + i * kRedThreads < A.nseg ? v[i] : 0.0;
+    }
+  }
+  const bool failed = A.status && *A.status;  // a failed earlier step: nothing is written
+  if (isblk) {
+    if (t < kRedSParts * 36) part[t] = ps;
+    if (t < kRedBParts * 6) partb[t] = pb;
+  } else if (iscost) {
+    cpart[t] = c;
+  }
+  __syncthreads();
+  if (isblk && !failed) {
+    const bool diag = m.z >= 0;
+    if (t < 36) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < kRedSParts; ++q) acc += part[36 * q + t];
+      if (diag && t % 7 == 0) acc += A.lambda;
+      st_sc1(A.sys + (o.x & ~kRedTranspose) + ((o.x & kRedTranspose) ? 6 * (t % 6) + t / 6 : t), acc);
+    } else if (diag && t >= 64 && t < 70) {
+      const int e = t - 64;
+      double acc = 0.0;
+      for (int q = 0; q < kRedBParts; ++q) acc += partb[6 * q + e];
+      st_sc1(A.sys + o.y + e, acc);
+    }
+  }
+  for (int mm = kRedThreads / 2; mm > 0; mm >>= 1) {  // the cost: K2's tree (barriers uniform)
+    if (iscost && t < mm) cpart[t] += cpart[t + mm];
+    __syncthreads();
+  }
+  if (iscost && t == 0 && !failed) st_sc1(A.sys + A.cost_off, cpart[0]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores done
+  __syncthreads();
+  if (tid == 0) __hip_atomic_fetch_add((gu32*)B.red_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Solver side of the fused launch: one lane polls red_count (relaxed, s_sleep between reads,
+// bounded), takes nred off it, then the agent-scope acquire; every wave waits at the barrier
+// for it.  Returns false on a timeout (then sys is not read: the solve reports "failed").
+__device__ __forceinline__ bool band_wait_reduced(const BandArgs& A, int tid, int* s_flag) {
+  if (tid == 0) {
+    int ok = 1;
+    unsigned spins = 0;
+    while (__hip_atomic_load((gu32*)A.red_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)A.nred) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 22)) {  // ~0.1 s: a reducer never arrived
+        ok = 0;
+        break;
+      }
+    }
+    if (ok) __hip_atomic_fetch_sub((gu32*)A.red_count, (unsigned)A.nred, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *s_flag = ok;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 // Loads below never feed a select or branch before their first real use: a value that
 // must be zero is loaded from the zero block (A.zero) instead, so the waitcnt pass can
 // leave every prefetch in flight.
@@ -214,13 +312,18 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
 #endif
   // wave (so role and side) is wave-uniform: readfirstlane lets the compiler branch on SGPRs
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if (A.nred > 0 && blockIdx.x > 0) {  // fused K2: a reducer workgroup (uniform branch)
+    band_reduce_wg(A, blockIdx.x - 1, dyn);
+    return;
+  }
+  __shared__ int s_red;
   // CS: doubles per column (K2 layout, factor record; full mode: SS == CS); SS per slot (ring mode: whole 1 KiB
   // pieces), RC slots per side (band_lds_layout)
   const int F = A.F, w = A.w, R = w + 1, CS = 36 * R + 12, CSP = (CS + 127) / 128 * 128;
   const int m = A.m, nb = A.nb, sp = A.s;
   const int ncolT = m + sp, ncolB = nb + sp;
   const int SS = kFull ? CS : CSP, RC = kFull ? max(ncolT, ncolB) : w + 4, SPAD = kFull ? 128 : 0;
-  const bool prior_fail = A.status && *A.status;
+  const bool prior_status = A.status && *A.status;
   double* ringT = dyn;
   double* ringB = ringT + RC * SS + SPAD;
   double* zs = ringB + RC * SS + SPAD;  // back substitution: z (6F)
@@ -241,13 +344,17 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
 
   if (tid < 40) s_zero[tid] = 0.0;
   if (tid < 40) dyn[ZOFF + tid] = 0.0;
+  // the poses for the tail's update, staged now (their load latency under the prologue's,
+  // or under the wait for the fused launch's reducers)
+  for (int e = tid; e < 12 * A.n_poses; e += kBandThreads) pose_l[e] = A.pose_cur[e];
+  // fused K2: sys is read only after every reducer workgroup has published it; a timeout
+  // fails the solve (status) without reading it
+  const bool reduced = A.nred > 0 ? band_wait_reduced(A, tid, &s_red) : true;
+  const bool prior_fail = prior_status || !reduced;
   if (tid == 0) {
     s_fail = prior_fail ? 1 : 0;
-    if (A.cost_out) *A.cost_out = A.sys[A.cost_off];
+    if (A.cost_out && reduced) *A.cost_out = A.sys[A.cost_off];
   }
-
-  // the poses for the tail's update, staged now (their load latency under the prologue's)
-  for (int e = tid; e < 12 * A.n_poses; e += kBandThreads) pose_l[e] = A.pose_cur[e];
   // Ring prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every
   // 16-byte load in flight, then the stores.  The loads do not wait for the status word
   // (one global round trip less on the launch's path); a failed earlier solve only skips
@@ -877,7 +984,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       se3_exp_apply(d, T, out);
     }
   }
-  if (tid == 0 && failed && !prior_fail) *A.status = A.iter_tag;
+  if (tid == 0 && failed && !prior_status) *A.status = A.iter_tag;
   BST(14);
 #if VO_BA_STAMPS
   if (lane == 0 && A.stamps)
@@ -887,16 +994,24 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
 
 }  // namespace
 
+// A fused launch's reducer workgroups need their K2 scratch (two halves) even when the
+// solver's own layout is smaller (narrow windows).
+static size_t band_launch_lds(const BandLds& L, bool fused) {
+  return fused ? std::max(L.bytes, (size_t)kBandRedItems * kRedScr * sizeof(double)) : L.bytes;
+}
+
 void band_set_attributes(const BandLds& L) {
   const void* f = L.full ? (const void*)ba_band_kernel<true> : (const void*)ba_band_kernel<false>;
-  VO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.bytes));
+  VO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)band_launch_lds(L, true)));
 }
 
 void launch_band_solve(const BandArgs& A, const BandLds& L, hipStream_t st) {
+  const dim3 grid(1 + std::max(A.nred, 0));  // the solver first, then the fused K2's reducers
+  const size_t lds = band_launch_lds(L, A.nred > 0);
   if (L.full)
-    hipLaunchKernelGGL(ba_band_kernel<true>, dim3(1), dim3(kBandThreads), L.bytes, st, A);
+    hipLaunchKernelGGL(ba_band_kernel<true>, grid, dim3(kBandThreads), lds, st, A);
   else
-    hipLaunchKernelGGL(ba_band_kernel<false>, dim3(1), dim3(kBandThreads), L.bytes, st, A);
+    hipLaunchKernelGGL(ba_band_kernel<false>, grid, dim3(kBandThreads), lds, st, A);
 }
 
 }  // namespace vo

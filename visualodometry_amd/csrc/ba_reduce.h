@@ -1,0 +1,61 @@
+// K2's slab reduction (shared by ba_reduce_kernel in ba.hip and the reducer workgroups of the
+// fused K2 + K3 launch in ba_band.hip): arguments, fixed-order row sums, partition constants.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace vo {
+
+// K2: fixed-order reduction of the slabs into [S profile | b | cost].
+struct ReduceArgs {
+  int nprof, F, nseg;
+  double lambda;
+  // per profile block, host-built (BAEngine::setup) so that one load level gives every
+  // address: slab rows [x, y); on a diagonal block its camera's rhs slab entries [z, w)
+  // (z < 0 otherwise)
+  const int4* meta;
+  // per profile block: output offset of its 36 values (| kRedTranspose), of its rhs (diagonal)
+  const int2* out;
+  const double* slab;
+  const double* slab_b;
+  const double* slab_cost;
+  double* sys;         // output: profile [S | b | cost] or the banded K3's column layout
+  long cost_off;       // output offset of the cost
+  const int* status;
+};
+constexpr int kRedTranspose = 1 << 30;  // dst flag: store the block transposed
+
+// Sums slab rows k0 + part + j*stride (entry e of each, rows of W doubles), j = 0, 1, ...,
+// in fixed order.  K1 wrote each block's window slots to consecutive rows in prof_src order,
+// so this is the former gather, bit for bit.  Rows go in batches of kRedBatch loads, all in
+// flight at once: the loads are unconditional (index clamped into [k0, k1)) and a row past
+// the end adds +0.0, which leaves the sum unchanged bit for bit (acc starts at +0.0, so it is
+// never -0.0).  A serial tail loop here cost one global round trip per leftover row: a
+// block of 40 rows took five dependent round trips in its threads.
+#ifndef VO_RED_BATCH
+#define VO_RED_BATCH 16
+#endif
+constexpr int kRedBatch = VO_RED_BATCH;
+template <int W>
+__device__ __forceinline__ double sum_rows(const double* __restrict__ slab, int k0, int k1, int part,
+                                           int stride, int e) {
+  double acc = 0.0;
+  if (k1 <= k0) return acc;  // no rows (uniform per block)
+  for (int k = k0 + part; k < k1; k += kRedBatch * stride) {
+    double v[kRedBatch];
+#pragma unroll
+    for (int i = 0; i < kRedBatch; ++i) v[i] = slab[(long)W * min(k + i * stride, k1 - 1) + e];
+#pragma unroll
+    for (int i = 0; i < kRedBatch; ++i) acc += k + i * stride < k1 ? v[i] : 0.0;
+  }
+  return acc;
+}
+
+#ifndef VO_RED_THREADS
+#define VO_RED_THREADS 256
+#endif
+constexpr int kRedThreads = VO_RED_THREADS;
+constexpr int kRedSParts = kRedThreads / 36;  // partial sums per S block entry
+constexpr int kRedBParts = kRedThreads / 6;   // partial sums per rhs entry
+
+}  // namespace vo
