@@ -15,6 +15,12 @@ extern "C" {
  * (RCCL refuses two ranks on one device).  Not a transport for production. */
 int vo_comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128]);
 
+/* Test/tool switch: on != 0 keeps the BA's slab reduction (K2) a launch of its own on this
+ * context, as on more than one rank (where the all-reduce sits between K2 and the solve);
+ * by default one rank runs K2 inside the banded solve's launch.  Results are identical
+ * either way (same sums).  tools/shard_projection.py times the multi-rank layout with it. */
+int vo_ba_split_reduce(vo_ctx* ctx, int on);
+
 #ifdef __cplusplus
 }
 #endif

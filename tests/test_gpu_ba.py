@@ -95,6 +95,32 @@ def test_deterministic_bitwise(ctx):
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "tiny"])
+def test_fused_reduce_equals_split_launches(ctx, cfg):
+    """One rank runs K2 inside the banded K3's launch (reducer workgroups hand the reduced
+    system to the solver workgroup); the split layout of N > 1 ranks launches K2 on its own.
+    Same sums in the same order: the runs agree bit for bit, and the fused one is the default."""
+    p = make_ba_problem(4, 160, 35, max_track=2) if cfg == "tiny" else make_ba_config(cfg)
+    out = []
+    for split in (False, True):
+        _lib.ba_split_reduce(ctx, split)
+        try:
+            _lib.profile_enable(ctx, True)
+            s = _session(p, ctx)
+            rc, costs = s.run(3)
+            assert rc == _lib.VO_OK
+            P, X = s.get_state()
+            prof = _lib.profile_read(ctx)
+            _lib.profile_enable(ctx, False)
+        finally:
+            _lib.ba_split_reduce(ctx, False)
+        assert ("ba_reduce" in prof) == split
+        assert s.plan_stats()["band_solver"] == 1
+        out.append((costs, P, X))
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_run_in_pieces_equals_one_run(ctx):
     p = make_ba_config("cfg2")
     s1 = _session(p, ctx)

@@ -25,6 +25,9 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg4"
 ITERS = 20
 p = make_ba_config(cfg)
 ctx = _lib.Context(0)
+# K2 as a launch of its own, as on N > 1 ranks (the all-reduce sits between K2 and K3); one
+# rank runs K2 inside K3's launch: "fused_1rank_us" below
+_lib.ba_split_reduce(ctx, True)
 
 
 def timed(ptr, cam, uv, pts):
@@ -41,7 +44,10 @@ def timed(ptr, cam, uv, pts):
 
 
 full, st = timed(p.point_ptr, p.obs_cam, p.obs_uv, p.points)
-out = {"config": cfg, "full_us": full, "reduced_system_bytes": int(st["profile_blocks"] * 288 + 48 * (p.n_poses - p.n_fixed) + 8),
+_lib.ba_split_reduce(ctx, False)
+fused, _ = timed(p.point_ptr, p.obs_cam, p.obs_uv, p.points)
+_lib.ba_split_reduce(ctx, True)
+out = {"config": cfg, "full_us": full, "fused_1rank_us": fused, "reduced_system_bytes": int(st["profile_blocks"] * 288 + 48 * (p.n_poses - p.n_fixed) + 8),
        "ranks": {}}
 for n in (1, 2, 4, 8):
     k1 = k2 = 0.0

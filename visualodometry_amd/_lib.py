@@ -15,7 +15,7 @@ from pathlib import Path
 # VO_LIB_PATH selects an alternative build of the same library (tuning experiments)
 LIB_PATH = Path(os.environ.get("VO_LIB_PATH") or Path(__file__).resolve().parent / "lib" / "libvo_hip.so")
 HEADER = Path(__file__).resolve().parents[1] / "include" / "vo_hip.h"
-# test-only entry points (the loopback communicator), outside the product header
+# test-only entry points (the loopback communicator, the split-reduce switch), outside the product header
 TEST_HEADER = HEADER.with_name("vo_hip_testing.h")
 
 VO_OK = 0
@@ -104,6 +104,7 @@ SIGNATURES = {
     "vo_sift_detect_and_compute_batch_async": (_I, [_P, _P, _I, _I, _I, _I, _D, _D, _D, _I, _I, _P, _P, _P]),
     "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
+    "vo_ba_split_reduce": (_I, [_P, _I]),
 }
 
 _lib = None
@@ -258,6 +259,12 @@ def comm_init_loopback(ctx: "Context", nranks: int, rank: int, group: bytes) -> 
     (contexts of this process, one host thread each); see vo_comm_init_loopback."""
     gid = C.create_string_buffer(group[:128].ljust(128, b"\0"), 128)
     check(ctx.lib.vo_comm_init_loopback(ctx.handle, nranks, rank, gid), "vo_comm_init_loopback")
+
+
+def ba_split_reduce(ctx: "Context", on: bool = True) -> None:
+    """Test/tool switch: keep the BA's slab reduction a launch of its own on this context (the
+    multi-rank layout); see vo_ba_split_reduce."""
+    check(ctx.lib.vo_ba_split_reduce(ctx.handle, int(bool(on))), "vo_ba_split_reduce")
 
 
 def ptr(a, ctype):

@@ -714,6 +714,13 @@ int vo_comm_init(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
 }
 
 // test-only (include/vo_hip_testing.h)
+int vo_ba_split_reduce(vo_ctx* ctx, int on) {
+  return guarded([&] {
+    VO_REQUIRE(ctx != nullptr, VO_ERR_ARG, "vo_ba_split_reduce: null context");
+    ctx->ba_split_reduce = on != 0;
+  });
+}
+
 int vo_comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
   return guarded([&] {
     vo::bind(ctx);

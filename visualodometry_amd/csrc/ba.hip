@@ -1599,7 +1599,7 @@ class BAEngine {
   }
 
   // K2 runs inside the banded K3's launch (one rank: no all-reduce between them)
-  bool fused() const { return fuse_ok_ && !(ctx_->comm && ctx_->comm->nranks > 1); }
+  bool fused() const { return fuse_ok_ && !ctx_->ba_split_reduce && !(ctx_->comm && ctx_->comm->nranks > 1); }
 
   ReduceArgs reduce_args() const {
     const BAPlan& P = plan_;

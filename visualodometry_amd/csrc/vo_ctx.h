@@ -91,6 +91,7 @@ struct vo_ctx {
   vo::Profiler prof;
   std::unique_ptr<vo::BAEngine> ba;
   std::unique_ptr<vo::Comm> comm;
+  bool ba_split_reduce = false;  // test/tool switch (vo_ba_split_reduce): K2 never fused into K3
   vo_ctx();
   ~vo_ctx();
 };
