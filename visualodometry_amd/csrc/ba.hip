@@ -1363,8 +1363,9 @@ class BAEngine {
       upload(d_red_meta_, meta, st);
       upload(d_red_out_, out, st);
       // K2 fused into the banded K3's launch when every workgroup of it fits one round at
-      // one per CU (the solver's LDS): cfg3's 356 blocks make 178 reducers + the solver
-      fuse_ok_ = VO_BA_FUSE && band_on_ && band_fused_workgroups(nprof) + 1 <= kFusedMaxWorkgroups;
+      // one per CU (the solver's LDS): cfg3's 356 blocks make 178 reducers + the solver on
+      // MI355X's 256 CUs (fewer CUs, e.g. a partitioned device: K2 stays a launch of its own)
+      fuse_ok_ = VO_BA_FUSE && band_on_ && band_fused_workgroups(nprof) + 1 <= ctx_->num_cus;
       d_red_count_.reserve(256);
       VO_HIP_CHECK(hipMemsetAsync(d_red_count_.ptr, 0, 256, st));
       d_zero_.reserve(512);  // zero block (masked prefetches)
@@ -1767,7 +1768,6 @@ class BAEngine {
   BandSplit band_{};
   bool band_on_ = false;
   bool fuse_ok_ = false;  // K2 fused into K3's launch (see fused())
-  static constexpr int kFusedMaxWorkgroups = 256;  // one round at one workgroup per CU (MI355X)
   BandLds band_lds_;
   BandTables band_tab_;
   DevBuf d_fac_, d_zero_, d_band_tab_, d_red_meta_, d_red_out_, d_red_count_;
