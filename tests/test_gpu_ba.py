@@ -185,6 +185,30 @@ def test_not_spd_reported(ctx):
     np.testing.assert_array_equal(X, p.points)
 
 
+def test_fused_reduce_after_failed_solve(ctx):
+    """A failed (not SPD) fused launch still counts every reducer and gives the count back:
+    the next window on the same context runs the fused launch to the split launches' bits."""
+    p = make_ba_problem(6, 100, 41)
+    cam = p.obs_cam.copy()
+    cam[cam == 5] = 4
+    bad = BASession(p.K, p.point_ptr, cam, p.obs_uv, p.n_poses, 2, 0.0, ctx)
+    bad.set_state(p.poses_cw, p.points)
+    assert bad.run(3)[0] == _lib.VO_ERR_NOT_SPD
+    q = make_ba_config("cfg2")
+    out = []
+    for split in (False, True):
+        _lib.ba_split_reduce(ctx, split)
+        try:
+            s = _session(q, ctx)
+            rc, costs = s.run(2)
+            assert rc == _lib.VO_OK
+            out.append((costs,) + tuple(s.get_state()))
+        finally:
+            _lib.ba_split_reduce(ctx, False)
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+
+
 def _pose_round(P):
     from visualodometry_amd.ba import poses_to_rt, rt_to_poses
 
