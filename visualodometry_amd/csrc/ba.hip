@@ -1455,6 +1455,7 @@ class BAEngine {
     VO_HIP_CHECK(hipMemcpyAsync(costs.data(), d_cost_.ptr, costs.size() * 8, hipMemcpyDeviceToHost, st));
     VO_HIP_CHECK(hipMemcpyAsync(&status, d_status_.ptr, sizeof(int), hipMemcpyDeviceToHost, st));
     VO_HIP_CHECK(hipStreamSynchronize(st));
+    const bool timed_out = clear_timeout(status);
     if (status) {
       // iteration `status` (1-based) failed: the state is its linearisation point
       for (int k = status; k <= iters; ++k) costs[k] = NAN;
@@ -1462,12 +1463,22 @@ class BAEngine {
       VO_HIP_CHECK(hipStreamSynchronize(st));
     }
     if (cost_out) std::copy(costs.begin(), costs.end(), cost_out);
+    VO_REQUIRE(!timed_out, VO_ERR_HIP, "vo_ba_run: fused reduction timed out at iteration %d (a reducer workgroup never arrived)", status - 1);
     if (status) {
       set_error("vo_ba_run: reduced camera system not positive definite at iteration %d",
                 status - 1);
       return VO_ERR_NOT_SPD;
     }
     return VO_OK;
+  }
+
+  // A fused launch whose solver timed out (kBandStatusTimeout): strip the flag from the status
+  // word's iteration and re-zero the reducer counter (the late reducers have arrived by now).
+  bool clear_timeout(int& status) {
+    if (!(status & kBandStatusTimeout)) return false;
+    status &= ~kBandStatusTimeout;
+    VO_HIP_CHECK(hipMemsetAsync(d_red_count_.ptr, 0, 256, ctx_->stream));
+    return true;
   }
 
   int gn_step(double* S_out, double* b_out, double* dc_out, double* cost_out) {
@@ -1511,9 +1522,11 @@ class BAEngine {
       for (int f = 0; f < F; ++f) std::copy(sys.begin() + red_rdst_[f], sys.begin() + red_rdst_[f] + 6, b_out + 6 * f);
     if (dc_out) std::copy(dc.begin(), dc.end(), dc_out);
     if (cost_out) *cost_out = sys[cost_off_];
+    const bool timed_out = clear_timeout(status);
     if (status) {
       VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
       VO_HIP_CHECK(hipStreamSynchronize(st));
+      VO_REQUIRE(!timed_out, VO_ERR_HIP, "vo_ba_gn_step: fused reduction timed out (a reducer workgroup never arrived)");
       set_error("vo_ba_gn_step: reduced camera system not positive definite");
       return VO_ERR_NOT_SPD;
     }

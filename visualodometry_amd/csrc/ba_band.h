@@ -72,6 +72,9 @@ struct BandArgs {
   unsigned* red_count;
   ReduceArgs red;
 };
+// Status word flag: the fused launch's solver gave up waiting for its reducers (the low bits
+// are the iteration, as for a failed factorisation).
+constexpr int kBandStatusTimeout = 1 << 30;
 // Reducer workgroups of a fused launch: items (profile blocks + the cost) per workgroup.
 constexpr int kBandRedItems = 2;
 inline int band_fused_workgroups(int nprof) { return (nprof + 1 + kBandRedItems - 1) / kBandRedItems; }

@@ -285,7 +285,7 @@ __device__ __forceinline__ bool band_wait_reduced(const BandArgs& A, int tid, in
     unsigned spins = 0;
     while (__hip_atomic_load((gu32*)A.red_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)A.nred) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 22)) {  // ~0.1 s: a reducer never arrived
+      if (++spins > (1u << 22)) {  // seconds (a reducer never arrived): fail, do not hang
         ok = 0;
         break;
       }
@@ -984,7 +984,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       se3_exp_apply(d, T, out);
     }
   }
-  if (tid == 0 && failed && !prior_status) *A.status = A.iter_tag;
+  if (tid == 0 && failed && !prior_status) *A.status = reduced ? A.iter_tag : A.iter_tag | kBandStatusTimeout;
   BST(14);
 #if VO_BA_STAMPS
   if (lane == 0 && A.stamps)
