@@ -52,6 +52,55 @@ def ba_kernel_bytes(kind: str, n_poses: int, n_points: int, n_obs: int, n_free: 
     return 0.0
 
 
+# Source files whose code a kernel group's PMC traffic depends on: a traffic file records their
+# digest (tools/pmc_traffic.py), and bench.py attaches its figures only to a run of the same
+# sources, configuration and kernel set (a stale file would describe another build).
+TRAFFIC_SOURCES = {
+    "ba": ["ba.hip", "ba_band.hip", "ba_band.h", "ba_math.h", "ba_reduce.h", "ba_plan.cpp", "ba_plan.h",
+           "vo_common.h", "vo_ctx.h", "Makefile"],
+    "match": ["match.hip", "match_bf16.hip", "match_short.h", "vo_common.h", "vo_ctx.h", "Makefile"],
+}
+
+
+def source_digest(group: str) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    src = ROOT / "visualodometry_amd" / "csrc"
+    for f in TRAFFIC_SOURCES[group]:
+        h.update(f.encode())
+        h.update((src / f).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def traffic_for(path, config: str, lam: float, world: int, group: str, kernels):
+    """PMC traffic per launch for `kernels` (short names) from a tools/pmc_traffic.py file, or
+    (None, reason) when the file was counted on another build (source digest), configuration,
+    damping, rank count or kernel set than the timed run."""
+    if not path or not Path(path).exists():
+        return {}, f"no traffic file {path}"
+    t = json.loads(Path(path).read_text())
+    key = t.get("_key")
+    if not key:
+        return {}, f"{path}: no build/config key (pre-r04 format)"
+    want = {"config": config, "lam": lam, "gpus": world, "digest": source_digest(group)}
+    got = {"config": key.get("config"), "lam": key.get("lam"), "gpus": key.get("gpus"),
+           "digest": key.get("digest", {}).get(group)}
+    if got != want:
+        return {}, f"{path}: counted on {got}, timed run is {want}"
+    # kernels launched on every counted step (a cost-only K2 of the parity guard launches once)
+    seen = {k for k, n in key.get("launches", {}).items() if n >= 5}
+    if group == "ba":
+        timed = {k for k in kernels if k.startswith("ba_")}
+        counted = {k for k in seen if k.startswith("ba_")}
+        if timed != counted:
+            return {}, f"{path}: counted kernel set {sorted(counted)} != timed {sorted(timed)}"
+    missing = [k for k in kernels if k not in seen]
+    if missing:
+        return {}, f"{path}: kernels {missing} not in the counted run ({sorted(seen)})"
+    return {k: t[k] for k in kernels if k in t}, None
+
+
 def host_cores():
     """Host cores this process may use: its CPU affinity, capped by a cgroup CPU quota
     (on the GPU box the job's share of a larger machine).  Returns (threads, note)."""
@@ -89,8 +138,7 @@ def cpu_baseline_ba(p, lam: float, budget_s: float = 3.0):
                       f"window: {n} GN iterations in {dt:.2f} s; {note}"}
 
 
-def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: int = 3, traffic_all=None):
-    traffic_all = traffic_all or {}
+def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: int = 3, traffic_path=None):
     from visualodometry_amd import _lib, matcher
     from visualodometry_amd.synthetic import sift_like_pair
 
@@ -130,6 +178,7 @@ def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: 
     avg_s = ms_i8 / max(cnt_i8, 1) / 1e3
     tops = 2.0 * 128 * batch * n * n / avg_s / 1e12 if avg_s > 0 else 0.0
     kern = {k: round(v[0] / v[1] * 1e3, 2) for k, v in prof.items()}
+    traffic, why = traffic_for(traffic_path, "cfg3", 1.0, 1, "match", ["match_i8"])
     res = {
         "metric": "descriptor-match Mpairs/sec",
         "value": pairs_total / dt / 1e6,
@@ -139,7 +188,8 @@ def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: 
                                f"{batch} frame pairs per call, knn2 + ratio 0.75", "calls": calls},
         "kernel_us": kern,
         "roofline": {"bound": "mfma", "kernel": "match_i8", "achieved": tops, "peak": I8_PEAK_TOPS,
-                     "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS, "traffic": traffic_all.get("match_i8"),
+                     "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS, "traffic": traffic.get("match_i8"),
+                     "traffic_note": why,
                      "note": "int8 ops (2*128 per pair) per match_i8 launch / its HIP-event duration"},
     }
     # CPU baseline: C oracle on a bounded sample of query rows
@@ -157,7 +207,7 @@ def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: 
 
 
 def bench_matcher_float(ctx, batch: int = 16, n: int = 2048, dim: int = 256, calls: int = 10, warmup: int = 2,
-                        traffic_all=None):
+                        traffic_path=None):
     """BASELINE config 5's matcher: SuperPoint-like L2-normalised float32 descriptors (not
     integer-valued: the bf16 MFMA shortlist + exact fp32 re-rank, bit-exact with the
     k-ordered fmaf chain), 2048 x 2048 x 256 per frame pair, knn2 + ratio
@@ -193,8 +243,10 @@ def bench_matcher_float(ctx, batch: int = 16, n: int = 2048, dim: int = 256, cal
     kern = {k: round(v[0] / v[1] * 1e3, 2) for k, v in prof.items()}
     ms_f, cnt_f = prof.get("match_f32", (0.0, 1))  # both bf16 MFMA sweeps of a call
     avg_s = ms_f / max(cnt_f, 1) / 1e3
-    # two sweeps of 2 flops per (pair, k) on the matrix cores
-    tfl = 2.0 * 2.0 * dim * batch * n * n / avg_s / 1e12 if avg_s > 0 else 0.0
+    # algorithmic flops: ONE contraction of 2 flops per (pair, k); the second sweep recomputes
+    # the first's products (it marks the shortlist), so it is time, not credited work
+    tfl = 2.0 * dim * batch * n * n / avg_s / 1e12 if avg_s > 0 else 0.0
+    traffic, why = traffic_for(traffic_path, "cfg3", 1.0, 1, "match", ["match_f32"])
     res = {
         "metric": "descriptor-match Mpairs/sec (float path)",
         "value": batch * n * n * calls / dt / 1e6,
@@ -205,9 +257,12 @@ def bench_matcher_float(ctx, batch: int = 16, n: int = 2048, dim: int = 256, cal
         "kernel_us": kern,
         "roofline": {"bound": "mfma", "kernel": "match_f32 (fsweep<1> + fsweep<2>, bf16 MFMA)", "achieved": tfl,
                      "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tfl / BF16_MFMA_PEAK_TFLOPS,
-                     "traffic": (traffic_all or {}).get("match_f32"),
-                     "note": "2 sweeps x 2 flops per pair and dimension / their summed HIP-event duration; the "
-                             "exact fp32 re-rank of the shortlisted candidates is kernel_us.match_rerank"},
+                     "traffic": traffic.get("match_f32"), "traffic_note": why,
+                     "issued_tflops": 2.0 * tfl,
+                     "note": "algorithmic flops (2 per pair and dimension, one contraction) / the summed HIP-event "
+                             "duration of both sweeps (fsweep<2> recomputes fsweep<1>'s products: issued_tflops "
+                             "counts both); the exact fp32 re-rank of the shortlisted candidates is "
+                             "kernel_us.match_rerank"},
     }
     rows = 256
     t0 = time.perf_counter()
@@ -451,9 +506,11 @@ def main() -> int:
     ap.add_argument("--lam", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-matcher", action="store_true")
-    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "traffic.json"),
-                    help="per-kernel HBM bytes per launch from the committed rocprofv3 --pmc passes "
-                         "(tools/pmc_traffic.py); the timed run itself is never profiled")
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-kernel HBM bytes per launch from rocprofv3 --pmc passes of this build and config "
+                         "(tools/pmc_traffic.py; default profiles/traffic_<config>.json); attached only when its "
+                         "key (source digest, config, lambda, ranks, kernel set) matches the timed run; the timed "
+                         "run itself is never profiled")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -538,10 +595,9 @@ def main() -> int:
         nbytes += ba_kernel_bytes("ba_reduce", p.n_poses, p1 - p0, int(ptr[-1]), n_free, stats["profile_blocks"])
     avg_s = prof[best][0] / prof[best][1] / 1e3
     achieved = nbytes / avg_s / 1e9
-    traffic_all = {}
-    if args.traffic_json and Path(args.traffic_json).exists():
-        traffic_all = json.loads(Path(args.traffic_json).read_text())
-    traffic = traffic_all.get(best)
+    tpath = args.traffic_json or str(ROOT / "profiles" / f"traffic_{args.config}.json")
+    ba_traffic, traffic_why = traffic_for(tpath, args.config, args.lam, world, "ba", sorted(prof))
+    traffic = ba_traffic.get(best)
     lin_bytes = ba_kernel_bytes("ba_lin", p.n_poses, p1 - p0, int(ptr[-1]), n_free, stats["profile_blocks"])
     lin_avg = prof["ba_lin"][0] / prof["ba_lin"][1] / 1e3
     line = {
@@ -571,6 +627,7 @@ def main() -> int:
         "roofline": {
             "bound": "hbm", "kernel": best, "achieved": achieved, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_note": traffic_why, "traffic_file": tpath, "traffic_all_kernels": ba_traffic or None,
             "bytes_per_launch": nbytes,
             "note": "algorithmic bytes per launch / HIP-event average duration on the library stream",
         },
@@ -583,8 +640,8 @@ def main() -> int:
         line["cpu_baseline"] = cpu_baseline_ba(p, args.lam)
         line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
     if rank == 0 and world == 1 and not args.no_matcher:
-        line["secondary"] = bench_matcher(ctx, traffic_all=traffic_all)
-        line["matcher_float"] = bench_matcher_float(ctx, traffic_all=traffic_all)
+        line["secondary"] = bench_matcher(ctx, traffic_path=tpath)
+        line["matcher_float"] = bench_matcher_float(ctx, traffic_path=tpath)
         line["triangulate"] = bench_triangulate(ctx)
         line["pnp"] = bench_pnp(ctx)
         line["sift"] = bench_sift(ctx)

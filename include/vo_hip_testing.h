@@ -21,6 +21,13 @@ int vo_comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128])
  * either way (same sums).  tools/shard_projection.py times the multi-rank layout with it. */
 int vo_ba_split_reduce(vo_ctx* ctx, int on);
 
+/* Test switch: n > 0 launches every fused slab-reduction + solve of this context with n fewer
+ * reducer workgroups than its solver waits for, so the solver's bounded wait times out (about
+ * a quarter of a second per launch).  vo_ba_run / vo_ba_gn_step then return VO_ERR_HIP naming
+ * the timeout, with the state left at the failed iteration's linearisation point, as for a
+ * failed factorisation.  n = 0 restores normal launches. */
+int vo_ba_testing_drop_reducers(vo_ctx* ctx, int n);
+
 #ifdef __cplusplus
 }
 #endif

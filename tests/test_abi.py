@@ -34,7 +34,8 @@ def test_product_header_has_no_test_entry_points():
     """The loopback communicator and the split-reduce switch are test-only: declared in
     vo_hip_testing.h, not vo_hip.h."""
     assert "vo_comm_init_loopback" not in header_functions(_lib.HEADER)
-    assert header_functions(_lib.TEST_HEADER) == ["vo_ba_split_reduce", "vo_comm_init_loopback"]
+    assert header_functions(_lib.TEST_HEADER) == ["vo_ba_split_reduce", "vo_ba_testing_drop_reducers",
+                                                  "vo_comm_init_loopback"]
 
 
 def test_no_device_fails_loudly(monkeypatch):

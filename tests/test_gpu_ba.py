@@ -209,6 +209,65 @@ def test_fused_reduce_after_failed_solve(ctx):
         np.testing.assert_array_equal(a, b)
 
 
+def _fused_equals_split(ctx, q, iters=2):
+    out = []
+    for split in (False, True):
+        _lib.ba_split_reduce(ctx, split)
+        try:
+            s = _session(q, ctx)
+            rc, costs = s.run(iters)
+            assert rc == _lib.VO_OK
+            out.append((costs,) + tuple(s.get_state()))
+        finally:
+            _lib.ba_split_reduce(ctx, False)
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_fused_reduce_timeout_fails_loudly_and_recovers(ctx):
+    """The fused launch's bounded wait (csrc/ba_band.hip band_wait_reduced): with one reducer
+    workgroup left out of every launch (test switch) the solver gives up, vo_ba_run fails with
+    VO_ERR_HIP naming the timeout, and the state stays at the failed iteration's linearisation
+    point.  The host re-zeroes the reducer counter, so the next window on the same context runs
+    the fused launch to the split launches' bits."""
+    p = make_ba_config("cfg2")
+    s = _session(p, ctx)
+    assert s.plan_stats()["band_solver"] == 1
+    _lib.ba_testing_drop_reducers(ctx, 1)
+    try:
+        with pytest.raises(_lib.VoError, match="timed out"):
+            s.run(2)
+    finally:
+        _lib.ba_testing_drop_reducers(ctx, 0)
+    P, X = s.get_state()
+    np.testing.assert_array_equal(P, _pose_round(p.poses_cw))
+    np.testing.assert_array_equal(X, p.points)
+    _fused_equals_split(ctx, p)
+
+
+def test_fused_reduce_timeout_after_failed_solve(ctx):
+    """A timeout in a launch whose earlier iteration already failed (not SPD) is still recorded
+    (ADVICE r3): the launches after the failure count their reducers, the host re-zeroes the
+    counter on any failed status, and the next window is exact."""
+    p = make_ba_problem(6, 100, 41)
+    cam = p.obs_cam.copy()
+    cam[cam == 5] = 4
+    bad = BASession(p.K, p.point_ptr, cam, p.obs_uv, p.n_poses, 2, 0.0, ctx)
+    bad.set_state(p.poses_cw, p.points)
+    if bad.plan_stats()["band_solver"] != 1:
+        pytest.skip("window not on the banded solver")
+    _lib.ba_testing_drop_reducers(ctx, 1)
+    try:
+        with pytest.raises(_lib.VoError, match="timed out"):
+            bad.run(3)
+    finally:
+        _lib.ba_testing_drop_reducers(ctx, 0)
+    # a not-SPD run without the switch: its later launches count every reducer
+    bad.set_state(p.poses_cw, p.points)
+    assert bad.run(3)[0] == _lib.VO_ERR_NOT_SPD
+    _fused_equals_split(ctx, make_ba_config("cfg2"))
+
+
 def _pose_round(P):
     from visualodometry_amd.ba import poses_to_rt, rt_to_poses
 

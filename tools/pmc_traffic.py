@@ -6,13 +6,23 @@ coalesced read, so reads are doubled.  The two counters cannot share a pass
 (TCC slots), hence two runs of the same command.
 
     python tools/pmc_traffic.py FETCH_DIR/run_counter_collection.csv \
-        WRITE_DIR/run_counter_collection.csv -o profiles/traffic.json
+        WRITE_DIR/run_counter_collection.csv --config cfg3 -o profiles/traffic_cfg3.json
+
+The output is keyed (``_key``): the configuration and damping of the profiled bench.py run,
+the source digests of the BA and matcher kernels (bench.source_digest) and the launches per
+kernel.  bench.py attaches a figure only to a timed run with the same key.  Per-launch values
+are medians over the dispatches (the parity guard's odd launches do not move them).
 """
 
 import argparse
 import csv
 import json
+import sys
 from collections import defaultdict
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import bench  # noqa: E402
 
 # first match wins: "fpack_kernel" before "pack_kernel"; the int8 sweep is attributed by
 # its template argument (match_kernel<2> = the D = 128 SIFT workload of the bench line;
@@ -43,7 +53,11 @@ def per_launch(path: str, counter: str):
     out = defaultdict(list)
     for (s, _), v in acc.items():
         out[s].append(v)
-    return {s: sum(v) / len(v) for s, v in out.items()}, {s: len(v) for s, v in out.items()}
+    med = {}
+    for s, v in out.items():
+        v = sorted(v)
+        med[s] = v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2])
+    return med, {s: len(v) for s, v in out.items()}
 
 
 def main():
@@ -51,11 +65,17 @@ def main():
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
     ap.add_argument("-o", "--out", required=True)
+    ap.add_argument("--config", default="cfg3", help="bench.py --config of the profiled runs")
+    ap.add_argument("--lam", type=float, default=1.0, help="bench.py --lam of the profiled runs")
+    ap.add_argument("--gpus", type=int, default=1)
     a = ap.parse_args()
     fetch, nf = per_launch(a.fetch_csv, "FETCH_SIZE")
     write, nw = per_launch(a.write_csv, "WRITE_SIZE")
-    res = {"_method": "bytes/launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024, gfx950 FETCH_SIZE half-count "
-                      "correction per MI355X_MICROARCH.md; separate --pmc passes",
+    res = {"_method": "bytes/launch = (2*median FETCH_SIZE + median WRITE_SIZE) * 1024 over the dispatches, "
+                      "gfx950 FETCH_SIZE half-count correction per MI355X_MICROARCH.md; separate --pmc passes",
+           "_key": {"config": a.config, "lam": a.lam, "gpus": a.gpus,
+                    "digest": {g: bench.source_digest(g) for g in bench.TRAFFIC_SOURCES},
+                    "launches": {s: min(nf.get(s, 0), nw.get(s, 0)) for s in set(nf) | set(nw)}},
            "_raw_kb": {}}
     for s in sorted(set(fetch) | set(write)):
         fk, wk = fetch.get(s, 0.0), write.get(s, 0.0)

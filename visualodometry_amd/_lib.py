@@ -105,6 +105,7 @@ SIGNATURES = {
     "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_ba_split_reduce": (_I, [_P, _I]),
+    "vo_ba_testing_drop_reducers": (_I, [_P, _I]),
 }
 
 _lib = None
@@ -265,6 +266,12 @@ def ba_split_reduce(ctx: "Context", on: bool = True) -> None:
     """Test/tool switch: keep the BA's slab reduction a launch of its own on this context (the
     multi-rank layout); see vo_ba_split_reduce."""
     check(ctx.lib.vo_ba_split_reduce(ctx.handle, int(bool(on))), "vo_ba_split_reduce")
+
+
+def ba_testing_drop_reducers(ctx: "Context", n: int) -> None:
+    """Test switch: fused launches of this context leave out ``n`` reducer workgroups, so
+    the solver's bounded wait times out; see vo_ba_testing_drop_reducers."""
+    check(ctx.lib.vo_ba_testing_drop_reducers(ctx.handle, int(n)), "vo_ba_testing_drop_reducers")
 
 
 def ptr(a, ctype):

@@ -721,6 +721,14 @@ int vo_ba_split_reduce(vo_ctx* ctx, int on) {
   });
 }
 
+int vo_ba_testing_drop_reducers(vo_ctx* ctx, int n) {
+  return guarded([&] {
+    VO_REQUIRE(ctx != nullptr, VO_ERR_ARG, "vo_ba_testing_drop_reducers: null context");
+    VO_REQUIRE(n >= 0, VO_ERR_ARG, "vo_ba_testing_drop_reducers: n < 0");
+    ctx->ba_drop_reducers = n;
+  });
+}
+
 int vo_comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
   return guarded([&] {
     vo::bind(ctx);

@@ -1472,12 +1472,14 @@ class BAEngine {
     return VO_OK;
   }
 
-  // A fused launch whose solver timed out (kBandStatusTimeout): strip the flag from the status
-  // word's iteration and re-zero the reducer counter (the late reducers have arrived by now).
+  // After a failed fused launch (any non-zero status; kBandStatusTimeout: the solver gave up
+  // waiting for its reducers) the reducer counter is re-zeroed -- the stream is synchronised,
+  // so every late reducer has counted itself by now -- and the timeout flag is stripped from
+  // the status word's iteration.  Returns whether a timeout was recorded.
   bool clear_timeout(int& status) {
+    if (status && fuse_ok_) VO_HIP_CHECK(hipMemsetAsync(d_red_count_.ptr, 0, 256, ctx_->stream));
     if (!(status & kBandStatusTimeout)) return false;
     status &= ~kBandStatusTimeout;
-    VO_HIP_CHECK(hipMemsetAsync(d_red_count_.ptr, 0, 256, ctx_->stream));
     return true;
   }
 
@@ -1673,6 +1675,7 @@ class BAEngine {
       B.status = A.status;
       B.stamps = nullptr;
       B.nred = fused() ? band_fused_workgroups(A.nprof) : 0;
+      B.red_drop = B.nred > 0 ? ctx_->ba_drop_reducers : 0;
       B.red_count = d_red_count_.as<unsigned>();
       B.red = reduce_args();
       if (stamps_on_) {

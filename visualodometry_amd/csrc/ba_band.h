@@ -69,6 +69,7 @@ struct BandArgs {
   // solver, reads sys only after red_count reached nred and its agent-scope acquire, and
   // takes nred back off the counter (zero between launches).
   int nred;
+  int red_drop;  // test switch (host only): reducer workgroups left out of the launch
   unsigned* red_count;
   ReduceArgs red;
 };

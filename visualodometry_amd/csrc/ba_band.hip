@@ -273,7 +273,9 @@ __device__ __forceinline__ void band_reduce_wg(const BandArgs& B, int r, double*
   if (iscost && t == 0 && !failed) st_sc1(A.sys + A.cost_off, cpart[0]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores done
   __syncthreads();
-  if (tid == 0) __hip_atomic_fetch_add((gu32*)B.red_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // release: every sc1 store above is ordered before the count (explicit in the memory model;
+  // the stores are agent atomics already, so this costs one fence per workgroup)
+  if (tid == 0) __hip_atomic_fetch_add((gu32*)B.red_count, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Solver side of the fused launch: one lane polls red_count (relaxed, s_sleep between reads,
@@ -323,7 +325,8 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   const int m = A.m, nb = A.nb, sp = A.s;
   const int ncolT = m + sp, ncolB = nb + sp;
   const int SS = kFull ? CS : CSP, RC = kFull ? max(ncolT, ncolB) : w + 4, SPAD = kFull ? 128 : 0;
-  const bool prior_status = A.status && *A.status;
+  const int prior_word = A.status ? *A.status : 0;
+  const bool prior_status = prior_word != 0;
   double* ringT = dyn;
   double* ringB = ringT + RC * SS + SPAD;
   double* zs = ringB + RC * SS + SPAD;  // back substitution: z (6F)
@@ -984,7 +987,13 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       se3_exp_apply(d, T, out);
     }
   }
-  if (tid == 0 && failed && !prior_status) *A.status = reduced ? A.iter_tag : A.iter_tag | kBandStatusTimeout;
+  // A timeout is recorded whatever the earlier status (the counter then holds this launch's
+  // reducers: the host re-zeroes it when it reads the flag); a failed factorisation only when
+  // no earlier step failed (the status names the first failed iteration).
+  if (tid == 0) {
+    if (!reduced) *A.status = (prior_status ? prior_word : A.iter_tag) | kBandStatusTimeout;
+    else if (failed && !prior_status) *A.status = A.iter_tag;
+  }
   BST(14);
 #if VO_BA_STAMPS
   if (lane == 0 && A.stamps)
@@ -1006,7 +1015,9 @@ void band_set_attributes(const BandLds& L) {
 }
 
 void launch_band_solve(const BandArgs& A, const BandLds& L, hipStream_t st) {
-  const dim3 grid(1 + std::max(A.nred, 0));  // the solver first, then the fused K2's reducers
+  // the solver first, then the fused K2's reducers (a test build of the context may launch
+  // fewer than the solver waits for: vo_ba_testing_drop_reducers)
+  const dim3 grid(1 + std::max(A.nred - std::max(A.red_drop, 0), 0));
   const size_t lds = band_launch_lds(L, A.nred > 0);
   if (L.full)
     hipLaunchKernelGGL(ba_band_kernel<true>, grid, dim3(kBandThreads), lds, st, A);

@@ -134,10 +134,13 @@ __device__ __forceinline__ double rsq_nr(double d) {
   const double q = __builtin_amdgcn_rsq(d);
   return __builtin_fma(0.5 * q, __builtin_fma(-(d * q), q, 1.0), q);
 }
+// rcp_nr(+-0) = +-inf as IEEE 1/z (the Newton steps alone would give NaN: fma(-0, inf, 1)),
+// so a zero-depth observation gives the oracle's infinite residual, not a NaN.
 __device__ __forceinline__ double rcp_nr(double z) {
-  double r = __builtin_amdgcn_rcp(z);
+  const double r0 = __builtin_amdgcn_rcp(z);
+  double r = __builtin_fma(r0, __builtin_fma(-z, r0, 1.0), r0);
   r = __builtin_fma(r, __builtin_fma(-z, r, 1.0), r);
-  return __builtin_fma(r, __builtin_fma(-z, r, 1.0), r);
+  return __builtin_isinf(r0) ? r0 : r;
 }
 
 // v[lane] for a register array without a runtime index (a runtime index would
