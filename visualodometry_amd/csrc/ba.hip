@@ -46,6 +46,9 @@
 #include "ba_plan.h"
 #include "vo_ctx.h"
 
+#ifndef VO_BA_CL
+#define VO_BA_CL 1  // tuning build: 0 keeps the per-step barrier elimination in full mode
+#endif
 #ifndef VO_BA_FUSE
 #define VO_BA_FUSE 1  // tuning build: 0 launches K2 on its own
 #endif
@@ -1664,6 +1667,11 @@ class BAEngine {
       B.cost_off = cost_off_;
       B.merge = band_tab_.merge;
       B.n_merge = band_tab_.n_merge;
+      // the critical-lane elimination: full mode, w >= 1 (tuning build: VO_BA_CL=0 keeps the
+      // per-step barrier kernel)
+      B.cl = (VO_BA_CL && band_lds_.full && band_.w >= 1) ? band_tab_.cl : -1;
+      B.cl_rounds0 = band_tab_.cl_rounds[0];
+      B.cl_rounds1 = band_tab_.cl_rounds[1];
       B.tab = d_band_tab_.as<int>();
       B.sys = A.sys;
       B.zero = d_zero_.as<double>();

@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <climits>
 
+#include "ba_band_cl.h"
 #include "ba_math.h"
 #include "vo_common.h"
 
@@ -96,6 +97,44 @@ BandTables band_tables(int F, const BandSplit& b, const BandLds& L) {
     }
   }
   T.n_merge = (int)T.tab.size() / 2;
+  // Critical-lane trailing update (ba_band_cl.h): the blocks (k + qi, k + jj), 1 <= jj <= qi <= w,
+  // of step k's update except the chain wave's own (qi, jj) = (1, 1) and (2, 1), one target row
+  // per lane, in 16-lane DPP rows that each serve one jj: lanes 0..5 hold the rows of
+  // L_{k+jj,k} (broadcast to the row), lanes 6..15 up to ten target rows.  Priority order:
+  // jj = 1 (column k + 1: the next forward wave's input), then jj = 2 (its first two blocks are
+  // the chain's next diagonal and sub-diagonal), then jj = 3 ... w.  DPP row d goes to trailing
+  // wave (d / 4) % 2, round d / 8, so the first round of both waves holds every row the chain
+  // and the forward wave wait for.
+  T.cl = (int)T.tab.size();
+  {
+    struct DRow {
+      int jj;
+      std::vector<int> tg;  // (qi << 4) | r
+    };
+    std::vector<DRow> rows;
+    for (int jj = 1; jj <= w; ++jj) {
+      std::vector<int> tg;
+      for (int qi = jj; qi <= w; ++qi) {
+        if (jj == 1 && qi < 3) continue;
+        for (int r = 0; r < 6; ++r) tg.push_back((qi << 4) | r);
+      }
+      for (size_t i = 0; i < tg.size(); i += 10)
+        rows.push_back(DRow{jj, std::vector<int>(tg.begin() + i, tg.begin() + std::min(tg.size(), i + 10))});
+    }
+    T.tab.resize(T.tab.size() + 2 * kClRounds * 64, -1);
+    for (int tw = 0; tw < 2; ++tw)
+      for (int rho = 0; rho < kClRounds; ++rho)
+        for (int lane = 0; lane < 64; ++lane) {
+          const int d = 8 * rho + 4 * tw + lane / 16, li = lane % 16;
+          if (d >= (int)rows.size()) continue;
+          int v = -1;
+          if (li < 6) v = (1 << 16) | (rows[d].jj << 8) | li;
+          else if (li - 6 < (int)rows[d].tg.size()) v = (rows[d].jj << 8) | rows[d].tg[li - 6];
+          T.tab[T.cl + (kClRounds * tw + rho) * 64 + lane] = v;
+          T.cl_rounds[tw] = std::max(T.cl_rounds[tw], rho + 1);
+        }
+    if ((int)rows.size() > 8 * kClRounds) T.cl = -1;  // more than the rounds hold: the general kernel
+  }
   if (T.tab.empty()) T.tab.push_back(0);
   return T;
 }
@@ -304,10 +343,14 @@ __device__ __forceinline__ bool band_wait_reduced(const BandArgs& A, int tid, in
 // Loads below never feed a select or branch before their first real use: a value that
 // must be zero is loaded from the zero block (A.zero) instead, so the waitcnt pass can
 // leave every prefetch in flight.
-template <bool kFull>
+// kCl (full mode, w >= 1): the elimination by the critical-lane layout (ba_band_cl.h and the
+// phase below); the back substitution and the pose update are the same code.
+template <bool kFull, bool kCl>
 __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
+  static_assert(kFull || !kCl, "critical-lane elimination in full mode only");
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int s_fail;
+  __shared__ int s_flags[16];  // kCl: per side, the steps each role has published
   __shared__ __attribute__((aligned(16))) double s_zero[40];   // full mode's zero block
 #if VO_BA_STAMPS
   unsigned long long st_acc[kBandStamps] = {}, st_t = __builtin_amdgcn_s_memtime();
@@ -358,11 +401,29 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     s_fail = prior_fail ? 1 : 0;
     if (A.cost_out && reduced) *A.cost_out = A.sys[A.cost_off];
   }
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) const void gbl_void;
+  if (tid < 16) s_flags[tid] = 0;
+  if constexpr (kCl) {
+    // every column of both sides by LDS-DMA (1 KiB wave pieces, spread over the eight waves;
+    // a column's last piece spills the next column's first K2 values into its slot, the same
+    // values that column's own pieces write), drained before the workgroup barrier below
+    if (!prior_fail) {
+      const int nD = CSP / 128, nT = ncolT * nD, nTot = nT + ncolB * nD;
+      for (int p = wave; p < nTot; p += kBandWaves) {
+        const bool top = p < nT;
+        const int pc = top ? p : p - nT, c = pc / nD, t = pc - nD * c;
+        const double* src = A.sys + (top ? 0l : (long)ncolT * CS) + (long)c * CS + 128 * t + 2 * lane;
+        double* dst = (top ? ringT : ringB) + c * SS + 128 * t;
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
   // Ring prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every
   // 16-byte load in flight, then the stores.  The loads do not wait for the status word
   // (one global round trip less on the launch's path); a failed earlier solve only skips
   // the stores.
-  {
     const int nT = min(w + 2, ncolT) * CS / 2, nB = min(w + 2, ncolB) * CS / 2;  // double2 pieces
     const double2* gT = reinterpret_cast<const double2*>(A.sys);
     const double2* gB = reinterpret_cast<const double2*>(A.sys + (long)ncolT * CS);
@@ -385,8 +446,6 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
 
   // ---- loader wave: column v by LDS-DMA, nDma 1 KiB wave pieces (16 bytes per lane)
   const int nDma = CSP / 128;
-  typedef __attribute__((address_space(3))) void lds_void;
-  typedef __attribute__((address_space(1))) const void gbl_void;
   auto dma_col = [&](int v, double* slot) __attribute__((always_inline)) {
     const double* src = ssys + (long)v * CS + 2 * lane;
     for (int t = 0; t < nDma; ++t)
@@ -670,7 +729,204 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     for (int c = 0; c < 6; ++c) col[6 * c] = gv[c];
   };
 
-  if (!prior_fail) {
+  if constexpr (kCl) {
+    if (!prior_fail) {
+      // ---- Critical-lane elimination (full mode).  Per side four waves, synchronised by LDS
+      // flags instead of a workgroup barrier per step (s_flags[8 side + f]: the number of
+      // steps a role has published):
+      //   chain (role 0)  lanes 0..15 of a DPP row hold [A_kk; A_{k+1,k}; y_k] (ba_band_cl.h).
+      //                   Step k: pivots -> L_kk, y'_k, r (flag 0); the pending step-(k-1) term
+      //                   of A_{k+1,k} (u = L_{k+1,k-1} from the forward wave, V = L_{k,k-1} kept
+      //                   in registers), its solve -> L_{k+1,k} (flag 1); the next panel:
+      //                   A_{k+1,k+1} - L_{k+1,k} L_{k+1,k}^T and y_{k+1} - L_{k+1,k} y'_k from
+      //                   the trailing waves' values through step k - 1, A_{k+2,k+1} (its step-k
+      //                   term waits for the next step).
+      //   forward (role 2) L_{k+q,k} = A_{k+q,k} L_kk^-T for q = 2..w (one lane per row, in
+      //                   place) and y_{k+q} -= L_{k+q,k} y'_k (flag 2).
+      //   trailing (roles 1, 3) blocks (k+qi, k+jj) -= L_{k+qi,k} L_{k+jj,k}^T for every other
+      //                   block of step k, one target row per lane, L_{k+jj,k} broadcast from
+      //                   lanes 0..5 of the DPP row (band_tables' descriptors); the first round
+      //                   (flags 3 / 5) holds column k + 1 and the chain's next two blocks, the
+      //                   last one is flag 4 / 6.
+      // Waits: chain(k) on forward(k-1) and both trailing waves' first round of step k-1;
+      // forward(k) on chain(k) and that round; trailing(k) on forward(k), chain(k)'s flag 1 and
+      // the other trailing wave's step k-1.  Every wait is on an earlier role of the dependency
+      // order, so the phase cannot deadlock, and every step of every role posts its flags.
+      // flags through an LDS-typed pointer (a generic one compiles to flat accesses that wait on
+      // vmcnt as well); the polled value goes through readfirstlane, so the loop is scalar
+      typedef __attribute__((address_space(3))) volatile int lds_flag;
+      lds_flag* const fl = (lds_flag*)s_flags + 8 * side;
+      const int li = lane & 15;
+      const double* const zb = dyn + ZOFF;
+      auto colp = [&](int c) __attribute__((always_inline)) { return sring + c * SS; };
+      auto wait_ge = [&](lds_flag* f, int v) __attribute__((always_inline)) {
+        while (__builtin_amdgcn_readfirstlane(*f) < v) __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+      };
+      auto post = [&](lds_flag* f, int v) __attribute__((always_inline)) {
+        asm volatile("" ::: "memory");
+        if (lane == 0) *f = v;
+      };
+      // chain wave, steps k0 .. kend - 1 of this side (ncol = the side's columns); flush: the
+      // state of column kend to LDS at the end (phase A with a separator)
+      auto cl_chain = [&](int k0, int kend, bool flush) __attribute__((always_inline)) {
+        double a[6], pp[6], vp[6], r[6];
+        bool lazy = false;
+        {
+          const double* c0 = colp(k0);
+          ld6g(li < 6 ? c0 + 6 * li : li == 12 ? c0 + 36 * R : zb, a);
+          ld6g((li >= 6 && li < 12) ? c0 + 36 + 6 * (li - 6) : zb, pp);
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c) vp[c] = 0.0;
+        int k = k0;
+        for (; k < kend; ++k) {
+          cl::pivots(a, r);
+          bad = bad | !isfinite(r[0] + r[1] + r[2] + r[3] + r[4] + r[5]) |
+                ((li == 12) & !isfinite(a[0] + a[1] + a[2] + a[3] + a[4] + a[5]));
+          double* ck = colp(k);
+          if (lane < 6) st6g(ck + 6 * lane, a);
+          else if (lane == 12) st6g(ck + 36 * R, a);
+          else if (lane == 13) st6g(ck + 36 * R + 6, r);
+          post(fl + 0, k + 1);
+          if (k + 1 >= snload) break;
+          if (lazy) {  // the step-(k-1) term of A_{k+1,k}
+            wait_ge(fl + 2, k);
+            double u[6];
+            ld6g((li >= 6 && li < 12) ? colp(k - 1) + 72 + 6 * (li - 6) : zb, u);
+            cl::sub_uvt<6>(pp, u, vp);
+          }
+          cl::solve_lt(pp, a, r);
+          if (lane >= 6 && lane < 12) st6g(ck + 36 + 6 * (lane - 6), pp);
+          post(fl + 1, k + 1);
+          // next panel (column k + 1) from the values through step k - 1
+          wait_ge(fl + 2, k);
+          wait_ge(fl + 3, k);
+          wait_ge(fl + 5, k);
+          double b0[6], b1[6], sh[6], u[6];
+          const double* c1 = colp(k + 1);
+          ld6g(li < 6 ? c1 + 6 * li : li == 12 ? c1 + 36 * R : zb, b0);
+          ld6g((li >= 6 && li < 12 && k + 2 < snload) ? c1 + 36 + 6 * (li - 6) : zb, b1);
+          cl::shl6(pp, sh);
+#pragma unroll
+          for (int c = 0; c < 6; ++c) u[c] = li < 6 ? sh[c] : li == 12 ? a[c] : 0.0;
+          cl::sub_uvt<6>(b0, u, pp);
+#pragma unroll
+          for (int c = 0; c < 6; ++c) {
+            vp[c] = pp[c];
+            pp[c] = b1[c];
+            a[c] = b0[c];
+          }
+          lazy = w >= 2;
+        }
+        if (flush && k == kend && kend < snload) {
+          // column kend through step kend - 1: the pending term of its sub-diagonal block, then
+          // the panel to LDS for the separator merge
+          if (lazy) {
+            wait_ge(fl + 2, kend);
+            double u[6];
+            ld6g((li >= 6 && li < 12) ? colp(kend - 1) + 72 + 6 * (li - 6) : zb, u);
+            cl::sub_uvt<6>(pp, u, vp);
+          }
+          double* ce = colp(kend);
+          if (lane < 6) st6g(ce + 6 * lane, a);
+          else if (lane == 12) st6g(ce + 36 * R, a);
+          else if (lane >= 6 && lane < 12 && kend + 1 < snload) st6g(ce + 36 + 6 * (lane - 6), pp);
+        }
+      };
+      // forward wave: lane 6 (q - 2) + r holds row r of block k + q, q = 2..w
+      auto cl_fwd = [&](int k0, int kend) __attribute__((always_inline)) {
+        const int qf = lane / 6 + 2, rf = lane - 6 * (lane / 6);
+        for (int k = k0; k < kend; ++k) {
+          wait_ge(fl + 0, k + 1);
+          wait_ge(fl + 3, k);
+          wait_ge(fl + 5, k);
+          const double* ck = colp(k);
+          double L[21], r[6], y[6], row[6];
+#pragma unroll
+          for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int c = 0; c <= i; c += 2) {
+              const double2 v = reinterpret_cast<const double2*>(ck + 6 * i)[c / 2];
+              L[P6(i, c)] = v.x;
+              if (c + 1 <= i) L[P6(i, c + 1)] = v.y;
+            }
+          ld6g(ck + 36 * R + 6, r);
+          ld6g(ck + 36 * R, y);
+          const bool on = (qf <= w) & (k + qf < snload);
+          ld6g(on ? ck + 36 * qf + 6 * rf : zb, row);
+          const double yo = on ? colp(k + qf)[36 * R + rf] : 0.0;
+          fwd6(L, r, row);
+          if (on) {
+            st6g(const_cast<double*>(ck) + 36 * qf + 6 * rf, row);
+            colp(k + qf)[36 * R + rf] =
+                yo - (row[0] * y[0] + row[1] * y[1] + row[2] * y[2] + row[3] * y[3] + row[4] * y[4] + row[5] * y[5]);
+          }
+          post(fl + 2, k + 1);
+        }
+      };
+      // trailing wave tw (0: role 1, 1: role 3)
+      auto cl_trail = [&](int k0, int kend, int tw) __attribute__((always_inline)) {
+        const int nr = tw ? A.cl_rounds1 : A.cl_rounds0;
+        int desc[kClRounds];
+#pragma unroll
+        for (int h = 0; h < kClRounds; ++h) desc[h] = A.tab[A.cl + (kClRounds * tw + h) * 64 + lane];
+        lds_flag* const f1 = fl + (tw ? 5 : 3);
+        lds_flag* const fa = fl + (tw ? 6 : 4);
+        lds_flag* const fo = fl + (tw ? 4 : 6);
+        for (int k = k0; k < kend; ++k) {
+          wait_ge(fl + 2, k + 1);
+          wait_ge(fl + 1, k + 1);
+          wait_ge(fo, k);
+          const double* ck = colp(k);
+#pragma unroll
+          for (int h = 0; h < kClRounds; ++h) {
+            if (h >= nr) break;
+            const int d = desc[h];
+            const bool isv = d >= 0 && (d >> 16);
+            const int jj = (d >> 8) & 15, qi = (d >> 4) & 15, rr = d & 15;
+            const bool vok = isv & (k + jj < snload);
+            const bool tok = (d >= 0) & !isv & (k + qi < snload);
+            double vrow[6], u[6], out[6];
+            ld6g(vok ? ck + 36 * jj + 6 * rr : zb, vrow);
+            ld6g(tok ? ck + 36 * qi + 6 * rr : zb, u);
+            double* tg = colp(k + jj) + 36 * (qi - jj) + 6 * rr;
+            ld6g(tok ? tg : zb, out);
+            cl::sub_uvt<0>(out, u, vrow);
+            if (tok) st6g(tg, out);
+            if (h == 0) post(f1, k + 1);
+          }
+          if (nr == 0) post(f1, k + 1);
+          post(fa, k + 1);
+        }
+      };
+      auto cl_phase = [&](int k0, int kend, bool flush) __attribute__((always_inline)) {
+        if (role == kChain) cl_chain(k0, kend, flush);
+        else if (role == 2) cl_fwd(k0, kend);
+        else cl_trail(k0, kend, role == 1 ? 0 : 1);
+      };
+      cl_phase(0, sna, sp > 0);
+      if (sp > 0) {
+        // both sides' state of the separator is in the rings: the bottom's contributions merged
+        // into the top's (fixed order), then the top's four waves continue through the
+        // separator while the bottom's form the G blocks of the rows final after phase A
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int e = tid; e < A.n_merge; e += kBandThreads) {
+          const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
+          dyn[d.x] += dyn[d.y];
+        }
+        __syncthreads();
+        if (side == 0) {
+          cl_phase(m, m + sp, false);
+        } else {
+          const int n0 = 6 * (m + nb) * w;
+          for (int e = 64 * role + lane; e < n0; e += 256) g_item(0, e);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  } else if (!prior_fail) {
     const int PA = max(m, nb);
     int sk = 0, skm = RC - 1;
     for (int p = 0; p < PA; ++p) {
@@ -736,7 +992,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       rec_store(last, v2);
     }
   }
-  if (lane == 0 && bad) s_fail = 1;
+  if ((kCl || lane == 0) && bad) s_fail = 1;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // factor records written
   BST(8);
   __syncthreads();
@@ -1010,8 +1266,10 @@ static size_t band_launch_lds(const BandLds& L, bool fused) {
 }
 
 void band_set_attributes(const BandLds& L) {
-  const void* f = L.full ? (const void*)ba_band_kernel<true> : (const void*)ba_band_kernel<false>;
-  VO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)band_launch_lds(L, true)));
+  const void* fs[3] = {(const void*)ba_band_kernel<true, false>, (const void*)ba_band_kernel<false, false>,
+                       (const void*)ba_band_kernel<true, true>};
+  for (const void* f : fs)
+    VO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)band_launch_lds(L, true)));
 }
 
 void launch_band_solve(const BandArgs& A, const BandLds& L, hipStream_t st) {
@@ -1019,10 +1277,12 @@ void launch_band_solve(const BandArgs& A, const BandLds& L, hipStream_t st) {
   // fewer than the solver waits for: vo_ba_testing_drop_reducers)
   const dim3 grid(1 + std::max(A.nred - std::max(A.red_drop, 0), 0));
   const size_t lds = band_launch_lds(L, A.nred > 0);
-  if (L.full)
-    hipLaunchKernelGGL(ba_band_kernel<true>, grid, dim3(kBandThreads), lds, st, A);
+  if (L.full && A.cl >= 0)
+    hipLaunchKernelGGL((ba_band_kernel<true, true>), grid, dim3(kBandThreads), lds, st, A);
+  else if (L.full)
+    hipLaunchKernelGGL((ba_band_kernel<true, false>), grid, dim3(kBandThreads), lds, st, A);
   else
-    hipLaunchKernelGGL(ba_band_kernel<false>, grid, dim3(kBandThreads), lds, st, A);
+    hipLaunchKernelGGL((ba_band_kernel<false, false>), grid, dim3(kBandThreads), lds, st, A);
 }
 
 }  // namespace vo
