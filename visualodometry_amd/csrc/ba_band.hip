@@ -789,7 +789,10 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
           else if (lane == 12) st6g(ck + 36 * R, a);
           else if (lane == 13) st6g(ck + 36 * R + 6, r);
           post(fl + 0, k + 1);
-          if (k + 1 >= snload) break;
+          if (k + 1 >= snload) {  // the side's last column: no sub-diagonal block to publish
+            post(fl + 1, k + 1);
+            break;
+          }
           if (lazy) {  // the step-(k-1) term of A_{k+1,k}
             wait_ge(fl + 2, k);
             double u[6];
