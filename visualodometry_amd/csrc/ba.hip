@@ -607,13 +607,14 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
     // two with two register sets: pair j+2's Z rows are fetched (16-byte LDS reads,
     // indices read two pairs ahead, clamped -- no branches) while pair j+1's 18 FMAs run.
     {
-      const int items = nslots * 6;
+      const int items = h3.z * 6;  // the chunk's active slots (ChunkImg::aslot)
       const int np = parts_for(items);
       for (int base = 0; base < items * np; base += kLinThreads) {
         const int idx = base + tid, item = idx / np, part = idx % np;
-        const int s = item / 6, a = item - 6 * (item / 6);
+        const int si = item / 6, a = item - 6 * (item / 6);
+        const int s = item < items ? S.img.aslot[si] : 0;
         double out[6] = {0, 0, 0, 0, 0, 0};
-        const int e0 = item < items ? S.img.slotp[s] + part : 0, e1 = item < items ? S.img.slotp[s + 1] : 0;
+        const int e0 = item < items ? S.img.slotp[si] + part : 0, e1 = item < items ? S.img.slotp[si + 1] : 0;
         if (e0 < e1) {
           auto zrow = [&](int pr, double (&za)[3], double2 (&zy)[9]) {
             const double2* py = reinterpret_cast<const double2*>(S.Z[pr >> 8]);
@@ -663,15 +664,16 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
     // (static observation list, indices read ahead) and b_c[a] = sum of bt over its
     // track entries; split over np lanes like the pairs when the window is narrow
     {
-      const int items = ncams * 6;
+      const int items = h3.w * 6;  // the chunk's active cameras (ChunkImg::acid)
       const int np = parts_for(items);
       for (int base = 0; base < items * np; base += kLinThreads) {
         const int idx = base + tid, item = idx / np, part = idx % np;
-        const int c = item / 6, a = item - 6 * (item / 6);
+        const int ci = item / 6, a = item - 6 * (item / 6);
+        const int c = item < items ? S.img.acid[ci] : 0;
         double out[6] = {0, 0, 0, 0, 0, 0};
         double acc = 0.0;
         if (item < items) {
-          const int q0 = S.img.camop[c] + part, q1 = S.img.camop[c + 1];
+          const int q0 = S.img.camop[ci] + part, q1 = S.img.camop[ci + 1];
           if (q1 > q0) {
             const int ql = q1 - 1;
             int on = S.img.camol[q0];
@@ -691,7 +693,7 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
               for (int cc = 0; cc < 6; ++cc) out[cc] += ja0 * j[cc] + ja1 * j[6 + cc];
             }
           }
-          const int e0 = S.img.camp[c] + part, e1 = S.img.camp[c + 1];
+          const int e0 = S.img.camp[ci] + part, e1 = S.img.camp[ci + 1];
           if (e1 > e0) {
             const int el = e1 - 1;
             int xn = S.img.caml[e0];
@@ -709,7 +711,7 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
         }
         if (item < items && part == 0) {
           S.bwin[6 * c + a] += acc;
-          double* w = &S.win[36 * S.img.dslot[c] + 6 * a];
+          double* w = &S.win[36 * S.img.dslot[ci] + 6 * a];
 #pragma unroll
           for (int cc = 0; cc < 6; ++cc) w[cc] += out[cc];
         }

@@ -713,15 +713,29 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
           g.te_lcam[i] = P.te_lcam[te0 + i];
         }
         for (int i = 0; i <= npt; ++i) g.pt_te[i] = P.pt_te[p0 + i] - te0;
-        for (int i = 0; i <= ns; ++i) g.slotp[i] = P.slot_ptr[sb + i] - e0;
+        // the slots with pairs in this chunk and the cameras with track entries or observations
+        // in it, compacted in window order (their lists keep their order)
+        int nas = 0, nac = 0;
+        for (int i = 0; i < ns; ++i)
+          if (P.slot_ptr[sb + i + 1] > P.slot_ptr[sb + i]) {
+            g.aslot[nas] = (uint8_t)i;
+            g.slotp[nas++] = P.slot_ptr[sb + i] - e0;
+          }
+        g.slotp[nas] = e1 - e0;
         for (int i = 0; i < e1 - e0; ++i) g.pairs[i] = P.pair_list[e0 + i];
-        for (int i = 0; i <= nc; ++i) {
-          g.camp[i] = P.cam_ptr[cb + i] - c0;
-          g.camop[i] = P.camo_ptr[cb + i] - q0;
-        }
+        for (int i = 0; i < nc; ++i)
+          if (P.cam_ptr[cb + i + 1] > P.cam_ptr[cb + i] || P.camo_ptr[cb + i + 1] > P.camo_ptr[cb + i]) {
+            g.acid[nac] = (uint8_t)i;
+            g.camp[nac] = P.cam_ptr[cb + i] - c0;
+            g.camop[nac] = P.camo_ptr[cb + i] - q0;
+            g.dslot[nac++] = P.segcam_diag[co + i];
+          }
+        g.camp[nac] = c1 - c0;
+        g.camop[nac] = q1 - q0;
         for (int i = 0; i < c1 - c0; ++i) g.caml[i] = P.cam_list[c0 + i];
         for (int i = 0; i < q1 - q0; ++i) g.camol[i] = P.camo_list[q0 + i];
-        for (int i = 0; i < nc; ++i) g.dslot[i] = P.segcam_diag[co + i];
+        h[14] = nas;
+        h[15] = nac;
       }
       // segment header (kSegHdr)
       int32_t* h = &P.seg_hdr[(size_t)si * kSegHdr];

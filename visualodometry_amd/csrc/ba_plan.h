@@ -65,6 +65,8 @@ constexpr int kPlanTableCams = 512;  // planner: flat lookup tables up to this m
 // offset; per-thread camera ids sit at fixed offsets (no dependent load).
 constexpr int kSegHdr = 48;
 
+// Per chunk header (kChunkHdr ints): ob0 nob te0 nte p0 npt sb cb e0 e1 c0 c1 q0 q1, then the
+// chunk's active window slots and active window cameras (ChunkImg).
 // Per chunk, the static part of K1's LDS staging as one image (offsets already made
 // chunk-relative, types as K1 reads them): staging a chunk is one 16-byte load and one
 // LDS store per thread instead of a load per list.  Unused entries are zero.
@@ -74,10 +76,15 @@ struct alignas(16) ChunkImg {
   int32_t te_pt[kChunkTe];         // track entry -> chunk landmark
   int32_t te_lcam[kChunkTe];       // track entry -> window camera, -1 if fixed
   int32_t pt_te[kChunkPts + 1];    // landmark -> first chunk track entry
-  int32_t slotp[kSegSlots + 1];    // window slot -> first pair-list entry
-  int32_t camp[kSegCams + 1];      // window camera -> first track-entry list entry
-  int32_t camop[kSegCams + 1];     // window camera -> first observation list entry
-  int32_t dslot[kSegCams];         // window camera -> its diagonal slot
+  // Only the window slots and cameras this chunk touches (header ints 14 and 15 count them),
+  // so K1's Schur loops run over the chunk's own items, not the whole segment window.
+  int32_t slotp[kSegSlots + 1];    // active slot i -> first pair-list entry (pairs by slot)
+  int32_t camp[kSegCams + 1];      // active camera i -> first track-entry list entry
+  int32_t camop[kSegCams + 1];     // active camera i -> first observation list entry
+  int32_t dslot[kSegCams];         // active camera i -> its diagonal slot
+  uint8_t aslot[kSegSlots];        // active slot i -> window slot
+  uint8_t acid[kSegCams];          // active camera i -> window camera
+  uint8_t pad_[8];
   uint16_t pairs[kChunkPairs];     // (te_x | te_y << 8) by slot
   uint8_t caml[kChunkTe];          // track entries by window camera
   uint8_t camol[kChunkObs];        // observations by window camera
