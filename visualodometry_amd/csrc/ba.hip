@@ -1672,8 +1672,6 @@ class BAEngine {
       // the critical-lane elimination: full mode, w >= 1 (tuning build: VO_BA_CL=0 keeps the
       // per-step barrier kernel)
       B.cl = (VO_BA_CL && band_lds_.full && band_.w >= 1) ? band_tab_.cl : -1;
-      B.cl_rounds0 = band_tab_.cl_rounds[0];
-      B.cl_rounds1 = band_tab_.cl_rounds[1];
       B.tab = d_band_tab_.as<int>();
       B.sys = A.sys;
       B.zero = d_zero_.as<double>();

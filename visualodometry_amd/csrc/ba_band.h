@@ -27,15 +27,11 @@ BandSplit band_split(int F, const std::vector<int>& first);
 
 // Merge pairs of one window structure (host-built, uploaded once): (destination, source)
 // LDS offsets (doubles) of the separator's blocks and rhs, top ring += bottom ring.
-// Critical-lane layout (full mode, w >= 1; ba_band_cl.h): per trailing wave tw (0, 1), round
-// rho and lane, one packed descriptor at cl + (kClRounds tw + rho) 64 + lane: -1 idle, else
-// (V << 16) | (jj << 8) | (qi << 4) | r -- a broadcast lane (V = 1: row r of L_{k+jj,k}) or a
-// target row r of block (k + qi, k + jj) (see band_tables).
-constexpr int kClRounds = 4;
+// cl >= 0: the window takes the critical-lane elimination (full mode; ba_band_cl.h).
 struct BandTables {
   std::vector<int> tab;
   int merge = 0, n_merge = 0;
-  int cl = 0, cl_rounds[2] = {0, 0};
+  int cl = -1;
 };
 // LDS layout of the two column stores.  Ring mode: w + 4 slots per side, each padded to
 // whole 1 KiB LDS-DMA pieces; factor records go to global memory.  Full mode (when it
@@ -58,7 +54,7 @@ struct BandArgs {
   int F, w, m, nb, s;
   int nprof, n_poses, n_fixed, iter_tag;
   int merge, n_merge;     // merge pairs in tab (BandTables)
-  int cl, cl_rounds0, cl_rounds1;  // critical-lane trailing descriptors in tab (BandTables); cl < 0: off
+  int cl;                // >= 0: the critical-lane elimination (full mode, BandTables::cl)
   long cost_off;          // the cost in sys
   const int* tab;
   const double* sys;      // K2's banded layout (above), padded by one ring slot

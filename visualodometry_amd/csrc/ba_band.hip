@@ -97,44 +97,7 @@ BandTables band_tables(int F, const BandSplit& b, const BandLds& L) {
     }
   }
   T.n_merge = (int)T.tab.size() / 2;
-  // Critical-lane trailing update (ba_band_cl.h): the blocks (k + qi, k + jj), 1 <= jj <= qi <= w,
-  // of step k's update except the chain wave's own (qi, jj) = (1, 1) and (2, 1), one target row
-  // per lane, in 16-lane DPP rows that each serve one jj: lanes 0..5 hold the rows of
-  // L_{k+jj,k} (broadcast to the row), lanes 6..15 up to ten target rows.  Priority order:
-  // jj = 1 (column k + 1: the next forward wave's input), then jj = 2 (its first two blocks are
-  // the chain's next diagonal and sub-diagonal), then jj = 3 ... w.  DPP row d goes to trailing
-  // wave (d / 4) % 2, round d / 8, so the first round of both waves holds every row the chain
-  // and the forward wave wait for.
-  T.cl = (int)T.tab.size();
-  {
-    struct DRow {
-      int jj;
-      std::vector<int> tg;  // (qi << 4) | r
-    };
-    std::vector<DRow> rows;
-    for (int jj = 1; jj <= w; ++jj) {
-      std::vector<int> tg;
-      for (int qi = jj; qi <= w; ++qi) {
-        if (jj == 1 && qi < 3) continue;
-        for (int r = 0; r < 6; ++r) tg.push_back((qi << 4) | r);
-      }
-      for (size_t i = 0; i < tg.size(); i += 10)
-        rows.push_back(DRow{jj, std::vector<int>(tg.begin() + i, tg.begin() + std::min(tg.size(), i + 10))});
-    }
-    T.tab.resize(T.tab.size() + 2 * kClRounds * 64, -1);
-    for (int tw = 0; tw < 2; ++tw)
-      for (int rho = 0; rho < kClRounds; ++rho)
-        for (int lane = 0; lane < 64; ++lane) {
-          const int d = 8 * rho + 4 * tw + lane / 16, li = lane % 16;
-          if (d >= (int)rows.size()) continue;
-          int v = -1;
-          if (li < 6) v = (1 << 16) | (rows[d].jj << 8) | li;
-          else if (li - 6 < (int)rows[d].tg.size()) v = (rows[d].jj << 8) | rows[d].tg[li - 6];
-          T.tab[T.cl + (kClRounds * tw + rho) * 64 + lane] = v;
-          T.cl_rounds[tw] = std::max(T.cl_rounds[tw], rho + 1);
-        }
-    if ((int)rows.size() > 8 * kClRounds) T.cl = -1;  // more than the rounds hold: the general kernel
-  }
+  T.cl = w >= 1 && w <= kBandMaxW ? 0 : -1;  // the critical-lane elimination (ba_band_cl.h) takes the window
   if (T.tab.empty()) T.tab.push_back(0);
   return T;
 }
@@ -176,11 +139,17 @@ constexpr int kBandThreads = 64 * kBandWaves;
 constexpr int kLdRegs = 6;      // ring loader: elements per lane of one column
 constexpr int kTaskRounds = 2;  // trailing (block, row pair) tasks per lane
 constexpr int kProLoads = 8;    // prologue: 16-byte pieces per thread (columns 0 .. w + 1 of both sides)
+constexpr int kClProLoads = 9;  // critical-lane prologue: columns 0 .. w + 2 of both sides
+constexpr int kClTileRows = (6 * kBandMaxW + 15) / 16;               // critical-lane MFMA tiles of the window
+constexpr int kClTiles = kClTileRows * (kClTileRows - 1) / 2 > kClTileRows ? kClTileRows * (kClTileRows - 1) / 2
+                                                                          : kClTileRows;  // per trailing wave
+typedef double __attribute__((ext_vector_type(4))) d4;
 static_assert(36 * (kBandMaxW + 1) + 12 <= 64 * kLdRegs, "one column per loader wave");
 static_assert(3 * (kBandMaxW - 1) * kBandMaxW / 2 <= 64 * kTaskRounds, "trailing tasks per helper wave");
 static_assert(6 * (kBandMaxW + 1) <= 64, "one lane per panel row");
 static_assert(36 * (kBandMaxW + 1) + 12 <= 3 * 128, "at most three 1 KiB LDS-DMA pieces per column");
 static_assert((kBandMaxW + 2) * (36 * (kBandMaxW + 1) + 12) <= kProLoads * kBandThreads, "prologue");
+static_assert((kBandMaxW + 3) * (36 * (kBandMaxW + 1) + 12) <= kClProLoads * kBandThreads, "prologue");
 // Wave roles (wave = 2 * role + side; wave w runs on SIMD w mod 4, so each side's chain
 // shares its SIMD only with that side's loader, which mostly waits on memory).
 enum { kChain = 0, kTrail = 1, kLoad = 2, kFwd = 3 };
@@ -405,20 +374,25 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   typedef __attribute__((address_space(1))) const void gbl_void;
   if (tid < 16) s_flags[tid] = 0;
   if constexpr (kCl) {
-    // every column of both sides by LDS-DMA (1 KiB wave pieces, spread over the eight waves;
-    // a column's last piece spills the next column's first K2 values into its slot, the same
-    // values that column's own pieces write), drained before the workgroup barrier below
-    if (!prior_fail) {
-      const int nD = CSP / 128, nT = ncolT * nD, nTot = nT + ncolB * nD;
-      for (int p = wave; p < nTot; p += kBandWaves) {
-        const bool top = p < nT;
-        const int pc = top ? p : p - nT, c = pc / nD, t = pc - nD * c;
-        const double* src = A.sys + (top ? 0l : (long)ncolT * CS) + (long)c * CS + 128 * t + 2 * lane;
-        double* dst = (top ? ringT : ringB) + c * SS + 128 * t;
-        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
-      }
+    // columns 0 .. w + 2 of both sides (the forward wave streams the rest by LDS-DMA, three
+    // steps ahead of their first use), every 16-byte load in flight, then the stores
+    const int nT = min(w + 3, ncolT) * CS / 2, nB = min(w + 3, ncolB) * CS / 2;  // double2 pieces
+    const double2* gT = reinterpret_cast<const double2*>(A.sys);
+    const double2* gB = reinterpret_cast<const double2*>(A.sys + (long)ncolT * CS);
+    double2 v[kClProLoads];
+#pragma unroll
+    for (int u = 0; u < kClProLoads; ++u) {
+      const int e = tid + u * kBandThreads;
+      v[u] = e < nT ? gT[e] : e < nT + nB ? gB[e - nT] : make_double2(0.0, 0.0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!prior_fail)
+#pragma unroll
+      for (int u = 0; u < kClProLoads; ++u) {
+        const int e = tid + u * kBandThreads;
+        const bool top = e < nT;
+        const int x = 2 * (top ? e : e - nT), col = x / CS;
+        if (e < nT + nB) *reinterpret_cast<double2*>((top ? ringT : ringB) + col * SS + x - col * CS) = v[u];
+      }
   } else {
   // Ring prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every
   // 16-byte load in flight, then the stores.  The loads do not wait for the status word
@@ -767,8 +741,9 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
         asm volatile("" ::: "memory");
         if (lane == 0) *f = v;
       };
-      // chain wave, steps k0 .. kend - 1 of this side (ncol = the side's columns); flush: the
-      // state of column kend to LDS at the end (phase A with a separator)
+      // chain wave, steps k0 .. kend - 1 of this side; flush: the state of column kend to LDS at
+      // the end (phase A with a separator).  The pending term's operand (the forward wave's
+      // L_{k+1,k-1}) is fetched at the step's start, under the pivots.
       auto cl_chain = [&](int k0, int kend, bool flush) __attribute__((always_inline)) {
         double a[6], pp[6], vp[6], r[6];
         bool lazy = false;
@@ -781,32 +756,36 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
         for (int c = 0; c < 6; ++c) vp[c] = 0.0;
         int k = k0;
         for (; k < kend; ++k) {
+          BST(30);
+          double u[6];
+          const bool more = k + 1 < snload;
+          if (lazy) {
+            wait_ge(fl + 2, k);
+            ld6g((li >= 6 && li < 12) ? colp(k - 1) + 72 + 6 * (li - 6) : zb, u);
+          }
+          BST(18);
           cl::pivots(a, r);
-          bad = bad | !isfinite(r[0] + r[1] + r[2] + r[3] + r[4] + r[5]) |
-                ((li == 12) & !isfinite(a[0] + a[1] + a[2] + a[3] + a[4] + a[5]));
           double* ck = colp(k);
           if (lane < 6) st6g(ck + 6 * lane, a);
           else if (lane == 12) st6g(ck + 36 * R, a);
           else if (lane == 13) st6g(ck + 36 * R + 6, r);
           post(fl + 0, k + 1);
-          if (k + 1 >= snload) {  // the side's last column: no sub-diagonal block to publish
+          BST(17);
+          if (!more) {  // the side's last column: no sub-diagonal block to publish
             post(fl + 1, k + 1);
             break;
           }
-          if (lazy) {  // the step-(k-1) term of A_{k+1,k}
-            wait_ge(fl + 2, k);
-            double u[6];
-            ld6g((li >= 6 && li < 12) ? colp(k - 1) + 72 + 6 * (li - 6) : zb, u);
-            cl::sub_uvt<6>(pp, u, vp);
-          }
+          if (lazy) cl::sub_uvt<6>(pp, u, vp);  // the step-(k-1) term of A_{k+1,k}
           cl::solve_lt(pp, a, r);
           if (lane >= 6 && lane < 12) st6g(ck + 36 + 6 * (lane - 6), pp);
           post(fl + 1, k + 1);
-          // next panel (column k + 1) from the values through step k - 1
-          wait_ge(fl + 2, k);
+          BST(19);
+          // next panel (column k + 1) from the values through step k - 1 (the first trailing
+          // wave's step k - 1, the forward wave's rhs update of step k - 1)
           wait_ge(fl + 3, k);
-          wait_ge(fl + 5, k);
-          double b0[6], b1[6], sh[6], u[6];
+          wait_ge(fl + 2, k);
+          BST(20);
+          double b0[6], b1[6], sh[6];
           const double* c1 = colp(k + 1);
           ld6g(li < 6 ? c1 + 6 * li : li == 12 ? c1 + 36 * R : zb, b0);
           ld6g((li >= 6 && li < 12 && k + 2 < snload) ? c1 + 36 + 6 * (li - 6) : zb, b1);
@@ -821,6 +800,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
             a[c] = b0[c];
           }
           lazy = w >= 2;
+          BST(21);
         }
         if (flush && k == kend && kend < snload) {
           // column kend through step kend - 1: the pending term of its sub-diagonal block, then
@@ -837,70 +817,152 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
           else if (lane >= 6 && lane < 12 && kend + 1 < snload) st6g(ce + 36 + 6 * (lane - 6), pp);
         }
       };
-      // forward wave: lane 6 (q - 2) + r holds row r of block k + q, q = 2..w
+      // forward wave.  Per 16-lane DPP row: lanes 0..5 hold the rows of L_kk, lanes 6..15 ten rows
+      // r of blocks k + q, q = 2..w (40 per pass), solved by broadcast FMAs (cl::solve_lt); then
+      // y_{k+q} -= L_{k+q,k} y'_k.  It also streams the side's columns: column k + w + 3 by
+      // LDS-DMA (inline asm: the compiler would otherwise wait for it before every LDS access),
+      // and before posting step k every DMA issued before step k - 1 has landed (column k + w + 1,
+      // first touched by the trailing waves at step k + 1, which wait for this post).
       auto cl_fwd = [&](int k0, int kend) __attribute__((always_inline)) {
-        const int qf = lane / 6 + 2, rf = lane - 6 * (lane / 6);
+        const int dr = lane >> 4;
+        const int npass = (6 * (w - 1) + 39) / 40;
+        int n_prev = 0;  // DMA pieces issued at the previous step
         for (int k = k0; k < kend; ++k) {
+          BST(30);
+          int n_now = 0;
+          if (k + w + 3 < snload) {
+            const double* src = ssys + (long)(k + w + 3) * CS + 2 * lane;
+            const unsigned dst = (unsigned)(uintptr_t)(colp(k + w + 3));
+            for (int t = 0; t < nDma; ++t)
+              asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst + 1024u * t),
+                           "v"(src + 128 * t)
+                           : "memory", "m0");
+            n_now = nDma;
+          }
           wait_ge(fl + 0, k + 1);
           wait_ge(fl + 3, k);
-          wait_ge(fl + 5, k);
+          BST(22);
           const double* ck = colp(k);
-          double L[21], r[6], y[6], row[6];
-#pragma unroll
-          for (int i = 0; i < 6; ++i)
-#pragma unroll
-            for (int c = 0; c <= i; c += 2) {
-              const double2 v = reinterpret_cast<const double2*>(ck + 6 * i)[c / 2];
-              L[P6(i, c)] = v.x;
-              if (c + 1 <= i) L[P6(i, c + 1)] = v.y;
-            }
+          double Lr[6], r[6], y[6];
+          ld6g(li < 6 ? ck + 6 * li : zb, Lr);
           ld6g(ck + 36 * R + 6, r);
           ld6g(ck + 36 * R, y);
-          const bool on = (qf <= w) & (k + qf < snload);
-          ld6g(on ? ck + 36 * qf + 6 * rf : zb, row);
-          const double yo = on ? colp(k + qf)[36 * R + rf] : 0.0;
-          fwd6(L, r, row);
-          if (on) {
-            st6g(const_cast<double*>(ck) + 36 * qf + 6 * rf, row);
-            colp(k + qf)[36 * R + rf] =
-                yo - (row[0] * y[0] + row[1] * y[1] + row[2] * y[2] + row[3] * y[3] + row[4] * y[4] + row[5] * y[5]);
+          for (int ps = 0; ps < npass; ++ps) {
+            const int ti = 40 * ps + 10 * dr + li - 6, q = 2 + ti / 6, rr = ti - 6 * (ti / 6);
+            const bool on = (li >= 6) & (ti < 6 * (w - 1)) & (k + q < snload);
+            double x[6];
+            ld6g(on ? ck + 36 * q + 6 * rr : zb, x);
+            const double yo = on ? colp(k + q)[36 * R + rr] : 0.0;
+            cl::solve_lt(x, Lr, r);
+            if (on) {
+              st6g(const_cast<double*>(ck) + 36 * q + 6 * rr, x);
+              colp(k + q)[36 * R + rr] =
+                  yo - (x[0] * y[0] + x[1] * y[1] + x[2] * y[2] + x[3] * y[3] + x[4] * y[4] + x[5] * y[5]);
+            }
           }
+          bad = bad | !isfinite(r[0] + r[1] + r[2] + r[3] + r[4] + r[5]) |
+                !isfinite(y[0] + y[1] + y[2] + y[3] + y[4] + y[5]);
+          switch (n_now + n_prev) {  // only the DMAs of this step and the previous one in flight
+            case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+            case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+            case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+            case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+            case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+            case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+            default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+          }
+          n_prev = n_now;
           post(fl + 2, k + 1);
+          BST(23);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       };
-      // trailing wave tw (0: role 1, 1: role 3)
+      // trailing waves: the step-k update X -= P P^T of the window X = blocks (k + 1 .. k + w)^2
+      // (lower blocks; the chain's (k+1, k+1) and (k+2, k+1) excluded) with P = the panel rows
+      // L_{k+1..k+w, k}, as 16x16 f64 tiles on the matrix cores (v_mfma_f64_16x16x4f64, two
+      // k-steps for the six panel columns; D element reg e of lane l: window row 16 ti +
+      // (l >> 4) + 4 e, column 16 tj + (l & 15); A / B operand: P[16 t + (l & 15)][4 s + (l >> 4)]).
+      // Wave 0 (role 1) owns tile column 0 (window blocks 0..2: everything the chain and the
+      // forward wave wait for), wave 1 (role 3) the other tiles.  Tile column 0 of step k + 1
+      // overlaps the other tiles of step k, so wave 0 waits for wave 1's previous step.
       auto cl_trail = [&](int k0, int kend, int tw) __attribute__((always_inline)) {
-        const int nr = tw ? A.cl_rounds1 : A.cl_rounds0;
-        int desc[kClRounds];
+        const int nt = (6 * w + 15) / 16;
+        int tti[kClTiles], ttj[kClTiles], nti = 0;
+        for (int ti = 0; ti < nt; ++ti)
+          for (int tj = 0; tj <= ti; ++tj)
+            if ((tj == 0) == (tw == 0) && nti < kClTiles) {
+              tti[nti] = ti;
+              ttj[nti] = tj;
+              ++nti;
+            }
+        // per element: offset from column k + 1 (-1: never stored) and its row block
+        int off[kClTiles][4], rb[kClTiles][4];
 #pragma unroll
-        for (int h = 0; h < kClRounds; ++h) desc[h] = A.tab[A.cl + (kClRounds * tw + h) * 64 + lane];
-        lds_flag* const f1 = fl + (tw ? 5 : 3);
-        lds_flag* const fa = fl + (tw ? 6 : 4);
-        lds_flag* const fo = fl + (tw ? 4 : 6);
+        for (int t = 0; t < kClTiles; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i = 16 * tti[t < nti ? t : 0] + (lane >> 4) + 4 * e, j = 16 * ttj[t < nti ? t : 0] + (lane & 15);
+            const int bi = i / 6, bj = j / 6;
+            const bool ok = t < nti && i < 6 * w && j < 6 * w && bi >= bj && !(bj == 0 && bi <= 1);
+            off[t][e] = ok ? bj * SS + 36 * (bi - bj) + 6 * (i - 6 * bi) + (j - 6 * bj) : -1;
+            rb[t][e] = bi;
+          }
+        // operands: P row 16 t + (l & 15), column 4 s + (l >> 4) of column k
+        int opo[kClTileRows][2], opb[kClTileRows];
+#pragma unroll
+        for (int t = 0; t < kClTileRows; ++t) {
+          const int i = 16 * t + (lane & 15), bi = i / 6;
+          opb[t] = bi;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int kk = 4 * s2 + (lane >> 4);
+            opo[t][s2] = (t < nt && i < 6 * w && kk < 6) ? 36 * (1 + bi) + 6 * (i - 6 * bi) + kk : -1;
+          }
+        }
+        lds_flag* const fme = fl + (tw ? 4 : 3);
         for (int k = k0; k < kend; ++k) {
+          BST(30);
           wait_ge(fl + 2, k + 1);
           wait_ge(fl + 1, k + 1);
-          wait_ge(fo, k);
+          if (tw == 0) wait_ge(fl + 4, k);
+          BST(24);
           const double* ck = colp(k);
+          const double* cx = colp(k + 1);
+          double opv[kClTileRows][2];
 #pragma unroll
-          for (int h = 0; h < kClRounds; ++h) {
-            if (h >= nr) break;
-            const int d = desc[h];
-            const bool isv = d >= 0 && (d >> 16);
-            const int jj = (d >> 8) & 15, qi = (d >> 4) & 15, rr = d & 15;
-            const bool vok = isv & (k + jj < snload);
-            const bool tok = (d >= 0) & !isv & (k + qi < snload);
-            double vrow[6], u[6], out[6];
-            ld6g(vok ? ck + 36 * jj + 6 * rr : zb, vrow);
-            ld6g(tok ? ck + 36 * qi + 6 * rr : zb, u);
-            double* tg = colp(k + jj) + 36 * (qi - jj) + 6 * rr;
-            ld6g(tok ? tg : zb, out);
-            cl::sub_uvt<0>(out, u, vrow);
-            if (tok) st6g(tg, out);
-            if (h == 0) post(f1, k + 1);
+          for (int t = 0; t < kClTileRows; ++t)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              const bool on = (opo[t][s2] >= 0) & (k + 1 + opb[t] < snload);
+              opv[t][s2] = *(on ? ck + opo[t][s2] : zb);
+            }
+          d4 acc[kClTiles];
+#pragma unroll
+          for (int t = 0; t < kClTiles; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const bool on = (off[t][e] >= 0) & (k + 1 + rb[t][e] < snload);
+              acc[t][e] = *(on ? cx + off[t][e] : zb);
+            }
+#pragma unroll
+          for (int t = 0; t < kClTiles; ++t) {
+            if (t >= nti) break;
+            double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+#pragma unroll
+            for (int tt = 0; tt < kClTileRows; ++tt) {
+              if (tt == tti[t]) { a0 = -opv[tt][0]; a1 = -opv[tt][1]; }
+              if (tt == ttj[t]) { b0 = opv[tt][0]; b1 = opv[tt][1]; }
+            }
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[t], 0, 0, 0);
           }
-          if (nr == 0) post(f1, k + 1);
-          post(fa, k + 1);
+#pragma unroll
+          for (int t = 0; t < kClTiles; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if ((off[t][e] >= 0) & (k + 1 + rb[t][e] < snload)) const_cast<double*>(cx)[off[t][e]] = acc[t][e];
+          post(fme, k + 1);
+          BST(25);
         }
       };
       auto cl_phase = [&](int k0, int kend, bool flush) __attribute__((always_inline)) {
@@ -914,17 +976,22 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
         // into the top's (fixed order), then the top's four waves continue through the
         // separator while the bottom's form the G blocks of the rows final after phase A
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        BST(30);
         __syncthreads();
+        BST(26);
         for (int e = tid; e < A.n_merge; e += kBandThreads) {
           const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
           dyn[d.x] += dyn[d.y];
         }
         __syncthreads();
+        BST(27);
         if (side == 0) {
           cl_phase(m, m + sp, false);
+          BST(28);
         } else {
           const int n0 = 6 * (m + nb) * w;
           for (int e = 64 * role + lane; e < n0; e += 256) g_item(0, e);
+          BST(29);
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
