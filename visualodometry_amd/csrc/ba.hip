@@ -47,7 +47,7 @@
 #include "vo_ctx.h"
 
 #ifndef VO_BA_CL
-#define VO_BA_CL 1  // tuning build: 0 keeps the per-step barrier elimination in full mode
+#define VO_BA_CL 0  // 1: the critical-lane elimination in full mode (experimental; slower so far)
 #endif
 #ifndef VO_BA_FUSE
 #define VO_BA_FUSE 1  // tuning build: 0 launches K2 on its own

@@ -85,8 +85,11 @@ BandTables band_tables(int F, const BandSplit& b, const BandLds& L) {
       const int j = m + jj, i = j + qq;
       for (int r = 0; r < 6; ++r)
         for (int c = 0; c < 6; ++c) {
+          // the bottom side stores its blocks transposed; a diagonal block is symmetric, so its
+          // own lower triangle is the source (the critical-lane trailing tiles keep only the
+          // lower triangle of a diagonal block that straddles two 16-row tiles up to date)
           T.tab.push_back((j % RC) * SS + 36 * qq + 6 * r + c);
-          T.tab.push_back(offB + ((F - 1 - i) % RC) * SS + 36 * qq + 6 * c + r);
+          T.tab.push_back(offB + ((F - 1 - i) % RC) * SS + 36 * qq + (qq == 0 ? 6 * r + c : 6 * c + r));
         }
     }
   for (int d = 0; d < sp; ++d) {
