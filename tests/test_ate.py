@@ -68,10 +68,15 @@ def test_long_drive_reaches_the_full_window():
     sizes = g["win_sizes"]
     assert sizes[:, 0].max() == 50
     assert sizes[:, 1].max() <= 20000 and sizes[:, 1].max() >= 19000
-    full, mid = (int(i) for i in g["win_index"])
+    full, mid = (int(i) for i in g["win_index"][:2])
     assert g["win0_poses"].shape[0] == 50 and sizes[full, 0] == 50
-    assert 0 < g["win1_poses"].shape[0] < 50 and tuple(sizes[mid]) == (
-        g["win1_poses"].shape[0], g["win1_points"].shape[0], g["win1_obs_uv"].shape[0])
+    assert 0 < g["win1_poses"].shape[0] < 50
+    # every kept window (the GPU replays each: tests/test_gpu_reference_trace.py) is the call
+    # win_index names, spread over the drive
+    assert int(g["n_win"]) == len(g["win_index"]) >= 2
+    for i, j in enumerate(g["win_index"]):
+        assert tuple(sizes[int(j)]) == (g[f"win{i}_poses"].shape[0], g[f"win{i}_points"].shape[0],
+                                        g[f"win{i}_obs_uv"].shape[0])
 
 
 def test_long_drive_mid_window_matches_c_oracle():

@@ -107,16 +107,21 @@ def long_trace():
     return dict(np.load(GOLDEN / "reference_trace_long.npz"))
 
 
-@pytest.mark.parametrize("i", [0, 1], ids=["full_window", "mid_window"])
+@pytest.mark.parametrize("i", range(8), ids=["full_window", "mid_window"] + [f"drive_window_{j}" for j in range(6)])
 def test_long_drive_window_ba_replay(long_trace, i):
     """The north-star window size assembled by the reference's own classes: the 1300-frame
     drive's last 50-keyframe window (``_create_keyframe``, ``vo.py:252-288``, with
-    ``_prune_map``'s cap, ``vo.py:35-47``) and a mid-size one, replayed through the HIP
-    ``SlidingWindowBA`` against the C oracle's solution recorded with them."""
+    ``_prune_map``'s cap, ``vo.py:35-47``), a mid-size one and six more spread over the drive's
+    51 keyframe calls (``win_index``), replayed through the HIP ``SlidingWindowBA`` against the
+    C oracle's solution recorded with them -- the windows behind ``test_ate.py``'s BA
+    trajectory."""
     g = long_trace
+    if i >= int(g["n_win"]):
+        pytest.skip("fixture keeps fewer windows")
     w = _call(g, "win", i)
     res = SlidingWindowBA(g["K"], iters=int(w["iters"]), lam=float(w["lam"])).optimize(
-        BAWindow(w["poses"], w["points"], w["obs_uv"], w["obs_cam"], w["obs_pt"], int(w["n_fixed"])))
+        BAWindow(w["poses"], np.asarray(w["points"], np.float64), w["obs_uv"], w["obs_cam"], w["obs_pt"],
+                 int(w["n_fixed"])))
     assert res.status == "ok", res.message
     np.testing.assert_allclose(res.cost_per_iter, w["costs"], rtol=REL)
     dP, dPr = res.poses_cw - w["poses"], w["P"] - w["poses"]

@@ -451,6 +451,18 @@ __device__ __forceinline__ double sum_parts(double v, int np) {
   return v;
 }
 
+// The same butterfly with a per-lane group width 2^lg (0..3): groups are aligned to their
+// width, so each step only ever combines lanes of one group; lanes of narrower groups keep
+// their value (select).  Every lane of the wave must execute it.
+__device__ __forceinline__ double sum_parts_lane(double v, int lg) {
+  const double a = dpp_f64<0xB1>(v);
+  v = lg >= 1 ? v + a : v;
+  const double b = dpp_f64<0x4E>(v);
+  v = lg >= 2 ? v + b : v;
+  const double c = dpp_f64<0x104>(v);
+  return lg >= 3 ? v + c : v;
+}
+
 // Diagnostic build (VO_BA_STAMPS=1): thread 0 accumulates s_memtime deltas per
 // phase; the production instantiation has kStamp = false and executes none.
 // dst[i] = src[i] + add, i < n, by the workgroup: U loads per thread issued before
@@ -607,14 +619,23 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
     // two with two register sets: pair j+2's Z rows are fetched (16-byte LDS reads,
     // indices read two pairs ahead, clamped -- no branches) while pair j+1's 18 FMAs run.
     {
-      const int items = h3.z * 6;  // the chunk's active slots (ChunkImg::aslot)
-      const int np = parts_for(items);
-      for (int base = 0; base < items * np; base += kLinThreads) {
-        const int idx = base + tid, item = idx / np, part = idx % np;
-        const int si = item / 6, a = item - 6 * (item / 6);
-        const int s = item < items ? S.img.aslot[si] : 0;
+      // the chunk's active slots on balanced lanes (ChunkImg::abase / anp): lane tid -> entry
+      // si (binary search over the lane bases), row a, part of 2^lgp
+      // (a chunk with more than 42 active slots takes a second pass of one lane per row item)
+      static_assert(kLinLanes == kLinThreads, "planner lane budget = K1 workgroup");
+      const int nas = h3.z, lanes = S.img.abase[nas];
+      for (int base = 0; base < lanes; base += kLinThreads) {
+      const int t = base + tid;
+      int si = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if (si + st < nas && S.img.abase[si + st] <= t) si += st;
+      const bool live = t < lanes;
+      const int lgp = live ? S.img.anp[si] : 0, np = 1 << lgp;
+      const int off = t - S.img.abase[si], a = off >> lgp, part = off & (np - 1);
+      const int s = live ? S.img.aslot[si] : 0;
         double out[6] = {0, 0, 0, 0, 0, 0};
-        const int e0 = item < items ? S.img.slotp[si] + part : 0, e1 = item < items ? S.img.slotp[si + 1] : 0;
+        const int e0 = live ? S.img.slotp[si] + part : 0, e1 = live ? S.img.slotp[si] + S.img.apcnt[si] : 0;
         if (e0 < e1) {
           auto zrow = [&](int pr, double (&za)[3], double2 (&zy)[9]) {
             const double2* py = reinterpret_cast<const double2*>(S.Z[pr >> 8]);
@@ -650,10 +671,9 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
           }
           if (j < n) accum(zaA, zyA);
         }
-        if (np > 1)
 #pragma unroll
-          for (int c = 0; c < 6; ++c) out[c] = sum_parts(out[c], np);
-        if (item < items && part == 0)
+        for (int c = 0; c < 6; ++c) out[c] = sum_parts_lane(out[c], lgp);
+        if (live && part == 0)
 #pragma unroll
           for (int c = 0; c < 6; ++c) S.win[36 * s + 6 * a + c] += out[c];
       }

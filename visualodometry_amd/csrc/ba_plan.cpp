@@ -716,12 +716,49 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         // the slots with pairs in this chunk and the cameras with track entries or observations
         // in it, compacted in window order (their lists keep their order)
         int nas = 0, nac = 0;
-        for (int i = 0; i < ns; ++i)
-          if (P.slot_ptr[sb + i + 1] > P.slot_ptr[sb + i]) {
-            g.aslot[nas] = (uint8_t)i;
-            g.slotp[nas++] = P.slot_ptr[sb + i] - e0;
+        {
+          // active slots; lanes per row item doubled greedily for the slot with the longest
+          // per-lane pair chain while 6 lanes x the sum fit K1's workgroup (kLinLanes; more
+          // than 42 active slots take one lane per row item, in two passes)
+          int sl[kSegSlots], cntp[kSegSlots], lg[kSegSlots];
+          for (int i = 0; i < ns; ++i)
+            if (P.slot_ptr[sb + i + 1] > P.slot_ptr[sb + i]) {
+              sl[nas] = i;
+              cntp[nas] = P.slot_ptr[sb + i + 1] - P.slot_ptr[sb + i];
+              lg[nas++] = 0;
+            }
+          int used = nas;
+          for (;;) {
+            int best = -1, chain = 0;
+            for (int i = 0; i < nas; ++i) {
+              const int c = (cntp[i] + (1 << lg[i]) - 1) >> lg[i];
+              if (c > chain) {
+                chain = c;
+                best = i;
+              }
+            }
+            if (best < 0 || chain <= 1 || lg[best] == 3 || 6 * (used + (1 << lg[best])) > kLinLanes) break;
+            used += 1 << lg[best];
+            ++lg[best];
           }
-        g.slotp[nas] = e1 - e0;
+          // order by lanes per row, descending (stable): every item group starts at a multiple
+          // of its own width
+          int ord[kSegSlots];
+          for (int i = 0; i < nas; ++i) ord[i] = i;
+          std::stable_sort(ord, ord + nas, [&](int a, int b) { return lg[a] > lg[b]; });
+          int base = 0;
+          for (int j = 0; j < nas; ++j) {
+            const int i = ord[j];
+            g.aslot[j] = (uint8_t)sl[i];
+            g.slotp[j] = P.slot_ptr[sb + sl[i]] - e0;
+            g.apcnt[j] = (uint16_t)cntp[i];
+            g.anp[j] = (uint8_t)lg[i];
+            g.abase[j] = (uint16_t)base;
+            base += 6 << lg[i];
+          }
+          g.abase[nas] = (uint16_t)base;
+          g.slotp[nas] = e1 - e0;
+        }
         for (int i = 0; i < e1 - e0; ++i) g.pairs[i] = P.pair_list[e0 + i];
         for (int i = 0; i < nc; ++i)
           if (P.cam_ptr[cb + i + 1] > P.cam_ptr[cb + i] || P.camo_ptr[cb + i + 1] > P.camo_ptr[cb + i]) {

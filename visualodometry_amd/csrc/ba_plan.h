@@ -52,6 +52,7 @@ constexpr int kChunkTe = VO_CHUNK_OBS;
 constexpr int kChunkPts = VO_CHUNK_OBS / 2;
 constexpr int kChunkPairs = 8 * VO_CHUNK_OBS;  // camera-pair (x, y) entries of one chunk, staged in LDS
 constexpr int kSegSlots = 64;
+constexpr int kLinLanes = 256;  // K1 workgroup size (ba.hip kLinThreads)
 constexpr int kChunkHdr = 16;
 
 constexpr int kSegCams = 24;     // free (window) cameras of a segment
@@ -71,27 +72,35 @@ constexpr int kSegHdr = 48;
 // chunk-relative, types as K1 reads them): staging a chunk is one 16-byte load and one
 // LDS store per thread instead of a load per list.  Unused entries are zero.
 struct alignas(16) ChunkImg {
-  int32_t obs_te[kChunkObs];       // observation -> chunk track entry
-  int32_t te_obs[kChunkTe + 1];    // track entry -> first chunk observation
-  int32_t te_pt[kChunkTe];         // track entry -> chunk landmark
-  int32_t te_lcam[kChunkTe];       // track entry -> window camera, -1 if fixed
-  int32_t pt_te[kChunkPts + 1];    // landmark -> first chunk track entry
+  // byte-wide lists (every index < 64 and every count <= 64, kChunkObs): the image, and K1's
+  // LDS with it, stays under a third of the CU after the LDS allocation granule
+  uint8_t obs_te[kChunkObs];       // observation -> chunk track entry
+  uint8_t te_obs[kChunkTe + 1];    // track entry -> first chunk observation
+  uint8_t te_pt[kChunkTe];         // track entry -> chunk landmark
+  int8_t te_lcam[kChunkTe];        // track entry -> window camera, -1 if fixed
+  uint8_t pt_te[kChunkPts + 1];    // landmark -> first chunk track entry
   // Only the window slots and cameras this chunk touches (header ints 14 and 15 count them),
   // so K1's Schur loops run over the chunk's own items, not the whole segment window.
-  int32_t slotp[kSegSlots + 1];    // active slot i -> first pair-list entry (pairs by slot)
-  int32_t camp[kSegCams + 1];      // active camera i -> first track-entry list entry
-  int32_t camop[kSegCams + 1];     // active camera i -> first observation list entry
-  int32_t dslot[kSegCams];         // active camera i -> its diagonal slot
+  uint16_t slotp[kSegSlots + 1];   // active slot i -> its first pair-list entry
+  uint8_t camp[kSegCams + 1];      // active camera i -> first track-entry list entry
+  uint8_t camop[kSegCams + 1];     // active camera i -> first observation list entry
+  uint8_t dslot[kSegCams];         // active camera i -> its diagonal slot
   uint8_t aslot[kSegSlots];        // active slot i -> window slot
   uint8_t acid[kSegCams];          // active camera i -> window camera
-  uint8_t pad_[8];
-  uint16_t pairs[kChunkPairs];     // (te_x | te_y << 8) by slot
+  // Schur-pair lanes, balanced: active slot i (ordered by lanes-per-row descending) sums its
+  // apcnt[i] pairs from slotp[i] on 6 << anp[i] lanes starting at abase[i] (2^anp lanes per
+  // row, their strided partial sums combined by an aligned butterfly); abase[nas] = lanes used
+  uint16_t apcnt[kSegSlots];
+  uint16_t abase[kSegSlots + 1];  // up to 6 x 64 lanes (two passes of the workgroup)
+  uint8_t anp[kSegSlots];
+  alignas(2) uint16_t pairs[kChunkPairs];  // (te_x | te_y << 8) by slot
   uint8_t caml[kChunkTe];          // track entries by window camera
   uint8_t camol[kChunkObs];        // observations by window camera
   alignas(8) float uv[2 * kChunkObs];
   uint8_t acam[kChunkObs];         // observation -> camera seen (pose index in LDS)
 };
 static_assert(sizeof(ChunkImg) % 16 == 0, "16-byte staging granules");
+static_assert(kChunkObs <= 64 && kChunkTe <= 64 && kChunkPairs <= 65535, "byte-wide chunk lists");
 
 // Host memory of the chunk images (defined in ba.hip): page-locked (hipHostMalloc) for the
 // BA engine's plan, so vo_ba_setup's upload of the largest plan array is an asynchronous
