@@ -21,8 +21,8 @@ KEEP = ("match_kernel", "fsweep_kernel", "frerank_kernel", "pack_kernel", "fpack
 
 def short(name: str) -> str:
     n = name.replace(" ", "")
-    for key, s in (("match_kernel<2>", "match_i8 (match_kernel<2>)"), ("fsweep_kernel<1>", "fsweep<1>"),
-                   ("fsweep_kernel<2>", "fsweep<2>"), ("frerank_kernel", "frerank"), ("fpack_kernel", "fpack"),
+    for key, s in (("match_kernel<2>", "match_i8 (match_kernel<2>)"), ("fsweep_kernel<1", "fsweep<1>"),
+                   ("fsweep_kernel<2", "fsweep<2>"), ("frerank_kernel", "frerank"), ("fpack_kernel", "fpack"),
                    ("pack_kernel", "pack"), ("merge_kernel", "merge")):
         if key in n:
             return s
