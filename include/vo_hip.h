@@ -169,7 +169,9 @@ int vo_ba_solve(vo_ctx* ctx, const vo_ba_problem* prob, double* poses, double* p
 /* Static plan statistics (for DESIGN.md/bench): fills up to n int64 values:
  * [0] chunks [1] segments [2] slab blocks [3] reduced blocks [4] profile
  * blocks [5] track entries [6] bytes read+written per GN iteration
- * (algorithmic) [7] wide landmarks. Returns count written. */
+ * (algorithmic) [7] banded solver in use [8] first-camera groups and
+ * [9] chunks the last vo_ba_setup took over from the previous window's plan (the slide)
+ * [10] observations per segment the plan was packed for. Returns count written. */
 int vo_ba_plan_stats(vo_ctx* ctx, int64_t* out, int n);
 
 /* Diagnostic only: with VO_BA_STAMPS=1 in the environment at vo_ba_setup, K1
@@ -216,7 +218,8 @@ int vo_ba_group_by_point(int n_points, int n_obs, const int32_t* obs_pt, int32_t
 int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* out, int n);
 /* Host only: a 64-bit FNV-1a digest of every array of the static plan (chunks, segments,
  * slab layout, pair and camera lists, profile, K3 step tables) for `prob`; it pins the plan
- * (and so every kernel's summation order) across planner changes (tests/golden). */
+ * (and so every kernel's summation order) across planner changes (tests/golden).  The plan is
+ * packed for ceil(n_obs / target_segments) observations per segment. */
 int vo_ba_plan_digest(const vo_ba_problem* prob, int target_segments, uint64_t* digest);
 
 /* ---- triangulation ----------------------------------- */

@@ -28,6 +28,13 @@ int vo_ba_split_reduce(vo_ctx* ctx, int on);
  * failed factorisation.  n = 0 restores normal launches. */
 int vo_ba_testing_drop_reducers(vo_ctx* ctx, int n);
 
+/* Host only: the digest (as vo_ba_plan_digest) of the plan of `cur` packed for seg_obs
+ * observations per segment, built from scratch when prev is NULL, else after a from-scratch
+ * plan of `prev` (same seg_obs) as vo_ba_setup builds it on a window slide: taking over
+ * prev's unchanged first-camera groups.  *reused_chunks (may be NULL): chunks taken over. */
+int vo_ba_testing_plan_slide(const vo_ba_problem* prev, const vo_ba_problem* cur, int seg_obs, uint64_t* digest,
+                             int64_t* reused_chunks);
+
 #ifdef __cplusplus
 }
 #endif

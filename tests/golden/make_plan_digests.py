@@ -1,9 +1,9 @@
 """Writes tests/golden/plan_digests.json: vo_ba_plan_digest of the synthetic BA windows at
 several segment targets.  A planner rewrite must reproduce these exactly (the plan fixes
-every kernel's summation order); a deliberate plan change regenerates them.  Round 2
-packs landmark ranges in parallel (a segment boundary at each of up to 8 range starts,
-ba_plan.cpp plan_parts); built with -DVO_PLAN_PARTS=1 it reproduces the round-1 digests
-bit for bit (cfg3@1024: 5fba5fac5e8400c5).  Usage: python tests/golden/make_plan_digests.py"""
+every kernel's summation order); a deliberate plan change regenerates them.  Round 4 packs
+every first-camera group on its own (a segment boundary at each group start: the
+slide-stable plan that a window's next plan can take groups over from, ba_plan.cpp).
+Usage: python tests/golden/make_plan_digests.py"""
 import json
 import sys
 from pathlib import Path

@@ -204,3 +204,70 @@ def test_plan_input_errors_report_the_first_violation():
     ptr[[17001, 4001]] = ptr[[17001, 4001]] + 10**6  # breaks monotonicity at 17001 and 4001
     assert "point_ptr not monotone at 4001" in err(ptr, cam)
     assert "point_ptr not monotone at 4001" in err(ptr, cam0)
+
+
+def _win(p):
+    return (p.point_ptr, p.obs_cam, p.obs_uv, p.poses_cw.shape[0], p.n_fixed)
+
+
+def test_slide_plan_equals_scratch_plan():
+    """A window's plan built by taking over the previous window's unchanged first-camera
+    groups (what vo_ba_setup does on every keyframe, the window having slid by one) is the
+    from-scratch plan of that window byte for byte, and takes most of the chunks over."""
+    from visualodometry_amd.ba import plan_slide_digest
+    from visualodometry_amd.synthetic import make_ba_slide
+
+    ws = make_ba_slide("cfg3", 3)
+    so = -(-ws[0].obs_cam.size // 671)
+    for a, b in zip(ws, ws[1:]):
+        d_inc, reused = plan_slide_digest(a.K, _win(a), _win(b), so)
+        d_new, none = plan_slide_digest(a.K, None, _win(b), so)
+        st = plan_probe(b.K, b.point_ptr, b.obs_cam, b.obs_uv, b.poses_cw.shape[0], b.n_fixed,
+                        -(-b.obs_cam.size // so))
+        assert d_inc == d_new and none == 0
+        assert reused >= 0.7 * st["chunks"], (reused, st["chunks"])
+
+
+def test_grown_and_repeated_window_plans_equal_scratch():
+    """A window that grew by one keyframe (no eviction: groups keep their cameras) and the
+    same window again take groups over at the same camera; the plans equal scratch plans."""
+    from visualodometry_amd.ba import plan_slide_digest
+
+    p = make_ba_problem(30, 3000, 5)
+    obs_pt = np.repeat(np.arange(p.n_points), np.diff(p.point_ptr))
+    inw = p.obs_cam < 29
+    cnt = np.bincount(obs_pt[inw], minlength=p.n_points)
+    keep = cnt >= 2
+    sel = inw & keep[obs_pt]
+    ptr = np.concatenate([[0], np.cumsum(cnt[keep])]).astype(np.int32)
+    small = (ptr, p.obs_cam[sel], p.obs_uv[sel], 29, p.n_fixed)
+    full = _win(p)
+    for prev, cur in ((small, full), (full, full)):
+        d_inc, reused = plan_slide_digest(p.K, prev, cur, 40)
+        d_new, _ = plan_slide_digest(p.K, None, cur, 40)
+        assert d_inc == d_new and reused > 0
+
+
+def test_slide_plan_with_changed_groups():
+    """Groups whose landmarks changed (an observation moved, a landmark's track cut, the
+    fixed/free boundary) are repacked; the rest taken over; still the scratch plan."""
+    from visualodometry_amd.ba import plan_slide_digest
+    from visualodometry_amd.synthetic import make_ba_slide
+
+    a, b = make_ba_slide("cfg2", 2)
+    so = 37
+    _, base = plan_slide_digest(a.K, _win(a), _win(b), so)
+    uv = b.obs_uv.copy()
+    mid = b.obs_cam.size // 2
+    uv[mid, 0] += np.float32(0.25)  # one observation of a middle group moved
+    ptr = b.point_ptr.copy()
+    cam = b.obs_cam.copy()
+    wb = (ptr, cam, uv, b.poses_cw.shape[0], b.n_fixed)
+    d_inc, reused = plan_slide_digest(a.K, _win(a), wb, so)
+    d_new, _ = plan_slide_digest(a.K, None, wb, so)
+    assert d_inc == d_new
+    assert 0 < reused < base
+    # different n_fixed or seg_obs: nothing is taken over (and still the scratch plan)
+    wf = (ptr, cam, uv, b.poses_cw.shape[0], b.n_fixed + 1)
+    d_inc, reused = plan_slide_digest(a.K, _win(a), wf, so)
+    assert reused == 0 and d_inc == plan_slide_digest(a.K, None, wf, so)[0]

@@ -383,3 +383,38 @@ def test_two_sessions_on_one_context(ctx):
     assert rc == _lib.VO_OK
     with pytest.raises(VoError):
         s2.get_state()
+
+
+def test_slide_takes_groups_over_and_matches_scratch(ctx):
+    """Consecutive keyframe windows on one context: each vo_ba_setup takes the unchanged
+    first-camera groups of the previous window's plan over (chunk images copied on the
+    device, not rebuilt or uploaded), and every result is bitwise the one of a setup from
+    scratch (an unrelated window set up in between), which also matches the C oracle."""
+    from visualodometry_amd.synthetic import make_ba_slide
+
+    ws = make_ba_slide("cfg3", 3)
+    other = make_ba_config("cfg1")
+    iters = 3
+    inc = []
+    for i, w in enumerate(ws):
+        s = _session(w, ctx)
+        st = s.plan_stats()
+        if i:
+            assert st["reused_chunks"] >= 0.7 * st["chunks"], st
+        rc, costs = s.run(iters)
+        assert rc == _lib.VO_OK
+        inc.append((costs, *s.get_state()))
+    for w, (costs, P, X) in zip(ws, inc):
+        _session(other, ctx).run(1)
+        s = _session(w, ctx)
+        assert s.plan_stats()["reused_chunks"] == 0
+        rc, c2 = s.run(iters)
+        P2, X2 = s.get_state()
+        np.testing.assert_array_equal(c2, costs)
+        np.testing.assert_array_equal(P2, P)
+        np.testing.assert_array_equal(X2, X)
+    w = ws[-1]
+    R = cref.BAProblemRef(w.K, w.point_ptr, w.obs_cam, w.obs_uv, w.n_poses, w.n_fixed, 1.0)
+    n, Pr, Xr, cr = R.solve(w.poses_cw, w.points, iters, nthreads=8)
+    np.testing.assert_allclose(inc[-1][0], cr, rtol=REL)
+    assert _rel(inc[-1][1], Pr) < REL

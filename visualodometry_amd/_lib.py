@@ -106,6 +106,7 @@ SIGNATURES = {
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_ba_split_reduce": (_I, [_P, _I]),
     "vo_ba_testing_drop_reducers": (_I, [_P, _I]),
+    "vo_ba_testing_plan_slide": (_I, [C.c_void_p, C.c_void_p, _I, C.POINTER(C.c_uint64), _PI64]),
 }
 
 _lib = None

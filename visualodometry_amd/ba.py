@@ -153,6 +153,29 @@ def plan_digest(K, point_ptr, obs_cam, obs_uv, n_poses: int, n_fixed: int = 2, t
     return int(d.value)
 
 
+def plan_slide_digest(K, prev, cur, seg_obs: int) -> tuple:
+    """Host-only (test): ``(digest, reused_chunks)`` of the plan of window ``cur`` packed for
+    ``seg_obs`` observations per segment, built from scratch (``prev`` None) or by taking over
+    the unchanged first-camera groups of ``prev``'s plan, as ``vo_ba_setup`` does on a slide
+    (``vo_ba_testing_plan_slide``).  Windows: ``(point_ptr, obs_cam, obs_uv, n_poses, n_fixed)``."""
+    keep = []
+
+    def struct(w):
+        pp, oc, uv, n, nf = w
+        a = (np.ascontiguousarray(pp, dtype=np.int32), np.ascontiguousarray(oc, dtype=np.int32),
+             np.ascontiguousarray(uv, dtype=np.float32).reshape(-1, 2))
+        keep.append(a)
+        return _problem_struct(K, a[0], a[1], a[2], n, nf, 0.0)
+
+    pc = struct(cur)
+    pv = struct(prev) if prev is not None else None
+    d = C.c_uint64(0)
+    r = C.c_int64(0)
+    check(_lib.load().vo_ba_testing_plan_slide(C.byref(pv) if pv is not None else None, C.byref(pc), int(seg_obs),
+                                               C.byref(d), C.byref(r)), "vo_ba_testing_plan_slide")
+    return int(d.value), int(r.value)
+
+
 class BASession:
     """A BA problem resident on one device (structure + state in HBM).
 
@@ -224,10 +247,11 @@ class BASession:
         return rc, S, b, dc, float(cost[0])
 
     def plan_stats(self) -> dict:
-        out = np.zeros(8, dtype=np.int64)
-        n = check(self.ctx.lib.vo_ba_plan_stats(self.ctx.handle, ptr(out, C.c_int64), 8), "stats")
+        out = np.zeros(11, dtype=np.int64)
+        n = check(self.ctx.lib.vo_ba_plan_stats(self.ctx.handle, ptr(out, C.c_int64), 11), "stats")
         keys = ["chunks", "segments", "slab_blocks", "reduced_blocks", "profile_blocks",
-                "track_entries", "algorithmic_bytes_per_iter", "band_solver"]
+                "track_entries", "algorithmic_bytes_per_iter", "band_solver", "reused_groups",
+                "reused_chunks", "seg_obs"]
         return dict(zip(keys[:n], out[:n].tolist()))
 
 

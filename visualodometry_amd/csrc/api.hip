@@ -622,10 +622,29 @@ int vo_ba_plan_digest(const vo_ba_problem* prob, int target_segments, uint64_t* 
     vo::BAPlan P;
     std::string err = vo::build_plan(P, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed,
                                      prob->n_points ? prob->point_ptr : zero.data(), prob->obs_cam,
-                                     prob->obs_uv, target_segments);
+                                     prob->obs_uv, vo::seg_obs_for(prob->n_obs, target_segments));
     VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_plan_digest: %s", err.c_str());
     vo::build_profile(P, vo::local_profile_first(P));
     *digest = vo::plan_digest(P);
+  });
+}
+
+int vo_ba_testing_plan_slide(const vo_ba_problem* prev, const vo_ba_problem* cur, int seg_obs, uint64_t* digest,
+                             int64_t* reused_chunks) {
+  return guarded([&] {
+    VO_REQUIRE(cur && digest && seg_obs >= 1, VO_ERR_ARG, "vo_ba_testing_plan_slide: bad argument");
+    std::vector<int32_t> zero(1, 0);
+    vo::BAPlan A, B;
+    auto build = [&](vo::BAPlan& P, const vo_ba_problem* p, const vo::BAPlan* from) {
+      std::string err = vo::build_plan(P, p->n_poses, p->n_points, p->n_obs, p->n_fixed,
+                                       p->n_points ? p->point_ptr : zero.data(), p->obs_cam, p->obs_uv, seg_obs, from);
+      VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_testing_plan_slide: %s", err.c_str());
+      vo::build_profile(P, vo::local_profile_first(P));
+    };
+    if (prev) build(A, prev, nullptr);
+    build(B, cur, prev ? &A : nullptr);
+    *digest = vo::plan_digest(B);
+    if (reused_chunks) *reused_chunks = B.reused_chunks;
   });
 }
 
@@ -675,7 +694,7 @@ int vo_ba_plan_probe(const vo_ba_problem* prob, int target_segments, int64_t* ou
     vo::BAPlan P;
     std::string err = vo::build_plan(P, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed,
                                      prob->n_points ? prob->point_ptr : zero.data(), prob->obs_cam,
-                                     prob->obs_uv, target_segments);
+                                     prob->obs_uv, vo::seg_obs_for(prob->n_obs, target_segments));
     VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_plan_probe: %s", err.c_str());
     vo::build_profile(P, vo::local_profile_first(P));
     int64_t max_pairs = 0, max_slots = 0, max_cams = 0;

@@ -1269,12 +1269,22 @@ class BAEngine {
     else if (!((prob->n_points == 0 || prob->point_ptr) && (prob->n_obs == 0 || (prob->obs_cam && prob->obs_uv))))
       err = "null arrays";
     else if (prob->n_points == 0 && prob->n_obs != 0) err = "observations without points";
+    // the last plan whose images reached the device: the next window's plan takes over its
+    // unchanged first-camera groups (ba_plan.h build_plan)
+    const bool prev_ok = plan_ok_;
+    plan_ok_ = false;
     if (err.empty()) {
-      const int target = segments_target(ctx_->num_cus);
+      const int ideal = seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus));
+      // the packing target stays the previous plan's while it is within 10 % of this window's
+      // (a plan can take over groups only from a plan with the same target)
+      const int so = prev_ok && plan_.seg_obs * 10 >= ideal * 9 && plan_.seg_obs * 10 <= ideal * 11 ? plan_.seg_obs
+                                                                                                  : ideal;
       std::vector<int32_t> zero_ptr(1, 0);
       const int32_t* pp = prob->n_points ? prob->point_ptr : zero_ptr.data();
+      std::swap(plan_, prev_plan_);
+      d_chunk_img_.swap(d_chunk_img_prev_);
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
-                       prob->obs_uv, target);
+                       prob->obs_uv, so, prev_ok ? &prev_plan_ : nullptr);
     }
     if (ctx_->comm && ctx_->comm->nranks > 1) {
       const int32_t F = err.empty() ? plan_.n_free : 0;
@@ -1289,8 +1299,27 @@ class BAEngine {
     }
     VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_setup: %s", err.c_str());
     // the largest plan array first: from page-locked memory the copy runs while the host
-    // builds the profile and the K3 tables
-    upload(d_chunk_img_, plan_.chunk_img, ctx_->stream);
+    // builds the profile and the K3 tables.  Images taken over from the previous plan are
+    // copied on the device, in runs of consecutive chunks.
+    {
+      const BAPlan& P = plan_;
+      const int nch = (int)P.chunk_img.size();
+      d_chunk_img_.reserve(std::max(nch, 1) * sizeof(ChunkImg));
+      for (int c0 = 0; c0 < nch;) {
+        const int src = c0 < (int)P.chunk_src.size() ? P.chunk_src[c0] : -1;
+        int c1 = c0 + 1;
+        while (c1 < nch && (src < 0 ? P.chunk_src[c1] < 0 : P.chunk_src[c1] == src + (c1 - c0))) ++c1;
+        ChunkImg* dst = d_chunk_img_.as<ChunkImg>() + c0;
+        const size_t bytes = (size_t)(c1 - c0) * sizeof(ChunkImg);
+        if (src >= 0)
+          VO_HIP_CHECK(hipMemcpyAsync(dst, d_chunk_img_prev_.as<ChunkImg>() + src, bytes, hipMemcpyDeviceToDevice,
+                                      ctx_->stream));
+        else
+          VO_HIP_CHECK(hipMemcpyAsync(dst, P.chunk_img.data() + c0, bytes, hipMemcpyHostToDevice, ctx_->stream));
+        c0 = c1;
+      }
+      plan_ok_ = true;
+    }
     PLAN_T("setup: plan");
     std::vector<int32_t> first = local_profile_first(plan_);
     if (ctx_->comm && ctx_->comm->nranks > 1 && !first.empty()) {
@@ -1562,9 +1591,10 @@ class BAEngine {
 
   int stats(int64_t* out, int n) const {
     const BAPlan& P = plan_;
-    const int64_t v[8] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), (int64_t)P.slot_i.size(),
-                          P.n_prof_blocks(), P.n_te, P.algorithmic_bytes_per_iter(), band_on_ ? 1 : 0};
-    const int k = std::min(n, 8);
+    const int64_t v[11] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), (int64_t)P.slot_i.size(),
+                           P.n_prof_blocks(), P.n_te, P.algorithmic_bytes_per_iter(), band_on_ ? 1 : 0,
+                           P.reused_groups, P.reused_chunks, P.seg_obs};
+    const int k = std::min(n, 11);
     for (int i = 0; i < k; ++i) out[i] = v[i];
     return k;
   }
@@ -1803,6 +1833,8 @@ class BAEngine {
 
   vo_ctx* ctx_;
   BAPlan plan_{true};  // page-locked chunk images (async upload)
+  BAPlan prev_plan_{true};  // the previous window's plan (group take-over), or scratch
+  bool plan_ok_ = false;    // plan_ built and its images in d_chunk_img_
   vo_ba_problem prob_{};
   bool have_problem_ = false, have_state_ = false, pending_ = false, solve_lds_ = false;
   uint64_t session_ = 0;
@@ -1821,7 +1853,8 @@ class BAEngine {
   HostBuf h_state_;  // page-locked staging of set_state / get_state
   hipEvent_t h_state_ev_ = nullptr;  // set_state's upload from h_state_ done
   bool h_state_busy_ = false;
-  DevBuf d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;  // K1's plan (the chunk images hold every list)
+  DevBuf d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;
+  DevBuf d_chunk_img_prev_;  // the previous plan's images (prev_plan_)  // K1's plan (the chunk images hold every list)
   DevBuf d_stamps_, d_stamps3_;
   static constexpr bool stamps_on_ = kBaStamps;
 

@@ -172,6 +172,11 @@ __device__ __forceinline__ void band_barrier() { asm volatile("s_waitcnt lgkmcnt
 #ifndef VO_BA_EXP
 #define VO_BA_EXP 0
 #endif
+// 1: the panel factored by broadcast pivots on two chain waves (fixed lane mapping, kDc below);
+// 0: the round-2 chain (redundant chol6 per lane, rotating rows) and the forward wave
+#ifndef VO_BA_DPPCHAIN
+#define VO_BA_DPPCHAIN 0
+#endif
 // Diagnostic build only (EXTRA=-DVO_BA_STAMPS=1): lane 0 of each wave accumulates
 // s_memtime deltas per phase; the product build executes none.
 #if VO_BA_STAMPS
@@ -667,7 +672,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       if (VO_BA_EXP != 1) trail_step(p, sk);
       if (!kFull && p >= 1) rec_store(p - 1, v2);
     } else if (role == kFwd) {
-      if (VO_BA_EXP != 2) fwd_step(p, sk);
+      if (VO_BA_EXP != 2 && !VO_BA_DPPCHAIN) fwd_step(p, sk);
     } else if (role == kLoad) {
       if (VO_BA_EXP != 3) load_step(p);
     }
@@ -706,6 +711,78 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     for (int c = 0; c < 6; ++c) col[6 * c] = gv[c];
   };
 
+  // ---- DPP chain (kDc, VO_BA_DPPCHAIN): the panel of block column k on two chain waves (roles
+  // 0 and 3) with a fixed lane -> row mapping, factored by the right-looking broadcast pivots of
+  // ba_band_cl.h.  Per 16-lane DPP row: lanes 0..5 a copy of the diagonal block A_kk (every DPP
+  // row factors it, the same instructions on the same values), lanes 6..15 panel slots p =
+  // 40 c + 10 (lane >> 4) + li - 6 (c: chain wave): row p % 6 of block k + 1 + p / 6 for p < 6w,
+  // the rhs y_k for p = 6w.  So the factor phase before the barrier needs no LDS round trip:
+  // the pivots give L_kk, every L_{k+q,k} and y'_k at once.  After the barrier each lane moves to
+  // its row of column k + 1: target - u L_{k+1,k}^T, with u its row of L_{k+1+q,k} (the step-k
+  // factor of the block that row comes from; the diagonal lanes: L_{k+1,k}; the rhs: y'_k) and
+  // L_{k+1,k} broadcast from LDS; the panel lanes of blocks q >= 2 also apply y_{k+q} -= L_{k+q,k}
+  // y'_k (the rhs lane does q = 1 with its own update).  The trailing wave keeps the blocks
+  // (i, j), j >= k + 2, and the loader wave its streaming.
+  constexpr bool kDc = VO_BA_DPPCHAIN != 0;
+  const int dc_c = role == kChain ? 0 : 1;
+  const bool dc_wave = kDc && (role == kChain || role == kFwd);
+  const int dc_li = lane & 15;
+  const int dc_p = 40 * dc_c + 10 * (lane >> 4) + dc_li - 6;
+  const bool dc_diag = dc_li < 6;
+  const bool dc_panel = !dc_diag && dc_p < 6 * w;
+  const bool dc_rhs = !dc_diag && dc_p == 6 * w;
+  const int dc_q = dc_diag ? 0 : dc_panel ? 1 + dc_p / 6 : 0;  // block index in the column
+  const int dc_r = dc_diag ? dc_li : dc_panel ? dc_p - 6 * (dc_p / 6) : 0;
+  // the row owner writes it (the diagonal copies of DPP row 0 of the first chain wave)
+  const bool dc_own = dc_panel || dc_rhs || (dc_diag && dc_c == 0 && lane < 16);
+  double dcA[6] = {0, 0, 0, 0, 0, 0}, dcR[6] = {0, 0, 0, 0, 0, 0};
+  // this lane's row in the column in slot sk (offsets into dyn; idle lanes: the zero block)
+  auto dc_row = [&](int sk) __attribute__((always_inline)) {
+    const int base = (int)(sring - dyn) + sk * SS;
+    return dc_diag ? base + 6 * dc_r : dc_panel ? base + 36 * dc_q + 6 * dc_r : dc_rhs ? base + 36 * R : ZOFF;
+  };
+  auto dc_load = [&](int sk, int k) __attribute__((always_inline)) {
+    const bool ok = dc_diag || dc_rhs || (dc_panel && k + dc_q < snload);
+    ld6g(dyn + (ok ? dc_row(sk) : ZOFF), dcA);
+  };
+  auto dc_store = [&](int sk, int k) __attribute__((always_inline)) {
+    if (dc_own && (!dc_panel || k + dc_q < snload)) st6g(dyn + dc_row(sk), dcA);
+  };
+  auto dc_pre = [&](int k, int sk) __attribute__((always_inline)) {
+    cl::pivots(dcA, dcR);
+    bad = bad || (dc_c == 0 && lane == 0 && !isfinite(dcR[0] + dcR[1] + dcR[2] + dcR[3] + dcR[4] + dcR[5])) ||
+          (dc_rhs && !isfinite(dcA[0] + dcA[1] + dcA[2] + dcA[3] + dcA[4] + dcA[5]));
+    dc_store(sk, k);
+    if (dc_c == 0 && lane == 0) st6g(sring + sk * SS + 36 * R + 6, dcR);
+  };
+  // column k (slot sk) -> column k + 1 (slot sk1), after the barrier
+  auto dc_post = [&](int k, int sk, int sk1) __attribute__((always_inline)) {
+    const double* col = sring + sk * SS;
+    const bool tok = dc_diag || dc_rhs || (dc_panel && k + 1 + dc_q < snload);
+    double tg[6], u[6], V[6][6];
+    ld6g(dyn + (tok ? dc_row(sk1) : ZOFF), tg);
+    // w == 0: no sub-diagonal block (u and V zero)
+    const bool uok = w >= 1 && (dc_diag || (dc_panel && dc_q + 1 <= w && k + 1 + dc_q < snload));
+    ld6g(uok ? col + 36 * (dc_q + 1) + 6 * dc_r : dyn + ZOFF, u);
+    if (dc_rhs && w >= 1)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) u[c] = dcA[c];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) ld6g(w >= 1 ? col + 36 + 6 * c : dyn + ZOFF, V[c]);
+    // y_{k+q} -= L_{k+q,k} y'_k (q >= 2; row r of block k + q, this lane's own factor row)
+    const bool yok = dc_panel && dc_q >= 2 && k + dc_q < snload;
+    if (yok) {
+      double yp[6];
+      ld6g(col + 36 * R, yp);
+      const int sq = sk + dc_q < RC ? sk + dc_q : sk + dc_q - RC;
+      double* yd = sring + sq * SS + 36 * R + dc_r;
+      *yd -= dcA[0] * yp[0] + dcA[1] * yp[1] + dcA[2] * yp[2] + dcA[3] * yp[3] + dcA[4] * yp[4] + dcA[5] * yp[5];
+    }
+#pragma unroll
+    for (int c = 0; c < 6; ++c)
+      dcA[c] = tg[c] - (u[0] * V[c][0] + u[1] * V[c][1] + u[2] * V[c][2] + u[3] * V[c][3] + u[4] * V[c][4] +
+                        u[5] * V[c][5]);
+  };
   if constexpr (kCl) {
     if (!prior_fail) {
       // ---- Critical-lane elimination (full mode).  Per side four waves, synchronised by LDS
@@ -1002,15 +1079,22 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   } else if (!prior_fail) {
     const int PA = max(m, nb);
     int sk = 0, skm = RC - 1;
+    if (dc_wave && sna > 0) dc_load(0, 0);
     for (int p = 0; p < PA; ++p) {
       const bool on = p < sna;
       const int sk1 = sk + 1 == RC ? 0 : sk + 1;
-      if (role == kChain && on) chain_pre(p, sk);
+      if (kDc) {
+        if (dc_wave && on) dc_pre(p, sk);
+      } else if (role == kChain && on) {
+        chain_pre(p, sk);
+      }
       BST(1);
       band_barrier();
       BST(2);
       if (on) {
-        if (role == kChain) {
+        if (kDc && dc_wave) {
+          if (p + 1 < snload) dc_post(p, sk, sk1);
+        } else if (!kDc && role == kChain) {
           if (p + 1 < snload) chain_post(sk1);
         } else {
           side_step(p, sk, skm);
@@ -1023,24 +1107,38 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     if (sp > 0) {
       // both sides' state of the separator into the rings, the bottom's contributions
       // merged into the top's (fixed order), then the top continues through the separator
-      if (act) st6g(sring + (sna % RC) * SS + 36 * q + 6 * sr, P);
+      if (kDc) {
+        if (dc_wave) dc_store(sna % RC, sna);
+      } else if (act) {
+        st6g(sring + (sna % RC) * SS + 36 * q + 6 * sr, P);
+      }
       __syncthreads();
       for (int e = tid; e < A.n_merge; e += kBandThreads) {
         const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
         dyn[d.x] += dyn[d.y];
       }
       __syncthreads();
-      if (act && side == 0) ld6g(ringT + (m % RC) * SS + 36 * q + 6 * sr, P);
+      if (kDc) {
+        if (dc_wave && side == 0) dc_load(m % RC, m);
+      } else if (act && side == 0) {
+        ld6g(ringT + (m % RC) * SS + 36 * q + 6 * sr, P);
+      }
       BST(4);
       int sk = m % RC, skm = sk == 0 ? RC - 1 : sk - 1;
       for (int p = m; p < m + sp; ++p) {
         const int sk1 = sk + 1 == RC ? 0 : sk + 1;
-        if (role == kChain && side == 0) chain_pre(p, sk);
+        if (kDc) {
+          if (dc_wave && side == 0) dc_pre(p, sk);
+        } else if (role == kChain && side == 0) {
+          chain_pre(p, sk);
+        }
         BST(5);
         band_barrier();
         BST(6);
         if (side == 0) {
-          if (role == kChain) {
+          if (kDc && dc_wave) {
+            if (p + 1 < ncolT) dc_post(p, sk, sk1);
+          } else if (!kDc && role == kChain) {
             if (p + 1 < ncolT) chain_post(sk1);
           } else {
             side_step(p, sk, skm);
@@ -1065,7 +1163,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       rec_store(last, v2);
     }
   }
-  if ((kCl || lane == 0) && bad) s_fail = 1;
+  if ((kCl || VO_BA_DPPCHAIN || lane == 0) && bad) s_fail = 1;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // factor records written
   BST(8);
   __syncthreads();

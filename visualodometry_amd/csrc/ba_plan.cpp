@@ -196,34 +196,38 @@ int plan_threads(int64_t work) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), work / 2048 + 1));
 }
 
-// Landmark ranges packed independently (a segment boundary at every range start): a
-// fixed function of the landmark count, never of the host, so the plan is the same on
-// every machine.
-#ifndef VO_PLAN_PARTS
-#define VO_PLAN_PARTS 16
-#endif
-constexpr int kPlanParts = VO_PLAN_PARTS;
-int plan_parts(int L) { return std::max(1, std::min(kPlanParts, L / 1024)); }
-
 struct PlanSeg {
   int chunk0;                               // first chunk (global index after the merge)
   std::vector<int32_t> cams, acams;         // free / all cameras (unsorted while growing)
   std::vector<std::pair<int32_t, int32_t>> slots;
+  int src = -1;                             // taken over: the previous plan's segment
 };
 
-// one landmark range's greedy packing: chunks (first landmark, pair count, free track
-// entries, free observations) and segments (first chunk, local index)
+// one first-camera group's greedy packing: chunks (first landmark, pair count, free track
+// entries, free observations) and segments (first chunk, local index); a group taken over
+// from the previous plan (src >= 0) copies them from there
 struct PlanPart {
   std::vector<int32_t> chunk_q, chunk_pairs, chunk_fte, chunk_fobs;
   std::vector<PlanSeg> segs;
+  int src = -1, shift = 0;
   int err_q = -1;
   std::string err;
 };
 
 }  // namespace
 
+int seg_obs_for(int64_t n_obs, int target_segments) {
+  const int64_t t = std::max(1, target_segments);
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n_obs + t - 1) / t, 1 << 30));
+}
+
 void BAPlan::reset() {
   n_poses = n_points = n_obs = n_fixed = n_free = n_te = 0;
+  seg_obs = reused_groups = reused_chunks = 0;
+  group_q.clear();
+  group_chunk.clear();
+  group_seg.clear();
+  chunk_src.clear();
   for (auto* v : {&pt_perm, &obs_cam, &obs_te, &te_cam, &te_pt, &te_obs, &pt_te, &slot_ptr, &cam_ptr, &camo_ptr,
                   &slot_i, &slot_j, &segcam_f, &segcam_diag})
     v->clear();
@@ -243,7 +247,7 @@ void BAPlan::reset() {
 }
 
 std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_t* point_ptr,
-                       const int32_t* obs_cam, const float* obs_uv, int target_segments) {
+                       const int32_t* obs_cam, const float* obs_uv, int seg_obs, const BAPlan* prev) {
 #ifdef VO_PLAN_TIMING
   auto t_ = std::chrono::steady_clock::now();
 #endif
@@ -259,6 +263,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   P.n_obs = M;
   P.n_fixed = n_fixed;
   P.n_free = N - n_fixed;
+  P.seg_obs = std::max(1, seg_obs);
   const int nthr = plan_threads(M);
 
   PlanArr<int32_t> ob_start(L + 1), sorted(std::max(M, 1)), te_start(L + 1);
@@ -298,13 +303,17 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     for (int t = 0; t < nt; ++t)
       if (bad_obs[t] >= 0) return fmt("obs_cam[%ld]=%ld out of range", bad_obs[t], obs_cam[bad_obs[t]]);
     int32_t off = 0;
-    for (int c = 0; c <= N; ++c)
+    P.group_q.resize(N + 2);
+    for (int c = 0; c <= N; ++c) {
+      P.group_q[c] = off;
       for (int t = 0; t < nt; ++t) {
         int32_t& h = hist[(size_t)t * (N + 1) + c];
         const int32_t n = h;
         h = off;
         off += n;
       }
+    }
+    P.group_q[N + 1] = off;
     P.pt_perm.resize(L);
     run_parallel(nt, [&](int t) {
       const auto [pa, pb] = lrange(t);
@@ -378,16 +387,64 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   P.te_lcam.assign(P.n_te, -1);
   PLAN_T("track entries");
 
-  // ---- chunks and segments: each landmark range packed greedily on its own thread
-  const int nseg_target = std::max(1, target_segments);
-  const int64_t seg_obs_target = std::max<int64_t>(1, (M + nseg_target - 1) / nseg_target);
+  // ---- chunks and segments: each first-camera group packed greedily on its own (so a
+  // group's packing depends on its own landmarks only), or taken over from prev
+  const int64_t seg_obs_target = P.seg_obs;
   const int Nf = N - n_fixed;
   const bool tables = Nf <= kPlanTableCams;
-  const int nparts = plan_parts(L);
+  const int nparts = N + 1;
   std::vector<PlanPart> parts(nparts);
+  const bool reuse = prev && prev != &P && prev->seg_obs == P.seg_obs && prev->n_fixed == n_fixed &&
+                     (int)prev->group_q.size() == prev->n_poses + 2;
+  // group g equals the previous plan's group g + s: the same landmarks in the same order, their
+  // cameras s lower, the same observations (uv bit for bit)
+  auto same_group = [&](int g, int src, int s) {
+    const BAPlan& Q = *prev;
+    const int q0 = P.group_q[g], q1 = P.group_q[g + 1], pq0 = Q.group_q[src], pq1 = Q.group_q[src + 1];
+    if (q1 - q0 != pq1 - pq0 || q1 == q0) return false;
+    const int t0 = P.pt_te[q0], t1 = P.pt_te[q1], pt0 = Q.pt_te[pq0];
+    if (t1 - t0 != Q.pt_te[pq1] - pt0) return false;
+    const int o0 = P.te_obs[t0], o1 = P.te_obs[t1], po0 = Q.te_obs[pt0];
+    if (o1 - o0 != Q.te_obs[Q.pt_te[pq1]] - po0) return false;
+    for (int i = 0; i < q1 - q0; ++i)
+      if (P.pt_te[q0 + i] - t0 != Q.pt_te[pq0 + i] - pt0) return false;
+    for (int i = 0; i < t1 - t0; ++i)
+      if (P.te_cam[t0 + i] + s != Q.te_cam[pt0 + i] || P.te_obs[t0 + i] - o0 != Q.te_obs[pt0 + i] - po0) return false;
+    return std::memcmp(&P.obs_uv[2 * (size_t)o0], &Q.obs_uv[2 * (size_t)po0], 8 * (size_t)(o1 - o0)) == 0;
+  };
+  // the previous plan's packing of group src, moved to group g (cameras s lower)
+  auto take_over = [&](PlanPart& R, int g, int src, int s) {
+    const BAPlan& Q = *prev;
+    R.src = src;
+    R.shift = s;
+    const int pc0 = Q.group_chunk[src], pc1 = Q.group_chunk[src + 1];
+    for (int pc = pc0; pc < pc1; ++pc) {
+      const int32_t* h = &Q.chunk_hdr[(size_t)pc * kChunkHdr];
+      R.chunk_q.push_back(Q.chunk_pt[pc] - Q.group_q[src] + P.group_q[g]);
+      R.chunk_pairs.push_back(h[9] - h[8]);
+      R.chunk_fte.push_back(h[11] - h[10]);
+      R.chunk_fobs.push_back(h[13] - h[12]);
+    }
+    for (int ps = Q.group_seg[src]; ps < Q.group_seg[src + 1]; ++ps) {
+      PlanSeg sg{Q.seg_chunk[ps] - pc0, {}, {}, {}, ps};
+      for (int e = Q.seg_cam_off[ps]; e < Q.seg_cam_off[ps + 1]; ++e) sg.cams.push_back(Q.segcam_f[e] - s);
+      for (int e = Q.seg_acam_off[ps]; e < Q.seg_acam_off[ps + 1]; ++e) sg.acams.push_back(Q.seg_acam[e] - s);
+      for (int e = Q.seg_slot_off[ps]; e < Q.seg_slot_off[ps + 1]; ++e)
+        sg.slots.push_back(std::make_pair(Q.slot_i[e] - s, Q.slot_j[e] - s));
+      R.segs.push_back(std::move(sg));
+    }
+  };
   auto pack = [&](int pi) {
     PlanPart& R = parts[pi];
-    const int qa = (int)((int64_t)L * pi / nparts), qb = (int)((int64_t)L * (pi + 1) / nparts);
+    const int qa = P.group_q[pi], qb = P.group_q[pi + 1];
+    // groups of free cameras only (no camera changes between fixed and free with the shift);
+    // the slide (s = 1) first, then the same camera (a growing or repeated window)
+    if (reuse && pi >= n_fixed && pi < N)
+      for (int s = 1; s >= 0; --s)
+        if (pi + s < prev->n_poses && same_group(pi, pi + s, s)) {
+          take_over(R, pi, pi + s, s);
+          return;
+        }
     // membership of the open segment's cameras and camera pairs: stamp tables (stamp = the
     // segment's local number) when the free cameras are few, the linear searches otherwise
     std::vector<int32_t> cam_stamp(tables ? N : 0, -1), fcam_stamp(tables ? std::max(Nf, 1) : 0, -1);
@@ -509,11 +566,22 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   });
   for (const PlanPart& R : parts)  // the first error in landmark order
     if (R.err_q >= 0) return R.err;
-  // merge the ranges: chunks and segments in landmark order
+  // merge the groups: chunks and segments in landmark order
   std::vector<PlanSeg> segs;
   std::vector<int32_t> ch_pairs, ch_fte, ch_fobs;
-  for (PlanPart& R : parts) {
+  P.group_chunk.resize(nparts + 1);
+  P.group_seg.resize(nparts + 1);
+  for (int pi = 0; pi < nparts; ++pi) {
+    PlanPart& R = parts[pi];
     const int base = (int)P.chunk_pt.size();
+    P.group_chunk[pi] = base;
+    P.group_seg[pi] = (int)segs.size();
+    for (size_t c = 0; c < R.chunk_q.size(); ++c)
+      P.chunk_src.push_back(R.src >= 0 ? prev->group_chunk[R.src] + (int)c : -1);
+    if (R.src >= 0) {
+      ++P.reused_groups;
+      P.reused_chunks += (int)R.chunk_q.size();
+    }
     for (size_t c = 0; c < R.chunk_q.size(); ++c) {
       const int q = R.chunk_q[c];
       P.chunk_obs.push_back(P.te_obs[P.pt_te[q]]);
@@ -528,6 +596,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       segs.push_back(std::move(s));
     }
   }
+  P.group_chunk[nparts] = (int)P.chunk_pt.size();
+  P.group_seg[nparts] = (int)segs.size();
   P.chunk_obs.push_back(M);
   P.chunk_te.push_back(P.n_te);
   P.chunk_pt.push_back(L);
@@ -587,6 +657,84 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   P.chunk_img.resize((size_t)std::max(nchunks, 1));
   if (nchunks == 0) P.chunk_img[0] = ChunkImg();
   P.seg_hdr.assign((size_t)std::max(nseg, 1) * kSegHdr, 0);
+  // chunk header: ob0 nob te0 nte p0 npt sb cb e0 e1 c0 c1 q0 q1 (14, 15: active slots and cameras)
+  auto chunk_header = [&](int ch, int ns, int nc) {
+    int32_t* h = &P.chunk_hdr[(size_t)ch * kChunkHdr];
+    const int sb = P.chunk_slot_base[ch], cb = P.chunk_cam_base[ch];
+    h[0] = P.chunk_obs[ch];
+    h[1] = P.chunk_obs[ch + 1] - h[0];
+    h[2] = P.chunk_te[ch];
+    h[3] = P.chunk_te[ch + 1] - h[2];
+    h[4] = P.chunk_pt[ch];
+    h[5] = P.chunk_pt[ch + 1] - P.chunk_pt[ch];
+    h[6] = sb;
+    h[7] = cb;
+    h[8] = P.slot_ptr[sb];
+    h[9] = P.slot_ptr[sb + ns];
+    h[10] = P.cam_ptr[cb];
+    h[11] = P.cam_ptr[cb + nc];
+    h[12] = P.camo_ptr[cb];
+    h[13] = P.camo_ptr[cb + nc];
+    return h;
+  };
+  // segment header (kSegHdr)
+  auto seg_header = [&](int si, const PlanSeg& s) {
+    int32_t* h = &P.seg_hdr[(size_t)si * kSegHdr];
+    const int ch0 = P.seg_chunk[si], ch1 = P.seg_chunk[si + 1];
+    h[0] = (int)s.slots.size();
+    h[1] = P.seg_slot_off[si];
+    h[2] = P.seg_cam_off[si];
+    h[3] = (int)s.cams.size();
+    h[4] = (int)s.acams.size();
+    h[5] = ch0;
+    h[6] = ch1;
+    int16_t* h16 = reinterpret_cast<int16_t*>(h);
+    for (int i = 0; i < h[4]; ++i) h16[16 + i] = (int16_t)s.acams[i];
+    for (int i = 0; i < h[3]; ++i) h16[32 + i] = (int16_t)s.cams[i];
+    if (ch1 > ch0) std::copy(&P.chunk_hdr[(size_t)ch0 * kChunkHdr], &P.chunk_hdr[(size_t)(ch0 + 1) * kChunkHdr], h + 32);
+  };
+  // a segment taken over from the previous plan: its lists and images copied, their offsets
+  // moved to this plan's (the values fill() would compute from the same landmarks)
+  auto fill_taken = [&](int si, const PlanSeg& s) {
+    const BAPlan& Q = *prev;
+    const int ps = s.src;
+    const int ch0 = P.seg_chunk[si], ch1 = P.seg_chunk[si + 1], pch0 = Q.seg_chunk[ps];
+    const int so = P.seg_slot_off[si], co = P.seg_cam_off[si];
+    const int ns = (int)s.slots.size(), nc = (int)s.cams.size();
+    for (int i = 0; i < ns; ++i) {
+      P.slot_i[so + i] = s.slots[i].first;
+      P.slot_j[so + i] = s.slots[i].second;
+    }
+    std::copy(s.acams.begin(), s.acams.end(), P.seg_acam.begin() + P.seg_acam_off[si]);
+    const int ob0 = P.chunk_obs[ch0], pob0 = Q.chunk_obs[pch0];
+    std::memcpy(P.obs_acam.data() + ob0, Q.obs_acam.data() + pob0, P.chunk_obs[ch1] - ob0);
+    for (int i = 0; i < nc; ++i) {
+      P.segcam_f[co + i] = s.cams[i];
+      P.segcam_diag[co + i] = Q.segcam_diag[Q.seg_cam_off[ps] + i];
+    }
+    for (int ch = ch0; ch < ch1; ++ch) {
+      const int pc = pch0 + (ch - ch0);
+      const int te0 = P.chunk_te[ch], pte0 = Q.chunk_te[pc];
+      std::copy(Q.te_lcam.data() + pte0, Q.te_lcam.data() + pte0 + (P.chunk_te[ch + 1] - te0), P.te_lcam.data() + te0);
+      const int sb = P.chunk_slot_base[ch], psb = Q.chunk_slot_base[pc];
+      const int32_t pb = pair_base[ch], qpb = Q.slot_ptr[psb];
+      for (int sl = 0; sl <= ns; ++sl) P.slot_ptr[sb + sl] = Q.slot_ptr[psb + sl] - qpb + pb;
+      std::memcpy(P.pair_list.data() + pb, Q.pair_list.data() + qpb, sizeof(uint16_t) * (pair_base[ch + 1] - pb));
+      const int cb = P.chunk_cam_base[ch], pcb = Q.chunk_cam_base[pc];
+      const int32_t clb = cl_base[ch], qcl = Q.cam_ptr[pcb], cob = col_base[ch], qco = Q.camo_ptr[pcb];
+      for (int c = 0; c <= nc; ++c) {
+        P.cam_ptr[cb + c] = Q.cam_ptr[pcb + c] - qcl + clb;
+        P.camo_ptr[cb + c] = Q.camo_ptr[pcb + c] - qco + cob;
+      }
+      std::memcpy(P.cam_list.data() + clb, Q.cam_list.data() + qcl, cl_base[ch + 1] - clb);
+      std::memcpy(P.camo_list.data() + cob, Q.camo_list.data() + qco, col_base[ch + 1] - cob);
+      int32_t* h = chunk_header(ch, ns, nc);
+      h[14] = Q.chunk_hdr[(size_t)pc * kChunkHdr + 14];
+      h[15] = Q.chunk_hdr[(size_t)pc * kChunkHdr + 15];
+      std::memcpy(&P.chunk_img[ch], &Q.chunk_img[pc], sizeof(ChunkImg));
+    }
+    seg_header(si, s);
+  };
   auto fill = [&](int sa, int sbnd) {
     // per-thread lookup tables (camera -> window index, camera pair -> slot) and counting-sort buffers
     std::vector<int32_t> fcam_idx(tables ? std::max(Nf, 1) : 0, -1), acam_idx(tables ? N : 0, -1);
@@ -595,6 +743,10 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     uint16_t ptmp[kChunkPairs];
     for (int si = sa; si < sbnd; ++si) {
       PlanSeg& s = segs[si];
+      if (s.src >= 0) {
+        fill_taken(si, s);
+        continue;
+      }
       std::sort(s.cams.begin(), s.cams.end());
       std::sort(s.slots.begin(), s.slots.end());
       std::sort(s.acams.begin(), s.acams.end());
@@ -679,23 +831,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
           const int lc = P.te_lcam[P.obs_te[o]];
           if (lc >= 0) P.camo_list[obase + cnt2[lc]++] = (uint8_t)(o - ob0);
         }
-        // chunk header: ob0 nob te0 nte p0 npt sb cb e0 e1 c0 c1 q0 q1 (+2 spare)
-        int32_t* h = &P.chunk_hdr[(size_t)ch * kChunkHdr];
+        int32_t* h = chunk_header(ch, ns, nc);
         const int sb = P.chunk_slot_base[ch], cb = P.chunk_cam_base[ch];
-        h[0] = ob0;
-        h[1] = P.chunk_obs[ch + 1] - ob0;
-        h[2] = te0;
-        h[3] = P.chunk_te[ch + 1] - te0;
-        h[4] = P.chunk_pt[ch];
-        h[5] = P.chunk_pt[ch + 1] - P.chunk_pt[ch];
-        h[6] = sb;
-        h[7] = cb;
-        h[8] = P.slot_ptr[sb];
-        h[9] = P.slot_ptr[sb + ns];
-        h[10] = P.cam_ptr[cb];
-        h[11] = P.cam_ptr[cb + nc];
-        h[12] = P.camo_ptr[cb];
-        h[13] = P.camo_ptr[cb + nc];
         // the chunk's LDS image (chunk-relative offsets, unused entries zero)
         ChunkImg& g = P.chunk_img[ch];
         g = ChunkImg();
@@ -774,19 +911,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         h[14] = nas;
         h[15] = nac;
       }
-      // segment header (kSegHdr)
-      int32_t* h = &P.seg_hdr[(size_t)si * kSegHdr];
-      h[0] = ns;
-      h[1] = so;
-      h[2] = co;
-      h[3] = nc;
-      h[4] = (int)s.acams.size();
-      h[5] = ch0;
-      h[6] = ch1;
-      int16_t* h16 = reinterpret_cast<int16_t*>(h);
-      for (int i = 0; i < h[4]; ++i) h16[16 + i] = (int16_t)s.acams[i];
-      for (int i = 0; i < nc; ++i) h16[32 + i] = (int16_t)s.cams[i];
-      if (ch1 > ch0) std::copy(&P.chunk_hdr[(size_t)ch0 * kChunkHdr], &P.chunk_hdr[(size_t)(ch0 + 1) * kChunkHdr], h + 32);
+      seg_header(si, s);
       if (tables) {  // clear this segment's table entries for the next one
         for (int32_t c : s.cams) fcam_idx[c] = -1;
         for (int32_t c : s.acams) acam_idx[c] = -1;
@@ -928,6 +1053,9 @@ uint64_t plan_digest(const BAPlan& P) {
   vec(P.segcam_diag); vec(P.seg_acam_off); vec(P.seg_acam); vec(P.obs_acam); vec(P.prof_first); vec(P.prof_off);
   vec(P.prof_last); vec(P.prof_src_ptr); vec(P.prof_src); vec(P.prof_diag); vec(P.camb_ptr); vec(P.camb_src);
   vec(P.solve_tab);
+  const int32_t so = P.seg_obs;
+  bytes(&so, sizeof so);
+  vec(P.group_q); vec(P.group_chunk); vec(P.group_seg);
   return h;
 }
 

@@ -213,6 +213,17 @@ struct BAPlan {
   // plus diag[k] (profile block (k, k)), off[k], first[k].
   std::vector<int32_t> solve_tab;
   SolveTableLayout solve_layout;
+  // slide-stable packing: landmarks are ordered by first camera, and every first-camera
+  // group is packed on its own (segments never cross a group), with seg_obs observations per
+  // segment as the packing target.  group_q / group_chunk / group_seg: per first camera c
+  // (0 .. N; N = landmarks without observations) its first landmark, chunk and segment.
+  int seg_obs = 0;
+  std::vector<int32_t> group_q, group_chunk, group_seg;
+  // Not part of the plan (never digested): how it was built.  chunk_src[c] = the chunk of
+  // the previous plan whose image chunk c copies (an incremental build), -1 if rebuilt;
+  // reused_groups / reused_chunks count the groups and chunks taken over.
+  std::vector<int32_t> chunk_src;
+  int reused_groups = 0, reused_chunks = 0;
 
   BAPlan() = default;
   explicit BAPlan(bool pinned_images) : chunk_img(PlanHostAlloc<ChunkImg>(pinned_images)) {}
@@ -224,11 +235,18 @@ struct BAPlan {
   int64_t algorithmic_bytes_per_iter() const;
 };
 
+// The packing target of a window of n_obs observations for target_segments K1 workgroups.
+int seg_obs_for(int64_t n_obs, int target_segments);
 // Builds everything except the profile (needs the global first[] on multi-GPU).
-// Returns an empty string on success, else the error message.
+// Returns an empty string on success, else the error message.  With prev (the plan of the
+// previous window on the same engine, built with the same seg_obs and n_fixed), every
+// first-camera group whose landmarks equal a group of prev one camera later (the window slid
+// by one keyframe) or at the same camera (the window grew, or the same window again) takes
+// over that group's chunks and segments: lists and images copied, offsets and camera ids
+// shifted, nothing repacked.  The result is the same plan, byte for byte, as without prev.
 std::string build_plan(BAPlan& plan, int n_poses, int n_points, int n_obs, int n_fixed,
                        const int32_t* point_ptr, const int32_t* obs_cam, const float* obs_uv,
-                       int target_segments);
+                       int seg_obs, const BAPlan* prev = nullptr);
 // first[i] of each free block row touched by this plan (i if untouched).
 std::vector<int32_t> local_profile_first(const BAPlan& plan);
 // Builds the profile and the K2 reduction index from a (possibly all-reduced) first[].

@@ -58,6 +58,10 @@ struct DevBuf {
     ptr = nullptr;
     bytes = 0;
   }
+  void swap(DevBuf& o) noexcept {
+    std::swap(ptr, o.ptr);
+    std::swap(bytes, o.bytes);
+  }
   ~DevBuf() { release(); }
 };
 

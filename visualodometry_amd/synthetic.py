@@ -198,6 +198,40 @@ def make_ba_config(name: str, **kw) -> BAProblemData:
     return make_ba_problem(n, l, seed, **kw)
 
 
+def make_ba_slide(name: str, n_windows: int, **kw) -> list:
+    """``n_windows`` windows of config ``name``'s size sliding one keyframe at a time along one
+    drive: window j holds poses j .. j + n - 1 of a drive of n + n_windows - 1 poses and every
+    landmark seen there by two or more of them (its observations outside clipped), in the
+    drive's landmark order -- what the reference's loop hands its BA per keyframe
+    (``vo.py:252-288``; the drop-in's ``KeyframeWindow.build``).  The drive's landmark density
+    per pose is the config's, so each window is the config's size give or take its edges."""
+    n, l, seed = BA_CONFIGS[name]
+    n_drive = n + n_windows - 1
+    d = make_ba_problem(n_drive, int(round(l * n_drive / n)), seed, **kw)
+    obs_pt = np.repeat(np.arange(d.points.shape[0]), np.diff(d.point_ptr))
+    out = []
+    for j in range(n_windows):
+        inw = (d.obs_cam >= j) & (d.obs_cam < j + n)
+        cnt = np.bincount(obs_pt[inw], minlength=d.points.shape[0])
+        keep_pt = cnt >= 2
+        sel = inw & keep_pt[obs_pt]
+        pts_idx = np.flatnonzero(keep_pt)
+        point_ptr = np.zeros(pts_idx.size + 1, np.int64)
+        point_ptr[1:] = np.cumsum(cnt[pts_idx])
+        out.append(BAProblemData(
+            K=d.K,
+            poses_cw=d.poses_cw[j:j + n].copy(),
+            points=d.points[pts_idx].copy(),
+            point_ptr=point_ptr.astype(np.int32),
+            obs_cam=(d.obs_cam[sel] - j).astype(np.int32),
+            obs_uv=d.obs_uv[sel].copy(),
+            n_fixed=d.n_fixed,
+            poses_true=d.poses_true[j:j + n].copy(),
+            points_true=d.points_true[pts_idx].copy(),
+        ))
+    return out
+
+
 def sift_like_descriptors(n: int, rng: np.random.Generator, dim: int = 128) -> np.ndarray:
     """Integer-valued 0..255 float32 descriptors with ~40 % zeros (SIFT-like).
 
