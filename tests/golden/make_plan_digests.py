@@ -2,7 +2,9 @@
 several segment targets.  A planner rewrite must reproduce these exactly (the plan fixes
 every kernel's summation order); a deliberate plan change regenerates them.  Round 4 packs
 every first-camera group on its own (a segment boundary at each group start: the
-slide-stable plan that a window's next plan can take groups over from, ba_plan.cpp).
+slide-stable plan that a window's next plan can take groups over from, ba_plan.cpp), and
+the one-wave K1 balances each chunk's Schur lanes over passes of 64; target 2**30 is the
+engine's (segments of one chunk).
 Usage: python tests/golden/make_plan_digests.py"""
 import json
 import sys
@@ -13,7 +15,8 @@ sys.path.insert(0, str(ROOT))
 from visualodometry_amd.ba import plan_digest  # noqa: E402
 from visualodometry_amd.synthetic import make_ba_config, make_ba_problem  # noqa: E402
 
-CASES = [("cfg2", 1024), ("cfg3", 1024), ("cfg3", 256), ("cfg3", 4096), ("small_8x200", 64), ("small_30x3000", 512)]
+CASES = [("cfg2", 1024), ("cfg3", 1024), ("cfg3", 256), ("cfg3", 4096), ("small_8x200", 64), ("small_30x3000", 512),
+         ("cfg3", 1 << 30), ("cfg4", 1 << 30)]
 
 
 def problem(name):

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Slide-stable plan: BA GPU tests (take-over == scratch), drop-in/trace replays, K1 with the
-# group-partitioned plan (bench without the matcher), per-call host latency.
+# group-partitioned plan (bench without the matcher), per-call host latency, K1 phase stamps.
 set -euo pipefail
 OUT=gpurun_out
 mkdir -p $OUT
@@ -10,4 +10,6 @@ timeout -k 10 200 python bench.py --no-matcher --no-cpu-baseline --steps 200 --w
 timeout -k 10 200 python bench.py --config cfg4 --no-matcher --no-cpu-baseline --steps 100 --warmup 10 > $OUT/slide_bench_cfg4.json 2> $OUT/slide_bench_cfg4.err
 timeout -k 10 300 python tools/host_call_latency.py > $OUT/slide_host_latency.json 2> $OUT/slide_host_latency.err
 timeout -k 10 200 python tools/ba_call_breakdown.py cfg3 > $OUT/slide_breakdown.json 2> $OUT/slide_breakdown.err
+VO_LIB_PATH=visualodometry_amd/lib/libvo_hip_stamps.so timeout -k 10 120 python tools/ba_phase_stamps.py cfg3 $OUT/slide_seg_cfg3.txt > $OUT/slide_stamps_cfg3.txt 2>&1
+VO_LIB_PATH=visualodometry_amd/lib/libvo_hip_stamps.so timeout -k 10 120 python tools/ba_phase_stamps.py cfg4 > $OUT/slide_stamps_cfg4.txt 2>&1
 echo done

@@ -622,7 +622,7 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
       // the chunk's active slots on balanced lanes (ChunkImg::abase / anp): lane tid -> entry
       // si (binary search over the lane bases), row a, part of 2^lgp
       // (a chunk with more than 42 active slots takes a second pass of one lane per row item)
-      static_assert(kLinLanes == kLinThreads, "planner lane budget = K1 workgroup");
+      static_assert(kLinWave || kLinLanes == kLinThreads, "planner lane budget = K1 workgroup");
       const int nas = h3.z, lanes = S.img.abase[nas];
       for (int base = 0; base < lanes; base += kLinThreads) {
       const int t = base + tid;
@@ -757,6 +757,394 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
     for (int w = 0; w < kLinThreads / 64; ++w) c += red[w];
     A.slab_cost[seg] = c;
   }
+  st.mark(kPhWrite);
+  st.flush(A.stamps);
+}
+
+// ---- K1, one wave per chunk (kLinWave) -----------------------------------------------
+// A segment is one chunk and one 64-lane workgroup: every phase of the chunk runs on one
+// wave (a workgroup barrier is then only the LDS wait), and six such workgroups share a CU,
+// so all of cfg3's chunks run at once instead of three four-wave workgroups per CU walking
+// two chunks each behind nine barriers a chunk.  The LDS image is ~25.5 KB: the track
+// entries' Z | bt region doubles as the observations' Jp | r during the linearisation and as
+// the back substitution's pose_o | dc; the camera blocks U and the rhs are summed by the
+// diagonal slots' lanes over their pairs' observations (a diagonal slot's pairs are exactly
+// its camera's track entries), so every window item is finished in registers and written to
+// its slab row once.
+constexpr int kZbStride = 24;                  // doubles per track entry: Z (18) | bt (6)
+constexpr int kZbR = 6 * kChunkObs;            // r (2 per observation) after Jp (6 per observation)
+constexpr int kZbDc = kZbR + 2 * kChunkObs;    // back substitution: dc of the window cameras
+constexpr int kZbPoseO = kZbDc + 6 * kSegCams; // back substitution: poses of the pending step
+static_assert(kZbPoseO + 12 * kSegAllCams <= kChunkTe * kZbStride, "Zb region aliases");
+
+struct alignas(16) LinWave {
+  ChunkImg img;
+  int spos[kSegSlots];
+  int cpos[kSegCams];
+  alignas(16) double Jc[kChunkObs][12];
+  alignas(16) double zb[kChunkTe * kZbStride];
+  double X[kChunkPts][3];
+  double L[kChunkPts][6];  // 1/l00, l10, 1/l11, l20, l21, 1/l22
+  double h[kChunkPts][3];
+  double pose_n[kSegAllCams][12];
+  uint8_t valid[kChunkPts];
+};
+// six per CU (cfg3's 1362 chunks in one round on 256 CUs)
+static_assert(sizeof(LinWave) <= 160 * 1024 / 6, "one-wave K1 LDS image");
+
+// point_block over the Zb region's Jp | r (same operation order)
+__device__ __forceinline__ bool point_block_w(const LinWave& S, double lambda, int p, double (&l)[6],
+                                              double (&h)[3]) {
+  double v00 = 0, v01 = 0, v02 = 0, v11 = 0, v12 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
+  const int o0 = S.img.te_obs[S.img.pt_te[p]], o1 = S.img.te_obs[S.img.pt_te[p + 1]];
+  for (int o = o0; o < o1; ++o) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const double a = S.zb[6 * o + 3 * k], b = S.zb[6 * o + 3 * k + 1], c = S.zb[6 * o + 3 * k + 2];
+      const double rk = S.zb[kZbR + 2 * o + k];
+      v00 += a * a; v01 += a * b; v02 += a * c;
+      v11 += b * b; v12 += b * c; v22 += c * c;
+      g0 += a * rk; g1 += b * rk; g2 += c * rk;
+    }
+  }
+  v00 += lambda; v11 += lambda; v22 += lambda;
+  const double eps = kPivotRelEps * (v00 + v11 + v22);
+  bool ok = v00 > eps;
+  const double i00 = rsq_nr(ok ? v00 : 1.0);
+  const double l10 = v01 * i00, l20 = v02 * i00;
+  const double d1 = v11 - l10 * l10;
+  ok = ok && d1 > eps;
+  const double i11 = rsq_nr(ok ? d1 : 1.0);
+  const double l21 = (v12 - l20 * l10) * i11;
+  const double d2 = v22 - l20 * l20 - l21 * l21;
+  ok = ok && d2 > eps;
+  const double i22 = rsq_nr(ok ? d2 : 1.0);
+  l[0] = i00; l[1] = l10; l[2] = i11; l[3] = l20; l[4] = l21; l[5] = i22;
+  h[0] = g0 * i00;
+  h[1] = (g1 - l10 * h[0]) * i11;
+  h[2] = (g2 - l20 * h[0] - l21 * h[1]) * i22;
+  return ok;
+}
+
+// Residual and Jacobians of observation o at pose T (lin_obs / chunk_backsub arithmetic);
+// r and Jp into the Zb region, Jc (kJc) into S.Jc.  The back substitution (kBack) adds
+// Jc dc for a free camera (dc non-null) and sums no cost.
+template <bool kJc, bool kBack>
+__device__ __forceinline__ void obs_lin_w(LinWave& S, const LinArgs& A, const double* T, int o,
+                                          const double* dc, double& cost) {
+  const int q = S.img.te_pt[S.img.obs_te[o]];
+  const double X0 = S.X[q][0], X1 = S.X[q][1], X2 = S.X[q][2];
+  const double x = T[0] * X0 + T[1] * X1 + T[2] * X2 + T[9];
+  const double y = T[3] * X0 + T[4] * X1 + T[5] * X2 + T[10];
+  const double z = T[6] * X0 + T[7] * X1 + T[8] * X2 + T[11];
+  const double iz = rcp_nr(z);
+  const float2 m = reinterpret_cast<const float2*>(S.img.uv)[o];
+  double r0 = A.fx * x * iz + A.cx - (double)m.x;
+  double r1 = A.fy * y * iz + A.cy - (double)m.y;
+  const double j00 = A.fx * iz, j02 = -A.fx * x * iz * iz;
+  const double j11 = A.fy * iz, j12 = -A.fy * y * iz * iz;
+  if (kBack && dc) {
+    r0 += j00 * dc[0] + j02 * dc[2] + (j02 * y) * dc[3] + (j00 * z - j02 * x) * dc[4] - (j00 * y) * dc[5];
+    r1 += j11 * dc[1] + j12 * dc[2] + (j12 * y - j11 * z) * dc[3] - (j12 * x) * dc[4] + (j11 * x) * dc[5];
+  }
+  if (!kBack) cost += r0 * r0 + r1 * r1;
+  S.zb[kZbR + 2 * o] = r0;
+  S.zb[kZbR + 2 * o + 1] = r1;
+  if (kJc) {
+    double* jc = S.Jc[o];
+    jc[0] = j00;
+    jc[1] = 0.0;
+    jc[2] = j02;
+    jc[3] = j02 * y;
+    jc[4] = j00 * z - j02 * x;
+    jc[5] = -j00 * y;
+    jc[6] = 0.0;
+    jc[7] = j11;
+    jc[8] = j12;
+    jc[9] = j12 * y - j11 * z;
+    jc[10] = -j12 * x;
+    jc[11] = j11 * x;
+  }
+  double* jp = &S.zb[6 * o];
+  jp[0] = j00 * T[0] + j02 * T[6];
+  jp[1] = j00 * T[1] + j02 * T[7];
+  jp[2] = j00 * T[2] + j02 * T[8];
+  jp[3] = j11 * T[3] + j12 * T[6];
+  jp[4] = j11 * T[4] + j12 * T[7];
+  jp[5] = j11 * T[5] + j12 * T[8];
+}
+
+template <int MODE, bool kStamp>
+__global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
+  __shared__ LinWave S;
+  static_assert(kLinLanes == 64, "one wave");
+  Stamper<kStamp> st;
+  st.start();
+  const int seg = blockIdx.x, tid = threadIdx.x;
+  // level 1: status, segment header (uniform), this lane's camera ids (fixed header offsets)
+  // and the chunk image (chunk = segment)
+  const int* SH = A.seg_hdr + (long)kSegHdr * seg;
+  const int4* SH4 = reinterpret_cast<const int4*>(SH);
+  const int16_t* SH16 = reinterpret_cast<const int16_t*>(SH);
+  const int stat = A.status ? *A.status : 0;
+  const int4 g0 = SH4[0], g1 = SH4[1];
+  const int4 h0 = SH4[8], h1 = SH4[9], h2 = SH4[10], h3 = SH4[11];
+  constexpr int kImgVec = (int)(sizeof(ChunkImg) / 16);
+  constexpr int kImgPer = (kImgVec + 63) / 64;
+  uint4 vimg[kImgPer];
+  const uint4* img = reinterpret_cast<const uint4*>(A.chunk_img + seg);
+#pragma unroll
+  for (int k = 0; k < kImgPer; ++k) vimg[k] = img[min(tid + 64 * k, kImgVec - 1)];
+  int i_acam[3], i_wcam[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    i_acam[k] = SH16[16 + min((tid + 64 * k) / 12, kSegAllCams - 1)];
+    i_wcam[k] = SH16[32 + min((tid + 64 * k) / 6, kSegCams - 1)];
+  }
+  if (stat) return;  // a previous solve failed: state frozen
+  const int nslots = g0.x, slot_off = g0.y, cam0 = g0.z, ncams = g0.w, na = g1.x;
+  const int nob = h0.y, nte = h0.w, p0 = h1.x, npt = h1.y;
+  // level 2: landmarks, poses, pending update, slab rows
+  double vx[2], vpn[3], vpo[3], vdc[3];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) vx[k] = A.points[3l * p0 + min(tid + 64 * k, max(3 * npt - 1, 0))];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int e = tid + 64 * k;
+    vpn[k] = A.pose_new[12l * i_acam[k] + e % 12];
+    if (MODE & kBacksub) {
+      vpo[k] = A.pose_old[12l * i_acam[k] + e % 12];
+      vdc[k] = A.dc[6l * i_wcam[k] + e % 6];
+    }
+  }
+  int vsp = 0, vcp = 0;
+  if ((MODE & kAccum) && nslots > 0) {
+    vsp = A.slab_pos[slot_off + min(tid, nslots - 1)];
+    vcp = A.cam_pos[cam0 + min(tid, max(ncams - 1, 0))];
+  }
+#pragma unroll
+  for (int k = 0; k < kImgPer; ++k)
+    if (tid + 64 * k < kImgVec) reinterpret_cast<uint4*>(&S.img)[tid + 64 * k] = vimg[k];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    if (tid + 64 * k < 3 * npt) (&S.X[0][0])[tid + 64 * k] = vx[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int e = tid + 64 * k;
+    if (e < 12 * na) {
+      (&S.pose_n[0][0])[e] = vpn[k];
+      if (MODE & kBacksub) S.zb[kZbPoseO + e] = vpo[k];
+    }
+    if ((MODE & kBacksub) && e < 6 * ncams) S.zb[kZbDc + e] = vdc[k];
+  }
+  if (MODE & kAccum) {
+    if (tid < nslots) S.spos[tid] = vsp;
+    if (tid < ncams) S.cpos[tid] = vcp;
+  }
+  st.count(kPhSlots, nslots);
+  st.count(kPhCams, ncams);
+  st.count(kPhObs, nob);
+  st.count(kPhTe, nte);
+  st.count(kPhPts, npt);
+  st.count(kPhPairs, h2.y - h2.x);
+  __syncthreads();
+  st.mark(kPhLoad);
+  double cost = 0.0;
+
+  if (MODE & kBacksub) {
+    // the pending step at its linearisation point: r + Jc dc and Jp per observation, then
+    // dp = -V^-1 sum Jp^T (r + Jc dc) per landmark (chunk_backsub)
+    if (tid < nob) {
+      const int lc = S.img.te_lcam[S.img.obs_te[tid]];
+      obs_lin_w<false, true>(S, A, &S.zb[kZbPoseO + 12 * S.img.acam[tid]], tid,
+                             lc >= 0 ? &S.zb[kZbDc + 6 * lc] : nullptr, cost);
+    }
+    __syncthreads();
+    if (tid < npt) {
+      double l[6], h[3];
+      if (point_block_w(S, A.lambda, tid, l, h)) {
+        const double x2 = -h[2] * l[5];
+        const double x1 = (-h[1] - l[4] * x2) * l[2];
+        const double x0 = (-h[0] - l[1] * x1 - l[3] * x2) * l[0];
+        S.X[tid][0] += x0;
+        S.X[tid][1] += x1;
+        S.X[tid][2] += x2;
+        A.points[3l * (p0 + tid)] = S.X[tid][0];
+        A.points[3l * (p0 + tid) + 1] = S.X[tid][1];
+        A.points[3l * (p0 + tid) + 2] = S.X[tid][2];
+      }
+    }
+    __syncthreads();
+    st.mark(kPhBacksub);
+  }
+
+  // residuals and Jacobians at the current linearisation point (cost at the updated state)
+  if (tid < nob) obs_lin_w<(MODE & kAccum) != 0, false>(S, A, S.pose_n[S.img.acam[tid]], tid, nullptr, cost);
+  if (MODE & kAccum) {
+    __syncthreads();
+    st.mark(kPhLinObs);
+    // per landmark: V (+lambda), its pivot-tested Cholesky and h = L^-1 g
+    if (tid < npt) {
+      double l[6], h[3];
+      const bool ok = point_block_w(S, A.lambda, tid, l, h);
+      S.valid[tid] = ok;
+#pragma unroll
+      for (int e = 0; e < 6; ++e) S.L[tid][e] = l[e];
+      S.h[tid][0] = ok ? h[0] : 0.0;
+      S.h[tid][1] = ok ? h[1] : 0.0;
+      S.h[tid][2] = ok ? h[2] : 0.0;
+    }
+    __syncthreads();
+    st.mark(kPhReduce);
+    // per track entry: W = Jc^T Jp, gc = Jc^T r over its observations, then Z = W L^-T and
+    // bt = -gc + Z h (zero, and the observations' Jc zeroed, for a frozen landmark or a
+    // fixed camera); Z | bt overwrite the Jp | r every lane has read
+    {
+      double W[18], g[6];
+#pragma unroll
+      for (int e = 0; e < 18; ++e) W[e] = 0.0;
+#pragma unroll
+      for (int e = 0; e < 6; ++e) g[e] = 0.0;
+      const int t = min(tid, max(nte - 1, 0));
+      const bool live = tid < nte;
+      const int oa = S.img.te_obs[t], ob = live ? S.img.te_obs[t + 1] : oa;
+      for (int o = oa; o < ob; ++o) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const double rk = S.zb[kZbR + 2 * o + k];
+          const double q0 = S.zb[6 * o + 3 * k], q1 = S.zb[6 * o + 3 * k + 1], q2 = S.zb[6 * o + 3 * k + 2];
+#pragma unroll
+          for (int a = 0; a < 6; ++a) {
+            const double jc = S.Jc[o][6 * k + a];
+            W[3 * a] += jc * q0;
+            W[3 * a + 1] += jc * q1;
+            W[3 * a + 2] += jc * q2;
+            g[a] += jc * rk;
+          }
+        }
+      }
+      const int p = S.img.te_pt[t];
+      const bool use = live && S.valid[p] && S.img.te_lcam[t] >= 0;
+      const double i00 = S.L[p][0], l10 = S.L[p][1], i11 = S.L[p][2];
+      const double l20 = S.L[p][3], l21 = S.L[p][4], i22 = S.L[p][5];
+      const double hh0 = S.h[p][0], hh1 = S.h[p][1], hh2 = S.h[p][2];
+      double bt[6];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const double z0 = W[3 * a] * i00;
+        const double z1 = (W[3 * a + 1] - l10 * z0) * i11;
+        const double z2 = (W[3 * a + 2] - l20 * z0 - l21 * z1) * i22;
+        W[3 * a] = use ? z0 : 0.0;
+        W[3 * a + 1] = use ? z1 : 0.0;
+        W[3 * a + 2] = use ? z2 : 0.0;
+        bt[a] = use ? -g[a] + (z0 * hh0 + z1 * hh1 + z2 * hh2) : 0.0;
+      }
+      if (live && !use)  // frozen landmark: its observations leave U too
+        for (int o = oa; o < ob; ++o)
+#pragma unroll
+          for (int e = 0; e < 12; ++e) S.Jc[o][e] = 0.0;
+      __syncthreads();  // every lane has read its Jp | r
+      if (live) {
+        double2* zr = reinterpret_cast<double2*>(&S.zb[kZbStride * t]);
+#pragma unroll
+        for (int e = 0; e < 9; ++e) zr[e] = make_double2(W[2 * e], W[2 * e + 1]);
+#pragma unroll
+        for (int e = 0; e < 3; ++e) zr[9 + e] = make_double2(bt[2 * e], bt[2 * e + 1]);
+      }
+    }
+    __syncthreads();
+    st.mark(kPhElim);
+
+    // Schur items: (active slot, row a) on 2^lg lanes each (ChunkImg::abase / anp), passes
+    // of 64 lanes.  Item value: -sum over its pairs of Z_x[a] Z_y^T (pairs j+2 fetched while
+    // j+1 accumulates, as the four-wave K1); a diagonal slot's lanes add U's row a and b[a]
+    // over their pairs' observations (pair (x, x): track entry x of the slot's camera).  The
+    // parts combine by the aligned butterfly; the item's first lane writes its slab row.
+    {
+      const int nas = h3.z, lanes = S.img.abase[nas];
+      for (int base = 0; base < lanes; base += kLinLanes) {
+        const int t = base + tid;
+        int si = 0;
+#pragma unroll
+        for (int sp = 32; sp > 0; sp >>= 1)
+          if (si + sp < nas && S.img.abase[si + sp] <= t) si += sp;
+        const bool live = t < lanes;
+        const int lgp = live ? S.img.anp[si] : 0, np = 1 << lgp;
+        const int off = t - S.img.abase[si], a = off >> lgp, part = off & (np - 1);
+        const int s = live ? S.img.aslot[si] : 0;
+        const int dcam = live ? S.img.adcam[si] : 0xFF;
+        double out[6] = {0, 0, 0, 0, 0, 0};
+        double ob = 0.0;
+        const int e0 = live ? S.img.slotp[si] + part : 0, e1 = live ? S.img.slotp[si] + S.img.apcnt[si] : 0;
+        if (e0 < e1) {
+          auto zrow = [&](int pr, double (&za)[3], double2 (&zy)[9]) {
+            const double2* py = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr >> 8)]);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) zy[k] = py[k];
+            const double* px = &S.zb[kZbStride * (pr & 255) + 3 * a];
+            za[0] = px[0];
+            za[1] = px[1];
+            za[2] = px[2];
+          };
+          auto accum = [&](const double (&za)[3], const double2 (&zy)[9]) {
+            const double* zf = reinterpret_cast<const double*>(zy);
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+              out[c] -= za[0] * zf[3 * c] + za[1] * zf[3 * c + 1] + za[2] * zf[3 * c + 2];
+          };
+          const int n = (e1 - e0 + np - 1) / np;  // this part's pairs
+          auto pid = [&](int j) { return (int)S.img.pairs[e0 + min(j, n - 1) * np]; };
+          double zaA[3], zaB[3];
+          double2 zyA[9], zyB[9];
+          zrow(pid(0), zaA, zyA);
+          zrow(pid(1), zaB, zyB);
+          int pc = pid(2), pd = pid(3);
+          int j = 0;
+          for (; j + 2 <= n; j += 2) {
+            const int pe = pid(j + 4), pf = pid(j + 5);
+            accum(zaA, zyA);
+            zrow(pc, zaA, zyA);
+            accum(zaB, zyB);
+            zrow(pd, zaB, zyB);
+            pc = pe;
+            pd = pf;
+          }
+          if (j < n) accum(zaA, zyA);
+          if (dcam != 0xFF) {
+            for (int e = e0; e < e1; e += np) {
+              const int x = S.img.pairs[e] & 255;
+              for (int o = S.img.te_obs[x]; o < S.img.te_obs[x + 1]; ++o) {
+                const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
+                double jj[12];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                  const double2 v = jr[k];
+                  jj[2 * k] = v.x;
+                  jj[2 * k + 1] = v.y;
+                }
+                const double ja0 = S.Jc[o][a], ja1 = S.Jc[o][6 + a];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) out[c] += ja0 * jj[c] + ja1 * jj[6 + c];
+              }
+              ob += S.zb[kZbStride * x + 18 + a];
+            }
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c) out[c] = sum_parts_lane(out[c], lgp);
+        ob = sum_parts_lane(ob, lgp);
+        if (live && part == 0) {
+          st6g(&A.slab[36l * S.spos[s] + 6 * a], out);
+          if (dcam != 0xFF) A.slab_b[6l * S.cpos[dcam] + a] = ob;
+        }
+      }
+    }
+    st.mark(kPhSchur);
+  }
+  // chunk cost: a fixed xor butterfly over the wave (deterministic)
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) cost += __shfl_xor(cost, m, 64);
+  if (tid == 0) A.slab_cost[seg] = cost;
   st.mark(kPhWrite);
   st.flush(A.stamps);
 }
@@ -1610,8 +1998,10 @@ class BAEngine {
   // the per-chunk latency, so one round of longer segments beats two rounds of shorter ones
   // (cfg4: 766 segments instead of 985; the cfg3 plan packs 678 either way).  Round 1's
   // sweep (profiles/r01_segment_sweep.md) predates the three-per-CU K1.
+  // The one-wave K1 (kLinWave) runs one chunk per segment: the largest target packs every
+  // segment as one chunk (seg_obs = 1).
   static int segments_target(int num_cus) {
-    return VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
+    return kLinWave ? (1 << 30) : VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
   }
 
   LinArgs lin_args() {
@@ -1645,7 +2035,9 @@ class BAEngine {
       return;
     }
     LinArgs A = lin_args();
-    dim3 g(nseg), b(kLinThreads);
+    // one-wave K1: the chunk image of segment s is chunk s
+    VO_REQUIRE(!kLinWave || nseg == plan_.n_chunks(), VO_ERR_STATE, "K1: segments of one chunk expected");
+    dim3 g(nseg), b(kLinWave ? kLinLanes : kLinThreads);
     ctx_->prof.begin(ctx_->stream, kKBaLin);
     if (stamps_on_) {
       d_stamps_.reserve((size_t)nseg * kPhCount * 8);
@@ -1653,7 +2045,11 @@ class BAEngine {
     }
 #define VO_LIN_LAUNCH(M)                                                               \
   do {                                                                                 \
-    if (stamps_on_)                                                                    \
+    if (kLinWave && stamps_on_)                                                        \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true>), g, b, 0, ctx_->stream, A);     \
+    else if (kLinWave)                                                                 \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false>), g, b, 0, ctx_->stream, A);    \
+    else if (stamps_on_)                                                               \
       hipLaunchKernelGGL((ba_lin_kernel<M, true>), g, b, 0, ctx_->stream, A);          \
     else                                                                               \
       hipLaunchKernelGGL((ba_lin_kernel<M, false>), g, b, 0, ctx_->stream, A);         \

@@ -855,34 +855,79 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         int nas = 0, nac = 0;
         {
           // active slots; lanes per row item doubled greedily for the slot with the longest
-          // per-lane pair chain while 6 lanes x the sum fit K1's workgroup (kLinLanes; more
-          // than 42 active slots take one lane per row item, in two passes)
-          int sl[kSegSlots], cntp[kSegSlots], lg[kSegSlots];
+          // per-lane pair chain while 6 lanes x the sum fit the lane budget.  Four-wave K1: one
+          // pass of its 256 lanes (more than 42 active slots take one lane per row item, in
+          // two passes).  One-wave K1 (kLinWave): passes of 64 lanes run one after another,
+          // each as long as its longest chain, so the budget is the smallest whole number of
+          // passes or one more, whichever the pass-time estimate prefers.  A diagonal slot's
+          // lanes also sum U and b over their pairs' observations (about twice a pair's work).
+          int sl[kSegSlots], cntp[kSegSlots], lg[kSegSlots], wt[kSegSlots];
           for (int i = 0; i < ns; ++i)
             if (P.slot_ptr[sb + i + 1] > P.slot_ptr[sb + i]) {
               sl[nas] = i;
               cntp[nas] = P.slot_ptr[sb + i + 1] - P.slot_ptr[sb + i];
+              wt[nas] = kLinWave && P.slot_i[so + i] == P.slot_j[so + i] ? 2 : 1;
               lg[nas++] = 0;
             }
-          int used = nas;
-          for (;;) {
-            int best = -1, chain = 0;
-            for (int i = 0; i < nas; ++i) {
-              const int c = (cntp[i] + (1 << lg[i]) - 1) >> lg[i];
-              if (c > chain) {
-                chain = c;
-                best = i;
+          auto chain_of = [&](int i, int l) { return ((cntp[i] + (1 << l) - 1) >> l) * wt[i]; };
+          auto balance = [&](int budget, int* lv) {
+            for (int i = 0; i < nas; ++i) lv[i] = 0;
+            int used = nas;
+            for (;;) {
+              int best = -1, chain = 0;
+              for (int i = 0; i < nas; ++i) {
+                const int c = chain_of(i, lv[i]);
+                if (c > chain) {
+                  chain = c;
+                  best = i;
+                }
               }
+              if (best < 0 || ((cntp[best] + (1 << lv[best]) - 1) >> lv[best]) <= 1 || lv[best] == 3 ||
+                  6 * (used + (1 << lv[best])) > budget)
+                break;
+              used += 1 << lv[best];
+              ++lv[best];
             }
-            if (best < 0 || chain <= 1 || lg[best] == 3 || 6 * (used + (1 << lg[best])) > kLinLanes) break;
-            used += 1 << lg[best];
-            ++lg[best];
-          }
-          // order by lanes per row, descending (stable): every item group starts at a multiple
-          // of its own width
+          };
+          // order by lanes per row, descending (stable; every item group starts at a multiple of
+          // its own width), then, for the one-wave K1, by chain descending (passes of alike chains)
           int ord[kSegSlots];
-          for (int i = 0; i < nas; ++i) ord[i] = i;
-          std::stable_sort(ord, ord + nas, [&](int a, int b) { return lg[a] > lg[b]; });
+          auto order = [&](const int* lv) {
+            for (int i = 0; i < nas; ++i) ord[i] = i;
+            std::stable_sort(ord, ord + nas, [&](int a, int b) {
+              if (lv[a] != lv[b]) return lv[a] > lv[b];
+              return kLinWave && chain_of(a, lv[a]) > chain_of(b, lv[b]);
+            });
+          };
+          if (!kLinWave) {
+            balance(kLinLanes, lg);
+            order(lg);
+          } else {
+            // pass-time estimate: per 64-lane pass its longest chain plus a fixed cost per pass
+            auto estimate = [&](const int* lv) {
+              order(lv);
+              int t = 0, pass = 0, pmax = 0, lane = 0;
+              for (int j = 0; j < nas; ++j) {
+                const int i = ord[j], c = chain_of(i, lv[i]);
+                for (int r = 0; r < 6; ++r, lane += 1 << lv[i]) {
+                  if (lane / kLinLanes != pass) {
+                    t += pmax + 4;
+                    pass = lane / kLinLanes;
+                    pmax = 0;
+                  }
+                  pmax = std::max(pmax, c);
+                }
+              }
+              return t + pmax + 4;
+            };
+            const int p0 = std::max(1, (6 * nas + kLinLanes - 1) / kLinLanes);
+            int lg1[kSegSlots];
+            balance(kLinLanes * p0, lg);
+            balance(kLinLanes * (p0 + 1), lg1);
+            if (estimate(lg1) < estimate(lg))
+              for (int i = 0; i < nas; ++i) lg[i] = lg1[i];
+            order(lg);
+          }
           int base = 0;
           for (int j = 0; j < nas; ++j) {
             const int i = ord[j];
@@ -890,6 +935,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
             g.slotp[j] = P.slot_ptr[sb + sl[i]] - e0;
             g.apcnt[j] = (uint16_t)cntp[i];
             g.anp[j] = (uint8_t)lg[i];
+            g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
             g.abase[j] = (uint16_t)base;
             base += 6 << lg[i];
           }

@@ -52,7 +52,13 @@ constexpr int kChunkTe = VO_CHUNK_OBS;
 constexpr int kChunkPts = VO_CHUNK_OBS / 2;
 constexpr int kChunkPairs = 8 * VO_CHUNK_OBS;  // camera-pair (x, y) entries of one chunk, staged in LDS
 constexpr int kSegSlots = 64;
-constexpr int kLinLanes = 256;  // K1 workgroup size (ba.hip kLinThreads)
+// K1 variant: one wave per chunk (segments of one chunk; the Schur-pair lanes balanced over
+// passes of 64 lanes) or the four-wave workgroup walking a segment's chunks (one pass of 256)
+#ifndef VO_BA_K1_WAVE
+#define VO_BA_K1_WAVE 1
+#endif
+constexpr bool kLinWave = VO_BA_K1_WAVE != 0;
+constexpr int kLinLanes = kLinWave ? 64 : 256;  // K1 lanes per Schur pass (ba.hip)
 constexpr int kChunkHdr = 16;
 
 constexpr int kSegCams = 24;     // free (window) cameras of a segment
@@ -93,6 +99,7 @@ struct alignas(16) ChunkImg {
   uint16_t apcnt[kSegSlots];
   uint16_t abase[kSegSlots + 1];  // up to 6 x 64 lanes (two passes of the workgroup)
   uint8_t anp[kSegSlots];
+  uint8_t adcam[kSegSlots];        // active slot i -> window camera if diagonal, else 0xFF
   alignas(2) uint16_t pairs[kChunkPairs];  // (te_x | te_y << 8) by slot
   uint8_t caml[kChunkTe];          // track entries by window camera
   uint8_t camol[kChunkObs];        // observations by window camera
