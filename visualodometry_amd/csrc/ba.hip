@@ -180,6 +180,7 @@ struct LinArgs {
   const double* dc;        // pending pose update (6 per free camera)
   const int* status;
   unsigned long long* stamps;  // diagnostic build only: per segment phase cycles
+  int wslots, wcams;           // one-wave K1 over multi-chunk segments: window capacity (dynamic LDS)
 };
 
 struct alignas(16) LinShared {
@@ -790,7 +791,10 @@ struct alignas(16) LinWave {
   uint8_t valid[kChunkPts];
 };
 // six per CU (cfg3's 1362 chunks in one round on 256 CUs)
-static_assert(sizeof(LinWave) <= 160 * 1024 / 6, "one-wave K1 LDS image");
+constexpr int kWaveSegsPerCu = 6;
+static_assert(sizeof(LinWave) <= 160 * 1024 / kWaveSegsPerCu, "one-wave K1 LDS image");
+constexpr int kWaveObsPerCu = kWaveSegsPerCu * 58;  // observations one round takes (chunks of ~58+)
+constexpr int kWaveWinSegsPerCu = 4;  // multi-chunk segments: static image + a 36-slot window
 
 // point_block over the Zb region's Jp | r (same operation order)
 __device__ __forceinline__ bool point_block_w(const LinWave& S, double lambda, int p, double (&l)[6],
@@ -874,40 +878,70 @@ __device__ __forceinline__ void obs_lin_w(LinWave& S, const LinArgs& A, const do
   jp[5] = j11 * T[5] + j12 * T[8];
 }
 
-template <int MODE, bool kStamp>
+// kWin: a segment of several chunks walked by its wave (windows too large for one chunk per
+// workgroup), its window accumulated in dynamic LDS [win (wslots x 36) | bwin (wcams x 6) |
+// dc (kSegCams x 6) | pose_o (kSegAllCams x 12)] and written once at the end; otherwise the
+// segment is one chunk and each item goes straight to its slab row.
+template <int MODE, bool kWin, bool kStamp>
 __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
   __shared__ LinWave S;
+  extern __shared__ double Wdyn[];
   static_assert(kLinLanes == 64, "one wave");
   Stamper<kStamp> st;
   st.start();
   const int seg = blockIdx.x, tid = threadIdx.x;
   // level 1: status, segment header (uniform), this lane's camera ids (fixed header offsets)
-  // and the chunk image (chunk = segment)
+  // and the first chunk's image (one chunk per segment: chunk = segment)
   const int* SH = A.seg_hdr + (long)kSegHdr * seg;
   const int4* SH4 = reinterpret_cast<const int4*>(SH);
   const int16_t* SH16 = reinterpret_cast<const int16_t*>(SH);
   const int stat = A.status ? *A.status : 0;
   const int4 g0 = SH4[0], g1 = SH4[1];
-  const int4 h0 = SH4[8], h1 = SH4[9], h2 = SH4[10], h3 = SH4[11];
+  int4 h0 = SH4[8], h1 = SH4[9], h2 = SH4[10], h3 = SH4[11];
   constexpr int kImgVec = (int)(sizeof(ChunkImg) / 16);
-  constexpr int kImgPer = (kImgVec + 63) / 64;
-  uint4 vimg[kImgPer];
-  const uint4* img = reinterpret_cast<const uint4*>(A.chunk_img + seg);
+  static_assert(kImgVec > 128 && kImgVec <= 192, "three 16-byte staging granules per lane");
+  struct Img3 {
+    uint4 a, b, c;
+  };
+  auto load_img = [&](int c) {
+    const uint4* img = reinterpret_cast<const uint4*>(A.chunk_img + c);
+    return Img3{img[tid], img[64 + tid], img[min(128 + tid, kImgVec - 1)]};
+  };
+  auto store_img = [&](const Img3& v) {
+    uint4* d = reinterpret_cast<uint4*>(&S.img);
+    d[tid] = v.a;
+    d[64 + tid] = v.b;
+    if (128 + tid < kImgVec) d[128 + tid] = v.c;
+  };
+  auto load_x = [&](const int4& hp, double (&v)[2]) {
 #pragma unroll
-  for (int k = 0; k < kImgPer; ++k) vimg[k] = img[min(tid + 64 * k, kImgVec - 1)];
+    for (int k = 0; k < 2; ++k) v[k] = A.points[3l * hp.x + min(tid + 64 * k, max(3 * hp.y - 1, 0))];
+  };
+  const int ch0 = kWin ? g1.y : seg, ch1 = kWin ? g1.z : seg + 1;
+  Img3 vimg = load_img(ch0);
   int i_acam[3], i_wcam[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     i_acam[k] = SH16[16 + min((tid + 64 * k) / 12, kSegAllCams - 1)];
     i_wcam[k] = SH16[32 + min((tid + 64 * k) / 6, kSegCams - 1)];
   }
+  int4 n0 = h0, n1 = h1, n2 = h2, n3 = h3;  // the next chunk's header (kWin)
+  if (kWin) {
+    const int chn = min(ch0 + 1, ch1 - 1);
+    n0 = A.chunk_hdr[4l * chn];
+    n1 = A.chunk_hdr[4l * chn + 1];
+    n2 = A.chunk_hdr[4l * chn + 2];
+    n3 = A.chunk_hdr[4l * chn + 3];
+  }
   if (stat) return;  // a previous solve failed: state frozen
   const int nslots = g0.x, slot_off = g0.y, cam0 = g0.z, ncams = g0.w, na = g1.x;
-  const int nob = h0.y, nte = h0.w, p0 = h1.x, npt = h1.y;
+  double* win = Wdyn;
+  double* bwin = Wdyn + 36 * A.wslots;
+  double* dcw = kWin ? bwin + 6 * A.wcams : &S.zb[kZbDc];
+  double* pose_o = kWin ? dcw + 6 * kSegCams : &S.zb[kZbPoseO];
   // level 2: landmarks, poses, pending update, slab rows
   double vx[2], vpn[3], vpo[3], vdc[3];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) vx[k] = A.points[3l * p0 + min(tid + 64 * k, max(3 * npt - 1, 0))];
+  load_x(h1, vx);
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int e = tid + 64 * k;
@@ -923,225 +957,263 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
     vcp = A.cam_pos[cam0 + min(tid, max(ncams - 1, 0))];
   }
 #pragma unroll
-  for (int k = 0; k < kImgPer; ++k)
-    if (tid + 64 * k < kImgVec) reinterpret_cast<uint4*>(&S.img)[tid + 64 * k] = vimg[k];
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-    if (tid + 64 * k < 3 * npt) (&S.X[0][0])[tid + 64 * k] = vx[k];
-#pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int e = tid + 64 * k;
     if (e < 12 * na) {
       (&S.pose_n[0][0])[e] = vpn[k];
-      if (MODE & kBacksub) S.zb[kZbPoseO + e] = vpo[k];
+      if (MODE & kBacksub) pose_o[e] = vpo[k];
     }
-    if ((MODE & kBacksub) && e < 6 * ncams) S.zb[kZbDc + e] = vdc[k];
+    if ((MODE & kBacksub) && e < 6 * ncams) dcw[e] = vdc[k];
   }
   if (MODE & kAccum) {
     if (tid < nslots) S.spos[tid] = vsp;
     if (tid < ncams) S.cpos[tid] = vcp;
+    if (kWin) {
+      for (int e = tid; e < 36 * nslots; e += 64) win[e] = 0.0;
+      for (int e = tid; e < 6 * ncams; e += 64) bwin[e] = 0.0;
+    }
   }
   st.count(kPhSlots, nslots);
   st.count(kPhCams, ncams);
-  st.count(kPhObs, nob);
-  st.count(kPhTe, nte);
-  st.count(kPhPts, npt);
-  st.count(kPhPairs, h2.y - h2.x);
-  __syncthreads();
-  st.mark(kPhLoad);
   double cost = 0.0;
 
-  if (MODE & kBacksub) {
-    // the pending step at its linearisation point: r + Jc dc and Jp per observation, then
-    // dp = -V^-1 sum Jp^T (r + Jc dc) per landmark (chunk_backsub)
-    if (tid < nob) {
-      const int lc = S.img.te_lcam[S.img.obs_te[tid]];
-      obs_lin_w<false, true>(S, A, &S.zb[kZbPoseO + 12 * S.img.acam[tid]], tid,
-                             lc >= 0 ? &S.zb[kZbDc + 6 * lc] : nullptr, cost);
+  for (int ch = ch0; ch < ch1; ++ch) {
+    // prefetch (kWin): the header two chunks ahead, the next chunk's image and landmarks
+    int4 m0 = n0, m1 = n1, m2 = n2, m3 = n3;
+    Img3 wimg = vimg;
+    double wx[2] = {0.0, 0.0};
+    if (kWin) {
+      const int chn2 = min(ch + 2, ch1 - 1);
+      m0 = A.chunk_hdr[4l * chn2];
+      m1 = A.chunk_hdr[4l * chn2 + 1];
+      m2 = A.chunk_hdr[4l * chn2 + 2];
+      m3 = A.chunk_hdr[4l * chn2 + 3];
+      wimg = load_img(min(ch + 1, ch1 - 1));
+      load_x(n1, wx);
     }
+    const int nob = h0.y, nte = h0.w, p0 = h1.x, npt = h1.y;
+    st.count(kPhObs, nob);
+    st.count(kPhTe, nte);
+    st.count(kPhPts, npt);
+    st.count(kPhPairs, h2.y - h2.x);
+    if (kWin) __syncthreads();  // the previous chunk is consumed
+    store_img(vimg);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (tid + 64 * k < 3 * npt) (&S.X[0][0])[tid + 64 * k] = vx[k];
     __syncthreads();
-    if (tid < npt) {
-      double l[6], h[3];
-      if (point_block_w(S, A.lambda, tid, l, h)) {
-        const double x2 = -h[2] * l[5];
-        const double x1 = (-h[1] - l[4] * x2) * l[2];
-        const double x0 = (-h[0] - l[1] * x1 - l[3] * x2) * l[0];
-        S.X[tid][0] += x0;
-        S.X[tid][1] += x1;
-        S.X[tid][2] += x2;
-        A.points[3l * (p0 + tid)] = S.X[tid][0];
-        A.points[3l * (p0 + tid) + 1] = S.X[tid][1];
-        A.points[3l * (p0 + tid) + 2] = S.X[tid][2];
-      }
-    }
-    __syncthreads();
-    st.mark(kPhBacksub);
-  }
+    st.mark(kPhLoad);
 
-  // residuals and Jacobians at the current linearisation point (cost at the updated state)
-  if (tid < nob) obs_lin_w<(MODE & kAccum) != 0, false>(S, A, S.pose_n[S.img.acam[tid]], tid, nullptr, cost);
-  if (MODE & kAccum) {
-    __syncthreads();
-    st.mark(kPhLinObs);
-    // per landmark: V (+lambda), its pivot-tested Cholesky and h = L^-1 g
-    if (tid < npt) {
-      double l[6], h[3];
-      const bool ok = point_block_w(S, A.lambda, tid, l, h);
-      S.valid[tid] = ok;
-#pragma unroll
-      for (int e = 0; e < 6; ++e) S.L[tid][e] = l[e];
-      S.h[tid][0] = ok ? h[0] : 0.0;
-      S.h[tid][1] = ok ? h[1] : 0.0;
-      S.h[tid][2] = ok ? h[2] : 0.0;
-    }
-    __syncthreads();
-    st.mark(kPhReduce);
-    // per track entry: W = Jc^T Jp, gc = Jc^T r over its observations, then Z = W L^-T and
-    // bt = -gc + Z h (zero, and the observations' Jc zeroed, for a frozen landmark or a
-    // fixed camera); Z | bt overwrite the Jp | r every lane has read
-    {
-      double W[18], g[6];
-#pragma unroll
-      for (int e = 0; e < 18; ++e) W[e] = 0.0;
-#pragma unroll
-      for (int e = 0; e < 6; ++e) g[e] = 0.0;
-      const int t = min(tid, max(nte - 1, 0));
-      const bool live = tid < nte;
-      const int oa = S.img.te_obs[t], ob = live ? S.img.te_obs[t + 1] : oa;
-      for (int o = oa; o < ob; ++o) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const double rk = S.zb[kZbR + 2 * o + k];
-          const double q0 = S.zb[6 * o + 3 * k], q1 = S.zb[6 * o + 3 * k + 1], q2 = S.zb[6 * o + 3 * k + 2];
-#pragma unroll
-          for (int a = 0; a < 6; ++a) {
-            const double jc = S.Jc[o][6 * k + a];
-            W[3 * a] += jc * q0;
-            W[3 * a + 1] += jc * q1;
-            W[3 * a + 2] += jc * q2;
-            g[a] += jc * rk;
-          }
+    if (MODE & kBacksub) {
+      // the pending step at its linearisation point: r + Jc dc and Jp per observation, then
+      // dp = -V^-1 sum Jp^T (r + Jc dc) per landmark (chunk_backsub)
+      if (tid < nob) {
+        const int lc = S.img.te_lcam[S.img.obs_te[tid]];
+        obs_lin_w<false, true>(S, A, &pose_o[12 * S.img.acam[tid]], tid, lc >= 0 ? &dcw[6 * lc] : nullptr, cost);
+      }
+      __syncthreads();
+      if (tid < npt) {
+        double l[6], h[3];
+        if (point_block_w(S, A.lambda, tid, l, h)) {
+          const double x2 = -h[2] * l[5];
+          const double x1 = (-h[1] - l[4] * x2) * l[2];
+          const double x0 = (-h[0] - l[1] * x1 - l[3] * x2) * l[0];
+          S.X[tid][0] += x0;
+          S.X[tid][1] += x1;
+          S.X[tid][2] += x2;
+          A.points[3l * (p0 + tid)] = S.X[tid][0];
+          A.points[3l * (p0 + tid) + 1] = S.X[tid][1];
+          A.points[3l * (p0 + tid) + 2] = S.X[tid][2];
         }
       }
-      const int p = S.img.te_pt[t];
-      const bool use = live && S.valid[p] && S.img.te_lcam[t] >= 0;
-      const double i00 = S.L[p][0], l10 = S.L[p][1], i11 = S.L[p][2];
-      const double l20 = S.L[p][3], l21 = S.L[p][4], i22 = S.L[p][5];
-      const double hh0 = S.h[p][0], hh1 = S.h[p][1], hh2 = S.h[p][2];
-      double bt[6];
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        const double z0 = W[3 * a] * i00;
-        const double z1 = (W[3 * a + 1] - l10 * z0) * i11;
-        const double z2 = (W[3 * a + 2] - l20 * z0 - l21 * z1) * i22;
-        W[3 * a] = use ? z0 : 0.0;
-        W[3 * a + 1] = use ? z1 : 0.0;
-        W[3 * a + 2] = use ? z2 : 0.0;
-        bt[a] = use ? -g[a] + (z0 * hh0 + z1 * hh1 + z2 * hh2) : 0.0;
-      }
-      if (live && !use)  // frozen landmark: its observations leave U too
-        for (int o = oa; o < ob; ++o)
-#pragma unroll
-          for (int e = 0; e < 12; ++e) S.Jc[o][e] = 0.0;
-      __syncthreads();  // every lane has read its Jp | r
-      if (live) {
-        double2* zr = reinterpret_cast<double2*>(&S.zb[kZbStride * t]);
-#pragma unroll
-        for (int e = 0; e < 9; ++e) zr[e] = make_double2(W[2 * e], W[2 * e + 1]);
-#pragma unroll
-        for (int e = 0; e < 3; ++e) zr[9 + e] = make_double2(bt[2 * e], bt[2 * e + 1]);
-      }
+      __syncthreads();
+      st.mark(kPhBacksub);
     }
-    __syncthreads();
-    st.mark(kPhElim);
 
-    // Schur items: (active slot, row a) on 2^lg lanes each (ChunkImg::abase / anp), passes
-    // of 64 lanes.  Item value: -sum over its pairs of Z_x[a] Z_y^T (pairs j+2 fetched while
-    // j+1 accumulates, as the four-wave K1); a diagonal slot's lanes add U's row a and b[a]
-    // over their pairs' observations (pair (x, x): track entry x of the slot's camera).  The
-    // parts combine by the aligned butterfly; the item's first lane writes its slab row.
-    {
-      const int nas = h3.z, lanes = S.img.abase[nas];
-      for (int base = 0; base < lanes; base += kLinLanes) {
-        const int t = base + tid;
-        int si = 0;
+    // residuals and Jacobians at the current linearisation point (cost at the updated state)
+    if (tid < nob) obs_lin_w<(MODE & kAccum) != 0, false>(S, A, S.pose_n[S.img.acam[tid]], tid, nullptr, cost);
+    if (MODE & kAccum) {
+      __syncthreads();
+      st.mark(kPhLinObs);
+      // per landmark: V (+lambda), its pivot-tested Cholesky and h = L^-1 g
+      if (tid < npt) {
+        double l[6], h[3];
+        const bool ok = point_block_w(S, A.lambda, tid, l, h);
+        S.valid[tid] = ok;
 #pragma unroll
-        for (int sp = 32; sp > 0; sp >>= 1)
-          if (si + sp < nas && S.img.abase[si + sp] <= t) si += sp;
-        const bool live = t < lanes;
-        const int lgp = live ? S.img.anp[si] : 0, np = 1 << lgp;
-        const int off = t - S.img.abase[si], a = off >> lgp, part = off & (np - 1);
-        const int s = live ? S.img.aslot[si] : 0;
-        const int dcam = live ? S.img.adcam[si] : 0xFF;
-        double out[6] = {0, 0, 0, 0, 0, 0};
-        double ob = 0.0;
-        const int e0 = live ? S.img.slotp[si] + part : 0, e1 = live ? S.img.slotp[si] + S.img.apcnt[si] : 0;
-        if (e0 < e1) {
-          auto zrow = [&](int pr, double (&za)[3], double2 (&zy)[9]) {
-            const double2* py = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr >> 8)]);
+        for (int e = 0; e < 6; ++e) S.L[tid][e] = l[e];
+        S.h[tid][0] = ok ? h[0] : 0.0;
+        S.h[tid][1] = ok ? h[1] : 0.0;
+        S.h[tid][2] = ok ? h[2] : 0.0;
+      }
+      __syncthreads();
+      st.mark(kPhReduce);
+      // per track entry: W = Jc^T Jp, gc = Jc^T r over its observations, then Z = W L^-T and
+      // bt = -gc + Z h (zero, and the observations' Jc zeroed, for a frozen landmark or a
+      // fixed camera); Z | bt overwrite the Jp | r every lane has read
+      {
+        double W[18], g[6];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) zy[k] = py[k];
-            const double* px = &S.zb[kZbStride * (pr & 255) + 3 * a];
-            za[0] = px[0];
-            za[1] = px[1];
-            za[2] = px[2];
-          };
-          auto accum = [&](const double (&za)[3], const double2 (&zy)[9]) {
-            const double* zf = reinterpret_cast<const double*>(zy);
+        for (int e = 0; e < 18; ++e) W[e] = 0.0;
 #pragma unroll
-            for (int c = 0; c < 6; ++c)
-              out[c] -= za[0] * zf[3 * c] + za[1] * zf[3 * c + 1] + za[2] * zf[3 * c + 2];
-          };
-          const int n = (e1 - e0 + np - 1) / np;  // this part's pairs
-          auto pid = [&](int j) { return (int)S.img.pairs[e0 + min(j, n - 1) * np]; };
-          double zaA[3], zaB[3];
-          double2 zyA[9], zyB[9];
-          zrow(pid(0), zaA, zyA);
-          zrow(pid(1), zaB, zyB);
-          int pc = pid(2), pd = pid(3);
-          int j = 0;
-          for (; j + 2 <= n; j += 2) {
-            const int pe = pid(j + 4), pf = pid(j + 5);
-            accum(zaA, zyA);
-            zrow(pc, zaA, zyA);
-            accum(zaB, zyB);
-            zrow(pd, zaB, zyB);
-            pc = pe;
-            pd = pf;
-          }
-          if (j < n) accum(zaA, zyA);
-          if (dcam != 0xFF) {
-            for (int e = e0; e < e1; e += np) {
-              const int x = S.img.pairs[e] & 255;
-              for (int o = S.img.te_obs[x]; o < S.img.te_obs[x + 1]; ++o) {
-                const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
-                double jj[12];
+        for (int e = 0; e < 6; ++e) g[e] = 0.0;
+        const int t = min(tid, max(nte - 1, 0));
+        const bool live = tid < nte;
+        const int oa = S.img.te_obs[t], ob = live ? S.img.te_obs[t + 1] : oa;
+        for (int o = oa; o < ob; ++o) {
 #pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                  const double2 v = jr[k];
-                  jj[2 * k] = v.x;
-                  jj[2 * k + 1] = v.y;
-                }
-                const double ja0 = S.Jc[o][a], ja1 = S.Jc[o][6 + a];
+          for (int k = 0; k < 2; ++k) {
+            const double rk = S.zb[kZbR + 2 * o + k];
+            const double q0 = S.zb[6 * o + 3 * k], q1 = S.zb[6 * o + 3 * k + 1], q2 = S.zb[6 * o + 3 * k + 2];
 #pragma unroll
-                for (int c = 0; c < 6; ++c) out[c] += ja0 * jj[c] + ja1 * jj[6 + c];
-              }
-              ob += S.zb[kZbStride * x + 18 + a];
+            for (int a = 0; a < 6; ++a) {
+              const double jc = S.Jc[o][6 * k + a];
+              W[3 * a] += jc * q0;
+              W[3 * a + 1] += jc * q1;
+              W[3 * a + 2] += jc * q2;
+              g[a] += jc * rk;
             }
           }
         }
+        const int p = S.img.te_pt[t];
+        const bool use = live && S.valid[p] && S.img.te_lcam[t] >= 0;
+        const double i00 = S.L[p][0], l10 = S.L[p][1], i11 = S.L[p][2];
+        const double l20 = S.L[p][3], l21 = S.L[p][4], i22 = S.L[p][5];
+        const double hh0 = S.h[p][0], hh1 = S.h[p][1], hh2 = S.h[p][2];
+        double bt[6];
 #pragma unroll
-        for (int c = 0; c < 6; ++c) out[c] = sum_parts_lane(out[c], lgp);
-        ob = sum_parts_lane(ob, lgp);
-        if (live && part == 0) {
-          st6g(&A.slab[36l * S.spos[s] + 6 * a], out);
-          if (dcam != 0xFF) A.slab_b[6l * S.cpos[dcam] + a] = ob;
+        for (int a = 0; a < 6; ++a) {
+          const double z0 = W[3 * a] * i00;
+          const double z1 = (W[3 * a + 1] - l10 * z0) * i11;
+          const double z2 = (W[3 * a + 2] - l20 * z0 - l21 * z1) * i22;
+          W[3 * a] = use ? z0 : 0.0;
+          W[3 * a + 1] = use ? z1 : 0.0;
+          W[3 * a + 2] = use ? z2 : 0.0;
+          bt[a] = use ? -g[a] + (z0 * hh0 + z1 * hh1 + z2 * hh2) : 0.0;
+        }
+        if (live && !use)  // frozen landmark: its observations leave U too
+          for (int o = oa; o < ob; ++o)
+#pragma unroll
+            for (int e = 0; e < 12; ++e) S.Jc[o][e] = 0.0;
+        __syncthreads();  // every lane has read its Jp | r
+        if (live) {
+          double2* zr = reinterpret_cast<double2*>(&S.zb[kZbStride * t]);
+#pragma unroll
+          for (int e = 0; e < 9; ++e) zr[e] = make_double2(W[2 * e], W[2 * e + 1]);
+#pragma unroll
+          for (int e = 0; e < 3; ++e) zr[9 + e] = make_double2(bt[2 * e], bt[2 * e + 1]);
         }
       }
+      __syncthreads();
+      st.mark(kPhElim);
+
+      // Schur items: (active slot, row a) on 2^lg lanes each (ChunkImg::abase / anp), passes
+      // of 64 lanes.  Item value: -sum over its pairs of Z_x[a] Z_y^T (pairs j+2 fetched while
+      // j+1 accumulates, as the four-wave K1); a diagonal slot's lanes add U's row a and b[a]
+      // over their pairs' observations (pair (x, x): track entry x of the slot's camera).  The
+      // parts combine by the aligned butterfly; the item's first lane writes its slab row.
+      {
+        const int nas = h3.z, lanes = S.img.abase[nas];
+        for (int base = 0; base < lanes; base += kLinLanes) {
+          const int t = base + tid;
+          int si = 0;
+#pragma unroll
+          for (int sp = 32; sp > 0; sp >>= 1)
+            if (si + sp < nas && S.img.abase[si + sp] <= t) si += sp;
+          const bool live = t < lanes;
+          const int lgp = live ? S.img.anp[si] : 0, np = 1 << lgp;
+          const int off = t - S.img.abase[si], a = off >> lgp, part = off & (np - 1);
+          const int s = live ? S.img.aslot[si] : 0;
+          const int dcam = live ? S.img.adcam[si] : 0xFF;
+          double out[6] = {0, 0, 0, 0, 0, 0};
+          double ob = 0.0;
+          const int e0 = live ? S.img.slotp[si] + part : 0, e1 = live ? S.img.slotp[si] + S.img.apcnt[si] : 0;
+          if (e0 < e1) {
+            auto zrow = [&](int pr, double (&za)[3], double2 (&zy)[9]) {
+              const double2* py = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr >> 8)]);
+#pragma unroll
+              for (int k = 0; k < 9; ++k) zy[k] = py[k];
+              const double* px = &S.zb[kZbStride * (pr & 255) + 3 * a];
+              za[0] = px[0];
+              za[1] = px[1];
+              za[2] = px[2];
+            };
+            auto accum = [&](const double (&za)[3], const double2 (&zy)[9]) {
+              const double* zf = reinterpret_cast<const double*>(zy);
+#pragma unroll
+              for (int c = 0; c < 6; ++c)
+                out[c] -= za[0] * zf[3 * c] + za[1] * zf[3 * c + 1] + za[2] * zf[3 * c + 2];
+            };
+            const int n = (e1 - e0 + np - 1) / np;  // this part's pairs
+            auto pid = [&](int j) { return (int)S.img.pairs[e0 + min(j, n - 1) * np]; };
+            double zaA[3], zaB[3];
+            double2 zyA[9], zyB[9];
+            zrow(pid(0), zaA, zyA);
+            zrow(pid(1), zaB, zyB);
+            int pc = pid(2), pd = pid(3);
+            int j = 0;
+            for (; j + 2 <= n; j += 2) {
+              const int pe = pid(j + 4), pf = pid(j + 5);
+              accum(zaA, zyA);
+              zrow(pc, zaA, zyA);
+              accum(zaB, zyB);
+              zrow(pd, zaB, zyB);
+              pc = pe;
+              pd = pf;
+            }
+            if (j < n) accum(zaA, zyA);
+            if (dcam != 0xFF) {
+              for (int e = e0; e < e1; e += np) {
+                const int x = S.img.pairs[e] & 255;
+                for (int o = S.img.te_obs[x]; o < S.img.te_obs[x + 1]; ++o) {
+                  const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
+                  double jj[12];
+#pragma unroll
+                  for (int k = 0; k < 6; ++k) {
+                    const double2 v = jr[k];
+                    jj[2 * k] = v.x;
+                    jj[2 * k + 1] = v.y;
+                  }
+                  const double ja0 = S.Jc[o][a], ja1 = S.Jc[o][6 + a];
+#pragma unroll
+                  for (int c = 0; c < 6; ++c) out[c] += ja0 * jj[c] + ja1 * jj[6 + c];
+                }
+                ob += S.zb[kZbStride * x + 18 + a];
+              }
+            }
+          }
+#pragma unroll
+          for (int c = 0; c < 6; ++c) out[c] = sum_parts_lane(out[c], lgp);
+          ob = sum_parts_lane(ob, lgp);
+          if (live && part == 0) {
+            if (kWin) {  // one owner lane per (slot, row) and chunk: chunk order per entry
+              double* w = &win[36 * s + 6 * a];
+#pragma unroll
+              for (int c = 0; c < 6; ++c) w[c] += out[c];
+              if (dcam != 0xFF) bwin[6 * dcam + a] += ob;
+            } else {
+              st6g(&A.slab[36l * S.spos[s] + 6 * a], out);
+              if (dcam != 0xFF) A.slab_b[6l * S.cpos[dcam] + a] = ob;
+            }
+          }
+        }
+      }
+      st.mark(kPhSchur);
+    }  // kAccum
+    if (kWin) {
+      h0 = n0; h1 = n1; h2 = n2; h3 = n3;
+      n0 = m0; n1 = m1; n2 = m2; n3 = m3;
+      vimg = wimg;
+      vx[0] = wx[0];
+      vx[1] = wx[1];
     }
-    st.mark(kPhSchur);
+  }  // chunks
+  if (kWin && (MODE & kAccum)) {  // the window to its profile-major slab rows
+    __syncthreads();
+    for (int e = tid; e < 36 * nslots; e += 64) A.slab[36l * S.spos[e / 36] + e % 36] = win[e];
+    for (int e = tid; e < 6 * ncams; e += 64) A.slab_b[6l * S.cpos[e / 6] + e % 6] = bwin[e];
   }
-  // chunk cost: a fixed xor butterfly over the wave (deterministic)
+  // segment cost: a fixed xor butterfly over the wave (deterministic)
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) cost += __shfl_xor(cost, m, 64);
   if (tid == 0) A.slab_cost[seg] = cost;
@@ -1662,7 +1734,11 @@ class BAEngine {
     const bool prev_ok = plan_ok_;
     plan_ok_ = false;
     if (err.empty()) {
-      const int ideal = seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus));
+      // one-wave K1: one chunk per segment while the window's chunks fit one round (six
+      // one-wave workgroups per CU); beyond, multi-chunk segments (window in LDS), one round
+      // of four per CU
+      bool win = kLinWave && (int64_t)prob->n_obs > (int64_t)kWaveObsPerCu * std::max(1, ctx_->num_cus);
+      const int ideal = seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, win));
       // the packing target stays the previous plan's while it is within 10 % of this window's
       // (a plan can take over groups only from a plan with the same target)
       const int so = prev_ok && plan_.seg_obs * 10 >= ideal * 9 && plan_.seg_obs * 10 <= ideal * 11 ? plan_.seg_obs
@@ -1673,6 +1749,20 @@ class BAEngine {
       d_chunk_img_.swap(d_chunk_img_prev_);
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
                        prob->obs_uv, so, prev_ok ? &prev_plan_ : nullptr);
+      if (err.empty() && kLinWave && !win && plan_.n_chunks() > kWaveSegsPerCu * std::max(1, ctx_->num_cus)) {
+        win = true;  // more chunks than one round: pack multi-chunk segments after all
+        err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
+                         prob->obs_uv, seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, true)),
+                         prev_ok ? &prev_plan_ : nullptr);
+      }
+      if (err.empty()) {
+        lin_win_ = kLinWave && plan_.n_segments() != plan_.n_chunks();
+        plan_max_slots_ = plan_max_cams_ = 0;
+        for (int s = 0; s < plan_.n_segments(); ++s) {
+          plan_max_slots_ = std::max(plan_max_slots_, plan_.seg_slot_off[s + 1] - plan_.seg_slot_off[s]);
+          plan_max_cams_ = std::max(plan_max_cams_, plan_.seg_cam_off[s + 1] - plan_.seg_cam_off[s]);
+        }
+      }
     }
     if (ctx_->comm && ctx_->comm->nranks > 1) {
       const int32_t F = err.empty() ? plan_.n_free : 0;
@@ -2000,8 +2090,9 @@ class BAEngine {
   // sweep (profiles/r01_segment_sweep.md) predates the three-per-CU K1.
   // The one-wave K1 (kLinWave) runs one chunk per segment: the largest target packs every
   // segment as one chunk (seg_obs = 1).
-  static int segments_target(int num_cus) {
-    return kLinWave ? (1 << 30) : VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
+  static int segments_target(int num_cus, bool win) {
+    if (kLinWave) return win ? kWaveWinSegsPerCu * std::max(1, num_cus) : (1 << 30);
+    return VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
   }
 
   LinArgs lin_args() {
@@ -2035,24 +2126,32 @@ class BAEngine {
       return;
     }
     LinArgs A = lin_args();
-    // one-wave K1: the chunk image of segment s is chunk s
-    VO_REQUIRE(!kLinWave || nseg == plan_.n_chunks(), VO_ERR_STATE, "K1: segments of one chunk expected");
+    // one-wave K1: one chunk per segment (the chunk image of segment s is chunk s), or
+    // multi-chunk segments with the window in dynamic LDS
+    VO_REQUIRE(!kLinWave || lin_win_ || nseg == plan_.n_chunks(), VO_ERR_STATE, "K1: segments of one chunk expected");
+    A.wslots = lin_win_ ? plan_max_slots_ : 0;
+    A.wcams = lin_win_ ? plan_max_cams_ : 0;
+    const size_t dyn = lin_win_ ? 8 * ((size_t)36 * A.wslots + 6 * A.wcams + 6 * kSegCams + 12 * kSegAllCams) : 0;
     dim3 g(nseg), b(kLinWave ? kLinLanes : kLinThreads);
     ctx_->prof.begin(ctx_->stream, kKBaLin);
     if (stamps_on_) {
       d_stamps_.reserve((size_t)nseg * kPhCount * 8);
       A.stamps = d_stamps_.as<unsigned long long>();
     }
-#define VO_LIN_LAUNCH(M)                                                               \
-  do {                                                                                 \
-    if (kLinWave && stamps_on_)                                                        \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true>), g, b, 0, ctx_->stream, A);     \
-    else if (kLinWave)                                                                 \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false>), g, b, 0, ctx_->stream, A);    \
-    else if (stamps_on_)                                                               \
-      hipLaunchKernelGGL((ba_lin_kernel<M, true>), g, b, 0, ctx_->stream, A);          \
-    else                                                                               \
-      hipLaunchKernelGGL((ba_lin_kernel<M, false>), g, b, 0, ctx_->stream, A);         \
+#define VO_LIN_LAUNCH(M)                                                                      \
+  do {                                                                                        \
+    if (kLinWave && lin_win_ && stamps_on_)                                                   \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true, true>), g, b, dyn, ctx_->stream, A);    \
+    else if (kLinWave && lin_win_)                                                            \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true, false>), g, b, dyn, ctx_->stream, A);   \
+    else if (kLinWave && stamps_on_)                                                          \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, true>), g, b, 0, ctx_->stream, A);     \
+    else if (kLinWave)                                                                        \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, false>), g, b, 0, ctx_->stream, A);    \
+    else if (stamps_on_)                                                                      \
+      hipLaunchKernelGGL((ba_lin_kernel<M, true>), g, b, 0, ctx_->stream, A);                 \
+    else                                                                                      \
+      hipLaunchKernelGGL((ba_lin_kernel<M, false>), g, b, 0, ctx_->stream, A);                \
   } while (0)
     switch (mode) {
       case kAccum: VO_LIN_LAUNCH(kAccum); break;
@@ -2240,6 +2339,8 @@ class BAEngine {
   BandSplit band_{};
   bool band_on_ = false;
   bool fuse_ok_ = false;  // K2 fused into K3's launch (see fused())
+  bool lin_win_ = false;  // one-wave K1 over multi-chunk segments (window in dynamic LDS)
+  int plan_max_slots_ = 0, plan_max_cams_ = 0;  // the plan's largest segment window
   BandLds band_lds_;
   BandTables band_tab_;
   DevBuf d_fac_, d_zero_, d_band_tab_, d_red_meta_, d_red_out_, d_red_count_;
