@@ -1,0 +1,116 @@
+// Host check of the one-wave K1's chunk images (tests/test_plan_wave_lanes.py): builds the
+// plan of a window and walks each chunk's Schur lanes exactly as ba_lin_wave_kernel assigns
+// them (passes of kLinLanes, binary search over abase, 2^anp lanes per row), checking that
+//   - every pair of every active slot is summed exactly once per row, by one part;
+//   - every row's parts are aligned lanes of one pass (the DPP butterfly's groups);
+//   - a diagonal slot's pairs are (x, x) over exactly its camera's track entries (so its lanes'
+//     U and b sums equal the camera lists'), adcam names the camera, off-diagonal slots 0xFF;
+//   - with one chunk per segment, every window slot is active and every window camera has a
+//     diagonal slot (every slab row and rhs entry is written).
+// Input (binary): int32 n_poses, n_points, n_obs, n_fixed, seg_obs; point_ptr; obs_cam; obs_uv.
+// Prints "ok <chunks> <segments> <passes> <max chain>" or the first violation.
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ba_plan.h"
+
+namespace vo {
+void* plan_host_alloc(size_t b, bool) { return ::operator new(b < 64 ? 64 : b, std::align_val_t(64)); }
+void plan_host_free(void* p, bool) noexcept {
+  if (p) ::operator delete(p, std::align_val_t(64));
+}
+}  // namespace vo
+
+#define FAIL(...)                      \
+  do {                                 \
+    std::printf("fail: " __VA_ARGS__); \
+    std::printf("\n");                 \
+    return 1;                          \
+  } while (0)
+
+int main(int argc, char** argv) {
+  if (argc < 2) return 2;
+  FILE* f = std::fopen(argv[1], "rb");
+  if (!f) return 2;
+  int32_t hd[5];
+  if (std::fread(hd, 4, 5, f) != 5) return 2;
+  const int N = hd[0], L = hd[1], M = hd[2], nf = hd[3], so = hd[4];
+  std::vector<int32_t> ptr(L + 1), cam(M);
+  std::vector<float> uv(2 * (size_t)M);
+  if (std::fread(ptr.data(), 4, L + 1, f) != (size_t)L + 1 || std::fread(cam.data(), 4, M, f) != (size_t)M ||
+      std::fread(uv.data(), 4, 2 * (size_t)M, f) != 2 * (size_t)M)
+    return 2;
+  std::fclose(f);
+  vo::BAPlan P;
+  const std::string err = vo::build_plan(P, N, L, M, nf, ptr.data(), cam.data(), uv.data(), so, nullptr);
+  if (!err.empty()) FAIL("plan: %s", err.c_str());
+  long passes = 0;
+  int max_chain = 0;
+  for (int si = 0; si < P.n_segments(); ++si) {
+    const int32_t* sh = &P.seg_hdr[(size_t)si * vo::kSegHdr];
+    const int nslots = sh[0], so_ = sh[1], co = sh[2], ncams = sh[3];
+    const bool one = sh[6] - sh[5] == 1;
+    std::vector<int> slot_seen(nslots, 0), cam_diag(ncams, 0);
+    for (int ch = sh[5]; ch < sh[6]; ++ch) {
+      const int32_t* h = &P.chunk_hdr[(size_t)ch * vo::kChunkHdr];
+      const vo::ChunkImg& g = P.chunk_img[ch];
+      const int nas = h[14], lanes = g.abase[nas], npairs = h[9] - h[8];
+      std::vector<int> cover(6 * (size_t)npairs, 0);
+      for (int base = 0; base < lanes; base += vo::kLinLanes, ++passes) {
+        for (int tid = 0; tid < vo::kLinLanes; ++tid) {
+          const int t = base + tid;
+          if (t >= lanes) continue;
+          int s = 0;
+          for (int sp = 32; sp > 0; sp >>= 1)
+            if (s + sp < nas && g.abase[s + sp] <= t) s += sp;
+          const int lgp = g.anp[s], np = 1 << lgp;
+          const int off = t - g.abase[s], a = off >> lgp, part = off & (np - 1);
+          if (a >= 6) FAIL("chunk %d lane %d: row %d", ch, t, a);
+          if ((t - part) / vo::kLinLanes != (t - part + np - 1) / vo::kLinLanes || (t - part) % np)
+            FAIL("chunk %d slot item %d: parts not aligned in one pass", ch, s);
+          int n = 0;
+          for (int e = g.slotp[s] + part; e < g.slotp[s] + g.apcnt[s]; e += np, ++n) ++cover[6 * (size_t)e + a];
+          max_chain = std::max(max_chain, n);
+        }
+      }
+      for (size_t k = 0; k < cover.size(); ++k)
+        if (cover[k] != 1) FAIL("chunk %d: pair %zu row %zu summed %d times", ch, k / 6, k % 6, cover[k]);
+      if (g.slotp[nas] != npairs) FAIL("chunk %d: active slots end at %d of %d pairs", ch, (int)g.slotp[nas], npairs);
+      const int te0 = h[2];
+      for (int s = 0; s < nas; ++s) {
+        const int ws = g.aslot[s];
+        slot_seen[ws] = 1;
+        const int ci = P.slot_i[so_ + ws], cj = P.slot_j[so_ + ws];
+        if (ci != cj) {
+          if (g.adcam[s] != 0xFF) FAIL("chunk %d: off-diagonal slot %d marked camera %d", ch, ws, (int)g.adcam[s]);
+          continue;
+        }
+        const int wc = g.adcam[s];
+        if (wc >= ncams || P.segcam_f[co + wc] != ci) FAIL("chunk %d: diagonal slot %d camera %d", ch, ws, wc);
+        cam_diag[wc] = 1;
+        // its pairs: (x, x) over the chunk's track entries of that camera, each once
+        std::vector<int> tes;
+        for (int e = g.slotp[s]; e < g.slotp[s] + g.apcnt[s]; ++e) {
+          const int x = g.pairs[e] & 255, y = g.pairs[e] >> 8;
+          if (x != y) FAIL("chunk %d: diagonal slot pair (%d, %d)", ch, x, y);
+          tes.push_back(x);
+        }
+        std::vector<int> want;
+        for (int t = te0; t < te0 + h[3]; ++t)
+          if (P.te_lcam[t] == wc) want.push_back(t - te0);
+        if (tes != want) FAIL("chunk %d: camera %d track entries differ", ch, wc);
+      }
+    }
+    if (one) {
+      for (int s = 0; s < nslots; ++s)
+        if (!slot_seen[s]) FAIL("segment %d: window slot %d never written", si, s);
+      for (int c = 0; c < ncams; ++c)
+        if (!cam_diag[c]) FAIL("segment %d: window camera %d without a diagonal slot", si, c);
+    }
+  }
+  std::printf("ok %d %d %ld %d\n", P.n_chunks(), P.n_segments(), passes, max_chain);
+  return 0;
+}
