@@ -393,7 +393,7 @@ def test_slide_takes_groups_over_and_matches_scratch(ctx):
     from visualodometry_amd.synthetic import make_ba_slide
 
     ws = make_ba_slide("cfg3", 3)
-    other = make_ba_config("cfg1")
+    other = make_ba_problem(8, 200, 11)
     iters = 3
     inc = []
     for i, w in enumerate(ws):

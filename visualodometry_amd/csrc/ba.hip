@@ -1107,11 +1107,13 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
       __syncthreads();
       st.mark(kPhElim);
 
-      // Schur items: (active slot, row a) on 2^lg lanes each (ChunkImg::abase / anp), passes
-      // of 64 lanes.  Item value: -sum over its pairs of Z_x[a] Z_y^T (pairs j+2 fetched while
-      // j+1 accumulates, as the four-wave K1); a diagonal slot's lanes add U's row a and b[a]
-      // over their pairs' observations (pair (x, x): track entry x of the slot's camera).  The
-      // parts combine by the aligned butterfly; the item's first lane writes its slab row.
+      // Schur items: a whole active slot block on 2^lg lanes (ChunkImg::abase / anp), passes
+      // of 64 lanes.  Each lane sums -Z_x Z_y^T over its part of the slot's pairs with both
+      // Z rows in registers (18 LDS loads per 108 FMAs; pair j+1's rows are fetched while
+      // pair j accumulates); a diagonal slot's lanes add U and b over their pairs'
+      // observations (pair (x, x): track entry x of the slot's camera).  Parts combine by the
+      // aligned butterfly (levels skipped when no lane of the pass has parts); the first lane
+      // of an item writes its slab row.
       {
         const int nas = h3.z, lanes = S.img.abase[nas];
         for (int base = 0; base < lanes; base += kLinLanes) {
@@ -1122,46 +1124,49 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
             if (si + sp < nas && S.img.abase[si + sp] <= t) si += sp;
           const bool live = t < lanes;
           const int lgp = live ? S.img.anp[si] : 0, np = 1 << lgp;
-          const int off = t - S.img.abase[si], a = off >> lgp, part = off & (np - 1);
+          const int part = (t - S.img.abase[si]) & (np - 1);
           const int s = live ? S.img.aslot[si] : 0;
           const int dcam = live ? S.img.adcam[si] : 0xFF;
-          double out[6] = {0, 0, 0, 0, 0, 0};
-          double ob = 0.0;
+          double out[36], ob[6];
+#pragma unroll
+          for (int e = 0; e < 36; ++e) out[e] = 0.0;
+#pragma unroll
+          for (int e = 0; e < 6; ++e) ob[e] = 0.0;
           const int e0 = live ? S.img.slotp[si] + part : 0, e1 = live ? S.img.slotp[si] + S.img.apcnt[si] : 0;
           if (e0 < e1) {
-            auto zrow = [&](int pr, double (&za)[3], double2 (&zy)[9]) {
+            auto zload = [&](int pr, double2 (&zx)[9], double2 (&zy)[9]) {
+              const double2* px = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr & 255)]);
               const double2* py = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr >> 8)]);
 #pragma unroll
-              for (int k = 0; k < 9; ++k) zy[k] = py[k];
-              const double* px = &S.zb[kZbStride * (pr & 255) + 3 * a];
-              za[0] = px[0];
-              za[1] = px[1];
-              za[2] = px[2];
+              for (int k = 0; k < 9; ++k) {
+                zx[k] = px[k];
+                zy[k] = py[k];
+              }
             };
-            auto accum = [&](const double (&za)[3], const double2 (&zy)[9]) {
-              const double* zf = reinterpret_cast<const double*>(zy);
+            auto accum = [&](const double2 (&zx)[9], const double2 (&zy)[9]) {
+              const double* x = reinterpret_cast<const double*>(zx);
+              const double* y = reinterpret_cast<const double*>(zy);
 #pragma unroll
-              for (int c = 0; c < 6; ++c)
-                out[c] -= za[0] * zf[3 * c] + za[1] * zf[3 * c + 1] + za[2] * zf[3 * c + 2];
+              for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int j = 0; j < 6; ++j)
+                  out[6 * i + j] -= x[3 * i] * y[3 * j] + x[3 * i + 1] * y[3 * j + 1] + x[3 * i + 2] * y[3 * j + 2];
             };
             const int n = (e1 - e0 + np - 1) / np;  // this part's pairs
             auto pid = [&](int j) { return (int)S.img.pairs[e0 + min(j, n - 1) * np]; };
-            double zaA[3], zaB[3];
-            double2 zyA[9], zyB[9];
-            zrow(pid(0), zaA, zyA);
-            zrow(pid(1), zaB, zyB);
-            int pc = pid(2), pd = pid(3);
+            double2 zxA[9], zyA[9], zxB[9], zyB[9];
+            zload(pid(0), zxA, zyA);
+            int pn = pid(1);
             int j = 0;
             for (; j + 2 <= n; j += 2) {
-              const int pe = pid(j + 4), pf = pid(j + 5);
-              accum(zaA, zyA);
-              zrow(pc, zaA, zyA);
-              accum(zaB, zyB);
-              zrow(pd, zaB, zyB);
-              pc = pe;
-              pd = pf;
+              zload(pn, zxB, zyB);
+              pn = pid(j + 2);
+              accum(zxA, zyA);
+              zload(pn, zxA, zyA);
+              pn = pid(j + 3);
+              accum(zxB, zyB);
             }
-            if (j < n) accum(zaA, zyA);
+            if (j < n) accum(zxA, zyA);
             if (dcam != 0xFF) {
               for (int e = e0; e < e1; e += np) {
                 const int x = S.img.pairs[e] & 255;
@@ -1174,26 +1179,63 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
                     jj[2 * k] = v.x;
                     jj[2 * k + 1] = v.y;
                   }
-                  const double ja0 = S.Jc[o][a], ja1 = S.Jc[o][6 + a];
 #pragma unroll
-                  for (int c = 0; c < 6; ++c) out[c] += ja0 * jj[c] + ja1 * jj[6 + c];
+                  for (int i = 0; i < 6; ++i)
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) out[6 * i + c] += jj[i] * jj[c] + jj[6 + i] * jj[6 + c];
                 }
-                ob += S.zb[kZbStride * x + 18 + a];
+                const double2* br = reinterpret_cast<const double2*>(&S.zb[kZbStride * x + 18]);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                  const double2 v = br[k];
+                  ob[2 * k] += v.x;
+                  ob[2 * k + 1] += v.y;
+                }
               }
             }
           }
+          // parts: the aligned butterfly, only the levels some lane of this pass needs
+          const bool b1 = __builtin_amdgcn_ballot_w64(lgp >= 1) != 0;
+          const bool b2 = __builtin_amdgcn_ballot_w64(lgp >= 2) != 0;
+          const bool b3 = __builtin_amdgcn_ballot_w64(lgp >= 3) != 0;
+          auto bfly = [&](double v) {  // sum_parts_lane, levels of this pass only (uniform)
+            if (b1) {
+              const double q = dpp_f64<0xB1>(v);
+              v = lgp >= 1 ? v + q : v;
+            }
+            if (b2) {
+              const double q = dpp_f64<0x4E>(v);
+              v = lgp >= 2 ? v + q : v;
+            }
+            if (b3) {
+              const double q = dpp_f64<0x104>(v);
+              v = lgp >= 3 ? v + q : v;
+            }
+            return v;
+          };
+          if (b1) {
 #pragma unroll
-          for (int c = 0; c < 6; ++c) out[c] = sum_parts_lane(out[c], lgp);
-          ob = sum_parts_lane(ob, lgp);
+            for (int e = 0; e < 36; ++e) out[e] = bfly(out[e]);
+#pragma unroll
+            for (int e = 0; e < 6; ++e) ob[e] = bfly(ob[e]);
+          }
           if (live && part == 0) {
-            if (kWin) {  // one owner lane per (slot, row) and chunk: chunk order per entry
-              double* w = &win[36 * s + 6 * a];
+            if (kWin) {  // one owner lane per slot and chunk: chunk order per entry
+              double* w = &win[36 * s];
 #pragma unroll
-              for (int c = 0; c < 6; ++c) w[c] += out[c];
-              if (dcam != 0xFF) bwin[6 * dcam + a] += ob;
+              for (int e = 0; e < 36; ++e) w[e] += out[e];
+              if (dcam != 0xFF)
+#pragma unroll
+                for (int e = 0; e < 6; ++e) bwin[6 * dcam + e] += ob[e];
             } else {
-              st6g(&A.slab[36l * S.spos[s] + 6 * a], out);
-              if (dcam != 0xFF) A.slab_b[6l * S.cpos[dcam] + a] = ob;
+              double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s]]);
+#pragma unroll
+              for (int e = 0; e < 18; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
+              if (dcam != 0xFF) {
+                double2* wb = reinterpret_cast<double2*>(&A.slab_b[6l * S.cpos[dcam]]);
+#pragma unroll
+                for (int e = 0; e < 3; ++e) wb[e] = make_double2(ob[2 * e], ob[2 * e + 1]);
+              }
             }
           }
         }

@@ -854,19 +854,22 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         // in it, compacted in window order (their lists keep their order)
         int nas = 0, nac = 0;
         {
-          // active slots; lanes per row item doubled greedily for the slot with the longest
-          // per-lane pair chain while 6 lanes x the sum fit the lane budget.  Four-wave K1: one
-          // pass of its 256 lanes (more than 42 active slots take one lane per row item, in
-          // two passes).  One-wave K1 (kLinWave): passes of 64 lanes run one after another,
-          // each as long as its longest chain, so the budget is the smallest whole number of
-          // passes or one more, whichever the pass-time estimate prefers.  A diagonal slot's
-          // lanes also sum U and b over their pairs' observations (about twice a pair's work).
+          // active slots; parts per item (2^lg lanes) doubled greedily for the slot with the
+          // longest per-lane pair chain while the lanes fit the budget.  Four-wave K1: an item
+          // is a (slot, row) on one lane per part, one pass of its 256 lanes (more than 42
+          // active slots take one lane per row item, in two passes).  One-wave K1 (kLinWave):
+          // an item is a whole slot block on one lane per part (kRowLanes = 1), passes of 64
+          // lanes run one after another, each as long as its longest chain, so the budget is the
+          // smallest whole number of passes or one more, whichever the pass-time estimate
+          // prefers.  A diagonal slot's lanes also sum U and b over their pairs' observations.
           int sl[kSegSlots], cntp[kSegSlots], lg[kSegSlots], wt[kSegSlots];
           for (int i = 0; i < ns; ++i)
             if (P.slot_ptr[sb + i + 1] > P.slot_ptr[sb + i]) {
               sl[nas] = i;
               cntp[nas] = P.slot_ptr[sb + i + 1] - P.slot_ptr[sb + i];
-              wt[nas] = kLinWave && P.slot_i[so + i] == P.slot_j[so + i] ? 2 : 1;
+              // cost units per pair: the one-wave K1's lane sums a whole 6x6 block per pair (a
+              // diagonal slot's also U and b of the pair's observations)
+              wt[nas] = !kLinWave ? 1 : P.slot_i[so + i] == P.slot_j[so + i] ? 4 : 3;
               lg[nas++] = 0;
             }
           auto chain_of = [&](int i, int l) { return ((cntp[i] + (1 << l) - 1) >> l) * wt[i]; };
@@ -883,7 +886,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
                 }
               }
               if (best < 0 || ((cntp[best] + (1 << lv[best]) - 1) >> lv[best]) <= 1 || lv[best] == 3 ||
-                  6 * (used + (1 << lv[best])) > budget)
+                  kRowLanes * (used + (1 << lv[best])) > budget)
                 break;
               used += 1 << lv[best];
               ++lv[best];
@@ -903,24 +906,26 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
             balance(kLinLanes, lg);
             order(lg);
           } else {
-            // pass-time estimate: per 64-lane pass its longest chain plus a fixed cost per pass
+            // pass-time estimate: per 64-lane pass its longest chain, a fixed cost and the
+            // butterfly levels its widest item needs (~one pair each)
             auto estimate = [&](const int* lv) {
               order(lv);
-              int t = 0, pass = 0, pmax = 0, lane = 0;
+              int t = 0, pass = 0, pmax = 0, lmax = 0, lane = 0;
               for (int j = 0; j < nas; ++j) {
                 const int i = ord[j], c = chain_of(i, lv[i]);
-                for (int r = 0; r < 6; ++r, lane += 1 << lv[i]) {
+                for (int r = 0; r < kRowLanes; ++r, lane += 1 << lv[i]) {
                   if (lane / kLinLanes != pass) {
-                    t += pmax + 4;
+                    t += pmax + 2 + 3 * lmax;
                     pass = lane / kLinLanes;
-                    pmax = 0;
+                    pmax = lmax = 0;
                   }
                   pmax = std::max(pmax, c);
+                  lmax = std::max(lmax, lv[i]);
                 }
               }
-              return t + pmax + 4;
+              return t + pmax + 2 + 3 * lmax;
             };
-            const int p0 = std::max(1, (6 * nas + kLinLanes - 1) / kLinLanes);
+            const int p0 = std::max(1, (kRowLanes * nas + kLinLanes - 1) / kLinLanes);
             int lg1[kSegSlots];
             balance(kLinLanes * p0, lg);
             balance(kLinLanes * (p0 + 1), lg1);
@@ -937,7 +942,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
             g.anp[j] = (uint8_t)lg[i];
             g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
             g.abase[j] = (uint16_t)base;
-            base += 6 << lg[i];
+            base += kRowLanes << lg[i];
           }
           g.abase[nas] = (uint16_t)base;
           g.slotp[nas] = e1 - e0;

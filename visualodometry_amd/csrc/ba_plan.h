@@ -59,6 +59,7 @@ constexpr int kSegSlots = 64;
 #endif
 constexpr bool kLinWave = VO_BA_K1_WAVE != 0;
 constexpr int kLinLanes = kLinWave ? 64 : 256;  // K1 lanes per Schur pass (ba.hip)
+constexpr int kRowLanes = kLinWave ? 1 : 6;      // lanes per Schur item part: one per block row, or one per block
 constexpr int kChunkHdr = 16;
 
 constexpr int kSegCams = 24;     // free (window) cameras of a segment
@@ -93,9 +94,10 @@ struct alignas(16) ChunkImg {
   uint8_t dslot[kSegCams];         // active camera i -> its diagonal slot
   uint8_t aslot[kSegSlots];        // active slot i -> window slot
   uint8_t acid[kSegCams];          // active camera i -> window camera
-  // Schur-pair lanes, balanced: active slot i (ordered by lanes-per-row descending) sums its
-  // apcnt[i] pairs from slotp[i] on 6 << anp[i] lanes starting at abase[i] (2^anp lanes per
-  // row, their strided partial sums combined by an aligned butterfly); abase[nas] = lanes used
+  // Schur-pair lanes, balanced: active slot i (ordered by lanes per item descending) sums its
+  // apcnt[i] pairs from slotp[i] on kRowLanes << anp[i] lanes starting at abase[i] (2^anp parts
+  // per row, or per block in the one-wave K1, their strided partial sums combined by an aligned
+  // butterfly); abase[nas] = lanes used
   uint16_t apcnt[kSegSlots];
   uint16_t abase[kSegSlots + 1];  // up to 6 x 64 lanes (two passes of the workgroup)
   uint8_t anp[kSegSlots];

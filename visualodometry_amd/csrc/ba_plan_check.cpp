@@ -67,12 +67,15 @@ int main(int argc, char** argv) {
           for (int sp = 32; sp > 0; sp >>= 1)
             if (s + sp < nas && g.abase[s + sp] <= t) s += sp;
           const int lgp = g.anp[s], np = 1 << lgp;
+          // four-wave K1: lane = (row a, part); one-wave K1: lane = part of the whole block
           const int off = t - g.abase[s], a = off >> lgp, part = off & (np - 1);
-          if (a >= 6) FAIL("chunk %d lane %d: row %d", ch, t, a);
+          if (a >= 6 / vo::kRowLanes) FAIL("chunk %d lane %d: row %d", ch, t, a);
           if ((t - part) / vo::kLinLanes != (t - part + np - 1) / vo::kLinLanes || (t - part) % np)
             FAIL("chunk %d slot item %d: parts not aligned in one pass", ch, s);
           int n = 0;
-          for (int e = g.slotp[s] + part; e < g.slotp[s] + g.apcnt[s]; e += np, ++n) ++cover[6 * (size_t)e + a];
+          for (int e = g.slotp[s] + part; e < g.slotp[s] + g.apcnt[s]; e += np, ++n)
+            for (int r = 0; r < 6; ++r)
+              if (vo::kRowLanes == 1 || r == a) ++cover[6 * (size_t)e + r];
           max_chain = std::max(max_chain, n);
         }
       }
