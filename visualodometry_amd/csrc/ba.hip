@@ -800,7 +800,7 @@ constexpr int kWaveWinSegsPerCu = 4;  // multi-chunk segments: static image + a 
 __device__ __forceinline__ bool point_block_w(const LinWave& S, double lambda, int p, double (&l)[6],
                                               double (&h)[3]) {
   double v00 = 0, v01 = 0, v02 = 0, v11 = 0, v12 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
-  const int o0 = S.img.te_obs[S.img.pt_te[p]], o1 = S.img.te_obs[S.img.pt_te[p + 1]];
+  const int o0 = S.img.pt_obs[p], o1 = S.img.pt_obs[p + 1];
   for (int o = o0; o < o1; ++o) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -836,7 +836,7 @@ __device__ __forceinline__ bool point_block_w(const LinWave& S, double lambda, i
 template <bool kJc, bool kBack>
 __device__ __forceinline__ void obs_lin_w(LinWave& S, const LinArgs& A, const double* T, int o,
                                           const double* dc, double& cost) {
-  const int q = S.img.te_pt[S.img.obs_te[o]];
+  const int q = S.img.obs_pt[o];
   const double X0 = S.X[q][0], X1 = S.X[q][1], X2 = S.X[q][2];
   const double x = T[0] * X0 + T[1] * X1 + T[2] * X2 + T[9];
   const double y = T[3] * X0 + T[4] * X1 + T[5] * X2 + T[10];
@@ -1008,7 +1008,7 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
       // the pending step at its linearisation point: r + Jc dc and Jp per observation, then
       // dp = -V^-1 sum Jp^T (r + Jc dc) per landmark (chunk_backsub)
       if (tid < nob) {
-        const int lc = S.img.te_lcam[S.img.obs_te[tid]];
+        const int lc = S.img.obs_lcam[tid];
         obs_lin_w<false, true>(S, A, &pose_o[12 * S.img.acam[tid]], tid, lc >= 0 ? &dcw[6 * lc] : nullptr, cost);
       }
       __syncthreads();

@@ -849,7 +849,14 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
           g.te_pt[i] = P.te_pt[te0 + i] - p0;
           g.te_lcam[i] = P.te_lcam[te0 + i];
         }
-        for (int i = 0; i <= npt; ++i) g.pt_te[i] = P.pt_te[p0 + i] - te0;
+        for (int i = 0; i <= npt; ++i) {
+          g.pt_te[i] = P.pt_te[p0 + i] - te0;
+          g.pt_obs[i] = P.te_obs[P.pt_te[p0 + i]] - ob0;
+        }
+        for (int i = 0; i < nob; ++i) {
+          g.obs_pt[i] = g.te_pt[g.obs_te[i]];
+          g.obs_lcam[i] = g.te_lcam[g.obs_te[i]];
+        }
         // the slots with pairs in this chunk and the cameras with track entries or observations
         // in it, compacted in window order (their lists keep their order)
         int nas = 0, nac = 0;

@@ -86,6 +86,10 @@ struct alignas(16) ChunkImg {
   uint8_t te_pt[kChunkTe];         // track entry -> chunk landmark
   int8_t te_lcam[kChunkTe];        // track entry -> window camera, -1 if fixed
   uint8_t pt_te[kChunkPts + 1];    // landmark -> first chunk track entry
+  // the same relations one LDS level shorter (one-wave K1)
+  uint8_t obs_pt[kChunkObs];       // observation -> chunk landmark
+  int8_t obs_lcam[kChunkObs];      // observation -> window camera, -1 if fixed
+  uint8_t pt_obs[kChunkPts + 1];   // landmark -> first chunk observation
   // Only the window slots and cameras this chunk touches (header ints 14 and 15 count them),
   // so K1's Schur loops run over the chunk's own items, not the whole segment window.
   uint16_t slotp[kSegSlots + 1];   // active slot i -> its first pair-list entry
