@@ -878,6 +878,100 @@ __device__ __forceinline__ void obs_lin_w(LinWave& S, const LinArgs& A, const do
   jp[5] = j11 * T[5] + j12 * T[8];
 }
 
+// One lane's share of a Schur item (one-wave K1): rows r0 .. r0 + R - 1 of active slot si's
+// block, -sum over the slot's pairs of Z_x[rows] Z_y^T as FMA chains with both Z rows in
+// registers (pair j+1's rows fetched while pair j accumulates); a diagonal slot's lane adds U's
+// and b's rows over its pairs' observations (pair (x, x): track entry x of the slot's camera).
+// The rows go straight to the slab (or, kWin, into the segment window).
+template <int R, bool kWin>
+__device__ __forceinline__ void schur_rows(const LinWave& S, const LinArgs& A, int si, int r0, bool live,
+                                           double* win, double* bwin) {
+  double out[6 * R], ob[R];
+#pragma unroll
+  for (int e = 0; e < 6 * R; ++e) out[e] = 0.0;
+#pragma unroll
+  for (int e = 0; e < R; ++e) ob[e] = 0.0;
+  const int e0 = S.img.slotp[si], n = live ? S.img.apcnt[si] : 0;
+  const int dcam = S.img.adcam[si], s = S.img.aslot[si];
+  if (n > 0) {
+    auto zload = [&](int pr, double (&zx)[3 * R], double2 (&zy)[9]) {
+      const double* px = &S.zb[kZbStride * (pr & 255) + 3 * r0];
+      const double2* py = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr >> 8)]);
+#pragma unroll
+      for (int k = 0; k < 3 * R; ++k) zx[k] = px[k];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) zy[k] = py[k];
+    };
+    auto accum = [&](const double (&x)[3 * R], const double2 (&zy)[9]) {
+      const double* y = reinterpret_cast<const double*>(zy);
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          double v = out[6 * i + j];
+          v = __builtin_fma(-x[3 * i], y[3 * j], v);
+          v = __builtin_fma(-x[3 * i + 1], y[3 * j + 1], v);
+          out[6 * i + j] = __builtin_fma(-x[3 * i + 2], y[3 * j + 2], v);
+        }
+    };
+    auto pid = [&](int j) { return (int)S.img.pairs[e0 + min(j, n - 1)]; };
+    double zxA[3 * R], zxB[3 * R];
+    double2 zyA[9], zyB[9];
+    zload(pid(0), zxA, zyA);
+    int pn = pid(1);
+    int j = 0;
+    for (; j + 2 <= n; j += 2) {
+      zload(pn, zxB, zyB);
+      pn = pid(j + 2);
+      accum(zxA, zyA);
+      zload(pn, zxA, zyA);
+      pn = pid(j + 3);
+      accum(zxB, zyB);
+    }
+    if (j < n) accum(zxA, zyA);
+    if (dcam != 0xFF) {
+      for (int e = e0; e < e0 + n; ++e) {
+        const int x = S.img.pairs[e] & 255;
+        for (int o = S.img.te_obs[x]; o < S.img.te_obs[x + 1]; ++o) {
+          const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
+          double jj[12];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            const double2 v = jr[k];
+            jj[2 * k] = v.x;
+            jj[2 * k + 1] = v.y;
+          }
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            const double ja0 = S.Jc[o][r0 + i], ja1 = S.Jc[o][6 + r0 + i];
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+              out[6 * i + c] = __builtin_fma(ja1, jj[6 + c], __builtin_fma(ja0, jj[c], out[6 * i + c]));
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) ob[i] += S.zb[kZbStride * x + 18 + r0 + i];
+      }
+    }
+  }
+  if (!live) return;
+  if (kWin) {  // one owner lane per (slot, rows) and chunk: chunk order per entry
+    double* w = &win[36 * s + 6 * r0];
+#pragma unroll
+    for (int e = 0; e < 6 * R; ++e) w[e] += out[e];
+    if (dcam != 0xFF)
+#pragma unroll
+      for (int i = 0; i < R; ++i) bwin[6 * dcam + r0 + i] += ob[i];
+  } else {
+    double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s] + 6 * r0]);
+#pragma unroll
+    for (int e = 0; e < 3 * R; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
+    if (dcam != 0xFF)
+#pragma unroll
+      for (int i = 0; i < R; ++i) A.slab_b[6l * S.cpos[dcam] + r0 + i] = ob[i];
+  }
+}
+
 // kWin: a segment of several chunks walked by its wave (windows too large for one chunk per
 // workgroup), its window accumulated in dynamic LDS [win (wslots x 36) | bwin (wcams x 6) |
 // dc (kSegCams x 6) | pose_o (kSegAllCams x 12)] and written once at the end; otherwise the
@@ -1107,13 +1201,9 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
       __syncthreads();
       st.mark(kPhElim);
 
-      // Schur items: a whole active slot block on 2^lg lanes (ChunkImg::abase / anp), passes
-      // of 64 lanes.  Each lane sums -Z_x Z_y^T over its part of the slot's pairs with both
-      // Z rows in registers (18 LDS loads per 108 FMAs; pair j+1's rows are fetched while
-      // pair j accumulates); a diagonal slot's lanes add U and b over their pairs'
-      // observations (pair (x, x): track entry x of the slot's camera).  Parts combine by the
-      // aligned butterfly (levels skipped when no lane of the pass has parts); the first lane
-      // of an item writes its slab row.
+      // Schur items: an active slot block split by rows over 6 / R lanes, R rows each
+      // (ChunkImg::abase / anp); every 64-lane pass has one R, so its lanes run one code path
+      // (schur_rows<R>) and no lane sums another's partials.
       {
         const int nas = h3.z, lanes = S.img.abase[nas];
         for (int base = 0; base < lanes; base += kLinLanes) {
@@ -1122,121 +1212,14 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
 #pragma unroll
           for (int sp = 32; sp > 0; sp >>= 1)
             if (si + sp < nas && S.img.abase[si + sp] <= t) si += sp;
-          const bool live = t < lanes;
-          const int lgp = live ? S.img.anp[si] : 0, np = 1 << lgp;
-          const int part = (t - S.img.abase[si]) & (np - 1);
-          const int s = live ? S.img.aslot[si] : 0;
-          const int dcam = live ? S.img.adcam[si] : 0xFF;
-          double out[36], ob[6];
-#pragma unroll
-          for (int e = 0; e < 36; ++e) out[e] = 0.0;
-#pragma unroll
-          for (int e = 0; e < 6; ++e) ob[e] = 0.0;
-          const int e0 = live ? S.img.slotp[si] + part : 0, e1 = live ? S.img.slotp[si] + S.img.apcnt[si] : 0;
-          if (e0 < e1) {
-            auto zload = [&](int pr, double2 (&zx)[9], double2 (&zy)[9]) {
-              const double2* px = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr & 255)]);
-              const double2* py = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr >> 8)]);
-#pragma unroll
-              for (int k = 0; k < 9; ++k) {
-                zx[k] = px[k];
-                zy[k] = py[k];
-              }
-            };
-            auto accum = [&](const double2 (&zx)[9], const double2 (&zy)[9]) {
-              const double* x = reinterpret_cast<const double*>(zx);
-              const double* y = reinterpret_cast<const double*>(zy);
-#pragma unroll
-              for (int i = 0; i < 6; ++i)
-#pragma unroll
-                for (int j = 0; j < 6; ++j)
-                  out[6 * i + j] -= x[3 * i] * y[3 * j] + x[3 * i + 1] * y[3 * j + 1] + x[3 * i + 2] * y[3 * j + 2];
-            };
-            const int n = (e1 - e0 + np - 1) / np;  // this part's pairs
-            auto pid = [&](int j) { return (int)S.img.pairs[e0 + min(j, n - 1) * np]; };
-            double2 zxA[9], zyA[9], zxB[9], zyB[9];
-            zload(pid(0), zxA, zyA);
-            int pn = pid(1);
-            int j = 0;
-            for (; j + 2 <= n; j += 2) {
-              zload(pn, zxB, zyB);
-              pn = pid(j + 2);
-              accum(zxA, zyA);
-              zload(pn, zxA, zyA);
-              pn = pid(j + 3);
-              accum(zxB, zyB);
-            }
-            if (j < n) accum(zxA, zyA);
-            if (dcam != 0xFF) {
-              for (int e = e0; e < e1; e += np) {
-                const int x = S.img.pairs[e] & 255;
-                for (int o = S.img.te_obs[x]; o < S.img.te_obs[x + 1]; ++o) {
-                  const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
-                  double jj[12];
-#pragma unroll
-                  for (int k = 0; k < 6; ++k) {
-                    const double2 v = jr[k];
-                    jj[2 * k] = v.x;
-                    jj[2 * k + 1] = v.y;
-                  }
-#pragma unroll
-                  for (int i = 0; i < 6; ++i)
-#pragma unroll
-                    for (int c = 0; c < 6; ++c) out[6 * i + c] += jj[i] * jj[c] + jj[6 + i] * jj[6 + c];
-                }
-                const double2* br = reinterpret_cast<const double2*>(&S.zb[kZbStride * x + 18]);
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                  const double2 v = br[k];
-                  ob[2 * k] += v.x;
-                  ob[2 * k + 1] += v.y;
-                }
-              }
-            }
-          }
-          // parts: the aligned butterfly, only the levels some lane of this pass needs
-          const bool b1 = __builtin_amdgcn_ballot_w64(lgp >= 1) != 0;
-          const bool b2 = __builtin_amdgcn_ballot_w64(lgp >= 2) != 0;
-          const bool b3 = __builtin_amdgcn_ballot_w64(lgp >= 3) != 0;
-          auto bfly = [&](double v) {  // sum_parts_lane, levels of this pass only (uniform)
-            if (b1) {
-              const double q = dpp_f64<0xB1>(v);
-              v = lgp >= 1 ? v + q : v;
-            }
-            if (b2) {
-              const double q = dpp_f64<0x4E>(v);
-              v = lgp >= 2 ? v + q : v;
-            }
-            if (b3) {
-              const double q = dpp_f64<0x104>(v);
-              v = lgp >= 3 ? v + q : v;
-            }
-            return v;
-          };
-          if (b1) {
-#pragma unroll
-            for (int e = 0; e < 36; ++e) out[e] = bfly(out[e]);
-#pragma unroll
-            for (int e = 0; e < 6; ++e) ob[e] = bfly(ob[e]);
-          }
-          if (live && part == 0) {
-            if (kWin) {  // one owner lane per slot and chunk: chunk order per entry
-              double* w = &win[36 * s];
-#pragma unroll
-              for (int e = 0; e < 36; ++e) w[e] += out[e];
-              if (dcam != 0xFF)
-#pragma unroll
-                for (int e = 0; e < 6; ++e) bwin[6 * dcam + e] += ob[e];
-            } else {
-              double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s]]);
-#pragma unroll
-              for (int e = 0; e < 18; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
-              if (dcam != 0xFF) {
-                double2* wb = reinterpret_cast<double2*>(&A.slab_b[6l * S.cpos[dcam]]);
-#pragma unroll
-                for (int e = 0; e < 3; ++e) wb[e] = make_double2(ob[2 * e], ob[2 * e + 1]);
-              }
-            }
+          const int R = __builtin_amdgcn_readfirstlane(S.img.anp[si]);  // one per pass
+          const int off = t - S.img.abase[si];
+          const bool live = t < lanes && off < 6 / R;
+          switch (R) {
+            case 6: schur_rows<6, kWin>(S, A, si, 0, live, win, bwin); break;
+            case 3: schur_rows<3, kWin>(S, A, si, 3 * off, live, win, bwin); break;
+            case 2: schur_rows<2, kWin>(S, A, si, 2 * off, live, win, bwin); break;
+            default: schur_rows<1, kWin>(S, A, si, off, live, win, bwin); break;
           }
         }
       }

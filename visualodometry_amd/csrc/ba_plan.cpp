@@ -909,47 +909,66 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
               return kLinWave && chain_of(a, lv[a]) > chain_of(b, lv[b]);
             });
           };
+          int base = 0;
           if (!kLinWave) {
             balance(kLinLanes, lg);
             order(lg);
+            for (int j = 0; j < nas; ++j) {
+              const int i = ord[j];
+              g.aslot[j] = (uint8_t)sl[i];
+              g.slotp[j] = P.slot_ptr[sb + sl[i]] - e0;
+              g.apcnt[j] = (uint16_t)cntp[i];
+              g.anp[j] = (uint8_t)lg[i];
+              g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
+              g.abase[j] = (uint16_t)base;
+              base += kRowLanes << lg[i];
+            }
           } else {
-            // pass-time estimate: per 64-lane pass its longest chain, a fixed cost and the
-            // butterfly levels its widest item needs (~one pair each)
-            auto estimate = [&](const int* lv) {
-              order(lv);
-              int t = 0, pass = 0, pmax = 0, lmax = 0, lane = 0;
-              for (int j = 0; j < nas; ++j) {
-                const int i = ord[j], c = chain_of(i, lv[i]);
-                for (int r = 0; r < kRowLanes; ++r, lane += 1 << lv[i]) {
-                  if (lane / kLinLanes != pass) {
-                    t += pmax + 2 + 3 * lmax;
-                    pass = lane / kLinLanes;
-                    pmax = lmax = 0;
-                  }
-                  pmax = std::max(pmax, c);
-                  lmax = std::max(lmax, lv[i]);
+            // One-wave K1: an item is a slot block split by rows over 6 / R lanes, R rows each
+            // (anp = R), and every 64-lane pass has one R (the lanes of a pass run the same
+            // code, no cross-lane sums).  The k items of longest pair chains (a diagonal slot's
+            // pair also carries U and b: weight 5 against 3) go to passes of R in {3, 2, 1},
+            // the rest one lane each (R = 6); k and R minimise the estimate sum over passes of
+            // longest chain x per-pair cost (18 R FMAs + loads) + a fixed cost per pass.
+            int w[kSegSlots];
+            for (int i = 0; i < nas; ++i) {
+              w[i] = cntp[i] * (wt[i] == 4 ? 5 : 3);
+              ord[i] = i;
+            }
+            std::stable_sort(ord, ord + nas, [&](int a, int b) { return w[a] > w[b]; });
+            auto cost = [](int R) { return 18 * R + 12; };
+            constexpr int kPassCost = 600;  // per pass (in the same units: chain x pair cost / 3)
+            auto light = [&](int k) {  // items k.. one lane each
+              long t = 0;
+              for (int j = k; j < nas; j += kLinLanes) t += (long)w[ord[j]] * cost(6) / 3 + kPassCost;
+              return t;
+            };
+            int bk = 0, bR = 6;
+            long best = light(0);
+            for (int R : {3, 2, 1}) {
+              const int m = kLinLanes / (6 / R);  // items per pass
+              for (int k = 1; k <= std::min(nas, 24); ++k) {
+                long t = light(k);
+                for (int j = 0; j < k; j += m) t += (long)w[ord[j]] * cost(R) / 3 + kPassCost;
+                if (t < best) {
+                  best = t;
+                  bk = k;
+                  bR = R;
                 }
               }
-              return t + pmax + 2 + 3 * lmax;
-            };
-            const int p0 = std::max(1, (kRowLanes * nas + kLinLanes - 1) / kLinLanes);
-            int lg1[kSegSlots];
-            balance(kLinLanes * p0, lg);
-            balance(kLinLanes * (p0 + 1), lg1);
-            if (estimate(lg1) < estimate(lg))
-              for (int i = 0; i < nas; ++i) lg[i] = lg1[i];
-            order(lg);
-          }
-          int base = 0;
-          for (int j = 0; j < nas; ++j) {
-            const int i = ord[j];
-            g.aslot[j] = (uint8_t)sl[i];
-            g.slotp[j] = P.slot_ptr[sb + sl[i]] - e0;
-            g.apcnt[j] = (uint16_t)cntp[i];
-            g.anp[j] = (uint8_t)lg[i];
-            g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
-            g.abase[j] = (uint16_t)base;
-            base += kRowLanes << lg[i];
+            }
+            for (int j = 0; j < nas; ++j) {
+              const int i = ord[j], R = j < bk ? bR : 6, nl = 6 / R;
+              if ((j == bk && base % kLinLanes) || base / kLinLanes != (base + nl - 1) / kLinLanes)
+                base = (base + kLinLanes - 1) / kLinLanes * kLinLanes;  // a new pass: R changes, or the item would straddle
+              g.aslot[j] = (uint8_t)sl[i];
+              g.slotp[j] = P.slot_ptr[sb + sl[i]] - e0;
+              g.apcnt[j] = (uint16_t)cntp[i];
+              g.anp[j] = (uint8_t)R;
+              g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
+              g.abase[j] = (uint16_t)base;
+              base += nl;
+            }
           }
           g.abase[nas] = (uint16_t)base;
           g.slotp[nas] = e1 - e0;

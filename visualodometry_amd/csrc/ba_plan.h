@@ -98,10 +98,12 @@ struct alignas(16) ChunkImg {
   uint8_t dslot[kSegCams];         // active camera i -> its diagonal slot
   uint8_t aslot[kSegSlots];        // active slot i -> window slot
   uint8_t acid[kSegCams];          // active camera i -> window camera
-  // Schur-pair lanes, balanced: active slot i (ordered by lanes per item descending) sums its
-  // apcnt[i] pairs from slotp[i] on kRowLanes << anp[i] lanes starting at abase[i] (2^anp parts
-  // per row, or per block in the one-wave K1, their strided partial sums combined by an aligned
-  // butterfly); abase[nas] = lanes used
+  // Schur-pair lanes, balanced.  Four-wave K1: active slot i (ordered by lanes per item
+  // descending) sums its apcnt[i] pairs from slotp[i] on 6 << anp[i] lanes starting at abase[i]
+  // (2^anp lanes per row, their strided partial sums combined by an aligned butterfly).
+  // One-wave K1: slot i's block is split by rows over 6 / anp[i] lanes from abase[i], anp[i] rows
+  // each, every pair on every lane; each 64-lane pass has one anp (lanes past an item's end
+  // idle).  abase[nas] = lanes used
   uint16_t apcnt[kSegSlots];
   uint16_t abase[kSegSlots + 1];  // up to 6 x 64 lanes (two passes of the workgroup)
   uint8_t anp[kSegSlots];

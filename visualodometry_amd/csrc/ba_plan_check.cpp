@@ -8,7 +8,7 @@
 //   - with one chunk per segment, every window slot is active and every window camera has a
 //     diagonal slot (every slab row and rhs entry is written).
 // Input (binary): int32 n_poses, n_points, n_obs, n_fixed, seg_obs; point_ptr; obs_cam; obs_uv.
-// Prints "ok <chunks> <segments> <passes> <max chain>" or the first violation.
+// Prints "ok <chunks> <segments> <passes> <max chain (pair rows)>" or the first violation.
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -60,23 +60,42 @@ int main(int argc, char** argv) {
       const int nas = h[14], lanes = g.abase[nas], npairs = h[9] - h[8];
       std::vector<int> cover(6 * (size_t)npairs, 0);
       for (int base = 0; base < lanes; base += vo::kLinLanes, ++passes) {
+        int pass_r = -1;
         for (int tid = 0; tid < vo::kLinLanes; ++tid) {
           const int t = base + tid;
           if (t >= lanes) continue;
           int s = 0;
           for (int sp = 32; sp > 0; sp >>= 1)
             if (s + sp < nas && g.abase[s + sp] <= t) s += sp;
-          const int lgp = g.anp[s], np = 1 << lgp;
-          // four-wave K1: lane = (row a, part); one-wave K1: lane = part of the whole block
-          const int off = t - g.abase[s], a = off >> lgp, part = off & (np - 1);
-          if (a >= 6 / vo::kRowLanes) FAIL("chunk %d lane %d: row %d", ch, t, a);
-          if ((t - part) / vo::kLinLanes != (t - part + np - 1) / vo::kLinLanes || (t - part) % np)
-            FAIL("chunk %d slot item %d: parts not aligned in one pass", ch, s);
+          const int off = t - g.abase[s];
+          int r0, r1, part, np;
+          if (vo::kLinWave) {  // rows [off R, off R + R) of the block, every pair
+            const int R = g.anp[s];
+            if (R != 1 && R != 2 && R != 3 && R != 6) FAIL("chunk %d item %d: %d rows per lane", ch, s, R);
+            if (off >= 6 / R) continue;  // idle lane past the item
+            if (pass_r >= 0 && pass_r != R) FAIL("chunk %d pass %d: rows per lane %d and %d", ch, base / 64, pass_r, R);
+            pass_r = R;
+            if (g.abase[s] / vo::kLinLanes != (g.abase[s] + 6 / R - 1) / vo::kLinLanes)
+              FAIL("chunk %d item %d straddles a pass", ch, s);
+            r0 = off * R;
+            r1 = r0 + R;
+            part = 0;
+            np = 1;
+          } else {  // lane = (row a, part)
+            const int lgp = g.anp[s];
+            np = 1 << lgp;
+            const int a = off >> lgp;
+            part = off & (np - 1);
+            if (a >= 6) FAIL("chunk %d lane %d: row %d", ch, t, a);
+            if ((t - part) / vo::kLinLanes != (t - part + np - 1) / vo::kLinLanes || (t - part) % np)
+              FAIL("chunk %d slot item %d: parts not aligned in one pass", ch, s);
+            r0 = a;
+            r1 = a + 1;
+          }
           int n = 0;
           for (int e = g.slotp[s] + part; e < g.slotp[s] + g.apcnt[s]; e += np, ++n)
-            for (int r = 0; r < 6; ++r)
-              if (vo::kRowLanes == 1 || r == a) ++cover[6 * (size_t)e + r];
-          max_chain = std::max(max_chain, n);
+            for (int r = r0; r < r1; ++r) ++cover[6 * (size_t)e + r];
+          max_chain = std::max(max_chain, n * (r1 - r0));
         }
       }
       for (size_t k = 0; k < cover.size(); ++k)
