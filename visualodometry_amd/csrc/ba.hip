@@ -878,11 +878,12 @@ __device__ __forceinline__ void obs_lin_w(LinWave& S, const LinArgs& A, const do
   jp[5] = j11 * T[5] + j12 * T[8];
 }
 
-// One lane's share of a Schur item (one-wave K1): rows r0 .. r0 + R - 1 of active slot si's
-// block, -sum over the slot's pairs of Z_x[rows] Z_y^T as FMA chains with both Z rows in
-// registers (pair j+1's rows fetched while pair j accumulates); a diagonal slot's lane adds U's
-// and b's rows over its pairs' observations (pair (x, x): track entry x of the slot's camera).
-// The rows go straight to the slab (or, kWin, into the segment window).
+// One lane's Schur item (one-wave K1): rows r0 .. r0 + R - 1 (R = 6: the whole block) of
+// active slot si, -sum over the slot's pairs of Z_x[rows] Z_y^T as FMA chains with both Z rows
+// in registers (pair j+1's rows fetched while pair j accumulates); a diagonal slot's lane adds
+// U's rows over its pairs' observations (pair (x, x): track entry x of the slot's camera) and,
+// for the first copy of the block, b's rows over abn pairs.  The rows go straight to the slab
+// (or, kWin, into the segment window).
 template <int R, bool kWin>
 __device__ __forceinline__ void schur_rows(const LinWave& S, const LinArgs& A, int si, int r0, bool live,
                                            double* win, double* bwin) {
@@ -949,8 +950,12 @@ __device__ __forceinline__ void schur_rows(const LinWave& S, const LinArgs& A, i
               out[6 * i + c] = __builtin_fma(ja1, jj[6 + c], __builtin_fma(ja0, jj[c], out[6 * i + c]));
           }
         }
+      }
+      // b: the first copy of the diagonal block sums bt over all of its copies' pairs
+      for (int e = e0; e < e0 + (live ? (int)S.img.abn[si] : 0); ++e) {
+        const double* br = &S.zb[kZbStride * (S.img.pairs[e] & 255) + 18 + r0];
 #pragma unroll
-        for (int i = 0; i < R; ++i) ob[i] += S.zb[kZbStride * x + 18 + r0 + i];
+        for (int i = 0; i < R; ++i) ob[i] += br[i];
       }
     }
   }
@@ -966,7 +971,7 @@ __device__ __forceinline__ void schur_rows(const LinWave& S, const LinArgs& A, i
     double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s] + 6 * r0]);
 #pragma unroll
     for (int e = 0; e < 3 * R; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
-    if (dcam != 0xFF)
+    if (dcam != 0xFF && S.img.abn[si] > 0)  // the first copy of the block carries b
 #pragma unroll
       for (int i = 0; i < R; ++i) A.slab_b[6l * S.cpos[dcam] + r0 + i] = ob[i];
   }
@@ -1201,27 +1206,11 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
       __syncthreads();
       st.mark(kPhElim);
 
-      // Schur items: an active slot block split by rows over 6 / R lanes, R rows each
-      // (ChunkImg::abase / anp); every 64-lane pass has one R, so its lanes run one code path
-      // (schur_rows<R>) and no lane sums another's partials.
+      // Schur items: lane j sums active slot j's whole block (ChunkImg::abase / abn; copies
+      // of a heavy slot balance the lanes, each its own slab row)
       {
-        const int nas = h3.z, lanes = S.img.abase[nas];
-        for (int base = 0; base < lanes; base += kLinLanes) {
-          const int t = base + tid;
-          int si = 0;
-#pragma unroll
-          for (int sp = 32; sp > 0; sp >>= 1)
-            if (si + sp < nas && S.img.abase[si + sp] <= t) si += sp;
-          const int R = __builtin_amdgcn_readfirstlane(S.img.anp[si]);  // one per pass
-          const int off = t - S.img.abase[si];
-          const bool live = t < lanes && off < 6 / R;
-          switch (R) {
-            case 6: schur_rows<6, kWin>(S, A, si, 0, live, win, bwin); break;
-            case 3: schur_rows<3, kWin>(S, A, si, 3 * off, live, win, bwin); break;
-            case 2: schur_rows<2, kWin>(S, A, si, 2 * off, live, win, bwin); break;
-            default: schur_rows<1, kWin>(S, A, si, off, live, win, bwin); break;
-          }
-        }
+        const int nas = h3.z;
+        for (int j = tid; j - tid < nas; j += kLinLanes) schur_rows<6, kWin>(S, A, min(j, nas - 1), 0, j < nas, win, bwin);
       }
       st.mark(kPhSchur);
     }  // kAccum

@@ -200,6 +200,7 @@ struct PlanSeg {
   int chunk0;                               // first chunk (global index after the merge)
   std::vector<int32_t> cams, acams;         // free / all cameras (unsorted while growing)
   std::vector<std::pair<int32_t, int32_t>> slots;
+  std::vector<int32_t> slot_cnt;            // pairs per slot (while packing)
   int src = -1;                             // taken over: the previous plan's segment
 };
 
@@ -426,7 +427,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       R.chunk_fobs.push_back(h[13] - h[12]);
     }
     for (int ps = Q.group_seg[src]; ps < Q.group_seg[src + 1]; ++ps) {
-      PlanSeg sg{Q.seg_chunk[ps] - pc0, {}, {}, {}, ps};
+      PlanSeg sg{Q.seg_chunk[ps] - pc0, {}, {}, {}, {}, ps};
       for (int e = Q.seg_cam_off[ps]; e < Q.seg_cam_off[ps + 1]; ++e) sg.cams.push_back(Q.segcam_f[e] - s);
       for (int e = Q.seg_acam_off[ps]; e < Q.seg_acam_off[ps + 1]; ++e) sg.acams.push_back(Q.seg_acam[e] - s);
       for (int e = Q.seg_slot_off[ps]; e < Q.seg_slot_off[ps + 1]; ++e)
@@ -449,6 +450,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     // segment's local number) when the free cameras are few, the linear searches otherwise
     std::vector<int32_t> cam_stamp(tables ? N : 0, -1), fcam_stamp(tables ? std::max(Nf, 1) : 0, -1);
     std::vector<int32_t> pair_stamp(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, -1);
+    std::vector<int32_t> pair_sidx(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, 0);
     std::vector<int32_t> cq;
     int c_obs = 0, c_te = 0, c_pts = 0, c_pairs = 0;
     int64_t s_obs = 0;
@@ -534,10 +536,14 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
           for (int b = 0; b <= a; ++b) {
             const int32_t hi = std::max(cq[a], cq[b]), lo = std::min(cq[a], cq[b]);
             int32_t& st = pair_stamp[(size_t)hi * Nf + lo];
+            int32_t& si = pair_sidx[(size_t)hi * Nf + lo];
             if (st != sid) {
               st = sid;
+              si = (int32_t)s.slots.size();
               s.slots.push_back(std::make_pair(hi, lo));
+              s.slot_cnt.push_back(0);
             }
+            ++s.slot_cnt[si];
           }
       } else {
         for (int c : cq)
@@ -547,7 +553,13 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         for (int a = 0; a < k; ++a)
           for (int b = 0; b <= a; ++b) {
             const auto pr = std::make_pair(std::max(cq[a], cq[b]), std::min(cq[a], cq[b]));
-            if (std::find(s.slots.begin(), s.slots.end(), pr) == s.slots.end()) s.slots.push_back(pr);
+            const auto it = std::find(s.slots.begin(), s.slots.end(), pr);
+            if (it == s.slots.end()) {
+              s.slots.push_back(pr);
+              s.slot_cnt.push_back(1);
+            } else {
+              ++s.slot_cnt[it - s.slots.begin()];
+            }
           }
       }
       c_obs += nob;
@@ -559,6 +571,37 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       R.chunk_fte.back() += k;
       R.chunk_fobs.back() += fobs;
     }
+#ifndef VO_BA_COPY_CHAIN
+#define VO_BA_COPY_CHAIN 21
+#endif
+    constexpr int kCopyChain = VO_BA_COPY_CHAIN;  // weighted chain below which no copy is made
+    // One-wave K1, segments of one chunk: a lane sums one window slot's block, so the slots of
+    // longest pair chains are split into copies of the same block (consecutive pair ranges,
+    // each its own slab row; K2 sums every row of a block) while the lanes last: a copy for
+    // the slot whose per-lane chain (pairs / copies, a diagonal slot's pair weighted 5 against
+    // 3 for its U and b) is longest, until 64 lanes or a chain of kCopyChain (each copy is one
+    // more slab row for K1 to write and K2 to read).
+    if (kLinWave)
+      for (size_t k = 0; k < R.segs.size(); ++k) {
+        PlanSeg& sg = R.segs[k];
+        const int nch = (k + 1 < R.segs.size() ? R.segs[k + 1].chunk0 : (int)R.chunk_q.size()) - sg.chunk0;
+        const int n = (int)sg.slots.size();
+        if (nch != 1 || n == 0) continue;
+        int cp[kSegSlots];
+        for (int i = 0; i < n; ++i) cp[i] = 1;
+        auto chain = [&](int i) {
+          return (sg.slot_cnt[i] + cp[i] - 1) / cp[i] * (sg.slots[i].first == sg.slots[i].second ? 5 : 3);
+        };
+        for (int lanes = n; lanes < std::min(kLinLanes, kSegSlots); ++lanes) {
+          int best = 0;
+          for (int i = 1; i < n; ++i)
+            if (chain(i) > chain(best)) best = i;
+          if (chain(best) <= kCopyChain) break;
+          ++cp[best];
+        }
+        for (int i = 0; i < n; ++i)
+          for (int c = 1; c < cp[i]; ++c) sg.slots.push_back(sg.slots[i]);
+      }
   };
   run_parallel(std::min(nparts, nthr), [&](int t) {
     const int nt = std::min(nparts, nthr);
@@ -759,7 +802,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       if (tables) {
         for (size_t i = 0; i < s.cams.size(); ++i) fcam_idx[s.cams[i]] = (int32_t)i;
         for (size_t i = 0; i < s.acams.size(); ++i) acam_idx[s.acams[i]] = (int32_t)i;
-        for (size_t i = 0; i < s.slots.size(); ++i) pair_slot[(size_t)s.slots[i].first * Nf + s.slots[i].second] = (int32_t)i;
+        for (size_t i = s.slots.size(); i-- > 0;)  // the first of equal slots (copies)
+          pair_slot[(size_t)s.slots[i].first * Nf + s.slots[i].second] = (int32_t)i;
       }
       auto lcam_of = [&](int32_t c) {  // window index of free camera c
         return tables ? fcam_idx[c] : (int32_t)(std::lower_bound(s.cams.begin(), s.cams.end(), c) - s.cams.begin());
@@ -806,6 +850,15 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         int32_t* sp = &P.slot_ptr[P.chunk_slot_base[ch]];
         for (int sl = 0; sl <= ns; ++sl) sp[sl] = pbase + cnt[sl];
         for (int e = 0; e < npair; ++e) P.pair_list[pbase + cnt[pslot[e]]++] = ptmp[e];
+        // copies of a slot (equal (i, j), adjacent after the sort): its pairs, counted to the
+        // first, in consecutive ranges of near-equal length
+        for (int a = 0; a < ns;) {
+          int b = a + 1;
+          while (b < ns && s.slots[b] == s.slots[a]) ++b;
+          const int32_t lo = sp[a], n = sp[b] - sp[a];
+          for (int c = a + 1; c < b; ++c) sp[c] = lo + (int32_t)((int64_t)n * (c - a) / (b - a));
+          a = b;
+        }
         // camera lists: track entries and observations by window camera, in order
         std::fill(cnt, cnt + nc + 1, 0);
         std::fill(cnt2, cnt2 + nc + 1, 0);
@@ -924,50 +977,24 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
               base += kRowLanes << lg[i];
             }
           } else {
-            // One-wave K1: an item is a slot block split by rows over 6 / R lanes, R rows each
-            // (anp = R), and every 64-lane pass has one R (the lanes of a pass run the same
-            // code, no cross-lane sums).  The k items of longest pair chains (a diagonal slot's
-            // pair also carries U and b: weight 5 against 3) go to passes of R in {3, 2, 1},
-            // the rest one lane each (R = 6); k and R minimise the estimate sum over passes of
-            // longest chain x per-pair cost (18 R FMAs + loads) + a fixed cost per pass.
-            int w[kSegSlots];
-            for (int i = 0; i < nas; ++i) {
-              w[i] = cntp[i] * (wt[i] == 4 ? 5 : 3);
-              ord[i] = i;
-            }
-            std::stable_sort(ord, ord + nas, [&](int a, int b) { return w[a] > w[b]; });
-            auto cost = [](int R) { return 18 * R + 12; };
-            constexpr int kPassCost = 600;  // per pass (in the same units: chain x pair cost / 3)
-            auto light = [&](int k) {  // items k.. one lane each
-              long t = 0;
-              for (int j = k; j < nas; j += kLinLanes) t += (long)w[ord[j]] * cost(6) / 3 + kPassCost;
-              return t;
-            };
-            int bk = 0, bR = 6;
-            long best = light(0);
-            for (int R : {3, 2, 1}) {
-              const int m = kLinLanes / (6 / R);  // items per pass
-              for (int k = 1; k <= std::min(nas, 24); ++k) {
-                long t = light(k);
-                for (int j = 0; j < k; j += m) t += (long)w[ord[j]] * cost(R) / 3 + kPassCost;
-                if (t < best) {
-                  best = t;
-                  bk = k;
-                  bR = R;
-                }
-              }
-            }
+            // One-wave K1: lane j sums active slot j's whole block (copies of a heavy slot are
+            // slots of their own, see pack); the first slot of a diagonal block's copies also
+            // sums the camera's b over all of their pairs
             for (int j = 0; j < nas; ++j) {
-              const int i = ord[j], R = j < bk ? bR : 6, nl = 6 / R;
-              if ((j == bk && base % kLinLanes) || base / kLinLanes != (base + nl - 1) / kLinLanes)
-                base = (base + kLinLanes - 1) / kLinLanes * kLinLanes;  // a new pass: R changes, or the item would straddle
-              g.aslot[j] = (uint8_t)sl[i];
-              g.slotp[j] = P.slot_ptr[sb + sl[i]] - e0;
-              g.apcnt[j] = (uint16_t)cntp[i];
-              g.anp[j] = (uint8_t)R;
-              g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
+              const int i = sl[j];
+              const bool diag = P.slot_i[so + i] == P.slot_j[so + i];
+              const bool first = i == 0 || P.slot_i[so + i - 1] != P.slot_i[so + i] ||
+                                 P.slot_j[so + i - 1] != P.slot_j[so + i];
+              int run = i + 1;
+              while (run < ns && P.slot_i[so + run] == P.slot_i[so + i] && P.slot_j[so + run] == P.slot_j[so + i]) ++run;
+              g.aslot[j] = (uint8_t)i;
+              g.slotp[j] = P.slot_ptr[sb + i] - e0;
+              g.apcnt[j] = (uint16_t)cntp[j];
+              g.anp[j] = 0;
+              g.adcam[j] = diag ? (uint8_t)lcam_of(P.slot_i[so + i]) : 0xFF;
+              g.abn[j] = diag && first ? (uint16_t)(P.slot_ptr[sb + run] - P.slot_ptr[sb + i]) : 0;
               g.abase[j] = (uint16_t)base;
-              base += nl;
+              base += 1;
             }
           }
           g.abase[nas] = (uint16_t)base;

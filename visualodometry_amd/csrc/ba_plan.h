@@ -101,13 +101,15 @@ struct alignas(16) ChunkImg {
   // Schur-pair lanes, balanced.  Four-wave K1: active slot i (ordered by lanes per item
   // descending) sums its apcnt[i] pairs from slotp[i] on 6 << anp[i] lanes starting at abase[i]
   // (2^anp lanes per row, their strided partial sums combined by an aligned butterfly).
-  // One-wave K1: slot i's block is split by rows over 6 / anp[i] lanes from abase[i], anp[i] rows
-  // each, every pair on every lane; each 64-lane pass has one anp (lanes past an item's end
-  // idle).  abase[nas] = lanes used
+  // One-wave K1: lane i sums active slot i's whole block over its apcnt[i] pairs (abase[i] = i;
+  // a heavy slot's pairs are split over copies of the slot, each with its own slab row); a
+  // diagonal slot's lanes add U over their pairs' observations, and the first copy sums the
+  // camera's b over the abn[i] pairs from slotp[i] (0 otherwise).  abase[nas] = lanes used
   uint16_t apcnt[kSegSlots];
   uint16_t abase[kSegSlots + 1];  // up to 6 x 64 lanes (two passes of the workgroup)
   uint8_t anp[kSegSlots];
   uint8_t adcam[kSegSlots];        // active slot i -> window camera if diagonal, else 0xFF
+  uint16_t abn[kSegSlots];         // one-wave K1: pairs whose bt the slot's lane sums into b
   alignas(2) uint16_t pairs[kChunkPairs];  // (te_x | te_y << 8) by slot
   uint8_t caml[kChunkTe];          // track entries by window camera
   uint8_t camol[kChunkObs];        // observations by window camera

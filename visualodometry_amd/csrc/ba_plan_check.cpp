@@ -10,6 +10,7 @@
 // Input (binary): int32 n_poses, n_points, n_obs, n_fixed, seg_obs; point_ptr; obs_cam; obs_uv.
 // Prints "ok <chunks> <segments> <passes> <max chain (pair rows)>" or the first violation.
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <new>
 #include <string>
@@ -60,7 +61,6 @@ int main(int argc, char** argv) {
       const int nas = h[14], lanes = g.abase[nas], npairs = h[9] - h[8];
       std::vector<int> cover(6 * (size_t)npairs, 0);
       for (int base = 0; base < lanes; base += vo::kLinLanes, ++passes) {
-        int pass_r = -1;
         for (int tid = 0; tid < vo::kLinLanes; ++tid) {
           const int t = base + tid;
           if (t >= lanes) continue;
@@ -69,16 +69,10 @@ int main(int argc, char** argv) {
             if (s + sp < nas && g.abase[s + sp] <= t) s += sp;
           const int off = t - g.abase[s];
           int r0, r1, part, np;
-          if (vo::kLinWave) {  // rows [off R, off R + R) of the block, every pair
-            const int R = g.anp[s];
-            if (R != 1 && R != 2 && R != 3 && R != 6) FAIL("chunk %d item %d: %d rows per lane", ch, s, R);
-            if (off >= 6 / R) continue;  // idle lane past the item
-            if (pass_r >= 0 && pass_r != R) FAIL("chunk %d pass %d: rows per lane %d and %d", ch, base / 64, pass_r, R);
-            pass_r = R;
-            if (g.abase[s] / vo::kLinLanes != (g.abase[s] + 6 / R - 1) / vo::kLinLanes)
-              FAIL("chunk %d item %d straddles a pass", ch, s);
-            r0 = off * R;
-            r1 = r0 + R;
+          if (vo::kLinWave) {  // lane = item: the whole block over the item's pairs
+            if (off != 0) FAIL("chunk %d: lane %d is not item %d", ch, t, s);
+            r0 = 0;
+            r1 = 6;
             part = 0;
             np = 1;
           } else {  // lane = (row a, part)
@@ -102,6 +96,8 @@ int main(int argc, char** argv) {
         if (cover[k] != 1) FAIL("chunk %d: pair %zu row %zu summed %d times", ch, k / 6, k % 6, cover[k]);
       if (g.slotp[nas] != npairs) FAIL("chunk %d: active slots end at %d of %d pairs", ch, (int)g.slotp[nas], npairs);
       const int te0 = h[2];
+      std::vector<std::vector<int>> upairs(ncams), bpairs(ncams);
+      std::vector<int> bsum(ncams, 0);
       for (int s = 0; s < nas; ++s) {
         const int ws = g.aslot[s];
         slot_seen[ws] = 1;
@@ -115,15 +111,29 @@ int main(int argc, char** argv) {
         cam_diag[wc] = 1;
         // its pairs: (x, x) over the chunk's track entries of that camera, each once
         std::vector<int> tes;
+        if (vo::kLinWave) {  // b: exactly one copy of the block sums it, over every copy's pairs
+          if (g.abn[s] > 0) {
+            if (++bsum[wc] != 1) FAIL("chunk %d: camera %d's b summed twice", ch, wc);
+            for (int e = g.slotp[s]; e < g.slotp[s] + g.abn[s]; ++e) bpairs[wc].push_back(g.pairs[e] & 255);
+          }
+        }
         for (int e = g.slotp[s]; e < g.slotp[s] + g.apcnt[s]; ++e) {
           const int x = g.pairs[e] & 255, y = g.pairs[e] >> 8;
           if (x != y) FAIL("chunk %d: diagonal slot pair (%d, %d)", ch, x, y);
           tes.push_back(x);
         }
+        upairs[wc].insert(upairs[wc].end(), tes.begin(), tes.end());
+      }
+      for (int wc = 0; wc < ncams; ++wc) {
         std::vector<int> want;
         for (int t = te0; t < te0 + h[3]; ++t)
           if (P.te_lcam[t] == wc) want.push_back(t - te0);
-        if (tes != want) FAIL("chunk %d: camera %d track entries differ", ch, wc);
+        std::sort(upairs[wc].begin(), upairs[wc].end());
+        if (!upairs[wc].empty() && upairs[wc] != want) FAIL("chunk %d: camera %d track entries (U) differ", ch, wc);
+        if (vo::kLinWave && !upairs[wc].empty()) {
+          std::sort(bpairs[wc].begin(), bpairs[wc].end());
+          if (bpairs[wc] != want) FAIL("chunk %d: camera %d track entries (b) differ", ch, wc);
+        }
       }
     }
     if (one) {
