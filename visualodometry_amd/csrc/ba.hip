@@ -964,7 +964,7 @@ __device__ __forceinline__ void schur_rows(const LinWave& S, const LinArgs& A, i
     double* w = &win[36 * s + 6 * r0];
 #pragma unroll
     for (int e = 0; e < 6 * R; ++e) w[e] += out[e];
-    if (dcam != 0xFF)
+    if (dcam != 0xFF && S.img.abn[si] > 0)  // only the first copy: the copies' lanes would race
 #pragma unroll
       for (int i = 0; i < R; ++i) bwin[6 * dcam + r0 + i] += ob[i];
   } else {
