@@ -772,7 +772,10 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
 // diagonal slots' lanes over their pairs' observations (a diagonal slot's pairs are exactly
 // its camera's track entries), so every window item is finished in registers and written to
 // its slab row once.
-constexpr int kZbStride = 24;                  // doubles per track entry: Z (18) | bt (6)
+// Z rows of 18 doubles (36 dwords: the rows start on 16 different 4-bank offsets of gfx950's
+// 64 banks, so a ds_read_b128 of 16 lanes on random rows rarely conflicts; a 24-double row of
+// Z | bt started on 4 offsets only, a 4-way conflict on every Schur load)
+constexpr int kZbStride = 18;                  // doubles per track entry's Z row
 constexpr int kZbR = 6 * kChunkObs;            // r (2 per observation) after Jp (6 per observation)
 constexpr int kZbDc = kZbR + 2 * kChunkObs;    // back substitution: dc of the window cameras
 constexpr int kZbPoseO = kZbDc + 6 * kSegCams; // back substitution: poses of the pending step
@@ -782,8 +785,9 @@ struct alignas(16) LinWave {
   ChunkImg img;
   int spos[kSegSlots];
   int cpos[kSegCams];
-  alignas(16) double Jc[kChunkObs][12];
+  alignas(16) double Jc[kChunkObs][10];  // compressed camera Jacobian rows (jc_load)
   alignas(16) double zb[kChunkTe * kZbStride];
+  alignas(16) double bt[kChunkTe][6];
   double X[kChunkPts][3];
   double L[kChunkPts][6];  // 1/l00, l10, 1/l11, l20, l21, 1/l22
   double h[kChunkPts][3];
@@ -854,20 +858,13 @@ __device__ __forceinline__ void obs_lin_w(LinWave& S, const LinArgs& A, const do
   if (!kBack) cost += r0 * r0 + r1 * r1;
   S.zb[kZbR + 2 * o] = r0;
   S.zb[kZbR + 2 * o + 1] = r1;
-  if (kJc) {
-    double* jc = S.Jc[o];
-    jc[0] = j00;
-    jc[1] = 0.0;
-    jc[2] = j02;
-    jc[3] = j02 * y;
-    jc[4] = j00 * z - j02 * x;
-    jc[5] = -j00 * y;
-    jc[6] = 0.0;
-    jc[7] = j11;
-    jc[8] = j12;
-    jc[9] = j12 * y - j11 * z;
-    jc[10] = -j12 * x;
-    jc[11] = j11 * x;
+  if (kJc) {  // compressed rows (jc_load): row 0 without column 1, row 1 without column 0
+    double2* jc = reinterpret_cast<double2*>(S.Jc[o]);
+    jc[0] = make_double2(j00, j02);
+    jc[1] = make_double2(j02 * y, j00 * z - j02 * x);
+    jc[2] = make_double2(-j00 * y, j11);
+    jc[3] = make_double2(j12, j12 * y - j11 * z);
+    jc[4] = make_double2(-j12 * x, j11 * x);
   }
   double* jp = &S.zb[6 * o];
   jp[0] = j00 * T[0] + j02 * T[6];
@@ -878,35 +875,46 @@ __device__ __forceinline__ void obs_lin_w(LinWave& S, const LinArgs& A, const do
   jp[5] = j11 * T[5] + j12 * T[8];
 }
 
-// One lane's Schur item (one-wave K1): rows r0 .. r0 + R - 1 (R = 6: the whole block) of
-// active slot si, -sum over the slot's pairs of Z_x[rows] Z_y^T as FMA chains with both Z rows
-// in registers (pair j+1's rows fetched while pair j accumulates); a diagonal slot's lane adds
-// U's rows over its pairs' observations (pair (x, x): track entry x of the slot's camera) and,
-// for the first copy of the block, b's rows over abn pairs.  The rows go straight to the slab
-// (or, kWin, into the segment window).
-template <int R, bool kWin>
-__device__ __forceinline__ void schur_rows(const LinWave& S, const LinArgs& A, int si, int r0, bool live,
-                                           double* win, double* bwin) {
-  double out[6 * R], ob[R];
+// Observation o's camera Jacobian rows from the compressed LDS row (10 doubles: row 0 without
+// its structural zero at column 1, row 1 without column 0; 80-byte rows start on 16 bank
+// offsets)
+__device__ __forceinline__ void jc_load(const LinWave& S, int o, double (&jj)[12]) {
+  const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
+  const double2 a = jr[0], b = jr[1], c = jr[2], d = jr[3], e = jr[4];
+  jj[0] = a.x; jj[1] = 0.0; jj[2] = a.y; jj[3] = b.x; jj[4] = b.y; jj[5] = c.x;
+  jj[6] = 0.0; jj[7] = c.y; jj[8] = d.x; jj[9] = d.y; jj[10] = e.x; jj[11] = e.y;
+}
+
+// One lane's Schur item (one-wave K1): active slot si's block, -sum over the slot's pairs of
+// Z_x Z_y^T as FMA chains with both Z rows in registers (pair j+1's rows fetched while pair j
+// accumulates); a diagonal slot's lane adds U over its pairs' observations (pair (x, x): track
+// entry x of the slot's camera) and, for the first copy of the block, b over abn pairs.  The
+// block goes straight to the slab (or, kWin, into the segment window).
+template <bool kWin>
+__device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, int si, bool live, double* win,
+                                            double* bwin) {
+  double out[36], ob[6];
 #pragma unroll
-  for (int e = 0; e < 6 * R; ++e) out[e] = 0.0;
+  for (int e = 0; e < 36; ++e) out[e] = 0.0;
 #pragma unroll
-  for (int e = 0; e < R; ++e) ob[e] = 0.0;
+  for (int e = 0; e < 6; ++e) ob[e] = 0.0;
   const int e0 = S.img.slotp[si], n = live ? S.img.apcnt[si] : 0;
-  const int dcam = S.img.adcam[si], s = S.img.aslot[si];
+  const int dcam = S.img.adcam[si], s = S.img.aslot[si], nb = live ? S.img.abn[si] : 0;
   if (n > 0) {
-    auto zload = [&](int pr, double (&zx)[3 * R], double2 (&zy)[9]) {
-      const double* px = &S.zb[kZbStride * (pr & 255) + 3 * r0];
+    auto zload = [&](int pr, double2 (&zx)[9], double2 (&zy)[9]) {
+      const double2* px = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr & 255)]);
       const double2* py = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr >> 8)]);
 #pragma unroll
-      for (int k = 0; k < 3 * R; ++k) zx[k] = px[k];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) zy[k] = py[k];
+      for (int k = 0; k < 9; ++k) {
+        zx[k] = px[k];
+        zy[k] = py[k];
+      }
     };
-    auto accum = [&](const double (&x)[3 * R], const double2 (&zy)[9]) {
+    auto accum = [&](const double2 (&zx)[9], const double2 (&zy)[9]) {
+      const double* x = reinterpret_cast<const double*>(zx);
       const double* y = reinterpret_cast<const double*>(zy);
 #pragma unroll
-      for (int i = 0; i < R; ++i)
+      for (int i = 0; i < 6; ++i)
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
           double v = out[6 * i + j];
@@ -916,8 +924,7 @@ __device__ __forceinline__ void schur_rows(const LinWave& S, const LinArgs& A, i
         }
     };
     auto pid = [&](int j) { return (int)S.img.pairs[e0 + min(j, n - 1)]; };
-    double zxA[3 * R], zxB[3 * R];
-    double2 zyA[9], zyB[9];
+    double2 zxA[9], zyA[9], zxB[9], zyB[9];
     zload(pid(0), zxA, zyA);
     int pn = pid(1);
     int j = 0;
@@ -934,46 +941,44 @@ __device__ __forceinline__ void schur_rows(const LinWave& S, const LinArgs& A, i
       for (int e = e0; e < e0 + n; ++e) {
         const int x = S.img.pairs[e] & 255;
         for (int o = S.img.te_obs[x]; o < S.img.te_obs[x + 1]; ++o) {
-          const double2* jr = reinterpret_cast<const double2*>(S.Jc[o]);
           double jj[12];
+          jc_load(S, o, jj);
 #pragma unroll
-          for (int k = 0; k < 6; ++k) {
-            const double2 v = jr[k];
-            jj[2 * k] = v.x;
-            jj[2 * k + 1] = v.y;
-          }
-#pragma unroll
-          for (int i = 0; i < R; ++i) {
-            const double ja0 = S.Jc[o][r0 + i], ja1 = S.Jc[o][6 + r0 + i];
+          for (int i = 0; i < 6; ++i)
 #pragma unroll
             for (int c = 0; c < 6; ++c)
-              out[6 * i + c] = __builtin_fma(ja1, jj[6 + c], __builtin_fma(ja0, jj[c], out[6 * i + c]));
-          }
+              out[6 * i + c] = __builtin_fma(jj[6 + i], jj[6 + c], __builtin_fma(jj[i], jj[c], out[6 * i + c]));
         }
       }
       // b: the first copy of the diagonal block sums bt over all of its copies' pairs
-      for (int e = e0; e < e0 + (live ? (int)S.img.abn[si] : 0); ++e) {
-        const double* br = &S.zb[kZbStride * (S.img.pairs[e] & 255) + 18 + r0];
+      for (int e = e0; e < e0 + nb; ++e) {
+        const double2* br = reinterpret_cast<const double2*>(S.bt[S.img.pairs[e] & 255]);
 #pragma unroll
-        for (int i = 0; i < R; ++i) ob[i] += br[i];
+        for (int k = 0; k < 3; ++k) {
+          const double2 v = br[k];
+          ob[2 * k] += v.x;
+          ob[2 * k + 1] += v.y;
+        }
       }
     }
   }
   if (!live) return;
-  if (kWin) {  // one owner lane per (slot, rows) and chunk: chunk order per entry
-    double* w = &win[36 * s + 6 * r0];
+  if (kWin) {  // one owner lane per slot and chunk: chunk order per entry
+    double* w = &win[36 * s];
 #pragma unroll
-    for (int e = 0; e < 6 * R; ++e) w[e] += out[e];
-    if (dcam != 0xFF && S.img.abn[si] > 0)  // only the first copy: the copies' lanes would race
+    for (int e = 0; e < 36; ++e) w[e] += out[e];
+    if (dcam != 0xFF && nb > 0)  // only the first copy: the copies' lanes would race
 #pragma unroll
-      for (int i = 0; i < R; ++i) bwin[6 * dcam + r0 + i] += ob[i];
+      for (int i = 0; i < 6; ++i) bwin[6 * dcam + i] += ob[i];
   } else {
-    double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s] + 6 * r0]);
+    double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s]]);
 #pragma unroll
-    for (int e = 0; e < 3 * R; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
-    if (dcam != 0xFF && S.img.abn[si] > 0)  // the first copy of the block carries b
+    for (int e = 0; e < 18; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
+    if (dcam != 0xFF && nb > 0) {  // the first copy of the block carries b
+      double2* wb = reinterpret_cast<double2*>(&A.slab_b[6l * S.cpos[dcam]]);
 #pragma unroll
-      for (int i = 0; i < R; ++i) A.slab_b[6l * S.cpos[dcam] + r0 + i] = ob[i];
+      for (int k = 0; k < 3; ++k) wb[k] = make_double2(ob[2 * k], ob[2 * k + 1]);
+    }
   }
 }
 
@@ -1160,13 +1165,15 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
         const bool live = tid < nte;
         const int oa = S.img.te_obs[t], ob = live ? S.img.te_obs[t + 1] : oa;
         for (int o = oa; o < ob; ++o) {
+          double jj[12];
+          jc_load(S, o, jj);
 #pragma unroll
           for (int k = 0; k < 2; ++k) {
             const double rk = S.zb[kZbR + 2 * o + k];
             const double q0 = S.zb[6 * o + 3 * k], q1 = S.zb[6 * o + 3 * k + 1], q2 = S.zb[6 * o + 3 * k + 2];
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
-              const double jc = S.Jc[o][6 * k + a];
+              const double jc = jj[6 * k + a];
               W[3 * a] += jc * q0;
               W[3 * a + 1] += jc * q1;
               W[3 * a + 2] += jc * q2;
@@ -1193,14 +1200,15 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
         if (live && !use)  // frozen landmark: its observations leave U too
           for (int o = oa; o < ob; ++o)
 #pragma unroll
-            for (int e = 0; e < 12; ++e) S.Jc[o][e] = 0.0;
+            for (int e = 0; e < 10; ++e) S.Jc[o][e] = 0.0;
         __syncthreads();  // every lane has read its Jp | r
         if (live) {
           double2* zr = reinterpret_cast<double2*>(&S.zb[kZbStride * t]);
 #pragma unroll
           for (int e = 0; e < 9; ++e) zr[e] = make_double2(W[2 * e], W[2 * e + 1]);
+          double2* br = reinterpret_cast<double2*>(S.bt[t]);
 #pragma unroll
-          for (int e = 0; e < 3; ++e) zr[9 + e] = make_double2(bt[2 * e], bt[2 * e + 1]);
+          for (int e = 0; e < 3; ++e) br[e] = make_double2(bt[2 * e], bt[2 * e + 1]);
         }
       }
       __syncthreads();
@@ -1210,7 +1218,7 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
       // of a heavy slot balance the lanes, each its own slab row)
       {
         const int nas = h3.z;
-        for (int j = tid; j - tid < nas; j += kLinLanes) schur_rows<6, kWin>(S, A, min(j, nas - 1), 0, j < nas, win, bwin);
+        for (int j = tid; j - tid < nas; j += kLinLanes) schur_block<kWin>(S, A, min(j, nas - 1), j < nas, win, bwin);
       }
       st.mark(kPhSchur);
     }  // kAccum
