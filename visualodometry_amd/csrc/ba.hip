@@ -888,18 +888,16 @@ __device__ __forceinline__ void jc_load(const LinWave& S, int o, double (&jj)[12
 // One lane's Schur item (one-wave K1): active slot si's block, -sum over the slot's pairs of
 // Z_x Z_y^T as FMA chains with both Z rows in registers (pair j+1's rows fetched while pair j
 // accumulates); a diagonal slot's lane adds U over its pairs' observations (pair (x, x): track
-// entry x of the slot's camera) and, for the first copy of the block, b over abn pairs.  The
-// block goes straight to the slab (or, kWin, into the segment window).
+// entry x of the slot's camera).  The block goes straight to the slab (or, kWin, into the
+// segment window).
 template <bool kWin>
 __device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, int si, bool live, double* win,
                                             double* bwin) {
-  double out[36], ob[6];
+  double out[36];
 #pragma unroll
   for (int e = 0; e < 36; ++e) out[e] = 0.0;
-#pragma unroll
-  for (int e = 0; e < 6; ++e) ob[e] = 0.0;
   const int e0 = S.img.slotp[si], n = live ? S.img.apcnt[si] : 0;
-  const int dcam = S.img.adcam[si], s = S.img.aslot[si], nb = live ? S.img.abn[si] : 0;
+  const int dcam = S.img.adcam[si], s = S.img.aslot[si];
   if (n > 0) {
     auto zload = [&](int pr, double2 (&zx)[9], double2 (&zy)[9]) {
       const double2* px = reinterpret_cast<const double2*>(&S.zb[kZbStride * (pr & 255)]);
@@ -950,16 +948,6 @@ __device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, 
               out[6 * i + c] = __builtin_fma(jj[6 + i], jj[6 + c], __builtin_fma(jj[i], jj[c], out[6 * i + c]));
         }
       }
-      // b: the first copy of the diagonal block sums bt over all of its copies' pairs
-      for (int e = e0; e < e0 + nb; ++e) {
-        const double2* br = reinterpret_cast<const double2*>(S.bt[S.img.pairs[e] & 255]);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const double2 v = br[k];
-          ob[2 * k] += v.x;
-          ob[2 * k + 1] += v.y;
-        }
-      }
     }
   }
   if (!live) return;
@@ -967,18 +955,32 @@ __device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, 
     double* w = &win[36 * s];
 #pragma unroll
     for (int e = 0; e < 36; ++e) w[e] += out[e];
-    if (dcam != 0xFF && nb > 0)  // only the first copy: the copies' lanes would race
-#pragma unroll
-      for (int i = 0; i < 6; ++i) bwin[6 * dcam + i] += ob[i];
   } else {
     double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s]]);
 #pragma unroll
     for (int e = 0; e < 18; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
-    if (dcam != 0xFF && nb > 0) {  // the first copy of the block carries b
-      double2* wb = reinterpret_cast<double2*>(&A.slab_b[6l * S.cpos[dcam]]);
+  }
+}
+
+// The rhs of the chunk's window cameras (one-wave K1): lane (active camera ci, row a) sums bt's
+// row a over the camera's track entries (ChunkImg::camp / caml), eight loads in flight, into
+// its slab entry (or, kWin, the window's).
+template <bool kWin>
+__device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int nac, int tid, double* bwin) {
+  for (int q = tid; q < 6 * nac; q += kLinLanes) {
+    const int ci = q / 6, a = q - 6 * ci;
+    const int c0 = S.img.camp[ci], c1 = S.img.camp[ci + 1];
+    double acc = 0.0;
+    for (int e = c0; e < c1; e += 8) {
+      double v[8];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) wb[k] = make_double2(ob[2 * k], ob[2 * k + 1]);
+      for (int k = 0; k < 8; ++k) v[k] = S.bt[S.img.caml[min(e + k, c1 - 1)]][a];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += e + k < c1 ? v[k] : 0.0;
     }
+    const int c = S.img.acid[ci];
+    if (kWin) bwin[6 * c + a] += acc;
+    else A.slab_b[6l * S.cpos[c] + a] = acc;
   }
 }
 
@@ -1219,6 +1221,7 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
       {
         const int nas = h3.z;
         for (int j = tid; j - tid < nas; j += kLinLanes) schur_block<kWin>(S, A, min(j, nas - 1), j < nas, win, bwin);
+        rhs_rows<kWin>(S, A, h3.w, tid, bwin);
       }
       st.mark(kPhSchur);
     }  // kAccum
