@@ -180,7 +180,6 @@ struct LinArgs {
   const double* dc;        // pending pose update (6 per free camera)
   const int* status;
   unsigned long long* stamps;  // diagnostic build only: per segment phase cycles
-  int wslots, wcams;           // one-wave K1 over multi-chunk segments: window capacity (dynamic LDS)
 };
 
 struct alignas(16) LinShared {
@@ -623,7 +622,7 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
       // the chunk's active slots on balanced lanes (ChunkImg::abase / anp): lane tid -> entry
       // si (binary search over the lane bases), row a, part of 2^lgp
       // (a chunk with more than 42 active slots takes a second pass of one lane per row item)
-      static_assert(kLinWave || kLinLanes == kLinThreads, "planner lane budget = K1 workgroup");
+      static_assert(kLinLanes == kLinThreads, "planner lane budget = K1 workgroup");
       const int nas = h3.z, lanes = S.img.abase[nas];
       for (int base = 0; base < lanes; base += kLinThreads) {
       const int t = base + tid;
@@ -762,7 +761,7 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
   st.flush(A.stamps);
 }
 
-// ---- K1, one wave per chunk (kLinWave) -----------------------------------------------
+// ---- K1, one wave per chunk (plans of one chunk per segment) --------------------------
 // A segment is one chunk and one 64-lane workgroup: every phase of the chunk runs on one
 // wave (a workgroup barrier is then only the LDS wait), and six such workgroups share a CU,
 // so all of cfg3's chunks run at once instead of three four-wave workgroups per CU walking
@@ -798,7 +797,6 @@ struct alignas(16) LinWave {
 constexpr int kWaveSegsPerCu = 6;
 static_assert(sizeof(LinWave) <= 160 * 1024 / kWaveSegsPerCu, "one-wave K1 LDS image");
 constexpr int kWaveObsPerCu = kWaveSegsPerCu * 58;  // observations one round takes (chunks of ~58+)
-constexpr int kWaveWinSegsPerCu = 4;  // multi-chunk segments: static image + a 36-slot window
 
 // point_block over the Zb region's Jp | r (same operation order)
 __device__ __forceinline__ bool point_block_w(const LinWave& S, double lambda, int p, double (&l)[6],
@@ -888,11 +886,8 @@ __device__ __forceinline__ void jc_load(const LinWave& S, int o, double (&jj)[12
 // One lane's Schur item (one-wave K1): active slot si's block, -sum over the slot's pairs of
 // Z_x Z_y^T as FMA chains with both Z rows in registers (pair j+1's rows fetched while pair j
 // accumulates); a diagonal slot's lane adds U over its pairs' observations (pair (x, x): track
-// entry x of the slot's camera).  The block goes straight to the slab (or, kWin, into the
-// segment window).
-template <bool kWin>
-__device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, int si, bool live, double* win,
-                                            double* bwin) {
+// entry x of the slot's camera).  The block goes straight to its slab row.
+__device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, int si, bool live) {
   double out[36];
 #pragma unroll
   for (int e = 0; e < 36; ++e) out[e] = 0.0;
@@ -951,11 +946,7 @@ __device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, 
     }
   }
   if (!live) return;
-  if (kWin) {  // one owner lane per slot and chunk: chunk order per entry
-    double* w = &win[36 * s];
-#pragma unroll
-    for (int e = 0; e < 36; ++e) w[e] += out[e];
-  } else {
+  {
     double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s]]);
 #pragma unroll
     for (int e = 0; e < 18; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
@@ -964,10 +955,9 @@ __device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, 
 
 // The rhs of the chunk's window cameras (one-wave K1): lane (active camera ci, row a) sums bt's
 // row a over the camera's track entries (ChunkImg::camp / caml), eight loads in flight, into
-// its slab entry (or, kWin, the window's).
-template <bool kWin>
-__device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int nac, int tid, double* bwin) {
-  for (int q = tid; q < 6 * nac; q += kLinLanes) {
+// its slab entry.
+__device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int nac, int tid) {
+  for (int q = tid; q < 6 * nac; q += kLinLanesWave) {
     const int ci = q / 6, a = q - 6 * ci;
     const int c0 = S.img.camp[ci], c1 = S.img.camp[ci + 1];
     double acc = 0.0;
@@ -979,75 +969,45 @@ __device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int
       for (int k = 0; k < 8; ++k) acc += e + k < c1 ? v[k] : 0.0;
     }
     const int c = S.img.acid[ci];
-    if (kWin) bwin[6 * c + a] += acc;
-    else A.slab_b[6l * S.cpos[c] + a] = acc;
+    A.slab_b[6l * S.cpos[c] + a] = acc;
   }
 }
 
-// kWin: a segment of several chunks walked by its wave (windows too large for one chunk per
-// workgroup), its window accumulated in dynamic LDS [win (wslots x 36) | bwin (wcams x 6) |
-// dc (kSegCams x 6) | pose_o (kSegAllCams x 12)] and written once at the end; otherwise the
-// segment is one chunk and each item goes straight to its slab row.
-template <int MODE, bool kWin, bool kStamp>
-__global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
+// The one-wave K1: segment = chunk = workgroup of one wave (the plan's seg_obs == 1).
+template <int MODE, bool kStamp>
+__global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
   __shared__ LinWave S;
-  extern __shared__ double Wdyn[];
-  static_assert(kLinLanes == 64, "one wave");
+  static_assert(kLinLanesWave == 64, "one wave");
   Stamper<kStamp> st;
   st.start();
   const int seg = blockIdx.x, tid = threadIdx.x;
   // level 1: status, segment header (uniform), this lane's camera ids (fixed header offsets)
-  // and the first chunk's image (one chunk per segment: chunk = segment)
+  // and the chunk's image (chunk = segment)
   const int* SH = A.seg_hdr + (long)kSegHdr * seg;
   const int4* SH4 = reinterpret_cast<const int4*>(SH);
   const int16_t* SH16 = reinterpret_cast<const int16_t*>(SH);
   const int stat = A.status ? *A.status : 0;
   const int4 g0 = SH4[0], g1 = SH4[1];
-  int4 h0 = SH4[8], h1 = SH4[9], h2 = SH4[10], h3 = SH4[11];
+  const int4 h0 = SH4[8], h1 = SH4[9], h2 = SH4[10], h3 = SH4[11];
   constexpr int kImgVec = (int)(sizeof(ChunkImg) / 16);
   static_assert(kImgVec > 128 && kImgVec <= 192, "three 16-byte staging granules per lane");
-  struct Img3 {
-    uint4 a, b, c;
-  };
-  auto load_img = [&](int c) {
-    const uint4* img = reinterpret_cast<const uint4*>(A.chunk_img + c);
-    return Img3{img[tid], img[64 + tid], img[min(128 + tid, kImgVec - 1)]};
-  };
-  auto store_img = [&](const Img3& v) {
-    uint4* d = reinterpret_cast<uint4*>(&S.img);
-    d[tid] = v.a;
-    d[64 + tid] = v.b;
-    if (128 + tid < kImgVec) d[128 + tid] = v.c;
-  };
-  auto load_x = [&](const int4& hp, double (&v)[2]) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) v[k] = A.points[3l * hp.x + min(tid + 64 * k, max(3 * hp.y - 1, 0))];
-  };
-  const int ch0 = kWin ? g1.y : seg, ch1 = kWin ? g1.z : seg + 1;
-  Img3 vimg = load_img(ch0);
+  const uint4* img = reinterpret_cast<const uint4*>(A.chunk_img + seg);
+  const uint4 img0 = img[tid], img1 = img[64 + tid], img2 = img[min(128 + tid, kImgVec - 1)];
   int i_acam[3], i_wcam[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     i_acam[k] = SH16[16 + min((tid + 64 * k) / 12, kSegAllCams - 1)];
     i_wcam[k] = SH16[32 + min((tid + 64 * k) / 6, kSegCams - 1)];
   }
-  int4 n0 = h0, n1 = h1, n2 = h2, n3 = h3;  // the next chunk's header (kWin)
-  if (kWin) {
-    const int chn = min(ch0 + 1, ch1 - 1);
-    n0 = A.chunk_hdr[4l * chn];
-    n1 = A.chunk_hdr[4l * chn + 1];
-    n2 = A.chunk_hdr[4l * chn + 2];
-    n3 = A.chunk_hdr[4l * chn + 3];
-  }
   if (stat) return;  // a previous solve failed: state frozen
   const int nslots = g0.x, slot_off = g0.y, cam0 = g0.z, ncams = g0.w, na = g1.x;
-  double* win = Wdyn;
-  double* bwin = Wdyn + 36 * A.wslots;
-  double* dcw = kWin ? bwin + 6 * A.wcams : &S.zb[kZbDc];
-  double* pose_o = kWin ? dcw + 6 * kSegCams : &S.zb[kZbPoseO];
+  const int nob = h0.y, nte = h0.w, p0 = h1.x, npt = h1.y;
+  double* dcw = &S.zb[kZbDc];
+  double* pose_o = &S.zb[kZbPoseO];
   // level 2: landmarks, poses, pending update, slab rows
   double vx[2], vpn[3], vpo[3], vdc[3];
-  load_x(h1, vx);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) vx[k] = A.points[3l * p0 + min(tid + 64 * k, max(3 * npt - 1, 0))];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int e = tid + 64 * k;
@@ -1062,6 +1022,15 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
     vsp = A.slab_pos[slot_off + min(tid, nslots - 1)];
     vcp = A.cam_pos[cam0 + min(tid, max(ncams - 1, 0))];
   }
+  {
+    uint4* d = reinterpret_cast<uint4*>(&S.img);
+    d[tid] = img0;
+    d[64 + tid] = img1;
+    if (128 + tid < kImgVec) d[128 + tid] = img2;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    if (tid + 64 * k < 3 * npt) (&S.X[0][0])[tid + 64 * k] = vx[k];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int e = tid + 64 * k;
@@ -1074,170 +1043,132 @@ __global__ __launch_bounds__(kLinLanes) void ba_lin_wave_kernel(LinArgs A) {
   if (MODE & kAccum) {
     if (tid < nslots) S.spos[tid] = vsp;
     if (tid < ncams) S.cpos[tid] = vcp;
-    if (kWin) {
-      for (int e = tid; e < 36 * nslots; e += 64) win[e] = 0.0;
-      for (int e = tid; e < 6 * ncams; e += 64) bwin[e] = 0.0;
-    }
   }
   st.count(kPhSlots, nslots);
   st.count(kPhCams, ncams);
+  st.count(kPhObs, nob);
+  st.count(kPhTe, nte);
+  st.count(kPhPts, npt);
+  st.count(kPhPairs, h2.y - h2.x);
   double cost = 0.0;
+  __syncthreads();
+  st.mark(kPhLoad);
 
-  for (int ch = ch0; ch < ch1; ++ch) {
-    // prefetch (kWin): the header two chunks ahead, the next chunk's image and landmarks
-    int4 m0 = n0, m1 = n1, m2 = n2, m3 = n3;
-    Img3 wimg = vimg;
-    double wx[2] = {0.0, 0.0};
-    if (kWin) {
-      const int chn2 = min(ch + 2, ch1 - 1);
-      m0 = A.chunk_hdr[4l * chn2];
-      m1 = A.chunk_hdr[4l * chn2 + 1];
-      m2 = A.chunk_hdr[4l * chn2 + 2];
-      m3 = A.chunk_hdr[4l * chn2 + 3];
-      wimg = load_img(min(ch + 1, ch1 - 1));
-      load_x(n1, wx);
+  if (MODE & kBacksub) {
+    // the pending step at its linearisation point: r + Jc dc and Jp per observation, then
+    // dp = -V^-1 sum Jp^T (r + Jc dc) per landmark (chunk_backsub)
+    if (tid < nob) {
+      const int lc = S.img.obs_lcam[tid];
+      obs_lin_w<false, true>(S, A, &pose_o[12 * S.img.acam[tid]], tid, lc >= 0 ? &dcw[6 * lc] : nullptr, cost);
     }
-    const int nob = h0.y, nte = h0.w, p0 = h1.x, npt = h1.y;
-    st.count(kPhObs, nob);
-    st.count(kPhTe, nte);
-    st.count(kPhPts, npt);
-    st.count(kPhPairs, h2.y - h2.x);
-    if (kWin) __syncthreads();  // the previous chunk is consumed
-    store_img(vimg);
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (tid + 64 * k < 3 * npt) (&S.X[0][0])[tid + 64 * k] = vx[k];
     __syncthreads();
-    st.mark(kPhLoad);
-
-    if (MODE & kBacksub) {
-      // the pending step at its linearisation point: r + Jc dc and Jp per observation, then
-      // dp = -V^-1 sum Jp^T (r + Jc dc) per landmark (chunk_backsub)
-      if (tid < nob) {
-        const int lc = S.img.obs_lcam[tid];
-        obs_lin_w<false, true>(S, A, &pose_o[12 * S.img.acam[tid]], tid, lc >= 0 ? &dcw[6 * lc] : nullptr, cost);
+    if (tid < npt) {
+      double l[6], h[3];
+      if (point_block_w(S, A.lambda, tid, l, h)) {
+        const double x2 = -h[2] * l[5];
+        const double x1 = (-h[1] - l[4] * x2) * l[2];
+        const double x0 = (-h[0] - l[1] * x1 - l[3] * x2) * l[0];
+        S.X[tid][0] += x0;
+        S.X[tid][1] += x1;
+        S.X[tid][2] += x2;
+        A.points[3l * (p0 + tid)] = S.X[tid][0];
+        A.points[3l * (p0 + tid) + 1] = S.X[tid][1];
+        A.points[3l * (p0 + tid) + 2] = S.X[tid][2];
       }
-      __syncthreads();
-      if (tid < npt) {
-        double l[6], h[3];
-        if (point_block_w(S, A.lambda, tid, l, h)) {
-          const double x2 = -h[2] * l[5];
-          const double x1 = (-h[1] - l[4] * x2) * l[2];
-          const double x0 = (-h[0] - l[1] * x1 - l[3] * x2) * l[0];
-          S.X[tid][0] += x0;
-          S.X[tid][1] += x1;
-          S.X[tid][2] += x2;
-          A.points[3l * (p0 + tid)] = S.X[tid][0];
-          A.points[3l * (p0 + tid) + 1] = S.X[tid][1];
-          A.points[3l * (p0 + tid) + 2] = S.X[tid][2];
-        }
-      }
-      __syncthreads();
-      st.mark(kPhBacksub);
     }
+    __syncthreads();
+    st.mark(kPhBacksub);
+  }
 
-    // residuals and Jacobians at the current linearisation point (cost at the updated state)
-    if (tid < nob) obs_lin_w<(MODE & kAccum) != 0, false>(S, A, S.pose_n[S.img.acam[tid]], tid, nullptr, cost);
-    if (MODE & kAccum) {
-      __syncthreads();
-      st.mark(kPhLinObs);
-      // per landmark: V (+lambda), its pivot-tested Cholesky and h = L^-1 g
-      if (tid < npt) {
-        double l[6], h[3];
-        const bool ok = point_block_w(S, A.lambda, tid, l, h);
-        S.valid[tid] = ok;
+  // residuals and Jacobians at the current linearisation point (cost at the updated state)
+  if (tid < nob) obs_lin_w<(MODE & kAccum) != 0, false>(S, A, S.pose_n[S.img.acam[tid]], tid, nullptr, cost);
+  if (MODE & kAccum) {
+    __syncthreads();
+    st.mark(kPhLinObs);
+    // per landmark: V (+lambda), its pivot-tested Cholesky and h = L^-1 g
+    if (tid < npt) {
+      double l[6], h[3];
+      const bool ok = point_block_w(S, A.lambda, tid, l, h);
+      S.valid[tid] = ok;
 #pragma unroll
-        for (int e = 0; e < 6; ++e) S.L[tid][e] = l[e];
-        S.h[tid][0] = ok ? h[0] : 0.0;
-        S.h[tid][1] = ok ? h[1] : 0.0;
-        S.h[tid][2] = ok ? h[2] : 0.0;
-      }
-      __syncthreads();
-      st.mark(kPhReduce);
-      // per track entry: W = Jc^T Jp, gc = Jc^T r over its observations, then Z = W L^-T and
-      // bt = -gc + Z h (zero, and the observations' Jc zeroed, for a frozen landmark or a
-      // fixed camera); Z | bt overwrite the Jp | r every lane has read
-      {
-        double W[18], g[6];
+      for (int e = 0; e < 6; ++e) S.L[tid][e] = l[e];
+      S.h[tid][0] = ok ? h[0] : 0.0;
+      S.h[tid][1] = ok ? h[1] : 0.0;
+      S.h[tid][2] = ok ? h[2] : 0.0;
+    }
+    __syncthreads();
+    st.mark(kPhReduce);
+    // per track entry: W = Jc^T Jp, gc = Jc^T r over its observations, then Z = W L^-T and
+    // bt = -gc + Z h (zero, and the observations' Jc zeroed, for a frozen landmark or a
+    // fixed camera); Z | bt overwrite the Jp | r every lane has read
+    {
+      double W[18], g[6];
 #pragma unroll
-        for (int e = 0; e < 18; ++e) W[e] = 0.0;
+      for (int e = 0; e < 18; ++e) W[e] = 0.0;
 #pragma unroll
-        for (int e = 0; e < 6; ++e) g[e] = 0.0;
-        const int t = min(tid, max(nte - 1, 0));
-        const bool live = tid < nte;
-        const int oa = S.img.te_obs[t], ob = live ? S.img.te_obs[t + 1] : oa;
-        for (int o = oa; o < ob; ++o) {
-          double jj[12];
-          jc_load(S, o, jj);
+      for (int e = 0; e < 6; ++e) g[e] = 0.0;
+      const int t = min(tid, max(nte - 1, 0));
+      const bool live = tid < nte;
+      const int oa = S.img.te_obs[t], ob = live ? S.img.te_obs[t + 1] : oa;
+      for (int o = oa; o < ob; ++o) {
+        double jj[12];
+        jc_load(S, o, jj);
 #pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const double rk = S.zb[kZbR + 2 * o + k];
-            const double q0 = S.zb[6 * o + 3 * k], q1 = S.zb[6 * o + 3 * k + 1], q2 = S.zb[6 * o + 3 * k + 2];
+        for (int k = 0; k < 2; ++k) {
+          const double rk = S.zb[kZbR + 2 * o + k];
+          const double q0 = S.zb[6 * o + 3 * k], q1 = S.zb[6 * o + 3 * k + 1], q2 = S.zb[6 * o + 3 * k + 2];
 #pragma unroll
-            for (int a = 0; a < 6; ++a) {
-              const double jc = jj[6 * k + a];
-              W[3 * a] += jc * q0;
-              W[3 * a + 1] += jc * q1;
-              W[3 * a + 2] += jc * q2;
-              g[a] += jc * rk;
-            }
+          for (int a = 0; a < 6; ++a) {
+            const double jc = jj[6 * k + a];
+            W[3 * a] += jc * q0;
+            W[3 * a + 1] += jc * q1;
+            W[3 * a + 2] += jc * q2;
+            g[a] += jc * rk;
           }
         }
-        const int p = S.img.te_pt[t];
-        const bool use = live && S.valid[p] && S.img.te_lcam[t] >= 0;
-        const double i00 = S.L[p][0], l10 = S.L[p][1], i11 = S.L[p][2];
-        const double l20 = S.L[p][3], l21 = S.L[p][4], i22 = S.L[p][5];
-        const double hh0 = S.h[p][0], hh1 = S.h[p][1], hh2 = S.h[p][2];
-        double bt[6];
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          const double z0 = W[3 * a] * i00;
-          const double z1 = (W[3 * a + 1] - l10 * z0) * i11;
-          const double z2 = (W[3 * a + 2] - l20 * z0 - l21 * z1) * i22;
-          W[3 * a] = use ? z0 : 0.0;
-          W[3 * a + 1] = use ? z1 : 0.0;
-          W[3 * a + 2] = use ? z2 : 0.0;
-          bt[a] = use ? -g[a] + (z0 * hh0 + z1 * hh1 + z2 * hh2) : 0.0;
-        }
-        if (live && !use)  // frozen landmark: its observations leave U too
-          for (int o = oa; o < ob; ++o)
-#pragma unroll
-            for (int e = 0; e < 10; ++e) S.Jc[o][e] = 0.0;
-        __syncthreads();  // every lane has read its Jp | r
-        if (live) {
-          double2* zr = reinterpret_cast<double2*>(&S.zb[kZbStride * t]);
-#pragma unroll
-          for (int e = 0; e < 9; ++e) zr[e] = make_double2(W[2 * e], W[2 * e + 1]);
-          double2* br = reinterpret_cast<double2*>(S.bt[t]);
-#pragma unroll
-          for (int e = 0; e < 3; ++e) br[e] = make_double2(bt[2 * e], bt[2 * e + 1]);
-        }
       }
-      __syncthreads();
-      st.mark(kPhElim);
-
-      // Schur items: lane j sums active slot j's whole block (ChunkImg::abase / abn; copies
-      // of a heavy slot balance the lanes, each its own slab row)
-      {
-        const int nas = h3.z;
-        for (int j = tid; j - tid < nas; j += kLinLanes) schur_block<kWin>(S, A, min(j, nas - 1), j < nas, win, bwin);
-        rhs_rows<kWin>(S, A, h3.w, tid, bwin);
+      const int p = S.img.te_pt[t];
+      const bool use = live && S.valid[p] && S.img.te_lcam[t] >= 0;
+      const double i00 = S.L[p][0], l10 = S.L[p][1], i11 = S.L[p][2];
+      const double l20 = S.L[p][3], l21 = S.L[p][4], i22 = S.L[p][5];
+      const double hh0 = S.h[p][0], hh1 = S.h[p][1], hh2 = S.h[p][2];
+      double bt[6];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const double z0 = W[3 * a] * i00;
+        const double z1 = (W[3 * a + 1] - l10 * z0) * i11;
+        const double z2 = (W[3 * a + 2] - l20 * z0 - l21 * z1) * i22;
+        W[3 * a] = use ? z0 : 0.0;
+        W[3 * a + 1] = use ? z1 : 0.0;
+        W[3 * a + 2] = use ? z2 : 0.0;
+        bt[a] = use ? -g[a] + (z0 * hh0 + z1 * hh1 + z2 * hh2) : 0.0;
       }
-      st.mark(kPhSchur);
-    }  // kAccum
-    if (kWin) {
-      h0 = n0; h1 = n1; h2 = n2; h3 = n3;
-      n0 = m0; n1 = m1; n2 = m2; n3 = m3;
-      vimg = wimg;
-      vx[0] = wx[0];
-      vx[1] = wx[1];
+      if (live && !use)  // frozen landmark: its observations leave U too
+        for (int o = oa; o < ob; ++o)
+#pragma unroll
+          for (int e = 0; e < 10; ++e) S.Jc[o][e] = 0.0;
+      __syncthreads();  // every lane has read its Jp | r
+      if (live) {
+        double2* zr = reinterpret_cast<double2*>(&S.zb[kZbStride * t]);
+#pragma unroll
+        for (int e = 0; e < 9; ++e) zr[e] = make_double2(W[2 * e], W[2 * e + 1]);
+        double2* br = reinterpret_cast<double2*>(S.bt[t]);
+#pragma unroll
+        for (int e = 0; e < 3; ++e) br[e] = make_double2(bt[2 * e], bt[2 * e + 1]);
+      }
     }
-  }  // chunks
-  if (kWin && (MODE & kAccum)) {  // the window to its profile-major slab rows
     __syncthreads();
-    for (int e = tid; e < 36 * nslots; e += 64) A.slab[36l * S.spos[e / 36] + e % 36] = win[e];
-    for (int e = tid; e < 6 * ncams; e += 64) A.slab_b[6l * S.cpos[e / 6] + e % 6] = bwin[e];
-  }
+    st.mark(kPhElim);
+
+    // Schur items: lane j sums active slot j's whole block (copies of a heavy slot balance
+    // the lanes, each its own slab row); then the rhs by camera-row lanes
+    {
+      const int nas = h3.z;
+      for (int j = tid; j - tid < nas; j += kLinLanesWave) schur_block(S, A, min(j, nas - 1), j < nas);
+      rhs_rows(S, A, h3.w, tid);
+    }
+    st.mark(kPhSchur);
+  }  // kAccum
   // segment cost: a fixed xor butterfly over the wave (deterministic)
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) cost += __shfl_xor(cost, m, 64);
@@ -1759,11 +1690,10 @@ class BAEngine {
     const bool prev_ok = plan_ok_;
     plan_ok_ = false;
     if (err.empty()) {
-      // one-wave K1: one chunk per segment while the window's chunks fit one round (six
-      // one-wave workgroups per CU); beyond, multi-chunk segments (window in LDS), one round
-      // of four per CU
-      bool win = kLinWave && (int64_t)prob->n_obs > (int64_t)kWaveObsPerCu * std::max(1, ctx_->num_cus);
-      const int ideal = seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, win));
+      // one-wave K1 (segments of one chunk) while the window's chunks fit one round of six
+      // one-wave workgroups per CU; the four-wave K1 over multi-chunk segments beyond
+      bool wave = (int64_t)prob->n_obs <= (int64_t)kWaveObsPerCu * std::max(1, ctx_->num_cus);
+      const int ideal = seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave));
       // the packing target stays the previous plan's while it is within 10 % of this window's
       // (a plan can take over groups only from a plan with the same target)
       const int so = prev_ok && plan_.seg_obs * 10 >= ideal * 9 && plan_.seg_obs * 10 <= ideal * 11 ? plan_.seg_obs
@@ -1774,19 +1704,11 @@ class BAEngine {
       d_chunk_img_.swap(d_chunk_img_prev_);
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
                        prob->obs_uv, so, prev_ok ? &prev_plan_ : nullptr);
-      if (err.empty() && kLinWave && !win && plan_.n_chunks() > kWaveSegsPerCu * std::max(1, ctx_->num_cus)) {
-        win = true;  // more chunks than one round: pack multi-chunk segments after all
+      if (err.empty() && plan_is_wave(plan_.seg_obs) && plan_.n_chunks() > kWaveSegsPerCu * std::max(1, ctx_->num_cus)) {
+        wave = false;  // more chunks than one round: the four-wave K1 after all
         err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
-                         prob->obs_uv, seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, true)),
+                         prob->obs_uv, seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, false)),
                          prev_ok ? &prev_plan_ : nullptr);
-      }
-      if (err.empty()) {
-        lin_win_ = kLinWave && plan_.n_segments() != plan_.n_chunks();
-        plan_max_slots_ = plan_max_cams_ = 0;
-        for (int s = 0; s < plan_.n_segments(); ++s) {
-          plan_max_slots_ = std::max(plan_max_slots_, plan_.seg_slot_off[s + 1] - plan_.seg_slot_off[s]);
-          plan_max_cams_ = std::max(plan_max_cams_, plan_.seg_cam_off[s + 1] - plan_.seg_cam_off[s]);
-        }
       }
     }
     if (ctx_->comm && ctx_->comm->nranks > 1) {
@@ -2113,11 +2035,10 @@ class BAEngine {
   // the per-chunk latency, so one round of longer segments beats two rounds of shorter ones
   // (cfg4: 766 segments instead of 985; the cfg3 plan packs 678 either way).  Round 1's
   // sweep (profiles/r01_segment_sweep.md) predates the three-per-CU K1.
-  // The one-wave K1 (kLinWave) runs one chunk per segment: the largest target packs every
+  // The one-wave K1 runs one chunk per segment: the largest target packs every
   // segment as one chunk (seg_obs = 1).
-  static int segments_target(int num_cus, bool win) {
-    if (kLinWave) return win ? kWaveWinSegsPerCu * std::max(1, num_cus) : (1 << 30);
-    return VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
+  static int segments_target(int num_cus, bool wave) {
+    return wave ? (1 << 30) : VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
   }
 
   LinArgs lin_args() {
@@ -2151,32 +2072,25 @@ class BAEngine {
       return;
     }
     LinArgs A = lin_args();
-    // one-wave K1: one chunk per segment (the chunk image of segment s is chunk s), or
-    // multi-chunk segments with the window in dynamic LDS
-    VO_REQUIRE(!kLinWave || lin_win_ || nseg == plan_.n_chunks(), VO_ERR_STATE, "K1: segments of one chunk expected");
-    A.wslots = lin_win_ ? plan_max_slots_ : 0;
-    A.wcams = lin_win_ ? plan_max_cams_ : 0;
-    const size_t dyn = lin_win_ ? 8 * ((size_t)36 * A.wslots + 6 * A.wcams + 6 * kSegCams + 12 * kSegAllCams) : 0;
-    dim3 g(nseg), b(kLinWave ? kLinLanes : kLinThreads);
+    // one-wave K1 for plans of one chunk per segment (the chunk image of segment s is chunk s)
+    const bool wave = plan_is_wave(plan_.seg_obs);
+    VO_REQUIRE(!wave || nseg == plan_.n_chunks(), VO_ERR_STATE, "K1: segments of one chunk expected");
+    dim3 g(nseg), b(wave ? kLinLanesWave : kLinThreads);
     ctx_->prof.begin(ctx_->stream, kKBaLin);
     if (stamps_on_) {
       d_stamps_.reserve((size_t)nseg * kPhCount * 8);
       A.stamps = d_stamps_.as<unsigned long long>();
     }
-#define VO_LIN_LAUNCH(M)                                                                      \
-  do {                                                                                        \
-    if (kLinWave && lin_win_ && stamps_on_)                                                   \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true, true>), g, b, dyn, ctx_->stream, A);    \
-    else if (kLinWave && lin_win_)                                                            \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true, false>), g, b, dyn, ctx_->stream, A);   \
-    else if (kLinWave && stamps_on_)                                                          \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, true>), g, b, 0, ctx_->stream, A);     \
-    else if (kLinWave)                                                                        \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, false>), g, b, 0, ctx_->stream, A);    \
-    else if (stamps_on_)                                                                      \
-      hipLaunchKernelGGL((ba_lin_kernel<M, true>), g, b, 0, ctx_->stream, A);                 \
-    else                                                                                      \
-      hipLaunchKernelGGL((ba_lin_kernel<M, false>), g, b, 0, ctx_->stream, A);                \
+#define VO_LIN_LAUNCH(M)                                                               \
+  do {                                                                                 \
+    if (wave && stamps_on_)                                                            \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true>), g, b, 0, ctx_->stream, A);     \
+    else if (wave)                                                                     \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false>), g, b, 0, ctx_->stream, A);    \
+    else if (stamps_on_)                                                               \
+      hipLaunchKernelGGL((ba_lin_kernel<M, true>), g, b, 0, ctx_->stream, A);          \
+    else                                                                               \
+      hipLaunchKernelGGL((ba_lin_kernel<M, false>), g, b, 0, ctx_->stream, A);         \
   } while (0)
     switch (mode) {
       case kAccum: VO_LIN_LAUNCH(kAccum); break;
@@ -2364,8 +2278,6 @@ class BAEngine {
   BandSplit band_{};
   bool band_on_ = false;
   bool fuse_ok_ = false;  // K2 fused into K3's launch (see fused())
-  bool lin_win_ = false;  // one-wave K1 over multi-chunk segments (window in dynamic LDS)
-  int plan_max_slots_ = 0, plan_max_cams_ = 0;  // the plan's largest segment window
   BandLds band_lds_;
   BandTables band_tab_;
   DevBuf d_fac_, d_zero_, d_band_tab_, d_red_meta_, d_red_out_, d_red_count_;

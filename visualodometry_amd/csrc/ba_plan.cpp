@@ -265,6 +265,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   P.n_fixed = n_fixed;
   P.n_free = N - n_fixed;
   P.seg_obs = std::max(1, seg_obs);
+  const bool wave = plan_is_wave(P.seg_obs);  // the one-wave K1's images (segments of one chunk)
   const int nthr = plan_threads(M);
 
   PlanArr<int32_t> ob_start(L + 1), sorted(std::max(M, 1)), te_start(L + 1);
@@ -581,7 +582,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     // the slot whose per-lane chain (pairs / copies, a diagonal slot's pair weighted 5 against
     // 3 for its U and b) is longest, until 64 lanes or a chain of kCopyChain (each copy is one
     // more slab row for K1 to write and K2 to read).
-    if (kLinWave)
+    if (wave)
       for (size_t k = 0; k < R.segs.size(); ++k) {
         PlanSeg& sg = R.segs[k];
         const int nch = (k + 1 < R.segs.size() ? R.segs[k + 1].chunk0 : (int)R.chunk_q.size()) - sg.chunk0;
@@ -592,7 +593,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         auto chain = [&](int i) {
           return (sg.slot_cnt[i] + cp[i] - 1) / cp[i] * (sg.slots[i].first == sg.slots[i].second ? 5 : 3);
         };
-        for (int lanes = n; lanes < std::min(kLinLanes, kSegSlots); ++lanes) {
+        for (int lanes = n; lanes < std::min(kLinLanesWave, kSegSlots); ++lanes) {
           int best = 0;
           for (int i = 1; i < n; ++i)
             if (chain(i) > chain(best)) best = i;
@@ -914,88 +915,47 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         // in it, compacted in window order (their lists keep their order)
         int nas = 0, nac = 0;
         {
-          // active slots; parts per item (2^lg lanes) doubled greedily for the slot with the
-          // longest per-lane pair chain while the lanes fit the budget.  Four-wave K1: an item
-          // is a (slot, row) on one lane per part, one pass of its 256 lanes (more than 42
-          // active slots take one lane per row item, in two passes).  One-wave K1 (kLinWave):
-          // an item is a whole slot block on one lane per part (kRowLanes = 1), passes of 64
-          // lanes run one after another, each as long as its longest chain, so the budget is the
-          // smallest whole number of passes or one more, whichever the pass-time estimate
-          // prefers.  A diagonal slot's lanes also sum U and b over their pairs' observations.
-          int sl[kSegSlots], cntp[kSegSlots], lg[kSegSlots], wt[kSegSlots];
+          // active slots.  Four-wave K1: lanes per row item (2^lg) doubled greedily for the slot
+          // with the longest per-lane pair chain while 6 lanes x the sum fit its 256 lanes (more
+          // than 42 active slots take one lane per row item, in two passes), items ordered by
+          // lanes per row descending (every item group starts at a multiple of its own width).
+          // One-wave K1: lane j = active slot j (copies of heavy slots made at packing).
+          int sl[kSegSlots], cntp[kSegSlots], lg[kSegSlots];
           for (int i = 0; i < ns; ++i)
             if (P.slot_ptr[sb + i + 1] > P.slot_ptr[sb + i]) {
               sl[nas] = i;
               cntp[nas] = P.slot_ptr[sb + i + 1] - P.slot_ptr[sb + i];
-              // cost units per pair: the one-wave K1's lane sums a whole 6x6 block per pair (a
-              // diagonal slot's also U and b of the pair's observations)
-              wt[nas] = !kLinWave ? 1 : P.slot_i[so + i] == P.slot_j[so + i] ? 4 : 3;
               lg[nas++] = 0;
             }
-          auto chain_of = [&](int i, int l) { return ((cntp[i] + (1 << l) - 1) >> l) * wt[i]; };
-          auto balance = [&](int budget, int* lv) {
-            for (int i = 0; i < nas; ++i) lv[i] = 0;
+          int ord[kSegSlots];
+          for (int i = 0; i < nas; ++i) ord[i] = i;
+          if (!wave) {
             int used = nas;
             for (;;) {
               int best = -1, chain = 0;
               for (int i = 0; i < nas; ++i) {
-                const int c = chain_of(i, lv[i]);
+                const int c = (cntp[i] + (1 << lg[i]) - 1) >> lg[i];
                 if (c > chain) {
                   chain = c;
                   best = i;
                 }
               }
-              if (best < 0 || ((cntp[best] + (1 << lv[best]) - 1) >> lv[best]) <= 1 || lv[best] == 3 ||
-                  kRowLanes * (used + (1 << lv[best])) > budget)
-                break;
-              used += 1 << lv[best];
-              ++lv[best];
+              if (best < 0 || chain <= 1 || lg[best] == 3 || 6 * (used + (1 << lg[best])) > kLinLanes) break;
+              used += 1 << lg[best];
+              ++lg[best];
             }
-          };
-          // order by lanes per row, descending (stable; every item group starts at a multiple of
-          // its own width), then, for the one-wave K1, by chain descending (passes of alike chains)
-          int ord[kSegSlots];
-          auto order = [&](const int* lv) {
-            for (int i = 0; i < nas; ++i) ord[i] = i;
-            std::stable_sort(ord, ord + nas, [&](int a, int b) {
-              if (lv[a] != lv[b]) return lv[a] > lv[b];
-              return kLinWave && chain_of(a, lv[a]) > chain_of(b, lv[b]);
-            });
-          };
+            std::stable_sort(ord, ord + nas, [&](int a, int b) { return lg[a] > lg[b]; });
+          }
           int base = 0;
-          if (!kLinWave) {
-            balance(kLinLanes, lg);
-            order(lg);
-            for (int j = 0; j < nas; ++j) {
-              const int i = ord[j];
-              g.aslot[j] = (uint8_t)sl[i];
-              g.slotp[j] = P.slot_ptr[sb + sl[i]] - e0;
-              g.apcnt[j] = (uint16_t)cntp[i];
-              g.anp[j] = (uint8_t)lg[i];
-              g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
-              g.abase[j] = (uint16_t)base;
-              base += kRowLanes << lg[i];
-            }
-          } else {
-            // One-wave K1: lane j sums active slot j's whole block (copies of a heavy slot are
-            // slots of their own, see pack); the first slot of a diagonal block's copies also
-            // sums the camera's b over all of their pairs
-            for (int j = 0; j < nas; ++j) {
-              const int i = sl[j];
-              const bool diag = P.slot_i[so + i] == P.slot_j[so + i];
-              const bool first = i == 0 || P.slot_i[so + i - 1] != P.slot_i[so + i] ||
-                                 P.slot_j[so + i - 1] != P.slot_j[so + i];
-              int run = i + 1;
-              while (run < ns && P.slot_i[so + run] == P.slot_i[so + i] && P.slot_j[so + run] == P.slot_j[so + i]) ++run;
-              g.aslot[j] = (uint8_t)i;
-              g.slotp[j] = P.slot_ptr[sb + i] - e0;
-              g.apcnt[j] = (uint16_t)cntp[j];
-              g.anp[j] = 0;
-              g.adcam[j] = diag ? (uint8_t)lcam_of(P.slot_i[so + i]) : 0xFF;
-              g.abn[j] = diag && first ? (uint16_t)(P.slot_ptr[sb + run] - P.slot_ptr[sb + i]) : 0;
-              g.abase[j] = (uint16_t)base;
-              base += 1;
-            }
+          for (int j = 0; j < nas; ++j) {
+            const int i = ord[j];
+            g.aslot[j] = (uint8_t)sl[i];
+            g.slotp[j] = P.slot_ptr[sb + sl[i]] - e0;
+            g.apcnt[j] = (uint16_t)cntp[i];
+            g.anp[j] = (uint8_t)lg[i];
+            g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
+            g.abase[j] = (uint16_t)base;
+            base += wave ? 1 : 6 << lg[i];
           }
           g.abase[nas] = (uint16_t)base;
           g.slotp[nas] = e1 - e0;

@@ -52,14 +52,12 @@ constexpr int kChunkTe = VO_CHUNK_OBS;
 constexpr int kChunkPts = VO_CHUNK_OBS / 2;
 constexpr int kChunkPairs = 8 * VO_CHUNK_OBS;  // camera-pair (x, y) entries of one chunk, staged in LDS
 constexpr int kSegSlots = 64;
-// K1 variant: one wave per chunk (segments of one chunk; the Schur-pair lanes balanced over
-// passes of 64 lanes) or the four-wave workgroup walking a segment's chunks (one pass of 256)
-#ifndef VO_BA_K1_WAVE
-#define VO_BA_K1_WAVE 1
-#endif
-constexpr bool kLinWave = VO_BA_K1_WAVE != 0;
-constexpr int kLinLanes = kLinWave ? 64 : 256;  // K1 lanes per Schur pass (ba.hip)
-constexpr int kRowLanes = kLinWave ? 1 : 6;      // lanes per Schur item part: one per block row, or one per block
+// K1 variants (a plan property): segments of one chunk (seg_obs == 1) run the one-wave K1
+// (one 64-lane workgroup per chunk, one lane per Schur slot block); any other packing runs the
+// four-wave K1 walking its segment's chunks (one pass of 256 lanes, one lane per block row).
+constexpr int kLinLanesWave = 64;   // one-wave K1 lanes (ba.hip ba_lin_wave_kernel)
+constexpr int kLinLanes = 256;      // four-wave K1 lanes per Schur pass (ba.hip kLinThreads)
+inline bool plan_is_wave(int seg_obs) { return seg_obs == 1; }
 constexpr int kChunkHdr = 16;
 
 constexpr int kSegCams = 24;     // free (window) cameras of a segment
@@ -98,18 +96,16 @@ struct alignas(16) ChunkImg {
   uint8_t dslot[kSegCams];         // active camera i -> its diagonal slot
   uint8_t aslot[kSegSlots];        // active slot i -> window slot
   uint8_t acid[kSegCams];          // active camera i -> window camera
-  // Schur-pair lanes, balanced.  Four-wave K1: active slot i (ordered by lanes per item
-  // descending) sums its apcnt[i] pairs from slotp[i] on 6 << anp[i] lanes starting at abase[i]
-  // (2^anp lanes per row, their strided partial sums combined by an aligned butterfly).
-  // One-wave K1: lane i sums active slot i's whole block over its apcnt[i] pairs (abase[i] = i;
-  // a heavy slot's pairs are split over copies of the slot, each with its own slab row); a
-  // diagonal slot's lanes add U over their pairs' observations, and the first copy sums the
-  // camera's b over the abn[i] pairs from slotp[i] (0 otherwise).  abase[nas] = lanes used
+  // Schur-pair lanes.  Four-wave K1: active slot i (ordered by lanes per item descending) sums
+  // its apcnt[i] pairs from slotp[i] on 6 << anp[i] lanes starting at abase[i] (2^anp lanes per
+  // row, their strided partial sums combined by an aligned butterfly).  One-wave K1: lane i sums
+  // active slot i's whole block (abase[i] = i, anp[i] = 0; a heavy slot's pairs are split over
+  // copies of the slot, each with its own slab row), a diagonal slot's lanes adding U over their
+  // pairs' observations.  abase[nas] = lanes used
   uint16_t apcnt[kSegSlots];
   uint16_t abase[kSegSlots + 1];  // up to 6 x 64 lanes (two passes of the workgroup)
   uint8_t anp[kSegSlots];
   uint8_t adcam[kSegSlots];        // active slot i -> window camera if diagonal, else 0xFF
-  uint16_t abn[kSegSlots];         // one-wave K1: pairs whose bt the slot's lane sums into b
   alignas(2) uint16_t pairs[kChunkPairs];  // (te_x | te_y << 8) by slot
   uint8_t caml[kChunkTe];          // track entries by window camera
   uint8_t camol[kChunkObs];        // observations by window camera

@@ -2,9 +2,10 @@
 // plan of a window and walks each chunk's Schur lanes exactly as ba_lin_wave_kernel assigns
 // them (passes of kLinLanes, binary search over abase, 2^anp lanes per row), checking that
 //   - every pair of every active slot is summed exactly once per row, by one part;
-//   - every row's parts are aligned lanes of one pass (the DPP butterfly's groups);
-//   - a diagonal slot's pairs are (x, x) over exactly its camera's track entries (so its lanes'
-//     U and b sums equal the camera lists'), adcam names the camera, off-diagonal slots 0xFF;
+//   - every row's parts are aligned lanes of one pass (the four-wave K1's butterfly groups);
+//   - the one-wave K1 (seg_obs 1): one lane per slot block, copies splitting heavy slots;
+//   - a diagonal slot's pairs (over its copies) are (x, x) over exactly its camera's track entries
+//     (so its lanes' U sums equal the camera lists'), adcam names the camera, off-diagonal 0xFF;
 //   - with one chunk per segment, every window slot is active and every window camera has a
 //     diagonal slot (every slab row and rhs entry is written).
 // Input (binary): int32 n_poses, n_points, n_obs, n_fixed, seg_obs; point_ptr; obs_cam; obs_uv.
@@ -46,6 +47,7 @@ int main(int argc, char** argv) {
     return 2;
   std::fclose(f);
   vo::BAPlan P;
+  const bool wave = vo::plan_is_wave(so);
   const std::string err = vo::build_plan(P, N, L, M, nf, ptr.data(), cam.data(), uv.data(), so, nullptr);
   if (!err.empty()) FAIL("plan: %s", err.c_str());
   long passes = 0;
@@ -60,8 +62,9 @@ int main(int argc, char** argv) {
       const vo::ChunkImg& g = P.chunk_img[ch];
       const int nas = h[14], lanes = g.abase[nas], npairs = h[9] - h[8];
       std::vector<int> cover(6 * (size_t)npairs, 0);
-      for (int base = 0; base < lanes; base += vo::kLinLanes, ++passes) {
-        for (int tid = 0; tid < vo::kLinLanes; ++tid) {
+      const int plane = wave ? vo::kLinLanesWave : vo::kLinLanes;
+      for (int base = 0; base < lanes; base += plane, ++passes) {
+        for (int tid = 0; tid < plane; ++tid) {
           const int t = base + tid;
           if (t >= lanes) continue;
           int s = 0;
@@ -69,7 +72,7 @@ int main(int argc, char** argv) {
             if (s + sp < nas && g.abase[s + sp] <= t) s += sp;
           const int off = t - g.abase[s];
           int r0, r1, part, np;
-          if (vo::kLinWave) {  // lane = item: the whole block over the item's pairs
+          if (wave) {  // lane = item: the whole block over the item's pairs
             if (off != 0) FAIL("chunk %d: lane %d is not item %d", ch, t, s);
             r0 = 0;
             r1 = 6;
@@ -81,7 +84,7 @@ int main(int argc, char** argv) {
             const int a = off >> lgp;
             part = off & (np - 1);
             if (a >= 6) FAIL("chunk %d lane %d: row %d", ch, t, a);
-            if ((t - part) / vo::kLinLanes != (t - part + np - 1) / vo::kLinLanes || (t - part) % np)
+            if ((t - part) / plane != (t - part + np - 1) / plane || (t - part) % np)
               FAIL("chunk %d slot item %d: parts not aligned in one pass", ch, s);
             r0 = a;
             r1 = a + 1;
@@ -96,8 +99,7 @@ int main(int argc, char** argv) {
         if (cover[k] != 1) FAIL("chunk %d: pair %zu row %zu summed %d times", ch, k / 6, k % 6, cover[k]);
       if (g.slotp[nas] != npairs) FAIL("chunk %d: active slots end at %d of %d pairs", ch, (int)g.slotp[nas], npairs);
       const int te0 = h[2];
-      std::vector<std::vector<int>> upairs(ncams), bpairs(ncams);
-      std::vector<int> bsum(ncams, 0);
+      std::vector<std::vector<int>> upairs(ncams);
       for (int s = 0; s < nas; ++s) {
         const int ws = g.aslot[s];
         slot_seen[ws] = 1;
@@ -111,12 +113,6 @@ int main(int argc, char** argv) {
         cam_diag[wc] = 1;
         // its pairs: (x, x) over the chunk's track entries of that camera, each once
         std::vector<int> tes;
-        if (vo::kLinWave) {  // b: exactly one copy of the block sums it, over every copy's pairs
-          if (g.abn[s] > 0) {
-            if (++bsum[wc] != 1) FAIL("chunk %d: camera %d's b summed twice", ch, wc);
-            for (int e = g.slotp[s]; e < g.slotp[s] + g.abn[s]; ++e) bpairs[wc].push_back(g.pairs[e] & 255);
-          }
-        }
         for (int e = g.slotp[s]; e < g.slotp[s] + g.apcnt[s]; ++e) {
           const int x = g.pairs[e] & 255, y = g.pairs[e] >> 8;
           if (x != y) FAIL("chunk %d: diagonal slot pair (%d, %d)", ch, x, y);
@@ -130,10 +126,6 @@ int main(int argc, char** argv) {
           if (P.te_lcam[t] == wc) want.push_back(t - te0);
         std::sort(upairs[wc].begin(), upairs[wc].end());
         if (!upairs[wc].empty() && upairs[wc] != want) FAIL("chunk %d: camera %d track entries (U) differ", ch, wc);
-        if (vo::kLinWave && !upairs[wc].empty()) {
-          std::sort(bpairs[wc].begin(), bpairs[wc].end());
-          if (bpairs[wc] != want) FAIL("chunk %d: camera %d track entries (b) differ", ch, wc);
-        }
       }
     }
     if (one) {
