@@ -1710,6 +1710,15 @@ class BAEngine {
                          prob->obs_uv, seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, false)),
                          prev_ok ? &prev_plan_ : nullptr);
       }
+      // four-wave K1: every first-camera group ends in a partial segment, so the packing target
+      // may give more segments than one round holds; then pack once more, proportionally wider
+      const int round = segments_target(ctx_->num_cus, false);
+      for (int k = 0; k < 4 && err.empty() && !plan_is_wave(plan_.seg_obs) && plan_.n_segments() > round; ++k) {
+        const int so2 = (int)std::min<int64_t>((int64_t)plan_.seg_obs * plan_.n_segments() / round + 1 + plan_.seg_obs / 50,
+                                               1 << 30);
+        err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
+                         prob->obs_uv, so2, prev_ok ? &prev_plan_ : nullptr);
+      }
     }
     if (ctx_->comm && ctx_->comm->nranks > 1) {
       const int32_t F = err.empty() ? plan_.n_free : 0;
