@@ -17,7 +17,7 @@ from visualodometry_amd import _lib  # noqa: E402
 from visualodometry_amd.ba import BASession  # noqa: E402
 from visualodometry_amd.synthetic import make_ba_config  # noqa: E402
 
-PHASES = ["load", "backsub", "lin_obs", "reduce", "eliminate", "schur_pairs", "write", "schur_cams", "-", "-",
+PHASES = ["load", "backsub", "lin_obs", "reduce", "eliminate", "schur_pairs", "write(rhs)", "schur_cams(U)", "-", "-",
           "n_obs", "n_te", "n_pts", "n_pairs", "n_slots", "n_cams"]
 NPH = len(PHASES)
 K3 = ["k3_setup", "k3_side_chol", "k3_backsub", "k3_tail", "k3_side_barrier", "k3_side_midbar", "k3_merge",

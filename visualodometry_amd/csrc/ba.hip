@@ -887,7 +887,8 @@ __device__ __forceinline__ void jc_load(const LinWave& S, int o, double (&jj)[12
 // Z_x Z_y^T as FMA chains with both Z rows in registers (pair j+1's rows fetched while pair j
 // accumulates); a diagonal slot's lane adds U over its pairs' observations (pair (x, x): track
 // entry x of the slot's camera).  The block goes straight to its slab row.
-__device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, int si, bool live) {
+template <class Stamp>
+__device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, int si, bool live, Stamp& st) {
   double out[36];
 #pragma unroll
   for (int e = 0; e < 36; ++e) out[e] = 0.0;
@@ -930,6 +931,9 @@ __device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, 
       accum(zxB, zyB);
     }
     if (j < n) accum(zxA, zyA);
+  }
+  st.mark(kPhSchur);  // stamped builds: the pair sums
+  if (n > 0) {
     if (dcam != 0xFF) {
       for (int e = e0; e < e0 + n; ++e) {
         const int x = S.img.pairs[e] & 255;
@@ -945,6 +949,7 @@ __device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, 
       }
     }
   }
+  st.mark(kPhSchurU);  // U
   if (!live) return;
   {
     double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s]]);
@@ -1164,10 +1169,10 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
     // the lanes, each its own slab row); then the rhs by camera-row lanes
     {
       const int nas = h3.z;
-      for (int j = tid; j - tid < nas; j += kLinLanesWave) schur_block(S, A, min(j, nas - 1), j < nas);
+      for (int j = tid; j - tid < nas; j += kLinLanesWave) schur_block(S, A, min(j, nas - 1), j < nas, st);
       rhs_rows(S, A, h3.w, tid);
     }
-    st.mark(kPhSchur);
+    st.mark(kPhWrite);  // stamped builds: the rhs (with the final write below)
   }  // kAccum
   // segment cost: a fixed xor butterfly over the wave (deterministic)
 #pragma unroll

@@ -589,16 +589,25 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         const int n = (int)sg.slots.size();
         if (nch != 1 || n == 0) continue;
         int cp[kSegSlots];
-        for (int i = 0; i < n; ++i) cp[i] = 1;
-        auto chain = [&](int i) {
-          return (sg.slot_cnt[i] + cp[i] - 1) / cp[i] * (sg.slots[i].first == sg.slots[i].second ? 5 : 3);
-        };
-        for (int lanes = n; lanes < std::min(kLinLanesWave, kSegSlots); ++lanes) {
-          int best = 0;
-          for (int i = 1; i < n; ++i)
-            if (chain(i) > chain(best)) best = i;
-          if (chain(best) <= kCopyChain) break;
-          ++cp[best];
+        auto wgt = [&](int i) { return sg.slots[i].first == sg.slots[i].second ? 5 : 3; };
+        auto chain = [&](int i) { return (sg.slot_cnt[i] + cp[i] - 1) / cp[i] * wgt(i); };
+        // each slot's fewest copies for a chain within kCopyChain (what the greedy below reaches
+        // while the lanes last), the greedy itself only when they do not
+        int lanes = 0;
+        for (int i = 0; i < n; ++i) {
+          const int per = std::max(1, kCopyChain / wgt(i));  // pairs per copy
+          cp[i] = std::max(1, (sg.slot_cnt[i] + per - 1) / per);
+          lanes += cp[i];
+        }
+        if (lanes > std::min(kLinLanesWave, kSegSlots)) {
+          for (int i = 0; i < n; ++i) cp[i] = 1;
+          for (lanes = n; lanes < std::min(kLinLanesWave, kSegSlots); ++lanes) {
+            int best = 0;
+            for (int i = 1; i < n; ++i)
+              if (chain(i) > chain(best)) best = i;
+            if (chain(best) <= kCopyChain) break;
+            ++cp[best];
+          }
         }
         for (int i = 0; i < n; ++i)
           for (int c = 1; c < cp[i]; ++c) sg.slots.push_back(sg.slots[i]);
