@@ -888,7 +888,7 @@ __device__ __forceinline__ void jc_load(const LinWave& S, int o, double (&jj)[12
 // accumulates); a diagonal slot's lane adds U over its pairs' observations (pair (x, x): track
 // entry x of the slot's camera).  The block goes straight to its slab row.
 template <class Stamp>
-__device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, int si, bool live, Stamp& st) {
+__device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si, bool live, Stamp& st) {
   double out[36];
 #pragma unroll
   for (int e = 0; e < 36; ++e) out[e] = 0.0;
@@ -933,10 +933,18 @@ __device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, 
     if (j < n) accum(zxA, zyA);
   }
   st.mark(kPhSchur);  // stamped builds: the pair sums
+  double ob[6] = {0, 0, 0, 0, 0, 0};
   if (n > 0) {
     if (dcam != 0xFF) {
       for (int e = e0; e < e0 + n; ++e) {
         const int x = S.img.pairs[e] & 255;
+        const double2* br = reinterpret_cast<const double2*>(S.bt[x]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const double2 v = br[k];
+          ob[2 * k] += v.x;
+          ob[2 * k + 1] += v.y;
+        }
         for (int o = S.img.te_obs[x]; o < S.img.te_obs[x + 1]; ++o) {
           double jj[12];
           jc_load(S, o, jj);
@@ -951,6 +959,11 @@ __device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, 
   }
   st.mark(kPhSchurU);  // U
   if (!live) return;
+  if (dcam != 0xFF) {  // this copy's share of the camera's b, for rhs_rows (the X | L | h region is dead)
+    double2* bp = reinterpret_cast<double2*>(&S.X[0][0]) + 3 * si;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) bp[k] = make_double2(ob[2 * k], ob[2 * k + 1]);
+  }
   {
     double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s]]);
 #pragma unroll
@@ -958,23 +971,21 @@ __device__ __forceinline__ void schur_block(const LinWave& S, const LinArgs& A, 
   }
 }
 
-// The rhs of the chunk's window cameras (one-wave K1): lane (active camera ci, row a) sums bt's
-// row a over the camera's track entries (ChunkImg::camp / caml), eight loads in flight, into
-// its slab entry.
+// The rhs of the chunk's window cameras (one-wave K1): lane (active camera ci, row a) adds row a
+// of the camera's diagonal copies' partial sums (consecutive items cdiag0 .. + cdiagn, left in
+// the X | L | h region by schur_block) in item order into its slab entry.
 __device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int nac, int tid) {
+  static_assert(sizeof(S.X) + sizeof(S.L) + sizeof(S.h) >= 6 * sizeof(double) * kSegSlots &&
+                    offsetof(LinWave, L) == offsetof(LinWave, X) + sizeof(S.X) &&
+                    offsetof(LinWave, h) == offsetof(LinWave, L) + sizeof(S.L),
+                "b partials of every item fit the X | L | h region");
+  const double* bp = &S.X[0][0];
   for (int q = tid; q < 6 * nac; q += kLinLanesWave) {
     const int ci = q / 6, a = q - 6 * ci;
-    const int c0 = S.img.camp[ci], c1 = S.img.camp[ci + 1];
+    const int j0 = S.img.cdiag0[ci], nj = S.img.cdiagn[ci];
     double acc = 0.0;
-    for (int e = c0; e < c1; e += 8) {
-      double v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = S.bt[S.img.caml[min(e + k, c1 - 1)]][a];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc += e + k < c1 ? v[k] : 0.0;
-    }
-    const int c = S.img.acid[ci];
-    A.slab_b[6l * S.cpos[c] + a] = acc;
+    for (int j = 0; j < nj; ++j) acc += bp[6 * (j0 + j) + a];
+    A.slab_b[6l * S.cpos[S.img.acid[ci]] + a] = acc;
   }
 }
 
@@ -1170,6 +1181,7 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
     {
       const int nas = h3.z;
       for (int j = tid; j - tid < nas; j += kLinLanesWave) schur_block(S, A, min(j, nas - 1), j < nas, st);
+      __syncthreads();  // the diagonal copies' b partials
       rhs_rows(S, A, h3.w, tid);
     }
     st.mark(kPhWrite);  // stamped builds: the rhs (with the final write below)

@@ -979,6 +979,17 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
           }
         g.camp[nac] = c1 - c0;
         g.camop[nac] = q1 - q0;
+        if (wave)  // each active camera's diagonal items (its copies are consecutive)
+          for (int ci = 0; ci < nac; ++ci) {
+            int j0 = -1, nj = 0;
+            for (int j = 0; j < nas; ++j)
+              if (g.adcam[j] == g.acid[ci]) {
+                if (j0 < 0) j0 = j;
+                ++nj;
+              }
+            g.cdiag0[ci] = (uint8_t)std::max(j0, 0);
+            g.cdiagn[ci] = (uint8_t)nj;
+          }
         for (int i = 0; i < c1 - c0; ++i) g.caml[i] = P.cam_list[c0 + i];
         for (int i = 0; i < q1 - q0; ++i) g.camol[i] = P.camo_list[q0 + i];
         h[14] = nas;

@@ -106,6 +106,8 @@ struct alignas(16) ChunkImg {
   uint16_t abase[kSegSlots + 1];  // up to 6 x 64 lanes (two passes of the workgroup)
   uint8_t anp[kSegSlots];
   uint8_t adcam[kSegSlots];        // active slot i -> window camera if diagonal, else 0xFF
+  uint8_t cdiag0[kSegCams];        // one-wave K1: active camera i -> its first diagonal item
+  uint8_t cdiagn[kSegCams];        //   and the number of copies (consecutive items)
   alignas(2) uint16_t pairs[kChunkPairs];  // (te_x | te_y << 8) by slot
   uint8_t caml[kChunkTe];          // track entries by window camera
   uint8_t camol[kChunkObs];        // observations by window camera
