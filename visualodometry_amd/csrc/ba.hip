@@ -774,6 +774,12 @@ __global__ __launch_bounds__(kLinThreads, 3) void ba_lin_kernel(LinArgs A) {  //
 // Z rows of 18 doubles (36 dwords: the rows start on 16 different 4-bank offsets of gfx950's
 // 64 banks, so a ds_read_b128 of 16 lanes on random rows rarely conflicts; a 24-double row of
 // Z | bt started on 4 offsets only, a 4-way conflict on every Schur load)
+// The one-wave K1's phase boundary: its workgroup is one wave, whose LDS operations complete
+// in order, so a phase only needs its LDS writes done and the compiler kept from moving LDS
+// accesses across (no s_barrier; and no workgroup fence, which would also wait for every
+// outstanding global store: the back substitution's points and the slab rows).
+__device__ __forceinline__ void lds_sync_wave() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 constexpr int kZbStride = 18;                  // doubles per track entry's Z row
 constexpr int kZbR = 6 * kChunkObs;            // r (2 per observation) after Jp (6 per observation)
 constexpr int kZbDc = kZbR + 2 * kChunkObs;    // back substitution: dc of the window cameras
@@ -1067,7 +1073,7 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
   st.count(kPhPts, npt);
   st.count(kPhPairs, h2.y - h2.x);
   double cost = 0.0;
-  __syncthreads();
+  lds_sync_wave();
   st.mark(kPhLoad);
 
   if (MODE & kBacksub) {
@@ -1077,7 +1083,7 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
       const int lc = S.img.obs_lcam[tid];
       obs_lin_w<false, true>(S, A, &pose_o[12 * S.img.acam[tid]], tid, lc >= 0 ? &dcw[6 * lc] : nullptr, cost);
     }
-    __syncthreads();
+    lds_sync_wave();
     if (tid < npt) {
       double l[6], h[3];
       if (point_block_w(S, A.lambda, tid, l, h)) {
@@ -1092,14 +1098,14 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
         A.points[3l * (p0 + tid) + 2] = S.X[tid][2];
       }
     }
-    __syncthreads();
+    lds_sync_wave();
     st.mark(kPhBacksub);
   }
 
   // residuals and Jacobians at the current linearisation point (cost at the updated state)
   if (tid < nob) obs_lin_w<(MODE & kAccum) != 0, false>(S, A, S.pose_n[S.img.acam[tid]], tid, nullptr, cost);
   if (MODE & kAccum) {
-    __syncthreads();
+    lds_sync_wave();
     st.mark(kPhLinObs);
     // per landmark: V (+lambda), its pivot-tested Cholesky and h = L^-1 g
     if (tid < npt) {
@@ -1112,7 +1118,7 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
       S.h[tid][1] = ok ? h[1] : 0.0;
       S.h[tid][2] = ok ? h[2] : 0.0;
     }
-    __syncthreads();
+    lds_sync_wave();
     st.mark(kPhReduce);
     // per track entry: W = Jc^T Jp, gc = Jc^T r over its observations, then Z = W L^-T and
     // bt = -gc + Z h (zero, and the observations' Jc zeroed, for a frozen landmark or a
@@ -1163,7 +1169,7 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
         for (int o = oa; o < ob; ++o)
 #pragma unroll
           for (int e = 0; e < 10; ++e) S.Jc[o][e] = 0.0;
-      __syncthreads();  // every lane has read its Jp | r
+      lds_sync_wave();  // every lane has read its Jp | r
       if (live) {
         double2* zr = reinterpret_cast<double2*>(&S.zb[kZbStride * t]);
 #pragma unroll
@@ -1173,7 +1179,7 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
         for (int e = 0; e < 3; ++e) br[e] = make_double2(bt[2 * e], bt[2 * e + 1]);
       }
     }
-    __syncthreads();
+    lds_sync_wave();
     st.mark(kPhElim);
 
     // Schur items: lane j sums active slot j's whole block (copies of a heavy slot balance
@@ -1181,7 +1187,7 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
     {
       const int nas = h3.z;
       for (int j = tid; j - tid < nas; j += kLinLanesWave) schur_block(S, A, min(j, nas - 1), j < nas, st);
-      __syncthreads();  // the diagonal copies' b partials
+      lds_sync_wave();  // the diagonal copies' b partials
       rhs_rows(S, A, h3.w, tid);
     }
     st.mark(kPhWrite);  // stamped builds: the rhs (with the final write below)
