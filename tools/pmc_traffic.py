@@ -27,7 +27,7 @@ import bench  # noqa: E402
 # first match wins: "fpack_kernel" before "pack_kernel"; the int8 sweep is attributed by
 # its template argument (match_kernel<2> = the D = 128 SIFT workload of the bench line;
 # the float line's match_kernel<4> only checks the flag and exits)
-SHORT = [("ba_lin_kernel", "ba_lin"), ("ba_reduce_kernel", "ba_reduce"), ("ba_band_kernel", "ba_solve"),
+SHORT = [("ba_lin_wave_kernel", "ba_lin"), ("ba_lin_kernel", "ba_lin"), ("ba_reduce_kernel", "ba_reduce"), ("ba_band_kernel", "ba_solve"),
          ("ba_solve_kernel", "ba_solve"), ("ba_solve2_kernel", "ba_solve"),
          ("fpack_kernel", "match_fpack"), ("fsweep_kernel", "match_f32"), ("frerank_kernel", "match_rerank"),
          ("pack_kernel", "match_pack"), ("match_kernel<2>", "match_i8"), ("match_kernel", "match_i8_other_d"),

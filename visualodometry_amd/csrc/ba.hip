@@ -963,8 +963,10 @@ __device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si
       }
     }
   }
-  st.mark(kPhSchurU);  // U
-  if (!live) return;
+  if (!live) {
+    st.mark(kPhSchurU);
+    return;
+  }
   if (dcam != 0xFF) {  // this copy's share of the camera's b, for rhs_rows (the X | L | h region is dead)
     double2* bp = reinterpret_cast<double2*>(&S.X[0][0]) + 3 * si;
 #pragma unroll
@@ -975,6 +977,7 @@ __device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si
 #pragma unroll
     for (int e = 0; e < 18; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
   }
+  st.mark(kPhSchurU);  // stamped builds: U, the b partials and the block's slab stores
 }
 
 // The rhs of the chunk's window cameras (one-wave K1): lane (active camera ci, row a) adds row a
