@@ -972,12 +972,36 @@ __device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si
 #pragma unroll
     for (int k = 0; k < 3; ++k) bp[k] = make_double2(ob[2 * k], ob[2 * k + 1]);
   }
-  {
+  if (S.img.anp[si] <= 1) {  // a slot of one item: its slab row
     double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s]]);
+#pragma unroll
+    for (int e = 0; e < 18; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
+  } else {  // a copy: its block to the scratch for copy_rows (the Jc | Z | bt region)
+    lds_sync_wave();  // every lane's reads of that region are done (one wave, in order)
+    double2* w = reinterpret_cast<double2*>(&S.Jc[0][0]) + 18 * si;
 #pragma unroll
     for (int e = 0; e < 18; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
   }
   st.mark(kPhSchurU);  // stamped builds: U, the b partials and the block's slab stores
+}
+
+// A slot's copies (one-wave K1): copy k of m sums entries [36 k / m, 36 (k + 1) / m) of the
+// slot's m partial blocks (scratch rows of consecutive items) in copy order into the slab row.
+static_assert(offsetof(LinWave, zb) == offsetof(LinWave, Jc) + sizeof(LinWave::Jc) &&
+                  offsetof(LinWave, bt) == offsetof(LinWave, zb) + sizeof(LinWave::zb) &&
+                  sizeof(LinWave::Jc) + sizeof(LinWave::zb) + sizeof(LinWave::bt) >= 36 * sizeof(double) * 60,
+              "the copies' scratch (60 items) fits the Jc | Z | bt region");
+__device__ __forceinline__ void copy_rows(const LinWave& S, const LinArgs& A, int si, bool live) {
+  const int m = S.img.anp[si];
+  if (!live || m <= 1) return;
+  const int k = S.img.acopy[si], j0 = si - k;
+  const double* sc = &S.Jc[0][0];
+  double* row = &A.slab[36l * S.spos[S.img.aslot[si]]];
+  for (int e = 36 * k / m; e < 36 * (k + 1) / m; ++e) {
+    double acc = sc[36 * j0 + e];
+    for (int c = 1; c < m; ++c) acc += sc[36 * (j0 + c) + e];
+    row[e] = acc;
+  }
 }
 
 // The rhs of the chunk's window cameras (one-wave K1): lane (active camera ci, row a) adds row a
@@ -1190,7 +1214,8 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
     {
       const int nas = h3.z;
       for (int j = tid; j - tid < nas; j += kLinLanesWave) schur_block(S, A, min(j, nas - 1), j < nas, st);
-      lds_sync_wave();  // the diagonal copies' b partials
+      lds_sync_wave();  // the copies' blocks and the diagonal items' b partials
+      for (int j = tid; j - tid < nas; j += kLinLanesWave) copy_rows(S, A, min(j, nas - 1), j < nas);
       rhs_rows(S, A, h3.w, tid);
     }
     st.mark(kPhWrite);  // stamped builds: the rhs (with the final write below)

@@ -217,6 +217,12 @@ struct PlanPart {
 
 }  // namespace
 
+#ifndef VO_BA_COPY_CHAIN
+#define VO_BA_COPY_CHAIN 21
+#endif
+constexpr int kCopyChain = VO_BA_COPY_CHAIN;  // one-wave K1: weighted chain below which no copy is made
+constexpr int kWaveItems = 60;                 // its lanes for slot copies (the combine's LDS scratch)
+
 int seg_obs_for(int64_t n_obs, int target_segments) {
   const int64_t t = std::max(1, target_segments);
   return (int)std::max<int64_t>(1, std::min<int64_t>((n_obs + t - 1) / t, 1 << 30));
@@ -572,46 +578,6 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       R.chunk_fte.back() += k;
       R.chunk_fobs.back() += fobs;
     }
-#ifndef VO_BA_COPY_CHAIN
-#define VO_BA_COPY_CHAIN 21
-#endif
-    constexpr int kCopyChain = VO_BA_COPY_CHAIN;  // weighted chain below which no copy is made
-    // One-wave K1, segments of one chunk: a lane sums one window slot's block, so the slots of
-    // longest pair chains are split into copies of the same block (consecutive pair ranges,
-    // each its own slab row; K2 sums every row of a block) while the lanes last: a copy for
-    // the slot whose per-lane chain (pairs / copies, a diagonal slot's pair weighted 5 against
-    // 3 for its U and b) is longest, until 64 lanes or a chain of kCopyChain (each copy is one
-    // more slab row for K1 to write and K2 to read).
-    if (wave)
-      for (size_t k = 0; k < R.segs.size(); ++k) {
-        PlanSeg& sg = R.segs[k];
-        const int nch = (k + 1 < R.segs.size() ? R.segs[k + 1].chunk0 : (int)R.chunk_q.size()) - sg.chunk0;
-        const int n = (int)sg.slots.size();
-        if (nch != 1 || n == 0) continue;
-        int cp[kSegSlots];
-        auto wgt = [&](int i) { return sg.slots[i].first == sg.slots[i].second ? 5 : 3; };
-        auto chain = [&](int i) { return (sg.slot_cnt[i] + cp[i] - 1) / cp[i] * wgt(i); };
-        // each slot's fewest copies for a chain within kCopyChain (what the greedy below reaches
-        // while the lanes last), the greedy itself only when they do not
-        int lanes = 0;
-        for (int i = 0; i < n; ++i) {
-          const int per = std::max(1, kCopyChain / wgt(i));  // pairs per copy
-          cp[i] = std::max(1, (sg.slot_cnt[i] + per - 1) / per);
-          lanes += cp[i];
-        }
-        if (lanes > std::min(kLinLanesWave, kSegSlots)) {
-          for (int i = 0; i < n; ++i) cp[i] = 1;
-          for (lanes = n; lanes < std::min(kLinLanesWave, kSegSlots); ++lanes) {
-            int best = 0;
-            for (int i = 1; i < n; ++i)
-              if (chain(i) > chain(best)) best = i;
-            if (chain(best) <= kCopyChain) break;
-            ++cp[best];
-          }
-        }
-        for (int i = 0; i < n; ++i)
-          for (int c = 1; c < cp[i]; ++c) sg.slots.push_back(sg.slots[i]);
-      }
   };
   run_parallel(std::min(nparts, nthr), [&](int t) {
     const int nt = std::min(nparts, nthr);
@@ -860,15 +826,6 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         int32_t* sp = &P.slot_ptr[P.chunk_slot_base[ch]];
         for (int sl = 0; sl <= ns; ++sl) sp[sl] = pbase + cnt[sl];
         for (int e = 0; e < npair; ++e) P.pair_list[pbase + cnt[pslot[e]]++] = ptmp[e];
-        // copies of a slot (equal (i, j), adjacent after the sort): its pairs, counted to the
-        // first, in consecutive ranges of near-equal length
-        for (int a = 0; a < ns;) {
-          int b = a + 1;
-          while (b < ns && s.slots[b] == s.slots[a]) ++b;
-          const int32_t lo = sp[a], n = sp[b] - sp[a];
-          for (int c = a + 1; c < b; ++c) sp[c] = lo + (int32_t)((int64_t)n * (c - a) / (b - a));
-          a = b;
-        }
         // camera lists: track entries and observations by window camera, in order
         std::fill(cnt, cnt + nc + 1, 0);
         std::fill(cnt2, cnt2 + nc + 1, 0);
@@ -938,6 +895,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
             }
           int ord[kSegSlots];
           for (int i = 0; i < nas; ++i) ord[i] = i;
+          int base = 0;
           if (!wave) {
             int used = nas;
             for (;;) {
@@ -954,17 +912,57 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
               ++lg[best];
             }
             std::stable_sort(ord, ord + nas, [&](int a, int b) { return lg[a] > lg[b]; });
-          }
-          int base = 0;
-          for (int j = 0; j < nas; ++j) {
-            const int i = ord[j];
-            g.aslot[j] = (uint8_t)sl[i];
-            g.slotp[j] = P.slot_ptr[sb + sl[i]] - e0;
-            g.apcnt[j] = (uint16_t)cntp[i];
-            g.anp[j] = (uint8_t)lg[i];
-            g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
-            g.abase[j] = (uint16_t)base;
-            base += wave ? 1 : 6 << lg[i];
+            for (int j = 0; j < nas; ++j) {
+              const int i = ord[j];
+              g.aslot[j] = (uint8_t)sl[i];
+              g.slotp[j] = P.slot_ptr[sb + sl[i]] - e0;
+              g.apcnt[j] = (uint16_t)cntp[i];
+              g.anp[j] = (uint8_t)lg[i];
+              g.acopy[j] = 0;
+              g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
+              g.abase[j] = (uint16_t)base;
+              base += 6 << lg[i];
+            }
+          } else {
+            // One-wave K1: an item is a copy of an active slot on one lane (the block over a
+            // consecutive range of the slot's pairs); each slot gets the fewest copies that bring
+            // its per-lane chain (pairs per copy, a diagonal pair weighted 5 against 3 for its U
+            // and b) within kCopyChain, or, past kWaveItems lanes, copies go one at a time to the
+            // slot of longest chain.  The copies' blocks are summed in copy order inside K1 (one
+            // slab row per window slot).
+            int cp[kSegSlots];
+            auto wgt = [&](int i) { return P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? 5 : 3; };
+            auto chain = [&](int i) { return (cntp[i] + cp[i] - 1) / cp[i] * wgt(i); };
+            int lanes = 0;
+            for (int i = 0; i < nas; ++i) {
+              const int per = std::max(1, kCopyChain / wgt(i));
+              cp[i] = std::max(1, (cntp[i] + per - 1) / per);
+              lanes += cp[i];
+            }
+            if (lanes > kWaveItems) {
+              for (int i = 0; i < nas; ++i) cp[i] = 1;
+              for (lanes = nas; lanes < kWaveItems; ++lanes) {
+                int best = 0;
+                for (int i = 1; i < nas; ++i)
+                  if (chain(i) > chain(best)) best = i;
+                if (chain(best) <= kCopyChain || cntp[best] <= cp[best]) break;
+                ++cp[best];
+              }
+            }
+            int j = 0;
+            for (int i = 0; i < nas; ++i)
+              for (int c = 0; c < cp[i]; ++c, ++j) {
+                const int lo = (int)((int64_t)cntp[i] * c / cp[i]), hi = (int)((int64_t)cntp[i] * (c + 1) / cp[i]);
+                g.aslot[j] = (uint8_t)sl[i];
+                g.slotp[j] = (uint16_t)(P.slot_ptr[sb + sl[i]] - e0 + lo);
+                g.apcnt[j] = (uint16_t)(hi - lo);
+                g.anp[j] = (uint8_t)cp[i];   // copies of the slot
+                g.acopy[j] = (uint8_t)c;     // this item's copy index
+                g.adcam[j] = P.slot_i[so + sl[i]] == P.slot_j[so + sl[i]] ? (uint8_t)lcam_of(P.slot_i[so + sl[i]]) : 0xFF;
+                g.abase[j] = (uint16_t)j;
+              }
+            nas = j;
+            base = j;
           }
           g.abase[nas] = (uint16_t)base;
           g.slotp[nas] = e1 - e0;

@@ -99,13 +99,15 @@ struct alignas(16) ChunkImg {
   // Schur-pair lanes.  Four-wave K1: active slot i (ordered by lanes per item descending) sums
   // its apcnt[i] pairs from slotp[i] on 6 << anp[i] lanes starting at abase[i] (2^anp lanes per
   // row, their strided partial sums combined by an aligned butterfly).  One-wave K1: lane i sums
-  // active slot i's whole block (abase[i] = i, anp[i] = 0; a heavy slot's pairs are split over
-  // copies of the slot, each with its own slab row), a diagonal slot's lanes adding U over their
-  // pairs' observations.  abase[nas] = lanes used
+  // item i's whole block over its apcnt[i] pairs from slotp[i] (abase[i] = i); the items of a
+  // slot are its anp[i] copies (acopy[i] = 0 .. anp[i] - 1, consecutive ranges of the slot's
+  // pairs, consecutive items), summed in copy order inside K1; a diagonal slot's items add U
+  // over their pairs' observations.  abase[nas] = lanes used
   uint16_t apcnt[kSegSlots];
   uint16_t abase[kSegSlots + 1];  // up to 6 x 64 lanes (two passes of the workgroup)
   uint8_t anp[kSegSlots];
   uint8_t adcam[kSegSlots];        // active slot i -> window camera if diagonal, else 0xFF
+  uint8_t acopy[kSegSlots];        // one-wave K1: item i's copy index (anp[i] = the slot's copies)
   uint8_t cdiag0[kSegCams];        // one-wave K1: active camera i -> its first diagonal item
   uint8_t cdiagn[kSegCams];        //   and the number of copies (consecutive items)
   alignas(2) uint16_t pairs[kChunkPairs];  // (te_x | te_y << 8) by slot
