@@ -995,13 +995,19 @@ __device__ __forceinline__ void copy_rows(const LinWave& S, const LinArgs& A, in
   const int m = S.img.anp[si];
   if (!live || m <= 1) return;
   const int k = S.img.acopy[si], j0 = si - k;
-  const double* sc = &S.Jc[0][0];
-  double* row = &A.slab[36l * S.spos[S.img.aslot[si]]];
-  for (int e = 36 * k / m; e < 36 * (k + 1) / m; ++e) {
-    double acc = sc[36 * j0 + e];
-    for (int c = 1; c < m; ++c) acc += sc[36 * (j0 + c) + e];
-    row[e] = acc;
+  const int e0 = 36 * k / m, ne = 36 * (k + 1) / m - e0;  // <= 18 entries (m >= 2)
+  const double* sc = &S.Jc[0][0] + 36 * j0 + e0;
+  double acc[18];
+#pragma unroll
+  for (int i = 0; i < 18; ++i) acc[i] = sc[min(i, ne - 1)];  // every load of a copy in flight
+  for (int c = 1; c < m; ++c) {
+#pragma unroll
+    for (int i = 0; i < 18; ++i) acc[i] += sc[36 * c + min(i, ne - 1)];
   }
+  double* row = &A.slab[36l * S.spos[S.img.aslot[si]] + e0];
+#pragma unroll
+  for (int i = 0; i < 18; ++i)
+    if (i < ne) row[i] = acc[i];
 }
 
 // The rhs of the chunk's window cameras (one-wave K1): lane (active camera ci, row a) adds row a
