@@ -1,8 +1,12 @@
 #!/bin/bash
-# BA kernel build variants (visualodometry_amd/lib/var_<name>): BA bench line each (no parity).
+# BA build variants (VO_LIB_PATH, built beside the product by make EXTRA=...): cfg3 bench lines
+# without the matcher, the default first and last.
 set -euo pipefail
-mkdir -p gpurun_out
-for v in "$@"; do
-  VO_LIB_PATH=$PWD/visualodometry_amd/lib/var_$v/libvo_hip.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-matcher --steps 100 > gpurun_out/bv_$v.json 2> gpurun_out/bv_$v.err || echo "variant $v failed"
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+for v in default "$@" default2; do
+  case $v in default|default2) L=visualodometry_amd/lib/libvo_hip.so ;; *) L=visualodometry_amd/lib/libvo_hip_$v.so ;; esac
+  VO_LIB_PATH=$L timeout -k 10 200 python bench.py --no-matcher --no-cpu-baseline --steps 300 --warmup 30 > $OUT/var_bench_$v.json 2> $OUT/var_bench_$v.err
 done
-echo ok
+echo done
