@@ -47,10 +47,20 @@ raw = np.zeros(nseg * NPH, dtype=np.uint64)
 k = ctx.lib.vo_ba_debug_stamps(ctx.handle, raw.ctypes.data_as(_lib.C.POINTER(_lib.C.c_uint64)), -raw.size)
 if k > 0:
     r = raw[:k].reshape(-1, NPH).astype(np.int64)
+    xcc = r[:, 15] >> 24  # the stamping lane's XCD (s_memtime counts per XCD)
+    r[:, 15] &= 0xFFFFFF
     t0, t1 = r[:, 8], r[:, 9]
-    base = t0.min()
     dur = t1 - t0
-    print(f"K1 workgroups: {len(r)}  start spread {t0.max() - base} cyc  end of last {t1.max() - base} cyc")
+    t0 = t0.copy()
+    t1 = t1.copy()
+    for x in np.unique(xcc):  # times relative to each XCD's first start
+        m = xcc == x
+        b = t0[m].min()
+        t0[m] -= b
+        t1[m] -= b
+    base = 0
+    print(f"K1 workgroups: {len(r)} over {len(np.unique(xcc))} XCDs; per XCD (start spread, end of last) cyc:",
+          [(int(t0[xcc == x].max()), int(t1[xcc == x].max())) for x in np.unique(xcc)])
     print(f"  duration min/median/p90/max: {dur.min()} {int(np.median(dur))} {int(np.percentile(dur, 90))} {dur.max()}")
     order = np.argsort(t0)
     print("  first 5 starts", (t0[order[:5]] - base).tolist(), " last 5 starts", (t0[order[-5:]] - base).tolist())

@@ -180,6 +180,7 @@ struct LinArgs {
   const double* dc;        // pending pose update (6 per free camera)
   const int* status;
   unsigned long long* stamps;  // diagnostic build only: per segment phase cycles
+  int nseg;                    // segments (the one-wave K1's last workgroup may hold spare waves)
 };
 
 struct alignas(16) LinShared {
@@ -486,24 +487,37 @@ enum { kPhLoad = 0, kPhBacksub, kPhLinObs, kPhReduce, kPhElim, kPhSchur, kPhWrit
        kPhObs, kPhTe, kPhPts, kPhPairs, kPhSlots, kPhCams, kPhCount };
 template <bool kStamp>
 struct Stamper {
+  // the stamping lane (thread 0, or lane 0 of each one-wave segment) and its output row;
+  // s_memtime counts per XCD (clocks of different XCDs are unrelated), so the row's
+  // window-camera count carries the XCD id in bits 24..31
   unsigned long long t = 0, acc[kPhCount] = {};
-  __device__ __forceinline__ void start() {
-    if (kStamp && threadIdx.x == 0) acc[kPhT0] = t = __builtin_amdgcn_s_memtime();
+  bool lead = false;
+  int row = 0;
+  __device__ __forceinline__ void start(bool ld, int r) {
+    lead = kStamp && ld;
+    row = r;
+    if (lead) {
+      acc[kPhT0] = t = __builtin_amdgcn_s_memtime();
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+      acc[kPhCams] = (unsigned long long)xcc << 24;
+    }
   }
+  __device__ __forceinline__ void start() { start(threadIdx.x == 0, blockIdx.x); }
   __device__ __forceinline__ void mark(int ph) {
-    if (kStamp && threadIdx.x == 0) {
+    if (lead) {
       const unsigned long long n = __builtin_amdgcn_s_memtime();
       acc[ph] += n - t;
       t = n;
     }
   }
   __device__ __forceinline__ void count(int k, int v) {
-    if (kStamp && threadIdx.x == 0) acc[k] += (unsigned long long)v;
+    if (lead) acc[k] += (unsigned long long)v;
   }
   __device__ __forceinline__ void flush(unsigned long long* out) {
-    if (kStamp && threadIdx.x == 0) acc[kPhT1] = __builtin_amdgcn_s_memtime();  // absolute
-    if (kStamp && threadIdx.x == 0 && out)
-      for (int k = 0; k < kPhCount; ++k) out[blockIdx.x * kPhCount + k] = acc[k];
+    if (lead) acc[kPhT1] = __builtin_amdgcn_s_memtime();  // absolute
+    if (lead && out)
+      for (int k = 0; k < kPhCount; ++k) out[(long)row * kPhCount + k] = acc[k];
   }
 };
 
@@ -939,27 +953,44 @@ __device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si
     if (j < n) accum(zxA, zyA);
   }
   st.mark(kPhSchur);  // stamped builds: the pair sums
+  // a diagonal item: U over its pairs' observations (camol entries [auo[si], auo[si + 1]), in
+  // observation order, observation i + 1's Jc fetched while i accumulates) and its share of
+  // b over its pairs (track entry x's bt row)
   double ob[6] = {0, 0, 0, 0, 0, 0};
-  if (n > 0) {
-    if (dcam != 0xFF) {
-      for (int e = e0; e < e0 + n; ++e) {
-        const int x = S.img.pairs[e] & 255;
-        const double2* br = reinterpret_cast<const double2*>(S.bt[x]);
+  const int u0 = S.img.auo[si], un = live ? S.img.auo[si + 1] - u0 : 0;
+  if (un > 0) {
+    auto uacc = [&](const double (&jj)[12]) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const double2 v = br[k];
-          ob[2 * k] += v.x;
-          ob[2 * k + 1] += v.y;
-        }
-        for (int o = S.img.te_obs[x]; o < S.img.te_obs[x + 1]; ++o) {
-          double jj[12];
-          jc_load(S, o, jj);
+      for (int i = 0; i < 6; ++i)
 #pragma unroll
-          for (int i = 0; i < 6; ++i)
+        for (int c = 0; c < 6; ++c)
+          out[6 * i + c] = __builtin_fma(jj[6 + i], jj[6 + c], __builtin_fma(jj[i], jj[c], out[6 * i + c]));
+    };
+    auto oid = [&](int i) { return (int)S.img.camol[u0 + min(i, un - 1)]; };
+    double jA[12], jB[12];
+    jc_load(S, oid(0), jA);
+    int on = oid(1);
+    int i = 0;
+    for (; i + 2 <= un; i += 2) {
+      jc_load(S, on, jB);
+      on = oid(i + 2);
+      uacc(jA);
+      jc_load(S, on, jA);
+      on = oid(i + 3);
+      uacc(jB);
+    }
+    if (i < un) uacc(jA);
+  }
+  if (n > 0 && dcam != 0xFF) {
+    int xn = S.img.pairs[e0] & 255;
+    for (int e = 0; e < n; ++e) {
+      const double2* br = reinterpret_cast<const double2*>(S.bt[xn]);
+      xn = S.img.pairs[e0 + min(e + 1, n - 1)] & 255;
 #pragma unroll
-            for (int c = 0; c < 6; ++c)
-              out[6 * i + c] = __builtin_fma(jj[6 + i], jj[6 + c], __builtin_fma(jj[i], jj[c], out[6 * i + c]));
-        }
+      for (int k = 0; k < 3; ++k) {
+        const double2 v = br[k];
+        ob[2 * k] += v.x;
+        ob[2 * k + 1] += v.y;
       }
     }
   }
@@ -1028,14 +1059,18 @@ __device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int
   }
 }
 
-// The one-wave K1: segment = chunk = workgroup of one wave (the plan's seg_obs == 1).
-template <int MODE, bool kStamp>
-__global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
-  __shared__ LinWave S;
+// The one-wave K1: segment = chunk = one wave (the plan's seg_obs == 1); a workgroup holds
+// NW such waves, each on its own LDS image and never waiting on another (no barrier).
+template <int MODE, bool kStamp, int NW>
+__global__ __launch_bounds__(kLinLanesWave * NW) void ba_lin_wave_kernel(LinArgs A) {
+  __shared__ LinWave Sw[NW];
   static_assert(kLinLanesWave == 64, "one wave");
+  const int wv = NW > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+  LinWave& S = Sw[wv];
+  const int seg = blockIdx.x * NW + wv, tid = threadIdx.x & 63;
+  if (NW > 1 && seg >= A.nseg) return;  // the last workgroup's spare waves (no barrier follows)
   Stamper<kStamp> st;
-  st.start();
-  const int seg = blockIdx.x, tid = threadIdx.x;
+  st.start(tid == 0, seg);
   // level 1: status, segment header (uniform), this lane's camera ids (fixed header offsets)
   // and the chunk's image (chunk = segment)
   const int* SH = A.seg_hdr + (long)kSegHdr * seg;
@@ -2141,7 +2176,9 @@ class BAEngine {
     // one-wave K1 for plans of one chunk per segment (the chunk image of segment s is chunk s)
     const bool wave = plan_is_wave(plan_.seg_obs);
     VO_REQUIRE(!wave || nseg == plan_.n_chunks(), VO_ERR_STATE, "K1: segments of one chunk expected");
-    dim3 g(nseg), b(wave ? kLinLanesWave : kLinThreads);
+    A.nseg = nseg;
+    const int nw = wave && !stamps_on_ ? k1_waves_ : 1;
+    dim3 g((nseg + nw - 1) / nw), b(wave ? kLinLanesWave * nw : kLinThreads);
     ctx_->prof.begin(ctx_->stream, kKBaLin);
     if (stamps_on_) {
       d_stamps_.reserve((size_t)nseg * kPhCount * 8);
@@ -2150,9 +2187,15 @@ class BAEngine {
 #define VO_LIN_LAUNCH(M)                                                               \
   do {                                                                                 \
     if (wave && stamps_on_)                                                            \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true>), g, b, 0, ctx_->stream, A);     \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true, 1>), g, b, 0, ctx_->stream, A);  \
+    else if (wave && nw == 2)                                                          \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, 2>), g, b, 0, ctx_->stream, A); \
+    else if (wave && nw == 3)                                                          \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, 3>), g, b, 0, ctx_->stream, A); \
+    else if (wave && nw == 6)                                                          \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, 6>), g, b, 0, ctx_->stream, A); \
     else if (wave)                                                                     \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false>), g, b, 0, ctx_->stream, A);    \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, 1>), g, b, 0, ctx_->stream, A); \
     else if (stamps_on_)                                                               \
       hipLaunchKernelGGL((ba_lin_kernel<M, true>), g, b, 0, ctx_->stream, A);          \
     else                                                                               \
@@ -2357,6 +2400,12 @@ class BAEngine {
   DevBuf d_chunk_img_prev_;  // the previous plan's images (prev_plan_)  // K1's plan (the chunk images hold every list)
   DevBuf d_stamps_, d_stamps3_;
   static constexpr bool stamps_on_ = kBaStamps;
+  // one-wave K1: segments (waves) per workgroup, 1, 2, 3 or 6 (VO_BA_K1_WAVES)
+  const int k1_waves_ = [] {
+    const char* e = std::getenv("VO_BA_K1_WAVES");
+    const int v = e ? std::atoi(e) : 1;
+    return v == 2 || v == 3 || v == 6 ? v : 1;
+  }();
 
  public:
   // Diagnostic: per-phase cycle sums of the last K1 launch (VO_BA_STAMPS=1 builds).
