@@ -13,3 +13,9 @@ for nw in 1 2 3 6 1; do
 done
 VO_LIB_PATH=visualodometry_amd/lib/libvo_hip_stamps.so timeout -k 10 120 python tools/ba_phase_stamps.py cfg3 > $OUT/k1nw_stamps_cfg3.txt 2>&1
 echo done
+# cfg4 on the one-wave K1 (nine rounds of one-chunk segments) against the four-wave default
+VO_BA_WAVE=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_ba.py -x -q --timeout 200 --timeout-method thread -k "cfg4" > $OUT/k1nw_cfg4wave_tests.log 2>&1
+for w in 1 0; do
+  VO_BA_WAVE=$w timeout -k 10 200 python bench.py --config cfg4 --no-matcher --no-cpu-baseline --steps 50 --warmup 5 > $OUT/k1nw_cfg4_wave$w.json 2> $OUT/k1nw_cfg4_wave$w.err
+done
+echo done2

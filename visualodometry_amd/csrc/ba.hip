@@ -1031,10 +1031,20 @@ __device__ __forceinline__ void copy_rows(const LinWave& S, const LinArgs& A, in
   double acc[18];
 #pragma unroll
   for (int i = 0; i < 18; ++i) acc[i] = sc[min(i, ne - 1)];  // every load of a copy in flight
-  for (int c = 1; c < m; ++c) {
+  int c = 1;
+  for (; c + 2 <= m; c += 2) {  // two copies' loads in flight, added in copy order
+    double v[18], u[18];
+#pragma unroll
+    for (int i = 0; i < 18; ++i) {
+      v[i] = sc[36 * c + min(i, ne - 1)];
+      u[i] = sc[36 * (c + 1) + min(i, ne - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < 18; ++i) acc[i] = (acc[i] + v[i]) + u[i];
+  }
+  if (c < m)
 #pragma unroll
     for (int i = 0; i < 18; ++i) acc[i] += sc[36 * c + min(i, ne - 1)];
-  }
   double* row = &A.slab[36l * S.spos[S.img.aslot[si]] + e0];
 #pragma unroll
   for (int i = 0; i < 18; ++i)
@@ -1054,7 +1064,14 @@ __device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int
     const int ci = q / 6, a = q - 6 * ci;
     const int j0 = S.img.cdiag0[ci], nj = S.img.cdiagn[ci];
     double acc = 0.0;
-    for (int j = 0; j < nj; ++j) acc += bp[6 * (j0 + j) + a];
+    for (int j = 0; j < nj; j += 8) {  // eight partials' loads in flight, added in item order
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = bp[6 * (j0 + min(j + k, nj - 1)) + a];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (j + k < nj) acc += v[k];
+    }
     A.slab_b[6l * S.cpos[S.img.acid[ci]] + a] = acc;
   }
 }
@@ -1784,7 +1801,13 @@ class BAEngine {
     if (err.empty()) {
       // one-wave K1 (segments of one chunk) while the window's chunks fit one round of six
       // one-wave workgroups per CU; the four-wave K1 over multi-chunk segments beyond
-      bool wave = (int64_t)prob->n_obs <= (int64_t)kWaveObsPerCu * std::max(1, ctx_->num_cus);
+      // (VO_BA_WAVE=1 / 0: the one-wave / four-wave K1 whatever the size, for measurements)
+      static const int wave_env = [] {
+        const char* e = std::getenv("VO_BA_WAVE");
+        return e ? std::atoi(e) : -1;
+      }();
+      bool wave = wave_env >= 0 ? wave_env == 1
+                                : (int64_t)prob->n_obs <= (int64_t)kWaveObsPerCu * std::max(1, ctx_->num_cus);
       const int ideal = seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave));
       // the packing target stays the previous plan's while it is within 10 % of this window's
       // (a plan can take over groups only from a plan with the same target)
@@ -1796,7 +1819,8 @@ class BAEngine {
       d_chunk_img_.swap(d_chunk_img_prev_);
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
                        prob->obs_uv, so, prev_ok ? &prev_plan_ : nullptr);
-      if (err.empty() && plan_is_wave(plan_.seg_obs) && plan_.n_chunks() > kWaveSegsPerCu * std::max(1, ctx_->num_cus)) {
+      if (err.empty() && wave_env < 0 && plan_is_wave(plan_.seg_obs) &&
+          plan_.n_chunks() > kWaveSegsPerCu * std::max(1, ctx_->num_cus)) {
         wave = false;  // more chunks than one round: the four-wave K1 after all
         err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
                          prob->obs_uv, seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, false)),
