@@ -19,3 +19,5 @@ for w in 1 0; do
   VO_BA_WAVE=$w timeout -k 10 200 python bench.py --config cfg4 --no-matcher --no-cpu-baseline --steps 50 --warmup 5 > $OUT/k1nw_cfg4_wave$w.json 2> $OUT/k1nw_cfg4_wave$w.err
 done
 echo done2
+timeout -k 10 300 python tools/host_call_latency.py > $OUT/k1nw_host_latency.json 2> $OUT/k1nw_host_latency.err
+echo done3
