@@ -180,7 +180,6 @@ struct LinArgs {
   const double* dc;        // pending pose update (6 per free camera)
   const int* status;
   unsigned long long* stamps;  // diagnostic build only: per segment phase cycles
-  int nseg;                    // segments (the one-wave K1's last workgroup may hold spare waves)
 };
 
 struct alignas(16) LinShared {
@@ -487,37 +486,24 @@ enum { kPhLoad = 0, kPhBacksub, kPhLinObs, kPhReduce, kPhElim, kPhSchur, kPhWrit
        kPhObs, kPhTe, kPhPts, kPhPairs, kPhSlots, kPhCams, kPhCount };
 template <bool kStamp>
 struct Stamper {
-  // the stamping lane (thread 0, or lane 0 of each one-wave segment) and its output row;
-  // s_memtime counts per XCD (clocks of different XCDs are unrelated), so the row's
-  // window-camera count carries the XCD id in bits 24..31
   unsigned long long t = 0, acc[kPhCount] = {};
-  bool lead = false;
-  int row = 0;
-  __device__ __forceinline__ void start(bool ld, int r) {
-    lead = kStamp && ld;
-    row = r;
-    if (lead) {
-      acc[kPhT0] = t = __builtin_amdgcn_s_memtime();
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-      acc[kPhCams] = (unsigned long long)xcc << 24;
-    }
+  __device__ __forceinline__ void start() {
+    if (kStamp && threadIdx.x == 0) acc[kPhT0] = t = __builtin_amdgcn_s_memtime();
   }
-  __device__ __forceinline__ void start() { start(threadIdx.x == 0, blockIdx.x); }
   __device__ __forceinline__ void mark(int ph) {
-    if (lead) {
+    if (kStamp && threadIdx.x == 0) {
       const unsigned long long n = __builtin_amdgcn_s_memtime();
       acc[ph] += n - t;
       t = n;
     }
   }
   __device__ __forceinline__ void count(int k, int v) {
-    if (lead) acc[k] += (unsigned long long)v;
+    if (kStamp && threadIdx.x == 0) acc[k] += (unsigned long long)v;
   }
   __device__ __forceinline__ void flush(unsigned long long* out) {
-    if (lead) acc[kPhT1] = __builtin_amdgcn_s_memtime();  // absolute
-    if (lead && out)
-      for (int k = 0; k < kPhCount; ++k) out[(long)row * kPhCount + k] = acc[k];
+    if (kStamp && threadIdx.x == 0) acc[kPhT1] = __builtin_amdgcn_s_memtime();  // absolute
+    if (kStamp && threadIdx.x == 0 && out)
+      for (int k = 0; k < kPhCount; ++k) out[blockIdx.x * kPhCount + k] = acc[k];
   }
 };
 
@@ -953,44 +939,27 @@ __device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si
     if (j < n) accum(zxA, zyA);
   }
   st.mark(kPhSchur);  // stamped builds: the pair sums
-  // a diagonal item: U over its pairs' observations (camol entries [auo[si], auo[si + 1]), in
-  // observation order, observation i + 1's Jc fetched while i accumulates) and its share of
-  // b over its pairs (track entry x's bt row)
   double ob[6] = {0, 0, 0, 0, 0, 0};
-  const int u0 = S.img.auo[si], un = live ? S.img.auo[si + 1] - u0 : 0;
-  if (un > 0) {
-    auto uacc = [&](const double (&jj)[12]) {
+  if (n > 0) {
+    if (dcam != 0xFF) {
+      for (int e = e0; e < e0 + n; ++e) {
+        const int x = S.img.pairs[e] & 255;
+        const double2* br = reinterpret_cast<const double2*>(S.bt[x]);
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
+        for (int k = 0; k < 3; ++k) {
+          const double2 v = br[k];
+          ob[2 * k] += v.x;
+          ob[2 * k + 1] += v.y;
+        }
+        for (int o = S.img.te_obs[x]; o < S.img.te_obs[x + 1]; ++o) {
+          double jj[12];
+          jc_load(S, o, jj);
 #pragma unroll
-        for (int c = 0; c < 6; ++c)
-          out[6 * i + c] = __builtin_fma(jj[6 + i], jj[6 + c], __builtin_fma(jj[i], jj[c], out[6 * i + c]));
-    };
-    auto oid = [&](int i) { return (int)S.img.camol[u0 + min(i, un - 1)]; };
-    double jA[12], jB[12];
-    jc_load(S, oid(0), jA);
-    int on = oid(1);
-    int i = 0;
-    for (; i + 2 <= un; i += 2) {
-      jc_load(S, on, jB);
-      on = oid(i + 2);
-      uacc(jA);
-      jc_load(S, on, jA);
-      on = oid(i + 3);
-      uacc(jB);
-    }
-    if (i < un) uacc(jA);
-  }
-  if (n > 0 && dcam != 0xFF) {
-    int xn = S.img.pairs[e0] & 255;
-    for (int e = 0; e < n; ++e) {
-      const double2* br = reinterpret_cast<const double2*>(S.bt[xn]);
-      xn = S.img.pairs[e0 + min(e + 1, n - 1)] & 255;
+          for (int i = 0; i < 6; ++i)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const double2 v = br[k];
-        ob[2 * k] += v.x;
-        ob[2 * k + 1] += v.y;
+            for (int c = 0; c < 6; ++c)
+              out[6 * i + c] = __builtin_fma(jj[6 + i], jj[6 + c], __builtin_fma(jj[i], jj[c], out[6 * i + c]));
+        }
       }
     }
   }
@@ -1031,20 +1000,10 @@ __device__ __forceinline__ void copy_rows(const LinWave& S, const LinArgs& A, in
   double acc[18];
 #pragma unroll
   for (int i = 0; i < 18; ++i) acc[i] = sc[min(i, ne - 1)];  // every load of a copy in flight
-  int c = 1;
-  for (; c + 2 <= m; c += 2) {  // two copies' loads in flight, added in copy order
-    double v[18], u[18];
-#pragma unroll
-    for (int i = 0; i < 18; ++i) {
-      v[i] = sc[36 * c + min(i, ne - 1)];
-      u[i] = sc[36 * (c + 1) + min(i, ne - 1)];
-    }
-#pragma unroll
-    for (int i = 0; i < 18; ++i) acc[i] = (acc[i] + v[i]) + u[i];
-  }
-  if (c < m)
+  for (int c = 1; c < m; ++c) {
 #pragma unroll
     for (int i = 0; i < 18; ++i) acc[i] += sc[36 * c + min(i, ne - 1)];
+  }
   double* row = &A.slab[36l * S.spos[S.img.aslot[si]] + e0];
 #pragma unroll
   for (int i = 0; i < 18; ++i)
@@ -1064,30 +1023,19 @@ __device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int
     const int ci = q / 6, a = q - 6 * ci;
     const int j0 = S.img.cdiag0[ci], nj = S.img.cdiagn[ci];
     double acc = 0.0;
-    for (int j = 0; j < nj; j += 8) {  // eight partials' loads in flight, added in item order
-      double v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = bp[6 * (j0 + min(j + k, nj - 1)) + a];
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (j + k < nj) acc += v[k];
-    }
+    for (int j = 0; j < nj; ++j) acc += bp[6 * (j0 + j) + a];
     A.slab_b[6l * S.cpos[S.img.acid[ci]] + a] = acc;
   }
 }
 
-// The one-wave K1: segment = chunk = one wave (the plan's seg_obs == 1); a workgroup holds
-// NW such waves, each on its own LDS image and never waiting on another (no barrier).
-template <int MODE, bool kStamp, int NW>
-__global__ __launch_bounds__(kLinLanesWave * NW) void ba_lin_wave_kernel(LinArgs A) {
-  __shared__ LinWave Sw[NW];
+// The one-wave K1: segment = chunk = workgroup of one wave (the plan's seg_obs == 1).
+template <int MODE, bool kStamp>
+__global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
+  __shared__ LinWave S;
   static_assert(kLinLanesWave == 64, "one wave");
-  const int wv = NW > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
-  LinWave& S = Sw[wv];
-  const int seg = blockIdx.x * NW + wv, tid = threadIdx.x & 63;
-  if (NW > 1 && seg >= A.nseg) return;  // the last workgroup's spare waves (no barrier follows)
   Stamper<kStamp> st;
-  st.start(tid == 0, seg);
+  st.start();
+  const int seg = blockIdx.x, tid = threadIdx.x;
   // level 1: status, segment header (uniform), this lane's camera ids (fixed header offsets)
   // and the chunk's image (chunk = segment)
   const int* SH = A.seg_hdr + (long)kSegHdr * seg;
@@ -1801,13 +1749,7 @@ class BAEngine {
     if (err.empty()) {
       // one-wave K1 (segments of one chunk) while the window's chunks fit one round of six
       // one-wave workgroups per CU; the four-wave K1 over multi-chunk segments beyond
-      // (VO_BA_WAVE=1 / 0: the one-wave / four-wave K1 whatever the size, for measurements)
-      static const int wave_env = [] {
-        const char* e = std::getenv("VO_BA_WAVE");
-        return e ? std::atoi(e) : -1;
-      }();
-      bool wave = wave_env >= 0 ? wave_env == 1
-                                : (int64_t)prob->n_obs <= (int64_t)kWaveObsPerCu * std::max(1, ctx_->num_cus);
+      bool wave = (int64_t)prob->n_obs <= (int64_t)kWaveObsPerCu * std::max(1, ctx_->num_cus);
       const int ideal = seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave));
       // the packing target stays the previous plan's while it is within 10 % of this window's
       // (a plan can take over groups only from a plan with the same target)
@@ -1819,8 +1761,7 @@ class BAEngine {
       d_chunk_img_.swap(d_chunk_img_prev_);
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
                        prob->obs_uv, so, prev_ok ? &prev_plan_ : nullptr);
-      if (err.empty() && wave_env < 0 && plan_is_wave(plan_.seg_obs) &&
-          plan_.n_chunks() > kWaveSegsPerCu * std::max(1, ctx_->num_cus)) {
+      if (err.empty() && plan_is_wave(plan_.seg_obs) && plan_.n_chunks() > kWaveSegsPerCu * std::max(1, ctx_->num_cus)) {
         wave = false;  // more chunks than one round: the four-wave K1 after all
         err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
                          prob->obs_uv, seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, false)),
@@ -2200,9 +2141,7 @@ class BAEngine {
     // one-wave K1 for plans of one chunk per segment (the chunk image of segment s is chunk s)
     const bool wave = plan_is_wave(plan_.seg_obs);
     VO_REQUIRE(!wave || nseg == plan_.n_chunks(), VO_ERR_STATE, "K1: segments of one chunk expected");
-    A.nseg = nseg;
-    const int nw = wave && !stamps_on_ ? k1_waves_ : 1;
-    dim3 g((nseg + nw - 1) / nw), b(wave ? kLinLanesWave * nw : kLinThreads);
+    dim3 g(nseg), b(wave ? kLinLanesWave : kLinThreads);
     ctx_->prof.begin(ctx_->stream, kKBaLin);
     if (stamps_on_) {
       d_stamps_.reserve((size_t)nseg * kPhCount * 8);
@@ -2211,15 +2150,9 @@ class BAEngine {
 #define VO_LIN_LAUNCH(M)                                                               \
   do {                                                                                 \
     if (wave && stamps_on_)                                                            \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true, 1>), g, b, 0, ctx_->stream, A);  \
-    else if (wave && nw == 2)                                                          \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, 2>), g, b, 0, ctx_->stream, A); \
-    else if (wave && nw == 3)                                                          \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, 3>), g, b, 0, ctx_->stream, A); \
-    else if (wave && nw == 6)                                                          \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, 6>), g, b, 0, ctx_->stream, A); \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true>), g, b, 0, ctx_->stream, A);     \
     else if (wave)                                                                     \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false, 1>), g, b, 0, ctx_->stream, A); \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false>), g, b, 0, ctx_->stream, A);    \
     else if (stamps_on_)                                                               \
       hipLaunchKernelGGL((ba_lin_kernel<M, true>), g, b, 0, ctx_->stream, A);          \
     else                                                                               \
@@ -2424,12 +2357,6 @@ class BAEngine {
   DevBuf d_chunk_img_prev_;  // the previous plan's images (prev_plan_)  // K1's plan (the chunk images hold every list)
   DevBuf d_stamps_, d_stamps3_;
   static constexpr bool stamps_on_ = kBaStamps;
-  // one-wave K1: segments (waves) per workgroup, 1, 2, 3 or 6 (VO_BA_K1_WAVES)
-  const int k1_waves_ = [] {
-    const char* e = std::getenv("VO_BA_K1_WAVES");
-    const int v = e ? std::atoi(e) : 1;
-    return v == 2 || v == 3 || v == 6 ? v : 1;
-  }();
 
  public:
   // Diagnostic: per-phase cycle sums of the last K1 launch (VO_BA_STAMPS=1 builds).
