@@ -138,6 +138,28 @@ def cpu_baseline_ba(p, lam: float, budget_s: float = 3.0):
                       f"window: {n} GN iterations in {dt:.2f} s; {note}"}
 
 
+def ba_parity_guard(sess, p, pts, p0: int, p1: int, lam: float, iters: int = 2, tol: float = 1e-5) -> dict:
+    """Untimed check of the timed build: reset the session to the window's start state, run
+    ``iters`` GN iterations and compare costs, poses and this rank's landmarks with the C
+    oracle (oracle/ba_ref.c) on the whole window, relative max-norm error <= ``tol``
+    (north_star's 1e-5).  On N ranks every rank runs the collective iterations and checks its
+    own landmark shard."""
+    from oracle import cref
+    from visualodometry_amd import _lib
+
+    def rel(a, b):
+        return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+    sess.set_state(p.poses_cw, pts)
+    rc, costs = sess.run(iters)
+    P, X = sess.get_state()
+    R = cref.BAProblemRef(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, lam)
+    _, Pr, Xr, cr = R.solve(p.poses_cw, p.points, iters, nthreads=host_cores())
+    err = {"cost": rel(np.asarray(costs), np.asarray(cr)), "poses": rel(P, Pr), "points": rel(X, Xr[p0:p1])}
+    ok = rc == _lib.VO_OK and all(np.isfinite(v) and v <= tol for v in err.values())
+    return {"ok": bool(ok), "iters": iters, "tol": tol, "rel_err": err, "checker": "oracle/ba_ref.c"}
+
+
 def bench_matcher(ctx, batch: int = 16, n: int = 4000, calls: int = 20, warmup: int = 3, traffic_path=None):
     from visualodometry_amd import _lib, matcher
     from visualodometry_amd.synthetic import sift_like_pair
@@ -580,6 +602,12 @@ def main() -> int:
     if rc != _lib.VO_OK or not np.all(np.isfinite(costs)):
         print(f"error: BA status {rc}, costs {costs}", file=sys.stderr)
         return 1
+    # parity guard (not timed): the same build from the window's start state, 2 iterations,
+    # against the C oracle at the north-star tolerance -- a wrong-result build prints no number
+    guard = ba_parity_guard(sess, p, pts, p0, p1, args.lam)
+    if not guard["ok"]:
+        print(f"error: BA parity guard failed: {guard}", file=sys.stderr)
+        return 1
 
     value = args.steps / dt
     n_free = p.n_poses - p.n_fixed
@@ -635,6 +663,7 @@ def main() -> int:
                             "unit": "GB/s", "frac": lin_bytes / lin_avg / 1e9 / HBM_PEAK_GBS,
                             "bytes_per_launch": lin_bytes},
         "algorithmic_bytes_per_iter": stats["algorithmic_bytes_per_iter"],
+        "parity_guard": guard,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_ba(p, args.lam)

@@ -68,12 +68,14 @@ def test_run_matches_c_oracle(ctx, cfg):
 
 def test_cfg4_matches_c_oracle(ctx):
     """100 poses x 200k landmarks: the profile (225 KB) exceeds LDS; the banded K3 streams
-    it through its LDS rings."""
+    it through its LDS rings.  K1 is the default one-wave K1 (one chunk per segment: 13.7k
+    workgroups, nine rounds)."""
     p = make_ba_config("cfg4")
     s = _session(p, ctx)
     st = s.plan_stats()
     assert st["profile_blocks"] * 288 > 150 * 1024
     assert st["band_solver"] == 1
+    assert st["seg_obs"] == 1 and st["segments"] == st["chunks"], st
     rc, costs = s.run(3)
     assert rc == _lib.VO_OK
     R = cref.BAProblemRef(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 1.0)
@@ -81,6 +83,34 @@ def test_cfg4_matches_c_oracle(ctx):
     np.testing.assert_allclose(costs, cr, rtol=REL)
     P, X = s.get_state()
     assert _rel(P, Pr) < REL and _rel(X, Xr) < REL
+
+
+@pytest.mark.parametrize("cfg", ["cfg3", "cfg4"])
+def test_four_wave_k1_matches_c_oracle(ctx, cfg):
+    """The four-wave K1 (multi-chunk segments, one 256-lane workgroup walking them; reached
+    through the testing switch vo_ba_testing_k1_four_wave) against the C oracle, and against the
+    default one-wave K1 to rounding (the summation order differs)."""
+    p = make_ba_config(cfg)
+    iters = 3
+    R = cref.BAProblemRef(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 1.0)
+    n, Pr, Xr, cr = R.solve(p.poses_cw, p.points, iters, nthreads=8)
+    out = []
+    for four in (True, False):
+        _lib.ba_testing_k1_four_wave(ctx, four)
+        try:
+            s = _session(p, ctx)
+            st = s.plan_stats()
+            assert (st["seg_obs"] > 1 and st["segments"] < st["chunks"]) == four, st
+            rc, costs = s.run(iters)
+            assert rc == _lib.VO_OK
+            P, X = s.get_state()
+        finally:
+            _lib.ba_testing_k1_four_wave(ctx, False)
+        np.testing.assert_allclose(costs, cr, rtol=REL)
+        assert _rel(P, Pr) < REL and _rel(X, Xr) < REL
+        out.append((costs, P, X))
+    assert _rel(out[0][0], out[1][0]) < 1e-9
+    assert _rel(out[0][1], out[1][1]) < 1e-8
 
 
 def test_deterministic_bitwise(ctx):
@@ -385,34 +415,43 @@ def test_two_sessions_on_one_context(ctx):
         s2.get_state()
 
 
-def test_slide_takes_groups_over_and_matches_scratch(ctx):
+@pytest.mark.parametrize("cfg,four", [("cfg3", False), ("cfg4", False), ("cfg4", True)])
+def test_slide_takes_groups_over_and_matches_scratch(ctx, cfg, four):
     """Consecutive keyframe windows on one context: each vo_ba_setup takes the unchanged
     first-camera groups of the previous window's plan over (chunk images copied on the
     device, not rebuilt or uploaded), and every result is bitwise the one of a setup from
-    scratch (an unrelated window set up in between), which also matches the C oracle."""
+    scratch (an unrelated window set up in between), which also matches the C oracle.  cfg4
+    on both K1 variants: the four-wave K1's multi-chunk segments (with its repacking to one
+    round) take groups over too, and its packing target depends on the window alone (ADVICE
+    r4), so the slid plan is the scratch plan."""
     from visualodometry_amd.synthetic import make_ba_slide
 
-    ws = make_ba_slide("cfg3", 3)
+    ws = make_ba_slide(cfg, 3)
     other = make_ba_problem(8, 200, 11)
-    iters = 3
+    iters = 2
     inc = []
-    for i, w in enumerate(ws):
-        s = _session(w, ctx)
-        st = s.plan_stats()
-        if i:
-            assert st["reused_chunks"] >= 0.7 * st["chunks"], st
-        rc, costs = s.run(iters)
-        assert rc == _lib.VO_OK
-        inc.append((costs, *s.get_state()))
-    for w, (costs, P, X) in zip(ws, inc):
-        _session(other, ctx).run(1)
-        s = _session(w, ctx)
-        assert s.plan_stats()["reused_chunks"] == 0
-        rc, c2 = s.run(iters)
-        P2, X2 = s.get_state()
-        np.testing.assert_array_equal(c2, costs)
-        np.testing.assert_array_equal(P2, P)
-        np.testing.assert_array_equal(X2, X)
+    _lib.ba_testing_k1_four_wave(ctx, four)
+    try:
+        for i, w in enumerate(ws):
+            s = _session(w, ctx)
+            st = s.plan_stats()
+            assert (st["seg_obs"] > 1) == four, st
+            if i:
+                assert st["reused_chunks"] >= 0.6 * st["chunks"], st
+            rc, costs = s.run(iters)
+            assert rc == _lib.VO_OK
+            inc.append((costs, *s.get_state()))
+        for w, (costs, P, X) in zip(ws, inc):
+            _session(other, ctx).run(1)
+            s = _session(w, ctx)
+            assert s.plan_stats()["reused_chunks"] == 0
+            rc, c2 = s.run(iters)
+            P2, X2 = s.get_state()
+            np.testing.assert_array_equal(c2, costs)
+            np.testing.assert_array_equal(P2, P)
+            np.testing.assert_array_equal(X2, X)
+    finally:
+        _lib.ba_testing_k1_four_wave(ctx, False)
     w = ws[-1]
     R = cref.BAProblemRef(w.K, w.point_ptr, w.obs_cam, w.obs_uv, w.n_poses, w.n_fixed, 1.0)
     n, Pr, Xr, cr = R.solve(w.poses_cw, w.points, iters, nthreads=8)

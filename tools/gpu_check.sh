@@ -1,8 +1,14 @@
 #!/bin/bash
-# GPU parity tests + one bench line (no profiler).  Usage: gpurun -- bash tools/gpu_check.sh [pytest args]
+# GPU parity tests + smoke + the cfg3 bench line and a cfg4 BA line (no profiler).
+# Usage: gpurun --timeout 900 -- bash tools/gpu_check.sh [tag] [pytest args]
 set -euo pipefail
-mkdir -p gpurun_out
+TAG=${1:-check}
+shift || true
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "$@" > gpurun_out/pytest_gpu.log 2>&1
-timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
+timeout -k 10 300 python bench.py --config cfg4 --no-matcher --no-cpu-baseline --steps 50 --warmup 5 > $OUT/bench_cfg4.json 2> $OUT/bench_cfg4.err
 echo done

@@ -106,6 +106,7 @@ SIGNATURES = {
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_ba_split_reduce": (_I, [_P, _I]),
     "vo_ba_testing_drop_reducers": (_I, [_P, _I]),
+    "vo_ba_testing_k1_four_wave": (_I, [_P, _I]),
     "vo_ba_testing_plan_slide": (_I, [C.c_void_p, C.c_void_p, _I, C.POINTER(C.c_uint64), _PI64]),
 }
 
@@ -273,6 +274,12 @@ def ba_testing_drop_reducers(ctx: "Context", n: int) -> None:
     """Test switch: fused launches of this context leave out ``n`` reducer workgroups, so
     the solver's bounded wait times out; see vo_ba_testing_drop_reducers."""
     check(ctx.lib.vo_ba_testing_drop_reducers(ctx.handle, int(n)), "vo_ba_testing_drop_reducers")
+
+
+def ba_testing_k1_four_wave(ctx: "Context", on: bool = True) -> None:
+    """Test switch: the context's later setups plan the four-wave K1 (multi-chunk segments)
+    instead of the one-wave K1; see vo_ba_testing_k1_four_wave."""
+    check(ctx.lib.vo_ba_testing_k1_four_wave(ctx.handle, int(bool(on))), "vo_ba_testing_k1_four_wave")
 
 
 def ptr(a, ctype):

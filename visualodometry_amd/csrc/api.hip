@@ -748,6 +748,13 @@ int vo_ba_testing_drop_reducers(vo_ctx* ctx, int n) {
   });
 }
 
+int vo_ba_testing_k1_four_wave(vo_ctx* ctx, int on) {
+  return guarded([&] {
+    VO_REQUIRE(ctx != nullptr, VO_ERR_ARG, "vo_ba_testing_k1_four_wave: null context");
+    ctx->ba_k1_four_wave = on != 0;
+  });
+}
+
 int vo_comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
   return guarded([&] {
     vo::bind(ctx);

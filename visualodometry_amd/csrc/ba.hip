@@ -46,9 +46,6 @@
 #include "ba_plan.h"
 #include "vo_ctx.h"
 
-#ifndef VO_BA_CL
-#define VO_BA_CL 0  // 1: the critical-lane elimination in full mode (experimental; slower so far)
-#endif
 #ifndef VO_BA_FUSE
 #define VO_BA_FUSE 1  // tuning build: 0 launches K2 on its own
 #endif
@@ -180,6 +177,7 @@ struct LinArgs {
   const double* dc;        // pending pose update (6 per free camera)
   const int* status;
   unsigned long long* stamps;  // diagnostic build only: per segment phase cycles
+  int nseg;                    // segments
 };
 
 struct alignas(16) LinShared {
@@ -486,24 +484,37 @@ enum { kPhLoad = 0, kPhBacksub, kPhLinObs, kPhReduce, kPhElim, kPhSchur, kPhWrit
        kPhObs, kPhTe, kPhPts, kPhPairs, kPhSlots, kPhCams, kPhCount };
 template <bool kStamp>
 struct Stamper {
+  // the stamping lane (thread 0, or lane 0 of each one-wave segment) and its output row;
+  // s_memtime counts per XCD (clocks of different XCDs are unrelated), so the row's
+  // window-camera count carries the XCD id in bits 24..31
   unsigned long long t = 0, acc[kPhCount] = {};
-  __device__ __forceinline__ void start() {
-    if (kStamp && threadIdx.x == 0) acc[kPhT0] = t = __builtin_amdgcn_s_memtime();
+  bool lead = false;
+  int row = 0;
+  __device__ __forceinline__ void start(bool ld, int r) {
+    lead = kStamp && ld;
+    row = r;
+    if (lead) {
+      acc[kPhT0] = t = __builtin_amdgcn_s_memtime();
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+      acc[kPhCams] = (unsigned long long)xcc << 24;
+    }
   }
+  __device__ __forceinline__ void start() { start(threadIdx.x == 0, blockIdx.x); }
   __device__ __forceinline__ void mark(int ph) {
-    if (kStamp && threadIdx.x == 0) {
+    if (lead) {
       const unsigned long long n = __builtin_amdgcn_s_memtime();
       acc[ph] += n - t;
       t = n;
     }
   }
   __device__ __forceinline__ void count(int k, int v) {
-    if (kStamp && threadIdx.x == 0) acc[k] += (unsigned long long)v;
+    if (lead) acc[k] += (unsigned long long)v;
   }
   __device__ __forceinline__ void flush(unsigned long long* out) {
-    if (kStamp && threadIdx.x == 0) acc[kPhT1] = __builtin_amdgcn_s_memtime();  // absolute
-    if (kStamp && threadIdx.x == 0 && out)
-      for (int k = 0; k < kPhCount; ++k) out[blockIdx.x * kPhCount + k] = acc[k];
+    if (lead) acc[kPhT1] = __builtin_amdgcn_s_memtime();  // absolute
+    if (lead && out)
+      for (int k = 0; k < kPhCount; ++k) out[(long)row * kPhCount + k] = acc[k];
   }
 };
 
@@ -802,7 +813,6 @@ struct alignas(16) LinWave {
 // six per CU (cfg3's 1362 chunks in one round on 256 CUs)
 constexpr int kWaveSegsPerCu = 6;
 static_assert(sizeof(LinWave) <= 160 * 1024 / kWaveSegsPerCu, "one-wave K1 LDS image");
-constexpr int kWaveObsPerCu = kWaveSegsPerCu * 58;  // observations one round takes (chunks of ~58+)
 
 // point_block over the Zb region's Jp | r (same operation order)
 __device__ __forceinline__ bool point_block_w(const LinWave& S, double lambda, int p, double (&l)[6],
@@ -939,27 +949,44 @@ __device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si
     if (j < n) accum(zxA, zyA);
   }
   st.mark(kPhSchur);  // stamped builds: the pair sums
+  // a diagonal item: U over its pairs' observations (camol entries [auo[si], auo[si + 1]), in
+  // observation order, observation i + 1's Jc fetched while i accumulates) and its share of
+  // b over its pairs (track entry x's bt row)
   double ob[6] = {0, 0, 0, 0, 0, 0};
-  if (n > 0) {
-    if (dcam != 0xFF) {
-      for (int e = e0; e < e0 + n; ++e) {
-        const int x = S.img.pairs[e] & 255;
-        const double2* br = reinterpret_cast<const double2*>(S.bt[x]);
+  const int u0 = S.img.auo[si], un = live ? S.img.auo[si + 1] - u0 : 0;
+  if (un > 0) {
+    auto uacc = [&](const double (&jj)[12]) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const double2 v = br[k];
-          ob[2 * k] += v.x;
-          ob[2 * k + 1] += v.y;
-        }
-        for (int o = S.img.te_obs[x]; o < S.img.te_obs[x + 1]; ++o) {
-          double jj[12];
-          jc_load(S, o, jj);
+      for (int i = 0; i < 6; ++i)
 #pragma unroll
-          for (int i = 0; i < 6; ++i)
+        for (int c = 0; c < 6; ++c)
+          out[6 * i + c] = __builtin_fma(jj[6 + i], jj[6 + c], __builtin_fma(jj[i], jj[c], out[6 * i + c]));
+    };
+    auto oid = [&](int i) { return (int)S.img.camol[u0 + min(i, un - 1)]; };
+    double jA[12], jB[12];
+    jc_load(S, oid(0), jA);
+    int on = oid(1);
+    int i = 0;
+    for (; i + 2 <= un; i += 2) {
+      jc_load(S, on, jB);
+      on = oid(i + 2);
+      uacc(jA);
+      jc_load(S, on, jA);
+      on = oid(i + 3);
+      uacc(jB);
+    }
+    if (i < un) uacc(jA);
+  }
+  if (n > 0 && dcam != 0xFF) {
+    int xn = S.img.pairs[e0] & 255;
+    for (int e = 0; e < n; ++e) {
+      const double2* br = reinterpret_cast<const double2*>(S.bt[xn]);
+      xn = S.img.pairs[e0 + min(e + 1, n - 1)] & 255;
 #pragma unroll
-            for (int c = 0; c < 6; ++c)
-              out[6 * i + c] = __builtin_fma(jj[6 + i], jj[6 + c], __builtin_fma(jj[i], jj[c], out[6 * i + c]));
-        }
+      for (int k = 0; k < 3; ++k) {
+        const double2 v = br[k];
+        ob[2 * k] += v.x;
+        ob[2 * k + 1] += v.y;
       }
     }
   }
@@ -1000,10 +1027,20 @@ __device__ __forceinline__ void copy_rows(const LinWave& S, const LinArgs& A, in
   double acc[18];
 #pragma unroll
   for (int i = 0; i < 18; ++i) acc[i] = sc[min(i, ne - 1)];  // every load of a copy in flight
-  for (int c = 1; c < m; ++c) {
+  int c = 1;
+  for (; c + 2 <= m; c += 2) {  // two copies' loads in flight, added in copy order
+    double v[18], u[18];
+#pragma unroll
+    for (int i = 0; i < 18; ++i) {
+      v[i] = sc[36 * c + min(i, ne - 1)];
+      u[i] = sc[36 * (c + 1) + min(i, ne - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < 18; ++i) acc[i] = (acc[i] + v[i]) + u[i];
+  }
+  if (c < m)
 #pragma unroll
     for (int i = 0; i < 18; ++i) acc[i] += sc[36 * c + min(i, ne - 1)];
-  }
   double* row = &A.slab[36l * S.spos[S.img.aslot[si]] + e0];
 #pragma unroll
   for (int i = 0; i < 18; ++i)
@@ -1023,19 +1060,28 @@ __device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int
     const int ci = q / 6, a = q - 6 * ci;
     const int j0 = S.img.cdiag0[ci], nj = S.img.cdiagn[ci];
     double acc = 0.0;
-    for (int j = 0; j < nj; ++j) acc += bp[6 * (j0 + j) + a];
+    for (int j = 0; j < nj; j += 8) {  // eight partials' loads in flight, added in item order
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = bp[6 * (j0 + min(j + k, nj - 1)) + a];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (j + k < nj) acc += v[k];
+    }
     A.slab_b[6l * S.cpos[S.img.acid[ci]] + a] = acc;
   }
 }
 
-// The one-wave K1: segment = chunk = workgroup of one wave (the plan's seg_obs == 1).
+// The one-wave K1: segment = chunk = one 64-lane workgroup (the plan's seg_obs == 1).
+// (Two, three or six such waves per workgroup, each on its own LDS image, measured no faster
+// at cfg3: the dispatch ramp is not what bounds K1)
 template <int MODE, bool kStamp>
 __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
   __shared__ LinWave S;
   static_assert(kLinLanesWave == 64, "one wave");
-  Stamper<kStamp> st;
-  st.start();
   const int seg = blockIdx.x, tid = threadIdx.x;
+  Stamper<kStamp> st;
+  st.start(tid == 0, seg);
   // level 1: status, segment header (uniform), this lane's camera ids (fixed header offsets)
   // and the chunk's image (chunk = segment)
   const int* SH = A.seg_hdr + (long)kSegHdr * seg;
@@ -1747,34 +1793,30 @@ class BAEngine {
     const bool prev_ok = plan_ok_;
     plan_ok_ = false;
     if (err.empty()) {
-      // one-wave K1 (segments of one chunk) while the window's chunks fit one round of six
-      // one-wave workgroups per CU; the four-wave K1 over multi-chunk segments beyond
-      bool wave = (int64_t)prob->n_obs <= (int64_t)kWaveObsPerCu * std::max(1, ctx_->num_cus);
-      const int ideal = seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave));
-      // the packing target stays the previous plan's while it is within 10 % of this window's
-      // (a plan can take over groups only from a plan with the same target)
-      const int so = prev_ok && plan_.seg_obs * 10 >= ideal * 9 && plan_.seg_obs * 10 <= ideal * 11 ? plan_.seg_obs
-                                                                                                  : ideal;
+      // K1 variant (a plan property, ba_plan.h plan_is_wave): the one-wave K1 (segments of
+      // one chunk) at every size -- cfg4's 13.7k chunks run in nine rounds of six per CU, faster
+      // than the four-wave K1's one round of two-chunk segments (148 against 222 us, DESIGN.md
+      // §K1); the four-wave K1 over multi-chunk segments only under the testing switch
+      // (vo_ba_testing_k1_four_wave).  The packing target is a function of this window alone,
+      // so a plan that takes groups over from the previous one is the plan a scratch setup
+      // builds (take-over needs equal targets: build_plan checks).
+      const bool wave = !ctx_->ba_k1_four_wave;
       std::vector<int32_t> zero_ptr(1, 0);
       const int32_t* pp = prob->n_points ? prob->point_ptr : zero_ptr.data();
       std::swap(plan_, prev_plan_);
       d_chunk_img_.swap(d_chunk_img_prev_);
+      const BAPlan* prev = prev_ok ? &prev_plan_ : nullptr;
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
-                       prob->obs_uv, so, prev_ok ? &prev_plan_ : nullptr);
-      if (err.empty() && plan_is_wave(plan_.seg_obs) && plan_.n_chunks() > kWaveSegsPerCu * std::max(1, ctx_->num_cus)) {
-        wave = false;  // more chunks than one round: the four-wave K1 after all
-        err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
-                         prob->obs_uv, seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, false)),
-                         prev_ok ? &prev_plan_ : nullptr);
-      }
+                       prob->obs_uv, seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave)), prev);
       // four-wave K1: every first-camera group ends in a partial segment, so the packing target
       // may give more segments than one round holds; then pack once more, proportionally wider
+      // (a function of the plan, which does not depend on prev)
       const int round = segments_target(ctx_->num_cus, false);
       for (int k = 0; k < 4 && err.empty() && !plan_is_wave(plan_.seg_obs) && plan_.n_segments() > round; ++k) {
         const int so2 = (int)std::min<int64_t>((int64_t)plan_.seg_obs * plan_.n_segments() / round + 1 + plan_.seg_obs / 50,
                                                1 << 30);
         err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
-                         prob->obs_uv, so2, prev_ok ? &prev_plan_ : nullptr);
+                         prob->obs_uv, so2, prev);
       }
     }
     if (ctx_->comm && ctx_->comm->nranks > 1) {
@@ -2141,22 +2183,19 @@ class BAEngine {
     // one-wave K1 for plans of one chunk per segment (the chunk image of segment s is chunk s)
     const bool wave = plan_is_wave(plan_.seg_obs);
     VO_REQUIRE(!wave || nseg == plan_.n_chunks(), VO_ERR_STATE, "K1: segments of one chunk expected");
+    A.nseg = nseg;
     dim3 g(nseg), b(wave ? kLinLanesWave : kLinThreads);
     ctx_->prof.begin(ctx_->stream, kKBaLin);
     if (stamps_on_) {
       d_stamps_.reserve((size_t)nseg * kPhCount * 8);
       A.stamps = d_stamps_.as<unsigned long long>();
     }
-#define VO_LIN_LAUNCH(M)                                                               \
-  do {                                                                                 \
-    if (wave && stamps_on_)                                                            \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, true>), g, b, 0, ctx_->stream, A);     \
-    else if (wave)                                                                     \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, false>), g, b, 0, ctx_->stream, A);    \
-    else if (stamps_on_)                                                               \
-      hipLaunchKernelGGL((ba_lin_kernel<M, true>), g, b, 0, ctx_->stream, A);          \
-    else                                                                               \
-      hipLaunchKernelGGL((ba_lin_kernel<M, false>), g, b, 0, ctx_->stream, A);         \
+#define VO_LIN_LAUNCH(M)                                                                    \
+  do {                                                                                      \
+    if (wave)                                                                               \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_>), g, b, 0, ctx_->stream, A);   \
+    else                                                                                    \
+      hipLaunchKernelGGL((ba_lin_kernel<M, stamps_on_>), g, b, 0, ctx_->stream, A);        \
   } while (0)
     switch (mode) {
       case kAccum: VO_LIN_LAUNCH(kAccum); break;
@@ -2219,9 +2258,6 @@ class BAEngine {
       B.cost_off = cost_off_;
       B.merge = band_tab_.merge;
       B.n_merge = band_tab_.n_merge;
-      // the critical-lane elimination: full mode, w >= 1 (tuning build: VO_BA_CL=0 keeps the
-      // per-step barrier kernel)
-      B.cl = (VO_BA_CL && band_lds_.full && band_.w >= 1) ? band_tab_.cl : -1;
       B.tab = d_band_tab_.as<int>();
       B.sys = A.sys;
       B.zero = d_zero_.as<double>();
@@ -2353,8 +2389,8 @@ class BAEngine {
   HostBuf h_state_;  // page-locked staging of set_state / get_state
   hipEvent_t h_state_ev_ = nullptr;  // set_state's upload from h_state_ done
   bool h_state_busy_ = false;
-  DevBuf d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;
-  DevBuf d_chunk_img_prev_;  // the previous plan's images (prev_plan_)  // K1's plan (the chunk images hold every list)
+  DevBuf d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;  // K1's plan (the chunk images hold every list)
+  DevBuf d_chunk_img_prev_;  // the previous plan's images (prev_plan_)
   DevBuf d_stamps_, d_stamps3_;
   static constexpr bool stamps_on_ = kBaStamps;
 

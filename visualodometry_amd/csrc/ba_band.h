@@ -27,11 +27,9 @@ BandSplit band_split(int F, const std::vector<int>& first);
 
 // Merge pairs of one window structure (host-built, uploaded once): (destination, source)
 // LDS offsets (doubles) of the separator's blocks and rhs, top ring += bottom ring.
-// cl >= 0: the window takes the critical-lane elimination (full mode; ba_band_cl.h).
 struct BandTables {
   std::vector<int> tab;
   int merge = 0, n_merge = 0;
-  int cl = -1;
 };
 // LDS layout of the two column stores.  Ring mode: w + 4 slots per side, each padded to
 // whole 1 KiB LDS-DMA pieces; factor records go to global memory.  Full mode (when it
@@ -54,7 +52,6 @@ struct BandArgs {
   int F, w, m, nb, s;
   int nprof, n_poses, n_fixed, iter_tag;
   int merge, n_merge;     // merge pairs in tab (BandTables)
-  int cl;                // >= 0: the critical-lane elimination (full mode, BandTables::cl)
   long cost_off;          // the cost in sys
   const int* tab;
   const double* sys;      // K2's banded layout (above), padded by one ring slot

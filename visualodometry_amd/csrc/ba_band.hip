@@ -33,7 +33,6 @@
 #include <algorithm>
 #include <climits>
 
-#include "ba_band_cl.h"
 #include "ba_math.h"
 #include "vo_common.h"
 
@@ -100,7 +99,6 @@ BandTables band_tables(int F, const BandSplit& b, const BandLds& L) {
     }
   }
   T.n_merge = (int)T.tab.size() / 2;
-  T.cl = w >= 1 && w <= kBandMaxW ? 0 : -1;  // the critical-lane elimination (ba_band_cl.h) takes the window
   if (T.tab.empty()) T.tab.push_back(0);
   return T;
 }
@@ -142,17 +140,11 @@ constexpr int kBandThreads = 64 * kBandWaves;
 constexpr int kLdRegs = 6;      // ring loader: elements per lane of one column
 constexpr int kTaskRounds = 2;  // trailing (block, row pair) tasks per lane
 constexpr int kProLoads = 8;    // prologue: 16-byte pieces per thread (columns 0 .. w + 1 of both sides)
-constexpr int kClProLoads = 9;  // critical-lane prologue: columns 0 .. w + 2 of both sides
-constexpr int kClTileRows = (6 * kBandMaxW + 15) / 16;               // critical-lane MFMA tiles of the window
-constexpr int kClTiles = kClTileRows * (kClTileRows - 1) / 2 > kClTileRows ? kClTileRows * (kClTileRows - 1) / 2
-                                                                          : kClTileRows;  // per trailing wave
-typedef double __attribute__((ext_vector_type(4))) d4;
 static_assert(36 * (kBandMaxW + 1) + 12 <= 64 * kLdRegs, "one column per loader wave");
 static_assert(3 * (kBandMaxW - 1) * kBandMaxW / 2 <= 64 * kTaskRounds, "trailing tasks per helper wave");
 static_assert(6 * (kBandMaxW + 1) <= 64, "one lane per panel row");
 static_assert(36 * (kBandMaxW + 1) + 12 <= 3 * 128, "at most three 1 KiB LDS-DMA pieces per column");
 static_assert((kBandMaxW + 2) * (36 * (kBandMaxW + 1) + 12) <= kProLoads * kBandThreads, "prologue");
-static_assert((kBandMaxW + 3) * (36 * (kBandMaxW + 1) + 12) <= kClProLoads * kBandThreads, "prologue");
 // Wave roles (wave = 2 * role + side; wave w runs on SIMD w mod 4, so each side's chain
 // shares its SIMD only with that side's loader, which mostly waits on memory).
 enum { kChain = 0, kTrail = 1, kLoad = 2, kFwd = 3 };
@@ -163,19 +155,6 @@ __device__ __forceinline__ void band_barrier() { asm volatile("s_waitcnt lgkmcnt
 
 #ifndef VO_BA_STAMPS
 #define VO_BA_STAMPS 0
-#endif
-// Tuning builds (EXTRA=-D...): VO_BA_DBCAST 0 broadcasts the diagonal block through LDS
-// instead of readlane; VO_BA_EXP != 0 disables one helper role (timing only, results wrong).
-#ifndef VO_BA_DBCAST
-#define VO_BA_DBCAST 0
-#endif
-#ifndef VO_BA_EXP
-#define VO_BA_EXP 0
-#endif
-// 1: the panel factored by broadcast pivots on two chain waves (fixed lane mapping, kDc below);
-// 0: the round-2 chain (redundant chol6 per lane, rotating rows) and the forward wave
-#ifndef VO_BA_DPPCHAIN
-#define VO_BA_DPPCHAIN 0
 #endif
 // Diagnostic build only (EXTRA=-DVO_BA_STAMPS=1): lane 0 of each wave accumulates
 // s_memtime deltas per phase; the product build executes none.
@@ -320,14 +299,10 @@ __device__ __forceinline__ bool band_wait_reduced(const BandArgs& A, int tid, in
 // Loads below never feed a select or branch before their first real use: a value that
 // must be zero is loaded from the zero block (A.zero) instead, so the waitcnt pass can
 // leave every prefetch in flight.
-// kCl (full mode, w >= 1): the elimination by the critical-lane layout (ba_band_cl.h and the
-// phase below); the back substitution and the pose update are the same code.
-template <bool kFull, bool kCl>
+template <bool kFull>
 __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
-  static_assert(kFull || !kCl, "critical-lane elimination in full mode only");
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int s_fail;
-  __shared__ int s_flags[16];  // kCl: per side, the steps each role has published
   __shared__ __attribute__((aligned(16))) double s_zero[40];   // full mode's zero block
 #if VO_BA_STAMPS
   unsigned long long st_acc[kBandStamps] = {}, st_t = __builtin_amdgcn_s_memtime();
@@ -380,32 +355,11 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   }
   typedef __attribute__((address_space(3))) void lds_void;
   typedef __attribute__((address_space(1))) const void gbl_void;
-  if (tid < 16) s_flags[tid] = 0;
-  if constexpr (kCl) {
-    // columns 0 .. w + 2 of both sides (the forward wave streams the rest by LDS-DMA, three
-    // steps ahead of their first use), every 16-byte load in flight, then the stores
-    const int nT = min(w + 3, ncolT) * CS / 2, nB = min(w + 3, ncolB) * CS / 2;  // double2 pieces
-    const double2* gT = reinterpret_cast<const double2*>(A.sys);
-    const double2* gB = reinterpret_cast<const double2*>(A.sys + (long)ncolT * CS);
-    double2 v[kClProLoads];
-#pragma unroll
-    for (int u = 0; u < kClProLoads; ++u) {
-      const int e = tid + u * kBandThreads;
-      v[u] = e < nT ? gT[e] : e < nT + nB ? gB[e - nT] : make_double2(0.0, 0.0);
-    }
-    if (!prior_fail)
-#pragma unroll
-      for (int u = 0; u < kClProLoads; ++u) {
-        const int e = tid + u * kBandThreads;
-        const bool top = e < nT;
-        const int x = 2 * (top ? e : e - nT), col = x / CS;
-        if (e < nT + nB) *reinterpret_cast<double2*>((top ? ringT : ringB) + col * SS + x - col * CS) = v[u];
-      }
-  } else {
-  // Ring prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every
-  // 16-byte load in flight, then the stores.  The loads do not wait for the status word
-  // (one global round trip less on the launch's path); a failed earlier solve only skips
-  // the stores.
+  {
+    // Prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every 16-byte
+    // load in flight, then the stores.  The loads do not wait for the status word (one
+    // global round trip less on the launch's path); a failed earlier solve only skips the
+    // stores.
     const int nT = min(w + 2, ncolT) * CS / 2, nB = min(w + 2, ncolB) * CS / 2;  // double2 pieces
     const double2* gT = reinterpret_cast<const double2*>(A.sys);
     const double2* gB = reinterpret_cast<const double2*>(A.sys + (long)ncolT * CS);
@@ -483,17 +437,6 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     double* col = sring + sk * SS;
     const int ocol = (int)(col - dyn);
     double L[21], r[6];
-#if VO_BA_DBCAST
-    // the diagonal block's rows (group q == 0: lanes 6 (k mod R) + i) to every lane by
-    // readlane (uniform lane index): no LDS round trip on the chain
-    {
-      const int dl = 6 * (k % R);
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int c = 0; c <= i; ++c) L[P6(i, c)] = readlane_d(P[c], dl + i);
-    }
-#else
     // the diagonal block's rows (group q == 0) to every lane through LDS (other lanes
     // store to the dummy row: no divergent code on the chain)
     {
@@ -510,7 +453,6 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
         L[P6(i, c)] = v.x;
         if (c + 1 <= i) L[P6(i, c + 1)] = v.y;
       }
-#endif
     BSETTLE(L[20]);
     BSTF(17);
     chol6_nochk(L, r);
@@ -662,19 +604,18 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   };
-  // VO_BA_EXP: 1 no trail, 2 no fwd, 3 no loader
   auto side_step = [&](int p, int sk, int skm) __attribute__((always_inline)) {
     if (role == kTrail) {
       // ring mode: column p - 1's record read first (its latency under the trailing
       // update), stored to global memory last
       i32x4 v2[3];
       if (!kFull && p >= 1) rec_load(skm, v2);
-      if (VO_BA_EXP != 1) trail_step(p, sk);
+      trail_step(p, sk);
       if (!kFull && p >= 1) rec_store(p - 1, v2);
     } else if (role == kFwd) {
-      if (VO_BA_EXP != 2 && !VO_BA_DPPCHAIN) fwd_step(p, sk);
+      fwd_step(p, sk);
     } else if (role == kLoad) {
-      if (VO_BA_EXP != 3) load_step(p);
+      load_step(p);
     }
   };
 
@@ -711,390 +652,18 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     for (int c = 0; c < 6; ++c) col[6 * c] = gv[c];
   };
 
-  // ---- DPP chain (kDc, VO_BA_DPPCHAIN): the panel of block column k on two chain waves (roles
-  // 0 and 3) with a fixed lane -> row mapping, factored by the right-looking broadcast pivots of
-  // ba_band_cl.h.  Per 16-lane DPP row: lanes 0..5 a copy of the diagonal block A_kk (every DPP
-  // row factors it, the same instructions on the same values), lanes 6..15 panel slots p =
-  // 40 c + 10 (lane >> 4) + li - 6 (c: chain wave): row p % 6 of block k + 1 + p / 6 for p < 6w,
-  // the rhs y_k for p = 6w.  So the factor phase before the barrier needs no LDS round trip:
-  // the pivots give L_kk, every L_{k+q,k} and y'_k at once.  After the barrier each lane moves to
-  // its row of column k + 1: target - u L_{k+1,k}^T, with u its row of L_{k+1+q,k} (the step-k
-  // factor of the block that row comes from; the diagonal lanes: L_{k+1,k}; the rhs: y'_k) and
-  // L_{k+1,k} broadcast from LDS; the panel lanes of blocks q >= 2 also apply y_{k+q} -= L_{k+q,k}
-  // y'_k (the rhs lane does q = 1 with its own update).  The trailing wave keeps the blocks
-  // (i, j), j >= k + 2, and the loader wave its streaming.
-  constexpr bool kDc = VO_BA_DPPCHAIN != 0;
-  const int dc_c = role == kChain ? 0 : 1;
-  const bool dc_wave = kDc && (role == kChain || role == kFwd);
-  const int dc_li = lane & 15;
-  const int dc_p = 40 * dc_c + 10 * (lane >> 4) + dc_li - 6;
-  const bool dc_diag = dc_li < 6;
-  const bool dc_panel = !dc_diag && dc_p < 6 * w;
-  const bool dc_rhs = !dc_diag && dc_p == 6 * w;
-  const int dc_q = dc_diag ? 0 : dc_panel ? 1 + dc_p / 6 : 0;  // block index in the column
-  const int dc_r = dc_diag ? dc_li : dc_panel ? dc_p - 6 * (dc_p / 6) : 0;
-  // the row owner writes it (the diagonal copies of DPP row 0 of the first chain wave)
-  const bool dc_own = dc_panel || dc_rhs || (dc_diag && dc_c == 0 && lane < 16);
-  double dcA[6] = {0, 0, 0, 0, 0, 0}, dcR[6] = {0, 0, 0, 0, 0, 0};
-  // this lane's row in the column in slot sk (offsets into dyn; idle lanes: the zero block)
-  auto dc_row = [&](int sk) __attribute__((always_inline)) {
-    const int base = (int)(sring - dyn) + sk * SS;
-    return dc_diag ? base + 6 * dc_r : dc_panel ? base + 36 * dc_q + 6 * dc_r : dc_rhs ? base + 36 * R : ZOFF;
-  };
-  auto dc_load = [&](int sk, int k) __attribute__((always_inline)) {
-    const bool ok = dc_diag || dc_rhs || (dc_panel && k + dc_q < snload);
-    ld6g(dyn + (ok ? dc_row(sk) : ZOFF), dcA);
-  };
-  auto dc_store = [&](int sk, int k) __attribute__((always_inline)) {
-    if (dc_own && (!dc_panel || k + dc_q < snload)) st6g(dyn + dc_row(sk), dcA);
-  };
-  auto dc_pre = [&](int k, int sk) __attribute__((always_inline)) {
-    cl::pivots(dcA, dcR);
-    bad = bad || (dc_c == 0 && lane == 0 && !isfinite(dcR[0] + dcR[1] + dcR[2] + dcR[3] + dcR[4] + dcR[5])) ||
-          (dc_rhs && !isfinite(dcA[0] + dcA[1] + dcA[2] + dcA[3] + dcA[4] + dcA[5]));
-    dc_store(sk, k);
-    if (dc_c == 0 && lane == 0) st6g(sring + sk * SS + 36 * R + 6, dcR);
-  };
-  // column k (slot sk) -> column k + 1 (slot sk1), after the barrier
-  auto dc_post = [&](int k, int sk, int sk1) __attribute__((always_inline)) {
-    const double* col = sring + sk * SS;
-    const bool tok = dc_diag || dc_rhs || (dc_panel && k + 1 + dc_q < snload);
-    double tg[6], u[6], V[6][6];
-    ld6g(dyn + (tok ? dc_row(sk1) : ZOFF), tg);
-    // w == 0: no sub-diagonal block (u and V zero)
-    const bool uok = w >= 1 && (dc_diag || (dc_panel && dc_q + 1 <= w && k + 1 + dc_q < snload));
-    ld6g(uok ? col + 36 * (dc_q + 1) + 6 * dc_r : dyn + ZOFF, u);
-    if (dc_rhs && w >= 1)
-#pragma unroll
-      for (int c = 0; c < 6; ++c) u[c] = dcA[c];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) ld6g(w >= 1 ? col + 36 + 6 * c : dyn + ZOFF, V[c]);
-    // y_{k+q} -= L_{k+q,k} y'_k (q >= 2; row r of block k + q, this lane's own factor row)
-    const bool yok = dc_panel && dc_q >= 2 && k + dc_q < snload;
-    if (yok) {
-      double yp[6];
-      ld6g(col + 36 * R, yp);
-      const int sq = sk + dc_q < RC ? sk + dc_q : sk + dc_q - RC;
-      double* yd = sring + sq * SS + 36 * R + dc_r;
-      *yd -= dcA[0] * yp[0] + dcA[1] * yp[1] + dcA[2] * yp[2] + dcA[3] * yp[3] + dcA[4] * yp[4] + dcA[5] * yp[5];
-    }
-#pragma unroll
-    for (int c = 0; c < 6; ++c)
-      dcA[c] = tg[c] - (u[0] * V[c][0] + u[1] * V[c][1] + u[2] * V[c][2] + u[3] * V[c][3] + u[4] * V[c][4] +
-                        u[5] * V[c][5]);
-  };
-  if constexpr (kCl) {
-    if (!prior_fail) {
-      // ---- Critical-lane elimination (full mode).  Per side four waves, synchronised by LDS
-      // flags instead of a workgroup barrier per step (s_flags[8 side + f]: the number of
-      // steps a role has published):
-      //   chain (role 0)  lanes 0..15 of a DPP row hold [A_kk; A_{k+1,k}; y_k] (ba_band_cl.h).
-      //                   Step k: pivots -> L_kk, y'_k, r (flag 0); the pending step-(k-1) term
-      //                   of A_{k+1,k} (u = L_{k+1,k-1} from the forward wave, V = L_{k,k-1} kept
-      //                   in registers), its solve -> L_{k+1,k} (flag 1); the next panel:
-      //                   A_{k+1,k+1} - L_{k+1,k} L_{k+1,k}^T and y_{k+1} - L_{k+1,k} y'_k from
-      //                   the trailing waves' values through step k - 1, A_{k+2,k+1} (its step-k
-      //                   term waits for the next step).
-      //   forward (role 2) L_{k+q,k} = A_{k+q,k} L_kk^-T for q = 2..w (one lane per row, in
-      //                   place) and y_{k+q} -= L_{k+q,k} y'_k (flag 2).
-      //   trailing (roles 1, 3) blocks (k+qi, k+jj) -= L_{k+qi,k} L_{k+jj,k}^T for every other
-      //                   block of step k, one target row per lane, L_{k+jj,k} broadcast from
-      //                   lanes 0..5 of the DPP row (band_tables' descriptors); the first round
-      //                   (flags 3 / 5) holds column k + 1 and the chain's next two blocks, the
-      //                   last one is flag 4 / 6.
-      // Waits: chain(k) on forward(k-1) and both trailing waves' first round of step k-1;
-      // forward(k) on chain(k) and that round; trailing(k) on forward(k), chain(k)'s flag 1 and
-      // the other trailing wave's step k-1.  Every wait is on an earlier role of the dependency
-      // order, so the phase cannot deadlock, and every step of every role posts its flags.
-      // flags through an LDS-typed pointer (a generic one compiles to flat accesses that wait on
-      // vmcnt as well); the polled value goes through readfirstlane, so the loop is scalar
-      typedef __attribute__((address_space(3))) volatile int lds_flag;
-      lds_flag* const fl = (lds_flag*)s_flags + 8 * side;
-      const int li = lane & 15;
-      const double* const zb = dyn + ZOFF;
-      auto colp = [&](int c) __attribute__((always_inline)) { return sring + c * SS; };
-      auto wait_ge = [&](lds_flag* f, int v) __attribute__((always_inline)) {
-        while (__builtin_amdgcn_readfirstlane(*f) < v) __builtin_amdgcn_s_sleep(1);
-        asm volatile("" ::: "memory");
-      };
-      auto post = [&](lds_flag* f, int v) __attribute__((always_inline)) {
-        asm volatile("" ::: "memory");
-        if (lane == 0) *f = v;
-      };
-      // chain wave, steps k0 .. kend - 1 of this side; flush: the state of column kend to LDS at
-      // the end (phase A with a separator).  The pending term's operand (the forward wave's
-      // L_{k+1,k-1}) is fetched at the step's start, under the pivots.
-      auto cl_chain = [&](int k0, int kend, bool flush) __attribute__((always_inline)) {
-        double a[6], pp[6], vp[6], r[6];
-        bool lazy = false;
-        {
-          const double* c0 = colp(k0);
-          ld6g(li < 6 ? c0 + 6 * li : li == 12 ? c0 + 36 * R : zb, a);
-          ld6g((li >= 6 && li < 12) ? c0 + 36 + 6 * (li - 6) : zb, pp);
-        }
-#pragma unroll
-        for (int c = 0; c < 6; ++c) vp[c] = 0.0;
-        int k = k0;
-        for (; k < kend; ++k) {
-          BST(30);
-          double u[6];
-          const bool more = k + 1 < snload;
-          if (lazy) {
-            wait_ge(fl + 2, k);
-            ld6g((li >= 6 && li < 12) ? colp(k - 1) + 72 + 6 * (li - 6) : zb, u);
-          }
-          BST(18);
-          cl::pivots(a, r);
-          double* ck = colp(k);
-          if (lane < 6) st6g(ck + 6 * lane, a);
-          else if (lane == 12) st6g(ck + 36 * R, a);
-          else if (lane == 13) st6g(ck + 36 * R + 6, r);
-          post(fl + 0, k + 1);
-          BST(17);
-          if (!more) {  // the side's last column: no sub-diagonal block to publish
-            post(fl + 1, k + 1);
-            break;
-          }
-          if (lazy) cl::sub_uvt<6>(pp, u, vp);  // the step-(k-1) term of A_{k+1,k}
-          cl::solve_lt(pp, a, r);
-          if (lane >= 6 && lane < 12) st6g(ck + 36 + 6 * (lane - 6), pp);
-          post(fl + 1, k + 1);
-          BST(19);
-          // next panel (column k + 1) from the values through step k - 1 (the first trailing
-          // wave's step k - 1, the forward wave's rhs update of step k - 1)
-          wait_ge(fl + 3, k);
-          wait_ge(fl + 2, k);
-          BST(20);
-          double b0[6], b1[6], sh[6];
-          const double* c1 = colp(k + 1);
-          ld6g(li < 6 ? c1 + 6 * li : li == 12 ? c1 + 36 * R : zb, b0);
-          ld6g((li >= 6 && li < 12 && k + 2 < snload) ? c1 + 36 + 6 * (li - 6) : zb, b1);
-          cl::shl6(pp, sh);
-#pragma unroll
-          for (int c = 0; c < 6; ++c) u[c] = li < 6 ? sh[c] : li == 12 ? a[c] : 0.0;
-          cl::sub_uvt<6>(b0, u, pp);
-#pragma unroll
-          for (int c = 0; c < 6; ++c) {
-            vp[c] = pp[c];
-            pp[c] = b1[c];
-            a[c] = b0[c];
-          }
-          lazy = w >= 2;
-          BST(21);
-        }
-        if (flush && k == kend && kend < snload) {
-          // column kend through step kend - 1: the pending term of its sub-diagonal block, then
-          // the panel to LDS for the separator merge
-          if (lazy) {
-            wait_ge(fl + 2, kend);
-            double u[6];
-            ld6g((li >= 6 && li < 12) ? colp(kend - 1) + 72 + 6 * (li - 6) : zb, u);
-            cl::sub_uvt<6>(pp, u, vp);
-          }
-          double* ce = colp(kend);
-          if (lane < 6) st6g(ce + 6 * lane, a);
-          else if (lane == 12) st6g(ce + 36 * R, a);
-          else if (lane >= 6 && lane < 12 && kend + 1 < snload) st6g(ce + 36 + 6 * (lane - 6), pp);
-        }
-      };
-      // forward wave.  Per 16-lane DPP row: lanes 0..5 hold the rows of L_kk, lanes 6..15 ten rows
-      // r of blocks k + q, q = 2..w (40 per pass), solved by broadcast FMAs (cl::solve_lt); then
-      // y_{k+q} -= L_{k+q,k} y'_k.  It also streams the side's columns: column k + w + 3 by
-      // LDS-DMA (inline asm: the compiler would otherwise wait for it before every LDS access),
-      // and before posting step k every DMA issued before step k - 1 has landed (column k + w + 1,
-      // first touched by the trailing waves at step k + 1, which wait for this post).
-      auto cl_fwd = [&](int k0, int kend) __attribute__((always_inline)) {
-        const int dr = lane >> 4;
-        const int npass = (6 * (w - 1) + 39) / 40;
-        int n_prev = 0;  // DMA pieces issued at the previous step
-        for (int k = k0; k < kend; ++k) {
-          BST(30);
-          int n_now = 0;
-          if (k + w + 3 < snload) {
-            const double* src = ssys + (long)(k + w + 3) * CS + 2 * lane;
-            const unsigned dst = (unsigned)(uintptr_t)(colp(k + w + 3));
-            for (int t = 0; t < nDma; ++t)
-              asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst + 1024u * t),
-                           "v"(src + 128 * t)
-                           : "memory", "m0");
-            n_now = nDma;
-          }
-          wait_ge(fl + 0, k + 1);
-          wait_ge(fl + 3, k);
-          BST(22);
-          const double* ck = colp(k);
-          double Lr[6], r[6], y[6];
-          ld6g(li < 6 ? ck + 6 * li : zb, Lr);
-          ld6g(ck + 36 * R + 6, r);
-          ld6g(ck + 36 * R, y);
-          for (int ps = 0; ps < npass; ++ps) {
-            const int ti = 40 * ps + 10 * dr + li - 6, q = 2 + ti / 6, rr = ti - 6 * (ti / 6);
-            const bool on = (li >= 6) & (ti < 6 * (w - 1)) & (k + q < snload);
-            double x[6];
-            ld6g(on ? ck + 36 * q + 6 * rr : zb, x);
-            const double yo = on ? colp(k + q)[36 * R + rr] : 0.0;
-            cl::solve_lt(x, Lr, r);
-            if (on) {
-              st6g(const_cast<double*>(ck) + 36 * q + 6 * rr, x);
-              colp(k + q)[36 * R + rr] =
-                  yo - (x[0] * y[0] + x[1] * y[1] + x[2] * y[2] + x[3] * y[3] + x[4] * y[4] + x[5] * y[5]);
-            }
-          }
-          bad = bad | !isfinite(r[0] + r[1] + r[2] + r[3] + r[4] + r[5]) |
-                !isfinite(y[0] + y[1] + y[2] + y[3] + y[4] + y[5]);
-          switch (n_now + n_prev) {  // only the DMAs of this step and the previous one in flight
-            case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-            case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-            case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-            case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-            case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-            case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-            default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-          }
-          n_prev = n_now;
-          post(fl + 2, k + 1);
-          BST(23);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      };
-      // trailing waves: the step-k update X -= P P^T of the window X = blocks (k + 1 .. k + w)^2
-      // (lower blocks; the chain's (k+1, k+1) and (k+2, k+1) excluded) with P = the panel rows
-      // L_{k+1..k+w, k}, as 16x16 f64 tiles on the matrix cores (v_mfma_f64_16x16x4f64, two
-      // k-steps for the six panel columns; D element reg e of lane l: window row 16 ti +
-      // (l >> 4) + 4 e, column 16 tj + (l & 15); A / B operand: P[16 t + (l & 15)][4 s + (l >> 4)]).
-      // Wave 0 (role 1) owns tile column 0 (window blocks 0..2: everything the chain and the
-      // forward wave wait for), wave 1 (role 3) the other tiles.  Tile column 0 of step k + 1
-      // overlaps the other tiles of step k, so wave 0 waits for wave 1's previous step.
-      auto cl_trail = [&](int k0, int kend, int tw) __attribute__((always_inline)) {
-        const int nt = (6 * w + 15) / 16;
-        int tti[kClTiles], ttj[kClTiles], nti = 0;
-        for (int ti = 0; ti < nt; ++ti)
-          for (int tj = 0; tj <= ti; ++tj)
-            if ((tj == 0) == (tw == 0) && nti < kClTiles) {
-              tti[nti] = ti;
-              ttj[nti] = tj;
-              ++nti;
-            }
-        // per element: offset from column k + 1 (-1: never stored) and its row block
-        int off[kClTiles][4], rb[kClTiles][4];
-#pragma unroll
-        for (int t = 0; t < kClTiles; ++t)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int i = 16 * tti[t < nti ? t : 0] + (lane >> 4) + 4 * e, j = 16 * ttj[t < nti ? t : 0] + (lane & 15);
-            const int bi = i / 6, bj = j / 6;
-            const bool ok = t < nti && i < 6 * w && j < 6 * w && bi >= bj && !(bj == 0 && bi <= 1);
-            off[t][e] = ok ? bj * SS + 36 * (bi - bj) + 6 * (i - 6 * bi) + (j - 6 * bj) : -1;
-            rb[t][e] = bi;
-          }
-        // operands: P row 16 t + (l & 15), column 4 s + (l >> 4) of column k
-        int opo[kClTileRows][2], opb[kClTileRows];
-#pragma unroll
-        for (int t = 0; t < kClTileRows; ++t) {
-          const int i = 16 * t + (lane & 15), bi = i / 6;
-          opb[t] = bi;
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const int kk = 4 * s2 + (lane >> 4);
-            opo[t][s2] = (t < nt && i < 6 * w && kk < 6) ? 36 * (1 + bi) + 6 * (i - 6 * bi) + kk : -1;
-          }
-        }
-        lds_flag* const fme = fl + (tw ? 4 : 3);
-        for (int k = k0; k < kend; ++k) {
-          BST(30);
-          wait_ge(fl + 2, k + 1);
-          wait_ge(fl + 1, k + 1);
-          if (tw == 0) wait_ge(fl + 4, k);
-          BST(24);
-          const double* ck = colp(k);
-          const double* cx = colp(k + 1);
-          double opv[kClTileRows][2];
-#pragma unroll
-          for (int t = 0; t < kClTileRows; ++t)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-              const bool on = (opo[t][s2] >= 0) & (k + 1 + opb[t] < snload);
-              opv[t][s2] = *(on ? ck + opo[t][s2] : zb);
-            }
-          d4 acc[kClTiles];
-#pragma unroll
-          for (int t = 0; t < kClTiles; ++t)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const bool on = (off[t][e] >= 0) & (k + 1 + rb[t][e] < snload);
-              acc[t][e] = *(on ? cx + off[t][e] : zb);
-            }
-#pragma unroll
-          for (int t = 0; t < kClTiles; ++t) {
-            if (t >= nti) break;
-            double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-#pragma unroll
-            for (int tt = 0; tt < kClTileRows; ++tt) {
-              if (tt == tti[t]) { a0 = -opv[tt][0]; a1 = -opv[tt][1]; }
-              if (tt == ttj[t]) { b0 = opv[tt][0]; b1 = opv[tt][1]; }
-            }
-            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[t], 0, 0, 0);
-          }
-#pragma unroll
-          for (int t = 0; t < kClTiles; ++t)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if ((off[t][e] >= 0) & (k + 1 + rb[t][e] < snload)) const_cast<double*>(cx)[off[t][e]] = acc[t][e];
-          post(fme, k + 1);
-          BST(25);
-        }
-      };
-      auto cl_phase = [&](int k0, int kend, bool flush) __attribute__((always_inline)) {
-        if (role == kChain) cl_chain(k0, kend, flush);
-        else if (role == 2) cl_fwd(k0, kend);
-        else cl_trail(k0, kend, role == 1 ? 0 : 1);
-      };
-      cl_phase(0, sna, sp > 0);
-      if (sp > 0) {
-        // both sides' state of the separator is in the rings: the bottom's contributions merged
-        // into the top's (fixed order), then the top's four waves continue through the
-        // separator while the bottom's form the G blocks of the rows final after phase A
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        BST(30);
-        __syncthreads();
-        BST(26);
-        for (int e = tid; e < A.n_merge; e += kBandThreads) {
-          const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
-          dyn[d.x] += dyn[d.y];
-        }
-        __syncthreads();
-        BST(27);
-        if (side == 0) {
-          cl_phase(m, m + sp, false);
-          BST(28);
-        } else {
-          const int n0 = 6 * (m + nb) * w;
-          for (int e = 64 * role + lane; e < n0; e += 256) g_item(0, e);
-          BST(29);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-  } else if (!prior_fail) {
+  if (!prior_fail) {
     const int PA = max(m, nb);
     int sk = 0, skm = RC - 1;
-    if (dc_wave && sna > 0) dc_load(0, 0);
     for (int p = 0; p < PA; ++p) {
       const bool on = p < sna;
       const int sk1 = sk + 1 == RC ? 0 : sk + 1;
-      if (kDc) {
-        if (dc_wave && on) dc_pre(p, sk);
-      } else if (role == kChain && on) {
-        chain_pre(p, sk);
-      }
+      if (role == kChain && on) chain_pre(p, sk);
       BST(1);
       band_barrier();
       BST(2);
       if (on) {
-        if (kDc && dc_wave) {
-          if (p + 1 < snload) dc_post(p, sk, sk1);
-        } else if (!kDc && role == kChain) {
+        if (role == kChain) {
           if (p + 1 < snload) chain_post(sk1);
         } else {
           side_step(p, sk, skm);
@@ -1107,38 +676,24 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     if (sp > 0) {
       // both sides' state of the separator into the rings, the bottom's contributions
       // merged into the top's (fixed order), then the top continues through the separator
-      if (kDc) {
-        if (dc_wave) dc_store(sna % RC, sna);
-      } else if (act) {
-        st6g(sring + (sna % RC) * SS + 36 * q + 6 * sr, P);
-      }
+      if (act) st6g(sring + (sna % RC) * SS + 36 * q + 6 * sr, P);
       __syncthreads();
       for (int e = tid; e < A.n_merge; e += kBandThreads) {
         const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
         dyn[d.x] += dyn[d.y];
       }
       __syncthreads();
-      if (kDc) {
-        if (dc_wave && side == 0) dc_load(m % RC, m);
-      } else if (act && side == 0) {
-        ld6g(ringT + (m % RC) * SS + 36 * q + 6 * sr, P);
-      }
+      if (act && side == 0) ld6g(ringT + (m % RC) * SS + 36 * q + 6 * sr, P);
       BST(4);
       int sk = m % RC, skm = sk == 0 ? RC - 1 : sk - 1;
       for (int p = m; p < m + sp; ++p) {
         const int sk1 = sk + 1 == RC ? 0 : sk + 1;
-        if (kDc) {
-          if (dc_wave && side == 0) dc_pre(p, sk);
-        } else if (role == kChain && side == 0) {
-          chain_pre(p, sk);
-        }
+        if (role == kChain && side == 0) chain_pre(p, sk);
         BST(5);
         band_barrier();
         BST(6);
         if (side == 0) {
-          if (kDc && dc_wave) {
-            if (p + 1 < ncolT) dc_post(p, sk, sk1);
-          } else if (!kDc && role == kChain) {
+          if (role == kChain) {
             if (p + 1 < ncolT) chain_post(sk1);
           } else {
             side_step(p, sk, skm);
@@ -1163,7 +718,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       rec_store(last, v2);
     }
   }
-  if ((kCl || VO_BA_DPPCHAIN || lane == 0) && bad) s_fail = 1;
+  if (lane == 0 && bad) s_fail = 1;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // factor records written
   BST(8);
   __syncthreads();
@@ -1437,8 +992,7 @@ static size_t band_launch_lds(const BandLds& L, bool fused) {
 }
 
 void band_set_attributes(const BandLds& L) {
-  const void* fs[3] = {(const void*)ba_band_kernel<true, false>, (const void*)ba_band_kernel<false, false>,
-                       (const void*)ba_band_kernel<true, true>};
+  const void* fs[2] = {(const void*)ba_band_kernel<true>, (const void*)ba_band_kernel<false>};
   for (const void* f : fs)
     VO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)band_launch_lds(L, true)));
 }
@@ -1448,12 +1002,10 @@ void launch_band_solve(const BandArgs& A, const BandLds& L, hipStream_t st) {
   // fewer than the solver waits for: vo_ba_testing_drop_reducers)
   const dim3 grid(1 + std::max(A.nred - std::max(A.red_drop, 0), 0));
   const size_t lds = band_launch_lds(L, A.nred > 0);
-  if (L.full && A.cl >= 0)
-    hipLaunchKernelGGL((ba_band_kernel<true, true>), grid, dim3(kBandThreads), lds, st, A);
-  else if (L.full)
-    hipLaunchKernelGGL((ba_band_kernel<true, false>), grid, dim3(kBandThreads), lds, st, A);
+  if (L.full)
+    hipLaunchKernelGGL((ba_band_kernel<true>), grid, dim3(kBandThreads), lds, st, A);
   else
-    hipLaunchKernelGGL((ba_band_kernel<false, false>), grid, dim3(kBandThreads), lds, st, A);
+    hipLaunchKernelGGL((ba_band_kernel<false>), grid, dim3(kBandThreads), lds, st, A);
 }
 
 }  // namespace vo

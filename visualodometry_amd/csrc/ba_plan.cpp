@@ -977,7 +977,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
           }
         g.camp[nac] = c1 - c0;
         g.camop[nac] = q1 - q0;
-        if (wave)  // each active camera's diagonal items (its copies are consecutive)
+        if (wave) {  // each active camera's diagonal items (its copies are consecutive)
           for (int ci = 0; ci < nac; ++ci) {
             int j0 = -1, nj = 0;
             for (int j = 0; j < nas; ++j)
@@ -988,6 +988,27 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
             g.cdiag0[ci] = (uint8_t)std::max(j0, 0);
             g.cdiagn[ci] = (uint8_t)nj;
           }
+          // the diagonal items' U observations: a diagonal slot's pairs (x, x) run over its
+          // camera's track entries in order, so copy k's observations are the next entries of
+          // the camera's observation list; diagonal items come in camera order (the slot of
+          // (c, c) is the last of row c), so the ranges tile camol and an off-diagonal item
+          // gets the empty range at the next diagonal item's start
+          g.auo[nas] = (uint8_t)(q1 - q0);
+          int run = 0;
+          for (int ci = 0, j = 0; ci < nac; ++ci) {
+            run = g.camop[ci];
+            for (; j < g.cdiag0[ci] + g.cdiagn[ci] && j < nas; ++j) {
+              if (g.adcam[j] != g.acid[ci]) continue;
+              g.auo[j] = (uint8_t)run;
+              for (int e = g.slotp[j]; e < g.slotp[j] + g.apcnt[j]; ++e) {
+                const int x = g.pairs[e] & 255;
+                run += g.te_obs[x + 1] - g.te_obs[x];
+              }
+            }
+          }
+          for (int j = nas; j-- > 0;)
+            if (g.adcam[j] == 0xFF) g.auo[j] = g.auo[j + 1];
+        }
         for (int i = 0; i < c1 - c0; ++i) g.caml[i] = P.cam_list[c0 + i];
         for (int i = 0; i < q1 - q0; ++i) g.camol[i] = P.camo_list[q0 + i];
         h[14] = nas;

@@ -110,6 +110,8 @@ struct alignas(16) ChunkImg {
   uint8_t acopy[kSegSlots];        // one-wave K1: item i's copy index (anp[i] = the slot's copies)
   uint8_t cdiag0[kSegCams];        // one-wave K1: active camera i -> its first diagonal item
   uint8_t cdiagn[kSegCams];        //   and the number of copies (consecutive items)
+  uint8_t auo[kSegSlots + 1];      // one-wave K1: item i's U observations, camol entries
+                                   //   [auo[i], auo[i + 1]) (empty off the diagonal)
   alignas(2) uint16_t pairs[kChunkPairs];  // (te_x | te_y << 8) by slot
   uint8_t caml[kChunkTe];          // track entries by window camera
   uint8_t camol[kChunkObs];        // observations by window camera

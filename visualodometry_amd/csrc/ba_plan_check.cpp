@@ -6,6 +6,7 @@
 //   - the one-wave K1 (seg_obs 1): one lane per slot block, copies splitting heavy slots;
 //   - a diagonal slot's pairs (over its copies) are (x, x) over exactly its camera's track entries
 //     (so its lanes' U sums equal the camera lists'), adcam names the camera, off-diagonal 0xFF;
+//     one-wave K1: each item's U observation range (auo) is exactly its pairs' observations;
 //   - with one chunk per segment, every window slot is active and every window camera has a
 //     diagonal slot (every slab row and rhs entry is written).
 // Input (binary): int32 n_poses, n_points, n_obs, n_fixed, seg_obs; point_ptr; obs_cam; obs_uv.
@@ -106,17 +107,25 @@ int main(int argc, char** argv) {
         const int ci = P.slot_i[so_ + ws], cj = P.slot_j[so_ + ws];
         if (ci != cj) {
           if (g.adcam[s] != 0xFF) FAIL("chunk %d: off-diagonal slot %d marked camera %d", ch, ws, (int)g.adcam[s]);
+          if (wave && g.auo[s] != g.auo[s + 1]) FAIL("chunk %d: off-diagonal item %d with U observations", ch, s);
           continue;
         }
         const int wc = g.adcam[s];
         if (wc >= ncams || P.segcam_f[co + wc] != ci) FAIL("chunk %d: diagonal slot %d camera %d", ch, ws, wc);
         cam_diag[wc] = 1;
         // its pairs: (x, x) over the chunk's track entries of that camera, each once
-        std::vector<int> tes;
+        std::vector<int> tes, uobs;
         for (int e = g.slotp[s]; e < g.slotp[s] + g.apcnt[s]; ++e) {
           const int x = g.pairs[e] & 255, y = g.pairs[e] >> 8;
           if (x != y) FAIL("chunk %d: diagonal slot pair (%d, %d)", ch, x, y);
           tes.push_back(x);
+          for (int o = g.te_obs[x]; o < g.te_obs[x + 1]; ++o) uobs.push_back(o);
+        }
+        // one-wave K1: the item's U observations (camol range) are exactly its pairs' ones
+        if (wave) {
+          std::vector<int> got;
+          for (int i = g.auo[s]; i < g.auo[s + 1]; ++i) got.push_back(g.camol[i]);
+          if (got != uobs) FAIL("chunk %d item %d: U observations differ from its pairs'", ch, s);
         }
         upairs[wc].insert(upairs[wc].end(), tes.begin(), tes.end());
       }

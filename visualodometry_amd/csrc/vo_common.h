@@ -37,6 +37,11 @@ struct Error {
     }                                 \
   } while (0)
 
+// Growth of the on-demand buffers: a quarter of headroom, so a window that grows by a few
+// landmarks per keyframe does not free (an implicit device synchronisation) and reallocate
+// its buffers on most calls.
+inline size_t buf_grow(size_t n) { return ((n ? n : 16) + n / 4 + 255) & ~(size_t)255; }
+
 // Device buffer that grows on demand and is freed with its owner.
 struct DevBuf {
   void* ptr = nullptr;
@@ -46,8 +51,9 @@ struct DevBuf {
     if (ptr) VO_HIP_CHECK(hipFree(ptr));
     ptr = nullptr;
     bytes = 0;
-    VO_HIP_CHECK(hipMalloc(&ptr, n ? n : 16));
-    bytes = n;
+    const size_t b = buf_grow(n);
+    VO_HIP_CHECK(hipMalloc(&ptr, b));
+    bytes = b;
   }
   template <class T>
   T* as() const {
@@ -74,8 +80,9 @@ struct HostBuf {
     if (ptr) VO_HIP_CHECK(hipHostFree(ptr));
     ptr = nullptr;
     bytes = 0;
-    VO_HIP_CHECK(hipHostMalloc(&ptr, n ? n : 16, hipHostMallocDefault));
-    bytes = n;
+    const size_t b = buf_grow(n);
+    VO_HIP_CHECK(hipHostMalloc(&ptr, b, hipHostMallocDefault));
+    bytes = b;
   }
   template <class T>
   T* as() const {
