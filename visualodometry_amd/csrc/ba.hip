@@ -1807,14 +1807,13 @@ class BAEngine {
       d_chunk_img_.swap(d_chunk_img_prev_);
       const BAPlan* prev = prev_ok ? &prev_plan_ : nullptr;
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
-                       prob->obs_uv, seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave)), prev);
+                       prob->obs_uv, seg_obs_grid(seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave))), prev);
       // four-wave K1: every first-camera group ends in a partial segment, so the packing target
       // may give more segments than one round holds; then pack once more, proportionally wider
-      // (a function of the plan, which does not depend on prev)
+      // (on the grid; a function of the plan, which does not depend on prev)
       const int round = segments_target(ctx_->num_cus, false);
       for (int k = 0; k < 4 && err.empty() && !plan_is_wave(plan_.seg_obs) && plan_.n_segments() > round; ++k) {
-        const int so2 = (int)std::min<int64_t>((int64_t)plan_.seg_obs * plan_.n_segments() / round + 1 + plan_.seg_obs / 50,
-                                               1 << 30);
+        const int so2 = seg_obs_grid((int64_t)plan_.seg_obs * plan_.n_segments() / round + 1);
         err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
                          prob->obs_uv, so2, prev);
       }

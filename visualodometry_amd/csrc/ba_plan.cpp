@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <numeric>
 
@@ -226,6 +227,13 @@ constexpr int kWaveItems = 60;                 // its lanes for slot copies (the
 int seg_obs_for(int64_t n_obs, int target_segments) {
   const int64_t t = std::max(1, target_segments);
   return (int)std::max<int64_t>(1, std::min<int64_t>((n_obs + t - 1) / t, 1 << 30));
+}
+
+int seg_obs_grid(int64_t x) {
+  if (x <= 1) return 1;
+  double g = 1.0;
+  while (std::ceil(g) < (double)x && g < (double)(1 << 30)) g *= 1.0905077326652577;  // 2^(1/8)
+  return (int)std::min<double>(std::ceil(g), 1 << 30);
 }
 
 void BAPlan::reset() {

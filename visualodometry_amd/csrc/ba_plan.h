@@ -256,6 +256,10 @@ struct BAPlan {
 
 // The packing target of a window of n_obs observations for target_segments K1 workgroups.
 int seg_obs_for(int64_t n_obs, int target_segments);
+// The smallest packing target of a fixed geometric grid (ceil(2^(k/8)), steps of ~9 %) that is
+// >= x: a function of x alone, so windows of nearly equal size (consecutive keyframes) share a
+// target, which group take-over needs, without making a plan depend on the window before it.
+int seg_obs_grid(int64_t x);
 // Builds everything except the profile (needs the global first[] on multi-GPU).
 // Returns an empty string on success, else the error message.  With prev (the plan of the
 // previous window on the same engine, built with the same seg_obs and n_fixed), every
