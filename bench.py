@@ -154,7 +154,7 @@ def ba_parity_guard(sess, p, pts, p0: int, p1: int, lam: float, iters: int = 2, 
     rc, costs = sess.run(iters)
     P, X = sess.get_state()
     R = cref.BAProblemRef(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, lam)
-    _, Pr, Xr, cr = R.solve(p.poses_cw, p.points, iters, nthreads=host_cores())
+    _, Pr, Xr, cr = R.solve(p.poses_cw, p.points, iters, nthreads=host_cores()[0])
     err = {"cost": rel(np.asarray(costs), np.asarray(cr)), "poses": rel(P, Pr), "points": rel(X, Xr[p0:p1])}
     ok = rc == _lib.VO_OK and all(np.isfinite(v) and v <= tol for v in err.values())
     return {"ok": bool(ok), "iters": iters, "tol": tol, "rel_err": err, "checker": "oracle/ba_ref.c"}
