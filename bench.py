@@ -528,6 +528,9 @@ def main() -> int:
     ap.add_argument("--lam", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-matcher", action="store_true")
+    ap.add_argument("--k1", type=int, default=0,
+                    help="tuning: K1 variant through the testing switch vo_ba_testing_k1 (0 = the product "
+                         "default, -1 four-wave K1, n = 1..3 one-wave K1 with n chunks per segment)")
     ap.add_argument("--traffic-json", default=None,
                     help="per-kernel HBM bytes per launch from rocprofv3 --pmc passes of this build and config "
                          "(tools/pmc_traffic.py; default profiles/traffic_<config>.json); attached only when its "
@@ -560,6 +563,8 @@ def main() -> int:
         dist.broadcast_object_list(uid, src=0)
         _lib.comm_init(ctx, world, rank, uid[0])
 
+    if args.k1:
+        _lib.ba_testing_k1(ctx, args.k1)
     p = make_ba_config(args.config)
     (p0, p1), ptr, cam, uv, pts = shard(p.point_ptr, p.obs_cam, p.obs_uv, p.points, world, rank)
     sess = BASession(p.K, ptr, cam, uv, p.n_poses, p.n_fixed, args.lam, ctx)
@@ -649,6 +654,7 @@ def main() -> int:
                         f"lambda={args.lam}); one step = one full GN iteration",
             "poses": p.n_poses, "landmarks": p.n_points, "observations": p.n_obs,
             "parallelism": f"landmark-sharded x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
+            "k1_variant": args.k1,
             "plan": stats,
         },
         "kernels": kern,

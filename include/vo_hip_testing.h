@@ -28,13 +28,14 @@ int vo_ba_split_reduce(vo_ctx* ctx, int on);
  * failed factorisation.  n = 0 restores normal launches. */
 int vo_ba_testing_drop_reducers(vo_ctx* ctx, int n);
 
-/* Test switch: on != 0 makes this context's later vo_ba_setup calls plan the four-wave K1
- * (segments of several chunks of one first-camera group, one 256-lane workgroup walking them,
- * one slab row per segment and window slot) instead of the default one-wave K1 (segments of
- * one chunk, one 64-lane workgroup each).  Same arithmetic, different summation order: results
- * agree to rounding, both within the oracle tolerance.  Keeps the four-wave K1 covered by the
- * GPU tests; takes effect at the next setup. */
-int vo_ba_testing_k1_four_wave(vo_ctx* ctx, int on);
+/* Test switch: the K1 variant this context's later vo_ba_setup calls plan.  0: the default;
+ * -1: the four-wave K1 (segments of several chunks of one first-camera group, one 256-lane
+ * workgroup walking them); n = 1, 2, 3: the one-wave K1 with n chunks of one first-camera group
+ * per segment (one wave per chunk, the segment's waves in one workgroup summing their slot
+ * blocks in chunk order: one slab row per segment slot).  Same arithmetic, different summation
+ * order: results agree to rounding, all within the oracle tolerance.  Keeps every K1 variant
+ * covered by the GPU tests; takes effect at the next setup. */
+int vo_ba_testing_k1(vo_ctx* ctx, int variant);
 
 /* Host only: the digest (as vo_ba_plan_digest) of the plan of `cur` packed for seg_obs
  * observations per segment, built from scratch when prev is NULL, else after a from-scratch

@@ -96,7 +96,7 @@ def test_four_wave_k1_matches_c_oracle(ctx, cfg):
     n, Pr, Xr, cr = R.solve(p.poses_cw, p.points, iters, nthreads=8)
     out = []
     for four in (True, False):
-        _lib.ba_testing_k1_four_wave(ctx, four)
+        _lib.ba_testing_k1(ctx, -1 if four else 0)
         try:
             s = _session(p, ctx)
             st = s.plan_stats()
@@ -105,12 +105,43 @@ def test_four_wave_k1_matches_c_oracle(ctx, cfg):
             assert rc == _lib.VO_OK
             P, X = s.get_state()
         finally:
-            _lib.ba_testing_k1_four_wave(ctx, False)
+            _lib.ba_testing_k1(ctx, 0)
         np.testing.assert_allclose(costs, cr, rtol=REL)
         assert _rel(P, Pr) < REL and _rel(X, Xr) < REL
         out.append((costs, P, X))
     assert _rel(out[0][0], out[1][0]) < 1e-9
     assert _rel(out[0][1], out[1][1]) < 1e-8
+
+
+@pytest.mark.parametrize("cfg,nch", [("cfg2", 2), ("cfg3", 2), ("cfg3", 3), ("cfg4", 2), ("cfg4", 3)])
+def test_group_segment_k1_matches_c_oracle(ctx, cfg, nch):
+    """The one-wave K1 with nch chunks of one first-camera group per segment (testing switch
+    vo_ba_testing_k1(ctx, nch)): the segment's waves sum their slot blocks in LDS in chunk order
+    into one slab row per segment slot.  Against the C oracle, the one-chunk plan to rounding,
+    and bitwise reproducible."""
+    p = make_ba_config(cfg)
+    iters = 3
+    R = cref.BAProblemRef(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 1.0)
+    n, Pr, Xr, cr = R.solve(p.poses_cw, p.points, iters, nthreads=8)
+    out = []
+    for variant in (nch, nch, 1):
+        _lib.ba_testing_k1(ctx, variant)
+        try:
+            s = _session(p, ctx)
+            st = s.plan_stats()
+            assert st["seg_obs"] == 1 and st["chunks"] == variant * st["segments"], st
+            rc, costs = s.run(iters)
+            assert rc == _lib.VO_OK
+            P, X = s.get_state()
+        finally:
+            _lib.ba_testing_k1(ctx, 0)
+        np.testing.assert_allclose(costs, cr, rtol=REL)
+        assert _rel(P, Pr) < REL and _rel(X, Xr) < REL
+        out.append((costs, P, X, st["slab_blocks"]))
+    for a_, b_ in zip(out[0][:3], out[1][:3]):
+        np.testing.assert_array_equal(a_, b_)
+    assert _rel(out[0][0], out[2][0]) < 1e-9
+    assert out[0][3] < 0.6 * out[2][3]  # slab rows: one per segment slot
 
 
 def test_deterministic_bitwise(ctx):
@@ -415,15 +446,16 @@ def test_two_sessions_on_one_context(ctx):
         s2.get_state()
 
 
-@pytest.mark.parametrize("cfg,four", [("cfg3", False), ("cfg4", False), ("cfg4", True)])
-def test_slide_takes_groups_over_and_matches_scratch(ctx, cfg, four):
+@pytest.mark.parametrize("cfg,variant", [("cfg3", 0), ("cfg3", 2), ("cfg4", 0), ("cfg4", 3), ("cfg4", -1)])
+def test_slide_takes_groups_over_and_matches_scratch(ctx, cfg, variant):
     """Consecutive keyframe windows on one context: each vo_ba_setup takes the unchanged
     first-camera groups of the previous window's plan over (chunk images copied on the
     device, not rebuilt or uploaded), and every result is bitwise the one of a setup from
-    scratch (an unrelated window set up in between), which also matches the C oracle.  cfg4
-    on both K1 variants: the four-wave K1's multi-chunk segments (with its repacking to one
-    round) take groups over too, and its packing target depends on the window alone (ADVICE
-    r4), so the slid plan is the scratch plan."""
+    scratch (an unrelated window set up in between), which also matches the C oracle.  Every
+    K1 variant: the default, the one-wave K1 with segments of several chunks, and the four-wave
+    K1's multi-chunk segments (with its repacking to one round; its packing target depends on
+    the window alone, ADVICE r4, so the slid plan is the scratch plan)."""
+    four = variant < 0
     from visualodometry_amd.synthetic import make_ba_slide
 
     ws = make_ba_slide(cfg, 3)
@@ -431,7 +463,7 @@ def test_slide_takes_groups_over_and_matches_scratch(ctx, cfg, four):
     iters = 2
     inc = []
     reused, prev_so = 0, None
-    _lib.ba_testing_k1_four_wave(ctx, four)
+    _lib.ba_testing_k1(ctx, variant)
     try:
         for i, w in enumerate(ws):
             s = _session(w, ctx)
@@ -456,7 +488,7 @@ def test_slide_takes_groups_over_and_matches_scratch(ctx, cfg, four):
             np.testing.assert_array_equal(P2, P)
             np.testing.assert_array_equal(X2, X)
     finally:
-        _lib.ba_testing_k1_four_wave(ctx, False)
+        _lib.ba_testing_k1(ctx, 0)
     assert reused > 0
     w = ws[-1]
     R = cref.BAProblemRef(w.K, w.point_ptr, w.obs_cam, w.obs_uv, w.n_poses, w.n_fixed, 1.0)

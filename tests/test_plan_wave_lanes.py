@@ -25,7 +25,7 @@ def exe():
     return EXE
 
 
-def check(exe, p, seg_obs):
+def check(exe, p, seg_obs, seg_chunks=1):
     with tempfile.TemporaryDirectory() as d:
         fi = os.path.join(d, "in")
         with open(fi, "wb") as f:
@@ -33,7 +33,7 @@ def check(exe, p, seg_obs):
             np.asarray(p.point_ptr, np.int32).tofile(f)
             np.asarray(p.obs_cam, np.int32).tofile(f)
             np.asarray(p.obs_uv, np.float32).tofile(f)
-        out = subprocess.run([str(exe), fi], capture_output=True, text=True)
+        out = subprocess.run([str(exe), fi, str(seg_chunks)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
     return [int(v) for v in out.stdout.split()[1:]]
 
@@ -48,6 +48,26 @@ def test_one_chunk_segments(exe, cfg):
 def test_small_windows(exe, seg_obs):
     for n, L, seed in [(8, 200, 11), (30, 3000, 11), (12, 800, 5)]:
         check(exe, make_ba_problem(n, L, seed), seg_obs)
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
+@pytest.mark.parametrize("seg_chunks", [2, 3])
+def test_group_segments(exe, cfg, seg_chunks):
+    """Wave plans of several chunks per segment: every segment exactly seg_chunks chunks of one
+    first-camera group (empty chunks pad a group's last segment), the union of its chunks'
+    active slots and cameras covers its window, and fewer segment slots (slab rows) than the
+    one-chunk plan's."""
+    p = make_ba_config(cfg)
+    chunks, segs, _, _ = check(exe, p, 1, seg_chunks)
+    assert chunks == seg_chunks * segs
+    c1, s1, _, _ = check(exe, p, 1, 1)
+    assert segs < s1 and chunks < c1 * 1.2
+
+
+def test_group_segments_small_windows(exe):
+    for n, L, seed in [(8, 200, 11), (30, 3000, 11), (12, 800, 5), (3, 40, 2)]:
+        for sc in (2, 3):
+            check(exe, make_ba_problem(n, L, seed), 1, sc)
 
 
 def test_multi_chunk_segments(exe):

@@ -106,7 +106,7 @@ SIGNATURES = {
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_ba_split_reduce": (_I, [_P, _I]),
     "vo_ba_testing_drop_reducers": (_I, [_P, _I]),
-    "vo_ba_testing_k1_four_wave": (_I, [_P, _I]),
+    "vo_ba_testing_k1": (_I, [_P, _I]),
     "vo_ba_testing_plan_slide": (_I, [C.c_void_p, C.c_void_p, _I, C.POINTER(C.c_uint64), _PI64]),
 }
 
@@ -276,10 +276,10 @@ def ba_testing_drop_reducers(ctx: "Context", n: int) -> None:
     check(ctx.lib.vo_ba_testing_drop_reducers(ctx.handle, int(n)), "vo_ba_testing_drop_reducers")
 
 
-def ba_testing_k1_four_wave(ctx: "Context", on: bool = True) -> None:
-    """Test switch: the context's later setups plan the four-wave K1 (multi-chunk segments)
-    instead of the one-wave K1; see vo_ba_testing_k1_four_wave."""
-    check(ctx.lib.vo_ba_testing_k1_four_wave(ctx.handle, int(bool(on))), "vo_ba_testing_k1_four_wave")
+def ba_testing_k1(ctx: "Context", variant: int = 0) -> None:
+    """Test switch: the K1 variant of the context's later setups (0 default, -1 four-wave K1,
+    n = 1..3 one-wave K1 with n chunks per segment); see vo_ba_testing_k1."""
+    check(ctx.lib.vo_ba_testing_k1(ctx.handle, int(variant)), "vo_ba_testing_k1")
 
 
 def ptr(a, ctype):

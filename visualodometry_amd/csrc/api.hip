@@ -748,10 +748,12 @@ int vo_ba_testing_drop_reducers(vo_ctx* ctx, int n) {
   });
 }
 
-int vo_ba_testing_k1_four_wave(vo_ctx* ctx, int on) {
+int vo_ba_testing_k1(vo_ctx* ctx, int variant) {
   return guarded([&] {
-    VO_REQUIRE(ctx != nullptr, VO_ERR_ARG, "vo_ba_testing_k1_four_wave: null context");
-    ctx->ba_k1_four_wave = on != 0;
+    VO_REQUIRE(ctx != nullptr, VO_ERR_ARG, "vo_ba_testing_k1: null context");
+    VO_REQUIRE(variant >= -1 && variant <= vo::kWaveMaxChunks, VO_ERR_ARG, "vo_ba_testing_k1: variant %d outside -1..%d",
+               variant, vo::kWaveMaxChunks);
+    ctx->ba_k1_variant = variant;
   });
 }
 

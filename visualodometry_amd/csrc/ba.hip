@@ -807,12 +807,20 @@ struct alignas(16) LinWave {
   double X[kChunkPts][3];
   double L[kChunkPts][6];  // 1/l00, l10, 1/l11, l20, l21, 1/l22
   double h[kChunkPts][3];
-  double pose_n[kSegAllCams][12];
+  double pose_n[kSegAllCams][12];  // after the linearisation: the chunk's b sums by window camera
   uint8_t valid[kChunkPts];
+  // segments of several chunks (one wave each): per window slot the scratch row of this chunk's
+  // block (0xFF: not active here), per window camera whether the chunk has its b, the cost
+  uint8_t srow[kSegSlots];
+  uint8_t crow[kSegCams];
+  double wcost;
 };
-// six per CU (cfg3's 1362 chunks in one round on 256 CUs)
+// six per CU (cfg3's 1362 chunks in one round on 256 CUs); segments of two chunks: three
+// workgroups of two waves, of three chunks: two of three
 constexpr int kWaveSegsPerCu = 6;
 static_assert(sizeof(LinWave) <= 160 * 1024 / kWaveSegsPerCu, "one-wave K1 LDS image");
+static_assert(kWaveMaxChunks <= 3 && kWaveItems * 36 * sizeof(double) <= 2176 * sizeof(double),
+              "the chunks of a segment fit six waves per CU; every item's block fits the scratch rows");
 
 // point_block over the Zb region's Jp | r (same operation order)
 __device__ __forceinline__ bool point_block_w(const LinWave& S, double lambda, int p, double (&l)[6],
@@ -903,7 +911,7 @@ __device__ __forceinline__ void jc_load(const LinWave& S, int o, double (&jj)[12
 // Z_x Z_y^T as FMA chains with both Z rows in registers (pair j+1's rows fetched while pair j
 // accumulates); a diagonal slot's lane adds U over its pairs' observations (pair (x, x): track
 // entry x of the slot's camera).  The block goes straight to its slab row.
-template <class Stamp>
+template <bool kGroup, class Stamp>
 __device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si, bool live, Stamp& st) {
   double out[36];
 #pragma unroll
@@ -999,11 +1007,11 @@ __device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si
 #pragma unroll
     for (int k = 0; k < 3; ++k) bp[k] = make_double2(ob[2 * k], ob[2 * k + 1]);
   }
-  if (S.img.anp[si] <= 1) {  // a slot of one item: its slab row
+  if (!kGroup && S.img.anp[si] <= 1) {  // a slot of one item: its slab row
     double2* w = reinterpret_cast<double2*>(&A.slab[36l * S.spos[s]]);
 #pragma unroll
     for (int e = 0; e < 18; ++e) w[e] = make_double2(out[2 * e], out[2 * e + 1]);
-  } else {  // a copy: its block to the scratch for copy_rows (the Jc | Z | bt region)
+  } else {  // a copy (or any item of a multi-chunk segment): its block to the scratch (Jc | Z | bt)
     lds_sync_wave();  // every lane's reads of that region are done (one wave, in order)
     double2* w = reinterpret_cast<double2*>(&S.Jc[0][0]) + 18 * si;
 #pragma unroll
@@ -1013,17 +1021,20 @@ __device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si
 }
 
 // A slot's copies (one-wave K1): copy k of m sums entries [36 k / m, 36 (k + 1) / m) of the
-// slot's m partial blocks (scratch rows of consecutive items) in copy order into the slab row.
+// slot's m partial blocks (scratch rows of consecutive items) in copy order into the slab row
+// (kGroup: into the first copy's scratch row, for the segment's combine; copy k only ever reads
+// and writes entry range k of that row).
 static_assert(offsetof(LinWave, zb) == offsetof(LinWave, Jc) + sizeof(LinWave::Jc) &&
                   offsetof(LinWave, bt) == offsetof(LinWave, zb) + sizeof(LinWave::zb) &&
                   sizeof(LinWave::Jc) + sizeof(LinWave::zb) + sizeof(LinWave::bt) >= 36 * sizeof(double) * 60,
               "the copies' scratch (60 items) fits the Jc | Z | bt region");
-__device__ __forceinline__ void copy_rows(const LinWave& S, const LinArgs& A, int si, bool live) {
+template <bool kGroup>
+__device__ __forceinline__ void copy_rows(LinWave& S, const LinArgs& A, int si, bool live) {
   const int m = S.img.anp[si];
   if (!live || m <= 1) return;
   const int k = S.img.acopy[si], j0 = si - k;
   const int e0 = 36 * k / m, ne = 36 * (k + 1) / m - e0;  // <= 18 entries (m >= 2)
-  const double* sc = &S.Jc[0][0] + 36 * j0 + e0;
+  double* sc = &S.Jc[0][0] + 36 * j0 + e0;
   double acc[18];
 #pragma unroll
   for (int i = 0; i < 18; ++i) acc[i] = sc[min(i, ne - 1)];  // every load of a copy in flight
@@ -1041,7 +1052,7 @@ __device__ __forceinline__ void copy_rows(const LinWave& S, const LinArgs& A, in
   if (c < m)
 #pragma unroll
     for (int i = 0; i < 18; ++i) acc[i] += sc[36 * c + min(i, ne - 1)];
-  double* row = &A.slab[36l * S.spos[S.img.aslot[si]] + e0];
+  double* row = kGroup ? sc : &A.slab[36l * S.spos[S.img.aslot[si]] + e0];
 #pragma unroll
   for (int i = 0; i < 18; ++i)
     if (i < ne) row[i] = acc[i];
@@ -1049,8 +1060,10 @@ __device__ __forceinline__ void copy_rows(const LinWave& S, const LinArgs& A, in
 
 // The rhs of the chunk's window cameras (one-wave K1): lane (active camera ci, row a) adds row a
 // of the camera's diagonal copies' partial sums (consecutive items cdiag0 .. + cdiagn, left in
-// the X | L | h region by schur_block) in item order into its slab entry.
-__device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int nac, int tid) {
+// the X | L | h region by schur_block) in item order into its slab entry (kGroup: into the dead
+// pose_n region by window camera, for the segment's combine).
+template <bool kGroup>
+__device__ __forceinline__ void rhs_rows(LinWave& S, const LinArgs& A, int nac, int tid) {
   static_assert(sizeof(S.X) + sizeof(S.L) + sizeof(S.h) >= 6 * sizeof(double) * kSegSlots &&
                     offsetof(LinWave, L) == offsetof(LinWave, X) + sizeof(S.X) &&
                     offsetof(LinWave, h) == offsetof(LinWave, L) + sizeof(S.L),
@@ -1068,20 +1081,28 @@ __device__ __forceinline__ void rhs_rows(const LinWave& S, const LinArgs& A, int
       for (int k = 0; k < 8; ++k)
         if (j + k < nj) acc += v[k];
     }
-    A.slab_b[6l * S.cpos[S.img.acid[ci]] + a] = acc;
+    if (kGroup) (&S.pose_n[0][0])[6 * S.img.acid[ci] + a] = acc;
+    else A.slab_b[6l * S.cpos[S.img.acid[ci]] + a] = acc;
   }
 }
 
-// The one-wave K1: segment = chunk = one 64-lane workgroup (the plan's seg_obs == 1).
-// (Two, three or six such waves per workgroup, each on its own LDS image, measured no faster
-// at cfg3: the dispatch ramp is not what bounds K1)
-template <int MODE, bool kStamp>
-__global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
-  __shared__ LinWave S;
+// The one-wave K1 (wave plans, seg_obs == 1): one wave per chunk, NW chunks of one first-camera
+// group per segment = workgroup (the plan's seg_chunks; chunk = segment * NW + wave, padded with
+// empty chunks).  NW == 1: each item's block goes straight to its slab row.  NW > 1: the waves
+// run on their own LDS images without waiting on each other, leave their blocks in their scratch
+// rows, and after one workgroup barrier the segment's slots are summed over its chunks in chunk
+// order into one slab row each (fewer rows for K2: one per segment slot, not per chunk slot).
+static_assert(sizeof(LinWave::pose_n) >= kSegCams * 6 * sizeof(double), "the chunk's b sums fit pose_n");
+template <int MODE, bool kStamp, int NW>
+__global__ __launch_bounds__(kLinLanesWave * NW) void ba_lin_wave_kernel(LinArgs A) {
+  constexpr bool kGroup = NW > 1;
+  __shared__ LinWave Sw[NW];
   static_assert(kLinLanesWave == 64, "one wave");
-  const int seg = blockIdx.x, tid = threadIdx.x;
+  const int wv = kGroup ? __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) : 0;
+  LinWave& S = Sw[wv];
+  const int seg = blockIdx.x, tid = (int)threadIdx.x & 63, chk = seg * NW + wv;
   Stamper<kStamp> st;
-  st.start(tid == 0, seg);
+  st.start(tid == 0, chk);
   // level 1: status, segment header (uniform), this lane's camera ids (fixed header offsets)
   // and the chunk's image (chunk = segment)
   const int* SH = A.seg_hdr + (long)kSegHdr * seg;
@@ -1089,10 +1110,12 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
   const int16_t* SH16 = reinterpret_cast<const int16_t*>(SH);
   const int stat = A.status ? *A.status : 0;
   const int4 g0 = SH4[0], g1 = SH4[1];
-  const int4 h0 = SH4[8], h1 = SH4[9], h2 = SH4[10], h3 = SH4[11];
+  // this wave's chunk header: the segment header's copy (one chunk per segment), or its own
+  const int4* CH = kGroup ? A.chunk_hdr + 4l * chk : SH4 + 8;
+  const int4 h0 = CH[0], h1 = CH[1], h2 = CH[2], h3 = CH[3];
   constexpr int kImgVec = (int)(sizeof(ChunkImg) / 16);
   static_assert(kImgVec > 128 && kImgVec <= 192, "three 16-byte staging granules per lane");
-  const uint4* img = reinterpret_cast<const uint4*>(A.chunk_img + seg);
+  const uint4* img = reinterpret_cast<const uint4*>(A.chunk_img + chk);
   const uint4 img0 = img[tid], img1 = img[64 + tid], img2 = img[min(128 + tid, kImgVec - 1)];
   int i_acam[3], i_wcam[3];
 #pragma unroll
@@ -1107,8 +1130,9 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
   double* pose_o = &S.zb[kZbPoseO];
   // level 2: landmarks, poses, pending update, slab rows
   double vx[2], vpn[3], vpo[3], vdc[3];
+  const long xb = npt > 0 ? 3l * p0 : 0;  // an empty (padding) chunk may start past the last landmark
 #pragma unroll
-  for (int k = 0; k < 2; ++k) vx[k] = A.points[3l * p0 + min(tid + 64 * k, max(3 * npt - 1, 0))];
+  for (int k = 0; k < 2; ++k) vx[k] = A.points[xb + min(tid + 64 * k, max(3 * npt - 1, 0))];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int e = tid + 64 * k;
@@ -1144,6 +1168,10 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
   if (MODE & kAccum) {
     if (tid < nslots) S.spos[tid] = vsp;
     if (tid < ncams) S.cpos[tid] = vcp;
+    if (kGroup) {
+      S.srow[tid] = 0xFF;
+      if (tid < kSegCams) S.crow[tid] = 0;
+    }
   }
   st.count(kPhSlots, nslots);
   st.count(kPhCams, ncams);
@@ -1265,17 +1293,63 @@ __global__ __launch_bounds__(kLinLanesWave) void ba_lin_wave_kernel(LinArgs A) {
     // the lanes, each its own slab row); then the rhs by camera-row lanes
     {
       const int nas = h3.z;
-      for (int j = tid; j - tid < nas; j += kLinLanesWave) schur_block(S, A, min(j, nas - 1), j < nas, st);
+      for (int j = tid; j - tid < nas; j += kLinLanesWave)
+        schur_block<kGroup>(S, A, min(j, nas - 1), j < nas, st);
       lds_sync_wave();  // the copies' blocks and the diagonal items' b partials
-      for (int j = tid; j - tid < nas; j += kLinLanesWave) copy_rows(S, A, min(j, nas - 1), j < nas);
-      rhs_rows(S, A, h3.w, tid);
+      for (int j = tid; j - tid < nas; j += kLinLanesWave) copy_rows<kGroup>(S, A, min(j, nas - 1), j < nas);
+      rhs_rows<kGroup>(S, A, h3.w, tid);
+      if (kGroup) {  // where the combine finds this chunk's blocks (nas <= kWaveItems < 64 lanes)
+        if (tid < nas && S.img.acopy[tid] == 0) S.srow[S.img.aslot[tid]] = (uint8_t)tid;
+        if (tid < h3.w) S.crow[S.img.acid[tid]] = 1;
+      }
     }
     st.mark(kPhWrite);  // stamped builds: the rhs (with the final write below)
   }  // kAccum
-  // segment cost: a fixed xor butterfly over the wave (deterministic)
+  // chunk cost: a fixed xor butterfly over the wave (deterministic)
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) cost += __shfl_xor(cost, m, 64);
-  if (tid == 0) A.slab_cost[seg] = cost;
+  if (!kGroup) {
+    if (tid == 0) A.slab_cost[seg] = cost;
+  } else {
+    if (tid == 0) S.wcost = cost;
+    __syncthreads();  // every wave's blocks, b sums, maps and cost
+    const int t = (int)threadIdx.x;
+    if (MODE & kAccum) {
+      // segment slot s, entry i: the chunks' blocks in chunk order (only the chunks that have it)
+      for (int e = t; e < nslots * 36; e += 64 * NW) {
+        const int s = e / 36, i = e - 36 * s;
+        double acc = 0.0;
+        bool any = false;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const int r = Sw[w].srow[s];
+          const double v = (&Sw[w].Jc[0][0])[36 * (r == 0xFF ? 0 : r) + i];
+          acc = r == 0xFF ? acc : any ? acc + v : v;
+          any = any || r != 0xFF;
+        }
+        A.slab[36l * S.spos[s] + i] = acc;
+      }
+      for (int e = t; e < ncams * 6; e += 64 * NW) {
+        const int c = e / 6;
+        double acc = 0.0;
+        bool any = false;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const bool on = Sw[w].crow[c] != 0;
+          const double v = (&Sw[w].pose_n[0][0])[e];
+          acc = !on ? acc : any ? acc + v : v;
+          any = any || on;
+        }
+        A.slab_b[6l * S.cpos[c] + (e - 6 * c)] = acc;
+      }
+    }
+    if (t == 0) {
+      double c = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) c += Sw[w].wcost;
+      A.slab_cost[seg] = c;
+    }
+  }
   st.mark(kPhWrite);
   st.flush(A.stamps);
 }
@@ -1793,21 +1867,23 @@ class BAEngine {
     const bool prev_ok = plan_ok_;
     plan_ok_ = false;
     if (err.empty()) {
-      // K1 variant (a plan property, ba_plan.h plan_is_wave): the one-wave K1 (segments of
-      // one chunk) at every size -- cfg4's 13.7k chunks run in nine rounds of six per CU, faster
-      // than the four-wave K1's one round of two-chunk segments (148 against 222 us, DESIGN.md
-      // §K1); the four-wave K1 over multi-chunk segments only under the testing switch
-      // (vo_ba_testing_k1_four_wave).  The packing target is a function of this window alone,
-      // so a plan that takes groups over from the previous one is the plan a scratch setup
-      // builds (take-over needs equal targets: build_plan checks).
-      const bool wave = !ctx_->ba_k1_four_wave;
+      // K1 variant (a plan property, ba_plan.h plan_is_wave): the one-wave K1 at every size --
+      // cfg4's 13.7k chunks run in nine rounds of six per CU, faster than the four-wave K1's one
+      // round of two-chunk segments (148 against 222 us) -- with wave_chunks()
+      // chunks per segment; the four-wave K1 over multi-chunk segments only under the testing
+      // switch (vo_ba_testing_k1).  The packing target is a function of this window alone, so a
+      // plan that takes groups over from the previous one is the plan a scratch setup builds
+      // (take-over needs equal targets: build_plan checks).
+      const bool wave = ctx_->ba_k1_variant >= 0;
+      const int nw = wave ? wave_chunks(prob->n_obs) : 1;
       std::vector<int32_t> zero_ptr(1, 0);
       const int32_t* pp = prob->n_points ? prob->point_ptr : zero_ptr.data();
       std::swap(plan_, prev_plan_);
       d_chunk_img_.swap(d_chunk_img_prev_);
       const BAPlan* prev = prev_ok ? &prev_plan_ : nullptr;
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
-                       prob->obs_uv, seg_obs_grid(seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave))), prev);
+                       prob->obs_uv, seg_obs_grid(seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave))), prev,
+                       nw);
       // four-wave K1: every first-camera group ends in a partial segment, so the packing target
       // may give more segments than one round holds; then pack once more, proportionally wider
       // (on the grid; a function of the plan, which does not depend on prev)
@@ -2147,6 +2223,11 @@ class BAEngine {
   static int segments_target(int num_cus, bool wave) {
     return wave ? (1 << 30) : VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
   }
+  // chunks per segment of the one-wave K1's plan (the testing switch's value if it sets one)
+  int wave_chunks(int64_t n_obs) const {
+    (void)n_obs;
+    return ctx_->ba_k1_variant >= 1 ? std::min(ctx_->ba_k1_variant, kWaveMaxChunks) : 1;
+  }
 
   LinArgs lin_args() {
     const BAPlan& P = plan_;
@@ -2181,20 +2262,26 @@ class BAEngine {
     LinArgs A = lin_args();
     // one-wave K1 for plans of one chunk per segment (the chunk image of segment s is chunk s)
     const bool wave = plan_is_wave(plan_.seg_obs);
-    VO_REQUIRE(!wave || nseg == plan_.n_chunks(), VO_ERR_STATE, "K1: segments of one chunk expected");
+    const int nw = wave ? plan_.seg_chunks : 1;
+    VO_REQUIRE(!wave || ((int64_t)nseg * nw == plan_.n_chunks() && nw >= 1 && nw <= kWaveMaxChunks), VO_ERR_STATE,
+               "K1: segments of seg_chunks chunks expected");
     A.nseg = nseg;
-    dim3 g(nseg), b(wave ? kLinLanesWave : kLinThreads);
+    dim3 g(nseg), b(wave ? kLinLanesWave * nw : kLinThreads);
     ctx_->prof.begin(ctx_->stream, kKBaLin);
-    if (stamps_on_) {
-      d_stamps_.reserve((size_t)nseg * kPhCount * 8);
+    if (stamps_on_) {  // one row per chunk (one-wave K1) or segment (four-wave K1)
+      d_stamps_.reserve((size_t)plan_.n_chunks() * kPhCount * 8);
       A.stamps = d_stamps_.as<unsigned long long>();
     }
-#define VO_LIN_LAUNCH(M)                                                                    \
-  do {                                                                                      \
-    if (wave)                                                                               \
-      hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_>), g, b, 0, ctx_->stream, A);   \
-    else                                                                                    \
-      hipLaunchKernelGGL((ba_lin_kernel<M, stamps_on_>), g, b, 0, ctx_->stream, A);        \
+#define VO_LIN_LAUNCH(M)                                                                      \
+  do {                                                                                        \
+    if (wave && nw == 3)                                                                      \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 3>), g, b, 0, ctx_->stream, A);  \
+    else if (wave && nw == 2)                                                                 \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 2>), g, b, 0, ctx_->stream, A);  \
+    else if (wave)                                                                            \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 1>), g, b, 0, ctx_->stream, A);  \
+    else                                                                                      \
+      hipLaunchKernelGGL((ba_lin_kernel<M, stamps_on_>), g, b, 0, ctx_->stream, A);          \
   } while (0)
     switch (mode) {
       case kAccum: VO_LIN_LAUNCH(kAccum); break;
@@ -2397,7 +2484,8 @@ class BAEngine {
   // Diagnostic: per-phase cycle sums of the last K1 launch (VO_BA_STAMPS=1 builds).
   int read_stamps(uint64_t* out, int n) {
     if (!stamps_on_) return 0;
-    const int nseg = plan_.n_segments();
+    // rows: chunks of a wave plan, segments of a four-wave plan
+    const int nseg = plan_is_wave(plan_.seg_obs) ? plan_.n_chunks() : plan_.n_segments();
     std::vector<unsigned long long> h((size_t)nseg * kPhCount);
     VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
     VO_HIP_CHECK(hipMemcpy(h.data(), d_stamps_.ptr, h.size() * 8, hipMemcpyDeviceToHost));

@@ -222,7 +222,6 @@ struct PlanPart {
 #define VO_BA_COPY_CHAIN 21
 #endif
 constexpr int kCopyChain = VO_BA_COPY_CHAIN;  // one-wave K1: weighted chain below which no copy is made
-constexpr int kWaveItems = 60;                 // its lanes for slot copies (the combine's LDS scratch)
 
 int seg_obs_for(int64_t n_obs, int target_segments) {
   const int64_t t = std::max(1, target_segments);
@@ -238,7 +237,7 @@ int seg_obs_grid(int64_t x) {
 
 void BAPlan::reset() {
   n_poses = n_points = n_obs = n_fixed = n_free = n_te = 0;
-  seg_obs = reused_groups = reused_chunks = 0;
+  seg_obs = seg_chunks = reused_groups = reused_chunks = 0;
   group_q.clear();
   group_chunk.clear();
   group_seg.clear();
@@ -262,7 +261,8 @@ void BAPlan::reset() {
 }
 
 std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_t* point_ptr,
-                       const int32_t* obs_cam, const float* obs_uv, int seg_obs, const BAPlan* prev) {
+                       const int32_t* obs_cam, const float* obs_uv, int seg_obs, const BAPlan* prev,
+                       int seg_chunks) {
 #ifdef VO_PLAN_TIMING
   auto t_ = std::chrono::steady_clock::now();
 #endif
@@ -279,7 +279,14 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   P.n_fixed = n_fixed;
   P.n_free = N - n_fixed;
   P.seg_obs = std::max(1, seg_obs);
-  const bool wave = plan_is_wave(P.seg_obs);  // the one-wave K1's images (segments of one chunk)
+  const bool wave = plan_is_wave(P.seg_obs);  // the one-wave K1's images
+  if (wave && (seg_chunks < 1 || seg_chunks > kWaveMaxChunks))
+    return fmt("seg_chunks=%ld outside 1..%ld", seg_chunks, kWaveMaxChunks);
+  P.seg_chunks = wave ? seg_chunks : 0;
+  // wave plans of several chunks per segment: segments padded to seg_chunks chunks, and a
+  // window of at most kWaveItems slots (every chunk's blocks fit the combine's scratch rows)
+  const int group_nch = wave && seg_chunks > 1 ? seg_chunks : 0;
+  const int max_slots = group_nch ? kWaveItems : kSegSlots;
   const int nthr = plan_threads(M);
 
   PlanArr<int32_t> ob_start(L + 1), sorted(std::max(M, 1)), te_start(L + 1);
@@ -410,7 +417,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   const bool tables = Nf <= kPlanTableCams;
   const int nparts = N + 1;
   std::vector<PlanPart> parts(nparts);
-  const bool reuse = prev && prev != &P && prev->seg_obs == P.seg_obs && prev->n_fixed == n_fixed &&
+  const bool reuse = prev && prev != &P && prev->seg_obs == P.seg_obs && prev->seg_chunks == P.seg_chunks &&
+                     prev->n_fixed == n_fixed &&
                      (int)prev->group_q.size() == prev->n_poses + 2;
   // group g equals the previous plan's group g + s: the same landmarks in the same order, their
   // cameras s lower, the same observations (uv bit for bit)
@@ -467,7 +475,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     std::vector<int32_t> pair_stamp(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, -1);
     std::vector<int32_t> pair_sidx(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, 0);
     std::vector<int32_t> cq;
-    int c_obs = 0, c_te = 0, c_pts = 0, c_pairs = 0;
+    int c_obs = 0, c_te = 0, c_pts = 0, c_pairs = 0, s_nch = 0;
     int64_t s_obs = 0;
     bool seg_open = false;
     auto open_chunk = [&](int q) {
@@ -476,6 +484,13 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       R.chunk_fte.push_back(0);
       R.chunk_fobs.push_back(0);
       c_obs = c_te = c_pts = c_pairs = 0;
+      ++s_nch;
+    };
+    // the open segment padded to group_nch chunks by empty chunks at landmark q (none of its
+    // landmarks: q starts the next chunk)
+    auto pad_segment = [&](int q) {
+      if (!seg_open) return;
+      while (s_nch < group_nch) open_chunk(q);
     };
     for (int q = qa; q < qb; ++q) {
       const int t0 = P.pt_te[q], t1 = P.pt_te[q + 1];
@@ -524,12 +539,14 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
             }
           for (int t = t0; t < t1; ++t) nacams += find_or_neg(s.acams, P.te_cam[t]) < 0;
         }
-        seg_fits = ncams <= kSegCams && nslots <= kSegSlots && nacams <= kSegAllCams;
+        seg_fits = ncams <= kSegCams && nslots <= max_slots && nacams <= kSegAllCams;
       }
-      if (!seg_fits || (!chunk_fits && s_obs >= seg_obs_target)) {
+      if (!seg_fits || (!chunk_fits && (group_nch ? s_nch >= group_nch : s_obs >= seg_obs_target))) {
+        pad_segment(q);
         R.segs.push_back(PlanSeg{(int)R.chunk_q.size(), {}, {}, {}});
         seg_open = true;
         s_obs = 0;
+        s_nch = 0;
         open_chunk(q);
       } else if (!chunk_fits) {
         open_chunk(q);
@@ -586,6 +603,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       R.chunk_fte.back() += k;
       R.chunk_fobs.back() += fobs;
     }
+    pad_segment(qb);
   };
   run_parallel(std::min(nparts, nthr), [&](int t) {
     const int nt = std::min(nparts, nthr);
@@ -1166,6 +1184,7 @@ uint64_t plan_digest(const BAPlan& P) {
   vec(P.solve_tab);
   const int32_t so = P.seg_obs;
   bytes(&so, sizeof so);
+  if (P.seg_chunks > 1) bytes(&P.seg_chunks, sizeof P.seg_chunks);  // (plans of one chunk per segment: as before)
   vec(P.group_q); vec(P.group_chunk); vec(P.group_seg);
   return h;
 }

@@ -52,12 +52,17 @@ constexpr int kChunkTe = VO_CHUNK_OBS;
 constexpr int kChunkPts = VO_CHUNK_OBS / 2;
 constexpr int kChunkPairs = 8 * VO_CHUNK_OBS;  // camera-pair (x, y) entries of one chunk, staged in LDS
 constexpr int kSegSlots = 64;
-// K1 variants (a plan property): segments of one chunk (seg_obs == 1) run the one-wave K1
-// (one 64-lane workgroup per chunk, one lane per Schur slot block); any other packing runs the
-// four-wave K1 walking its segment's chunks (one pass of 256 lanes, one lane per block row).
+// K1 variants (a plan property): wave plans (seg_obs == 1) run the one-wave K1, one 64-lane wave
+// per chunk, one lane per Schur slot block; a segment holds seg_chunks chunks of one
+// first-camera group (padded with empty chunks: chunk = segment * seg_chunks + wave), whose
+// waves share one workgroup and sum their slot blocks in LDS in chunk order (one slab row per
+// segment slot).  Any other packing runs the four-wave K1 walking its segment's chunks (one
+// pass of 256 lanes, one lane per block row).
 constexpr int kLinLanesWave = 64;   // one-wave K1 lanes (ba.hip ba_lin_wave_kernel)
 constexpr int kLinLanes = 256;      // four-wave K1 lanes per Schur pass (ba.hip kLinThreads)
 inline bool plan_is_wave(int seg_obs) { return seg_obs == 1; }
+constexpr int kWaveMaxChunks = 3;  // chunks (waves) per segment of a wave plan (ba.hip instantiates 1..3)
+constexpr int kWaveItems = 60;     // one-wave K1 lanes for slot items (the scratch rows of the combine)
 constexpr int kChunkHdr = 16;
 
 constexpr int kSegCams = 24;     // free (window) cameras of a segment
@@ -237,6 +242,7 @@ struct BAPlan {
   // segment as the packing target.  group_q / group_chunk / group_seg: per first camera c
   // (0 .. N; N = landmarks without observations) its first landmark, chunk and segment.
   int seg_obs = 0;
+  int seg_chunks = 0;  // wave plans: chunks per segment (1 .. kWaveMaxChunks); 0 otherwise
   std::vector<int32_t> group_q, group_chunk, group_seg;
   // Not part of the plan (never digested): how it was built.  chunk_src[c] = the chunk of
   // the previous plan whose image chunk c copies (an incremental build), -1 if rebuilt;
@@ -267,9 +273,10 @@ int seg_obs_grid(int64_t x);
 // by one keyframe) or at the same camera (the window grew, or the same window again) takes
 // over that group's chunks and segments: lists and images copied, offsets and camera ids
 // shifted, nothing repacked.  The result is the same plan, byte for byte, as without prev.
+// seg_chunks: chunks per segment of a wave plan (seg_obs == 1; ignored otherwise).
 std::string build_plan(BAPlan& plan, int n_poses, int n_points, int n_obs, int n_fixed,
                        const int32_t* point_ptr, const int32_t* obs_cam, const float* obs_uv,
-                       int seg_obs, const BAPlan* prev = nullptr);
+                       int seg_obs, const BAPlan* prev = nullptr, int seg_chunks = 1);
 // first[i] of each free block row touched by this plan (i if untouched).
 std::vector<int32_t> local_profile_first(const BAPlan& plan);
 // Builds the profile and the K2 reduction index from a (possibly all-reduced) first[].

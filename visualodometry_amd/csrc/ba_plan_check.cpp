@@ -7,12 +7,17 @@
 //   - a diagonal slot's pairs (over its copies) are (x, x) over exactly its camera's track entries
 //     (so its lanes' U sums equal the camera lists'), adcam names the camera, off-diagonal 0xFF;
 //     one-wave K1: each item's U observation range (auo) is exactly its pairs' observations;
-//   - with one chunk per segment, every window slot is active and every window camera has a
-//     diagonal slot (every slab row and rhs entry is written).
+//   - one-wave K1: every window slot is active and every window camera has a diagonal slot in
+//     some chunk of its segment (every slab row and rhs entry is written); a segment of several
+//     chunks (seg_chunks > 1) has exactly seg_chunks of them (padded with empty chunks), all of
+//     one first-camera group, at most kWaveItems window slots and items per chunk (the combine's
+//     scratch rows).
 // Input (binary): int32 n_poses, n_points, n_obs, n_fixed, seg_obs; point_ptr; obs_cam; obs_uv.
+// Optional argv[2]: seg_chunks (wave plans; default 1).
 // Prints "ok <chunks> <segments> <passes> <max chain (pair rows)>" or the first violation.
 #include <cstdio>
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -49,19 +54,30 @@ int main(int argc, char** argv) {
   std::fclose(f);
   vo::BAPlan P;
   const bool wave = vo::plan_is_wave(so);
-  const std::string err = vo::build_plan(P, N, L, M, nf, ptr.data(), cam.data(), uv.data(), so, nullptr);
+  const int sc = argc > 2 ? std::atoi(argv[2]) : 1;
+  const std::string err = vo::build_plan(P, N, L, M, nf, ptr.data(), cam.data(), uv.data(), so, nullptr, sc);
   if (!err.empty()) FAIL("plan: %s", err.c_str());
+  if (wave && P.seg_chunks != sc) FAIL("plan seg_chunks %d, asked %d", P.seg_chunks, sc);
   long passes = 0;
   int max_chain = 0;
   for (int si = 0; si < P.n_segments(); ++si) {
     const int32_t* sh = &P.seg_hdr[(size_t)si * vo::kSegHdr];
     const int nslots = sh[0], so_ = sh[1], co = sh[2], ncams = sh[3];
-    const bool one = sh[6] - sh[5] == 1;
     std::vector<int> slot_seen(nslots, 0), cam_diag(ncams, 0);
+    if (wave) {
+      if (sh[6] - sh[5] != sc || sh[5] != si * sc) FAIL("segment %d: chunks [%d, %d), seg_chunks %d", si, sh[5], sh[6], sc);
+      if (sc > 1 && nslots > vo::kWaveItems) FAIL("segment %d: %d window slots", si, nslots);
+      // one first-camera group: the segment's landmarks inside one group's range
+      const int q0 = P.chunk_pt[sh[5]], q1 = P.chunk_pt[sh[6]];
+      int g = 0;
+      while (g + 1 < (int)P.group_q.size() && P.group_q[g + 1] <= q0 && P.group_q[g + 1] < q1) ++g;
+      if (q1 > q0 && (q0 < P.group_q[g] || q1 > P.group_q[g + 1])) FAIL("segment %d crosses a first-camera group", si);
+    }
     for (int ch = sh[5]; ch < sh[6]; ++ch) {
       const int32_t* h = &P.chunk_hdr[(size_t)ch * vo::kChunkHdr];
       const vo::ChunkImg& g = P.chunk_img[ch];
       const int nas = h[14], lanes = g.abase[nas], npairs = h[9] - h[8];
+      if (wave && sc > 1 && nas > vo::kWaveItems) FAIL("chunk %d: %d items", ch, nas);
       std::vector<int> cover(6 * (size_t)npairs, 0);
       const int plane = wave ? vo::kLinLanesWave : vo::kLinLanes;
       for (int base = 0; base < lanes; base += plane, ++passes) {
@@ -137,7 +153,7 @@ int main(int argc, char** argv) {
         if (!upairs[wc].empty() && upairs[wc] != want) FAIL("chunk %d: camera %d track entries (U) differ", ch, wc);
       }
     }
-    if (one) {
+    if (wave) {
       for (int s = 0; s < nslots; ++s)
         if (!slot_seen[s]) FAIL("segment %d: window slot %d never written", si, s);
       for (int c = 0; c < ncams; ++c)
@@ -145,5 +161,6 @@ int main(int argc, char** argv) {
     }
   }
   std::printf("ok %d %d %ld %d\n", P.n_chunks(), P.n_segments(), passes, max_chain);
+  std::fprintf(stderr, "slab_slots %d\n", P.n_slab_slots());
   return 0;
 }
