@@ -68,14 +68,14 @@ def test_run_matches_c_oracle(ctx, cfg):
 
 def test_cfg4_matches_c_oracle(ctx):
     """100 poses x 200k landmarks: the profile (225 KB) exceeds LDS; the banded K3 streams
-    it through its LDS rings.  K1 is the default one-wave K1 (one chunk per segment: 13.7k
-    workgroups, nine rounds)."""
+    it through its LDS rings.  K1 is the default one-wave K1 (three chunks of one first-camera
+    group per segment: 4.6k workgroups of three waves, nine rounds)."""
     p = make_ba_config("cfg4")
     s = _session(p, ctx)
     st = s.plan_stats()
     assert st["profile_blocks"] * 288 > 150 * 1024
     assert st["band_solver"] == 1
-    assert st["seg_obs"] == 1 and st["segments"] == st["chunks"], st
+    assert st["seg_obs"] == 1 and st["chunks"] == 3 * st["segments"], st
     rc, costs = s.run(3)
     assert rc == _lib.VO_OK
     R = cref.BAProblemRef(p.K, p.point_ptr, p.obs_cam, p.obs_uv, p.n_poses, p.n_fixed, 1.0)

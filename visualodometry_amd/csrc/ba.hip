@@ -2223,10 +2223,13 @@ class BAEngine {
   static int segments_target(int num_cus, bool wave) {
     return wave ? (1 << 30) : VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
   }
-  // chunks per segment of the one-wave K1's plan (the testing switch's value if it sets one)
+  // Chunks per segment of the one-wave K1's plan (the testing switch's value if it sets one):
+  // three at every size -- a third of the slab rows K2 reads for a barrier per segment; cfg3
+  // 14.89k -> 15.27k GN-iters/s (42 148 -> 15 538 rows), cfg4 3.91k -> 4.04k (K2 34 -> 16 us,
+  // K1 148 -> 158 us); two chunks sit between (profiles/r05_k1g)
   int wave_chunks(int64_t n_obs) const {
     (void)n_obs;
-    return ctx_->ba_k1_variant >= 1 ? std::min(ctx_->ba_k1_variant, kWaveMaxChunks) : 1;
+    return ctx_->ba_k1_variant >= 1 ? std::min(ctx_->ba_k1_variant, kWaveMaxChunks) : kWaveMaxChunks;
   }
 
   LinArgs lin_args() {
