@@ -38,11 +38,12 @@ int vo_ba_testing_drop_reducers(vo_ctx* ctx, int n);
 int vo_ba_testing_k1(vo_ctx* ctx, int variant);
 
 /* Host only: the digest (as vo_ba_plan_digest) of the plan of `cur` packed for seg_obs
- * observations per segment, built from scratch when prev is NULL, else after a from-scratch
- * plan of `prev` (same seg_obs) as vo_ba_setup builds it on a window slide: taking over
- * prev's unchanged first-camera groups.  *reused_chunks (may be NULL): chunks taken over. */
-int vo_ba_testing_plan_slide(const vo_ba_problem* prev, const vo_ba_problem* cur, int seg_obs, uint64_t* digest,
-                             int64_t* reused_chunks);
+ * observations per segment (seg_obs 1: the one-wave K1's plan of seg_chunks chunks per
+ * segment), built from scratch when prev is NULL, else after a from-scratch plan of `prev`
+ * (same packing) as vo_ba_setup builds it on a window slide: taking over prev's unchanged
+ * first-camera groups.  *reused_chunks (may be NULL): chunks taken over. */
+int vo_ba_testing_plan_slide(const vo_ba_problem* prev, const vo_ba_problem* cur, int seg_obs, int seg_chunks,
+                             uint64_t* digest, int64_t* reused_chunks);
 
 #ifdef __cplusplus
 }

@@ -228,6 +228,23 @@ def test_slide_plan_equals_scratch_plan():
         assert reused >= 0.7 * st["chunks"], (reused, st["chunks"])
 
 
+@pytest.mark.parametrize("seg_chunks", [1, 3])
+def test_wave_plan_slide_equals_scratch_plan(seg_chunks):
+    """The one-wave K1's plans (one or three chunks per segment; padded segments of one
+    first-camera group) taken over on a slide equal the scratch plans byte for byte."""
+    from visualodometry_amd.ba import plan_slide_digest
+    from visualodometry_amd.synthetic import make_ba_slide
+
+    ws = make_ba_slide("cfg3", 3)
+    for a, b in zip(ws, ws[1:]):
+        d_inc, reused = plan_slide_digest(a.K, _win(a), _win(b), 1, seg_chunks)
+        d_new, none = plan_slide_digest(a.K, None, _win(b), 1, seg_chunks)
+        assert d_inc == d_new and none == 0 and reused > 1000
+    d1 = plan_slide_digest(ws[0].K, None, _win(ws[1]), 1, 1)[0]
+    d3 = plan_slide_digest(ws[0].K, None, _win(ws[1]), 1, 3)[0]
+    assert d1 != d3  # three chunks per segment: another plan
+
+
 def test_grown_and_repeated_window_plans_equal_scratch():
     """A window that grew by one keyframe (no eviction: groups keep their cameras) and the
     same window again take groups over at the same camera; the plans equal scratch plans."""

@@ -107,7 +107,7 @@ SIGNATURES = {
     "vo_ba_split_reduce": (_I, [_P, _I]),
     "vo_ba_testing_drop_reducers": (_I, [_P, _I]),
     "vo_ba_testing_k1": (_I, [_P, _I]),
-    "vo_ba_testing_plan_slide": (_I, [C.c_void_p, C.c_void_p, _I, C.POINTER(C.c_uint64), _PI64]),
+    "vo_ba_testing_plan_slide": (_I, [C.c_void_p, C.c_void_p, _I, _I, C.POINTER(C.c_uint64), _PI64]),
 }
 
 _lib = None

@@ -153,9 +153,10 @@ def plan_digest(K, point_ptr, obs_cam, obs_uv, n_poses: int, n_fixed: int = 2, t
     return int(d.value)
 
 
-def plan_slide_digest(K, prev, cur, seg_obs: int) -> tuple:
+def plan_slide_digest(K, prev, cur, seg_obs: int, seg_chunks: int = 1) -> tuple:
     """Host-only (test): ``(digest, reused_chunks)`` of the plan of window ``cur`` packed for
-    ``seg_obs`` observations per segment, built from scratch (``prev`` None) or by taking over
+    ``seg_obs`` observations per segment (1: the one-wave K1's plan of ``seg_chunks`` chunks per
+    segment), built from scratch (``prev`` None) or by taking over
     the unchanged first-camera groups of ``prev``'s plan, as ``vo_ba_setup`` does on a slide
     (``vo_ba_testing_plan_slide``).  Windows: ``(point_ptr, obs_cam, obs_uv, n_poses, n_fixed)``."""
     keep = []
@@ -172,7 +173,7 @@ def plan_slide_digest(K, prev, cur, seg_obs: int) -> tuple:
     d = C.c_uint64(0)
     r = C.c_int64(0)
     check(_lib.load().vo_ba_testing_plan_slide(C.byref(pv) if pv is not None else None, C.byref(pc), int(seg_obs),
-                                               C.byref(d), C.byref(r)), "vo_ba_testing_plan_slide")
+                                               int(seg_chunks), C.byref(d), C.byref(r)), "vo_ba_testing_plan_slide")
     return int(d.value), int(r.value)
 
 

@@ -629,15 +629,16 @@ int vo_ba_plan_digest(const vo_ba_problem* prob, int target_segments, uint64_t* 
   });
 }
 
-int vo_ba_testing_plan_slide(const vo_ba_problem* prev, const vo_ba_problem* cur, int seg_obs, uint64_t* digest,
-                             int64_t* reused_chunks) {
+int vo_ba_testing_plan_slide(const vo_ba_problem* prev, const vo_ba_problem* cur, int seg_obs, int seg_chunks,
+                             uint64_t* digest, int64_t* reused_chunks) {
   return guarded([&] {
     VO_REQUIRE(cur && digest && seg_obs >= 1, VO_ERR_ARG, "vo_ba_testing_plan_slide: bad argument");
     std::vector<int32_t> zero(1, 0);
     vo::BAPlan A, B;
     auto build = [&](vo::BAPlan& P, const vo_ba_problem* p, const vo::BAPlan* from) {
       std::string err = vo::build_plan(P, p->n_poses, p->n_points, p->n_obs, p->n_fixed,
-                                       p->n_points ? p->point_ptr : zero.data(), p->obs_cam, p->obs_uv, seg_obs, from);
+                                       p->n_points ? p->point_ptr : zero.data(), p->obs_cam, p->obs_uv, seg_obs, from,
+                                       seg_chunks);
       VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_testing_plan_slide: %s", err.c_str());
       vo::build_profile(P, vo::local_profile_first(P));
     };
