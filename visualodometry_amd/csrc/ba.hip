@@ -1357,23 +1357,25 @@ __global__ __launch_bounds__(kLinLanesWave * NW) void ba_lin_wave_kernel(LinArgs
 // K2: fixed-order reduction of the slabs into [S profile | b | cost] (ReduceArgs, sum_rows:
 // ba_reduce.h).
 
-// One workgroup per profile block: 7 strided partial sums per S entry and, on a
-// diagonal block, 42 per rhs entry of that camera, combined in fixed order (the
-// result is bitwise reproducible).  The last workgroup sums the cost.  Every load of a
+// One workgroup per profile block: 14 strided partial sums per S entry (16-byte loads) and, on
+// a diagonal block, 42 per rhs entry of that camera, combined in fixed order (the result is
+// bitwise reproducible).  The last workgroup sums the cost.  Every load of a
 // workgroup is issued before the status test (a failed earlier step: nothing is written).
 __global__ __launch_bounds__(kRedThreads) void ba_reduce_kernel(ReduceArgs A) {
-  __shared__ double part[kRedSParts * 36], partb[kRedBParts * 6];
+  __shared__ __attribute__((aligned(16))) double part[kRedSParts * 36];
+  __shared__ double partb[kRedBParts * 6];
   const int blk = blockIdx.x, tid = threadIdx.x;
   if (blk < A.nprof) {
     const int4 m = A.meta[blk];
     const int2 o = A.out[blk];
     const int failed = A.status ? *A.status : 0;
     const bool diag = m.z >= 0;
-    double ps = 0.0, pb = 0.0;
-    if (tid < kRedSParts * 36) ps = sum_rows<36>(A.slab, m.x, m.y, tid / 36, kRedSParts, tid % 36);
+    double2 ps = make_double2(0.0, 0.0);
+    double pb = 0.0;
+    if (tid < kRedSParts * 18) ps = sum_rows2(A.slab, m.x, m.y, tid / 18, kRedSParts, tid % 18);
     if (diag && tid < kRedBParts * 6) pb = sum_rows<6>(A.slab_b, m.z, m.w, tid / 6, kRedBParts, tid % 6);
     if (failed) return;  // uniform
-    if (tid < kRedSParts * 36) part[tid] = ps;
+    if (tid < kRedSParts * 18) reinterpret_cast<double2*>(part)[tid] = ps;
     if (tid < kRedBParts * 6) partb[tid] = pb;
     __syncthreads();
     if (tid < 36) {

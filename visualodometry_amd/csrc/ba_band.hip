@@ -223,11 +223,12 @@ __device__ __forceinline__ void band_reduce_wg(const BandArgs& B, int r, double*
   const bool isblk = blk < A.nprof, iscost = blk == A.nprof;
   int4 m = make_int4(0, 0, -1, 0);
   int2 o = make_int2(0, 0);
-  double ps = 0.0, pb = 0.0, c = 0.0;
+  double2 ps = make_double2(0.0, 0.0);
+  double pb = 0.0, c = 0.0;
   if (isblk) {
     m = A.meta[blk];
     o = A.out[blk];
-    if (t < kRedSParts * 36) ps = sum_rows<36>(A.slab, m.x, m.y, t / 36, kRedSParts, t % 36);
+    if (t < kRedSParts * 18) ps = sum_rows2(A.slab, m.x, m.y, t / 18, kRedSParts, t % 18);
     if (m.z >= 0 && t < kRedBParts * 6) pb = sum_rows<6>(A.slab_b, m.z, m.w, t / 6, kRedBParts, t % 6);
   } else if (iscost && A.nseg > 0) {
     for (int s = t; s < A.nseg; s += 4 * kRedThreads) {
@@ -240,7 +241,7 @@ __device__ __forceinline__ void band_reduce_wg(const BandArgs& B, int r, double*
   }
   const bool failed = A.status && *A.status;  // a failed earlier step: nothing is written
   if (isblk) {
-    if (t < kRedSParts * 36) part[t] = ps;
+    if (t < kRedSParts * 18) reinterpret_cast<double2*>(part)[t] = ps;
     if (t < kRedBParts * 6) partb[t] = pb;
   } else if (iscost) {
     cpart[t] = c;

@@ -51,11 +51,32 @@ __device__ __forceinline__ double sum_rows(const double* __restrict__ slab, int 
   return acc;
 }
 
+// The same for 36-double S rows with 16-byte loads: lane (part, e2) sums entries 2 e2, 2 e2 + 1
+// of rows k0 + part + j * stride in fixed order (18 lanes cover a row's 288 contiguous bytes).
+__device__ __forceinline__ double2 sum_rows2(const double* __restrict__ slab, int k0, int k1, int part, int stride,
+                                             int e2) {
+  double2 acc = make_double2(0.0, 0.0);
+  if (k1 <= k0) return acc;
+  const double2* __restrict__ s2 = reinterpret_cast<const double2*>(slab);
+  for (int k = k0 + part; k < k1; k += kRedBatch * stride) {
+    double2 v[kRedBatch];
+#pragma unroll
+    for (int i = 0; i < kRedBatch; ++i) v[i] = s2[18l * min(k + i * stride, k1 - 1) + e2];
+#pragma unroll
+    for (int i = 0; i < kRedBatch; ++i) {
+      const bool on = k + i * stride < k1;
+      acc.x += on ? v[i].x : 0.0;
+      acc.y += on ? v[i].y : 0.0;
+    }
+  }
+  return acc;
+}
+
 #ifndef VO_RED_THREADS
 #define VO_RED_THREADS 256
 #endif
 constexpr int kRedThreads = VO_RED_THREADS;
-constexpr int kRedSParts = kRedThreads / 36;  // partial sums per S block entry
+constexpr int kRedSParts = kRedThreads / 18;  // partial sums per S block entry (16-byte lanes: 18 per row)
 constexpr int kRedBParts = kRedThreads / 6;   // partial sums per rhs entry
 
 }  // namespace vo
