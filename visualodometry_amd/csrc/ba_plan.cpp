@@ -76,20 +76,20 @@ int host_threads() {
 // disjoint, precomputed ranges, so the plan never depends on the thread count or timing.
 // Workers persist across plans (thread creation would cost more than a small phase); a
 // caller that finds the pool busy (another context planning) starts its own threads.
-// Tuning builds only (EXTRA=-DVO_PLAN_SPIN_US=n): a worker that finished a phase, and the
-// caller waiting for one, poll for up to n microseconds before sleeping on the condition
-// variable (consecutive phases are tens of microseconds apart).
-#ifndef VO_PLAN_SPIN_US
-#define VO_PLAN_SPIN_US 0
+// While a plan is being built (PlanSession, one build_plan call: about half a millisecond of
+// consecutive phases tens of microseconds apart), the workers and the caller poll for the next
+// phase / the phase's end instead of sleeping on the condition variables: a futex wake of
+// fifteen threads costs about as much as a phase.  Between plans they sleep (polling there
+// would eat the job's CPU quota).  Tuning build: -DVO_PLAN_SESSION_SPIN=0 never polls.
+#ifndef VO_PLAN_SESSION_SPIN
+#define VO_PLAN_SESSION_SPIN 1
 #endif
-constexpr int kPlanSpinUs = VO_PLAN_SPIN_US;
+constexpr bool kPlanSessionSpin = VO_PLAN_SESSION_SPIN != 0;
 
-template <class Pred>
-void spin_until(Pred&& done) {
-  if (kPlanSpinUs <= 0) return;
-  const auto t0 = std::chrono::steady_clock::now();
-  while (!done() && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(kPlanSpinUs)) {
-  }
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#endif
 }
 
 class PlanPool {
@@ -137,13 +137,20 @@ class PlanPool {
     }
     cv_.notify_all();
     safe(0);
-    spin_until([&] { return pending_.load(std::memory_order_acquire) == 0; });
+    while (session_.load(std::memory_order_acquire) > 0 && pending_.load(std::memory_order_acquire) != 0) cpu_relax();
     {
       std::unique_lock<std::mutex> lk(mu_);
       done_.wait(lk, [&] { return pending_ == 0; });
       job_ = nullptr;
     }
     if (first) std::rethrow_exception(first);
+  }
+  // a plan is being built: workers poll between its phases (see kPlanSessionSpin)
+  void begin_session() {
+    if (kPlanSessionSpin) session_.fetch_add(1, std::memory_order_acq_rel);
+  }
+  void end_session() {
+    if (kPlanSessionSpin) session_.fetch_sub(1, std::memory_order_acq_rel);
   }
   ~PlanPool() {
     {
@@ -162,7 +169,7 @@ class PlanPool {
     long seen = 0;
     for (;;) {
       std::function<void(int)>* job;
-      spin_until([&] { return gen_.load(std::memory_order_acquire) != seen; });
+      while (session_.load(std::memory_order_acquire) > 0 && gen_.load(std::memory_order_acquire) == seen) cpu_relax();
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
@@ -182,9 +189,23 @@ class PlanPool {
   std::condition_variable cv_, done_;
   std::function<void(int)>* job_ = nullptr;
   int active_ = 0;
-  std::atomic<int> pending_{0};  // written under mu_; atomic for the optional spin
+  std::atomic<int> pending_{0};  // written under mu_; atomic for the polling
   std::atomic<long> gen_{0};
+  std::atomic<int> session_{0};  // plans being built (begin_session / end_session)
   bool stop_ = false;
+};
+
+// The polling window of one build_plan call (plans of one thread start no session).
+struct PlanSession {
+  bool on;
+  explicit PlanSession(bool multi) : on(multi) {
+    if (on) PlanPool::get().begin_session();
+  }
+  ~PlanSession() {
+    if (on) PlanPool::get().end_session();
+  }
+  PlanSession(const PlanSession&) = delete;
+  PlanSession& operator=(const PlanSession&) = delete;
 };
 
 template <class Fn>
@@ -288,6 +309,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   const int group_nch = wave && seg_chunks > 1 ? seg_chunks : 0;
   const int max_slots = group_nch ? kWaveItems : kSegSlots;
   const int nthr = plan_threads(M);
+  PlanSession session(nthr > 1);
 
   PlanArr<int32_t> ob_start(L + 1), sorted(std::max(M, 1)), te_start(L + 1);
   // landmarks ordered by first camera (stable counting sort; no observation: last), which
@@ -740,6 +762,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   };
   // a segment taken over from the previous plan: its lists and images copied, their offsets
   // moved to this plan's (the values fill() would compute from the same landmarks)
+  const bool host_images_pinned = P.chunk_img.get_allocator().pinned;
   auto fill_taken = [&](int si, const PlanSeg& s) {
     const BAPlan& Q = *prev;
     const int ps = s.src;
@@ -776,7 +799,10 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       int32_t* h = chunk_header(ch, ns, nc);
       h[14] = Q.chunk_hdr[(size_t)pc * kChunkHdr + 14];
       h[15] = Q.chunk_hdr[(size_t)pc * kChunkHdr + 15];
-      std::memcpy(&P.chunk_img[ch], &Q.chunk_img[pc], sizeof(ChunkImg));
+      // the engine's plans keep their images in page-locked memory, uncached for the CPU (a
+      // read is slow): they take images over on the device (d_chunk_img_prev_ -> d_chunk_img_)
+      // and leave the host copy unwritten; host-only plans (digests, probes) copy it
+      if (!host_images_pinned) std::memcpy(&P.chunk_img[ch], &Q.chunk_img[pc], sizeof(ChunkImg));
     }
     seg_header(si, s);
   };

@@ -272,7 +272,9 @@ int seg_obs_grid(int64_t x);
 // first-camera group whose landmarks equal a group of prev one camera later (the window slid
 // by one keyframe) or at the same camera (the window grew, or the same window again) takes
 // over that group's chunks and segments: lists and images copied, offsets and camera ids
-// shifted, nothing repacked.  The result is the same plan, byte for byte, as without prev.
+// shifted, nothing repacked.  The result is the same plan, byte for byte, as without prev --
+// except that a plan with page-locked images (the BA engine's) leaves the host copies of the
+// images it takes over unwritten: the engine copies them from the previous plan's device images.
 // seg_chunks: chunks per segment of a wave plan (seg_obs == 1; ignored otherwise).
 std::string build_plan(BAPlan& plan, int n_poses, int n_points, int n_obs, int n_fixed,
                        const int32_t* point_ptr, const int32_t* obs_cam, const float* obs_uv,
