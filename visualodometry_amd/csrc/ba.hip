@@ -1855,6 +1855,7 @@ class BAEngine {
     // the previous setup's chunk-image DMA may still read the page-locked images the
     // planner is about to rewrite (a setup that failed after its upload returns unsynced)
     VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
+    PLAN_T("setup: sync");
     have_problem_ = false;
     have_state_ = false;
     std::string err;
@@ -1908,6 +1909,7 @@ class BAEngine {
       if (err.empty() && agree[1] != -agree[2]) err = "ranks disagree on the number of free poses";
     }
     VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_setup: %s", err.c_str());
+    PLAN_T("setup: planned");
     // the largest plan array first: from page-locked memory the copy runs while the host
     // builds the profile and the K3 tables.  Images taken over from the previous plan are
     // copied on the device, in runs of consecutive chunks.
@@ -1930,7 +1932,7 @@ class BAEngine {
       }
       plan_ok_ = true;
     }
-    PLAN_T("setup: plan");
+    PLAN_T("setup: images");
     std::vector<int32_t> first = local_profile_first(plan_);
     if (ctx_->comm && ctx_->comm->nranks > 1 && !first.empty()) {
       DevBuf tmp;

@@ -316,7 +316,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   // keeps each workgroup's camera window narrow.  Per-thread histograms over landmark
   // ranges, offsets in (camera, range) order, then each range scatters its landmarks.
   {
-    std::vector<int32_t> first(L);
+    std::vector<int32_t> first(L), tecnt(L);
     const int nt = std::max(1, std::min(nthr, L / 1024 + 1));
     std::vector<int32_t> hist((size_t)nt * (N + 1), 0);
     std::vector<int32_t> bad_ptr(nt, -1), bad_obs(nt, -1);  // first violation of each range
@@ -337,9 +337,18 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         }
       int32_t* h = &hist[(size_t)t * (N + 1)];
       for (int p = pa; p < pb; ++p) {
-        int f = N;
-        for (int o = point_ptr[p]; o < point_ptr[p + 1]; ++o) f = std::min(f, (int)obs_cam[o]);
+        // first camera and track entries (distinct cameras; tracks are short)
+        int f = N, nte = 0;
+        const int o0 = point_ptr[p], o1 = point_ptr[p + 1];
+        for (int o = o0; o < o1; ++o) {
+          const int c = obs_cam[o];
+          f = std::min(f, c);
+          bool fresh = true;
+          for (int u = o0; u < o; ++u) fresh = fresh && obs_cam[u] != c;
+          nte += fresh;
+        }
         first[p] = f;
+        tecnt[p] = nte;
         ++h[f];
       }
     });
@@ -366,18 +375,32 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       for (int p = pa; p < pb; ++p) {
         const int32_t q = h[first[p]]++;
         P.pt_perm[q] = p;
-        ob_start[q + 1] = point_ptr[p + 1] - point_ptr[p];  // the prefix sum follows
+        ob_start[q + 1] = point_ptr[p + 1] - point_ptr[p];  // the prefix sums follow
+        te_start[q + 1] = tecnt[p];
       }
     });
   }
   PLAN_T("order");
 
-  // observations grouped by (landmark, camera) -> track entries.  Pass A sorts each
-  // landmark's observations by camera (stable) into its slot and counts its track
-  // entries; pass B writes every array at the prefix offsets.
+  // observations grouped by (landmark, camera) -> track entries: one pass per landmark sorts
+  // its observations by camera (stable) into its slot and writes every array at the prefix
+  // offsets (the track-entry counts came with the order)
   ob_start[0] = 0;
-  for (int q = 0; q < L; ++q) ob_start[q + 1] += ob_start[q];
+  te_start[0] = 0;
+  for (int q = 0; q < L; ++q) {
+    ob_start[q + 1] += ob_start[q];
+    te_start[q + 1] += te_start[q];
+  }
   auto qrange = [&](int t, int n) { return std::make_pair((int)((int64_t)L * t / n), (int)((int64_t)L * (t + 1) / n)); };
+  P.n_te = te_start[L];
+  P.obs_uv.resize(2 * (size_t)M);
+  P.obs_cam.resize(M);
+  P.obs_te.resize(M);
+  P.te_cam.resize(P.n_te);
+  P.te_pt.resize(P.n_te);
+  P.te_obs.resize(P.n_te + 1);
+  P.te_lcam.resize(P.n_te);
+  P.pt_te.resize(L + 1);
   run_parallel(nthr, [&](int t) {
     const auto [qa, qb] = qrange(t, nthr);
     for (int q = qa; q < qb; ++q) {
@@ -392,24 +415,6 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         }
         idx[j] = v;
       }
-      int nte = 0;
-      for (int k = 0; k < n; ++k) nte += k == 0 || obs_cam[idx[k]] != obs_cam[idx[k - 1]];
-      te_start[q + 1] = nte;
-    }
-  });
-  te_start[0] = 0;
-  for (int q = 0; q < L; ++q) te_start[q + 1] += te_start[q];
-  P.n_te = te_start[L];
-  P.obs_uv.resize(2 * (size_t)M);
-  P.obs_cam.resize(M);
-  P.obs_te.resize(M);
-  P.te_cam.resize(P.n_te);
-  P.te_pt.resize(P.n_te);
-  P.te_obs.resize(P.n_te + 1);
-  P.pt_te.resize(L + 1);
-  run_parallel(nthr, [&](int t) {
-    const auto [qa, qb] = qrange(t, nthr);
-    for (int q = qa; q < qb; ++q) {
       int te = te_start[q] - 1;
       P.pt_te[q] = te_start[q];
       for (int pos = ob_start[q]; pos < ob_start[q + 1]; ++pos) {
@@ -419,6 +424,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
           P.te_cam[te] = obs_cam[o];
           P.te_pt[te] = q;
           P.te_obs[te] = pos;
+          P.te_lcam[te] = -1;  // window camera: set by the packing (free cameras)
         }
         P.obs_uv[2 * (size_t)pos] = obs_uv[2 * (size_t)o];
         P.obs_uv[2 * (size_t)pos + 1] = obs_uv[2 * (size_t)o + 1];
@@ -429,7 +435,6 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   });
   P.pt_te[L] = P.n_te;
   P.te_obs[P.n_te] = M;
-  P.te_lcam.assign(P.n_te, -1);
   PLAN_T("track entries");
 
   // ---- chunks and segments: each first-camera group packed greedily on its own (so a
@@ -627,10 +632,12 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     }
     pad_segment(qb);
   };
-  run_parallel(std::min(nparts, nthr), [&](int t) {
-    const int nt = std::min(nparts, nthr);
-    for (int pi = t; pi < nparts; pi += nt) pack(pi);
-  });
+  {  // groups handed out one at a time (taken-over groups cost little, packed ones more)
+    std::atomic<int> next{0};
+    run_parallel(std::min(nparts, nthr), [&](int) {
+      for (int pi = next.fetch_add(1); pi < nparts; pi = next.fetch_add(1)) pack(pi);
+    });
+  }
   for (const PlanPart& R : parts)  // the first error in landmark order
     if (R.err_q >= 0) return R.err;
   // merge the groups: chunks and segments in landmark order
@@ -806,13 +813,18 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     }
     seg_header(si, s);
   };
-  auto fill = [&](int sa, int sbnd) {
+  // segments handed out in batches from a shared counter (dynamic scheduling: on a slide the
+  // freshly packed segments, the expensive ones, are the newest groups, all at the end)
+  std::atomic<int> fill_next{0};
+  constexpr int kFillBatch = 4;
+  auto fill = [&]() {
     // per-thread lookup tables (camera -> window index, camera pair -> slot) and counting-sort buffers
     std::vector<int32_t> fcam_idx(tables ? std::max(Nf, 1) : 0, -1), acam_idx(tables ? N : 0, -1);
     std::vector<int32_t> pair_slot(tables ? (size_t)std::max(Nf, 1) * std::max(Nf, 1) : 0, -1);
     int32_t cnt[std::max(kSegSlots, kSegCams) + 1], cnt2[kSegCams + 1], pslot[kChunkPairs];
     uint16_t ptmp[kChunkPairs];
-    for (int si = sa; si < sbnd; ++si) {
+    for (int sa = fill_next.fetch_add(kFillBatch); sa < nseg; sa = fill_next.fetch_add(kFillBatch))
+    for (int si = sa; si < std::min(sa + kFillBatch, nseg); ++si) {
       PlanSeg& s = segs[si];
       if (s.src >= 0) {
         fill_taken(si, s);
@@ -1075,8 +1087,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     }
   };
   {
-    const int nt = std::max(1, std::min(nthr, nseg));
-    run_parallel(nt, [&](int t) { fill((int)((int64_t)nseg * t / nt), (int)((int64_t)nseg * (t + 1) / nt)); });
+    const int nt = std::max(1, std::min(nthr, (nseg + kFillBatch - 1) / kFillBatch));
+    run_parallel(nt, [&](int) { fill(); });
   }
   if (P.pair_list.empty()) P.pair_list.push_back(0);  // keep device arrays non-empty
   if (P.cam_list.empty()) P.cam_list.push_back(0);

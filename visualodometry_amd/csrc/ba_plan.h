@@ -199,7 +199,7 @@ struct BAPlan {
   PlanArr<int32_t> obs_cam, obs_te;
   // track entries
   PlanArr<int32_t> te_cam, te_pt, te_obs;  // te_obs: n_te+1
-  std::vector<int16_t> te_lcam;                // segment-local free camera, -1 if fixed
+  PlanArr<int16_t> te_lcam;                    // segment-local free camera, -1 if fixed
   PlanArr<int32_t> pt_te;                  // n_points+1
   // chunks
   std::vector<int32_t> chunk_obs, chunk_te, chunk_pt;  // n_chunks+1
