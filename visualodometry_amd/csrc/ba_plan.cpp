@@ -214,6 +214,26 @@ void run_parallel(int n, Fn&& fn) {
   PlanPool::get().run(n, fn);
 }
 
+// Plan arrays grow with a quarter of headroom: consecutive keyframe windows differ by a few
+// landmarks, and an exact-size reallocation (fresh pages to fault in; for the page-locked chunk
+// images a hipHostMalloc) on most calls cost more than the phase that fills the array.
+template <class V>
+void fit(V& v, size_t n) {
+  if (v.capacity() >= n) return;
+  v.clear();
+  v.reserve(n + n / 4 + 64);
+}
+template <class V>
+void sized(V& v, size_t n) {
+  fit(v, n);
+  v.resize(n);
+}
+template <class V, class T>
+void filled(V& v, size_t n, const T& x) {
+  fit(v, n);
+  v.assign(n, x);
+}
+
 int plan_threads(int64_t work) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), work / 2048 + 1));
 }
@@ -311,7 +331,12 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   const int nthr = plan_threads(M);
   PlanSession session(nthr > 1);
 
-  PlanArr<int32_t> ob_start(L + 1), sorted(std::max(M, 1)), te_start(L + 1);
+  PlanArr<int32_t>& ob_start = P.scr_ob_start;
+  PlanArr<int32_t>& sorted = P.scr_sorted;
+  PlanArr<int32_t>& te_start = P.scr_te_start;
+  sized(ob_start, L + 1);
+  sized(sorted, std::max(M, 1));
+  sized(te_start, L + 1);
   // landmarks ordered by first camera (stable counting sort; no observation: last), which
   // keeps each workgroup's camera window narrow.  Per-thread histograms over landmark
   // ranges, offsets in (camera, range) order, then each range scatters its landmarks.
@@ -357,7 +382,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     for (int t = 0; t < nt; ++t)
       if (bad_obs[t] >= 0) return fmt("obs_cam[%ld]=%ld out of range", bad_obs[t], obs_cam[bad_obs[t]]);
     int32_t off = 0;
-    P.group_q.resize(N + 2);
+    sized(P.group_q, N + 2);
     for (int c = 0; c <= N; ++c) {
       P.group_q[c] = off;
       for (int t = 0; t < nt; ++t) {
@@ -368,7 +393,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       }
     }
     P.group_q[N + 1] = off;
-    P.pt_perm.resize(L);
+    sized(P.pt_perm, L);
     run_parallel(nt, [&](int t) {
       const auto [pa, pb] = lrange(t);
       int32_t* h = &hist[(size_t)t * (N + 1)];
@@ -393,14 +418,14 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   }
   auto qrange = [&](int t, int n) { return std::make_pair((int)((int64_t)L * t / n), (int)((int64_t)L * (t + 1) / n)); };
   P.n_te = te_start[L];
-  P.obs_uv.resize(2 * (size_t)M);
-  P.obs_cam.resize(M);
-  P.obs_te.resize(M);
-  P.te_cam.resize(P.n_te);
-  P.te_pt.resize(P.n_te);
-  P.te_obs.resize(P.n_te + 1);
-  P.te_lcam.resize(P.n_te);
-  P.pt_te.resize(L + 1);
+  sized(P.obs_uv, 2 * (size_t)M);
+  sized(P.obs_cam, M);
+  sized(P.obs_te, M);
+  sized(P.te_cam, P.n_te);
+  sized(P.te_pt, P.n_te);
+  sized(P.te_obs, P.n_te + 1);
+  sized(P.te_lcam, P.n_te);
+  sized(P.pt_te, L + 1);
   run_parallel(nthr, [&](int t) {
     const auto [qa, qb] = qrange(t, nthr);
     for (int q = qa; q < qb; ++q) {
@@ -643,8 +668,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   // merge the groups: chunks and segments in landmark order
   std::vector<PlanSeg> segs;
   std::vector<int32_t> ch_pairs, ch_fte, ch_fobs;
-  P.group_chunk.resize(nparts + 1);
-  P.group_seg.resize(nparts + 1);
+  sized(P.group_chunk, nparts + 1);
+  sized(P.group_seg, nparts + 1);
   for (int pi = 0; pi < nparts; ++pi) {
     PlanPart& R = parts[pi];
     const int base = (int)P.chunk_pt.size();
@@ -683,10 +708,10 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   const int nchunks = (int)P.chunk_obs.size() - 1;
   const int nseg = (int)segs.size();
   std::vector<int32_t> seg_of(std::max(nchunks, 1), 0);
-  P.seg_chunk.resize(nseg + 1);
-  P.seg_slot_off.resize(nseg + 1);
-  P.seg_cam_off.resize(nseg + 1);
-  P.seg_acam_off.resize(nseg + 1);
+  sized(P.seg_chunk, nseg + 1);
+  sized(P.seg_slot_off, nseg + 1);
+  sized(P.seg_cam_off, nseg + 1);
+  sized(P.seg_acam_off, nseg + 1);
   P.seg_chunk[0] = P.seg_slot_off[0] = P.seg_cam_off[0] = P.seg_acam_off[0] = 0;
   for (int si = 0; si < nseg; ++si) {
     const PlanSeg& s = segs[si];
@@ -699,8 +724,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   }
   // per chunk: its slot_ptr / cam_ptr rows and its pair / camera list ranges
   std::vector<int32_t> pair_base(nchunks + 1), cl_base(nchunks + 1), col_base(nchunks + 1);
-  P.chunk_slot_base.resize(nchunks);
-  P.chunk_cam_base.resize(nchunks);
+  sized(P.chunk_slot_base, nchunks);
+  sized(P.chunk_cam_base, nchunks);
   {
     int32_t sb = 0, cb = 0;
     pair_base[0] = cl_base[0] = col_base[0] = 0;
@@ -714,23 +739,23 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       cl_base[ch + 1] = cl_base[ch] + ch_fte[ch];
       col_base[ch + 1] = col_base[ch] + ch_fobs[ch];
     }
-    P.slot_ptr.resize(sb);
-    P.cam_ptr.resize(cb);
-    P.camo_ptr.resize(cb);
+    sized(P.slot_ptr, sb);
+    sized(P.cam_ptr, cb);
+    sized(P.camo_ptr, cb);
   }
-  P.slot_i.resize(P.seg_slot_off[nseg]);
-  P.slot_j.resize(P.seg_slot_off[nseg]);
-  P.segcam_f.resize(P.seg_cam_off[nseg]);
-  P.segcam_diag.resize(P.seg_cam_off[nseg]);
-  P.seg_acam.resize(P.seg_acam_off[nseg]);
-  P.obs_acam.assign(std::max(M, 1), 0);
-  P.pair_list.resize(pair_base[nchunks]);
-  P.cam_list.resize(cl_base[nchunks]);
-  P.camo_list.resize(col_base[nchunks]);
-  P.chunk_hdr.assign((size_t)std::max(nchunks, 1) * kChunkHdr, 0);
-  P.chunk_img.resize((size_t)std::max(nchunks, 1));
+  sized(P.slot_i, P.seg_slot_off[nseg]);
+  sized(P.slot_j, P.seg_slot_off[nseg]);
+  sized(P.segcam_f, P.seg_cam_off[nseg]);
+  sized(P.segcam_diag, P.seg_cam_off[nseg]);
+  sized(P.seg_acam, P.seg_acam_off[nseg]);
+  filled(P.obs_acam, std::max(M, 1), 0);
+  sized(P.pair_list, pair_base[nchunks]);
+  sized(P.cam_list, cl_base[nchunks]);
+  sized(P.camo_list, col_base[nchunks]);
+  filled(P.chunk_hdr, (size_t)std::max(nchunks, 1) * kChunkHdr, 0);
+  sized(P.chunk_img, (size_t)std::max(nchunks, 1));
   if (nchunks == 0) P.chunk_img[0] = ChunkImg();
-  P.seg_hdr.assign((size_t)std::max(nseg, 1) * kSegHdr, 0);
+  filled(P.seg_hdr, (size_t)std::max(nseg, 1) * kSegHdr, 0);
   // chunk header: ob0 nob te0 nte p0 npt sb cb e0 e1 c0 c1 q0 q1 (14, 15: active slots and cameras)
   auto chunk_header = [&](int ch, int ns, int nc) {
     int32_t* h = &P.chunk_hdr[(size_t)ch * kChunkHdr];
@@ -1109,27 +1134,27 @@ std::vector<int32_t> local_profile_first(const BAPlan& P) {
 void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
   const int F = P.n_free;
   P.prof_first = first;
-  P.prof_off.assign(F + 1, 0);
+  filled(P.prof_off, F + 1, 0);
   for (int i = 0; i < F; ++i) P.prof_off[i + 1] = P.prof_off[i] + (i - first[i] + 1);
-  P.prof_last.assign(F, 0);
+  filled(P.prof_last, F, 0);
   for (int k = 0; k < F; ++k) P.prof_last[k] = k;
   for (int i = 0; i < F; ++i)
     for (int k = first[i]; k <= i; ++k) P.prof_last[k] = std::max(P.prof_last[k], i);
   const int nb = P.prof_off[F];
-  P.prof_diag.assign(nb, 0);
+  filled(P.prof_diag, nb, 0);
   for (int i = 0; i < F; ++i) P.prof_diag[P.prof_off[i] + (i - first[i])] = 1;
   // per profile block its slab slots, per free camera its rhs entries: stable counting
   // sorts (slots / entries in plan order within a block), and the inverse positions
   const size_t nslot = P.slot_i.size(), nent = P.segcam_f.size();
   std::vector<int32_t> sblk(nslot);
-  P.prof_src_ptr.assign(nb + 1, 0);
+  filled(P.prof_src_ptr, nb + 1, 0);
   for (size_t s = 0; s < nslot; ++s) {
     sblk[s] = P.prof_off[P.slot_i[s]] + (P.slot_j[s] - first[P.slot_i[s]]);
     ++P.prof_src_ptr[sblk[s] + 1];
   }
   for (int b = 0; b < nb; ++b) P.prof_src_ptr[b + 1] += P.prof_src_ptr[b];
-  P.prof_src.resize(nslot);
-  P.slab_pos.assign(std::max<size_t>(nslot, 1), 0);
+  sized(P.prof_src, nslot);
+  filled(P.slab_pos, std::max<size_t>(nslot, 1), 0);
   {
     std::vector<int32_t> next(P.prof_src_ptr.begin(), P.prof_src_ptr.end() - 1);
     for (size_t s = 0; s < nslot; ++s) {
@@ -1138,11 +1163,11 @@ void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
       P.slab_pos[s] = k;
     }
   }
-  P.camb_ptr.assign(F + 1, 0);
+  filled(P.camb_ptr, F + 1, 0);
   for (size_t e = 0; e < nent; ++e) ++P.camb_ptr[P.segcam_f[e] + 1];
   for (int f = 0; f < F; ++f) P.camb_ptr[f + 1] += P.camb_ptr[f];
-  P.camb_src.resize(nent);
-  P.cam_pos.assign(std::max<size_t>(nent, 1), 0);
+  sized(P.camb_src, nent);
+  filled(P.cam_pos, std::max<size_t>(nent, 1), 0);
   {
     std::vector<int32_t> next(P.camb_ptr.begin(), P.camb_ptr.end() - 1);
     for (size_t e = 0; e < nent; ++e) {

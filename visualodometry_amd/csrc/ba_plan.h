@@ -249,6 +249,8 @@ struct BAPlan {
   // reused_groups / reused_chunks count the groups and chunks taken over.
   std::vector<int32_t> chunk_src;
   int reused_groups = 0, reused_chunks = 0;
+  // planner scratch (never digested; kept across plans so a session's next window reuses it)
+  PlanArr<int32_t> scr_ob_start, scr_sorted, scr_te_start;
 
   BAPlan() = default;
   explicit BAPlan(bool pinned_images) : chunk_img(PlanHostAlloc<ChunkImg>(pinned_images)) {}
