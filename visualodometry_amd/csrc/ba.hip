@@ -1887,6 +1887,7 @@ class BAEngine {
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
                        prob->obs_uv, seg_obs_grid(seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave))), prev,
                        nw);
+      PLAN_T("setup: returned");
       // four-wave K1: every first-camera group ends in a partial segment, so the packing target
       // may give more segments than one round holds; then pack once more, proportionally wider
       // (on the grid; a function of the plan, which does not depend on prev)

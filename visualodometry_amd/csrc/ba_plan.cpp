@@ -29,11 +29,6 @@ std::string fmt(const char* f, long a = 0, long b = 0, long c = 0) {
   return buf;
 }
 
-int find_or_neg(const std::vector<int32_t>& v, int32_t x) {
-  for (size_t i = 0; i < v.size(); ++i)
-    if (v[i] == x) return (int)i;
-  return -1;
-}
 
 }  // namespace
 
@@ -238,12 +233,46 @@ int plan_threads(int64_t work) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), work / 2048 + 1));
 }
 
+}  // namespace
+
+// A vector of at most N trivially copyable elements stored inline (a segment's windows are
+// bounded by kSegCams / kSegAllCams / kSegSlots, checked before anything is added): no heap
+// allocation per segment, so a plan frees nothing per segment either.
+template <class T, int N>
+struct FixVec {
+  T v[N];
+  int n = 0;
+  int size() const { return n; }
+  bool empty() const { return n == 0; }
+  void clear() { n = 0; }
+  void push_back(const T& x) {
+    if (n >= N) throw std::length_error("plan: segment window overflow");
+    v[n++] = x;
+  }
+  T& operator[](int i) { return v[i]; }
+  const T& operator[](int i) const { return v[i]; }
+  T* begin() { return v; }
+  T* end() { return v + n; }
+  const T* begin() const { return v; }
+  const T* end() const { return v + n; }
+};
+
+template <class V, class X>
+int find_or_neg(const V& v, const X& x) {
+  for (int i = 0; i < (int)v.size(); ++i)
+    if (v[i] == x) return i;
+  return -1;
+}
+
 struct PlanSeg {
-  int chunk0;                               // first chunk (global index after the merge)
-  std::vector<int32_t> cams, acams;         // free / all cameras (unsorted while growing)
-  std::vector<std::pair<int32_t, int32_t>> slots;
-  std::vector<int32_t> slot_cnt;            // pairs per slot (while packing)
+  int chunk0 = 0;                           // first chunk (global index after the merge)
   int src = -1;                             // taken over: the previous plan's segment
+  FixVec<int32_t, kSegCams> cams;           // free cameras (unsorted while growing)
+  FixVec<int32_t, kSegAllCams> acams;       // all cameras its observations see
+  FixVec<std::pair<int32_t, int32_t>, kSegSlots> slots;
+  FixVec<int32_t, kSegSlots> slot_cnt;      // pairs per slot (while packing)
+  PlanSeg() = default;
+  PlanSeg(int c0, int s) : chunk0(c0), src(s) {}
 };
 
 // one first-camera group's greedy packing: chunks (first landmark, pair count, free track
@@ -255,9 +284,25 @@ struct PlanPart {
   int src = -1, shift = 0;
   int err_q = -1;
   std::string err;
+  void reset() {  // empty, capacity kept (the plan's next window reuses it)
+    chunk_q.clear();
+    chunk_pairs.clear();
+    chunk_fte.clear();
+    chunk_fobs.clear();
+    segs.clear();
+    src = -1;
+    shift = 0;
+    err_q = -1;
+    err.clear();
+  }
 };
 
-}  // namespace
+// The planner's working containers, kept across the plans of one BAPlan (ba_plan.h).
+struct PlanScratch {
+  std::vector<PlanPart> parts;
+  std::vector<PlanSeg*> segp;  // the plan's segments in order (into parts[].segs)
+  std::vector<int32_t> first, tecnt, hist, seg_of, pair_base, cl_base, col_base, ch_pairs, ch_fte, ch_fobs;
+};
 
 #ifndef VO_BA_COPY_CHAIN
 #define VO_BA_COPY_CHAIN 21
@@ -330,6 +375,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   const int max_slots = group_nch ? kWaveItems : kSegSlots;
   const int nthr = plan_threads(M);
   PlanSession session(nthr > 1);
+  if (!P.scratch) P.scratch = std::make_shared<PlanScratch>();
+  PlanScratch& X = *P.scratch;
 
   PlanArr<int32_t>& ob_start = P.scr_ob_start;
   PlanArr<int32_t>& sorted = P.scr_sorted;
@@ -341,9 +388,11 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   // keeps each workgroup's camera window narrow.  Per-thread histograms over landmark
   // ranges, offsets in (camera, range) order, then each range scatters its landmarks.
   {
-    std::vector<int32_t> first(L), tecnt(L);
+    std::vector<int32_t>&first = X.first, &tecnt = X.tecnt, &hist = X.hist;
+    sized(first, L);
+    sized(tecnt, L);
     const int nt = std::max(1, std::min(nthr, L / 1024 + 1));
-    std::vector<int32_t> hist((size_t)nt * (N + 1), 0);
+    filled(hist, (size_t)nt * (N + 1), 0);
     std::vector<int32_t> bad_ptr(nt, -1), bad_obs(nt, -1);  // first violation of each range
     auto lrange = [&](int t) { return std::make_pair((int)((int64_t)L * t / nt), (int)((int64_t)L * (t + 1) / nt)); };
     run_parallel(nt, [&](int t) {
@@ -468,7 +517,9 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   const int Nf = N - n_fixed;
   const bool tables = Nf <= kPlanTableCams;
   const int nparts = N + 1;
-  std::vector<PlanPart> parts(nparts);
+  std::vector<PlanPart>& parts = X.parts;
+  parts.resize(nparts);
+  for (PlanPart& R : parts) R.reset();
   const bool reuse = prev && prev != &P && prev->seg_obs == P.seg_obs && prev->seg_chunks == P.seg_chunks &&
                      prev->n_fixed == n_fixed &&
                      (int)prev->group_q.size() == prev->n_poses + 2;
@@ -502,12 +553,12 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       R.chunk_fobs.push_back(h[13] - h[12]);
     }
     for (int ps = Q.group_seg[src]; ps < Q.group_seg[src + 1]; ++ps) {
-      PlanSeg sg{Q.seg_chunk[ps] - pc0, {}, {}, {}, {}, ps};
+      R.segs.emplace_back(Q.seg_chunk[ps] - pc0, ps);
+      PlanSeg& sg = R.segs.back();
       for (int e = Q.seg_cam_off[ps]; e < Q.seg_cam_off[ps + 1]; ++e) sg.cams.push_back(Q.segcam_f[e] - s);
       for (int e = Q.seg_acam_off[ps]; e < Q.seg_acam_off[ps + 1]; ++e) sg.acams.push_back(Q.seg_acam[e] - s);
       for (int e = Q.seg_slot_off[ps]; e < Q.seg_slot_off[ps + 1]; ++e)
         sg.slots.push_back(std::make_pair(Q.slot_i[e] - s, Q.slot_j[e] - s));
-      R.segs.push_back(std::move(sg));
     }
   };
   auto pack = [&](int pi) {
@@ -595,7 +646,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       }
       if (!seg_fits || (!chunk_fits && (group_nch ? s_nch >= group_nch : s_obs >= seg_obs_target))) {
         pad_segment(q);
-        R.segs.push_back(PlanSeg{(int)R.chunk_q.size(), {}, {}, {}});
+        R.segs.emplace_back((int)R.chunk_q.size(), -1);
         seg_open = true;
         s_obs = 0;
         s_nch = 0;
@@ -666,8 +717,12 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   for (const PlanPart& R : parts)  // the first error in landmark order
     if (R.err_q >= 0) return R.err;
   // merge the groups: chunks and segments in landmark order
-  std::vector<PlanSeg> segs;
-  std::vector<int32_t> ch_pairs, ch_fte, ch_fobs;
+  std::vector<PlanSeg*>& segs = X.segp;  // (pointers into the groups' segment lists)
+  std::vector<int32_t>&ch_pairs = X.ch_pairs, &ch_fte = X.ch_fte, &ch_fobs = X.ch_fobs;
+  segs.clear();
+  ch_pairs.clear();
+  ch_fte.clear();
+  ch_fobs.clear();
   sized(P.group_chunk, nparts + 1);
   sized(P.group_seg, nparts + 1);
   for (int pi = 0; pi < nparts; ++pi) {
@@ -692,7 +747,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     ch_fobs.insert(ch_fobs.end(), R.chunk_fobs.begin(), R.chunk_fobs.end());
     for (PlanSeg& s : R.segs) {
       s.chunk0 += base;
-      segs.push_back(std::move(s));
+      segs.push_back(&s);
     }
   }
   P.group_chunk[nparts] = (int)P.chunk_pt.size();
@@ -707,15 +762,16 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   // segments and chunks), then segment ranges filled in parallel.
   const int nchunks = (int)P.chunk_obs.size() - 1;
   const int nseg = (int)segs.size();
-  std::vector<int32_t> seg_of(std::max(nchunks, 1), 0);
+  std::vector<int32_t>& seg_of = X.seg_of;
+  filled(seg_of, std::max(nchunks, 1), 0);
   sized(P.seg_chunk, nseg + 1);
   sized(P.seg_slot_off, nseg + 1);
   sized(P.seg_cam_off, nseg + 1);
   sized(P.seg_acam_off, nseg + 1);
   P.seg_chunk[0] = P.seg_slot_off[0] = P.seg_cam_off[0] = P.seg_acam_off[0] = 0;
   for (int si = 0; si < nseg; ++si) {
-    const PlanSeg& s = segs[si];
-    const int ch1 = si + 1 < nseg ? segs[si + 1].chunk0 : nchunks;
+    const PlanSeg& s = *segs[si];
+    const int ch1 = si + 1 < nseg ? segs[si + 1]->chunk0 : nchunks;
     for (int ch = s.chunk0; ch < ch1; ++ch) seg_of[ch] = si;
     P.seg_chunk[si + 1] = ch1;
     P.seg_slot_off[si + 1] = P.seg_slot_off[si] + (int)s.slots.size();
@@ -723,14 +779,17 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     P.seg_acam_off[si + 1] = P.seg_acam_off[si] + (int)s.acams.size();
   }
   // per chunk: its slot_ptr / cam_ptr rows and its pair / camera list ranges
-  std::vector<int32_t> pair_base(nchunks + 1), cl_base(nchunks + 1), col_base(nchunks + 1);
+  std::vector<int32_t>&pair_base = X.pair_base, &cl_base = X.cl_base, &col_base = X.col_base;
+  sized(pair_base, nchunks + 1);
+  sized(cl_base, nchunks + 1);
+  sized(col_base, nchunks + 1);
   sized(P.chunk_slot_base, nchunks);
   sized(P.chunk_cam_base, nchunks);
   {
     int32_t sb = 0, cb = 0;
     pair_base[0] = cl_base[0] = col_base[0] = 0;
     for (int ch = 0; ch < nchunks; ++ch) {
-      const PlanSeg& s = segs[seg_of[ch]];
+      const PlanSeg& s = *segs[seg_of[ch]];
       P.chunk_slot_base[ch] = sb;
       P.chunk_cam_base[ch] = cb;
       sb += (int)s.slots.size() + 1;
@@ -850,7 +909,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     uint16_t ptmp[kChunkPairs];
     for (int sa = fill_next.fetch_add(kFillBatch); sa < nseg; sa = fill_next.fetch_add(kFillBatch))
     for (int si = sa; si < std::min(sa + kFillBatch, nseg); ++si) {
-      PlanSeg& s = segs[si];
+      PlanSeg& s = *segs[si];
       if (s.src >= 0) {
         fill_taken(si, s);
         continue;
@@ -860,14 +919,14 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       std::sort(s.acams.begin(), s.acams.end());
       const int ch0 = P.seg_chunk[si], ch1 = P.seg_chunk[si + 1];
       const int so = P.seg_slot_off[si], co = P.seg_cam_off[si];
-      for (size_t i = 0; i < s.slots.size(); ++i) {
+      for (int i = 0; i < s.slots.size(); ++i) {
         P.slot_i[so + i] = s.slots[i].first;
         P.slot_j[so + i] = s.slots[i].second;
       }
       if (tables) {
-        for (size_t i = 0; i < s.cams.size(); ++i) fcam_idx[s.cams[i]] = (int32_t)i;
-        for (size_t i = 0; i < s.acams.size(); ++i) acam_idx[s.acams[i]] = (int32_t)i;
-        for (size_t i = s.slots.size(); i-- > 0;)  // the first of equal slots (copies)
+        for (int i = 0; i < s.cams.size(); ++i) fcam_idx[s.cams[i]] = (int32_t)i;
+        for (int i = 0; i < s.acams.size(); ++i) acam_idx[s.acams[i]] = (int32_t)i;
+        for (int i = s.slots.size(); i-- > 0;)  // the first of equal slots (copies)
           pair_slot[(size_t)s.slots[i].first * Nf + s.slots[i].second] = (int32_t)i;
       }
       auto lcam_of = [&](int32_t c) {  // window index of free camera c
@@ -882,7 +941,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         P.obs_acam[o] = (uint8_t)(tables ? acam_idx[P.obs_cam[o]]
                                          : std::lower_bound(s.acams.begin(), s.acams.end(), P.obs_cam[o]) -
                                                s.acams.begin());
-      for (size_t i = 0; i < s.cams.size(); ++i) {
+      for (int i = 0; i < s.cams.size(); ++i) {
         P.segcam_f[co + i] = s.cams[i];
         P.segcam_diag[co + i] = slot_of(std::make_pair(s.cams[i], s.cams[i]));
       }

@@ -184,6 +184,8 @@ struct DefaultInitAlloc : std::allocator<T> {
 template <class T>
 using PlanArr = std::vector<T, DefaultInitAlloc<T>>;
 
+struct PlanScratch;  // ba_plan.cpp
+
 struct SolveTableLayout {
   int diag = 0, off = 0, first = 0, step_ptr = 0, panel_i = 0, panel_blk = 0, item_ptr = 0,
       item_blk = 0, item_q = 0, len = 0;
@@ -251,6 +253,7 @@ struct BAPlan {
   int reused_groups = 0, reused_chunks = 0;
   // planner scratch (never digested; kept across plans so a session's next window reuses it)
   PlanArr<int32_t> scr_ob_start, scr_sorted, scr_te_start;
+  std::shared_ptr<PlanScratch> scratch;  // the planner's working containers (ba_plan.cpp)
 
   BAPlan() = default;
   explicit BAPlan(bool pinned_images) : chunk_img(PlanHostAlloc<ChunkImg>(pinned_images)) {}
