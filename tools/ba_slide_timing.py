@@ -54,4 +54,14 @@ for w in ws:
     st = call(w, log)
 out["slide"] = {k: round(float(np.median(v[2:])), 3) for k, v in log.items()}
 out["slide_last_plan"] = st
+# the same windows from scratch: an unrelated window set up before each (nothing to take over)
+from visualodometry_amd.synthetic import make_ba_problem  # noqa: E402
+
+other = make_ba_problem(8, 200, 11)
+log = {k: [] for k in steps}
+for w in ws:
+    sys.stderr.write("-- slide windows from scratch\n")
+    BASession(other.K, other.point_ptr, other.obs_cam, other.obs_uv, other.n_poses, other.n_fixed, 1.0, ctx)
+    call(w, log)
+out["slide_windows_scratch"] = {k: round(float(np.median(v[2:])), 3) for k, v in log.items()}
 print(json.dumps(out))

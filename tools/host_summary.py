@@ -11,7 +11,8 @@ for f in sorted(glob.glob(f"{d0}/spin_*.json")) + [f"{d0}/host_latency.json"]:
     d = json.load(open(f))
     if "scratch" in d:
         print(f.split("/")[-1], "scratch", d["scratch"]["total"], d["scratch"]["setup"], "slide", d["slide"]["total"],
-              d["slide"]["setup"])
+              d["slide"]["setup"], "slide windows from scratch", d.get("slide_windows_scratch", {}).get("total"),
+              d.get("slide_windows_scratch", {}).get("setup"))
     else:
         print(f.split("/")[-1], d["ba_cfg3_10iters_ms"], d["ba_cfg3_slide_ms"])
 secs = collections.defaultdict(lambda: collections.defaultdict(list))

@@ -378,21 +378,22 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   if (!P.scratch) P.scratch = std::make_shared<PlanScratch>();
   PlanScratch& X = *P.scratch;
 
-  PlanArr<int32_t>& ob_start = P.scr_ob_start;
   PlanArr<int32_t>& sorted = P.scr_sorted;
-  PlanArr<int32_t>& te_start = P.scr_te_start;
-  sized(ob_start, L + 1);
   sized(sorted, std::max(M, 1));
-  sized(te_start, L + 1);
-  // landmarks ordered by first camera (stable counting sort; no observation: last), which
-  // keeps each workgroup's camera window narrow.  Per-thread histograms over landmark
-  // ranges, offsets in (camera, range) order, then each range scatters its landmarks.
+  // Landmarks ordered by first camera (stable counting sort; no observation: last), which
+  // keeps each workgroup's camera window narrow, and their observations grouped by (landmark,
+  // camera) into track entries.  Pass 1 over landmark ranges: the checks, each landmark's first
+  // camera and track-entry count, and per (range, camera) the landmarks, observations and track
+  // entries; offsets in (camera, range) order; pass 2 over the same ranges: each landmark takes
+  // its internal index and its observation and track-entry slots from its bucket's running
+  // offsets, sorts its observations by camera (stable) into them and writes every array.
   {
     std::vector<int32_t>&first = X.first, &tecnt = X.tecnt, &hist = X.hist;
     sized(first, L);
     sized(tecnt, L);
     const int nt = std::max(1, std::min(nthr, L / 1024 + 1));
-    filled(hist, (size_t)nt * (N + 1), 0);
+    const size_t nb = (size_t)nt * (N + 1);
+    filled(hist, 3 * nb, 0);  // landmarks | observations | track entries per (range, camera)
     std::vector<int32_t> bad_ptr(nt, -1), bad_obs(nt, -1);  // first violation of each range
     auto lrange = [&](int t) { return std::make_pair((int)((int64_t)L * t / nt), (int)((int64_t)L * (t + 1) / nt)); };
     run_parallel(nt, [&](int t) {
@@ -410,6 +411,8 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
           return;
         }
       int32_t* h = &hist[(size_t)t * (N + 1)];
+      int32_t* ho = h + nb;
+      int32_t* ht = ho + nb;
       for (int p = pa; p < pb; ++p) {
         // first camera and track entries (distinct cameras; tracks are short)
         int f = N, nte = 0;
@@ -424,92 +427,83 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         first[p] = f;
         tecnt[p] = nte;
         ++h[f];
+        ho[f] += o1 - o0;
+        ht[f] += nte;
       }
     });
     for (int t = 0; t < nt; ++t)  // the lowest violation, as a serial scan would find it
       if (bad_ptr[t] >= 0) return fmt("point_ptr not monotone at %ld", bad_ptr[t]);
     for (int t = 0; t < nt; ++t)
       if (bad_obs[t] >= 0) return fmt("obs_cam[%ld]=%ld out of range", bad_obs[t], obs_cam[bad_obs[t]]);
-    int32_t off = 0;
+    int32_t off = 0, ooff = 0, toff = 0;
     sized(P.group_q, N + 2);
     for (int c = 0; c <= N; ++c) {
       P.group_q[c] = off;
       for (int t = 0; t < nt; ++t) {
-        int32_t& h = hist[(size_t)t * (N + 1) + c];
-        const int32_t n = h;
-        h = off;
+        int32_t* h = &hist[(size_t)t * (N + 1) + c];
+        const int32_t n = h[0], no = h[nb], ne = h[2 * nb];
+        h[0] = off;
+        h[nb] = ooff;
+        h[2 * nb] = toff;
         off += n;
+        ooff += no;
+        toff += ne;
       }
     }
     P.group_q[N + 1] = off;
+    P.n_te = toff;
     sized(P.pt_perm, L);
+    sized(P.obs_uv, 2 * (size_t)M);
+    sized(P.obs_cam, M);
+    sized(P.obs_te, M);
+    sized(P.te_cam, P.n_te);
+    sized(P.te_pt, P.n_te);
+    sized(P.te_obs, P.n_te + 1);
+    sized(P.te_lcam, P.n_te);
+    sized(P.pt_te, L + 1);
     run_parallel(nt, [&](int t) {
       const auto [pa, pb] = lrange(t);
       int32_t* h = &hist[(size_t)t * (N + 1)];
+      int32_t* ho = h + nb;
+      int32_t* ht = ho + nb;
       for (int p = pa; p < pb; ++p) {
-        const int32_t q = h[first[p]]++;
+        const int c = first[p], n = point_ptr[p + 1] - point_ptr[p];
+        const int32_t q = h[c]++, ob = ho[c], te0 = ht[c];
+        ho[c] += n;
+        ht[c] += tecnt[p];
         P.pt_perm[q] = p;
-        ob_start[q + 1] = point_ptr[p + 1] - point_ptr[p];  // the prefix sums follow
-        te_start[q + 1] = tecnt[p];
+        P.pt_te[q] = te0;
+        int32_t* idx = &sorted[ob];
+        for (int i = 0; i < n; ++i) {  // stable insertion sort by camera (tracks are short)
+          const int32_t v = point_ptr[p] + i;
+          int j = i;
+          while (j > 0 && obs_cam[idx[j - 1]] > obs_cam[v]) {
+            idx[j] = idx[j - 1];
+            --j;
+          }
+          idx[j] = v;
+        }
+        int te = te0 - 1;
+        for (int pos = ob; pos < ob + n; ++pos) {
+          const int o = sorted[pos];
+          if (pos == ob || obs_cam[o] != obs_cam[sorted[pos - 1]]) {
+            ++te;
+            P.te_cam[te] = obs_cam[o];
+            P.te_pt[te] = q;
+            P.te_obs[te] = pos;
+            P.te_lcam[te] = -1;  // window camera: set by the packing (free cameras)
+          }
+          P.obs_uv[2 * (size_t)pos] = obs_uv[2 * (size_t)o];
+          P.obs_uv[2 * (size_t)pos + 1] = obs_uv[2 * (size_t)o + 1];
+          P.obs_cam[pos] = obs_cam[o];
+          P.obs_te[pos] = te;
+        }
       }
     });
   }
-  PLAN_T("order");
-
-  // observations grouped by (landmark, camera) -> track entries: one pass per landmark sorts
-  // its observations by camera (stable) into its slot and writes every array at the prefix
-  // offsets (the track-entry counts came with the order)
-  ob_start[0] = 0;
-  te_start[0] = 0;
-  for (int q = 0; q < L; ++q) {
-    ob_start[q + 1] += ob_start[q];
-    te_start[q + 1] += te_start[q];
-  }
-  auto qrange = [&](int t, int n) { return std::make_pair((int)((int64_t)L * t / n), (int)((int64_t)L * (t + 1) / n)); };
-  P.n_te = te_start[L];
-  sized(P.obs_uv, 2 * (size_t)M);
-  sized(P.obs_cam, M);
-  sized(P.obs_te, M);
-  sized(P.te_cam, P.n_te);
-  sized(P.te_pt, P.n_te);
-  sized(P.te_obs, P.n_te + 1);
-  sized(P.te_lcam, P.n_te);
-  sized(P.pt_te, L + 1);
-  run_parallel(nthr, [&](int t) {
-    const auto [qa, qb] = qrange(t, nthr);
-    for (int q = qa; q < qb; ++q) {
-      const int p = P.pt_perm[q], n = point_ptr[p + 1] - point_ptr[p];
-      int32_t* idx = &sorted[ob_start[q]];
-      for (int i = 0; i < n; ++i) {  // stable insertion sort by camera (tracks are short)
-        const int32_t v = point_ptr[p] + i;
-        int j = i;
-        while (j > 0 && obs_cam[idx[j - 1]] > obs_cam[v]) {
-          idx[j] = idx[j - 1];
-          --j;
-        }
-        idx[j] = v;
-      }
-      int te = te_start[q] - 1;
-      P.pt_te[q] = te_start[q];
-      for (int pos = ob_start[q]; pos < ob_start[q + 1]; ++pos) {
-        const int o = sorted[pos];
-        if (pos == ob_start[q] || obs_cam[o] != obs_cam[sorted[pos - 1]]) {
-          ++te;
-          P.te_cam[te] = obs_cam[o];
-          P.te_pt[te] = q;
-          P.te_obs[te] = pos;
-          P.te_lcam[te] = -1;  // window camera: set by the packing (free cameras)
-        }
-        P.obs_uv[2 * (size_t)pos] = obs_uv[2 * (size_t)o];
-        P.obs_uv[2 * (size_t)pos + 1] = obs_uv[2 * (size_t)o + 1];
-        P.obs_cam[pos] = obs_cam[o];
-        P.obs_te[pos] = te;
-      }
-    }
-  });
   P.pt_te[L] = P.n_te;
   P.te_obs[P.n_te] = M;
-  PLAN_T("track entries");
+  PLAN_T("order + track entries");
 
   // ---- chunks and segments: each first-camera group packed greedily on its own (so a
   // group's packing depends on its own landmarks only), or taken over from prev

@@ -252,7 +252,7 @@ struct BAPlan {
   std::vector<int32_t> chunk_src;
   int reused_groups = 0, reused_chunks = 0;
   // planner scratch (never digested; kept across plans so a session's next window reuses it)
-  PlanArr<int32_t> scr_ob_start, scr_sorted, scr_te_start;
+  PlanArr<int32_t> scr_sorted;
   std::shared_ptr<PlanScratch> scratch;  // the planner's working containers (ba_plan.cpp)
 
   BAPlan() = default;
