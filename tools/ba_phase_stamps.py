@@ -11,7 +11,8 @@ from pathlib import Path
 import numpy as np
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-os.environ.setdefault("VO_BA_STAMPS", "1")
+os.environ.setdefault("VO_LIB_PATH", str(Path(__file__).resolve().parents[1] / "visualodometry_amd" / "lib" /
+                                         "libvo_hip_stamps.so"))
 
 from visualodometry_amd import _lib  # noqa: E402
 from visualodometry_amd.ba import BASession  # noqa: E402
@@ -42,7 +43,8 @@ for k in range(len(PHASES), n):
     print(f"{K3[k - len(PHASES)]:18s} {int(out[k]):14d} cycles (one WG)  {100 * out[k] / max(t3, 1):5.1f} %")
 
 # per-workgroup timeline of the last K1 launch (start/end absolute stamps)
-nseg = s.plan_stats()["segments"]
+st_ = s.plan_stats()
+nseg = st_["chunks"] if st_["seg_obs"] == 1 else st_["segments"]  # rows: chunks of the one-wave K1
 raw = np.zeros(nseg * NPH, dtype=np.uint64)
 k = ctx.lib.vo_ba_debug_stamps(ctx.handle, raw.ctypes.data_as(_lib.C.POINTER(_lib.C.c_uint64)), -raw.size)
 if k > 0:
