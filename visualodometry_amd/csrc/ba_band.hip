@@ -269,14 +269,17 @@ __device__ __forceinline__ void band_reduce_wg(const BandArgs& B, int r, double*
   if (iscost && t == 0 && !failed) st_sc1(A.sys + A.cost_off, cpart[0]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores done
   __syncthreads();
-  // release: every sc1 store above is ordered before the count (explicit in the memory model;
-  // the stores are agent atomics already, so this costs one fence per workgroup)
-  if (tid == 0) __hip_atomic_fetch_add((gu32*)B.red_count, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  // one lane counts the workgroup, behind every storing wave's drain: with write-through (sc1)
+  // stores and a consumer that reads every handed-off byte by sc1 loads, no release fence
+  // (MI355X_MICROARCH.md, inter-workgroup visibility, hand-off table row 1; a fence here cost
+  // each reducer ~1.7 us of write-back on the solver's path)
+  if (tid == 0) __hip_atomic_fetch_add((gu32*)B.red_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Solver side of the fused launch: one lane polls red_count (relaxed, s_sleep between reads,
-// bounded), takes nred off it, then the agent-scope acquire; every wave waits at the barrier
-// for it.  Returns false on a timeout (then sys is not read: the solve reports "failed").
+// Solver side of the fused launch: one lane polls red_count (relaxed sc1 loads, s_sleep between
+// reads, bounded) and takes nred off it; every wave waits at the barrier for it.  No acquire:
+// every load of sys after it is an sc1 load (sys_ld), as the hand-off row requires.  Returns
+// false on a timeout (then sys is not read: the solve reports "failed").
 __device__ __forceinline__ bool band_wait_reduced(const BandArgs& A, int tid, int* s_flag) {
   if (tid == 0) {
     int ok = 1;
@@ -289,13 +292,31 @@ __device__ __forceinline__ bool band_wait_reduced(const BandArgs& A, int tid, in
       }
     }
     if (ok) __hip_atomic_fetch_sub((gu32*)A.red_count, (unsigned)A.nred, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     *s_flag = ok;
   }
   __syncthreads();
   return *s_flag != 0;
 }
+
+// The solver reads sys (written by the fused launch's reducers, or by K2) only by sc1 buffer
+// loads: L2-served, never a stale L1 line, so the in-launch hand-off needs no acquire fence.
+// Offsets in doubles; past the buffer's end a buffer load returns zero.
+struct SysLoads {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ explicit SysLoads(const double* sys, long n) {
+    r = __builtin_amdgcn_make_buffer_rsrc((void*)sys, (short)0, (int)min(n * 8, (long)0x7fffffff), 0x00020000);
+  }
+  __device__ __forceinline__ double2 ld2(long off) const {  // 16 bytes at sys[off] (off even)
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const v4i v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off * 8), 0, 16);
+    return __builtin_bit_cast(double2, v);
+  }
+  __device__ __forceinline__ double ld(long off) const {
+    typedef int v2i __attribute__((ext_vector_type(2)));
+    const v2i v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(off * 8), 0, 16);
+    return __builtin_bit_cast(double, v);
+  }
+};
 
 // Loads below never feed a select or branch before their first real use: a value that
 // must be zero is loaded from the zero block (A.zero) instead, so the waitcnt pass can
@@ -338,7 +359,8 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   double* const sring = sbot ? ringB : ringT;
   const double* const recT = kFull ? ringT : A.fac;  // the top side's records
   const double* const sfac = kFull ? sring : sbot ? A.fac + (long)ncolT * CS : A.fac;
-  const double* const ssys = A.sys + (sbot ? (long)ncolT * CS : 0);  // this side's columns (K2)
+  const long sbase = sbot ? (long)ncolT * CS : 0;  // this side's columns in sys (K2)
+  const SysLoads sysl(A.sys, A.cost_off + 1);
   const int sna = sbot ? nb : m, snload = sbot ? ncolB : ncolT;
 
   if (tid < 40) s_zero[tid] = 0.0;
@@ -352,23 +374,20 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   const bool prior_fail = prior_status || !reduced;
   if (tid == 0) {
     s_fail = prior_fail ? 1 : 0;
-    if (A.cost_out && reduced) *A.cost_out = A.sys[A.cost_off];
+    if (A.cost_out && reduced) *A.cost_out = sysl.ld(A.cost_off);
   }
-  typedef __attribute__((address_space(3))) void lds_void;
-  typedef __attribute__((address_space(1))) const void gbl_void;
   {
     // Prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every 16-byte
     // load in flight, then the stores.  The loads do not wait for the status word (one
     // global round trip less on the launch's path); a failed earlier solve only skips the
     // stores.
     const int nT = min(w + 2, ncolT) * CS / 2, nB = min(w + 2, ncolB) * CS / 2;  // double2 pieces
-    const double2* gT = reinterpret_cast<const double2*>(A.sys);
-    const double2* gB = reinterpret_cast<const double2*>(A.sys + (long)ncolT * CS);
     double2 v[kProLoads];
 #pragma unroll
     for (int u = 0; u < kProLoads; ++u) {
       const int e = tid + u * kBandThreads;
-      v[u] = e < nT ? gT[e] : e < nT + nB ? gB[e - nT] : make_double2(0.0, 0.0);
+      const double2 x = sysl.ld2(2l * (e < nT ? e : (long)ncolT * CS / 2 + (e - nT)));
+      v[u] = e < nT + nB ? x : make_double2(0.0, 0.0);
     }
     if (!prior_fail)
 #pragma unroll
@@ -381,18 +400,24 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     }
   }
 
-  // ---- loader wave: column v by LDS-DMA, nDma 1 KiB wave pieces (16 bytes per lane)
+  // ---- loader wave: column v by sc1 register loads, nDma 1 KiB wave pieces (16 bytes per lane),
+  // written into its LDS slot one step later (the loads in flight across the barrier)
   const int nDma = CSP / 128;
-  auto dma_col = [&](int v, double* slot) __attribute__((always_inline)) {
-    const double* src = ssys + (long)v * CS + 2 * lane;
-    for (int t = 0; t < nDma; ++t)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(src + 128 * t), (lds_void*)(slot + 128 * t), 16, 0, 0);
+  static_assert(36 * (kBandMaxW + 1) + 12 <= 3 * 128, "at most three 1 KiB pieces per column");
+  double2 ldv[3];
+  int ld_pend = -1;  // the column whose pieces are in ldv
+  auto col_issue = [&](int v) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) ldv[t] = sysl.ld2(sbase + (long)v * CS + 2 * lane + 128 * t);
+    ld_pend = v;
   };
-  // every DMA but the last column's nDma pieces complete
-  auto dma_wait_prev = [&]() __attribute__((always_inline)) {
-    if (nDma == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else if (nDma == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  auto col_write = [&]() __attribute__((always_inline)) {
+    if (ld_pend < 0) return;
+    double* slot = sring + (kFull ? ld_pend : ld_pend % RC) * SS;
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      if (t < nDma && 128 * t + 2 * lane < CS) *reinterpret_cast<double2*>(slot + 128 * t + 2 * lane) = ldv[t];
+    ld_pend = -1;
   };
   // ---- trailing wave: task lane + 64 h = block (k + qi, k + qj), rows r and r + 3
   // (blocks by qj, then qi): target column offset qj, offsets of the target row r, of
@@ -592,18 +617,15 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       st6g(out + 18, o1);
     }
   };
-  // Loader wave, step k: column k + w + 2 into its slot (ring mode: column c in slot
-  // c mod (w + 4), i.e. column k - 2's, whose record the trailing wave copied a step ago;
-  // first read at step k + 2), then the previous column's pieces retired.
+  // Loader wave, step k: the column loaded at step k - 1 (k + w + 1) into its slot (ring mode:
+  // column c in slot c mod (w + 4), i.e. column k - 3's, whose record the trailing wave copied
+  // two steps ago; first read at step k + 1, after this step's barrier), then the loads of
+  // column k + w + 2.
   auto load_step = [&](int k) __attribute__((always_inline)) {
-    if (k + w + 2 < snload) {
-      dma_col(k + w + 2, sring + (kFull ? k + w + 2 : (k + w + 2) % RC) * SS);
-      BSTF(20);
-      dma_wait_prev();
-      BSTF(21);
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    col_write();
+    BSTF(21);
+    if (k + w + 2 < snload) col_issue(k + w + 2);
+    BSTF(20);
   };
   auto side_step = [&](int p, int sk, int skm) __attribute__((always_inline)) {
     if (role == kTrail) {
