@@ -400,9 +400,12 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     }
   }
 
-  // ---- loader wave: column v by sc1 register loads, nDma 1 KiB wave pieces (16 bytes per lane),
-  // written into its LDS slot one step later (the loads in flight across the barrier)
+  // ---- loader wave, nDma 1 KiB wave pieces (16 bytes per lane) per column.  In a fused launch
+  // (sys from this launch's reducers): sc1 register loads, written into the column's LDS slot one
+  // step later (the loads in flight across the barrier); otherwise (sys from an earlier launch):
+  // LDS-DMA, faster in ring mode (cfg4 K3 77 against 89 us with the register loads).
   const int nDma = CSP / 128;
+  const bool ld_sc1 = A.nred > 0;
   static_assert(36 * (kBandMaxW + 1) + 12 <= 3 * 128, "at most three 1 KiB pieces per column");
   double2 ldv[3];
   int ld_pend = -1;  // the column whose pieces are in ldv
@@ -418,6 +421,19 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     for (int t = 0; t < 3; ++t)
       if (t < nDma && 128 * t + 2 * lane < CS) *reinterpret_cast<double2*>(slot + 128 * t + 2 * lane) = ldv[t];
     ld_pend = -1;
+  };
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) const void gbl_void;
+  auto dma_col = [&](int v, double* slot) __attribute__((always_inline)) {
+    const double* src = A.sys + sbase + (long)v * CS + 2 * lane;
+    for (int t = 0; t < nDma; ++t)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + 128 * t), (lds_void*)(slot + 128 * t), 16, 0, 0);
+  };
+  // every DMA but the last column's nDma pieces complete
+  auto dma_wait_prev = [&]() __attribute__((always_inline)) {
+    if (nDma == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if (nDma == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
   };
   // ---- trailing wave: task lane + 64 h = block (k + qi, k + qj), rows r and r + 3
   // (blocks by qj, then qi): target column offset qj, offsets of the target row r, of
@@ -617,15 +633,25 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       st6g(out + 18, o1);
     }
   };
-  // Loader wave, step k: the column loaded at step k - 1 (k + w + 1) into its slot (ring mode:
-  // column c in slot c mod (w + 4), i.e. column k - 3's, whose record the trailing wave copied
-  // two steps ago; first read at step k + 1, after this step's barrier), then the loads of
-  // column k + w + 2.
+  // Loader wave, step k, sc1: the column loaded at step k - 1 (k + w + 1) into its slot (ring
+  // mode: column c in slot c mod (w + 4), i.e. column k - 3's, whose record the trailing wave
+  // copied two steps ago; first read at step k + 1, after this step's barrier), then the loads
+  // of column k + w + 2.  LDS-DMA: column k + w + 2 issued into its slot (column k - 2's, whose
+  // record the trailing wave copied a step ago), then the previous column's pieces retired.
   auto load_step = [&](int k) __attribute__((always_inline)) {
-    col_write();
-    BSTF(21);
-    if (k + w + 2 < snload) col_issue(k + w + 2);
-    BSTF(20);
+    if (ld_sc1) {
+      col_write();
+      BSTF(21);
+      if (k + w + 2 < snload) col_issue(k + w + 2);
+      BSTF(20);
+    } else if (k + w + 2 < snload) {
+      dma_col(k + w + 2, sring + (kFull ? k + w + 2 : (k + w + 2) % RC) * SS);
+      BSTF(20);
+      dma_wait_prev();
+      BSTF(21);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   };
   auto side_step = [&](int p, int sk, int skm) __attribute__((always_inline)) {
     if (role == kTrail) {
