@@ -2032,7 +2032,9 @@ class BAEngine {
       // K2 fused into the banded K3's launch when every workgroup of it fits one round at
       // one per CU (the solver's LDS): cfg3's 356 blocks make 178 reducers + the solver on
       // MI355X's 256 CUs (fewer CUs, e.g. a partitioned device: K2 stays a launch of its own)
-      fuse_ok_ = VO_BA_FUSE && band_on_ && band_fused_workgroups(nprof) + 1 <= ctx_->num_cus;
+      // (full mode only: the ring-mode solver reads sys with plain loads, so it must come from an
+      // earlier launch)
+      fuse_ok_ = VO_BA_FUSE && band_on_ && band_lds_.full && band_fused_workgroups(nprof) + 1 <= ctx_->num_cus;
       d_red_count_.reserve(256);
       VO_HIP_CHECK(hipMemsetAsync(d_red_count_.ptr, 0, 256, st));
       d_zero_.reserve(512);  // zero block (masked prefetches)

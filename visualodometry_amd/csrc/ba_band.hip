@@ -360,7 +360,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   const double* const recT = kFull ? ringT : A.fac;  // the top side's records
   const double* const sfac = kFull ? sring : sbot ? A.fac + (long)ncolT * CS : A.fac;
   const long sbase = sbot ? (long)ncolT * CS : 0;  // this side's columns in sys (K2)
-  const SysLoads sysl(A.sys, A.cost_off + 1);
+  const SysLoads sysl(A.sys, kFull ? A.cost_off + 1 : 0);
   const int sna = sbot ? nb : m, snload = sbot ? ncolB : ncolT;
 
   if (tid < 40) s_zero[tid] = 0.0;
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   const bool prior_fail = prior_status || !reduced;
   if (tid == 0) {
     s_fail = prior_fail ? 1 : 0;
-    if (A.cost_out && reduced) *A.cost_out = sysl.ld(A.cost_off);
+    if (A.cost_out && reduced) *A.cost_out = kFull ? sysl.ld(A.cost_off) : A.sys[A.cost_off];
   }
   {
     // Prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every 16-byte
@@ -386,8 +386,13 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
 #pragma unroll
     for (int u = 0; u < kProLoads; ++u) {
       const int e = tid + u * kBandThreads;
-      const double2 x = sysl.ld2(2l * (e < nT ? e : (long)ncolT * CS / 2 + (e - nT)));
-      v[u] = e < nT + nB ? x : make_double2(0.0, 0.0);
+      const long o2 = e < nT ? e : (long)ncolT * CS / 2 + (e - nT);
+      if constexpr (kFull) {
+        const double2 x = sysl.ld2(2 * o2);
+        v[u] = e < nT + nB ? x : make_double2(0.0, 0.0);
+      } else {
+        v[u] = e < nT + nB ? reinterpret_cast<const double2*>(A.sys)[o2] : make_double2(0.0, 0.0);
+      }
     }
     if (!prior_fail)
 #pragma unroll
@@ -401,11 +406,12 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   }
 
   // ---- loader wave, nDma 1 KiB wave pieces (16 bytes per lane) per column.  In a fused launch
-  // (sys from this launch's reducers): sc1 register loads, written into the column's LDS slot one
-  // step later (the loads in flight across the barrier); otherwise (sys from an earlier launch):
-  // LDS-DMA, faster in ring mode (cfg4 K3 77 against 89 us with the register loads).
+  // (full mode; sys from this launch's reducers): sc1 register loads, written into the column's
+  // LDS slot one step later (the loads in flight across the barrier); otherwise (sys from an
+  // earlier launch): LDS-DMA.  The ring-mode kernel carries no sc1 path (its registers and the
+  // buffer descriptor pushed it past 256 VGPRs into spills: cfg4 K3 77 -> 89 us).
   const int nDma = CSP / 128;
-  const bool ld_sc1 = A.nred > 0;
+  const bool ld_sc1 = kFull && A.nred > 0;
   static_assert(36 * (kBandMaxW + 1) + 12 <= 3 * 128, "at most three 1 KiB pieces per column");
   double2 ldv[3];
   int ld_pend = -1;  // the column whose pieces are in ldv
@@ -639,7 +645,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // of column k + w + 2.  LDS-DMA: column k + w + 2 issued into its slot (column k - 2's, whose
   // record the trailing wave copied a step ago), then the previous column's pieces retired.
   auto load_step = [&](int k) __attribute__((always_inline)) {
-    if (ld_sc1) {
+    if (kFull && ld_sc1) {
       col_write();
       BSTF(21);
       if (k + w + 2 < snload) col_issue(k + w + 2);
