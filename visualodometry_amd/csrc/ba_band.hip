@@ -939,37 +939,35 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     int k = khi;
     // pseudo steps (the bottom side's separator rows, k >= kp): z_k is the top side's,
     // already in zs, so nothing is stored and each z is fetched one step ahead: the steps
-    // are independent subtractions instead of LDS round trips.  Every step's g operands come
-    // two steps ahead (the two register sets), the pseudo steps' too.
-    double zc[6] = {0, 0, 0, 0, 0, 0};
-    if (k >= kp && k >= klo) ld6g(dyn + zk, zc);
-    auto pstep = [&](int kk, const double (&gv)[6], double yin) __attribute__((always_inline)) {
-      double zn[6];
-      int on = kk - 1 >= kp ? zk + dz : zk;
-      asm volatile("" : "+v"(on));
-      ld6g(dyn + on, zn);
-      double d = gv[0] * zc[0] + gv[1] * zc[1] + gv[2] * zc[2] + gv[3] * zc[3] + gv[4] * zc[4] + gv[5] * zc[5];
-      asm volatile("" : "+v"(d));
-      Yb = qb == 0 ? yin : Yb - d;
-      qb = qb == 0 ? w : qb - 1;
-      zk += dz;
+    // are independent subtractions instead of LDS round trips
+    if (k >= kp && k >= klo) {
+      double zc[6];
+      ld6g(dyn + zk, zc);
+      for (; k >= kp && k >= klo; --k) {
+        double gv[6], yin, zn[6];
+        fetch(gv, yin);
+        int on = k - 1 >= kp ? zk + dz : zk;
+        asm volatile("" : "+v"(on));
+        ld6g(dyn + on, zn);
+        double d = gv[0] * zc[0] + gv[1] * zc[1] + gv[2] * zc[2] + gv[3] * zc[3] + gv[4] * zc[4] + gv[5] * zc[5];
+        asm volatile("" : "+v"(d));
+        Yb = qb == 0 ? yin : Yb - d;
+        qb = qb == 0 ? w : qb - 1;
+        zk += dz;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) zc[c] = zn[c];
-    };
-    auto any = [&](int kk, const double (&gv)[6], double yin) __attribute__((always_inline)) {
-      if (kk >= kp) pstep(kk, gv, yin);  // uniform
-      else step(kk, gv, yin);
-    };
+        for (int c = 0; c < 6; ++c) zc[c] = zn[c];
+      }
+    }
     double gA[6], gB[6], yA, yB;
     fetch(gA, yA);
     fetch(gB, yB);
     for (; k - 1 >= klo; k -= 2) {
-      any(k, gA, yA);
+      step(k, gA, yA);
       fetch(gA, yA);
-      any(k - 1, gB, yB);
+      step(k - 1, gB, yB);
       fetch(gB, yB);
     }
-    if (k >= klo) any(k, gA, yA);
+    if (k >= klo) step(k, gA, yA);
   };
   auto bs_go = [&](int khi, int klo, int kp) __attribute__((always_inline)) {
     if constexpr (kFull) bs_run_full(khi, klo, kp);
