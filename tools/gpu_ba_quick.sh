@@ -13,4 +13,5 @@ done
 timeout -k 10 200 python bench.py --config cfg4 --no-matcher --no-cpu-baseline --steps 50 --warmup 5 > $OUT/bench_cfg4.json 2> $OUT/bench_cfg4.err
 timeout -k 10 120 python tools/band_stamps.py cfg3 > $OUT/k3_stamps_cfg3.txt 2>&1
 timeout -k 10 300 python tools/host_call_latency.py > $OUT/host_latency.json 2> $OUT/host_latency.err
+timeout -k 10 300 python tools/ba_call_steps.py > $OUT/call_steps.json 2> $OUT/call_steps.err
 echo done
