@@ -171,11 +171,15 @@ int vo_ba_solve(vo_ctx* ctx, const vo_ba_problem* prob, double* poses, double* p
  * blocks [5] track entries [6] bytes read+written per GN iteration
  * (algorithmic) [7] banded solver in use [8] first-camera groups and
  * [9] chunks the last vo_ba_setup took over from the previous window's plan (the slide)
- * [10] observations per segment the plan was packed for. Returns count written. */
+ * [10] observations per segment the plan was packed for (1: the one-wave K1's plan);
+ * [11..22] host time of the last vo_ba_setup's sections in nanoseconds: stream sync, landmark
+ * order and track entries, segments, lists and chunk images, the rest of planning, plan checks,
+ * image uploads, reduction profile, uploads, buffers, banded-solver tables, attributes.
+ * Returns count written. */
 int vo_ba_plan_stats(vo_ctx* ctx, int64_t* out, int n);
 
-/* Diagnostic only: with VO_BA_STAMPS=1 in the environment at vo_ba_setup, K1
- * runs a separate stamped instantiation; returns per-phase shader-cycle sums over
+/* Diagnostic only: in a stamped build of the library (make EXTRA=-DVO_BA_STAMPS=1), K1
+ * and K3 record s_memtime phase stamps; returns per-phase shader-cycle sums over
  * all workgroups of the last K1 launch (load, backsub, linobs, reduce, elim,
  * schur_pairs, write, schur_cams, then two unused slots) followed by the K3 phase
  * cycles.  With n < 0 it instead writes up to -n raw per-segment values (10 per

@@ -52,6 +52,8 @@ def call(w, log, sync_after_setup):
     d = np.diff(t)
     for k, v in zip(steps, list(d) + [t[-1] - t[0]]):
         log[k].append(v * 1e3)
+    for k, v in s.plan_stats().get("setup_us", {}).items():  # the setup's own sections (us)
+        log.setdefault("setup_us." + k, []).append(v)
 
 
 out = {}

@@ -247,13 +247,19 @@ class BASession:
             check(rc, "vo_ba_gn_step")
         return rc, S, b, dc, float(cost[0])
 
+    SETUP_SECTIONS = ["sync", "order", "segments", "lists_images", "plan_rest", "plan_checks", "images",
+                      "profile", "uploads", "buffers", "band_tables", "attributes"]
+
     def plan_stats(self) -> dict:
-        out = np.zeros(11, dtype=np.int64)
-        n = check(self.ctx.lib.vo_ba_plan_stats(self.ctx.handle, ptr(out, C.c_int64), 11), "stats")
+        out = np.zeros(23, dtype=np.int64)
+        n = check(self.ctx.lib.vo_ba_plan_stats(self.ctx.handle, ptr(out, C.c_int64), 23), "stats")
         keys = ["chunks", "segments", "slab_blocks", "reduced_blocks", "profile_blocks",
                 "track_entries", "algorithmic_bytes_per_iter", "band_solver", "reused_groups",
                 "reused_chunks", "seg_obs"]
-        return dict(zip(keys[:n], out[:n].tolist()))
+        st = dict(zip(keys[:n], out[:n].tolist()))
+        if n > 11:  # the last setup's host sections (ns)
+            st["setup_us"] = {k: round(v / 1e3, 1) for k, v in zip(self.SETUP_SECTIONS, out[11:n].tolist())}
+        return st
 
 
 class SlidingWindowBA:

@@ -1849,13 +1849,12 @@ class BAEngine {
   // collective: with a communicator, all ranks then agree (min all-reduce of [ok, F, -F])
   // and fail together, so one rank's bad shard is an error everywhere, not a hang.
   uint64_t setup(const vo_ba_problem* prob) {
-#ifdef VO_PLAN_TIMING
-    auto t_ = std::chrono::steady_clock::now();
-#endif
+    PLAN_T_START();
+    for (int64_t& v : setup_clock().ns) v = 0;
     // the previous setup's chunk-image DMA may still read the page-locked images the
     // planner is about to rewrite (a setup that failed after its upload returns unsynced)
     VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
-    PLAN_T("setup: sync");
+    PLAN_T(0, "setup: sync");
     have_problem_ = false;
     have_state_ = false;
     std::string err;
@@ -1887,7 +1886,7 @@ class BAEngine {
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
                        prob->obs_uv, seg_obs_grid(seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave))), prev,
                        nw);
-      PLAN_T("setup: returned");
+      PLAN_T(4, "setup: returned");
       // four-wave K1: every first-camera group ends in a partial segment, so the packing target
       // may give more segments than one round holds; then pack once more, proportionally wider
       // (on the grid; a function of the plan, which does not depend on prev)
@@ -1910,7 +1909,7 @@ class BAEngine {
       if (err.empty() && agree[1] != -agree[2]) err = "ranks disagree on the number of free poses";
     }
     VO_REQUIRE(err.empty(), VO_ERR_ARG, "vo_ba_setup: %s", err.c_str());
-    PLAN_T("setup: planned");
+    PLAN_T(5, "setup: planned");
     // the largest plan array first: from page-locked memory the copy runs while the host
     // builds the profile and the K3 tables.  Images taken over from the previous plan are
     // copied on the device, in runs of consecutive chunks.
@@ -1933,7 +1932,7 @@ class BAEngine {
       }
       plan_ok_ = true;
     }
-    PLAN_T("setup: images");
+    PLAN_T(6, "setup: images");
     std::vector<int32_t> first = local_profile_first(plan_);
     if (ctx_->comm && ctx_->comm->nranks > 1 && !first.empty()) {
       DevBuf tmp;
@@ -1944,7 +1943,7 @@ class BAEngine {
       VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
     }
     build_profile(plan_, first);
-    PLAN_T("setup: profile");
+    PLAN_T(7, "setup: profile");
     prob_ = *prob;
     prob_.point_ptr = nullptr;
     prob_.obs_cam = nullptr;
@@ -1956,7 +1955,7 @@ class BAEngine {
     upload(d_slab_pos_, P.slab_pos, st);
     upload(d_cam_pos_, P.cam_pos, st);
     upload(d_seg_hdr_, P.seg_hdr, st);
-    PLAN_T("setup: uploads");
+    PLAN_T(8, "setup: uploads");
     const int F = P.n_free;
     d_points_.reserve(std::max(1, P.n_points) * 24ull);
     d_pose_[0].reserve(P.n_poses * 96ull);
@@ -1978,7 +1977,7 @@ class BAEngine {
                  "vo_ba_setup: %d free poses / panel of %d blocks exceed the solver's LDS budget", F,
                  TL.max_panel);
     }
-    PLAN_T("setup: bufs");
+    PLAN_T(9, "setup: bufs");
     const size_t lds = solve_layout_.total;
     solve_lds_size_ = lds;
     {  // banded K3 when the block bandwidth and F fit it; the profile solver otherwise
@@ -2040,13 +2039,14 @@ class BAEngine {
       d_zero_.reserve(512);  // zero block (masked prefetches)
       VO_HIP_CHECK(hipMemsetAsync(d_zero_.ptr, 0, 512, st));
     }
-    PLAN_T("setup: band");
+    PLAN_T(10, "setup: band");
     {
       const int l = (int)lds;
       set_solve_lds<true>(l);
       set_solve_lds<false>(l);
     }
-    PLAN_T("setup: attrs");
+    PLAN_T(11, "setup: attrs");
+    std::copy(setup_clock().ns, setup_clock().ns + kSetupSections, setup_ns_);
     // no sync: everything above is stream-ordered before the first iteration, pageable
     // sources are staged when their copy is issued, and the page-locked chunk images are
     // only rewritten after the sync at the top of the next setup
@@ -2206,10 +2206,11 @@ class BAEngine {
 
   int stats(int64_t* out, int n) const {
     const BAPlan& P = plan_;
-    const int64_t v[11] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), (int64_t)P.slot_i.size(),
-                           P.n_prof_blocks(), P.n_te, P.algorithmic_bytes_per_iter(), band_on_ ? 1 : 0,
-                           P.reused_groups, P.reused_chunks, P.seg_obs};
-    const int k = std::min(n, 11);
+    int64_t v[11 + kSetupSections] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), (int64_t)P.slot_i.size(),
+                                      P.n_prof_blocks(), P.n_te, P.algorithmic_bytes_per_iter(), band_on_ ? 1 : 0,
+                                      P.reused_groups, P.reused_chunks, P.seg_obs};
+    for (int i = 0; i < kSetupSections; ++i) v[11 + i] = setup_ns_[i];  // the last setup's sections
+    const int k = std::min(n, 11 + kSetupSections);
     for (int i = 0; i < k; ++i) out[i] = v[i];
     return k;
   }
@@ -2467,6 +2468,7 @@ class BAEngine {
   BAPlan plan_{true};  // page-locked chunk images (async upload)
   BAPlan prev_plan_{true};  // the previous window's plan (group take-over), or scratch
   bool plan_ok_ = false;    // plan_ built and its images in d_chunk_img_
+  int64_t setup_ns_[kSetupSections] = {};  // the last setup's host sections (vo_ba_plan_stats)
   vo_ba_problem prob_{};
   bool have_problem_ = false, have_state_ = false, pending_ = false, solve_lds_ = false;
   uint64_t session_ = 0;

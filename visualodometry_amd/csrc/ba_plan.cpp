@@ -349,9 +349,6 @@ void BAPlan::reset() {
 std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_t* point_ptr,
                        const int32_t* obs_cam, const float* obs_uv, int seg_obs, const BAPlan* prev,
                        int seg_chunks) {
-#ifdef VO_PLAN_TIMING
-  auto t_ = std::chrono::steady_clock::now();
-#endif
   P.reset();
   if (N < 1 || L < 0 || M < 0) return fmt("bad sizes n_poses=%ld n_points=%ld n_obs=%ld", N, L, M);
   if (N > 32767) return fmt("n_poses=%ld exceeds the 32767 camera ids of a segment header", N);
@@ -503,7 +500,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   }
   P.pt_te[L] = P.n_te;
   P.te_obs[P.n_te] = M;
-  PLAN_T("order + track entries");
+  PLAN_T(1, "order + track entries");
 
   // ---- chunks and segments: each first-camera group packed greedily on its own (so a
   // group's packing depends on its own landmarks only), or taken over from prev
@@ -749,7 +746,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   P.chunk_obs.push_back(M);
   P.chunk_te.push_back(P.n_te);
   P.chunk_pt.push_back(L);
-  PLAN_T("segments");
+  PLAN_T(2, "segments");
 
   // ---- per segment: sorted windows, slab offsets, per chunk pair and camera lists,
   // chunk headers and LDS images, segment headers.  Offsets first (prefix sums over
@@ -1172,7 +1169,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   if (P.cam_list.empty()) P.cam_list.push_back(0);
   if (P.camo_list.empty()) P.camo_list.push_back(0);
   if (P.segcam_diag.empty()) P.segcam_diag.push_back(0);
-  PLAN_T("lists+images");
+  PLAN_T(3, "lists+images");
   return "";
 }
 

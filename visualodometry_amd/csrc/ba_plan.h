@@ -26,21 +26,40 @@
 #include <utility>
 #include <string>
 #include <vector>
-// Diagnostic build only (EXTRA=-DVO_PLAN_TIMING): host setup section times to stderr.
-#include <cstdio>
-#ifdef VO_PLAN_TIMING
+// Host setup sections: PLAN_T(i, name) records the time since the previous mark of the calling
+// thread as section i (kSetupSections, read back by vo_ba_plan_stats; a steady_clock read, tens
+// of nanoseconds); diagnostic builds (EXTRA=-DVO_PLAN_TIMING) also print it to stderr.
 #include <chrono>
-#define PLAN_T(name)                                                                                          \
-  do {                                                                                                        \
-    const auto n_ = std::chrono::steady_clock::now();                                                         \
-    std::fprintf(stderr, "  %-14s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(n_ - t_).count()); \
-    t_ = n_;                                                                                                  \
-  } while (0)
+#include <cstdio>
+namespace vo {
+constexpr int kSetupSections = 12;  // sync, order, segments, lists, returned, planned, images, profile,
+                                    // uploads, bufs, band, attrs
+struct SetupClock {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  int64_t ns[kSetupSections] = {};
+};
+inline SetupClock& setup_clock() {
+  static thread_local SetupClock c;
+  return c;
+}
+}  // namespace vo
+#ifdef VO_PLAN_TIMING
+#define PLAN_T_PRINT(name, ns) std::fprintf(stderr, "  %-14s %8.3f ms\n", name, (ns) * 1e-6)
 #else
-#define PLAN_T(name) \
-  do {               \
+#define PLAN_T_PRINT(name, ns) \
+  do {                         \
   } while (0)
 #endif
+#define PLAN_T(i, name)                                                                             \
+  do {                                                                                              \
+    ::vo::SetupClock& c_ = ::vo::setup_clock();                                                     \
+    const auto n_ = std::chrono::steady_clock::now();                                               \
+    const int64_t d_ = std::chrono::duration_cast<std::chrono::nanoseconds>(n_ - c_.t).count();     \
+    c_.ns[i] = d_;                                                                                  \
+    c_.t = n_;                                                                                      \
+    PLAN_T_PRINT(name, d_);                                                                         \
+  } while (0)
+#define PLAN_T_START() (::vo::setup_clock().t = std::chrono::steady_clock::now())
 
 namespace vo {
 
