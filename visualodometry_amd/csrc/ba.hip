@@ -1822,6 +1822,32 @@ __global__ __launch_bounds__(64 * NW) void ba_solve_kernel(SolveArgs A) {
 }
 
 
+// Chunk images taken over from the previous plan: runs of consecutive chunks copied on the
+// device by a kernel (hipMemcpyAsync device-to-device went through a copy engine at ~12 GB/s on
+// some boxes: 0.36-0.45 ms for a slid cfg3 window's 3.5 MB).  The runs travel in the arguments.
+constexpr int kImgRuns = 48;
+struct ImgRuns {
+  int n;                    // runs in this launch
+  int src[kImgRuns], dst[kImgRuns], end[kImgRuns];  // run r: chunks [end[r-1], end[r]) of the launch
+};
+__global__ __launch_bounds__(64) void ba_img_copy_kernel(const uint4* __restrict__ prev, uint4* __restrict__ cur,
+                                                          ImgRuns R) {
+  constexpr int kVec = (int)(sizeof(ChunkImg) / 16);
+  const int b = blockIdx.x;
+  int r = 0;
+  while (r + 1 < R.n && R.end[r] <= b) ++r;  // uniform
+  const int off = b - (r ? R.end[r - 1] : 0);
+  const uint4* s = prev + (long)(R.src[r] + off) * kVec;
+  uint4* d = cur + (long)(R.dst[r] + off) * kVec;
+  uint4 v[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) v[k] = s[min((int)threadIdx.x + 64 * k, kVec - 1)];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    if ((int)threadIdx.x + 64 * k < kVec) d[threadIdx.x + 64 * k] = v[k];
+}
+static_assert(sizeof(ChunkImg) / 16 <= 192, "three 16-byte pieces per lane");
+
 template <class T, class A>
 void upload(DevBuf& buf, const std::vector<T, A>& v, hipStream_t st) {
   buf.reserve(std::max<size_t>(v.size(), 1) * sizeof(T));
@@ -1917,19 +1943,33 @@ class BAEngine {
       const BAPlan& P = plan_;
       const int nch = (int)P.chunk_img.size();
       d_chunk_img_.reserve(std::max(nch, 1) * sizeof(ChunkImg));
+      ImgRuns R{};
+      int copied = 0;
+      auto flush = [&]() {
+        if (R.n == 0) return;
+        hipLaunchKernelGGL(ba_img_copy_kernel, dim3(copied), dim3(64), 0, ctx_->stream,
+                           d_chunk_img_prev_.as<uint4>(), d_chunk_img_.as<uint4>(), R);
+        VO_HIP_CHECK(hipGetLastError());
+        R.n = 0;
+        copied = 0;
+      };
       for (int c0 = 0; c0 < nch;) {
         const int src = c0 < (int)P.chunk_src.size() ? P.chunk_src[c0] : -1;
         int c1 = c0 + 1;
         while (c1 < nch && (src < 0 ? P.chunk_src[c1] < 0 : P.chunk_src[c1] == src + (c1 - c0))) ++c1;
-        ChunkImg* dst = d_chunk_img_.as<ChunkImg>() + c0;
-        const size_t bytes = (size_t)(c1 - c0) * sizeof(ChunkImg);
-        if (src >= 0)
-          VO_HIP_CHECK(hipMemcpyAsync(dst, d_chunk_img_prev_.as<ChunkImg>() + src, bytes, hipMemcpyDeviceToDevice,
-                                      ctx_->stream));
-        else
-          VO_HIP_CHECK(hipMemcpyAsync(dst, P.chunk_img.data() + c0, bytes, hipMemcpyHostToDevice, ctx_->stream));
+        if (src >= 0) {  // taken over: a run of the copy kernel
+          if (R.n == kImgRuns) flush();
+          R.src[R.n] = src;
+          R.dst[R.n] = c0;
+          copied += c1 - c0;
+          R.end[R.n++] = copied;
+        } else {  // built by this plan: from the page-locked images
+          VO_HIP_CHECK(hipMemcpyAsync(d_chunk_img_.as<ChunkImg>() + c0, P.chunk_img.data() + c0,
+                                      (size_t)(c1 - c0) * sizeof(ChunkImg), hipMemcpyHostToDevice, ctx_->stream));
+        }
         c0 = c1;
       }
+      flush();
       plan_ok_ = true;
     }
     PLAN_T(6, "setup: images");
