@@ -1877,6 +1877,9 @@ class BAEngine {
   uint64_t setup(const vo_ba_problem* prob) {
     PLAN_T_START();
     for (int64_t& v : setup_clock().ns) v = 0;
+    // the planner's threads wake now (their wake-up runs under the stream sync below) and poll
+    // until the plan is built
+    std::unique_ptr<PlanSessionGuard> planning(new PlanSessionGuard);
     // the previous setup's chunk-image DMA may still read the page-locked images the
     // planner is about to rewrite (a setup that failed after its upload returns unsynced)
     VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
@@ -1923,6 +1926,7 @@ class BAEngine {
                          prob->obs_uv, so2, prev);
       }
     }
+    planning.reset();  // the plan is built: the threads may sleep
     if (ctx_->comm && ctx_->comm->nranks > 1) {
       const int32_t F = err.empty() ? plan_.n_free : 0;
       std::vector<int32_t> agree = {err.empty() ? 1 : 0, F, -F};
