@@ -46,6 +46,9 @@
 #include "ba_plan.h"
 #include "vo_ctx.h"
 
+#ifndef VO_PLAN_EARLY_WAKE
+#define VO_PLAN_EARLY_WAKE 1  // tuning build: 0 leaves the planner's threads asleep until its first phase
+#endif
 #ifndef VO_BA_FUSE
 #define VO_BA_FUSE 1  // tuning build: 0 launches K2 on its own
 #endif
@@ -1879,7 +1882,7 @@ class BAEngine {
     for (int64_t& v : setup_clock().ns) v = 0;
     // the planner's threads wake now (their wake-up runs under the stream sync below) and poll
     // until the plan is built
-    std::unique_ptr<PlanSessionGuard> planning(new PlanSessionGuard);
+    std::unique_ptr<PlanSessionGuard> planning(VO_PLAN_EARLY_WAKE ? new PlanSessionGuard : nullptr);
     // the previous setup's chunk-image DMA may still read the page-locked images the
     // planner is about to rewrite (a setup that failed after its upload returns unsynced)
     VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));

@@ -80,6 +80,9 @@ int host_threads() {
 #define VO_PLAN_SESSION_SPIN 1
 #endif
 constexpr bool kPlanSessionSpin = VO_PLAN_SESSION_SPIN != 0;
+#ifndef VO_PLAN_LOCAL_IMG
+#define VO_PLAN_LOCAL_IMG 1  // tuning build: 0 builds each chunk image in place
+#endif
 
 inline void cpu_relax() {
 #if defined(__x86_64__) || defined(__i386__)
@@ -1008,7 +1011,12 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         // the chunk's LDS image (chunk-relative offsets, unused entries zero), built in a local
         // buffer and copied out whole: the engine's images are page-locked memory, which the CPU
         // reads uncached (the build reads its own fields back) and writes best in whole lines
+#if VO_PLAN_LOCAL_IMG
         ChunkImg g{};
+#else
+        ChunkImg& g = P.chunk_img[ch];
+        g = ChunkImg();
+#endif
         const int nob = h[1], nte = h[3], p0 = h[4], npt = h[5];
         const int e0 = h[8], e1 = h[9], c0 = h[10], c1 = h[11], q0 = h[12], q1 = h[13];
         for (int i = 0; i < nob; ++i) {
@@ -1164,7 +1172,9 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         }
         for (int i = 0; i < c1 - c0; ++i) g.caml[i] = P.cam_list[c0 + i];
         for (int i = 0; i < q1 - q0; ++i) g.camol[i] = P.camo_list[q0 + i];
+#if VO_PLAN_LOCAL_IMG
         std::memcpy(&P.chunk_img[ch], &g, sizeof g);
+#endif
         h[14] = nas;
         h[15] = nac;
       }
