@@ -46,9 +46,6 @@
 #include "ba_plan.h"
 #include "vo_ctx.h"
 
-#ifndef VO_PLAN_EARLY_WAKE
-#define VO_PLAN_EARLY_WAKE 1  // tuning build: 0 leaves the planner's threads asleep until its first phase
-#endif
 #ifndef VO_BA_FUSE
 #define VO_BA_FUSE 1  // tuning build: 0 launches K2 on its own
 #endif
@@ -1880,9 +1877,6 @@ class BAEngine {
   uint64_t setup(const vo_ba_problem* prob) {
     PLAN_T_START();
     for (int64_t& v : setup_clock().ns) v = 0;
-    // the planner's threads wake now (their wake-up runs under the stream sync below) and poll
-    // until the plan is built
-    std::unique_ptr<PlanSessionGuard> planning(VO_PLAN_EARLY_WAKE ? new PlanSessionGuard : nullptr);
     // the previous setup's chunk-image DMA may still read the page-locked images the
     // planner is about to rewrite (a setup that failed after its upload returns unsynced)
     VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
@@ -1929,7 +1923,6 @@ class BAEngine {
                          prob->obs_uv, so2, prev);
       }
     }
-    planning.reset();  // the plan is built: the threads may sleep
     if (ctx_->comm && ctx_->comm->nranks > 1) {
       const int32_t F = err.empty() ? plan_.n_free : 0;
       std::vector<int32_t> agree = {err.empty() ? 1 : 0, F, -F};

@@ -80,9 +80,7 @@ int host_threads() {
 #define VO_PLAN_SESSION_SPIN 1
 #endif
 constexpr bool kPlanSessionSpin = VO_PLAN_SESSION_SPIN != 0;
-#ifndef VO_PLAN_LOCAL_IMG
-#define VO_PLAN_LOCAL_IMG 1  // tuning build: 0 builds each chunk image in place
-#endif
+
 
 inline void cpu_relax() {
 #if defined(__x86_64__) || defined(__i386__)
@@ -143,14 +141,11 @@ class PlanPool {
     }
     if (first) std::rethrow_exception(first);
   }
-  // a plan is being built: workers poll between its phases (see kPlanSessionSpin); sleeping
-  // workers are woken now, so that they poll by the time the first phase starts
+  // a plan is being built: workers poll between its phases (see kPlanSessionSpin).  (Waking
+  // them at the start of vo_ba_setup, before the plan, measured slower: 0.66 -> 0.83 ms per
+  // cfg3 setup, the polling threads competing with the setup thread.)
   void begin_session() {
-    if (!kPlanSessionSpin) return;
-    if (session_.fetch_add(1, std::memory_order_acq_rel) == 0) {
-      { std::lock_guard<std::mutex> lk(mu_); }
-      cv_.notify_all();
-    }
+    if (kPlanSessionSpin) session_.fetch_add(1, std::memory_order_acq_rel);
   }
   void end_session() {
     if (kPlanSessionSpin) session_.fetch_sub(1, std::memory_order_acq_rel);
@@ -175,9 +170,8 @@ class PlanPool {
       while (session_.load(std::memory_order_acquire) > 0 && gen_.load(std::memory_order_acquire) == seen) cpu_relax();
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || gen_ != seen || session_.load(std::memory_order_acquire) > 0; });
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
         if (stop_) return;
-        if (gen_ == seen) continue;  // woken by a session's start: poll for its first phase
         seen = gen_;
         if (t > active_) continue;  // not needed this round
         job = job_;
@@ -198,13 +192,6 @@ class PlanPool {
   std::atomic<int> session_{0};  // plans being built (begin_session / end_session)
   bool stop_ = false;
 };
-
-}  // namespace
-
-PlanSessionGuard::PlanSessionGuard() { PlanPool::get().begin_session(); }
-PlanSessionGuard::~PlanSessionGuard() { PlanPool::get().end_session(); }
-
-namespace {
 
 // The polling window of one build_plan call (plans of one thread start no session).
 struct PlanSession {
@@ -1011,12 +998,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         // the chunk's LDS image (chunk-relative offsets, unused entries zero), built in a local
         // buffer and copied out whole: the engine's images are page-locked memory, which the CPU
         // reads uncached (the build reads its own fields back) and writes best in whole lines
-#if VO_PLAN_LOCAL_IMG
         ChunkImg g{};
-#else
-        ChunkImg& g = P.chunk_img[ch];
-        g = ChunkImg();
-#endif
         const int nob = h[1], nte = h[3], p0 = h[4], npt = h[5];
         const int e0 = h[8], e1 = h[9], c0 = h[10], c1 = h[11], q0 = h[12], q1 = h[13];
         for (int i = 0; i < nob; ++i) {
@@ -1172,9 +1154,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         }
         for (int i = 0; i < c1 - c0; ++i) g.caml[i] = P.cam_list[c0 + i];
         for (int i = 0; i < q1 - q0; ++i) g.camol[i] = P.camo_list[q0 + i];
-#if VO_PLAN_LOCAL_IMG
         std::memcpy(&P.chunk_img[ch], &g, sizeof g);
-#endif
         h[14] = nas;
         h[15] = nac;
       }

@@ -284,15 +284,6 @@ struct BAPlan {
   int64_t algorithmic_bytes_per_iter() const;
 };
 
-// The planner's host threads poll for work (instead of sleeping) while a guard lives; vo_ba_setup
-// takes one at its start, so that the threads are awake when its plan's first phase starts.
-struct PlanSessionGuard {
-  PlanSessionGuard();
-  ~PlanSessionGuard();
-  PlanSessionGuard(const PlanSessionGuard&) = delete;
-  PlanSessionGuard& operator=(const PlanSessionGuard&) = delete;
-};
-
 // The packing target of a window of n_obs observations for target_segments K1 workgroups.
 int seg_obs_for(int64_t n_obs, int target_segments);
 // The smallest packing target of a fixed geometric grid (ceil(2^(k/8)), steps of ~9 %) that is
