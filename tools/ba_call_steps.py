@@ -24,7 +24,7 @@ small = make_ba_problem(8, 200, 11)
 
 
 def call(w, log, sync_after_setup):
-    obs_pt = np.repeat(np.arange(w.n_points), np.diff(w.point_ptr))
+    obs_pt = np.repeat(np.arange(w.n_points, dtype=np.int32), np.diff(w.point_ptr))
     win = BAWindow(w.poses_cw, w.points, w.obs_uv, w.obs_cam, obs_pt, w.n_fixed)
     t = [time.perf_counter()]
     point_ptr, obs_cam, obs_uv = group_window(w.n_points, win)

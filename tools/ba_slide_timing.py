@@ -21,7 +21,7 @@ steps = ["csr", "setup", "set_state", "run10", "get_state", "total"]
 
 
 def call(w, log):
-    obs_pt = np.repeat(np.arange(w.n_points), np.diff(w.point_ptr))
+    obs_pt = np.repeat(np.arange(w.n_points, dtype=np.int32), np.diff(w.point_ptr))
     win = BAWindow(w.poses_cw, w.points, w.obs_uv, w.obs_cam, obs_pt, w.n_fixed)
     t0 = time.perf_counter()
     point_ptr, obs_cam, obs_uv = group_window(w.n_points, win)

@@ -51,13 +51,13 @@ out["tri_ms"] = timed(lambda: triangulate.triangulate_all(T1, T2, q1, q2, K, 0.0
 X, uv, Kp, _, _ = pnp_case(1000, 5)
 out["pnp_ms"] = timed(lambda: pnp.pnp_ransac(X, uv, Kp, 1.0, ctx=ctx))
 p = make_ba_config("cfg3")
-obs_pt = np.repeat(np.arange(p.n_points), np.diff(p.point_ptr))
+obs_pt = np.repeat(np.arange(p.n_points, dtype=np.int32), np.diff(p.point_ptr))
 win = BAWindow(p.poses_cw, p.points, p.obs_uv, p.obs_cam, obs_pt, p.n_fixed)
 ba = SlidingWindowBA(p.K, iters=10, lam=1.0, device=0)
 out["ba_cfg3_10iters_ms"] = timed(lambda: ba.optimize(win), reps=5, warm=1)
 small = make_ba_problem(8, 200, 11)
 small_win = BAWindow(small.poses_cw, small.points, small.obs_uv, small.obs_cam,
-                     np.repeat(np.arange(small.n_points), np.diff(small.point_ptr)), small.n_fixed)
+                     np.repeat(np.arange(small.n_points, dtype=np.int32), np.diff(small.point_ptr)), small.n_fixed)
 
 
 def scratch_call(w):
@@ -71,7 +71,7 @@ out["ba_cfg3_scratch_ms"] = float(np.median([scratch_call(win) for _ in range(12
 slides = []
 for w in make_ba_slide("cfg3", 18):
     slides.append(BAWindow(w.poses_cw, w.points, w.obs_uv, w.obs_cam,
-                           np.repeat(np.arange(w.n_points), np.diff(w.point_ptr)), w.n_fixed))
+                           np.repeat(np.arange(w.n_points, dtype=np.int32), np.diff(w.point_ptr)), w.n_fixed))
 ba.optimize(slides[0])
 ba.optimize(slides[1])
 t = []
