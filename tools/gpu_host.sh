@@ -1,5 +1,5 @@
 #!/bin/bash
-# Host-call latency (product library), the setup's sections (a -DVO_PLAN_TIMING build), and the
+# Host-call latency and the setup's sections (product library: vo_ba_plan_stats), and the
 # landmark-shard projections.  Usage: gpurun --timeout 900 -- bash tools/gpu_host.sh [tag]
 set -euo pipefail
 TAG=${1:-host}
@@ -8,8 +8,6 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python tools/host_call_latency.py > $OUT/host_latency.json 2> $OUT/host_latency.err
 timeout -k 10 300 python tools/ba_slide_timing.py 12 > $OUT/slide_timing.json 2> $OUT/slide_timing.err
-VO_LIB_PATH=visualodometry_amd/lib/libvo_hip_ptiming.so timeout -k 10 300 python tools/ba_slide_timing.py 8 \
-  > $OUT/slide_timing_sections.json 2> $OUT/slide_timing_sections.err
 timeout -k 10 300 python tools/shard_projection.py cfg3 > $OUT/shard_projection_cfg3.json 2> $OUT/shard_projection_cfg3.err
 timeout -k 10 300 python tools/shard_projection.py cfg4 > $OUT/shard_projection_cfg4.json 2> $OUT/shard_projection_cfg4.err
 echo done

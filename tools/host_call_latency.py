@@ -80,8 +80,8 @@ for w in slides[2:]:
     ba.optimize(w)
     t.append(time.perf_counter() - t0)
 out["ba_cfg3_slide_ms"] = float(np.median(t)) * 1e3
-out["ba_cfg3_slide_windows_scratch_ms"] = float(np.median([scratch_call(w) for w in slides[2:]])) * 1e3
-st = np.zeros(11, dtype=np.int64)
+st = np.zeros(11, dtype=np.int64)  # the last slid window's plan (before the scratch calls below)
 ctx.lib.vo_ba_plan_stats(ctx.handle, _lib.ptr(st, _lib.C.c_int64), 11)
 out["ba_cfg3_slide_last"] = {"chunks": int(st[0]), "reused_chunks": int(st[9]), "reused_groups": int(st[8])}
+out["ba_cfg3_slide_windows_scratch_ms"] = float(np.median([scratch_call(w) for w in slides[2:]])) * 1e3
 print(json.dumps(out))

@@ -1982,7 +1982,12 @@ class BAEngine {
                                   ctx_->stream));
       VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
     }
-    build_profile(plan_, first);
+    // banded K3 when the block bandwidth and F fit it (decided on first[], before the
+    // profile, whose step tables only the profile solver reads); the profile solver otherwise
+    const int F = plan_.n_free;
+    band_ = band_split(F, std::vector<int>(first.begin(), first.end()));
+    band_on_ = F > 0 && band_supported(F, band_.w, plan_.n_poses);
+    build_profile(plan_, first, !band_on_);
     PLAN_T(7, "setup: profile");
     prob_ = *prob;
     prob_.point_ptr = nullptr;
@@ -1991,12 +1996,12 @@ class BAEngine {
 
     hipStream_t st = ctx_->stream;
     const BAPlan& P = plan_;
-    upload(d_chunk_hdr_, P.chunk_hdr, st);
-    upload(d_slab_pos_, P.slab_pos, st);
-    upload(d_cam_pos_, P.cam_pos, st);
-    upload(d_seg_hdr_, P.seg_hdr, st);
+    // the plan's small tables, placed in one device buffer and sent with one copy (below)
+    TablePack pack;
+    const size_t o_chunk_hdr = pack.add(P.chunk_hdr), o_slab_pos = pack.add(P.slab_pos),
+                 o_cam_pos = pack.add(P.cam_pos), o_seg_hdr = pack.add(P.seg_hdr);
+    size_t o_solve_tab = 0, o_band_tab = 0;
     PLAN_T(8, "setup: uploads");
-    const int F = P.n_free;
     d_points_.reserve(std::max(1, P.n_points) * 24ull);
     d_pose_[0].reserve(P.n_poses * 96ull);
     d_pose_[1].reserve(P.n_poses * 96ull);
@@ -2005,10 +2010,8 @@ class BAEngine {
     d_slab_b_.reserve(std::max<size_t>(1, P.segcam_f.size()) * 48ull);
     d_slab_cost_.reserve(std::max(1, P.n_segments()) * 8ull);
     d_linv_.reserve(std::max(1, F) * 288ull);
-    d_status_.reserve(sizeof(int));
-    VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
-    upload(d_solve_tab_, P.solve_tab, st);
-    {
+    if (!band_on_) {
+      o_solve_tab = pack.add(P.solve_tab);
       const SolveTableLayout& TL = P.solve_layout;
       const SolveLds in_lds = solve_lds_layout(true, P.n_prof_blocks(), F, TL.max_panel, TL.len, P.n_poses);
       solve_lds_ = in_lds.total <= kSolveLdsMax;
@@ -2016,14 +2019,10 @@ class BAEngine {
       VO_REQUIRE(solve_layout_.total <= kSolveLdsMax, VO_ERR_ARG,
                  "vo_ba_setup: %d free poses / panel of %d blocks exceed the solver's LDS budget", F,
                  TL.max_panel);
+      solve_lds_size_ = solve_layout_.total;
     }
     PLAN_T(9, "setup: bufs");
-    const size_t lds = solve_layout_.total;
-    solve_lds_size_ = lds;
-    {  // banded K3 when the block bandwidth and F fit it; the profile solver otherwise
-      std::vector<int> first(P.prof_first.begin(), P.prof_first.end());
-      band_ = band_split(F, first);
-      band_on_ = F > 0 && band_supported(F, band_.w, P.n_poses);
+    {
       // K2's output layout: the profile [S | b | cost], or the banded K3's columns
       const int nprof = P.n_prof_blocks();
       red_dst_.assign(std::max(1, nprof), 0);
@@ -2044,8 +2043,8 @@ class BAEngine {
         pad = band_slot_stride(w);  // the ring loader's last LDS-DMA piece reads past the end
         band_lds_ = band_lds_layout(F, band_, P.n_poses);
         band_tab_ = band_tables(F, band_, band_lds_);
-        upload(d_band_tab_, band_tab_.tab, st);
-        band_set_attributes(band_lds_);
+        o_band_tab = pack.add(band_tab_.tab);
+        band_set_attributes(band_lds_);  // (a no-op unless the LDS size grows)
         if (!band_lds_.full) d_fac_.reserve(band_fac_doubles(F, w) * 8);
       } else {
         for (int b = 0; b < nprof; ++b) red_dst_[b] = 36 * b;
@@ -2057,31 +2056,50 @@ class BAEngine {
       // entries K2 never writes (outside the profile, the bottom side's separator) stay 0
       VO_HIP_CHECK(hipMemsetAsync(d_sys_.ptr, 0, (sys_len_ + pad) * 8, st));
       // K2's per-block table: slab rows, the diagonal blocks' rhs entries, output offsets
-      std::vector<int4> meta(std::max(1, nprof), int4{0, 0, -1, -1});
-      std::vector<int2> out(std::max(1, nprof), int2{0, 0});
+      red_meta_.assign(std::max(1, nprof), int4{0, 0, -1, -1});
+      red_out_.assign(std::max(1, nprof), int2{0, 0});
       for (int i = 0; i < F; ++i)
         for (int b = P.prof_off[i]; b < P.prof_off[i + 1]; ++b) {
           const bool diag = P.prof_diag[b] != 0;
-          meta[b] = int4{P.prof_src_ptr[b], P.prof_src_ptr[b + 1], diag ? P.camb_ptr[i] : -1,
-                         diag ? P.camb_ptr[i + 1] : -1};
-          out[b] = int2{red_dst_[b], diag ? red_rdst_[i] : 0};
+          red_meta_[b] = int4{P.prof_src_ptr[b], P.prof_src_ptr[b + 1], diag ? P.camb_ptr[i] : -1,
+                              diag ? P.camb_ptr[i + 1] : -1};
+          red_out_[b] = int2{red_dst_[b], diag ? red_rdst_[i] : 0};
         }
-      upload(d_red_meta_, meta, st);
-      upload(d_red_out_, out, st);
+      const size_t o_meta = pack.add(red_meta_), o_out = pack.add(red_out_);
       // K2 fused into the banded K3's launch when every workgroup of it fits one round at
       // one per CU (the solver's LDS): cfg3's 356 blocks make 178 reducers + the solver on
       // MI355X's 256 CUs (fewer CUs, e.g. a partitioned device: K2 stays a launch of its own)
       // (full mode only: the ring-mode solver reads sys with plain loads, so it must come from an
       // earlier launch)
       fuse_ok_ = VO_BA_FUSE && band_on_ && band_lds_.full && band_fused_workgroups(nprof) + 1 <= ctx_->num_cus;
-      d_red_count_.reserve(256);
-      VO_HIP_CHECK(hipMemsetAsync(d_red_count_.ptr, 0, 256, st));
-      d_zero_.reserve(512);  // zero block (masked prefetches)
-      VO_HIP_CHECK(hipMemsetAsync(d_zero_.ptr, 0, 512, st));
+
+      // one page-locked staging buffer, one device buffer, one copy (each table a pageable
+      // copy of its own cost several µs of host time apiece); both are rewritten only after the
+      // stream sync at the top of the next setup
+      h_tab_.reserve(pack.bytes);
+      d_tab_.reserve(pack.bytes);
+      for (const TablePack::Part& q : pack.parts)
+        if (q.n) std::memcpy(h_tab_.as<char>() + q.off, q.src, q.n);
+      VO_HIP_CHECK(hipMemcpyAsync(d_tab_.ptr, h_tab_.ptr, pack.bytes, hipMemcpyHostToDevice, st));
+      char* base = d_tab_.as<char>();
+      d_chunk_hdr_.ptr = base + o_chunk_hdr;
+      d_slab_pos_.ptr = base + o_slab_pos;
+      d_cam_pos_.ptr = base + o_cam_pos;
+      d_seg_hdr_.ptr = base + o_seg_hdr;
+      d_solve_tab_.ptr = band_on_ ? nullptr : base + o_solve_tab;
+      d_band_tab_.ptr = band_on_ ? base + o_band_tab : nullptr;
+      d_red_meta_.ptr = base + o_meta;
+      d_red_out_.ptr = base + o_out;
+      // the status word, K2's fused-round counter and the zero block (masked prefetches)
+      d_misc_.reserve(kMiscBytes);
+      d_status_.ptr = d_misc_.ptr;
+      d_red_count_.ptr = d_misc_.as<char>() + 256;
+      d_zero_.ptr = d_misc_.as<char>() + 512;
+      VO_HIP_CHECK(hipMemsetAsync(d_misc_.ptr, 0, kMiscBytes, st));
     }
     PLAN_T(10, "setup: band");
-    {
-      const int l = (int)lds;
+    if (!band_on_) {
+      const int l = (int)solve_lds_size_;
       set_solve_lds<true>(l);
       set_solve_lds<false>(l);
     }
@@ -2422,10 +2440,17 @@ class BAEngine {
     else
       hipLaunchKernelGGL((ba_solve_kernel<false, kBaStamps, 4>), dim3(1), dim3(256), solve_lds_size_, ctx_->stream, A);
   }
+  // the kernel's dynamic-LDS limit, raised only when a window needs more than any before it
+  // (a process-wide attribute of the kernel)
   template <bool kL>
   static void set_solve_lds(int lds) {
+    static std::atomic<int> set{-1};
+    int cur = set.load(std::memory_order_relaxed);
+    if (lds <= cur) return;
     VO_HIP_CHECK(hipFuncSetAttribute((const void*)ba_solve_kernel<kL, kBaStamps, 4>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    while (cur < lds && !set.compare_exchange_weak(cur, lds, std::memory_order_relaxed)) {
+    }
   }
 
   void enqueue_solve(int iter_tag, double* cost_slot = nullptr) {
@@ -2520,14 +2545,45 @@ class BAEngine {
   bool fuse_ok_ = false;  // K2 fused into K3's launch (see fused())
   BandLds band_lds_;
   BandTables band_tab_;
-  DevBuf d_fac_, d_zero_, d_band_tab_, d_red_meta_, d_red_out_, d_red_count_;
+  // views into d_tab_ (the plan's small tables, one upload per setup) and d_misc_
+  struct DevView {
+    void* ptr = nullptr;
+    template <class T>
+    T* as() const {
+      return static_cast<T*>(ptr);
+    }
+  };
+  struct TablePack {  // the tables' places in d_tab_ (256-byte aligned) and their host sources
+    struct Part {
+      size_t off;
+      const void* src;
+      size_t n;
+    };
+    std::vector<Part> parts;
+    size_t bytes = 0;
+    template <class V>
+    size_t add(const V& v) {
+      const size_t off = (bytes + 255) & ~(size_t)255, n = v.size() * sizeof(v[0]);
+      parts.push_back({off, v.data(), n});
+      bytes = off + std::max<size_t>(n, 16);
+      return off;
+    }
+  };
+  HostBuf h_tab_;
+  DevBuf d_tab_;
+  DevView d_chunk_hdr_, d_seg_hdr_, d_slab_pos_, d_cam_pos_, d_solve_tab_, d_band_tab_, d_red_meta_, d_red_out_;
+  static constexpr size_t kMiscBytes = 1024;
+  DevBuf d_misc_;  // [status | K2 fused-round counter | zero block (512 B)]
+  DevView d_status_, d_red_count_, d_zero_;
+  std::vector<int4> red_meta_;
+  std::vector<int2> red_out_;
+  DevBuf d_fac_;
   std::vector<int32_t> red_dst_, red_rdst_;  // K2 output offsets (host copies for gn_step)
   long cost_off_ = 0;
-  DevBuf d_solve_tab_;
   HostBuf h_state_;  // page-locked staging of set_state / get_state
   hipEvent_t h_state_ev_ = nullptr;  // set_state's upload from h_state_ done
   bool h_state_busy_ = false;
-  DevBuf d_chunk_hdr_, d_seg_hdr_, d_chunk_img_, d_slab_pos_, d_cam_pos_;  // K1's plan (the chunk images hold every list)
+  DevBuf d_chunk_img_;  // K1's plan (the chunk images hold every list)
   DevBuf d_chunk_img_prev_;  // the previous plan's images (prev_plan_)
   DevBuf d_stamps_, d_stamps3_;
   static constexpr bool stamps_on_ = kBaStamps;
@@ -2562,7 +2618,7 @@ class BAEngine {
 
  private:
   DevBuf d_points_, d_pose_[2], d_dc_, d_slab_, d_slab_b_, d_slab_cost_, d_sys_, d_linv_;
-  DevBuf d_status_, d_cost_, d_cost_tmp_;
+  DevBuf d_cost_, d_cost_tmp_;
 };
 
 // ---- entry points used by api.hip -------------------------------------------------

@@ -28,6 +28,7 @@
 // LDS: full mode (the cfg3 window) keeps every column of both sides; ring mode (cfg4:
 // F = 98, a 225 KB profile) keeps w + 4 column slots per side and writes the factor
 // records to global memory.  Plus z (6F), the poses and the merge table.
+#include <atomic>
 #include "ba_band.h"
 
 #include <algorithm>
@@ -1046,10 +1047,17 @@ static size_t band_launch_lds(const BandLds& L, bool fused) {
   return fused ? std::max(L.bytes, (size_t)kBandRedItems * kRedScr * sizeof(double)) : L.bytes;
 }
 
+// The kernels' dynamic-LDS limit (process-wide), raised only when a window needs more than
+// any before it: a hipFuncSetAttribute costs host time on every keyframe otherwise.
 void band_set_attributes(const BandLds& L) {
+  static std::atomic<int> set{-1};
+  const int lds = (int)band_launch_lds(L, true);
+  int cur = set.load(std::memory_order_relaxed);
+  if (lds <= cur) return;
   const void* fs[2] = {(const void*)ba_band_kernel<true>, (const void*)ba_band_kernel<false>};
-  for (const void* f : fs)
-    VO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)band_launch_lds(L, true)));
+  for (const void* f : fs) VO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  while (cur < lds && !set.compare_exchange_weak(cur, lds, std::memory_order_relaxed)) {
+  }
 }
 
 void launch_band_solve(const BandArgs& A, const BandLds& L, hipStream_t st) {

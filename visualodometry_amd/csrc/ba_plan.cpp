@@ -1186,7 +1186,7 @@ std::vector<int32_t> local_profile_first(const BAPlan& P) {
   return first;
 }
 
-void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
+void build_profile(BAPlan& P, const std::vector<int32_t>& first, bool step_tables) {
   const int F = P.n_free;
   P.prof_first = first;
   filled(P.prof_off, F + 1, 0);
@@ -1234,7 +1234,12 @@ void build_profile(BAPlan& P, const std::vector<int32_t>& first) {
   if (P.prof_src.empty()) P.prof_src.push_back(0);
   if (P.camb_src.empty()) P.camb_src.push_back(0);
 
-  // K3 step tables
+  // K3 step tables (the profile solver's; the banded solver has its own)
+  if (!step_tables) {
+    P.solve_tab.assign(1, 0);
+    P.solve_layout = SolveTableLayout();
+    return;
+  }
   auto blk = [&](int i, int j) { return P.prof_off[i] + (j - first[i]); };
   std::vector<int32_t> sptr{0}, pi, pblk, iptr{0}, iblk, iq;
   int maxnb = 0;

@@ -305,8 +305,10 @@ std::string build_plan(BAPlan& plan, int n_poses, int n_points, int n_obs, int n
                        int seg_obs, const BAPlan* prev = nullptr, int seg_chunks = 1);
 // first[i] of each free block row touched by this plan (i if untouched).
 std::vector<int32_t> local_profile_first(const BAPlan& plan);
-// Builds the profile and the K2 reduction index from a (possibly all-reduced) first[].
-void build_profile(BAPlan& plan, const std::vector<int32_t>& first);
+// Builds the profile and the K2 reduction index from a (possibly all-reduced) first[];
+// step_tables: also the profile solver's K3 step tables (solve_tab; skipped when the banded
+// solver takes the window).
+void build_profile(BAPlan& plan, const std::vector<int32_t>& first, bool step_tables = true);
 // 64-bit FNV-1a over every plan array in a fixed order (vo_ba_plan_digest).
 uint64_t plan_digest(const BAPlan& plan);
 
