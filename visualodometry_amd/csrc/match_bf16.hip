@@ -369,7 +369,9 @@ __device__ __forceinline__ void merge2s(uint64_t& a1, uint64_t& a2, uint64_t b1,
 // (staged in LDS), keys (sqrtf(d2), j) go to LDS, and thread r merges row r's keys.  The
 // candidate set is complete (masks have no capacity); a block with more than kPool
 // candidates takes its rows one at a time through the same code.
-constexpr int kPool = 512;
+// 384 candidates: the kernel's LDS (40 KB) then admits four workgroups per CU, the limit its
+// 118 VGPRs set (at 512 it took 42 KB: three)
+constexpr int kPool = 384;
 constexpr int kQStr = 260;  // floats per staged query row
 #ifndef VO_CHAIN_SPAN
 #define VO_CHAIN_SPAN 128
@@ -526,7 +528,18 @@ __device__ __forceinline__ float chain_scalar(const float* x, const float* y, in
 // (2 MB at 2048 x 256) are fetched from the fabric once per XCD instead of by every XCD.
 // Under the float hint no exact sweep is launched: a call with non-finite values (fpack's
 // flag) is answered here by an exact scan of every train row instead (rare; see below).
-__global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int nR, int nitems) {
+// Waves that run candidate chains (each stages train rows in its own 4 KB of LDS) and the
+// workgroups per CU the kernel is compiled for (tuning builds: EXTRA=-DVO_RERANK_CW=n /
+// -DVO_RERANK_WGS=n)
+#ifndef VO_RERANK_CW
+#define VO_RERANK_CW 4
+#endif
+#ifndef VO_RERANK_WGS
+#define VO_RERANK_WGS 4
+#endif
+constexpr int kChainWaves = VO_RERANK_CW;
+static_assert(kChainWaves >= 1 && kChainWaves <= 4, "chain waves of a 256-thread workgroup");
+__global__ __launch_bounds__(256, VO_RERANK_WGS) void frerank_kernel(ShortArgs p, int v4, int nR, int nitems) {
   const bool exact_scan = p.forced && p.flag[1] == p.gen;  // uniform
   if (!exact_scan && !short_active(p)) return;
   const int per = (nitems + 7) / 8, L = blockIdx.x, item = (L & 7) * per + (L >> 3);
@@ -538,7 +551,7 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
   __shared__ int scol[kPool];
   __shared__ uint64_t skey[kPool];
   __shared__ int sscan[256];
-  __shared__ __attribute__((aligned(16))) float sbuf[4][64 * kRerankRowStr];  // per-wave row staging
+  __shared__ __attribute__((aligned(16))) float sbuf[kChainWaves][64 * kRerankRowStr];  // per-wave row staging
   const int row0 = 16 * R;
   if (v4) {  // the block's 16 query rows as float4s, every load in flight before the stores
     const int nv = p.dim / 4, nall = 16 * nv;  // dim <= 256: at most 4 per thread
@@ -575,12 +588,13 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
         const float d = chain_scalar(sq + r * kQStr, B_row(p, b, j), p.dim);
         if (d < __builtin_huge_valf()) merge2s(a1, a2, key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)j), ~0ull);
       }
-    static_assert(kPool >= 512, "the partial top-2s fit the key pool");
-    skey[tid] = a1;
-    skey[256 + tid] = a2;
+    uint64_t* pt = reinterpret_cast<uint64_t*>(&sbuf[0][0]);  // the row staging is idle here
+    static_assert(sizeof(sbuf) >= 512 * sizeof(uint64_t), "the partial top-2s fit the staging buffer");
+    pt[tid] = a1;
+    pt[256 + tid] = a2;
     __syncthreads();
     if (tid < 16)
-      for (int q = 0; q < 16; ++q) merge2s(k1, k2, skey[tid + 16 * q], skey[256 + tid + 16 * q]);
+      for (int q = 0; q < 16; ++q) merge2s(k1, k2, pt[tid + 16 * q], pt[256 + tid + 16 * q]);
   } else {
   // the block's 16 rows are M tile mt = R & 1 of wave row group R >> 1: in each of its
   // nch x 64 words, bits 8 u + 4 mt + r
@@ -638,7 +652,7 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
     if (v4) {
       // wave w takes candidates 64 (w + 4 q) + lane (the loop bound is wave-uniform)
       const int wv = tid >> 6;
-      for (int c0 = 64 * wv; c0 < total; c0 += 256) {
+      for (int c0 = 64 * wv; wv < kChainWaves && c0 < total; c0 += 64 * kChainWaves) {
         const float d = VO_RERANK_EXP == 1 ? 0.0f : chain_staged(B, sq, slist, scol, sbuf[wv], c0, total, p.dim);
         const int c = c0 + (tid & 63);
         if (c < total) skey[c] = key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)scol[c]);
@@ -658,13 +672,12 @@ __global__ __launch_bounds__(256) void frerank_kernel(ShortArgs p, int v4, int n
       uint64_t a1 = ~0ull, a2 = ~0ull;
       for (int c = part; c < total; c += 16)
         if (slist[c] == r) merge2s(a1, a2, skey[c], ~0ull);
-      __syncthreads();  // skey / scol are free now: partials in their place
-      skey[tid] = a1;
-      reinterpret_cast<uint64_t*>(slist)[tid] = a2;
+      uint64_t* pt = reinterpret_cast<uint64_t*>(&sbuf[0][0]);  // the row staging is idle now
+      pt[tid] = a1;
+      pt[256 + tid] = a2;
       __syncthreads();
       if (tid < 16)
-        for (int q = 0; q < 16; ++q)
-          merge2s(k1, k2, skey[tid + 16 * q], reinterpret_cast<const uint64_t*>(slist)[tid + 16 * q]);
+        for (int q = 0; q < 16; ++q) merge2s(k1, k2, pt[tid + 16 * q], pt[256 + tid + 16 * q]);
     }
   } else if (tid < 16) {  // rare: thread rl walks row rl's candidates itself
     const int g = tid >> 2, r = tid & 3;
