@@ -67,14 +67,16 @@ int host_threads() {
   return n;
 }
 
-// fn(t) for t = 0 .. n - 1 on n host threads (t = 0 on the caller).  Every use writes
-// disjoint, precomputed ranges, so the plan never depends on the thread count or timing.
-// Workers persist across plans (thread creation would cost more than a small phase); a
-// caller that finds the pool busy (another context planning) starts its own threads.
-// While a plan is being built (PlanSession, one build_plan call: about half a millisecond of
-// consecutive phases tens of microseconds apart), the workers and the caller poll for the next
-// phase / the phase's end instead of sleeping on the condition variables: a futex wake of
-// fifteen threads costs about as much as a phase.  Between plans they sleep (polling there
+// fn(t) for t = 0 .. n - 1, each exactly once, on the caller and the pool's workers.  The items
+// are claimed from a counter, so a phase ends when its items are done, not when every worker has
+// arrived: a worker that wakes late finds them taken (the first phase of a plan follows a futex
+// wake of every worker, and on a loaded host the slowest wake had set that phase's length).
+// Every use writes disjoint, precomputed ranges per item, so the plan never depends on the
+// thread count or timing.  Workers persist across plans (thread creation would cost more than a
+// small phase); a caller that finds the pool busy (another context planning) starts its own
+// threads.  While a plan is being built (PlanSession, one build_plan call: about half a
+// millisecond of consecutive phases tens of microseconds apart), the workers poll for the next
+// phase instead of sleeping on the condition variable; between plans they sleep (polling there
 // would eat the job's CPU quota).  Tuning build: -DVO_PLAN_SESSION_SPIN=0 never polls.
 #ifndef VO_PLAN_SESSION_SPIN
 #define VO_PLAN_SESSION_SPIN 1
@@ -94,9 +96,9 @@ class PlanPool {
     static PlanPool pool;
     return pool;
   }
-  // Exceptions (bad_alloc in a phase) never escape a thread: each call of fn is caught,
-  // the first exception is kept, every thread finishes the phase, then the caller rethrows
-  // it (guarded() maps it to an error code).
+  // Exceptions (bad_alloc in a phase) never escape a thread: each item is caught, the first
+  // exception is kept, every item still runs, then the caller rethrows it (guarded() maps it to
+  // an error code).
   template <class Fn>
   void run(int n, Fn&& fn) {
     std::exception_ptr first;
@@ -111,7 +113,7 @@ class PlanPool {
     };
     // a forked child inherits the pool object but not its threads: it plans on its own
     std::unique_lock<std::mutex> busy(use_, std::defer_lock);
-    if (getpid() != owner_ || !busy.try_lock() || n - 1 > (int)workers_.size()) {
+    if (getpid() != owner_ || !busy.try_lock()) {
       std::vector<std::thread> pool;
       try {
         for (int t = 1; t < n; ++t) pool.emplace_back([&safe, t] { safe(t); });
@@ -124,21 +126,24 @@ class PlanPool {
       return;
     }
     std::function<void(int)> job = [&safe](int t) { safe(t); };
+    // publish: the job's fields are written while the pool is retired (a worker that enters now
+    // backs off without reading them), then opened with a new generation
+    job_ = &job;
+    n_items_ = n;
+    next_.store(0, std::memory_order_relaxed);
+    ndone_.store(0, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> lk(mu_);
-      job_ = &job;
-      active_ = n - 1;
-      pending_ = n - 1;
-      ++gen_;
+      retired_.store(false, std::memory_order_seq_cst);
+      gen_.fetch_add(1, std::memory_order_seq_cst);
     }
-    cv_.notify_all();
-    safe(0);
-    while (session_.load(std::memory_order_acquire) > 0 && pending_.load(std::memory_order_acquire) != 0) cpu_relax();
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      done_.wait(lk, [&] { return pending_ == 0; });
-      job_ = nullptr;
-    }
+    cv_.notify_all();  // (cheap when every worker is polling: no waiter to wake)
+    work();
+    while (ndone_.load(std::memory_order_acquire) < n) cpu_relax();
+    // retire: workers inside the job finish their (claimed-nothing) loop; later ones back off
+    retired_.store(true, std::memory_order_seq_cst);
+    while (entered_.load(std::memory_order_seq_cst) != 0) cpu_relax();
+    job_ = nullptr;
     if (first) std::rethrow_exception(first);
   }
   // a plan is being built: workers poll between its phases (see kPlanSessionSpin).  (Waking
@@ -161,33 +166,41 @@ class PlanPool {
 
  private:
   PlanPool() : owner_(getpid()) {
-    for (int t = 1; t < host_threads(); ++t) workers_.emplace_back([this, t] { loop(t); });
+    for (int t = 1; t < host_threads(); ++t) workers_.emplace_back([this] { loop(); });
   }
-  void loop(int t) {
+  // items of the current job until none is left (the caller, and workers that entered it)
+  void work() {
+    for (;;) {
+      const int t = next_.fetch_add(1, std::memory_order_relaxed);
+      if (t >= n_items_) return;
+      (*job_)(t);
+      ndone_.fetch_add(1, std::memory_order_release);
+    }
+  }
+  void loop() {
     long seen = 0;
     for (;;) {
-      std::function<void(int)>* job;
       while (session_.load(std::memory_order_acquire) > 0 && gen_.load(std::memory_order_acquire) == seen) cpu_relax();
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        cv_.wait(lk, [&] { return stop_ || gen_.load(std::memory_order_relaxed) != seen; });
         if (stop_) return;
-        seen = gen_;
-        if (t > active_) continue;  // not needed this round
-        job = job_;
+        seen = gen_.load(std::memory_order_relaxed);
       }
-      (*job)(t);
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--pending_ == 0) done_.notify_one();
+      entered_.fetch_add(1, std::memory_order_seq_cst);
+      if (!retired_.load(std::memory_order_seq_cst)) work();
+      entered_.fetch_sub(1, std::memory_order_seq_cst);
     }
   }
   pid_t owner_;
   std::vector<std::thread> workers_;
   std::mutex use_, mu_;
-  std::condition_variable cv_, done_;
+  std::condition_variable cv_;
+  // the current job: written only while retired_ is true and no worker is inside it
   std::function<void(int)>* job_ = nullptr;
-  int active_ = 0;
-  std::atomic<int> pending_{0};  // written under mu_; atomic for the polling
+  int n_items_ = 0;
+  std::atomic<int> next_{0}, ndone_{0}, entered_{0};
+  std::atomic<bool> retired_{true};
   std::atomic<long> gen_{0};
   std::atomic<int> session_{0};  // plans being built (begin_session / end_session)
   bool stop_ = false;
