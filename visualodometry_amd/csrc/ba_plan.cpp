@@ -391,6 +391,16 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   if (!P.scratch) P.scratch = std::make_shared<PlanScratch>();
   PlanScratch& X = *P.scratch;
 
+#ifdef VO_PLAN_TIMING  // diagnostic builds: the order pass's own steps
+  auto sub_t0 = std::chrono::steady_clock::now();
+  auto sub = [&](const char* name) {
+    const auto n = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "    %-12s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(n - sub_t0).count());
+    sub_t0 = n;
+  };
+#else
+  auto sub = [](const char*) {};
+#endif
   PlanArr<int32_t>& sorted = P.scr_sorted;
   sized(sorted, std::max(M, 1));
   // Landmarks ordered by first camera (stable counting sort; no observation: last), which
@@ -444,6 +454,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
         ht[f] += nte;
       }
     });
+    sub("pass 1");
     for (int t = 0; t < nt; ++t)  // the lowest violation, as a serial scan would find it
       if (bad_ptr[t] >= 0) return fmt("point_ptr not monotone at %ld", bad_ptr[t]);
     for (int t = 0; t < nt; ++t)
@@ -514,6 +525,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
       }
     });
   }
+  sub("pass 2");
   P.pt_te[L] = P.n_te;
   P.te_obs[P.n_te] = M;
   PLAN_T(1, "order + track entries");
