@@ -320,10 +320,13 @@ struct PlanScratch {
   std::vector<int32_t> first, tecnt, hist, seg_of, pair_base, cl_base, col_base, ch_pairs, ch_fte, ch_fobs;
 };
 
+// One-wave K1: weighted chain below which a slot's pairs stay on one lane (copies split longer
+// ones).  15 with three-chunk segments (same-box A/B, profiles/r05_ab/copy_chain*.txt: K1 cfg3
+// 24.69 -> 24.51 us, cfg4 158.5 -> 155.8 us against 21; 9, 12 and 30 slower).
 #ifndef VO_BA_COPY_CHAIN
-#define VO_BA_COPY_CHAIN 21
+#define VO_BA_COPY_CHAIN 15
 #endif
-constexpr int kCopyChain = VO_BA_COPY_CHAIN;  // one-wave K1: weighted chain below which no copy is made
+constexpr int kCopyChain = VO_BA_COPY_CHAIN;
 
 int seg_obs_for(int64_t n_obs, int target_segments) {
   const int64_t t = std::max(1, target_segments);
