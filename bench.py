@@ -523,7 +523,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=100)  # ~7 ms at cfg3: the clocks settle before the timed region
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--lam", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
