@@ -197,8 +197,10 @@ int vo_ba_debug_stamps(vo_ctx* ctx, uint64_t* out, int n);
  *      and downsample launches of one call), 12 sift_extrema (all octaves),
  *      13 sift_orient, 14 sift_select (sort keys, segmented sort, duplicate removal,
  *      retainBest, compaction), 15 sift_desc, 16 match_rerank (the float path's exact
- *      re-rank; before it had an id of its own it was timed under match_merge). */
-#define VO_PROFILE_KERNELS 17
+ *      re-rank; before it had an id of its own it was timed under match_merge),
+ *      17 pnp_decide, 18 pnp_hyp_tail, 19 pnp_score_tail (large batches: the replay after
+ *      the first hypotheses of every frame, then the rest for the frames still looping). */
+#define VO_PROFILE_KERNELS 20
 int vo_profile_enable(vo_ctx* ctx, int on);
 int vo_profile_read(vo_ctx* ctx, double* ms_out, int64_t* counts_out);
 

@@ -45,6 +45,17 @@ int vo_ba_testing_k1(vo_ctx* ctx, int variant);
 int vo_ba_testing_plan_slide(const vo_ba_problem* prev, const vo_ba_problem* cur, int seg_obs, int seg_chunks,
                              uint64_t* digest, int64_t* reused_chunks);
 
+/* Test/tool switch for this context's PnP calls (vo_pnp_ransac*): h1 > 0 solves and scores
+ * the first h1 hypotheses of every frame, replays the serial RANSAC loop over them and solves
+ * the rest only for the frames whose loop goes on; h1 = 0 (default) does that for batches of
+ * more hypotheses than one wave per SIMD holds, h1 sized to that; h1 = -1 solves all at once.
+ * Results are identical in every mode. */
+int vo_pnp_testing_split(vo_ctx* ctx, int h1);
+
+/* Synchronises the context stream and reports the last PnP call: *h1 hypotheses solved for
+ * every frame, *tail_frames frames whose hypotheses [h1, iterations) were solved too. */
+int vo_pnp_testing_last_split(vo_ctx* ctx, int* h1, int* tail_frames);
+
 #ifdef __cplusplus
 }
 #endif

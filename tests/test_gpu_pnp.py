@@ -103,3 +103,76 @@ def test_large_frame_properties(ctx):
     assert ok and not (mask & out).any() and mask.sum() > 0.8 * (~out).sum()
     R = P.rodrigues_to_mat(rv[None])[0]
     assert np.abs(R - T[:3, :3]).max() < 1e-3 and np.abs(tv - T[:3, 3]).max() < 0.02
+
+
+def _run_batch(ctx, Xs, Us, K, thr=2.0):
+    sizes = [len(x) for x in Xs]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    dX = _lib.DeviceArray.from_numpy(ctx, np.concatenate(Xs).reshape(-1, 3))
+    dU = _lib.DeviceArray.from_numpy(ctx, np.concatenate(Us).reshape(-1, 2))
+    dP = _lib.DeviceArray(ctx, (len(sizes), 6), np.float64)
+    dM = _lib.DeviceArray(ctx, (max(int(off[-1]), 1),), np.uint8)
+    dS = _lib.DeviceArray(ctx, (len(sizes), 2), np.int32)
+    pnp.pnp_ransac_device(dX, dU, off, K, thr, dP, dM, dS, ctx=ctx)
+    return off, dP.numpy(), dM.numpy()[: off[-1]].astype(bool), dS.numpy()
+
+
+def _split_cases(count, n_max, seed0):
+    """Frames of mixed sizes and outlier fractions: some stop the serial loop within a few
+    hypotheses, some run all 100 (60 % outliers, pure noise)."""
+    rng = np.random.default_rng(seed0)
+    fracs = [0.0, 0.1, 0.25, 0.45, 0.6]
+    Xs, Us = [], []
+    for i in range(count):
+        n = [0, 5, 6][i] if i < 3 else int(rng.integers(8, n_max))
+        X, uv, K, _, _ = pnp_case(max(n, 1), seed0 + i, noise_px=0.3, outlier_frac=fracs[i % 5] if n > 20 else 0.0)
+        if i == 3:  # pure noise: no model has more than 4 inliers
+            uv = rng.uniform(0, 1000, uv.shape).astype(np.float32)
+        Xs.append(X[:n])
+        Us.append(uv[:n])
+    return Xs, Us, K
+
+
+@pytest.mark.parametrize("h1", [1, 5, 16, 40])
+def test_split_replay_matches_all_at_once(ctx, h1):
+    """pnp_run's split (the first h1 hypotheses of every frame, the RANSAC replay, the rest
+    only for the frames whose serial loop goes on): the same bits as solving all hypotheses
+    at once, and the oracle's masks and poses."""
+    Xs, Us, K = _split_cases(24, 700, 300)
+    try:
+        _lib.pnp_testing_split(ctx, -1)
+        off, pose0, mask0, st0 = _run_batch(ctx, Xs, Us, K)
+        assert _lib.pnp_testing_last_split(ctx) == (100, 0)
+        _lib.pnp_testing_split(ctx, h1)
+        off, pose1, mask1, st1 = _run_batch(ctx, Xs, Us, K)
+        got_h1, tail = _lib.pnp_testing_last_split(ctx)
+    finally:
+        _lib.pnp_testing_split(ctx, 0)
+    assert got_h1 == h1 and 0 < tail < len(Xs) - 3
+    np.testing.assert_array_equal(pose1, pose0)
+    np.testing.assert_array_equal(mask1, mask0)
+    np.testing.assert_array_equal(st1, st0)
+    for f in range(len(Xs)) if h1 == 16 else range(0, len(Xs), 4):
+        ref = P.solve_pnp_ransac(Xs[f], Us[f], K, 2.0)
+        _check((bool(st1[f, 0]), pose1[f, :3], pose1[f, 3:], mask1[off[f]:off[f + 1]]), ref)
+
+
+def test_split_auto_large_batch(ctx):
+    """A batch of more hypotheses than one wave per SIMD holds splits by itself; the results
+    are the bits of the all-at-once run."""
+    Xs, Us, K = _split_cases(1100, 120, 900)
+    try:
+        _lib.pnp_testing_split(ctx, -1)
+        _, pose0, mask0, st0 = _run_batch(ctx, Xs, Us, K)
+        _lib.pnp_testing_split(ctx, 0)
+        off, pose1, mask1, st1 = _run_batch(ctx, Xs, Us, K)
+        h1, tail = _lib.pnp_testing_last_split(ctx)
+    finally:
+        _lib.pnp_testing_split(ctx, 0)
+    assert 16 <= h1 < 100 and tail > 0
+    np.testing.assert_array_equal(pose1, pose0)
+    np.testing.assert_array_equal(mask1, mask0)
+    np.testing.assert_array_equal(st1, st0)
+    for f in range(0, 40, 3):
+        ref = P.solve_pnp_ransac(Xs[f], Us[f], K, 2.0)
+        _check((bool(st1[f, 0]), pose1[f, :3], pose1[f, 3:], mask1[off[f]:off[f + 1]]), ref)

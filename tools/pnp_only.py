@@ -9,6 +9,9 @@ import bench  # noqa: E402
 from visualodometry_amd import _lib  # noqa: E402
 
 ctx = _lib.context(0)
+if len(sys.argv) > 1:  # h1 for vo_pnp_testing_split (0 auto, -1 all hypotheses at once)
+    _lib.pnp_testing_split(ctx, int(sys.argv[1]))
 r = bench.bench_pnp(ctx)
 r.pop("cpu_baseline", None)
-print(json.dumps({"value": r["value"], "kernel_us": r["kernel_us"]}))
+print(json.dumps({"value": r["value"], "kernel_us": r["kernel_us"], "split": r.get("split"),
+                  "roofline_frac": r["roofline"]["frac"]}))

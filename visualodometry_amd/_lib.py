@@ -107,6 +107,8 @@ SIGNATURES = {
     "vo_ba_split_reduce": (_I, [_P, _I]),
     "vo_ba_testing_drop_reducers": (_I, [_P, _I]),
     "vo_ba_testing_k1": (_I, [_P, _I]),
+    "vo_pnp_testing_split": (_I, [_P, _I]),
+    "vo_pnp_testing_last_split": (_I, [_P, _PI32, _PI32]),
     "vo_ba_testing_plan_slide": (_I, [C.c_void_p, C.c_void_p, _I, _I, C.POINTER(C.c_uint64), _PI64]),
 }
 
@@ -229,7 +231,8 @@ class DeviceArray:
 
 KERNEL_NAMES = ["ba_lin", "ba_reduce", "ba_solve", "match_pack", "match_i8", "match_f32",
                 "match_merge", "triangulate", "pnp_hyp", "pnp_score", "pnp_final", "sift_pyramid",
-                "sift_extrema", "sift_orient", "sift_select", "sift_desc", "match_rerank"]
+                "sift_extrema", "sift_orient", "sift_select", "sift_desc", "match_rerank", "pnp_decide",
+                "pnp_hyp_tail", "pnp_score_tail"]
 
 
 def profile_enable(ctx: "Context", on: bool = True) -> None:
@@ -280,6 +283,19 @@ def ba_testing_k1(ctx: "Context", variant: int = 0) -> None:
     """Test switch: the K1 variant of the context's later setups (0 default, -1 four-wave K1,
     n = 1..3 one-wave K1 with n chunks per segment); see vo_ba_testing_k1."""
     check(ctx.lib.vo_ba_testing_k1(ctx.handle, int(variant)), "vo_ba_testing_k1")
+
+
+def pnp_testing_split(ctx: "Context", h1: int = 0) -> None:
+    """Test/tool switch: PnP calls of the context solve the first ``h1`` hypotheses of every
+    frame before replaying the RANSAC loop (0 auto, -1 all at once); see vo_pnp_testing_split."""
+    check(ctx.lib.vo_pnp_testing_split(ctx.handle, int(h1)), "vo_pnp_testing_split")
+
+
+def pnp_testing_last_split(ctx: "Context") -> tuple:
+    """(h1, tail_frames) of the context's last PnP call; see vo_pnp_testing_last_split."""
+    h1, tail = C.c_int32(0), C.c_int32(0)
+    check(ctx.lib.vo_pnp_testing_last_split(ctx.handle, C.byref(h1), C.byref(tail)), "vo_pnp_testing_last_split")
+    return h1.value, tail.value
 
 
 def ptr(a, ctype):

@@ -758,6 +758,30 @@ int vo_ba_testing_k1(vo_ctx* ctx, int variant) {
   });
 }
 
+int vo_pnp_testing_split(vo_ctx* ctx, int h1) {
+  return guarded([&] {
+    VO_REQUIRE(ctx != nullptr, VO_ERR_ARG, "vo_pnp_testing_split: null context");
+    VO_REQUIRE(h1 >= -1, VO_ERR_ARG, "vo_pnp_testing_split: h1 %d < -1", h1);
+    ctx->pnp_split = h1;
+  });
+}
+
+int vo_pnp_testing_last_split(vo_ctx* ctx, int* h1, int* tail_frames) {
+  return guarded([&] {
+    VO_REQUIRE(ctx != nullptr && h1 && tail_frames, VO_ERR_ARG, "vo_pnp_testing_last_split: bad arguments");
+    vo::bind(ctx);
+    vo::PnpWorkspace& ws = ctx->pnp;
+    const int batch = (int)ws.offsets.size() - 1;
+    *h1 = ws.last_h1;
+    *tail_frames = 0;
+    if (batch <= 0 || ws.last_h1 >= ws.H) return;
+    std::vector<int32_t> need(batch);
+    VO_HIP_CHECK(hipMemcpyAsync(need.data(), ws.need.ptr, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, ctx->stream));
+    VO_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    for (int v : need) *tail_frames += v != 0;
+  });
+}
+
 int vo_comm_init_loopback(vo_ctx* ctx, int nranks, int rank, const char id[128]) {
   return guarded([&] {
     vo::bind(ctx);

@@ -39,6 +39,7 @@ using namespace pnpm;
 // ---------------------------------------------------------------- kernels
 constexpr int kScoreGroupMax = 128;  // hypotheses scored by one workgroup, at most
 constexpr int kScoreRegPts = 4;      // points per thread held in registers (frames up to 1024 points)
+constexpr int kSplitMin = 16;        // hypotheses solved for every frame before the replay decides (pnp_run)
 
 struct PnpArgs {
   const float* X;          // (total, 3) object points, frames back to back
@@ -62,10 +63,14 @@ __device__ __forceinline__ void load3(const float* X, int i, float (&M)[3]) {
   M[2] = X[3l * i + 2];
 }
 
-__global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a) {
-  const int g = blockIdx.x * 64 + threadIdx.x;
-  if (g >= a.batch * a.H) return;
-  const int f = g / a.H, h = g - f * a.H;
+// Hypotheses [h_lo, h_hi) of every frame (of the frames with need[f] != 0 when need is given).
+__global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a, int h_lo, int h_hi, const int32_t* need) {
+  const int hr = h_hi - h_lo;
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= a.batch * hr) return;
+  const int f = k / hr, h = h_lo + (k - f * hr);
+  if (need && !need[f]) return;
+  const int g = f * a.H + h;
   const int o = a.off[f], n = a.off[f + 1] - o;
   double* model = a.models + (size_t)g * kModel;
   const bool run = n > kPts || (n == kPts && h == 0);
@@ -100,11 +105,13 @@ __global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a) {
   model[15] = ok ? 1.0 : 0.0;
 }
 
-__global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group) {
-  // one workgroup per (frame, group of `group` hypotheses): the frame's points stay in L1
-  // across its hypotheses; the host sizes groups so the grid still fills the chip
-  const int ngroups = (a.H + group - 1) / group;
-  const int f = blockIdx.x / ngroups, h0 = (blockIdx.x % ngroups) * group, h1 = min(h0 + group, a.H);
+__global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, int h_lo, int h_hi,
+                                                        const int32_t* need) {
+  // one workgroup per (frame, group of `group` hypotheses of [h_lo, h_hi)): the frame's points
+  // stay in L1 across its hypotheses; the host sizes groups so the grid still fills the chip
+  const int ngroups = (h_hi - h_lo + group - 1) / group;
+  const int f = blockIdx.x / ngroups, h0 = h_lo + (blockIdx.x % ngroups) * group, h1 = min(h0 + group, h_hi);
+  if (need && !need[f]) return;  // uniform per workgroup, before any barrier
   const int o = a.off[f], n = a.off[f + 1] - o;
   __shared__ int s_count[kScoreGroupMax];
   for (int h = threadIdx.x; h < h1 - h0; h += 256) s_count[h] = 0;
@@ -180,6 +187,62 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group) {
   for (int h = threadIdx.x; h < h1 - h0; h += 256) a.counts[(size_t)f * a.H + h0 + h] = s_count[h];
 }
 
+// The serial loop of RANSACPointSetRegistrator::run (OpenCV calib3d/src/ptsetreg.cpp) over the
+// inlier counts of hypotheses [0, h_end) of frame f (n > kPts points).  A hypothesis without a
+// model (EPnP failed) has count 0, which never beats max(max_good, kPts - 1): the loop's skip.
+// The whole workgroup (kThreads threads, every one calling) stages each chunk of counts in LDS
+// with independent loads; thread 0 runs the loop.  On return every thread reads s_state: the
+// iteration reached, the loop's bound niters when it stopped (> h_end: the serial loop would go
+// on to hypothesis h_end), the best hypothesis (-1: none) and its count.
+template <int kThreads>
+__device__ void ransac_replay(const PnpArgs& a, int f, int n, int h_end, int* s_cnt, int* s_state) {
+  if (threadIdx.x == 0) {
+    s_state[0] = 0;
+    s_state[1] = a.H;
+    s_state[2] = -1;
+    s_state[3] = 0;
+  }
+  const int32_t* counts = a.counts + (size_t)f * a.H;
+  for (int base = 0; base < h_end; base += kThreads) {
+    __syncthreads();  // s_state written, the previous chunk consumed
+    const int stop = min(min(s_state[1], h_end), base + kThreads);  // niters only shrinks
+    if (base >= stop) break;  // uniform: every thread read the same s_state
+    if (base + (int)threadIdx.x < stop) s_cnt[threadIdx.x] = counts[base + threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int it = s_state[0], niters = s_state[1], best = s_state[2], max_good = s_state[3];
+      for (; it < niters && it < stop; ++it) {
+        const int good = s_cnt[it - base];
+        if (good > (max_good > kPts - 1 ? max_good : kPts - 1)) {
+          best = it;
+          max_good = good;
+          niters = update_num_iters(a.confidence, (double)(n - good) / n, kPts, niters);
+        }
+      }
+      s_state[0] = it;
+      s_state[1] = niters;
+      s_state[2] = best;
+      s_state[3] = max_good;
+    }
+  }
+  __syncthreads();
+}
+
+// After the first h_end hypotheses of every frame are scored: need[f] = 1 where the serial
+// loop has not stopped yet, i.e. the frames whose hypotheses [h_end, H) are solved next.
+// One wave per frame.
+__global__ __launch_bounds__(64) void pnp_decide_kernel(PnpArgs a, int h_end, int32_t* need) {
+  __shared__ int s_cnt[64], s_state[4];
+  const int f = blockIdx.x;
+  const int n = a.off[f + 1] - a.off[f];
+  if (n <= kPts) {
+    if (threadIdx.x == 0) need[f] = 0;
+    return;
+  }
+  ransac_replay<64>(a, f, n, h_end, s_cnt, s_state);
+  if (threadIdx.x == 0) need[f] = s_state[1] > h_end ? 1 : 0;
+}
+
 // Sum of one double over a wave in a fixed order (butterfly).
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -187,12 +250,22 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// Normal equations of the inliers at (R, t): this thread's partial sums (points i = tid mod 256).
+// pnp_final: threads per frame.  At two waves per SIMD (<= 256 VGPRs) a CU holds 8 / kFinalWaves
+// frames: with 128 threads a batch of 1024 frames is one round on 256 CUs (256 threads: two).
+#ifndef VO_PNP_FINAL_THREADS
+#define VO_PNP_FINAL_THREADS 128
+#endif
+constexpr int kFinalThreads = VO_PNP_FINAL_THREADS;
+constexpr int kFinalWaves = kFinalThreads / 64;
+static_assert(kFinalThreads % 64 == 0 && kFinalThreads <= 256, "pnp_final: 1..4 waves");
+
+// Normal equations of the inliers at (R, t): this thread's partial sums (points i = tid mod
+// kFinalThreads).
 __device__ __forceinline__ void lm_accumulate(const PnpArgs& a, int o, int n, const double* R, const double* t,
                                               double (&acc)[kNe]) {
 #pragma unroll
   for (int k = 0; k < kNe; ++k) acc[k] = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) {
+  for (int i = threadIdx.x; i < n; i += kFinalThreads) {
     if (!a.mask[o + i]) continue;
     float M[3];
     load3(a.X, o + i, M);
@@ -211,44 +284,30 @@ __device__ __forceinline__ void lm_reduce(double (&acc)[kNe], double* red, doubl
   __syncthreads();
   if (threadIdx.x < kNe) {
     const int k = threadIdx.x;
-    out[k] = ((red[k] + red[kNe + k]) + red[2 * kNe + k]) + red[3 * kNe + k];
+    double v = red[k];
+#pragma unroll
+    for (int w = 1; w < kFinalWaves; ++w) v = v + red[w * kNe + k];
+    out[k] = v;
   }
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256, 2) void pnp_final_kernel(PnpArgs a) {  // two per CU: <= 256 VGPRs
+__global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) {  // 2 waves per SIMD
   const int f = blockIdx.x;
   const int o = a.off[f], n = a.off[f + 1] - o;
-  __shared__ int s_best, s_count, s_go;
+  __shared__ int s_count, s_go;
+  __shared__ int s_cnt[kFinalThreads], s_state[4];
   __shared__ double s_R[9], s_t[3];
-  __shared__ double s_red[4 * kNe];
+  __shared__ double s_red[kFinalWaves * kNe];
   __shared__ double s_ne[kNe];
-  if (threadIdx.x == 0) {
-    // the serial RANSAC loop of RANSACPointSetRegistrator::run over the precomputed counts
-    int best = -1;
-    if (n == kPts) {
-      best = a.models[(size_t)f * a.H * kModel + 15] != 0.0 ? 0 : -1;
-    } else if (n > kPts) {
-      int niters = a.H, max_good = 0;
-      for (int it = 0; it < niters; ++it) {
-        const size_t g = (size_t)f * a.H + it;
-        if (a.models[g * kModel + 15] == 0.0) continue;
-        const int good = a.counts[g];
-        if (good > (max_good > kPts - 1 ? max_good : kPts - 1)) {
-          best = it;
-          max_good = good;
-          niters = update_num_iters(a.confidence, (double)(n - good) / n, kPts, niters);
-        }
-      }
-    }
-    s_best = best;
-    s_count = 0;
-  }
+  // the serial RANSAC loop over the precomputed counts (uniform branch: n is per frame)
+  if (n > kPts) ransac_replay<kFinalThreads>(a, f, n, a.H, s_cnt, s_state);
+  if (threadIdx.x == 0) s_count = 0;
+  const int best = n > kPts ? s_state[2] : n == kPts && a.models[(size_t)f * a.H * kModel + 15] != 0.0 ? 0 : -1;
   __syncthreads();
-  const int best = s_best;
   const double* model = a.models + ((size_t)f * a.H + (best < 0 ? 0 : best)) * kModel;
   if (best < 0 || n == kPts) {
-    for (int i = threadIdx.x; i < n; i += 256) a.mask[o + i] = best < 0 ? 0 : 1;
+    for (int i = threadIdx.x; i < n; i += kFinalThreads) a.mask[o + i] = best < 0 ? 0 : 1;
     if (threadIdx.x == 0) {
       for (int k = 0; k < 3; ++k) {
         a.pose[6 * f + k] = best < 0 ? 0.0 : model[12 + k];
@@ -265,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void pnp_final_kernel(PnpArgs a) {  // two 
 #pragma unroll
   for (int k = 0; k < 3; ++k) t[k] = model[9 + k];
   int cnt = 0;
-  for (int i = threadIdx.x; i < n; i += 256) {
+  for (int i = threadIdx.x; i < n; i += kFinalThreads) {
     const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
     float M[3];
     load3(a.X, o + i, M);
@@ -391,21 +450,49 @@ void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* of
   a.confidence = confidence;
   a.batch = batch;
   a.H = H;
-  const int nh = batch * H;
-  ctx->prof.begin(ctx->stream, kKPnpHyp);
-  hipLaunchKernelGGL(pnp_hyp_kernel, dim3(ceil_div(nh, 64)), dim3(64), 0, ctx->stream, a);
-  ctx->prof.end(ctx->stream);
-  VO_HIP_CHECK(hipGetLastError());
-  ctx->prof.begin(ctx->stream, kKPnpScore);
-  // hypotheses per scoring workgroup: one for small batches (single-frame latency), up to
-  // kScoreGroupMax while the grid keeps ~4 workgroups per CU
-  const int group = std::max(1, std::min({H, kScoreGroupMax, nh / std::max(1, 4 * ctx->num_cus)}));
-  const int ngroups = ceil_div(H, group);
-  hipLaunchKernelGGL(pnp_score_kernel, dim3(batch * ngroups), dim3(256), 0, ctx->stream, a, group);
-  ctx->prof.end(ctx->stream);
-  VO_HIP_CHECK(hipGetLastError());
+  // The serial loop stops after niters <= H hypotheses (niters shrinks as better models turn
+  // up: about 17 at 25 % outliers and confidence 0.99), and one pnp_hyp thread is a long
+  // dependent chain (one wave per SIMD, 512 VGPRs): a launch of more waves than SIMDs takes
+  // twice as long.  So large batches solve the first h1 hypotheses of every frame (h1 sized
+  // to one wave per SIMD), replay the loop over them (pnp_decide), and solve and score
+  // hypotheses [h1, H) only for the frames whose loop has not stopped by h1.  pnp_final's
+  // replay reads no count past where the loop stops, so the result is the same as solving all
+  // H.  ctx->pnp_split (vo_pnp_testing_split): > 0 forces h1, -1 solves all H at once.
+  const long fill = 4l * ctx->num_cus * 64;
+  int h1 = H;
+  if (ctx->pnp_split > 0)
+    h1 = std::min(H, ctx->pnp_split);
+  else if (ctx->pnp_split == 0 && (long)batch * H > fill)
+    h1 = std::min(H, std::max(kSplitMin, (int)(fill / batch)));
+  ws.last_h1 = h1;
+  auto solve_and_score = [&](int h_lo, int h_hi, const int32_t* need, int kid_hyp, int kid_score) {
+    const int hr = h_hi - h_lo, nh = batch * hr;
+    ctx->prof.begin(ctx->stream, kid_hyp);
+    hipLaunchKernelGGL(pnp_hyp_kernel, dim3(ceil_div(nh, 64)), dim3(64), 0, ctx->stream, a, h_lo, h_hi, need);
+    ctx->prof.end(ctx->stream);
+    VO_HIP_CHECK(hipGetLastError());
+    ctx->prof.begin(ctx->stream, kid_score);
+    // hypotheses per scoring workgroup: one for small batches (single-frame latency), up to
+    // kScoreGroupMax while the grid keeps ~4 workgroups per CU
+    const int group = std::max(1, std::min({hr, kScoreGroupMax, nh / std::max(1, 4 * ctx->num_cus)}));
+    const int ngroups = ceil_div(hr, group);
+    hipLaunchKernelGGL(pnp_score_kernel, dim3(batch * ngroups), dim3(256), 0, ctx->stream, a, group, h_lo, h_hi,
+                       need);
+    ctx->prof.end(ctx->stream);
+    VO_HIP_CHECK(hipGetLastError());
+  };
+  solve_and_score(0, h1, nullptr, kKPnpHyp, kKPnpScore);
+  if (h1 < H) {
+    ws.need.reserve((size_t)batch * sizeof(int32_t));
+    int32_t* need = ws.need.as<int32_t>();
+    ctx->prof.begin(ctx->stream, kKPnpDecide);
+    hipLaunchKernelGGL(pnp_decide_kernel, dim3(batch), dim3(64), 0, ctx->stream, a, h1, need);
+    ctx->prof.end(ctx->stream);
+    VO_HIP_CHECK(hipGetLastError());
+    solve_and_score(h1, H, need, kKPnpHypTail, kKPnpScoreTail);
+  }
   ctx->prof.begin(ctx->stream, kKPnpFinal);
-  hipLaunchKernelGGL(pnp_final_kernel, dim3(batch), dim3(256), 0, ctx->stream, a);
+  hipLaunchKernelGGL(pnp_final_kernel, dim3(batch), dim3(kFinalThreads), 0, ctx->stream, a);
   ctx->prof.end(ctx->stream);
   VO_HIP_CHECK(hipGetLastError());
 }

@@ -62,15 +62,16 @@ VO_HD void jacobi_rows(double (&A)[N][M], double (&W)[N], double (&Vt)[N][N]) {
           p = p * 2.0;
           // hypot(p, beta) from correctly rounded ops only, as the oracle: bitwise reproducible
           const double beta = a - b, gamma = sqrt(p * p + beta * beta);
-          double c, s;
-          if (beta < 0) {
-            const double delta = (gamma - beta) * 0.5;
-            s = sqrt(delta / gamma);
-            c = p / (gamma * s * 2.0);
-          } else {
-            c = sqrt((gamma + beta) / (gamma * 2.0));
-            s = p / (gamma * c * 2.0);
-          }
+          // the reference's two branches as one (same operations on the same operands), so a
+          // wave whose lanes disagree on the sign of beta runs one division chain, not both:
+          //   beta < 0: delta = (gamma - beta) * 0.5, s = sqrt(delta / gamma), c = p / (gamma * s * 2)
+          //   else:     c = sqrt((gamma + beta) / (gamma * 2)),                s = p / (gamma * c * 2)
+          const bool neg = beta < 0;
+          const double num = neg ? (gamma - beta) * 0.5 : gamma + beta;
+          const double den = neg ? gamma : gamma * 2.0;
+          const double x = sqrt(num / den);
+          const double y = p / (gamma * x * 2.0);
+          const double c = neg ? y : x, s = neg ? x : y;
           double na = 0.0, nb = 0.0;
 #pragma unroll
           for (int k = 0; k < M; ++k) {

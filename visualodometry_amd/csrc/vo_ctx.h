@@ -35,9 +35,11 @@ struct PnpWorkspace {
   DevBuf off;     // int32 (batch + 1) frame offsets
   DevBuf models;  // double (batch, H, 16)
   DevBuf counts;  // int32 (batch, H)
+  DevBuf need;    // int32 (batch): frames whose hypotheses past the first h1 are solved
   DevBuf stage;   // host-call staging: points, outputs
   std::vector<int32_t> offsets;  // layout the cached subsets were made for
   int H = 0;
+  int last_h1 = 0;  // hypotheses solved for every frame by the last call (pnp_run)
 };
 
 // SIFT detection workspace (sift.hip): Gaussian and DoG pyramids of a batch.
@@ -62,7 +64,7 @@ struct Comm;      // ba.hip (RCCL communicator)
 enum KernelId {
   kKBaLin = 0, kKBaReduce, kKBaSolve, kKMatchPack, kKMatchI8, kKMatchF32, kKMatchMerge,
   kKTriangulate, kKPnpHyp, kKPnpScore, kKPnpFinal, kKSiftPyramid, kKSiftExtrema, kKSiftOrient, kKSiftSelect,
-  kKSiftDesc, kKMatchRerank, kKCount
+  kKSiftDesc, kKMatchRerank, kKPnpDecide, kKPnpHypTail, kKPnpScoreTail, kKCount
 };
 
 // HIP-event timing of individual kernels on the context stream (off by default).
@@ -93,6 +95,7 @@ struct vo_ctx {
   std::unique_ptr<vo::Comm> comm;
   bool ba_split_reduce = false;  // test/tool switch (vo_ba_split_reduce): K2 never fused into K3
   int ba_drop_reducers = 0;      // test switch (vo_ba_testing_drop_reducers): fused launches short of reducers
+  int pnp_split = 0;      // test/tool switch (vo_pnp_testing_split): 0 auto, -1 never, n > 0 first n hypotheses
   int ba_k1_variant = 0;  // test switch (vo_ba_testing_k1): -1 four-wave K1, n >= 1 one-wave K1 of n chunks per segment
   vo_ctx();
   ~vo_ctx();
