@@ -78,7 +78,11 @@ __global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a, int h_lo, int h_
     model[15] = 0.0;
     return;
   }
+  // alphas and v in LDS, one column per lane (one wave per workgroup)
+  __shared__ double s_cols[kEpnpColDoubles * 64];
   EpnpState S;
+  S.alphas = Col{s_cols + threadIdx.x, 64};
+  S.v = Col{s_cols + kPts * 4 * 64 + threadIdx.x, 64};
 #pragma unroll
   for (int p = 0; p < kPts; ++p) {
     const int i = o + (n == kPts ? p : a.subsets[(size_t)g * kPts + p]);

@@ -70,6 +70,9 @@ int run_full(const char* in_path, const char* out_path) {
   std::vector<int> counts(nh ? nh : 1, 0);
   for (int h = 0; h < nh; ++h) {
     EpnpState S;
+    double cols[kEpnpColDoubles];
+    S.alphas = Col{cols, 1};
+    S.v = Col{cols + kPts * 4, 1};
     for (int p = 0; p < kPts; ++p) {
       const int i = n == kPts ? p : sub[5 * (size_t)h + p];
       for (int c = 0; c < 3; ++c) S.pw[p][c] = X[3 * (size_t)i + c];
@@ -173,6 +176,9 @@ int main(int argc, char** argv) {
   for (int h = 0; h < count; ++h) {
     const double* src = &in[(size_t)h * 25];
     EpnpState S;
+    double cols[kEpnpColDoubles];
+    S.alphas = Col{cols, 1};
+    S.v = Col{cols + kPts * 4, 1};
     for (int p = 0; p < kPts; ++p) {
       for (int c = 0; c < 3; ++c) S.pw[p][c] = src[3 * p + c];
       for (int c = 0; c < 2; ++c) S.us[p][c] = src[15 + 2 * p + c];

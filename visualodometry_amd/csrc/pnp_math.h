@@ -181,15 +181,29 @@ VO_HD void qr_solve(double (&A)[NR][NC], double (&b)[NR], double (&X)[NC]) {
   }
 }
 
+// Doubles at p[k * stride]: a local array (stride 1), or on the device one lane's column of a
+// wave's LDS block (stride 64), which keeps EPnP's read-mostly arrays out of the VGPRs that
+// the 12x12 Jacobi sweep needs.  The arithmetic is the same either way.
+struct Col {
+  double* p;
+  int stride;
+  VO_HD double& operator[](int k) const { return p[k * stride]; }
+};
+
 struct EpnpState {
-  double pw[kPts][3];
-  double us[kPts][2];
-  double alphas[kPts][4];
+  float pw[kPts][3];  // object points (float32, as the caller holds them)
+  float us[kPts][2];  // image points (float32)
+  Col alphas;         // [p * 4 + c]: barycentric coordinates
+  Col v;              // [i * 12 + k]: v[i] = ut row 11 - i (right singular vectors, smallest first)
   double cws[4][3];
-  double v[4][12];  // v[i] = ut row 11 - i (right singular vectors, smallest first)
   double L[6][10];
   double rho[6];
 };
+constexpr int kEpnpColDoubles = kPts * 4 + 4 * 12;  // alphas, v
+
+VO_HD double dot3f(const double* a, const float* b) {
+  return a[0] * (double)b[0] + a[1] * (double)b[1] + a[2] * (double)b[2];
+}
 
 VO_HD void gauss_newton(const EpnpState& S, double (&betas)[4]) {
   double x[4] = {0.0, 0.0, 0.0, 0.0};
@@ -226,14 +240,14 @@ VO_HD double compute_R_and_t(const EpnpState& S, const Cam& K, const double (&be
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) ccs[j][k] = ccs[j][k] + betas[i] * S.v[i][3 * j + k];
+      for (int k = 0; k < 3; ++k) ccs[j][k] = ccs[j][k] + betas[i] * S.v[i * 12 + 3 * j + k];
   double pcs[kPts][3];
 #pragma unroll
   for (int p = 0; p < kPts; ++p)
 #pragma unroll
     for (int k = 0; k < 3; ++k)
-      pcs[p][k] = S.alphas[p][0] * ccs[0][k] + S.alphas[p][1] * ccs[1][k] + S.alphas[p][2] * ccs[2][k] +
-                  S.alphas[p][3] * ccs[3][k];
+      pcs[p][k] = S.alphas[p * 4] * ccs[0][k] + S.alphas[p * 4 + 1] * ccs[1][k] + S.alphas[p * 4 + 2] * ccs[2][k] +
+                  S.alphas[p * 4 + 3] * ccs[3][k];
   if (pcs[0][2] < 0.0) {  // solve_for_sign
 #pragma unroll
     for (int p = 0; p < kPts; ++p)
@@ -297,9 +311,9 @@ VO_HD double compute_R_and_t(const EpnpState& S, const Cam& K, const double (&be
   double err = 0.0;
 #pragma unroll
   for (int p = 0; p < kPts; ++p) {
-    const double Xc = dot3(R[0], S.pw[p]) + t[0];
-    const double Yc = dot3(R[1], S.pw[p]) + t[1];
-    const double inv_Zc = 1.0 / (dot3(R[2], S.pw[p]) + t[2]);
+    const double Xc = dot3f(R[0], S.pw[p]) + t[0];
+    const double Yc = dot3f(R[1], S.pw[p]) + t[1];
+    const double inv_Zc = 1.0 / (dot3f(R[2], S.pw[p]) + t[2]);
     const double ue = K.uc + K.fu * Xc * inv_Zc;
     const double ve = K.vc + K.fv * Yc * inv_Zc;
     const double du = S.us[p][0] - ue, dv = S.us[p][1] - ve;
@@ -386,9 +400,23 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) 
 #pragma unroll
     for (int p = 0; p < kPts; ++p) {
       const double d0 = S.pw[p][0] - S.cws[0][0], d1 = S.pw[p][1] - S.cws[0][1], d2 = S.pw[p][2] - S.cws[0][2];
+      double al[4];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) S.alphas[p][1 + j] = ci[j][0] * d0 + ci[j][1] * d1 + ci[j][2] * d2;
-      S.alphas[p][0] = 1.0 - S.alphas[p][1] - S.alphas[p][2] - S.alphas[p][3];
+      for (int j = 0; j < 3; ++j) al[1 + j] = ci[j][0] * d0 + ci[j][1] * d1 + ci[j][2] * d2;
+      al[0] = 1.0 - al[1] - al[2] - al[3];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) S.alphas[p * 4 + c] = al[c];
+    }
+  }
+  // compute_rho (ahead of the 12x12 SVD, so that the control points are dead during it)
+  {
+    constexpr int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      double e[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) e[k] = S.cws[pa[i]][k] - S.cws[pb[i]][k];
+      S.rho[i] = dot3(e, e);
     }
   }
   // M (2n x 12), M^T M, its four smallest right singular vectors
@@ -403,7 +431,7 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) 
       double m1[12], m2[12];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const double al = S.alphas[p][c];
+        const double al = S.alphas[p * 4 + c];
         m1[3 * c] = al * K.fu;
         m1[3 * c + 1] = 0.0;
         m1[3 * c + 2] = al * (K.uc - S.us[p][0]);
@@ -424,20 +452,23 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) 
     jacobi_rows<12, 12, false>(A, W, dummy);  // M^T M is symmetric: its rows are A^T's
     int rk[12];
     desc_rank<12>(W, rk);
+    double s[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
       ok &= W[i] > kDblMin;
-      const double s = 1.0 / W[i];
+      s[i] = 1.0 / W[i];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int k = 0; k < 12; ++k) {
-        const double val = A[i][k] * s;
+        double val = 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (rk[i] == 11 - q) S.v[q][k] = val;
+        for (int i = 0; i < 12; ++i) val = rk[i] == 11 - q ? A[i][k] * s[i] : val;
+        S.v[q * 12 + k] = val;
       }
-    }
   }
-  // compute_L_6x10, compute_rho
+  // compute_L_6x10
   {
     constexpr int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
     double dv[4][6][3];
@@ -446,7 +477,7 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) 
 #pragma unroll
       for (int j = 0; j < 6; ++j)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) dv[i][j][k] = S.v[i][3 * pa[j] + k] - S.v[i][3 * pb[j] + k];
+        for (int k = 0; k < 3; ++k) dv[i][j][k] = S.v[i * 12 + 3 * pa[j] + k] - S.v[i * 12 + 3 * pb[j] + k];
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       double* row = S.L[i];
@@ -460,15 +491,14 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) 
       row[7] = 2.0 * dot3(dv[1][i], dv[3][i]);
       row[8] = 2.0 * dot3(dv[2][i], dv[3][i]);
       row[9] = dot3(dv[3][i], dv[3][i]);
-      double e[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) e[k] = S.cws[pa[i]][k] - S.cws[pb[i]][k];
-      S.rho[i] = dot3(e, e);
     }
   }
   // three beta approximations, each refined by Gauss-Newton; keep the lowest error
   double bestR[3][3], bestt[3], best_err = 0.0;
   for (int kind = 1; kind <= 3; ++kind) {
+    // keeps the reads of S.alphas / S.v (LDS on the device) inside the loop: hoisted out of
+    // it they would take registers across all three kinds
+    asm volatile("" ::: "memory");
     double betas[4] = {0.0, 0.0, 0.0, 0.0};
     double rho[6];
 #pragma unroll
