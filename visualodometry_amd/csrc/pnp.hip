@@ -109,8 +109,67 @@ __global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a, int h_lo, int h_
   model[15] = ok ? 1.0 : 0.0;
 }
 
+// The serial loop of RANSACPointSetRegistrator::run (OpenCV calib3d/src/ptsetreg.cpp) over
+// precomputed inlier counts.  A hypothesis without a model (EPnP failed) has count 0, which
+// never beats max(max_good, kPts - 1): the loop's skip.  State (thread 0's, in LDS): the
+// iteration reached, the loop's bound niters (> h_end when it stopped at h_end: the serial loop
+// would go on), the best hypothesis (-1: none) and its count.
+struct ReplayState {
+  int it, niters, best, max_good;
+};
+
+__device__ __forceinline__ void replay_init(const PnpArgs& a, ReplayState* st) {
+  if (threadIdx.x == 0) *st = ReplayState{0, a.H, -1, 0};
+}
+
+// Hypotheses [st->it, stop) of frame f (n > kPts points) whose counts cnt[h - base] (h < stop,
+// cnt holding at most kThreads) are in LDS.  Every thread first evaluates the logarithms of the
+// niters update for its count (num_iters_terms: they depend on the count alone), then thread 0
+// runs the loop, applying them in order.  Every thread of the workgroup calls; two barriers.
+template <int kThreads>
+__device__ void replay_chunk(const PnpArgs& a, int n, const int* cnt, int base, int stop, ItersTerms* s_terms,
+                             ReplayState* st) {
+  const int t = threadIdx.x;
+  if (base + t < stop && cnt[t] > kPts - 1) s_terms[t] = num_iters_terms(a.confidence, (double)(n - cnt[t]) / n, kPts);
+  __syncthreads();
+  if (t == 0) {
+    ReplayState r = *st;
+    for (; r.it < r.niters && r.it < stop; ++r.it) {
+      const int good = cnt[r.it - base];
+      if (good > (r.max_good > kPts - 1 ? r.max_good : kPts - 1)) {
+        r.best = r.it;
+        r.max_good = good;
+        r.niters = num_iters_apply(s_terms[r.it - base], r.niters);
+      }
+    }
+    *st = r;
+  }
+  __syncthreads();
+}
+
+// The replay over hypotheses [0, h_end) of frame f (n > kPts) from the counts in global memory,
+// staged in LDS a chunk of kThreads at a time with independent loads.  Every thread calls; on
+// return every thread may read *st.
+template <int kThreads>
+__device__ void ransac_replay(const PnpArgs& a, int f, int n, int h_end, int* s_cnt, ItersTerms* s_terms,
+                              ReplayState* st) {
+  replay_init(a, st);
+  const int32_t* counts = a.counts + (size_t)f * a.H;
+  for (int base = 0; base < h_end; base += kThreads) {
+    __syncthreads();  // *st written, the previous chunk consumed
+    const int stop = min(min(st->niters, h_end), base + kThreads);  // niters only shrinks
+    if (base >= stop) break;  // uniform: every thread read the same *st
+    if (base + (int)threadIdx.x < stop) s_cnt[threadIdx.x] = counts[base + threadIdx.x];
+    __syncthreads();
+    replay_chunk<kThreads>(a, n, s_cnt, base, stop, s_terms, st);
+  }
+  __syncthreads();
+}
+
+// need_out (phase 1 with one workgroup per frame, h_lo = 0): the workgroup then replays the RANSAC
+// loop over the counts it just made and writes need_out[f] as pnp_decide would.
 __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, int h_lo, int h_hi,
-                                                        const int32_t* need) {
+                                                        const int32_t* need, int32_t* need_out) {
   // one workgroup per (frame, group of `group` hypotheses of [h_lo, h_hi)): the frame's points
   // stay in L1 across its hypotheses; the host sizes groups so the grid still fills the chip
   const int ngroups = (h_hi - h_lo + group - 1) / group;
@@ -189,62 +248,33 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, in
   }
   __syncthreads();
   for (int h = threadIdx.x; h < h1 - h0; h += 256) a.counts[(size_t)f * a.H + h0 + h] = s_count[h];
-}
-
-// The serial loop of RANSACPointSetRegistrator::run (OpenCV calib3d/src/ptsetreg.cpp) over the
-// inlier counts of hypotheses [0, h_end) of frame f (n > kPts points).  A hypothesis without a
-// model (EPnP failed) has count 0, which never beats max(max_good, kPts - 1): the loop's skip.
-// The whole workgroup (kThreads threads, every one calling) stages each chunk of counts in LDS
-// with independent loads; thread 0 runs the loop.  On return every thread reads s_state: the
-// iteration reached, the loop's bound niters when it stopped (> h_end: the serial loop would go
-// on to hypothesis h_end), the best hypothesis (-1: none) and its count.
-template <int kThreads>
-__device__ void ransac_replay(const PnpArgs& a, int f, int n, int h_end, int* s_cnt, int* s_state) {
-  if (threadIdx.x == 0) {
-    s_state[0] = 0;
-    s_state[1] = a.H;
-    s_state[2] = -1;
-    s_state[3] = 0;
-  }
-  const int32_t* counts = a.counts + (size_t)f * a.H;
-  for (int base = 0; base < h_end; base += kThreads) {
-    __syncthreads();  // s_state written, the previous chunk consumed
-    const int stop = min(min(s_state[1], h_end), base + kThreads);  // niters only shrinks
-    if (base >= stop) break;  // uniform: every thread read the same s_state
-    if (base + (int)threadIdx.x < stop) s_cnt[threadIdx.x] = counts[base + threadIdx.x];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int it = s_state[0], niters = s_state[1], best = s_state[2], max_good = s_state[3];
-      for (; it < niters && it < stop; ++it) {
-        const int good = s_cnt[it - base];
-        if (good > (max_good > kPts - 1 ? max_good : kPts - 1)) {
-          best = it;
-          max_good = good;
-          niters = update_num_iters(a.confidence, (double)(n - good) / n, kPts, niters);
-        }
-      }
-      s_state[0] = it;
-      s_state[1] = niters;
-      s_state[2] = best;
-      s_state[3] = max_good;
+  if (need_out) {  // uniform; here h0 = 0 and h1 = h_hi
+    __shared__ ItersTerms s_terms[kScoreGroupMax];
+    __shared__ ReplayState s_st;
+    if (n > kPts) {  // uniform
+      replay_init(a, &s_st);
+      __syncthreads();
+      replay_chunk<kScoreGroupMax>(a, n, s_count, 0, h1, s_terms, &s_st);
     }
+    if (threadIdx.x == 0) need_out[f] = n > kPts && s_st.niters > h1 ? 1 : 0;
   }
-  __syncthreads();
 }
 
 // After the first h_end hypotheses of every frame are scored: need[f] = 1 where the serial
 // loop has not stopped yet, i.e. the frames whose hypotheses [h_end, H) are solved next.
 // One wave per frame.
 __global__ __launch_bounds__(64) void pnp_decide_kernel(PnpArgs a, int h_end, int32_t* need) {
-  __shared__ int s_cnt[64], s_state[4];
+  __shared__ int s_cnt[64];
+  __shared__ ItersTerms s_terms[64];
+  __shared__ ReplayState s_st;
   const int f = blockIdx.x;
   const int n = a.off[f + 1] - a.off[f];
   if (n <= kPts) {
     if (threadIdx.x == 0) need[f] = 0;
     return;
   }
-  ransac_replay<64>(a, f, n, h_end, s_cnt, s_state);
-  if (threadIdx.x == 0) need[f] = s_state[1] > h_end ? 1 : 0;
+  ransac_replay<64>(a, f, n, h_end, s_cnt, s_terms, &s_st);
+  if (threadIdx.x == 0) need[f] = s_st.niters > h_end ? 1 : 0;
 }
 
 // Sum of one double over a wave in a fixed order (butterfly).
@@ -300,14 +330,16 @@ __global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) 
   const int f = blockIdx.x;
   const int o = a.off[f], n = a.off[f + 1] - o;
   __shared__ int s_count, s_go;
-  __shared__ int s_cnt[kFinalThreads], s_state[4];
+  __shared__ int s_cnt[kFinalThreads];
+  __shared__ ItersTerms s_terms[kFinalThreads];
+  __shared__ ReplayState s_st;
   __shared__ double s_R[9], s_t[3];
   __shared__ double s_red[kFinalWaves * kNe];
   __shared__ double s_ne[kNe];
   // the serial RANSAC loop over the precomputed counts (uniform branch: n is per frame)
-  if (n > kPts) ransac_replay<kFinalThreads>(a, f, n, a.H, s_cnt, s_state);
+  if (n > kPts) ransac_replay<kFinalThreads>(a, f, n, a.H, s_cnt, s_terms, &s_st);
   if (threadIdx.x == 0) s_count = 0;
-  const int best = n > kPts ? s_state[2] : n == kPts && a.models[(size_t)f * a.H * kModel + 15] != 0.0 ? 0 : -1;
+  const int best = n > kPts ? s_st.best : n == kPts && a.models[(size_t)f * a.H * kModel + 15] != 0.0 ? 0 : -1;
   __syncthreads();
   const double* model = a.models + ((size_t)f * a.H + (best < 0 ? 0 : best)) * kModel;
   if (best < 0 || n == kPts) {
@@ -469,10 +501,16 @@ void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* of
   else if (ctx->pnp_split == 0 && (long)batch * H > fill)
     h1 = std::min(H, std::max(kSplitMin, (int)(fill / batch)));
   ws.last_h1 = h1;
-  auto solve_and_score = [&](int h_lo, int h_hi, const int32_t* need, int kid_hyp, int kid_score) {
+  int32_t* need = nullptr;
+  if (h1 < H) {
+    ws.need.reserve((size_t)batch * sizeof(int32_t));
+    need = ws.need.as<int32_t>();
+  }
+  bool decided = false;  // need written by the phase-1 scoring launch
+  auto solve_and_score = [&](int h_lo, int h_hi, const int32_t* need_in, int kid_hyp, int kid_score) {
     const int hr = h_hi - h_lo, nh = batch * hr;
     ctx->prof.begin(ctx->stream, kid_hyp);
-    hipLaunchKernelGGL(pnp_hyp_kernel, dim3(ceil_div(nh, 64)), dim3(64), 0, ctx->stream, a, h_lo, h_hi, need);
+    hipLaunchKernelGGL(pnp_hyp_kernel, dim3(ceil_div(nh, 64)), dim3(64), 0, ctx->stream, a, h_lo, h_hi, need_in);
     ctx->prof.end(ctx->stream);
     VO_HIP_CHECK(hipGetLastError());
     ctx->prof.begin(ctx->stream, kid_score);
@@ -480,19 +518,21 @@ void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* of
     // kScoreGroupMax while the grid keeps ~4 workgroups per CU
     const int group = std::max(1, std::min({hr, kScoreGroupMax, nh / std::max(1, 4 * ctx->num_cus)}));
     const int ngroups = ceil_div(hr, group);
+    int32_t* need_out = need && !need_in && ngroups == 1 && h_lo == 0 ? need : nullptr;
+    decided |= need_out != nullptr;
     hipLaunchKernelGGL(pnp_score_kernel, dim3(batch * ngroups), dim3(256), 0, ctx->stream, a, group, h_lo, h_hi,
-                       need);
+                       need_in, need_out);
     ctx->prof.end(ctx->stream);
     VO_HIP_CHECK(hipGetLastError());
   };
   solve_and_score(0, h1, nullptr, kKPnpHyp, kKPnpScore);
   if (h1 < H) {
-    ws.need.reserve((size_t)batch * sizeof(int32_t));
-    int32_t* need = ws.need.as<int32_t>();
-    ctx->prof.begin(ctx->stream, kKPnpDecide);
-    hipLaunchKernelGGL(pnp_decide_kernel, dim3(batch), dim3(64), 0, ctx->stream, a, h1, need);
-    ctx->prof.end(ctx->stream);
-    VO_HIP_CHECK(hipGetLastError());
+    if (!decided) {  // phase 1 scored a frame in more than one workgroup
+      ctx->prof.begin(ctx->stream, kKPnpDecide);
+      hipLaunchKernelGGL(pnp_decide_kernel, dim3(batch), dim3(64), 0, ctx->stream, a, h1, need);
+      ctx->prof.end(ctx->stream);
+      VO_HIP_CHECK(hipGetLastError());
+    }
     solve_and_score(h1, H, need, kKPnpHypTail, kKPnpScoreTail);
   }
   ctx->prof.begin(ctx->stream, kKPnpFinal);

@@ -643,8 +643,14 @@ VO_HD void rodrigues_to_mat(const double (&r)[3], double (&R)[3][3]) {
     for (int j = 0; j < 3; ++j) R[i][j] = c * (i == j ? 1.0 : 0.0) + c1 * rrt[i][j] + s * rx[i][j];
 }
 
-// RANSACUpdateNumIters (ptsetreg.cpp)
-VO_HD int update_num_iters(double p, double ep, int model_points, int max_iters) {
+// RANSACUpdateNumIters (ptsetreg.cpp), in two parts: the logarithms depend only on the
+// inlier fraction, so a replay can evaluate them for many counts at once and apply them in
+// the serial order (num_iters_apply is the rest of the function, the max_iters cap).
+struct ItersTerms {
+  double num, denom;
+  bool zero;  // denom < DBL_MIN: the function returns 0
+};
+VO_HD ItersTerms num_iters_terms(double p, double ep, int model_points) {
   p = p > 0. ? p : 0.;
   p = p < 1. ? p : 1.;
   ep = ep > 0. ? ep : 0.;
@@ -652,10 +658,15 @@ VO_HD int update_num_iters(double p, double ep, int model_points, int max_iters)
   double num = 1. - p;
   num = num > kDblMin ? num : kDblMin;
   double denom = 1. - pow(1. - ep, (double)model_points);
-  if (denom < kDblMin) return 0;
-  num = log(num);
-  denom = log(denom);
-  return denom >= 0 || -num >= max_iters * (-denom) ? max_iters : (int)rint(num / denom);
+  if (denom < kDblMin) return {0.0, 0.0, true};
+  return {log(num), log(denom), false};
+}
+VO_HD int num_iters_apply(const ItersTerms& t, int max_iters) {
+  if (t.zero) return 0;
+  return t.denom >= 0 || -t.num >= max_iters * (-t.denom) ? max_iters : (int)rint(t.num / t.denom);
+}
+VO_HD int update_num_iters(double p, double ep, int model_points, int max_iters) {
+  return num_iters_apply(num_iters_terms(p, ep, model_points), max_iters);
 }
 
 VO_HD void se3_exp(const double (&d)[6], double (&R)[3][3], double (&t)[3]) {
