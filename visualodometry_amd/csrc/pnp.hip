@@ -180,8 +180,7 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, in
   for (int h = threadIdx.x; h < h1 - h0; h += 256) s_count[h] = 0;
   __syncthreads();
   if (n > kPts && n <= kScoreRegPts * 256) {
-    // the thread's points in registers for all the group's hypotheses, two hypotheses per
-    // pass (independent chains through the f64 division); per point the same arithmetic
+    // the thread's points in registers for all the group's hypotheses
     float P[kScoreRegPts][5];
 #pragma unroll
     for (int u = 0; u < kScoreRegPts; ++u) {
@@ -195,7 +194,11 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, in
       P[u][3] = q.x;
       P[u][4] = q.y;
     }
-    auto score = [&](const double* model) __attribute__((always_inline)) {
+    // one hypothesis at a time (at four waves per SIMD the other waves hide the latency of the
+    // f64 division); the wave's inliers counted by ballot
+    for (int h = h0; h < h1; ++h) {
+      const double* model = a.models + ((size_t)f * a.H + h) * kModel;  // uniform
+      if (model[15] == 0.0) continue;
       double R[9], t[3];
 #pragma unroll
       for (int k = 0; k < 9; ++k) R[k] = model[k];
@@ -205,25 +208,10 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, in
 #pragma unroll
       for (int u = 0; u < kScoreRegPts; ++u) {
         const float M[3] = {P[u][0], P[u][1], P[u][2]};
-        cnt += ((int)threadIdx.x + 256 * u < n && is_inlier(R, t, M, P[u][3], P[u][4], a.K, a.thr2)) ? 1 : 0;
+        const bool in = (int)threadIdx.x + 256 * u < n && is_inlier(R, t, M, P[u][3], P[u][4], a.K, a.thr2);
+        cnt += __popcll(__ballot(in));
       }
-      return cnt;
-    };
-    for (int h = h0; h < h1; h += 2) {
-      const double* m0 = a.models + ((size_t)f * a.H + h) * kModel;  // uniform
-      const double* m1 = a.models + ((size_t)f * a.H + min(h + 1, h1 - 1)) * kModel;
-      const bool on0 = m0[15] != 0.0, on1 = h + 1 < h1 && m1[15] != 0.0;
-      int c0 = on0 ? score(m0) : 0;
-      int c1 = on1 ? score(m1) : 0;
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) {
-        c0 += __shfl_xor(c0, m, 64);
-        c1 += __shfl_xor(c1, m, 64);
-      }
-      if ((threadIdx.x & 63) == 0) {
-        if (c0) atomicAdd(&s_count[h - h0], c0);
-        if (c1) atomicAdd(&s_count[h + 1 - h0], c1);
-      }
+      if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_count[h - h0], cnt);
     }
   } else if (n > kPts) {
     for (int h = h0; h < h1; ++h) {
@@ -235,6 +223,7 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, in
 #pragma unroll
       for (int k = 0; k < 3; ++k) t[k] = model[9 + k];
       int cnt = 0;
+#pragma unroll 1  // frames over 1024 points only: kept small, so it does not set the kernel's VGPRs
       for (int i = threadIdx.x; i < n; i += 256) {
         const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
         float M[3];
