@@ -196,19 +196,31 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, in
     }
     // one hypothesis at a time (at four waves per SIMD the other waves hide the latency of the
     // f64 division); the wave's inliers counted by ballot
-    for (int h = h0; h < h1; ++h) {
-      const double* model = a.models + ((size_t)f * a.H + h) * kModel;  // uniform
-      if (model[15] == 0.0) continue;
+    // (the next hypothesis's model is loaded while this one is scored: uniform, scalar loads)
+    const double* model = a.models + ((size_t)f * a.H + h0) * kModel;
+    double next[13];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) next[k] = model[k];
+    next[12] = model[15];
+    for (int h = h0; h < h1; ++h, model += kModel) {
       double R[9], t[3];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) R[k] = model[k];
+      for (int k = 0; k < 9; ++k) R[k] = next[k];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) t[k] = model[9 + k];
+      for (int k = 0; k < 3; ++k) t[k] = next[9 + k];
+      const bool on = next[12] != 0.0;
+      if (h + 1 < h1) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) next[k] = model[kModel + k];
+        next[12] = model[kModel + 15];
+      }
+      if (!on) continue;
       int cnt = 0;
 #pragma unroll
       for (int u = 0; u < kScoreRegPts; ++u) {
         const float M[3] = {P[u][0], P[u][1], P[u][2]};
-        const bool in = (int)threadIdx.x + 256 * u < n && is_inlier(R, t, M, P[u][3], P[u][4], a.K, a.thr2);
+        // every lane tests its (clamped) point, so no lane-divergent branch; the tail lanes' bits are masked
+        const bool in = (int)is_inlier(R, t, M, P[u][3], P[u][4], a.K, a.thr2) & (int)((int)threadIdx.x + 256 * u < n);
         cnt += __popcll(__ballot(in));
       }
       if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_count[h - h0], cnt);
