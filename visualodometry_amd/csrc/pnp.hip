@@ -278,11 +278,26 @@ __global__ __launch_bounds__(64) void pnp_decide_kernel(PnpArgs a, int h_end, in
   if (threadIdx.x == 0) need[f] = s_st.niters > h_end ? 1 : 0;
 }
 
-// Sum of one double over a wave in a fixed order (butterfly).
+// v plus the value DPP control kCtrl moves into this lane (rows outside kRowMask add +0.0).
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ double dpp_add(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), kCtrl, kRowMask, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), kCtrl, kRowMask, 0xF, false);
+  return v + __hiloint2double(hi, lo);
+}
+
+// Sum of one double over a wave in a fixed order, on DPP lane moves (no LDS traffic): quads,
+// half rows, rows (every lane then holds its row's sum), rows 0 + 1 and 2 + 3 by row_bcast15,
+// all four by row_bcast31 into row 3; lane 63's value broadcast.
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = v + __shfl_xor(v, m, 64);
-  return v;
+  v = dpp_add<0xB1>(v);         // quad_perm [1, 0, 3, 2]
+  v = dpp_add<0x4E>(v);         // quad_perm [2, 3, 0, 1]
+  v = dpp_add<0x141>(v);        // row_half_mirror
+  v = dpp_add<0x140>(v);        // row_mirror
+  v = dpp_add<0x142, 0xA>(v);   // row_bcast15 into rows 1 and 3
+  v = dpp_add<0x143, 0xC>(v);   // row_bcast31 into rows 2 and 3
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63),
+                          __builtin_amdgcn_readlane(__double2loint(v), 63));
 }
 
 // pnp_final: threads per frame.  At two waves per SIMD (<= 256 VGPRs) a CU holds 8 / kFinalWaves
@@ -293,6 +308,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 constexpr int kFinalThreads = VO_PNP_FINAL_THREADS;
 constexpr int kFinalWaves = kFinalThreads / 64;
 static_assert(kFinalThreads % 64 == 0 && kFinalThreads <= 256, "pnp_final: 1..4 waves");
+constexpr int kLmStage = 1024;  // inliers pnp_final stages in LDS for its LM passes (20 KB)
 
 // Normal equations of the inliers at (R, t): this thread's partial sums (points i = tid mod
 // kFinalThreads).
@@ -337,6 +353,8 @@ __global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) 
   __shared__ double s_R[9], s_t[3];
   __shared__ double s_red[kFinalWaves * kNe];
   __shared__ double s_ne[kNe];
+  __shared__ float s_pt[kLmStage * 5];  // staged inliers: X, Y, Z, u, v
+  __shared__ int s_wc[kFinalWaves];
   // the serial RANSAC loop over the precomputed counts (uniform branch: n is per frame)
   if (n > kPts) ransac_replay<kFinalThreads>(a, f, n, a.H, s_cnt, s_terms, &s_st);
   if (threadIdx.x == 0) s_count = 0;
@@ -360,21 +378,61 @@ __global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) 
   for (int k = 0; k < 9; ++k) R[k] = model[k];
 #pragma unroll
   for (int k = 0; k < 3; ++k) t[k] = model[9 + k];
-  int cnt = 0;
-  for (int i = threadIdx.x; i < n; i += kFinalThreads) {
-    const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
-    float M[3];
-    load3(a.X, o + i, M);
-    const bool in = is_inlier(R, t, M, q.x, q.y, a.K, a.thr2);
-    a.mask[o + i] = in ? 1 : 0;
-    cnt += in ? 1 : 0;
+  // The inlier mask of the best model; the inliers, in point order, staged in LDS for the LM
+  // passes (a frame of more than kLmStage inliers reads them from global memory each pass).
+  // Positions by ballot ranks, so the order does not depend on timing.
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int ninl = 0;  // uniform
+  for (int c0 = 0; c0 < n; c0 += kFinalThreads) {
+    const int i = c0 + (int)threadIdx.x;
+    float M[3] = {0.f, 0.f, 0.f};
+    float2 q = make_float2(0.f, 0.f);
+    bool in = false;
+    if (i < n) {
+      q = reinterpret_cast<const float2*>(a.uv)[o + i];
+      load3(a.X, o + i, M);
+      in = is_inlier(R, t, M, q.x, q.y, a.K, a.thr2);
+      a.mask[o + i] = in ? 1 : 0;
+    }
+    const uint64_t b = __ballot(in);
+    if (lane == 0) s_wc[wave] = __popcll(b);
+    __syncthreads();
+    int pos = ninl + __popcll(b & ((1ull << lane) - 1)), tot = 0;
+#pragma unroll
+    for (int w = 0; w < kFinalWaves; ++w) {
+      pos += w < wave ? s_wc[w] : 0;
+      tot += s_wc[w];
+    }
+    if (in && pos < kLmStage) {
+      float* d = &s_pt[5 * pos];
+      d[0] = M[0];
+      d[1] = M[1];
+      d[2] = M[2];
+      d[3] = q.x;
+      d[4] = q.y;
+    }
+    ninl += tot;
+    __syncthreads();  // s_wc is rewritten by the next chunk
   }
-  if (cnt) atomicAdd(&s_count, cnt);
-  // lm_accumulate reads mask[o + i] for the same i this thread wrote (same stride).
+  if (threadIdx.x == 0) s_count = ninl;
+  // normal equations of the inliers at (R, t), this thread's partial sums
+  auto accumulate = [&](const double* Rc, const double* tc, double (&acc)[kNe]) {
+    if (ninl > kLmStage) {
+      lm_accumulate(a, o, n, Rc, tc, acc);  // reads mask[o + i] for the i this thread wrote
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < kNe; ++k) acc[k] = 0.0;
+    for (int j = threadIdx.x; j < ninl; j += kFinalThreads) {
+      const float* d = &s_pt[5 * j];
+      const float M[3] = {d[0], d[1], d[2]};
+      lm_point(Rc, tc, M, d[3], d[4], a.K, acc);
+    }
+  };
   // Levenberg-Marquardt on the inliers: thread 0 holds the state (pnp_math.h LmState),
   // every pass evaluates the normal equations at the pose in s_R/s_t.
   double acc[kNe];
-  lm_accumulate(a, o, n, R, t, acc);
+  accumulate(R, t, acc);
   lm_reduce(acc, s_red, s_ne);
   LmState lm;
   if (threadIdx.x == 0) {
@@ -388,7 +446,7 @@ __global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) 
     for (int k = 0; k < 9; ++k) nR[k] = s_R[k];
 #pragma unroll
     for (int k = 0; k < 3; ++k) nt[k] = s_t[k];
-    lm_accumulate(a, o, n, nR, nt, acc);
+    accumulate(nR, nt, acc);
     lm_reduce(acc, s_red, s_ne);  // ends with a barrier: every thread has read s_R/s_t
     if (threadIdx.x == 0) s_go = lm.update(nR, nt, s_ne) && lm.propose(s_R, s_t) ? 1 : 0;
     __syncthreads();
