@@ -819,8 +819,9 @@ struct alignas(16) LinWave {
 // workgroups of two waves, of three chunks: two of three
 constexpr int kWaveSegsPerCu = 6;
 static_assert(sizeof(LinWave) <= 160 * 1024 / kWaveSegsPerCu, "one-wave K1 LDS image");
-static_assert(kWaveMaxChunks <= 3 && kWaveItems * 36 * sizeof(double) <= 2176 * sizeof(double),
-              "the chunks of a segment fit six waves per CU; every item's block fits the scratch rows");
+static_assert(kWaveMaxChunks <= 6 && kWaveMaxChunks * sizeof(LinWave) <= 160 * 1024 &&
+                  kWaveItems * 36 * sizeof(double) <= 2176 * sizeof(double),
+              "the chunks of a segment fit one CU; every item's block fits the scratch rows");
 
 // point_block over the Zb region's Jp | r (same operation order)
 __device__ __forceinline__ bool point_block_w(const LinWave& S, double lambda, int p, double (&l)[6],
@@ -1912,6 +1913,12 @@ class BAEngine {
       err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
                        prob->obs_uv, seg_obs_grid(seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave))), prev,
                        nw);
+      // six-chunk segments beyond one round (one workgroup per CU): plan with three
+      if (err.empty() && wave && ctx_->ba_k1_variant == 0 && nw == kWaveChunksOneRound &&
+          plan_.n_segments() > ctx_->num_cus)
+        err = build_plan(plan_, prob->n_poses, prob->n_points, prob->n_obs, prob->n_fixed, pp, prob->obs_cam,
+                         prob->obs_uv, seg_obs_grid(seg_obs_for(prob->n_obs, segments_target(ctx_->num_cus, wave))),
+                         prev, kWaveChunksRounds);
       PLAN_T(4, "setup: returned");
       // four-wave K1: every first-camera group ends in a partial segment, so the packing target
       // may give more segments than one round holds; then pack once more, proportionally wider
@@ -2289,13 +2296,21 @@ class BAEngine {
   static int segments_target(int num_cus, bool wave) {
     return wave ? (1 << 30) : VO_BA_SEGMENTS_PER_CU * std::max(1, num_cus);
   }
-  // Chunks per segment of the one-wave K1's plan (the testing switch's value if it sets one):
-  // three at every size -- a third of the slab rows K2 reads for a barrier per segment; cfg3
+  // Chunks per segment of the one-wave K1's plan (the testing switch's value if it sets one).
+  // Three instead of one: a third of the slab rows K2 reads for a barrier per segment; cfg3
   // 14.89k -> 15.27k GN-iters/s (42 148 -> 15 538 rows), cfg4 3.91k -> 4.04k (K2 34 -> 16 us,
-  // K1 148 -> 158 us); two chunks sit between (profiles/r05_k1g)
+  // K1 148 -> 158 us); two chunks sit between (profiles/r05_k1g).  Six (one 153 KB workgroup
+  // per CU, the same six waves per CU) halves the rows again, which pays while the segments fit
+  // one round: cfg3 15.71k -> 15.94k (246 segments, 8 175 rows; K1 24.7 -> 24.0 us, the fused
+  // K3 43.7 -> 43.3 us), but cfg4's nine rounds of single workgroups lose the overlap of one
+  // workgroup's combine with another's chunks: 4.09k -> 3.69k (profiles/r05_ab/k1_six_chunks).
+  // So six for windows whose six-chunk segments are predicted to fit one round (56 observations
+  // per chunk with padding, cfg3's; setup re-plans with three when they do not), else three.
+  static constexpr int kWaveChunksOneRound = std::min(6, kWaveMaxChunks), kWaveChunksRounds = std::min(3, kWaveMaxChunks);
   int wave_chunks(int64_t n_obs) const {
-    (void)n_obs;
-    return ctx_->ba_k1_variant >= 1 ? std::min(ctx_->ba_k1_variant, kWaveMaxChunks) : kWaveMaxChunks;
+    if (ctx_->ba_k1_variant >= 1) return std::min(ctx_->ba_k1_variant, kWaveMaxChunks);
+    const int64_t one_round_obs = (int64_t)ctx_->num_cus * kWaveChunksOneRound * 56;
+    return n_obs * 10 <= one_round_obs * 11 ? kWaveChunksOneRound : kWaveChunksRounds;
   }
 
   LinArgs lin_args() {
@@ -2343,7 +2358,13 @@ class BAEngine {
     }
 #define VO_LIN_LAUNCH(M)                                                                      \
   do {                                                                                        \
-    if (wave && nw == 3)                                                                      \
+    if (wave && nw == 6)                                                                      \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 6>), g, b, 0, ctx_->stream, A);  \
+    else if (wave && nw == 5)                                                                 \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 5>), g, b, 0, ctx_->stream, A);  \
+    else if (wave && nw == 4)                                                                 \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 4>), g, b, 0, ctx_->stream, A);  \
+    else if (wave && nw == 3)                                                                 \
       hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 3>), g, b, 0, ctx_->stream, A);  \
     else if (wave && nw == 2)                                                                 \
       hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 2>), g, b, 0, ctx_->stream, A);  \

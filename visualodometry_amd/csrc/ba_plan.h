@@ -80,7 +80,10 @@ constexpr int kSegSlots = 64;
 constexpr int kLinLanesWave = 64;   // one-wave K1 lanes (ba.hip ba_lin_wave_kernel)
 constexpr int kLinLanes = 256;      // four-wave K1 lanes per Schur pass (ba.hip kLinThreads)
 inline bool plan_is_wave(int seg_obs) { return seg_obs == 1; }
-constexpr int kWaveMaxChunks = 3;  // chunks (waves) per segment of a wave plan (ba.hip instantiates 1..3)
+#ifndef VO_WAVE_MAX_CHUNKS
+#define VO_WAVE_MAX_CHUNKS 6
+#endif
+constexpr int kWaveMaxChunks = VO_WAVE_MAX_CHUNKS;  // chunks (waves) per segment of a wave plan (ba.hip instantiates 1..6)
 constexpr int kWaveItems = 60;     // one-wave K1 lanes for slot items (the scratch rows of the combine)
 constexpr int kChunkHdr = 16;
 
