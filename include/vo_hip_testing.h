@@ -28,10 +28,11 @@ int vo_ba_split_reduce(vo_ctx* ctx, int on);
  * failed factorisation.  n = 0 restores normal launches. */
 int vo_ba_testing_drop_reducers(vo_ctx* ctx, int n);
 
-/* Test switch: the K1 variant this context's later vo_ba_setup calls plan.  0: the default;
- * -1: the four-wave K1 (segments of several chunks of one first-camera group, one 256-lane
- * workgroup walking them); n = 1, 2, 3: the one-wave K1 with n chunks of one first-camera group
- * per segment (one wave per chunk, the segment's waves in one workgroup summing their slot
+/* Test switch: the K1 variant this context's later vo_ba_setup calls plan.  0: the default
+ * (the one-wave K1 with six chunks per segment while they fit one round of workgroups, else
+ * three); -1: the four-wave K1 (segments of several chunks of one first-camera group, one
+ * 256-lane workgroup walking them); n = 1 .. 6: the one-wave K1 with n chunks of one first-camera
+ * group per segment (one wave per chunk, the segment's waves in one workgroup summing their slot
  * blocks in chunk order: one slab row per segment slot).  Same arithmetic, different summation
  * order: results agree to rounding, all within the oracle tolerance.  Keeps every K1 variant
  * covered by the GPU tests; takes effect at the next setup. */

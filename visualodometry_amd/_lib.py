@@ -281,7 +281,7 @@ def ba_testing_drop_reducers(ctx: "Context", n: int) -> None:
 
 def ba_testing_k1(ctx: "Context", variant: int = 0) -> None:
     """Test switch: the K1 variant of the context's later setups (0 default, -1 four-wave K1,
-    n = 1..3 one-wave K1 with n chunks per segment); see vo_ba_testing_k1."""
+    n = 1..6 one-wave K1 with n chunks per segment); see vo_ba_testing_k1."""
     check(ctx.lib.vo_ba_testing_k1(ctx.handle, int(variant)), "vo_ba_testing_k1")
 
 
