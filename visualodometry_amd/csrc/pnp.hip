@@ -39,6 +39,7 @@ using namespace pnpm;
 // ---------------------------------------------------------------- kernels
 constexpr int kScoreGroupMax = 128;  // hypotheses scored by one workgroup, at most
 constexpr int kScoreRegPts = 4;      // points per thread held in registers (frames up to 1024 points)
+constexpr int kScoreStep = 16;       // hypotheses scored between two replay steps (pnp_score_kernel)
 constexpr int kSplitMin = 16;        // hypotheses solved for every frame before the replay decides (pnp_run)
 
 struct PnpArgs {
@@ -168,7 +169,9 @@ __device__ void ransac_replay(const PnpArgs& a, int f, int n, int h_end, int* s_
 
 // need_out (phase 1 with one workgroup per frame, h_lo = 0): the workgroup then replays the RANSAC
 // loop over the counts it just made and writes need_out[f] as pnp_decide would.
-__global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, int h_lo, int h_hi,
+// (four waves per SIMD: 1024 one-frame workgroups in one round; the replay's log/pow would
+// otherwise take the kernel to 135 VGPRs)
+__global__ __launch_bounds__(256, 4) void pnp_score_kernel(PnpArgs a, int group, int h_lo, int h_hi,
                                                         const int32_t* need, int32_t* need_out) {
   // one workgroup per (frame, group of `group` hypotheses of [h_lo, h_hi)): the frame's points
   // stay in L1 across its hypotheses; the host sizes groups so the grid still fills the chip
@@ -177,7 +180,14 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, in
   if (need && !need[f]) return;  // uniform per workgroup, before any barrier
   const int o = a.off[f], n = a.off[f + 1] - o;
   __shared__ int s_count[kScoreGroupMax];
+  __shared__ ItersTerms s_terms[kScoreGroupMax];
+  __shared__ ReplayState s_st;
   for (int h = threadIdx.x; h < h1 - h0; h += 256) s_count[h] = 0;
+  // With need_out (phase 1, h0 = 0) the replay follows the scoring kScoreStep hypotheses at a
+  // time, and the scoring stops where the serial loop stops: its later counts are never read
+  // (pnp_decide and pnp_final stop at the same hypothesis).
+  const bool incremental = need_out && n > kPts && n <= kScoreRegPts * 256;  // uniform
+  if (incremental) replay_init(a, &s_st);
   __syncthreads();
   if (n > kPts && n <= kScoreRegPts * 256) {
     // the thread's points in registers for all the group's hypotheses
@@ -194,36 +204,45 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, in
       P[u][3] = q.x;
       P[u][4] = q.y;
     }
-    // one hypothesis at a time (at four waves per SIMD the other waves hide the latency of the
-    // f64 division); the wave's inliers counted by ballot
-    // (the next hypothesis's model is loaded while this one is scored: uniform, scalar loads)
-    const double* model = a.models + ((size_t)f * a.H + h0) * kModel;
-    double next[13];
+    for (int hc = h0; hc < h1;) {  // uniform
+      const int hc1 = incremental ? min(hc + kScoreStep, h1) : h1;
+      // one hypothesis at a time (at four waves per SIMD the other waves hide the latency of the
+      // f64 division); the wave's inliers counted by ballot
+      // (the next hypothesis's model is loaded while this one is scored: uniform, scalar loads)
+      const double* model = a.models + ((size_t)f * a.H + hc) * kModel;
+      double next[13];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) next[k] = model[k];
-    next[12] = model[15];
-    for (int h = h0; h < h1; ++h, model += kModel) {
-      double R[9], t[3];
+      for (int k = 0; k < 12; ++k) next[k] = model[k];
+      next[12] = model[15];
+      for (int h = hc; h < hc1; ++h, model += kModel) {
+        double R[9], t[3];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) R[k] = next[k];
+        for (int k = 0; k < 9; ++k) R[k] = next[k];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) t[k] = next[9 + k];
-      const bool on = next[12] != 0.0;
-      if (h + 1 < h1) {
+        for (int k = 0; k < 3; ++k) t[k] = next[9 + k];
+        const bool on = next[12] != 0.0;
+        if (h + 1 < hc1) {
 #pragma unroll
-        for (int k = 0; k < 12; ++k) next[k] = model[kModel + k];
-        next[12] = model[kModel + 15];
+          for (int k = 0; k < 12; ++k) next[k] = model[kModel + k];
+          next[12] = model[kModel + 15];
+        }
+        if (!on) continue;
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < kScoreRegPts; ++u) {
+          const float M[3] = {P[u][0], P[u][1], P[u][2]};
+          // every lane tests its (clamped) point, so no lane-divergent branch; the tail lanes' bits are masked
+          const bool in = (int)is_inlier(R, t, M, P[u][3], P[u][4], a.K, a.thr2) & (int)((int)threadIdx.x + 256 * u < n);
+          cnt += __popcll(__ballot(in));
+        }
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_count[h - h0], cnt);
       }
-      if (!on) continue;
-      int cnt = 0;
-#pragma unroll
-      for (int u = 0; u < kScoreRegPts; ++u) {
-        const float M[3] = {P[u][0], P[u][1], P[u][2]};
-        // every lane tests its (clamped) point, so no lane-divergent branch; the tail lanes' bits are masked
-        const bool in = (int)is_inlier(R, t, M, P[u][3], P[u][4], a.K, a.thr2) & (int)((int)threadIdx.x + 256 * u < n);
-        cnt += __popcll(__ballot(in));
+      if (incremental) {
+        __syncthreads();  // the step's counts are in s_count
+        replay_chunk<kScoreGroupMax>(a, n, s_count + (hc - h0), hc, hc1, s_terms, &s_st);
+        if (s_st.niters <= hc1) break;  // the serial loop stopped in this step (uniform)
       }
-      if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_count[h - h0], cnt);
+      hc = hc1;
     }
   } else if (n > kPts) {
     for (int h = h0; h < h1; ++h) {
@@ -250,9 +269,7 @@ __global__ __launch_bounds__(256) void pnp_score_kernel(PnpArgs a, int group, in
   __syncthreads();
   for (int h = threadIdx.x; h < h1 - h0; h += 256) a.counts[(size_t)f * a.H + h0 + h] = s_count[h];
   if (need_out) {  // uniform; here h0 = 0 and h1 = h_hi
-    __shared__ ItersTerms s_terms[kScoreGroupMax];
-    __shared__ ReplayState s_st;
-    if (n > kPts) {  // uniform
+    if (n > kPts && !incremental) {  // uniform: frames over 1024 points replay here
       replay_init(a, &s_st);
       __syncthreads();
       replay_chunk<kScoreGroupMax>(a, n, s_count, 0, h1, s_terms, &s_st);
