@@ -38,7 +38,15 @@ using namespace pnpm;
 
 // ---------------------------------------------------------------- kernels
 constexpr int kScoreGroupMax = 128;  // hypotheses scored by one workgroup, at most
-constexpr int kScoreRegPts = 4;      // points per thread held in registers (frames up to 1024 points)
+// pnp_score: threads per workgroup and the points each holds in registers (frames up to 1024
+// points take the register path); waves per SIMD the kernel's registers must allow so that one
+// workgroup per frame of a 1024-frame batch is one round on 256 CUs
+#ifndef VO_PNP_SCORE_THREADS
+#define VO_PNP_SCORE_THREADS 256
+#endif
+constexpr int kScoreThreads = VO_PNP_SCORE_THREADS;
+constexpr int kScoreRegPts = 1024 / kScoreThreads;
+constexpr int kScoreWavesPerSimd = kScoreThreads / 64;  // four workgroups per CU
 constexpr int kScoreStep = 16;       // hypotheses scored between two replay steps (pnp_score_kernel)
 constexpr int kSplitMin = 16;        // hypotheses solved for every frame before the replay decides (pnp_run)
 
@@ -169,9 +177,9 @@ __device__ void ransac_replay(const PnpArgs& a, int f, int n, int h_end, int* s_
 
 // need_out (phase 1 with one workgroup per frame, h_lo = 0): the workgroup then replays the RANSAC
 // loop over the counts it just made and writes need_out[f] as pnp_decide would.
-// (four waves per SIMD: 1024 one-frame workgroups in one round; the replay's log/pow would
+// (four workgroups per CU: 1024 one-frame workgroups in one round; the replay's log/pow would
 // otherwise take the kernel to 135 VGPRs)
-__global__ __launch_bounds__(256, 4) void pnp_score_kernel(PnpArgs a, int group, int h_lo, int h_hi,
+__global__ __launch_bounds__(kScoreThreads, kScoreWavesPerSimd) void pnp_score_kernel(PnpArgs a, int group, int h_lo, int h_hi,
                                                         const int32_t* need, int32_t* need_out) {
   // one workgroup per (frame, group of `group` hypotheses of [h_lo, h_hi)): the frame's points
   // stay in L1 across its hypotheses; the host sizes groups so the grid still fills the chip
@@ -182,19 +190,19 @@ __global__ __launch_bounds__(256, 4) void pnp_score_kernel(PnpArgs a, int group,
   __shared__ int s_count[kScoreGroupMax];
   __shared__ ItersTerms s_terms[kScoreGroupMax];
   __shared__ ReplayState s_st;
-  for (int h = threadIdx.x; h < h1 - h0; h += 256) s_count[h] = 0;
+  for (int h = threadIdx.x; h < h1 - h0; h += kScoreThreads) s_count[h] = 0;
   // With need_out (phase 1, h0 = 0) the replay follows the scoring kScoreStep hypotheses at a
   // time, and the scoring stops where the serial loop stops: its later counts are never read
   // (pnp_decide and pnp_final stop at the same hypothesis).
-  const bool incremental = need_out && n > kPts && n <= kScoreRegPts * 256;  // uniform
+  const bool incremental = need_out && n > kPts && n <= kScoreRegPts * kScoreThreads;  // uniform
   if (incremental) replay_init(a, &s_st);
   __syncthreads();
-  if (n > kPts && n <= kScoreRegPts * 256) {
+  if (n > kPts && n <= kScoreRegPts * kScoreThreads) {
     // the thread's points in registers for all the group's hypotheses
     float P[kScoreRegPts][5];
 #pragma unroll
     for (int u = 0; u < kScoreRegPts; ++u) {
-      const int i = min((int)threadIdx.x + 256 * u, n - 1);
+      const int i = min((int)threadIdx.x + kScoreThreads * u, n - 1);
       const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
       float M[3];
       load3(a.X, o + i, M);
@@ -232,7 +240,7 @@ __global__ __launch_bounds__(256, 4) void pnp_score_kernel(PnpArgs a, int group,
         for (int u = 0; u < kScoreRegPts; ++u) {
           const float M[3] = {P[u][0], P[u][1], P[u][2]};
           // every lane tests its (clamped) point, so no lane-divergent branch; the tail lanes' bits are masked
-          const bool in = (int)is_inlier(R, t, M, P[u][3], P[u][4], a.K, a.thr2) & (int)((int)threadIdx.x + 256 * u < n);
+          const bool in = (int)is_inlier(R, t, M, P[u][3], P[u][4], a.K, a.thr2) & (int)((int)threadIdx.x + kScoreThreads * u < n);
           cnt += __popcll(__ballot(in));
         }
         if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_count[h - h0], cnt);
@@ -255,7 +263,7 @@ __global__ __launch_bounds__(256, 4) void pnp_score_kernel(PnpArgs a, int group,
       for (int k = 0; k < 3; ++k) t[k] = model[9 + k];
       int cnt = 0;
 #pragma unroll 1  // frames over 1024 points only: kept small, so it does not set the kernel's VGPRs
-      for (int i = threadIdx.x; i < n; i += 256) {
+      for (int i = threadIdx.x; i < n; i += kScoreThreads) {
         const float2 q = reinterpret_cast<const float2*>(a.uv)[o + i];
         float M[3];
         load3(a.X, o + i, M);
@@ -267,7 +275,7 @@ __global__ __launch_bounds__(256, 4) void pnp_score_kernel(PnpArgs a, int group,
     }
   }
   __syncthreads();
-  for (int h = threadIdx.x; h < h1 - h0; h += 256) a.counts[(size_t)f * a.H + h0 + h] = s_count[h];
+  for (int h = threadIdx.x; h < h1 - h0; h += kScoreThreads) a.counts[(size_t)f * a.H + h0 + h] = s_count[h];
   if (need_out) {  // uniform; here h0 = 0 and h1 = h_hi
     if (n > kPts && !incremental) {  // uniform: frames over 1024 points replay here
       replay_init(a, &s_st);
@@ -596,7 +604,7 @@ void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* of
     const int ngroups = ceil_div(hr, group);
     int32_t* need_out = need && !need_in && ngroups == 1 && h_lo == 0 ? need : nullptr;
     decided |= need_out != nullptr;
-    hipLaunchKernelGGL(pnp_score_kernel, dim3(batch * ngroups), dim3(256), 0, ctx->stream, a, group, h_lo, h_hi,
+    hipLaunchKernelGGL(pnp_score_kernel, dim3(batch * ngroups), dim3(kScoreThreads), 0, ctx->stream, a, group, h_lo, h_hi,
                        need_in, need_out);
     ctx->prof.end(ctx->stream);
     VO_HIP_CHECK(hipGetLastError());
