@@ -47,7 +47,10 @@ constexpr int kScoreGroupMax = 128;  // hypotheses scored by one workgroup, at m
 constexpr int kScoreThreads = VO_PNP_SCORE_THREADS;
 constexpr int kScoreRegPts = 1024 / kScoreThreads;
 constexpr int kScoreWavesPerSimd = kScoreThreads / 64;  // four workgroups per CU
-constexpr int kScoreStep = 16;       // hypotheses scored between two replay steps (pnp_score_kernel)
+#ifndef VO_PNP_SCORE_STEP
+#define VO_PNP_SCORE_STEP 8
+#endif
+constexpr int kScoreStep = VO_PNP_SCORE_STEP;  // hypotheses scored between two replay steps (pnp_score_kernel)
 constexpr int kSplitMin = 16;        // hypotheses solved for every frame before the replay decides (pnp_run)
 
 struct PnpArgs {
