@@ -577,7 +577,9 @@ void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* of
   // up: about 17 at 25 % outliers and confidence 0.99), and one pnp_hyp thread is a long
   // dependent chain (one wave per SIMD, 512 VGPRs): a launch of more waves than SIMDs takes
   // twice as long.  So large batches solve the first h1 hypotheses of every frame (h1 sized
-  // to one wave per SIMD), replay the loop over them (pnp_decide), and solve and score
+  // to one wave per SIMD), replay the loop over them (inside the scoring launch when one
+  // workgroup scores a frame, which then also stops scoring where the loop stops; else
+  // pnp_decide), and solve and score
   // hypotheses [h1, H) only for the frames whose loop has not stopped by h1.  pnp_final's
   // replay reads no count past where the loop stops, so the result is the same as solving all
   // H.  ctx->pnp_split (vo_pnp_testing_split): > 0 forces h1, -1 solves all H at once.
