@@ -92,6 +92,20 @@ int vo_match_knn2_ratio(vo_ctx* ctx, const float* des0, int n0, const float* des
 /* Top-2 per query without the ratio test.  idx_out: (n0, 2) int32 (-1 when
  * fewer than 2 neighbours exist), dist_out: (n0, 2) float32 distances
  * (FLT_MAX where idx is -1). */
+/* The same with a cached query side: the reference matches every frame against the same
+ * keyframe (vo.py:64-65, des0 = the keyframe's descriptors), so a nonzero des0_tag keys a cache
+ * of des0's device copy and packed rows.  A call whose (des0 pointer, n0, dim, des0_tag) equal
+ * the cached ones skips des0's upload and packing; the caller gives a new tag whenever des0's
+ * contents may have changed (0 = no cache).  Results are vo_match_knn2_ratio's. */
+int vo_match_knn2_ratio_q(vo_ctx* ctx, const float* des0, int n0, uint64_t des0_tag, const float* des1,
+                          int n1, int dim, double ratio, int32_t* out_pairs, int32_t* out_count);
+/* Device-resident descriptors (pointers into this process's HIP device memory, e.g. the
+ * feature dicts' GPU tensors, which frontend.py:66-67 moves to config.device): no descriptor
+ * crosses PCIe, only the pairs come back to the host.  The caller orders the producer of the
+ * descriptors before the call (e.g. synchronises its stream).  des0_tag as in _q. */
+int vo_match_knn2_ratio_dev(vo_ctx* ctx, const float* d_des0, int n0, uint64_t des0_tag,
+                            const float* d_des1, int n1, int dim, double ratio, int32_t* out_pairs,
+                            int32_t* out_count);
 int vo_match_knn2(vo_ctx* ctx, const float* des0, int n0, const float* des1, int n1,
                   int dim, int32_t* idx_out, float* dist_out);
 
@@ -143,6 +157,14 @@ typedef struct {
  * communicator (vo_comm_init) every rank reaches the same verdict: a shard that
  * fails its checks on one rank is VO_ERR_ARG on all ranks. */
 int vo_ba_setup(vo_ctx* ctx, const vo_ba_problem* prob, uint64_t* session_out);
+/* Optional, once per context before its first keyframe (SlidingWindowBA's constructor, with
+ * the window and map capacity of the VO configuration): pre-sizes every host and device
+ * buffer a window of about n_poses cameras, n_points landmarks and n_obs observations needs
+ * (page-locked plan images, device slabs and systems, kernel attributes), so the first
+ * vo_ba_setup of the drive (vo.py:252-288, the first keyframe) allocates nothing and faults in
+ * no page.  The context has no problem afterwards.  VO_ERR_STATE with a communicator of more
+ * than one rank (call it before vo_comm_init). */
+int vo_ba_reserve(vo_ctx* ctx, int n_poses, int n_points, int64_t n_obs, int n_fixed);
 /* poses: (n_poses, 12) float64 = R_cw row-major (9) then t_cw (3);
  * points: (n_points, 3) float64 -- the sizes of the session's problem. */
 int vo_ba_set_state(vo_ctx* ctx, uint64_t session, const double* poses, const double* points);
@@ -327,6 +349,14 @@ typedef struct vo_sift_keypoint {
 int vo_sift_detect_and_compute(vo_ctx* ctx, const uint8_t* img, int h, int w, int nfeatures, double contrast,
                                double edge, double sigma, int n_layers, int capacity, vo_sift_keypoint* kps,
                                float* desc, int32_t* count);
+/* The same call with device outputs: FeatureFrontend.process_image's SIFT branch
+ * (frontend.py:51-75) keeps only k.pt and the descriptors and moves both to config.device
+ * (:66-67), so the drop-in writes them straight into the caller's GPU buffers (pointers of
+ * this process's HIP runtime on the context's GPU, validated before any launch: VO_ERR_ARG
+ * otherwise) and only *count crosses PCIe.  d_kps[capacity], d_desc[capacity x 128]. */
+int vo_sift_detect_and_compute_dev(vo_ctx* ctx, const uint8_t* img, int h, int w, int nfeatures, double contrast,
+                                   double edge, double sigma, int n_layers, int capacity, vo_sift_keypoint* d_kps,
+                                   float* d_desc, int32_t* count);
 /* Batch of equally sized images in HBM (d_imgs: batch x h x w uint8).  Per image b:
  * d_kps[b * capacity + i], d_desc[(b * capacity + i) * 128], i < d_counts[b]
  * (d_counts[b] < 0 when a capacity overflowed: -d_counts[b] is the working capacity that

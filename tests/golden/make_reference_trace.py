@@ -284,6 +284,7 @@ def run_dropin(out_path: str, ba: bool = False) -> None:
         return ba_mod.BAResult(P, X, costs, "ok")
 
     ba_mod.SlidingWindowBA.optimize = optimize
+    ba_mod.SlidingWindowBA.reserve = lambda self, *a, **k: None  # no device here
     # visualodometry_amd.dropin.run.main, with recording wrappers added after install()
     main_py = REF_SRC / "main.py"
     sys.path[:0] = [str(ROOT / "visualodometry_amd" / "dropin"), str(REF_SRC)]

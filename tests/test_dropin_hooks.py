@@ -9,6 +9,7 @@ from oracle import ba_ref
 from tests.vo_scene import Cfg, FakeVO, Scene, drive
 from visualodometry_amd import _lib
 from visualodometry_amd.ba import BAResult, csr_from_obs_pt
+from visualodometry_amd import sift
 from visualodometry_amd.dropin import hooks
 
 
@@ -111,6 +112,9 @@ class _Front:
     def match_frames(self, f0, f1):
         return "original"
 
+    def process_image(self, img):
+        return "original"
+
 
 def test_match_frames_routing():
     patched = hooks._wrap_match_frames(_Front.match_frames)
@@ -148,6 +152,21 @@ def test_frontend_init_swaps_in_the_gpu_sift():
     assert f.extractor == "cv2.SIFT"
 
 
+def test_process_image_routing():
+    """The process_image hook takes the GPU-tensor path only for the drop-in's SIFT extractor
+    on a CUDA device and a single-channel image; everything else runs the reference's body."""
+    import types
+
+    patched = hooks._wrap_process_image(_Front.process_image)
+    f = _Front("sift")
+    assert patched(f, np.zeros((4, 4), np.uint8)) == "original"  # extractor is not the drop-in's
+    f.extractor = sift.SIFT_create(nfeatures=10)
+    f.device = types.SimpleNamespace(type="cpu")
+    assert patched(f, np.zeros((4, 4), np.uint8)) == "original"  # torch on the CPU
+    f.device = types.SimpleNamespace(type="cuda")
+    assert patched(f, np.zeros((4, 4, 3), np.uint8)) == "original"  # colour: the reference converts it
+
+
 def test_install_is_idempotent():
     class F(_Front):
         pass
@@ -156,9 +175,9 @@ def test_install_is_idempotent():
         pass
 
     hooks.install(F, V)
-    m1, k1 = F.match_frames, V._create_keyframe
+    m1, k1, p1 = F.match_frames, V._create_keyframe, F.process_image
     hooks.install(F, V)
-    assert F.match_frames is m1 and V._create_keyframe is k1
+    assert F.match_frames is m1 and V._create_keyframe is k1 and F.process_image is p1
     assert V._create_keyframe._vo_amd_wrapped is FakeVO._create_keyframe
 
 

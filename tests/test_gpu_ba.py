@@ -164,6 +164,34 @@ def test_deterministic_bitwise(ctx):
         np.testing.assert_array_equal(a, b)
 
 
+def test_reserve_then_window_equals_plain(ctx):
+    """vo_ba_reserve pre-sizes the context (a synthetic window set up twice, then dropped): the
+    next window's results are bitwise those of a context that never reserved, the reserved
+    context holds no problem, and a window larger than the reservation still runs."""
+    p = make_ba_config("cfg2")
+    ref_s = _session(p, ctx)
+    rc0, c0 = ref_s.run(4)
+    P0, X0 = ref_s.get_state()
+    fresh = _lib.Context(ctx.device)
+    _lib.ba_reserve(fresh, p.n_poses, p.n_points, p.n_obs, p.n_fixed)
+    with pytest.raises(VoError):  # no problem after a reservation
+        _lib.check(fresh.lib.vo_ba_run(fresh.handle, 0, 1, None), "vo_ba_run")
+    s = _session(p, fresh)
+    rc1, c1 = s.run(4)
+    P1, X1 = s.get_state()
+    assert rc0 == rc1 == _lib.VO_OK
+    np.testing.assert_array_equal(c0, c1)
+    np.testing.assert_array_equal(P0, P1)
+    np.testing.assert_array_equal(X0, X1)
+    big = make_ba_config("cfg3")  # larger than the reservation: grows
+    s = _session(big, fresh)
+    rc2, c2 = s.run(2)
+    assert rc2 == _lib.VO_OK and np.all(np.isfinite(c2))
+    with pytest.raises(VoError):
+        _lib.ba_reserve(fresh, 1, 10, 20, 0)  # bad sizes
+    fresh.close()
+
+
 @pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "tiny"])
 def test_fused_reduce_equals_split_launches(ctx, cfg):
     """One rank runs K2 inside the banded K3's launch (reducer workgroups hand the reduced

@@ -256,3 +256,70 @@ def test_sift_hint_with_float_values_takes_the_exact_sweep(ctx):
         _check_knn2(s0, s1, ctx)
     finally:
         matcher.set_descriptor_kind(matcher.DESC_AUTO, ctx)
+
+
+def test_query_cache_torch_cpu_tensors(ctx):
+    """cache_query=True keeps the keyframe side (vo.py:64-65) packed across calls while the same
+    unmodified torch tensor comes back; an in-place write (version bump) or another tensor
+    repacks it.  Every result equals the oracle's."""
+    torch = pytest.importorskip("torch")
+    d0, d1 = sift_like_pair(1500, 1600, 21)
+    _, d2 = sift_like_pair(1500, 1400, 22)
+    t0 = torch.from_numpy(d0.copy())[None]
+    for other in (d1, d2, d1):  # hit, hit (a different train side each time)
+        got = matcher.match_knn2_ratio(t0, other, ctx=ctx, kind=matcher.DESC_SIFT, cache_query=True)
+        np.testing.assert_array_equal(got, match_ref.match_int(d0, other))
+    t0[0, 5, :] = t0[0, 9, :]  # in place: the cached rows are stale now
+    m0 = t0[0].numpy().copy()
+    got = matcher.match_knn2_ratio(t0, d1, ctx=ctx, kind=matcher.DESC_SIFT, cache_query=True)
+    np.testing.assert_array_equal(got, match_ref.match_int(m0, d1))
+    t1 = torch.from_numpy(d2.copy())[None]  # another keyframe
+    got = matcher.match_knn2_ratio(t1, d1, ctx=ctx, kind=matcher.DESC_SIFT, cache_query=True)
+    np.testing.assert_array_equal(got, match_ref.match_int(d2, d1))
+    # a float query behind the cache takes the exact sweep, as an uncached call does
+    f0 = torch.from_numpy((d0 + 0.25).astype(np.float32))[None]
+    got = matcher.match_knn2_ratio(f0, d1, ctx=ctx, kind=matcher.DESC_SIFT, cache_query=True)
+    np.testing.assert_array_equal(got, matcher.match_knn2_ratio(f0[0].numpy(), d1, ctx=ctx))
+
+
+def test_query_cache_tag_and_pointer_keyed(ctx):
+    """The C-level cache key: (pointer, n0, dim, tag).  The same tag with another pointer or
+    size is a miss; numpy arrays are never cached by the Python layer (no version counter)."""
+    from visualodometry_amd._lib import C, check, ptr
+
+    d0, d1 = sift_like_pair(700, 900, 31)
+    e0, _ = sift_like_pair(700, 900, 32)
+    out = np.empty((700, 2), dtype=np.int32)
+    cnt = np.zeros(1, dtype=np.int32)
+    for a in (d0, e0, d0[:650].copy()):
+        check(ctx.lib.vo_match_knn2_ratio_q(ctx.handle, ptr(a, C.c_float), a.shape[0], C.c_uint64(7),
+                                            ptr(d1, C.c_float), d1.shape[0], 128, 0.75, ptr(out, C.c_int32),
+                                            ptr(cnt, C.c_int32)), "q")
+        np.testing.assert_array_equal(out[: cnt[0]], match_ref.match_int(a, d1))
+    assert matcher._tags(ctx).tag_for(d0) == 0
+
+
+def test_dev_entry_refuses_host_pointers(ctx):
+    """vo_match_knn2_ratio_dev validates both pointers as this runtime's device memory of the
+    context's GPU before any launch: host memory is VO_ERR_ARG, never a kernel fault."""
+    from visualodometry_amd import _lib
+    from visualodometry_amd._lib import C, ptr
+
+    d0, d1 = sift_like_pair(64, 64, 41)
+    out = np.empty((64, 2), dtype=np.int32)
+    cnt = np.zeros(1, dtype=np.int32)
+    rc = ctx.lib.vo_match_knn2_ratio_dev(ctx.handle, C.c_void_p(d0.ctypes.data), 64, C.c_uint64(0),
+                                         C.c_void_p(d1.ctypes.data), 64, 128, 0.75, ptr(out, C.c_int32),
+                                         ptr(cnt, C.c_int32))
+    assert rc == _lib.VO_ERR_ARG
+    # device memory of the library itself is accepted, and a range past its allocation is not
+    a = _lib.DeviceArray.from_numpy(ctx, d0)
+    b = _lib.DeviceArray.from_numpy(ctx, d1)
+    rc = ctx.lib.vo_match_knn2_ratio_dev(ctx.handle, C.c_void_p(a.ptr), 64, C.c_uint64(0), C.c_void_p(b.ptr), 64,
+                                         128, 0.75, ptr(out, C.c_int32), ptr(cnt, C.c_int32))
+    assert rc == _lib.VO_OK
+    np.testing.assert_array_equal(out[: cnt[0]], match_ref.match_int(d0, d1))
+    big = np.empty((64 + 4096, 2), dtype=np.int32)  # rows far past the allocation (any rounding of it)
+    rc = ctx.lib.vo_match_knn2_ratio_dev(ctx.handle, C.c_void_p(a.ptr), 64 + 4096, C.c_uint64(0), C.c_void_p(b.ptr),
+                                         64, 128, 0.75, ptr(big, C.c_int32), ptr(cnt, C.c_int32))
+    assert rc == _lib.VO_ERR_ARG

@@ -28,23 +28,27 @@ def exe():
     return EXE
 
 
-def host_models(exe, pw, us, K):
+def host_models(exe, pw, us, K, steps=False):
     with tempfile.TemporaryDirectory() as d:
         fi, fo = os.path.join(d, "in"), os.path.join(d, "out")
         with open(fi, "wb") as f:
             np.array([pw.shape[0]], np.int32).tofile(f)
             np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2]]).tofile(f)
             np.concatenate([pw.reshape(-1, 15), us.reshape(-1, 10)], 1).astype(np.float64).tofile(f)
-        subprocess.run([str(exe), fi, fo], check=True)
+        subprocess.run([str(exe)] + (["steps"] if steps else []) + [fi, fo], check=True)
         return np.fromfile(fo).reshape(-1, 25)
 
 
+@pytest.mark.parametrize("steps", [False, True])
 @pytest.mark.parametrize("seed,noise,frac", [(100, 0.3, 0.25), (7, 0.0, 0.0), (8, 2.0, 0.5)])
-def test_hypotheses_bitwise_equal_oracle(exe, seed, noise, frac):
+def test_hypotheses_bitwise_equal_oracle(exe, seed, noise, frac, steps):
+    """steps: EPnP's 12 x 12 Jacobi SVD in the order of pnp.hip's lane-group kernel (step t runs
+    the pairs (i, j) with i + j == t), which must apply every row's rotations as the cyclic
+    sweep does: the same bits as the oracle."""
     X, uv, K, T, out = pnp_case(1000, seed, noise_px=noise, outlier_frac=frac)
     sub = P.ransac_subsets(1000, 100)
     pw, us = X[sub].astype(np.float64), uv[sub].astype(np.float64)
-    h = host_models(exe, pw, us, K)
+    h = host_models(exe, pw, us, K, steps)
     R, t, ok = P.epnp(pw, us, K)
     rv = P.rodrigues_to_vec(np.where(ok[:, None, None], R, np.eye(3)))
     np.testing.assert_array_equal(h[:, 24] == 1, ok)

@@ -1,0 +1,32 @@
+#!/bin/bash
+# GPU session for round-6 changes: BA / matcher / PnP / torch-coexistence GPU tests, K3 stamps,
+# per-frame latencies, cfg3 A/B bench lines (base vs product, three rounds) and the PnP leg A/B.
+# Usage: gpurun --timeout 900 -- bash tools/gpu_quick2.sh tag base_name
+set -euo pipefail
+TAG=$1
+BASE=$2
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+L=$PWD/visualodometry_amd/lib
+if [ -z "${NO_TESTS:-}" ]; then
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_ba.py tests/test_gpu_match.py tests/test_gpu_pnp.py \
+    tests/test_gpu_torch_coexist.py -x -q --timeout 150 --timeout-method thread > $OUT/tests.log 2>&1
+fi
+if [ -f $L/libvo_hip_stamps.so ]; then
+  VO_LIB_PATH=$L/libvo_hip_stamps.so timeout -k 10 120 python tools/band_stamps.py cfg3 > $OUT/stamps.txt 2>&1
+fi
+timeout -k 10 180 python tools/frame_latency.py > $OUT/frame_latency.json 2> $OUT/frame_latency.err
+for rep in 1 2 3; do
+  for n in $BASE prod; do
+    LIB=$L/libvo_hip_$n.so
+    [ $n = prod ] && LIB=$L/libvo_hip.so
+    VO_LIB_PATH=$LIB timeout -k 10 120 python bench.py --no-matcher --no-cpu-baseline > $OUT/cfg3_${n}_$rep.json 2> $OUT/cfg3_${n}_$rep.err
+  done
+done
+for n in $BASE prod; do
+  LIB=$L/libvo_hip_$n.so
+  [ $n = prod ] && LIB=$L/libvo_hip.so
+  VO_LIB_PATH=$LIB timeout -k 10 200 python tools/pnp_only.py > $OUT/pnp_${n}.json 2> $OUT/pnp_${n}.err
+done
+echo done

@@ -1,6 +1,6 @@
 """Kernel timings of the float-path matcher on bench.bench_matcher_float's workload, with no
-parity guard: for timing-only builds (VO_LIB_PATH=..., e.g. EXTRA=-DVO_RERANK_EXP=n, whose
-results are wrong by design).  Prints one JSON line: HIP-event microseconds per kernel."""
+parity guard: for tuning builds of the library (VO_LIB_PATH=...; timing-only variants are patches
+applied outside the product sources).  Prints one JSON line: HIP-event microseconds per kernel."""
 import json
 import sys
 from pathlib import Path

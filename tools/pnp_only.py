@@ -14,4 +14,4 @@ if len(sys.argv) > 1:  # h1 for vo_pnp_testing_split (0 auto, -1 all hypotheses 
 r = bench.bench_pnp(ctx)
 r.pop("cpu_baseline", None)
 print(json.dumps({"value": r["value"], "kernel_us": r["kernel_us"], "split": r.get("split"),
-                  "roofline_frac": r["roofline"]["frac"]}))
+                  "roofline_frac": r["roofline"]["frac"], "single_frame_ms": r.get("single_frame_ms")}))

@@ -72,11 +72,14 @@ SIGNATURES = {
     "vo_memcpy_h2d": (_I, [_P, _P, _P, C.c_uint64]),
     "vo_memcpy_d2h": (_I, [_P, _P, _P, C.c_uint64]),
     "vo_match_knn2_ratio": (_I, [_P, _PF, _I, _PF, _I, _I, _D, _PI32, _PI32]),
+    "vo_match_knn2_ratio_q": (_I, [_P, _PF, _I, C.c_uint64, _PF, _I, _I, _D, _PI32, _PI32]),
+    "vo_match_knn2_ratio_dev": (_I, [_P, C.c_void_p, _I, C.c_uint64, C.c_void_p, _I, _I, _D, _PI32, _PI32]),
     "vo_match_knn2": (_I, [_P, _PF, _I, _PF, _I, _I, _PI32, _PF]),
     "vo_match_batch_async": (_I, [_P, _P, _P, _I, _I, _I, _I, _D, _P]),
     "vo_match_hint": (_I, [_P, _I]),
     "vo_ba_setup": (_I, [_P, C.POINTER(BAProblemC), C.POINTER(C.c_uint64)]),
     "vo_ba_set_state": (_I, [_P, C.c_uint64, _PD, _PD]),
+    "vo_ba_reserve": (_I, [_P, _I, _I, C.c_int64, _I]),
     "vo_ba_get_state": (_I, [_P, C.c_uint64, _PD, _PD]),
     "vo_ba_run": (_I, [_P, C.c_uint64, _I, _PD]),
     "vo_ba_run_async": (_I, [_P, C.c_uint64, _I]),
@@ -101,6 +104,7 @@ SIGNATURES = {
     "vo_sift_pyramid": (_I, [_P, C.POINTER(C.c_uint8), _I, _I, _D, _I, _PF, C.c_int64, _PF, C.c_int64]),
     "vo_sift_layout": (_I, [_I, _I, _I, _PI64, _I]),
     "vo_sift_detect_and_compute": (_I, [_P, C.POINTER(C.c_uint8), _I, _I, _I, _D, _D, _D, _I, _I, _P, _PF, _PI32]),
+    "vo_sift_detect_and_compute_dev": (_I, [_P, C.POINTER(C.c_uint8), _I, _I, _I, _D, _D, _D, _I, _I, C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)]),
     "vo_sift_detect_and_compute_batch_async": (_I, [_P, _P, _I, _I, _I, _I, _D, _D, _D, _I, _I, _P, _P, _P]),
     "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
@@ -127,8 +131,14 @@ def load() -> C.CDLL:
                     " (hipcc --offload-arch=gfx950)"
                 )
             lib = C.CDLL(str(LIB_PATH))
+            tuning = bool(os.environ.get("VO_LIB_PATH"))
             for name, (res, args) in SIGNATURES.items():
-                fn = getattr(lib, name)
+                try:
+                    fn = getattr(lib, name)
+                except AttributeError:
+                    if tuning:  # an older tuning build (A/B runs): entry points it predates stay unbound
+                        continue
+                    raise
                 fn.restype = res
                 fn.argtypes = args
             if lib.vo_abi_version() != 1:
@@ -277,6 +287,13 @@ def ba_testing_drop_reducers(ctx: "Context", n: int) -> None:
     """Test switch: fused launches of this context leave out ``n`` reducer workgroups, so
     the solver's bounded wait times out; see vo_ba_testing_drop_reducers."""
     check(ctx.lib.vo_ba_testing_drop_reducers(ctx.handle, int(n)), "vo_ba_testing_drop_reducers")
+
+
+def ba_reserve(ctx: "Context", n_poses: int, n_points: int, n_obs: int, n_fixed: int = 2) -> None:
+    """``vo_ba_reserve``: pre-size the context's BA buffers for windows of about this size
+    (once, before the first keyframe); the context has no BA problem afterwards."""
+    check(ctx.lib.vo_ba_reserve(ctx.handle, int(n_poses), int(n_points), int(n_obs), int(n_fixed)),
+          "vo_ba_reserve")
 
 
 def ba_testing_k1(ctx: "Context", variant: int = 0) -> None:

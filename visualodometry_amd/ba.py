@@ -277,6 +277,14 @@ class SlidingWindowBA:
         self.lam = float(getattr(cfg, "ba_lambda", lam))
         self.device = device
 
+    def reserve(self, n_poses: int, n_points: int, obs_per_point: float = 5.0, n_fixed: int = 2) -> None:
+        """Pre-size the device context for windows of up to about ``n_poses`` keyframes and
+        ``n_points`` landmarks (``vo_ba_reserve``), once, before the drive's first keyframe:
+        the first :meth:`optimize` then allocates nothing and faults in no page."""
+        n_points = max(1, int(n_points))
+        n_obs = max(2 * n_points, int(round(obs_per_point * n_points)))
+        _lib.ba_reserve(_lib.context(self.device), max(2, int(n_poses)), n_points, n_obs, int(n_fixed))
+
     def optimize(self, window: BAWindow) -> BAResult:
         poses = np.asarray(window.poses_cw, dtype=np.float64)
         pts = np.asarray(window.points, dtype=np.float64).reshape(-1, 3)

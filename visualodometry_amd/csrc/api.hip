@@ -70,6 +70,7 @@ Profiler::~Profiler() {
 
 // ba.hip
 uint64_t ba_setup(vo_ctx*, const vo_ba_problem*);
+void ba_reserve(vo_ctx*, int, int, int64_t, int);
 void ba_check_session(vo_ctx*, uint64_t);
 void ba_set_state(vo_ctx*, const double*, const double*);
 void ba_get_state(vo_ctx*, double*, double*);
@@ -89,8 +90,27 @@ void bind(vo_ctx* ctx) {
 }
 
 // Host-array matcher call: descriptors staged into the workspace, results copied back.
+// A caller's device pointer must be device memory of the context's GPU, known to this HIP runtime,
+// whose allocation covers [p, p + bytes).
+void check_device_range(vo_ctx* ctx, const void* p, size_t bytes, const char* what) {
+  if (bytes == 0) return;
+  VO_REQUIRE(p != nullptr, VO_ERR_ARG, "%s: null device pointer", what);
+  hipPointerAttribute_t at{};
+  const hipError_t e = hipPointerGetAttributes(&at, p);
+  if (e != hipSuccess) (void)hipGetLastError();
+  VO_REQUIRE(e == hipSuccess && at.type == hipMemoryTypeDevice && at.device == ctx->device, VO_ERR_ARG,
+             "%s: not device memory of device %d in this process's HIP runtime", what, ctx->device);
+  void* base = nullptr;
+  size_t size = 0;
+  const hipError_t e2 = hipMemGetAddressRange(&base, &size, const_cast<void*>(p));
+  if (e2 != hipSuccess) (void)hipGetLastError();
+  VO_REQUIRE(e2 == hipSuccess && (const char*)p + bytes <= (const char*)base + size, VO_ERR_ARG,
+             "%s: %zu bytes past its allocation", what, bytes);
+}
+
 void match_host(vo_ctx* ctx, const float* des0, int n0, const float* des1, int n1, int dim,
-                double ratio, int32_t* pairs, int32_t* count, int32_t* idx2, float* dist2) {
+                double ratio, int32_t* pairs, int32_t* count, int32_t* idx2, float* dist2, uint64_t q_tag = 0,
+                bool device_src = false) {
   VO_REQUIRE(n0 >= 0 && n1 >= 0 && dim >= 1, VO_ERR_ARG, "match: bad shape n0=%d n1=%d dim=%d",
              n0, n1, dim);
   VO_REQUIRE((n0 == 0 || des0) && (n1 == 0 || des1), VO_ERR_ARG, "match: null descriptors");
@@ -98,12 +118,41 @@ void match_host(vo_ctx* ctx, const float* des0, int n0, const float* des1, int n
   if (n0 == 0) return;
   hipStream_t st = ctx->stream;
   MatchWorkspace& ws = ctx->match;
+  MatchQueryCache& qc = ctx->match_q;
+  // the query side's cache (a nonzero tag; the int8 path's dimensions): a hit skips the query's
+  // upload and packing, a miss packs it into the cache first
+  const bool use_cache = q_tag != 0 && n1 > 0 && dim <= 256;
+  const bool hit = use_cache && qc.valid && qc.tag == q_tag && qc.src == (const void*)des0 && qc.n0 == n0 &&
+                   qc.dim == dim && qc.device_src == device_src;
   const size_t b0 = (size_t)n0 * dim * 4, b1 = (size_t)n1 * dim * 4;
-  ws.des.reserve(b0 + b1 + 16);
-  float* d0 = ws.des.as<float>();
-  float* d1 = d0 + (size_t)n0 * dim;
-  VO_HIP_CHECK(hipMemcpyAsync(d0, des0, b0, hipMemcpyHostToDevice, st));
-  if (n1) VO_HIP_CHECK(hipMemcpyAsync(d1, des1, b1, hipMemcpyHostToDevice, st));
+  const float* d0 = des0;
+  const float* d1 = des1;
+  if (!device_src) {
+    ws.des.reserve((use_cache ? 0 : b0) + b1 + 16);
+    float* stage1 = ws.des.as<float>() + (use_cache ? 0 : (size_t)n0 * dim);
+    if (use_cache) {
+      if (!hit) {
+        qc.des.reserve(b0);
+        VO_HIP_CHECK(hipMemcpyAsync(qc.des.ptr, des0, b0, hipMemcpyHostToDevice, st));
+      }
+      d0 = qc.des.as<float>();
+    } else {
+      VO_HIP_CHECK(hipMemcpyAsync(ws.des.ptr, des0, b0, hipMemcpyHostToDevice, st));
+      d0 = ws.des.as<float>();
+    }
+    if (n1) VO_HIP_CHECK(hipMemcpyAsync(stage1, des1, b1, hipMemcpyHostToDevice, st));
+    d1 = stage1;
+  }
+  if (use_cache && !hit) {
+    qc.valid = false;
+    match_pack_query(ctx, d0, n0, dim, qc);
+    qc.tag = q_tag;
+    qc.src = des0;
+    qc.n0 = n0;
+    qc.dim = dim;
+    qc.device_src = device_src;
+    qc.valid = true;
+  }
   ws.best.reserve((size_t)n0 * 4);
   int32_t* d_idx2 = nullptr;
   float* d_dist2 = nullptr;
@@ -112,16 +161,16 @@ void match_host(vo_ctx* ctx, const float* des0, int n0, const float* des1, int n
     d_idx2 = ws.top2.as<int32_t>();
     d_dist2 = reinterpret_cast<float*>(d_idx2 + 2 * (size_t)n0);
   }
-  match_run(ctx, d0, d1, 1, n0, n1, dim, ratio, ws.best.as<int32_t>(), d_idx2, d_dist2);
+  match_run(ctx, d0, d1, 1, n0, n1, dim, ratio, ws.best.as<int32_t>(), d_idx2, d_dist2, use_cache ? &qc : nullptr);
   if (pairs) {
     ws.pairs.reserve((size_t)n0 * 8 + 16);
     int32_t* d_pairs = ws.pairs.as<int32_t>();
     int32_t* d_count = d_pairs + 2 * (size_t)n0;
     compact_pairs(ctx, ws.best.as<int32_t>(), n0, d_pairs, d_count);
+    // the count and all n0 pair slots (out_pairs' capacity; the slots past the count are left
+    // unspecified) in one round trip: 8 n0 bytes more over PCIe instead of a second sync
     VO_HIP_CHECK(hipMemcpyAsync(count, d_count, 4, hipMemcpyDeviceToHost, st));
-    VO_HIP_CHECK(hipStreamSynchronize(st));
-    if (*count)
-      VO_HIP_CHECK(hipMemcpyAsync(pairs, d_pairs, (size_t)*count * 8, hipMemcpyDeviceToHost, st));
+    VO_HIP_CHECK(hipMemcpyAsync(pairs, d_pairs, (size_t)n0 * 8, hipMemcpyDeviceToHost, st));
   }
   if (idx2) {
     VO_HIP_CHECK(hipMemcpyAsync(idx2, d_idx2, (size_t)n0 * 8, hipMemcpyDeviceToHost, st));
@@ -219,6 +268,29 @@ int vo_match_knn2_ratio(vo_ctx* ctx, const float* des0, int n0, const float* des
     vo::bind(ctx);
     VO_REQUIRE(out_pairs && out_count, VO_ERR_ARG, "vo_match_knn2_ratio: null outputs");
     vo::match_host(ctx, des0, n0, des1, n1, dim, ratio, out_pairs, out_count, nullptr, nullptr);
+  });
+}
+
+int vo_match_knn2_ratio_q(vo_ctx* ctx, const float* des0, int n0, uint64_t des0_tag, const float* des1, int n1,
+                          int dim, double ratio, int32_t* out_pairs, int32_t* out_count) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(out_pairs && out_count, VO_ERR_ARG, "vo_match_knn2_ratio_q: null outputs");
+    vo::match_host(ctx, des0, n0, des1, n1, dim, ratio, out_pairs, out_count, nullptr, nullptr, des0_tag, false);
+  });
+}
+
+int vo_match_knn2_ratio_dev(vo_ctx* ctx, const float* d_des0, int n0, uint64_t des0_tag, const float* d_des1,
+                            int n1, int dim, double ratio, int32_t* out_pairs, int32_t* out_count) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(out_pairs && out_count, VO_ERR_ARG, "vo_match_knn2_ratio_dev: null outputs");
+    VO_REQUIRE(n0 >= 0 && n1 >= 0 && dim >= 1, VO_ERR_ARG, "vo_match_knn2_ratio_dev: bad shape");
+    // no kernel reads a pointer this runtime does not know as device memory of the context's GPU
+    // covering the rows (a pointer of another HIP runtime instance, or of host memory, is refused)
+    vo::check_device_range(ctx, d_des0, (size_t)n0 * dim * 4, "des0");
+    vo::check_device_range(ctx, d_des1, (size_t)n1 * dim * 4, "des1");
+    vo::match_host(ctx, d_des0, n0, d_des1, n1, dim, ratio, out_pairs, out_count, nullptr, nullptr, des0_tag, true);
   });
 }
 
@@ -463,6 +535,49 @@ int vo_sift_detect_and_compute(vo_ctx* ctx, const uint8_t* img, int h, int w, in
   });
 }
 
+int vo_sift_detect_and_compute_dev(vo_ctx* ctx, const uint8_t* img, int h, int w, int nfeatures, double contrast,
+                                   double edge, double sigma, int n_layers, int capacity, vo_sift_keypoint* d_kps,
+                                   float* d_desc, int32_t* count) {
+  return guarded([&] {
+    vo::bind(ctx);
+    VO_REQUIRE(img && d_kps && d_desc && count && capacity >= 1 && h >= 1 && w >= 1, VO_ERR_ARG,
+               "vo_sift_detect_and_compute_dev: bad arguments");
+    // the caller's buffers: device memory of this runtime on the context's GPU, capacity entries each
+    vo::check_device_range(ctx, d_kps, (size_t)capacity * sizeof(vo_sift_keypoint), "kps");
+    vo::check_device_range(ctx, d_desc, (size_t)capacity * 128 * sizeof(float), "desc");
+    vo::SiftWorkspace& ws = ctx->sift;
+    const size_t nimg = (size_t)h * w;
+    ws.img.reserve(nimg);
+    hipStream_t s = ctx->stream;
+    VO_HIP_CHECK(hipMemcpyAsync(ws.img.ptr, img, nimg, hipMemcpyHostToDevice, s));
+    // the working capacity and its retries as vo_sift_detect_and_compute's
+    // (before retainBest the oriented keypoints outnumber the output many times: the working
+    // capacity starts at 32768, as the host entry's default buffers do)
+    int cap = std::min(std::max(capacity, 1 << 15), vo::sift_max_capacity()), n = -1;
+    vo_sift_keypoint* dK = nullptr;
+    float* dD = nullptr;
+    for (;;) {
+      ws.out.reserve((size_t)cap * (sizeof(vo_sift_keypoint) + 128 * sizeof(float)) + 64);
+      dK = ws.out.as<vo_sift_keypoint>();
+      dD = reinterpret_cast<float*>(dK + cap);
+      int32_t* dC = reinterpret_cast<int32_t*>(dD + (size_t)cap * 128);
+      sift_full(ctx, ws.img.as<uint8_t>(), 1, h, w, nfeatures, contrast, edge, sigma, n_layers, cap, dK, dD, dC);
+      VO_HIP_CHECK(hipMemcpyAsync(&n, dC, 4, hipMemcpyDeviceToHost, s));
+      VO_HIP_CHECK(hipStreamSynchronize(s));
+      if (n >= 0 || cap >= vo::sift_max_capacity()) break;
+      cap = (int)std::min<int64_t>(std::max<int64_t>(-(int64_t)n, 2ll * cap), vo::sift_max_capacity());
+    }
+    VO_REQUIRE(n >= 0, VO_ERR_ARG, "vo_sift_detect_and_compute_dev: more than %d keypoints in one image", cap);
+    VO_REQUIRE(n <= capacity, VO_ERR_ARG, "vo_sift_detect_and_compute_dev: %d keypoints exceed capacity=%d", n,
+               capacity);
+    *count = n;
+    if (n == 0) return;
+    VO_HIP_CHECK(hipMemcpyAsync(d_kps, dK, (size_t)n * sizeof(vo_sift_keypoint), hipMemcpyDeviceToDevice, s));
+    VO_HIP_CHECK(hipMemcpyAsync(d_desc, dD, (size_t)n * 128 * sizeof(float), hipMemcpyDeviceToDevice, s));
+    VO_HIP_CHECK(hipStreamSynchronize(s));
+  });
+}
+
 int vo_sift_detect_and_compute_batch_async(vo_ctx* ctx, const uint8_t* d_imgs, int batch, int h, int w,
                                            int nfeatures, double contrast, double edge, double sigma,
                                            int n_layers, int capacity, vo_sift_keypoint* d_kps, float* d_desc,
@@ -515,6 +630,13 @@ int vo_ba_setup(vo_ctx* ctx, const vo_ba_problem* prob, uint64_t* session_out) {
     VO_REQUIRE(session_out, VO_ERR_ARG, "vo_ba_setup: null session_out");
     *session_out = 0;
     *session_out = vo::ba_setup(ctx, prob);
+  });
+}
+
+int vo_ba_reserve(vo_ctx* ctx, int n_poses, int n_points, int64_t n_obs, int n_fixed) {
+  return guarded([&] {
+    vo::bind(ctx);
+    vo::ba_reserve(ctx, n_poses, n_points, n_obs, n_fixed);
   });
 }
 

@@ -2072,7 +2072,23 @@ class BAEngine {
                               diag ? P.camb_ptr[i + 1] : -1};
           red_out_[b] = int2{red_dst_[b], diag ? red_rdst_[i] : 0};
         }
-      const size_t o_meta = pack.add(red_meta_), o_out = pack.add(red_out_);
+      // the fused launch's readiness counters: the column each profile block's reducer stores
+      // into (top columns j of rows i < m + s, then bottom column F - 1 - i at m + s + F - 1 - i),
+      // the cost at F, and how many items each counter waits for
+      red_col_.assign(std::max(1, nprof), 0);
+      col_need_.assign(F + 1, 0);
+      if (band_on_) {
+        const int top = band_.m + band_.s;
+        for (int i = 0; i < F; ++i)
+          for (int b = P.prof_off[i]; b < P.prof_off[i + 1]; ++b) {
+            const int j = P.prof_first[i] + (b - P.prof_off[i]);
+            red_col_[b] = i < top ? j : top + (F - 1 - i);
+            ++col_need_[red_col_[b]];
+          }
+        col_need_[F] = 1;  // the cost item
+      }
+      const size_t o_meta = pack.add(red_meta_), o_out = pack.add(red_out_), o_rcol = pack.add(red_col_),
+                   o_need = pack.add(col_need_);
       // K2 fused into the banded K3's launch when every workgroup of it fits one round at
       // one per CU (the solver's LDS): cfg3's 356 blocks make 178 reducers + the solver on
       // MI355X's 256 CUs (fewer CUs, e.g. a partitioned device: K2 stays a launch of its own)
@@ -2097,12 +2113,16 @@ class BAEngine {
       d_band_tab_.ptr = band_on_ ? base + o_band_tab : nullptr;
       d_red_meta_.ptr = base + o_meta;
       d_red_out_.ptr = base + o_out;
+      d_red_col_.ptr = base + o_rcol;
+      d_col_need_.ptr = base + o_need;
       // the status word, K2's fused-round counter and the zero block (masked prefetches)
       d_misc_.reserve(kMiscBytes);
       d_status_.ptr = d_misc_.ptr;
-      d_red_count_.ptr = d_misc_.as<char>() + 256;
-      d_zero_.ptr = d_misc_.as<char>() + 512;
+      d_zero_.ptr = d_misc_.as<char>() + 256;
       VO_HIP_CHECK(hipMemsetAsync(d_misc_.ptr, 0, kMiscBytes, st));
+      colcnt_bytes_ = band_col_count_bytes(F);
+      d_colcnt_.reserve(colcnt_bytes_);
+      VO_HIP_CHECK(hipMemsetAsync(d_colcnt_.ptr, 0, colcnt_bytes_, st));
     }
     PLAN_T(10, "setup: band");
     if (!band_on_) {
@@ -2121,6 +2141,50 @@ class BAEngine {
     cur_ = 0;
     session_ = ++g_ba_sessions;
     return session_;
+  }
+
+  // Pre-sizes what a window of about (n_poses, n_points, n_obs) needs, outside the keyframe
+  // calls: both plan objects' host arrays (plan_ and prev_plan_ alternate between setups; the
+  // page-locked chunk images included), every device buffer, the kernels' LDS attributes (the
+  // first one also loads the library's code object) and the state staging buffer.  It sets a
+  // synthetic window of that size up twice -- landmark p seen by a run of consecutive cameras,
+  // the runs spread over the window -- and then drops it: the context has no problem after it,
+  // and the next setup takes nothing over from it.  A later, larger window still grows what it
+  // needs (every array keeps a quarter of headroom).
+  void reserve(int n_poses, int n_points, int64_t n_obs, int n_fixed) {
+    VO_REQUIRE(n_poses >= 2 && n_points >= 1 && n_obs >= 2 * (int64_t)n_points && n_obs <= INT32_MAX &&
+                   n_fixed >= 0 && n_fixed < n_poses,
+               VO_ERR_ARG, "vo_ba_reserve: bad sizes");
+    VO_REQUIRE(!(ctx_->comm && ctx_->comm->nranks > 1), VO_ERR_STATE,
+               "vo_ba_reserve: before vo_comm_init (a setup with a communicator is collective)");
+    const int len0 = (int)std::min<int64_t>(n_poses, n_obs / n_points);
+    const int64_t extra = std::min<int64_t>(n_obs - (int64_t)len0 * n_points, n_points);
+    std::vector<int32_t> ptr(n_points + 1), cam;
+    cam.reserve(n_obs);
+    for (int p = 0; p < n_points; ++p) {
+      const int len = std::min(n_poses, len0 + (p < extra ? 1 : 0));
+      const int c0 = (int)((int64_t)p * (n_poses - len + 1) / n_points);
+      for (int c = 0; c < len; ++c) cam.push_back(c0 + c);
+      ptr[p + 1] = (int32_t)cam.size();
+    }
+    std::vector<float> uv(2 * cam.size(), 0.0f);
+    vo_ba_problem pr{};
+    pr.n_poses = n_poses;
+    pr.n_points = n_points;
+    pr.n_obs = (int32_t)cam.size();
+    pr.n_fixed = n_fixed;
+    pr.fx = pr.fy = 500.0;
+    pr.lambda = 1.0;
+    pr.point_ptr = ptr.data();
+    pr.obs_cam = cam.data();
+    pr.obs_uv = uv.data();
+    for (int k = 0; k < 2; ++k) setup(&pr);
+    h_state_.reserve((3ull * n_points + 12ull * n_poses) * 8);
+    d_cost_.reserve(64 * 8);
+    VO_HIP_CHECK(hipStreamSynchronize(ctx_->stream));
+    plan_ok_ = false;  // nothing of the synthetic plan is taken over
+    have_problem_ = false;
+    have_state_ = false;
   }
 
   // The caller's session must be the engine's current problem (VO_ERR_STATE otherwise):
@@ -2151,7 +2215,7 @@ class BAEngine {
     VO_HIP_CHECK(hipEventRecord(h_state_ev_, st));
     h_state_busy_ = true;
     VO_HIP_CHECK(hipMemsetAsync(d_status_.ptr, 0, sizeof(int), st));
-    if (fuse_ok_) VO_HIP_CHECK(hipMemsetAsync(d_red_count_.ptr, 0, 256, st));  // after a timed-out solve
+    if (fuse_ok_) VO_HIP_CHECK(hipMemsetAsync(d_colcnt_.ptr, 0, colcnt_bytes_, st));  // after a timed-out solve
     cur_ = 0;
     pending_ = false;
     have_state_ = true;
@@ -2211,7 +2275,7 @@ class BAEngine {
   // so every late reducer has counted itself by now -- and the timeout flag is stripped from
   // the status word's iteration.  Returns whether a timeout was recorded.
   bool clear_timeout(int& status) {
-    if (status && fuse_ok_) VO_HIP_CHECK(hipMemsetAsync(d_red_count_.ptr, 0, 256, ctx_->stream));
+    if (status && fuse_ok_) VO_HIP_CHECK(hipMemsetAsync(d_colcnt_.ptr, 0, colcnt_bytes_, ctx_->stream));
     if (!(status & kBandStatusTimeout)) return false;
     status &= ~kBandStatusTimeout;
     return true;
@@ -2446,10 +2510,12 @@ class BAEngine {
       B.stamps = nullptr;
       B.nred = fused() ? band_fused_workgroups(A.nprof) : 0;
       B.red_drop = B.nred > 0 ? ctx_->ba_drop_reducers : 0;
-      B.red_count = d_red_count_.as<unsigned>();
+      B.red_count = d_colcnt_.as<unsigned>();
+      B.red_col = d_red_col_.as<int>();
+      B.col_need = d_col_need_.as<int>();
       B.red = reduce_args();
-      if (stamps_on_) {
-        d_stamps3_.reserve(8 * kBandStamps * 8);
+      if (stamps_on_) {  // per wave phase cycles, then realtime stamps of the solver and each reducer
+        d_stamps3_.reserve((8 * kBandStamps + 8 + 4 * (B.nred + 1)) * 8);
         B.stamps = d_stamps3_.as<unsigned long long>();
       }
       (void)P;
@@ -2593,9 +2659,13 @@ class BAEngine {
   HostBuf h_tab_;
   DevBuf d_tab_;
   DevView d_chunk_hdr_, d_seg_hdr_, d_slab_pos_, d_cam_pos_, d_solve_tab_, d_band_tab_, d_red_meta_, d_red_out_;
-  static constexpr size_t kMiscBytes = 1024;
-  DevBuf d_misc_;  // [status | K2 fused-round counter | zero block (512 B)]
-  DevView d_status_, d_red_count_, d_zero_;
+  static constexpr size_t kMiscBytes = 256 + 512;
+  DevBuf d_misc_;  // [status | zero block (512 B)]
+  DevView d_status_, d_zero_;
+  DevBuf d_colcnt_;  // the fused launch's column readiness counters (band_col_count_bytes)
+  size_t colcnt_bytes_ = 0;
+  DevView d_red_col_, d_col_need_;
+  std::vector<int32_t> red_col_, col_need_;
   std::vector<int4> red_meta_;
   std::vector<int2> red_out_;
   DevBuf d_fac_;
@@ -2631,8 +2701,11 @@ class BAEngine {
     }
     const int n3 = band_on_ ? 8 * kBandStamps : (int)kS3Count;  // K3: banded or profile solver
     if (n >= kPhCount + n3 && d_stamps3_.ptr) {
-      VO_HIP_CHECK(hipMemcpy(out + kPhCount, d_stamps3_.ptr, n3 * 8, hipMemcpyDeviceToHost));
-      k += n3;
+      // the banded solver's realtime stamps follow when the caller asked for them (fused launch)
+      const int nx = band_on_ && fused() ? 8 + 4 * (band_fused_workgroups(plan_.n_prof_blocks()) + 1) : 0;
+      const int n3x = n >= kPhCount + n3 + nx ? n3 + nx : n3;
+      VO_HIP_CHECK(hipMemcpy(out + kPhCount, d_stamps3_.ptr, n3x * 8, hipMemcpyDeviceToHost));
+      k += n3x;
     }
     return k;
   }
@@ -2648,6 +2721,9 @@ BAEngine* ba_engine(vo_ctx* ctx) {
   return ctx->ba.get();
 }
 uint64_t ba_setup(vo_ctx* ctx, const vo_ba_problem* p) { return ba_engine(ctx)->setup(p); }
+void ba_reserve(vo_ctx* ctx, int n_poses, int n_points, int64_t n_obs, int n_fixed) {
+  ba_engine(ctx)->reserve(n_poses, n_points, n_obs, n_fixed);
+}
 void ba_check_session(vo_ctx* ctx, uint64_t s) { ba_engine(ctx)->check_session(s); }
 void ba_set_state(vo_ctx* ctx, const double* poses, const double* pts) {
   ba_engine(ctx)->set_state(poses, pts);

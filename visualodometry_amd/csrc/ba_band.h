@@ -65,12 +65,14 @@ struct BandArgs {
   unsigned long long* stamps;  // diagnostic build: 4 waves x kBandStamps phase cycles
   // Fused K2 (nred > 0, one rank): workgroups 1..nred of the launch reduce the slabs into sys
   // (two profile blocks each, the cost in the item after the last block: K2's sums bit for
-  // bit), store them write-through (sc1) and count themselves in red_count; workgroup 0, the
-  // solver, reads sys only after red_count reached nred and its agent-scope acquire, and
-  // takes nred back off the counter (zero between launches).
+  // bit), store them write-through (sc1) and count themselves in red_count's shards; workgroup
+  // 0, the solver, reads sys (by sc1 loads only) after every shard reached its count, and takes
+  // the counts back off (zero between launches).
   int nred;
   int red_drop;  // test switch (host only): reducer workgroups left out of the launch
-  unsigned* red_count;
+  unsigned* red_count;   // F + 1 column readiness counters, kBandRedShardStride words apart
+  const int* red_col;    // per reduction item (profile block): its column's counter
+  const int* col_need;   // per counter: the items that store into that column (F + 1)
   ReduceArgs red;
 };
 // Status word flag: the fused launch's solver gave up waiting for its reducers (the low bits
@@ -78,6 +80,15 @@ struct BandArgs {
 constexpr int kBandStatusTimeout = 1 << 30;
 // Reducer workgroups of a fused launch: items (profile blocks + the cost) per workgroup.
 constexpr int kBandRedItems = 2;
+// The fused launch's hand-off is per column of K2's banded layout: one readiness counter per
+// column that K2 writes (top columns 0 .. m + s - 1, then bottom columns 0 .. nb - 1: F counters)
+// and one for the cost, each on a 128-byte line of its own (kBandRedShardStride words).  A reducer
+// item counts itself in its column's counter; the solver starts loading a column as soon as its
+// counter holds the column's item count (col_need), so the prologue's loads overlap the slower
+// reducers instead of waiting for the last one.  (One counter for all took the 178 arrivals of
+// cfg3 one after another at the memory side: MI355X_MICROARCH.md, fanin row.)
+constexpr int kBandRedShardStride = 32;
+inline size_t band_col_count_bytes(int F) { return (size_t)(F + 1) * kBandRedShardStride * 4; }
 inline int band_fused_workgroups(int nprof) { return (nprof + 1 + kBandRedItems - 1) / kBandRedItems; }
 
 // Doubles per ring slot / factor record: (w + 1) blocks of 36, the rhs row (6) and the

@@ -226,6 +226,12 @@ __device__ __forceinline__ void band_reduce_wg(const BandArgs& B, int r, double*
   int2 o = make_int2(0, 0);
   double2 ps = make_double2(0.0, 0.0);
   double pb = 0.0, c = 0.0;
+#if VO_BA_STAMPS  // diagnostic build: reducer r's realtime stamps (start, loads in, stored, counted)
+  unsigned long long* rst = B.stamps ? B.stamps + 8 * kBandStamps + 8 + 4 * r : nullptr;
+  if (rst && tid == 0) rst[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+  // the readiness counter this item counts itself in (loaded beside its meta: no extra latency)
+  const int col = isblk ? B.red_col[blk] : B.F;
   if (isblk) {
     m = A.meta[blk];
     o = A.out[blk];
@@ -248,6 +254,9 @@ __device__ __forceinline__ void band_reduce_wg(const BandArgs& B, int r, double*
     cpart[t] = c;
   }
   __syncthreads();
+#if VO_BA_STAMPS
+  if (rst && tid == 0) rst[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (isblk && !failed) {
     const bool diag = m.z >= 0;
     if (t < 36) {
@@ -263,40 +272,72 @@ __device__ __forceinline__ void band_reduce_wg(const BandArgs& B, int r, double*
       st_sc1(A.sys + o.y + e, acc);
     }
   }
-  for (int mm = kRedThreads / 2; mm > 0; mm >>= 1) {  // the cost: K2's tree (barriers uniform)
-    if (iscost && t < mm) cpart[t] += cpart[t + mm];
-    __syncthreads();
-  }
+  // the cost: K2's tree, in the one workgroup that holds the cost item (uniform per workgroup)
+  if (A.nprof >= kBandRedItems * r && A.nprof < kBandRedItems * (r + 1))
+    for (int mm = kRedThreads / 2; mm > 0; mm >>= 1) {
+      if (iscost && t < mm) cpart[t] += cpart[t + mm];
+      __syncthreads();
+    }
   if (iscost && t == 0 && !failed) st_sc1(A.sys + A.cost_off, cpart[0]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores done
   __syncthreads();
   // one lane counts the workgroup, behind every storing wave's drain: with write-through (sc1)
   // stores and a consumer that reads every handed-off byte by sc1 loads, no release fence
-  // (MI355X_MICROARCH.md, inter-workgroup visibility, hand-off table row 1; a fence here cost
-  // each reducer ~1.7 us of write-back on the solver's path)
-  if (tid == 0) __hip_atomic_fetch_add((gu32*)B.red_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // (MI355X_MICROARCH.md, inter-workgroup visibility, hand-off table row 1, a sharded counter;
+  // a fence here cost each reducer ~1.7 us of write-back on the solver's path)
+  // lane 0 of each half counts its item in its column's counter, behind the barrier that follows
+  // every storing wave's drain (the column's consumer loads only what the items it counted stored)
+#if VO_BA_STAMPS
+  if (rst && tid == 0) rst[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (t == 0 && (isblk || iscost)) {
+    const unsigned v = __hip_atomic_fetch_add((gu32*)(B.red_count + kBandRedShardStride * col), 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+#if VO_BA_STAMPS
+    if (rst && tid == 0) rst[3] = __builtin_amdgcn_s_memrealtime() + (v & 0);
+#endif
+    (void)v;
+  }
 }
 
-// Solver side of the fused launch: one lane polls red_count (relaxed sc1 loads, s_sleep between
-// reads, bounded) and takes nred off it; every wave waits at the barrier for it.  No acquire:
-// every load of sys after it is an sc1 load (sys_ld), as the hand-off row requires.  Returns
-// false on a timeout (then sys is not read: the solve reports "failed").
-__device__ __forceinline__ bool band_wait_reduced(const BandArgs& A, int tid, int* s_flag) {
-  if (tid == 0) {
-    int ok = 1;
-    unsigned spins = 0;
-    while (__hip_atomic_load((gu32*)A.red_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)A.nred) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 22)) {  // seconds (a reducer never arrived): fail, do not hang
-        ok = 0;
-        break;
-      }
-    }
-    if (ok) __hip_atomic_fetch_sub((gu32*)A.red_count, (unsigned)A.nred, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *s_flag = ok;
+// Solver side of the fused launch: a column's readiness.  The polling wave (every lane the same
+// address: wave-uniform c) reads the column's counter by relaxed sc1 loads, s_sleep between
+// reads, bounded, until it holds col_need[c]; then takes the count back off (zero between
+// launches).  No acquire: every load of sys is an sc1 load (SysLoads), and a wave loads a column
+// only after its own poll of that column matched; other waves read the column from LDS after a
+// workgroup barrier (MI355X_MICROARCH.md, hand-off table row 1, one counter per column).
+// Returns false on a timeout (the solve then reports "failed" and reads nothing it depends on).
+__device__ __forceinline__ bool band_col_wait(const BandArgs& A, int c) {
+  const unsigned need = (unsigned)A.col_need[c];
+  if (need == 0) return true;
+  gu32* cnt = (gu32*)(A.red_count + kBandRedShardStride * c);
+  unsigned spins = 0;
+  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 22)) return false;  // seconds (a reducer never arrived): fail, do not hang
   }
-  __syncthreads();
-  return *s_flag != 0;
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_sub(cnt, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+// Columns [c0, c1) at once, one lane each (64 per round): the loader's check of the columns after
+// the prologue's (by step 0 their reducers are long done).  Wave-uniform loop.
+__device__ __forceinline__ bool band_cols_wait(const BandArgs& A, int c0, int c1) {
+  const int lane = threadIdx.x & 63;
+  for (int b = c0; b < c1; b += 64) {
+    const int c = b + lane;
+    const bool on = c < c1;
+    const unsigned need = on ? (unsigned)A.col_need[c] : 0u;
+    gu32* cnt = (gu32*)(A.red_count + kBandRedShardStride * (on ? c : 0));
+    unsigned spins = 0;
+    for (;;) {
+      const unsigned v = need ? __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      if (__builtin_amdgcn_ballot_w64(v < need) == 0) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) return false;
+    }
+    if (need) __hip_atomic_fetch_sub(cnt, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return true;
 }
 
 // The solver reads sys (written by the fused launch's reducers, or by K2) only by sc1 buffer
@@ -336,7 +377,6 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     band_reduce_wg(A, blockIdx.x - 1, dyn);
     return;
   }
-  __shared__ int s_red;
   // CS: doubles per column (K2 layout, factor record; full mode: SS == CS); SS per slot (ring mode: whole 1 KiB
   // pieces), RC slots per side (band_lds_layout)
   const int F = A.F, w = A.w, R = w + 1, CS = 36 * R + 12, CSP = (CS + 127) / 128 * 128;
@@ -369,15 +409,104 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // the poses for the tail's update, staged now (their load latency under the prologue's,
   // or under the wait for the fused launch's reducers)
   for (int e = tid; e < 12 * A.n_poses; e += kBandThreads) pose_l[e] = A.pose_cur[e];
-  // fused K2: sys is read only after every reducer workgroup has published it; a timeout
-  // fails the solve (status) without reading it
-  const bool reduced = A.nred > 0 ? band_wait_reduced(A, tid, &s_red) : true;
-  const bool prior_fail = prior_status || !reduced;
-  if (tid == 0) {
-    s_fail = prior_fail ? 1 : 0;
-    if (A.cost_out && reduced) *A.cost_out = kFull ? sysl.ld(A.cost_off) : A.sys[A.cost_off];
+  // fused K2 (one rank): sys is read column by column, each after its reducers have counted
+  // themselves (band_col_wait); a timeout fails the solve (status) without using what was read
+  const bool fused = kFull && A.nred > 0;
+  __shared__ int s_late;  // a column's reducers never arrived
+  if (fused) {
+    if (tid == 0) s_late = 0;
+    __syncthreads();
   }
-  {
+#if VO_BA_STAMPS
+  unsigned long long* sst = A.stamps ? A.stamps + 8 * kBandStamps : nullptr;
+  if (sst && tid == 0) sst[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (fused) {
+    // Prologue of a fused launch: the prologue columns (top 0 .. nTc - 1, then bottom 0 .. nBc -
+    // 1) are dealt to the waves, column pc to wave pc mod 8; a wave issues a column's loads as soon
+    // as that column's counter is full, keeping every issued column in flight while it polls the
+    // next, so the loads overlap the later reducers.  Each loader wave then checks the rest of
+    // its side's columns (the top one also the cost, which it hands to cost_out) -- their first
+    // loads follow at step 0 -- and every wave stores its columns into the rings.
+    const int nTc = min(w + 2, ncolT), nBc = min(w + 2, ncolB), np = nTc + nBc;
+    static_assert(36 * (kBandMaxW + 1) + 12 <= 2 * 3 * 64, "three 16-byte pieces per lane and column");
+    static_assert(2 * (kBandMaxW + 2) <= 3 * kBandWaves, "three prologue columns per wave");
+    double2 pv[3][3];
+    bool ok = true;
+    // this wave's prologue columns u = 0..2 (pc = wave + 8 u): side, column and counter (-1: a
+    // bottom separator column, which K2 does not write: no wait)
+    int uc[3], ucid[3];
+    bool utop[3];
+    unsigned pend = 0;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int pc = wave + kBandWaves * u;
+      utop[u] = pc < nTc;
+      uc[u] = utop[u] ? pc : pc - nTc;
+      ucid[u] = pc >= np ? -1 : utop[u] ? uc[u] : (uc[u] < nb ? ncolT + uc[u] : -1);
+      if (pc < np) pend |= 1u << u;
+    }
+    auto issue = [&](int u) __attribute__((always_inline)) {
+      const long base = (utop[u] ? 0 : (long)ncolT * CS) + (long)uc[u] * CS;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int piece = lane + 64 * t;
+        pv[u][t] = sysl.ld2(base + 2 * (long)min(piece, CS / 2 - 1));
+      }
+    };
+    // one poll of every pending column per round (lane u polls column u), the loads of each
+    // column issued in the round its counter is found full: the first columns' loads overlap the
+    // wait for the slower reducers, and the wave pays one round trip, not one per column
+    unsigned spins = 0;
+    while (pend) {
+      const int cid = lane == 0 ? ucid[0] : lane == 1 ? ucid[1] : lane == 2 ? ucid[2] : -1;
+      const bool mine = lane < 3 && ((pend >> lane) & 1u);
+      const unsigned need = mine && cid >= 0 ? (unsigned)A.col_need[cid] : 0u;
+      gu32* cnt = (gu32*)(A.red_count + kBandRedShardStride * (cid >= 0 ? cid : 0));
+      const unsigned v = need ? __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      const unsigned ready = (unsigned)__builtin_amdgcn_ballot_w64(lane < 3 && v >= need) & pend;
+      if (ready & 1u) issue(0);
+      if (ready & 2u) issue(1);
+      if (ready & 4u) issue(2);
+      if (mine && need && ((ready >> lane) & 1u))
+        __hip_atomic_fetch_sub(cnt, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pend &= ~ready;
+      if (pend) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) {  // seconds (a reducer never arrived): fail, do not hang
+          ok = false;
+          break;
+        }
+      }
+    }
+    if (role == kLoad && ok) {
+      ok = sbot ? band_cols_wait(A, ncolT + nBc, ncolT + nb) : band_cols_wait(A, nTc, ncolT);
+      if (!sbot && ok) {
+        ok = band_col_wait(A, F);  // the cost
+        if (ok && lane == 0 && A.cost_out) *A.cost_out = sysl.ld(A.cost_off);
+      }
+    }
+    if (!ok && lane == 0) s_late = 1;
+    BST(15);
+#if VO_BA_STAMPS
+    if (sst && tid == 0) sst[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int pc = wave + kBandWaves * u;
+      if (pc < np) {
+        const bool top = pc < nTc;
+        const int c = top ? pc : pc - nTc;
+        double* dst = (top ? ringT : ringB) + c * SS;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int piece = lane + 64 * t;
+          if (piece < CS / 2) *reinterpret_cast<double2*>(dst + 2 * piece) = pv[u][t];
+        }
+      }
+    }
+  } else {
+    if (tid == 0 && A.cost_out) *A.cost_out = A.sys[A.cost_off];
     // Prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every 16-byte
     // load in flight, then the stores.  The loads do not wait for the status word (one
     // global round trip less on the launch's path); a failed earlier solve only skips the
@@ -388,14 +517,9 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     for (int u = 0; u < kProLoads; ++u) {
       const int e = tid + u * kBandThreads;
       const long o2 = e < nT ? e : (long)ncolT * CS / 2 + (e - nT);
-      if constexpr (kFull) {
-        const double2 x = sysl.ld2(2 * o2);
-        v[u] = e < nT + nB ? x : make_double2(0.0, 0.0);
-      } else {
-        v[u] = e < nT + nB ? reinterpret_cast<const double2*>(A.sys)[o2] : make_double2(0.0, 0.0);
-      }
+      v[u] = e < nT + nB ? reinterpret_cast<const double2*>(A.sys)[o2] : make_double2(0.0, 0.0);
     }
-    if (!prior_fail)
+    if (!prior_status)
 #pragma unroll
     for (int u = 0; u < kProLoads; ++u) {
       const int e = tid + u * kBandThreads;
@@ -470,6 +594,13 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   }
   band_barrier();
   BST(0);
+#if VO_BA_STAMPS
+  if (sst && tid == 0) sst[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+  // every wave's polls are behind the barrier: one verdict for the whole solve
+  const bool reduced = !fused || s_late == 0;
+  const bool prior_fail = prior_status || !reduced;
+  if (tid == 0) s_fail = prior_fail ? 1 : 0;
 
   // ---- chain wave: lane 6 g + sr holds row sr of block (k + q, k), q = (g - k) mod R
   const bool act = role == kChain && lane < 6 * R;

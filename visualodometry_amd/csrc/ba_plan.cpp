@@ -5,6 +5,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <exception>
+#include <stdexcept>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -89,6 +90,15 @@ inline void cpu_relax() {
   __builtin_ia32_pause();
 #endif
 }
+// Every spin is bounded: past kSpinYield pauses (tens of microseconds) a waiting caller yields its
+// core on each further check, and a polling worker goes back to its condition variable.  With
+// several ranks per node each sizing its pool to the cgroup quota, an unbounded spinner could hold
+// a core that a throttled or preempted worker needs to finish the item the spinner waits for.
+constexpr long kSpinYield = 1L << 14;
+inline void spin_wait(long& spins) {
+  if (++spins < kSpinYield) cpu_relax();
+  else std::this_thread::yield();
+}
 
 class PlanPool {
  public:
@@ -139,10 +149,12 @@ class PlanPool {
     }
     cv_.notify_all();  // (cheap when every worker is polling: no waiter to wake)
     work();
-    while (ndone_.load(std::memory_order_acquire) < n) cpu_relax();
+    long spins = 0;
+    while (ndone_.load(std::memory_order_acquire) < n) spin_wait(spins);
     // retire: workers inside the job finish their (claimed-nothing) loop; later ones back off
     retired_.store(true, std::memory_order_seq_cst);
-    while (entered_.load(std::memory_order_seq_cst) != 0) cpu_relax();
+    spins = 0;
+    while (entered_.load(std::memory_order_seq_cst) != 0) spin_wait(spins);
     job_ = nullptr;
     if (first) std::rethrow_exception(first);
   }
@@ -180,7 +192,11 @@ class PlanPool {
   void loop() {
     long seen = 0;
     for (;;) {
-      while (session_.load(std::memory_order_acquire) > 0 && gen_.load(std::memory_order_acquire) == seen) cpu_relax();
+      // poll while a plan is being built, for at most kSpinYield pauses, then sleep
+      for (long spins = 0; spins < kSpinYield && session_.load(std::memory_order_acquire) > 0 &&
+                           gen_.load(std::memory_order_acquire) == seen;
+           ++spins)
+        cpu_relax();
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return stop_ || gen_.load(std::memory_order_relaxed) != seen; });
@@ -343,6 +359,7 @@ int seg_obs_grid(int64_t x) {
 void BAPlan::reset() {
   n_poses = n_points = n_obs = n_fixed = n_free = n_te = 0;
   seg_obs = seg_chunks = reused_groups = reused_chunks = 0;
+  host_images_partial = false;
   group_q.clear();
   group_chunk.clear();
   group_seg.clear();
@@ -757,6 +774,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
     if (R.src >= 0) {
       ++P.reused_groups;
       P.reused_chunks += (int)R.chunk_q.size();
+      if (P.chunk_img.get_allocator().pinned && !R.chunk_q.empty()) P.host_images_partial = true;
     }
     for (size_t c = 0; c < R.chunk_q.size(); ++c) {
       const int q = R.chunk_q[c];
@@ -1313,6 +1331,8 @@ void build_profile(BAPlan& P, const std::vector<int32_t>& first, bool step_table
 }
 
 uint64_t plan_digest(const BAPlan& P) {
+  if (P.host_images_partial)
+    throw std::logic_error("plan_digest: the plan's host chunk images are partial (taken over on the device)");
   uint64_t h = 1469598103934665603ull;
   auto bytes = [&](const void* p, size_t n) {
     const unsigned char* c = static_cast<const unsigned char*>(p);

@@ -273,6 +273,11 @@ struct BAPlan {
   // reused_groups / reused_chunks count the groups and chunks taken over.
   std::vector<int32_t> chunk_src;
   int reused_groups = 0, reused_chunks = 0;
+  // true when this plan's host chunk_img holds stale bytes for the chunks it took over: a plan
+  // with page-locked images takes them over on the device only (ba.hip setup), so its host copy
+  // is not the plan a scratch build makes.  plan_digest and any other host reader of chunk_img
+  // refuse such a plan (host-only plans, digests and probes, always copy the images).
+  bool host_images_partial = false;
   // planner scratch (never digested; kept across plans so a session's next window reuses it)
   PlanArr<int32_t> scr_sorted;
   std::shared_ptr<PlanScratch> scratch;  // the planner's working containers (ba_plan.cpp)

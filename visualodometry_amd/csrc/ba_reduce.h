@@ -36,39 +36,59 @@ constexpr int kRedTranspose = 1 << 30;  // dst flag: store the block transposed
 #define VO_RED_BATCH 16
 #endif
 constexpr int kRedBatch = VO_RED_BATCH;
+// Rows per batch: as many as the block's busiest part needs, up to kRedBatch (uniform per block:
+// k0, k1 and stride are).  A batch larger than the rows only adds clamped duplicate loads (each a
+// whole wave-instruction through L1: at cfg3's ~2 rows per part, 16-row batches issued 8x the
+// loads); the sum adds the same rows in the same order either way.
+template <int B, int W>
+__device__ __forceinline__ void sum_rows_b(const double* __restrict__ slab, int k0, int k1, int part, int stride,
+                                           int e, double& acc) {
+  for (int k = k0 + part; k < k1; k += B * stride) {
+    double v[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) v[i] = slab[(long)W * min(k + i * stride, k1 - 1) + e];
+#pragma unroll
+    for (int i = 0; i < B; ++i) acc += k + i * stride < k1 ? v[i] : 0.0;
+  }
+}
 template <int W>
 __device__ __forceinline__ double sum_rows(const double* __restrict__ slab, int k0, int k1, int part,
                                            int stride, int e) {
   double acc = 0.0;
   if (k1 <= k0) return acc;  // no rows (uniform per block)
-  for (int k = k0 + part; k < k1; k += kRedBatch * stride) {
-    double v[kRedBatch];
-#pragma unroll
-    for (int i = 0; i < kRedBatch; ++i) v[i] = slab[(long)W * min(k + i * stride, k1 - 1) + e];
-#pragma unroll
-    for (int i = 0; i < kRedBatch; ++i) acc += k + i * stride < k1 ? v[i] : 0.0;
-  }
+  const int per = (k1 - k0 + stride - 1) / stride;
+  if (per <= 2) sum_rows_b<2, W>(slab, k0, k1, part, stride, e, acc);
+  else if (per <= 4) sum_rows_b<4, W>(slab, k0, k1, part, stride, e, acc);
+  else sum_rows_b<kRedBatch, W>(slab, k0, k1, part, stride, e, acc);
   return acc;
 }
 
 // The same for 36-double S rows with 16-byte loads: lane (part, e2) sums entries 2 e2, 2 e2 + 1
 // of rows k0 + part + j * stride in fixed order (18 lanes cover a row's 288 contiguous bytes).
-__device__ __forceinline__ double2 sum_rows2(const double* __restrict__ slab, int k0, int k1, int part, int stride,
-                                             int e2) {
-  double2 acc = make_double2(0.0, 0.0);
-  if (k1 <= k0) return acc;
-  const double2* __restrict__ s2 = reinterpret_cast<const double2*>(slab);
-  for (int k = k0 + part; k < k1; k += kRedBatch * stride) {
-    double2 v[kRedBatch];
+template <int B>
+__device__ __forceinline__ void sum_rows2_b(const double2* __restrict__ s2, int k0, int k1, int part, int stride,
+                                            int e2, double2& acc) {
+  for (int k = k0 + part; k < k1; k += B * stride) {
+    double2 v[B];
 #pragma unroll
-    for (int i = 0; i < kRedBatch; ++i) v[i] = s2[18l * min(k + i * stride, k1 - 1) + e2];
+    for (int i = 0; i < B; ++i) v[i] = s2[18l * min(k + i * stride, k1 - 1) + e2];
 #pragma unroll
-    for (int i = 0; i < kRedBatch; ++i) {
+    for (int i = 0; i < B; ++i) {
       const bool on = k + i * stride < k1;
       acc.x += on ? v[i].x : 0.0;
       acc.y += on ? v[i].y : 0.0;
     }
   }
+}
+__device__ __forceinline__ double2 sum_rows2(const double* __restrict__ slab, int k0, int k1, int part, int stride,
+                                             int e2) {
+  double2 acc = make_double2(0.0, 0.0);
+  if (k1 <= k0) return acc;
+  const double2* __restrict__ s2 = reinterpret_cast<const double2*>(slab);
+  const int per = (k1 - k0 + stride - 1) / stride;
+  if (per <= 2) sum_rows2_b<2>(s2, k0, k1, part, stride, e2, acc);
+  else if (per <= 4) sum_rows2_b<4>(s2, k0, k1, part, stride, e2, acc);
+  else sum_rows2_b<kRedBatch>(s2, k0, k1, part, stride, e2, acc);
   return acc;
 }
 

@@ -34,11 +34,6 @@
 #ifndef VO_MATCH_PRIO
 #define VO_MATCH_PRIO 0
 #endif
-// Timing-only builds (results wrong): 1 replaces the top-2 epilogue by one op per pair,
-// 2 skips the MFMAs (the epilogue runs on the B fragments)
-#ifndef VO_MATCH_EXP
-#define VO_MATCH_EXP 0
-#endif
 
 namespace vo {
 namespace {
@@ -136,7 +131,13 @@ struct PackSide {
 
 __global__ __launch_bounds__(256) void pack_kernel(PackSide sa, PackSide sb, int dim, int Dp,
                                                    int vec4, uint32_t* __restrict__ flag,
-                                                   uint32_t gen) {
+                                                   uint32_t gen, const uint32_t* __restrict__ qflag) {
+  // a cached query side (sa.wgs == 0; packed by an earlier call into its own buffers): its
+  // integer / finiteness verdicts (qflag, 1 = seen) join this call's flag
+  if (qflag && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    if (qflag[0]) flag[0] = gen;
+    if (qflag[1]) flag[1] = gen;
+  }
   const bool is_b = (int)blockIdx.x >= sa.wgs;
   const PackSide P = is_b ? sb : sa;
   const int b = blockIdx.y;
@@ -336,8 +337,7 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
     for (int mt = 0; mt < kMT; ++mt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        a.v[mt] = VO_MATCH_EXP == 2 ? a.v[mt] + f.bf[ks] + afrag[mt][ks]
-                                    : __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], f.bf[ks], a.v[mt], 0, 0, 0);
+        a.v[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[mt][ks], f.bf[ks], a.v[mt], 0, 0, 0);
     if (kMatchPrio) __builtin_amdgcn_s_setprio(0);
     return a;
   };
@@ -346,10 +346,6 @@ __device__ __forceinline__ void sweep_i8(const MatchArgs& p) {
     for (int mt = 0; mt < kMT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (VO_MATCH_EXP == 1) {  // timing only: one op per pair instead of the top-2 update
-          m1[mt][r] ^= (uint32_t)a.v[mt][r];
-          continue;
-        }
         const uint32_t p = ((uint32_t)a.v[mt][r] << 9) + ccol;
         m2[mt][r] = med3_u32(m1[mt][r], m2[mt][r], p);
         m1[mt][r] = max(m1[mt][r], p);
@@ -688,9 +684,30 @@ int pow2_floor(int x) {
 
 }  // namespace
 
+// Packs one query side (batch 1) into the cache's own buffers, with its own flag words
+// (generation 1: [0] = 1 if a value is not an integer in [0, 255], [1] = 1 if one is not finite).
+void match_pack_query(vo_ctx* ctx, const float* d_des0, int n0, int dim, MatchQueryCache& qc) {
+  hipStream_t st = ctx->stream;
+  const int Dp = ceil_div(dim, kKStep) * kKStep;
+  const int n0_pad = ceil_div(std::max(n0, 1), kRowsPerWG) * kRowsPerWG;
+  qc.q8.reserve((size_t)n0_pad * Dp);
+  qc.norms.reserve((size_t)n0_pad * sizeof(int));
+  qc.flag.reserve(2 * sizeof(uint32_t));
+  VO_HIP_CHECK(hipMemsetAsync(qc.flag.ptr, 0, 2 * sizeof(uint32_t), st));
+  PackSide pa{d_des0, n0, n0_pad, ceil_div((int64_t)n0_pad * 16, 256), (long)n0 * dim, (long)n0_pad * Dp,
+              qc.q8.as<int8_t>(), qc.norms.as<int>(), nullptr};
+  PackSide pb{nullptr, 0, 0, 0, 0, 0, nullptr, nullptr, nullptr};
+  const int vec4 = dim % 4 == 0 && (uintptr_t)d_des0 % 16 == 0;
+  ctx->prof.begin(st, kKMatchPack);
+  hipLaunchKernelGGL(pack_kernel, dim3(pa.wgs, 1), dim3(256), 0, st, pa, pb, dim, Dp, vec4, qc.flag.as<uint32_t>(),
+                     1u, (const uint32_t*)nullptr);
+  ctx->prof.end(st);
+  VO_HIP_CHECK(hipGetLastError());
+}
+
 void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch, int n0,
                int n1, int dim, double ratio, int32_t* d_best, int32_t* d_idx2,
-               float* d_dist2) {
+               float* d_dist2, const MatchQueryCache* qc) {
   VO_REQUIRE(batch >= 1 && n0 >= 0 && n1 >= 0 && dim >= 1, VO_ERR_ARG,
              "match: bad shape batch=%d n0=%d n1=%d dim=%d", batch, n0, n1, dim);
   if (n0 == 0) return;
@@ -756,27 +773,30 @@ void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch,
     return;
   }
   if (int_ok && !float_hint) {
+    // a cached query side (batch 1: match_pack_query packed it for an earlier call) is read
+    // from the cache's buffers; only the train side is packed
+    const bool cached = qc != nullptr && batch == 1;
     a.qa_bstride = (long)n0_pad * Dp;
     a.qb_bstride = (long)n1_pad * Dp;
     ws.q8.reserve((size_t)batch * (a.qa_bstride + a.qb_bstride));
     ws.norms.reserve((size_t)batch * (n0_pad + n1_pad) * sizeof(int));
     ws.colconst.reserve((size_t)batch * n1_pad * sizeof(uint32_t));
-    int8_t* qa = ws.q8.as<int8_t>();
-    int8_t* qb = qa + batch * a.qa_bstride;
-    int* na = ws.norms.as<int>();
-    int* nb = na + (size_t)batch * n0_pad;
+    int8_t* qa = cached ? qc->q8.as<int8_t>() : ws.q8.as<int8_t>();
+    int8_t* qb = ws.q8.as<int8_t>() + batch * a.qa_bstride;
+    int* na = cached ? qc->norms.as<int>() : ws.norms.as<int>();
+    int* nb = ws.norms.as<int>() + (size_t)batch * n0_pad;
     a.qa = qa;
     a.qb = qb;
     a.colconst = ws.colconst.as<uint32_t>();
     a.norma = na;
-    PackSide pa{d_des0, n0, n0_pad, ceil_div((int64_t)n0_pad * 16, 256), a.a_bstride,
+    PackSide pa{d_des0, n0, n0_pad, cached ? 0 : ceil_div((int64_t)n0_pad * 16, 256), a.a_bstride,
                 a.qa_bstride, qa, na, nullptr};
     PackSide pb{d_des1, n1, n1_pad, ceil_div((int64_t)n1_pad * 16, 256), a.b_bstride,
                 a.qb_bstride, qb, nb, ws.colconst.as<uint32_t>()};
     const int vec4 = dim % 4 == 0 && (uintptr_t)d_des0 % 16 == 0 && (uintptr_t)d_des1 % 16 == 0;
     ctx->prof.begin(st, kKMatchPack);
     hipLaunchKernelGGL(pack_kernel, dim3(pa.wgs + pb.wgs, batch), dim3(256), 0, st, pa, pb, dim,
-                       Dp, vec4, flag, ws.gen);
+                       Dp, vec4, flag, ws.gen, cached ? qc->flag.as<uint32_t>() : (const uint32_t*)nullptr);
     ctx->prof.end(st);
   }
   auto sweep = [&]() {  // int8 sweep, and the exact fp32 sweep (float calls the shortlist cannot take)

@@ -69,11 +69,6 @@ __device__ __forceinline__ float min_f32(float a, float b) {
 }
 
 // ---- bf16 images, norms ------------------------------------------------------------
-// Timing-only builds (EXTRA=-DVO_FPACK_EXP=n, results wrong): 1 no max-|b| atomic, 2 no bf16
-// stores, 3 every thread loads the same 64 bytes.
-#ifndef VO_FPACK_EXP
-#define VO_FPACK_EXP 0
-#endif
 // 16 threads per row, 8 consecutive elements per thread and step.  Rows past n are
 // written as zeros (train padding rows get |b'|^2 = +inf: never a candidate).
 __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int v4) {
@@ -96,7 +91,7 @@ __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int 
     const float* s0 = (is_b ? p.db + b * p.b_bstride : p.da + b * p.a_bstride) + (long)min(row, n - 1) * p.dim;
     const int k0 = 8 * sub, k1 = k0 + 128;
     const bool g0 = in && k0 < p.Dp, g1 = in && k1 < p.Dp;
-    const float4* q = reinterpret_cast<const float4*>(VO_FPACK_EXP == 3 ? (const float*)p.nbq : s0);
+    const float4* q = reinterpret_cast<const float4*>(s0);
     const float4 x0 = q[min(k0, p.Dp - 8) / 4], x1 = q[min(k0, p.Dp - 8) / 4 + 1];
     const float4 x2v = q[min(k1, p.Dp - 8) / 4], x3 = q[min(k1, p.Dp - 8) / 4 + 1];
     const float vv[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
@@ -115,7 +110,7 @@ __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int 
         x2 = fmaf(v, v, x2);
         nonfinite |= !isfinite(v);
       }
-      if ((gi == 0 ? g0 : g1) && VO_FPACK_EXP != 2) *reinterpret_cast<v8bf*>(dst + (gi == 0 ? k0 : k1)) = h;
+      if (gi == 0 ? g0 : g1) *reinterpret_cast<v8bf*>(dst + (gi == 0 ? k0 : k1)) = h;
     }
     // the row's 16 lanes: quad_perm xor 1, xor 2, then row_half_mirror and row_mirror (every
     // lane ends with the row sum; a fixed order, inside the bound's summation allowance)
@@ -178,7 +173,7 @@ __global__ __launch_bounds__(256) void fpack_kernel(ShortArgs p, int a_wgs, int 
   __syncthreads();
   if (threadIdx.x == 0) {
     m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-    if (m && VO_FPACK_EXP != 1) atomicMax(p.bmax + kBmaxStride * b, m);
+    if (m) atomicMax(p.bmax + kBmaxStride * b, m);
   }
 }
 
@@ -404,11 +399,6 @@ __device__ __forceinline__ float chain_regs(const float* x, const float* y, int 
   return acc;
 }
 
-// Timing-only builds (EXTRA=-DVO_RERANK_EXP=n, results wrong): 1 no chains, 2 chains without
-// the train-row loads, 3 the loads without the chains.
-#ifndef VO_RERANK_EXP
-#define VO_RERANK_EXP 0
-#endif
 // Exact chains of the wave's (up to) 64 candidates, candidate c0 + lane, with the train rows
 // staged through LDS: a span of kRerankSpan elements of 16 rows per load instruction (4
 // lanes x 16 bytes per row: 16 x 64 contiguous bytes, not 64 rows' scattered 16 bytes), every
@@ -439,15 +429,13 @@ __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const
     if (h + kRerankSpan <= dim) {  // a whole span (uniform): unconditional loads
 #pragma unroll
       for (int t = 0; t < kSpanF4; ++t)
-        v[t] = VO_RERANK_EXP != 2 ? reinterpret_cast<const float4*>(B + (long)jrow[t] * dim)[k4]
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[t] = reinterpret_cast<const float4*>(B + (long)jrow[t] * dim)[k4];
       return;
     }
     const bool in = 4 * k4 < dim;
 #pragma unroll
     for (int t = 0; t < kSpanF4; ++t)
-      v[t] = in && VO_RERANK_EXP != 2 ? reinterpret_cast<const float4*>(B + (long)jrow[t] * dim)[k4]
-                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[t] = in ? reinterpret_cast<const float4*>(B + (long)jrow[t] * dim)[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   auto consume = [&](int h, const float4 (&v)[kSpanF4], float& acc) __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();  // every lane's reads of the previous span are done (in-order LDS)
@@ -484,15 +472,6 @@ __device__ __forceinline__ float chain_staged(const float* __restrict__ B, const
     }
   };
   float acc = 0.0f;
-  if (VO_RERANK_EXP == 3) {  // timing only: the loads, no staging or chain
-    float4 v[kSpanF4];
-    for (int h = 0; h < dim; h += kRerankSpan) {
-      fetch(h, v);
-#pragma unroll
-      for (int t = 0; t < kSpanF4; ++t) acc += v[t].x;
-    }
-    return acc;
-  }
   float4 v0[kSpanF4], v1[kSpanF4], v2[kSpanF4];
   fetch(0, v0);
   if (kRerankSpan < dim) fetch(kRerankSpan, v1);
@@ -653,7 +632,7 @@ __global__ __launch_bounds__(256, VO_RERANK_WGS) void frerank_kernel(ShortArgs p
       // wave w takes candidates 64 (w + 4 q) + lane (the loop bound is wave-uniform)
       const int wv = tid >> 6;
       for (int c0 = 64 * wv; wv < kChainWaves && c0 < total; c0 += 64 * kChainWaves) {
-        const float d = VO_RERANK_EXP == 1 ? 0.0f : chain_staged(B, sq, slist, scol, sbuf[wv], c0, total, p.dim);
+        const float d = chain_staged(B, sq, slist, scol, sbuf[wv], c0, total, p.dim);
         const int c = c0 + (tid & 63);
         if (c < total) skey[c] = key64s(__float_as_uint(sqrtf_rn2(d)), (uint32_t)scol[c]);
       }

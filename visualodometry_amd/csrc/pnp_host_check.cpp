@@ -1,7 +1,8 @@
 // Runs the PnP kernels' scalar math (pnp_math.h) on the host, for
 // tests/test_pnp_host_math.py to compare with oracle/pnp_ref.py without a GPU.
 // Diagnostic build only: never part of libvo_hip.so.
-//   pnp_host_check in.bin out.bin        per hypothesis (what pnp_hyp_kernel computes)
+//   pnp_host_check [steps] in.bin out.bin   per hypothesis (what pnp_hyp_kernel computes; steps: the
+//                                        12 x 12 SVD in the lane-group kernel's step order)
 // in:  int32 count, double K[4] (fu, fv, uc, vc), then count x (pw[5][3], us[5][2]) doubles
 // out: count x (R[9] of EPnP, t[3], rvec[3], Rm[9] = Rodrigues(rvec), ok) doubles
 //   pnp_host_check full in.bin out.bin   one frame through the three kernels' logic, with
@@ -160,8 +161,11 @@ int run_full(const char* in_path, const char* out_path) {
 
 int main(int argc, char** argv) {
   if (argc == 4 && std::string(argv[1]) == "full") return run_full(argv[2], argv[3]);
-  if (argc != 3) {
-    std::fprintf(stderr, "usage: %s in.bin out.bin\n", argv[0]);
+  // "steps": EPnP's 12 x 12 SVD in the lane-group kernel's step order (Jacobi12Steps)
+  const bool steps = argc == 4 && std::string(argv[1]) == "steps";
+  if (steps) ++argv;
+  else if (argc != 3) {
+    std::fprintf(stderr, "usage: %s [steps] in.bin out.bin\n", argv[0]);
     return 2;
   }
   FILE* fi = std::fopen(argv[1], "rb");
@@ -184,7 +188,7 @@ int main(int argc, char** argv) {
       for (int c = 0; c < 2; ++c) S.us[p][c] = src[15 + 2 * p + c];
     }
     double R[3][3], t[3], rv[3], Rm[3][3];
-    const bool ok = epnp5(S, K, R, t);
+    const bool ok = steps ? epnp5(S, K, R, t, Jacobi12Steps{}) : epnp5(S, K, R, t);
     rodrigues_to_vec(R, rv);
     rodrigues_to_mat(rv, Rm);
     double* dst = &out[(size_t)h * 25];

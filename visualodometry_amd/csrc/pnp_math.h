@@ -31,8 +31,54 @@ struct Cam {
 };
 
 // ---------------------------------------------------------------- Jacobi SVD
+// One pair (i, j) of JacobiSVDImpl_'s cyclic sweep (OpenCV core/lapack.cpp) on rows ai, aj of
+// A and their squared norms wi, wj: rotates both rows when they are not yet orthogonal to
+// eps and returns the rotation (c, s) through c_out / s_out.  jacobi_rows runs the pairs in
+// the reference's order; pnp.hip's group kernel runs the same pairs on several lanes in an
+// order that applies the same rotations to every row in the same sequence (bitwise equal).
+template <int M>
+VO_HD bool jacobi_pair(double* ai_row, double* aj_row, double& wi, double& wj, double& c_out, double& s_out) {
+  constexpr double eps = 10.0 * kDblEps;
+  const double a = wi, b = wj;
+  double p = 0.0;
+#pragma unroll
+  for (int k = 0; k < M; ++k) p = p + ai_row[k] * aj_row[k];
+  if (fabs(p) <= eps * sqrt(a * b)) return false;
+  p = p * 2.0;
+  // hypot(p, beta) from correctly rounded ops only, as the oracle: bitwise reproducible
+  const double beta = a - b, gamma = sqrt(p * p + beta * beta);
+  // the reference's two branches as one (same operations on the same operands), so a
+  // wave whose lanes disagree on the sign of beta runs one division chain, not both:
+  //   beta < 0: delta = (gamma - beta) * 0.5, s = sqrt(delta / gamma), c = p / (gamma * s * 2)
+  //   else:     c = sqrt((gamma + beta) / (gamma * 2)),                s = p / (gamma * c * 2)
+  const bool neg = beta < 0;
+  const double num = neg ? (gamma - beta) * 0.5 : gamma + beta;
+  const double den = neg ? gamma : gamma * 2.0;
+  const double x = sqrt(num / den);
+  const double y = p / (gamma * x * 2.0);
+  const double c = neg ? y : x, s = neg ? x : y;
+  double na = 0.0, nb = 0.0;
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const double ai = ai_row[k], aj = aj_row[k];
+    const double t0 = c * ai + s * aj;
+    const double t1 = -s * ai + c * aj;
+    ai_row[k] = t0;
+    aj_row[k] = t1;
+    na = na + t0 * t0;
+    nb = nb + t1 * t1;
+  }
+  wi = na;
+  wj = nb;
+  c_out = c;
+  s_out = s;
+  return true;
+}
+
 // JacobiSVDImpl_ (OpenCV core/lapack.cpp) on the rows of A (rotated in place): W[i] ends
-// as the norm of row i (unsorted); Vt accumulates the rotations when WANT_V.
+// as the norm of row i (unsorted); Vt accumulates the rotations when WANT_V.  (The pair body is
+// jacobi_pair's, operation for operation, written out here: passed row pointers, the compiler
+// kept more of the batch kernel's state in scratch.)
 template <int N, int M, bool WANT_V>
 VO_HD void jacobi_rows(double (&A)[N][M], double (&W)[N], double (&Vt)[N][N]) {
   constexpr double eps = 10.0 * kDblEps;
@@ -60,12 +106,7 @@ VO_HD void jacobi_rows(double (&A)[N][M], double (&W)[N], double (&Vt)[N][N]) {
         for (int k = 0; k < M; ++k) p = p + A[i][k] * A[j][k];
         if (!(fabs(p) <= eps * sqrt(a * b))) {
           p = p * 2.0;
-          // hypot(p, beta) from correctly rounded ops only, as the oracle: bitwise reproducible
           const double beta = a - b, gamma = sqrt(p * p + beta * beta);
-          // the reference's two branches as one (same operations on the same operands), so a
-          // wave whose lanes disagree on the sign of beta runs one division chain, not both:
-          //   beta < 0: delta = (gamma - beta) * 0.5, s = sqrt(delta / gamma), c = p / (gamma * s * 2)
-          //   else:     c = sqrt((gamma + beta) / (gamma * 2)),                s = p / (gamma * c * 2)
           const bool neg = beta < 0;
           const double num = neg ? (gamma - beta) * 0.5 : gamma + beta;
           const double den = neg ? gamma : gamma * 2.0;
@@ -107,6 +148,44 @@ VO_HD void jacobi_rows(double (&A)[N][M], double (&W)[N], double (&Vt)[N][N]) {
     W[i] = sqrt(sd);
   }
 }
+
+// The pairs of one cyclic sweep of an N-row jacobi_rows in steps: step t holds the pairs (i, j)
+// with i + j == t.  A pair touching row i or j precedes (i, j) in the cyclic order exactly when
+// its index sum is below i + j, and the pairs of one step are disjoint, so running the steps in
+// order (the pairs of a step in any order, or at once) applies every row's rotations in the
+// cyclic order: bitwise jacobi_rows.  The host restatement of pnp.hip's lane-group SVD
+// (tests/test_pnp_host_math.py runs EPnP with it against the oracle).
+struct Jacobi12Steps {
+  VO_HD void operator()(double (&A)[12][12], double (&W)[12], double (&)[12][12]) const {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      double sd = 0.0;
+      for (int k = 0; k < 12; ++k) sd = sd + A[i][k] * A[i][k];
+      W[i] = sd;
+    }
+    for (int sweep = 0; sweep < 30; ++sweep) {
+      bool changed = false;
+      for (int t = 1; t <= 21; ++t)
+        for (int i = t - 11 > 0 ? t - 11 : 0; i < t - i; ++i) {
+          double c, s;
+          changed |= jacobi_pair<12>(A[i], A[t - i], W[i], W[t - i], c, s);
+        }
+      if (!changed) break;
+    }
+    for (int i = 0; i < 12; ++i) {
+      double sd = 0.0;
+      for (int k = 0; k < 12; ++k) sd = sd + A[i][k] * A[i][k];
+      W[i] = sqrt(sd);
+    }
+  }
+};
+
+// The 12 x 12 SVD of EPnP's M^T M as jacobi_rows runs it (host check and the batch kernel).
+struct Jacobi12Serial {
+  VO_HD void operator()(double (&A)[12][12], double (&W)[12], double (&dummy)[12][12]) const {
+    jacobi_rows<12, 12, false>(A, W, dummy);
+  }
+};
 
 // Position of each singular value in the descending order (the selection sort of
 // JacobiSVDImpl_; equal values keep their index order, which the selection sort also
@@ -323,7 +402,8 @@ VO_HD double compute_R_and_t(const EpnpState& S, const Cam& K, const double (&be
 }
 
 // epnp::compute_pose on 5 correspondences.  Returns false for a degenerate subset.
-VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) {
+template <class Svd12>
+VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3], const Svd12& svd12) {
   bool ok = true;
   // choose_control_points: centroid + PCA of the points
   double c0[3] = {0.0, 0.0, 0.0};
@@ -449,7 +529,7 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) 
         for (int b = 0; b < 12; ++b) A[a][b] = A[a][b] + m2[a] * m2[b];
     }
     double W[12], dummy[12][12];
-    jacobi_rows<12, 12, false>(A, W, dummy);  // M^T M is symmetric: its rows are A^T's
+    svd12(A, W, dummy);  // jacobi_rows<12, 12, false>: M^T M is symmetric, its rows are A^T's
     int rk[12];
     desc_rank<12>(W, rk);
     double s[12];
@@ -585,6 +665,10 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) 
 // ---------------------------------------------------------------- Rodrigues
 // Matrix -> vector (calibration.cpp); R's columns are first scaled to unit norm, which is
 // what OpenCV's U Vt re-orthonormalisation does to an already orthonormal R.
+VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) {
+  return epnp5(S, K, R, t, Jacobi12Serial{});
+}
+
 VO_HD void rodrigues_to_vec(const double (&Rin)[3][3], double (&r)[3]) {
   double R[3][3];
 #pragma unroll

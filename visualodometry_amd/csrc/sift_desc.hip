@@ -532,16 +532,11 @@ void sift_desc_kernel(DescArgs A) {
             const float r_rot = (float)j * sin_t + (float)i * cos_t;
             const float rbin = r_rot + (float)(kD / 2) - 0.5f, cbin = c_rot + (float)(kD / 2) - 0.5f;
             const int r = py + i, c = px + j;
-#ifdef VO_DESC_DIAG_NOSAMPLE  // timing-only diagnostic: no gathers, no transcendental math
-            const float w = 1.0f, Ori = (float)(k & 255), Mag = 1.0f;
-            (void)r; (void)c;
-#else
             const float dx = img[(long)r * pitch + c + 1] - img[(long)r * pitch + c - 1];
             const float dy = img[(long)(r - 1) * pitch + c] - img[(long)(r + 1) * pitch + c];
             const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, A.tab.v);
             const float Ori = fast_atan2_deg(dy, dx);
             const float Mag = sqrt_rn(dx * dx + dy * dy);
-#endif
             const float obin = (Ori - ori) * bins_per_rad;
             const float mag = Mag * w;
             o0 = (int)floorf(obin);
@@ -650,11 +645,7 @@ void sift_desc_kernel(DescArgs A) {
         __syncthreads();
         // the owner of list L adds its terms in order.  No barrier follows: the next block
         // writes s_pool, s_lb and s_lt only after two barriers every owner must reach first.
-#ifdef VO_DESC_DIAG_NOCONSUME  // timing-only diagnostic: no list sums
-        if (tid < 0) {
-#else
         if (tid < kLists) {
-#endif
   #pragma unroll
           for (int w = 0; w < kOwn; ++w) {
             const int L = tid + w * kDescThreads;

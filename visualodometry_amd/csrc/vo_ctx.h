@@ -29,6 +29,23 @@ struct MatchWorkspace {
   bool flag_fresh = true;   // flag not yet zeroed
 };
 
+// The matcher's cached query side (vo_match_knn2_ratio_dev / _q with a nonzero tag): the
+// reference matches every frame against the same keyframe (vo.py:64-65), so the keyframe's
+// packed int8 rows, norms and integer verdict are kept across calls.  Keyed on (tag, source
+// pointer, n0, dim, device or host source); host sources also keep their float copy (the
+// exact sweep and the float path read it).
+struct MatchQueryCache {
+  DevBuf des;    // host sources: the query's float32 rows on the device
+  DevBuf q8;     // packed int8 (a - 128) rows (n0_pad x Dp)
+  DevBuf norms;  // int32 squared norms
+  DevBuf flag;   // [0] 1 = a value is not a 0..255 integer, [1] 1 = a value is not finite
+  uint64_t tag = 0;
+  const void* src = nullptr;
+  int n0 = -1, dim = -1;
+  bool device_src = false;
+  bool valid = false;
+};
+
 // PnP-RANSAC workspace (pnp.hip): RANSAC subsets cached per frame layout.
 struct PnpWorkspace {
   DevBuf sub;     // int32 (batch, H, 5) subsets
@@ -88,6 +105,7 @@ struct vo_ctx {
   hipStream_t stream = nullptr;
   int num_cus = 0;
   vo::MatchWorkspace match;
+  vo::MatchQueryCache match_q;
   vo::PnpWorkspace pnp;
   vo::SiftWorkspace sift;
   vo::Profiler prof;
@@ -105,7 +123,8 @@ namespace vo {
 // Matcher entry points (match.hip).
 void match_run(vo_ctx* ctx, const float* d_des0, const float* d_des1, int batch, int n0,
                int n1, int dim, double ratio, int32_t* d_best, int32_t* d_idx2,
-               float* d_dist2);
+               float* d_dist2, const MatchQueryCache* qc = nullptr);
+void match_pack_query(vo_ctx* ctx, const float* d_des0, int n0, int dim, MatchQueryCache& qc);
 void compact_pairs(vo_ctx* ctx, const int32_t* d_best, int n0, int32_t* d_pairs,
                    int32_t* d_count);
 // Triangulation entry point (tri.hip): host matrices, device points.

@@ -218,6 +218,12 @@ def _wrap_init(orig):
         orig(self, *args, **kw)
         _PNP_ON_GPU[0] = bool(getattr(self.cfg, "pnp_on_gpu", True))
         _use_map_store(self)
+        if getattr(self.cfg, "ba_enabled", False):
+            # the BA context pre-sized for a full window (ba_window keyframes, the map's
+            # MAX_POINTS cap, vo.py:38) now, so no keyframe call of the drive pays for it
+            self._vo_amd_ba = SlidingWindowBA(self.K, self.cfg)
+            self._vo_amd_ba.reserve(getattr(self.cfg, "ba_window", 50), MAX_POINTS,
+                                    n_fixed=getattr(self.cfg, "ba_fixed", 2))
 
     __init__._vo_amd_wrapped = orig
     return __init__
@@ -263,6 +269,32 @@ def _wrap_frontend_init(orig):
     return __init__
 
 
+def _wrap_process_image(orig):
+    from .. import sift
+
+    def process_image(self, img):  # FeatureFrontend.process_image, frontend.py:36-75
+        ext = getattr(self, "extractor", None)
+        dev = getattr(self, "device", None)
+        if isinstance(ext, sift.SIFT) and getattr(dev, "type", None) == "cuda" and np.ndim(img) == 2:
+            # the SIFT branch (:51-75) keeps k.pt and the descriptors and moves both to the GPU:
+            # the kernels write them into torch's memory there, no keypoint objects on the host
+            import torch
+
+            r = sift.detect_and_compute_torch(img, ext.nfeatures, ext.contrast, ext.edge, ext.sigma, ext.n_layers,
+                                              device=dev, ctx=ext._ctx or None)
+            if r is not None:
+                pts, des = r
+                return {
+                    "keypoints": pts.unsqueeze(0),  # (1, N, 2)
+                    "descriptors": des.unsqueeze(0),  # (1, N, 128)
+                    "image_size": torch.tensor([(img.shape[1], img.shape[0])]).to(dev),
+                }
+        return orig(self, img)
+
+    process_image._vo_amd_wrapped = orig
+    return process_image
+
+
 def _wrap_match_frames(orig):
     from .. import matcher
 
@@ -270,8 +302,9 @@ def _wrap_match_frames(orig):
         if getattr(self.conf, "extractor_type", None) == "sift" and getattr(self.conf, "match_on_gpu", True):
             # SIFT integers: the int8 path only, hinted for this call (the context's own hint,
             # which other users of the context may rely on, is restored afterwards)
+            # feats0 is the keyframe's (vo.py:64-65): its packed rows stay cached across frames
             return matcher.match_knn2_ratio(feats0["descriptors"], feats1["descriptors"],
-                                            kind=matcher.DESC_SIFT)
+                                            kind=matcher.DESC_SIFT, cache_query=True)
         return orig(self, feats0, feats1)
 
     match_frames._vo_amd_wrapped = orig
@@ -330,6 +363,9 @@ def install(frontend_cls=None, vo_cls=None) -> None:
         frontend_cls.__init__ = _wrap_frontend_init(frontend_cls.__init__)
     if not hasattr(frontend_cls.match_frames, "_vo_amd_wrapped"):
         frontend_cls.match_frames = _wrap_match_frames(frontend_cls.match_frames)
+    pi = getattr(frontend_cls, "process_image", None)
+    if pi is not None and not hasattr(pi, "_vo_amd_wrapped"):
+        frontend_cls.process_image = _wrap_process_image(pi)
     if not hasattr(vo_cls._create_keyframe, "_vo_amd_wrapped"):
         vo_cls._create_keyframe = _wrap_create_keyframe(vo_cls._create_keyframe)
     if not hasattr(vo_cls._reset_system, "_vo_amd_wrapped"):

@@ -31,36 +31,111 @@ def _as_des(d) -> np.ndarray:
     return np.ascontiguousarray(d, dtype=np.float32)
 
 
+class _QueryTags:
+    """Tags for the library's cached query side (``vo_match_knn2_ratio_q`` / ``_dev``).
+
+    A descriptor object gets a tag while it is the cached query: the cache holds a strong
+    reference to it, so neither the object nor its memory can be recycled under the same
+    identity, and torch tensors carry a version counter that every in-place write bumps.  A
+    numpy array has no such counter (a write could go unnoticed), so it is never cached."""
+
+    def __init__(self):
+        self.obj, self.version, self.tag, self.next = None, None, 0, 1
+
+    def tag_for(self, d) -> int:
+        version = getattr(d, "_version", None)
+        if version is None:
+            return 0
+        if d is not self.obj or version != self.version:
+            self.obj, self.version, self.tag = d, version, self.next
+            self.next += 1
+        return self.tag
+
+
+def _tensor_2d(d):
+    """A torch tensor as its (N, D) float32 contiguous view (the feature dict's (1, N, D))."""
+    if d.dim() == 3 and d.shape[0] == 1:
+        d = d[0]
+    if d.dim() != 2:
+        raise ValueError(f"descriptors must be (N, D), got shape {tuple(d.shape)}")
+    return d.detach().float().contiguous()
+
+
 def match_knn2_ratio(des0, des1, ratio: float = RATIO_THRESH, ctx: _lib.Context | None = None,
-                     kind: int | None = None) -> np.ndarray:
+                     kind: int | None = None, cache_query: bool = False) -> np.ndarray:
     """Ratio-test matches as an ``int64`` array ``(M, 2)`` of (query, train), ascending query.
 
     ``kind`` (``DESC_SIFT`` / ``DESC_FLOAT``) is a hint for this call only: the context's own
-    hint (:func:`set_descriptor_kind`) is restored afterwards.  Results never depend on it."""
-    a, b = _as_des(des0), _as_des(des1)
-    if a.shape[0] == 0 or b.shape[0] == 0:  # frontend.py:97-98
-        return np.empty((0, 2), dtype=np.int64)
-    if a.shape[1] != b.shape[1]:
-        raise ValueError(f"descriptor dims differ: {a.shape[1]} vs {b.shape[1]}")
+    hint (:func:`set_descriptor_kind`) is restored afterwards.  Results never depend on it.
+
+    ``cache_query``: ``des0`` is the keyframe side the reference matches every frame against
+    (``vo.py:64-65``): the library keeps its device copy and packed rows across calls while the
+    same unmodified torch tensor comes back.  Torch tensors already on the GPU are read in place
+    (``vo_match_knn2_ratio_dev``: no descriptor crosses PCIe); results never depend on either."""
     ctx = ctx or _lib.context()
-    out = np.empty((a.shape[0], 2), dtype=np.int32)
+    dev = None if getattr(ctx, "_foreign_tensors", False) else _gpu_tensors(des0, des1, ctx)
+    if dev is not None:
+        a, b = dev
+        n0, n1, dim = a.shape[0], b.shape[0], a.shape[1]
+    else:
+        a, b = _as_des(des0), _as_des(des1)
+        n0, n1, dim = a.shape[0], b.shape[0], a.shape[1]
+    if n0 == 0 or n1 == 0:  # frontend.py:97-98
+        return np.empty((0, 2), dtype=np.int64)
+    if dim != b.shape[1]:
+        raise ValueError(f"descriptor dims differ: {dim} vs {b.shape[1]}")
+    tag = _tags(ctx).tag_for(des0) if cache_query else 0
+    out = np.empty((n0, 2), dtype=np.int32)
     cnt = np.zeros(1, dtype=np.int32)
     prior = getattr(ctx, "desc_kind", DESC_AUTO)
     scoped = kind is not None and kind != prior
     if scoped:
         check(ctx.lib.vo_match_hint(ctx.handle, int(kind)), "vo_match_hint")
     try:
-        check(
-            ctx.lib.vo_match_knn2_ratio(
-                ctx.handle, ptr(a, C.c_float), a.shape[0], ptr(b, C.c_float), b.shape[0], a.shape[1],
-                float(ratio), ptr(out, C.c_int32), ptr(cnt, C.c_int32),
-            ),
-            "vo_match_knn2_ratio",
-        )
+        if dev is not None:
+            import torch
+
+            torch.cuda.current_stream(a.device).synchronize()  # the tensors' producer is done
+            rc = ctx.lib.vo_match_knn2_ratio_dev(
+                ctx.handle, C.c_void_p(a.data_ptr()), n0, C.c_uint64(tag), C.c_void_p(b.data_ptr()), n1, dim,
+                float(ratio), ptr(out, C.c_int32), ptr(cnt, C.c_int32))
+            if rc == _lib.VO_ERR_ARG and n0 and n1:
+                # torch's device memory is not this library's HIP runtime's (the library refuses
+                # such pointers before any launch): the host path from here on
+                ctx._foreign_tensors = True
+                return match_knn2_ratio(des0.detach().cpu(), des1.detach().cpu(), ratio, ctx, kind, False)
+            check(rc, "vo_match_knn2_ratio_dev")
+        elif tag:
+            check(ctx.lib.vo_match_knn2_ratio_q(
+                ctx.handle, ptr(a, C.c_float), n0, C.c_uint64(tag), ptr(b, C.c_float), n1, dim, float(ratio),
+                ptr(out, C.c_int32), ptr(cnt, C.c_int32)), "vo_match_knn2_ratio_q")
+        else:
+            check(ctx.lib.vo_match_knn2_ratio(
+                ctx.handle, ptr(a, C.c_float), n0, ptr(b, C.c_float), n1, dim, float(ratio),
+                ptr(out, C.c_int32), ptr(cnt, C.c_int32)), "vo_match_knn2_ratio")
     finally:
         if scoped:
             check(ctx.lib.vo_match_hint(ctx.handle, int(prior)), "vo_match_hint")
     return out[: int(cnt[0])].astype(np.int64)
+
+
+def _tags(ctx) -> _QueryTags:
+    t = getattr(ctx, "_query_tags", None)
+    if t is None:
+        t = ctx._query_tags = _QueryTags()
+    return t
+
+
+def _gpu_tensors(des0, des1, ctx):
+    """Both descriptor sets as (N, D) float32 torch tensors on the context's GPU, or None (host
+    path): only tensors torch already holds on ``cuda:<ctx.device>`` qualify."""
+    if not (hasattr(des0, "is_cuda") and hasattr(des1, "is_cuda")):
+        return None
+    if not (des0.is_cuda and des1.is_cuda):
+        return None
+    if des0.device.index != ctx.device or des1.device.index != ctx.device:
+        return None
+    return _tensor_2d(des0), _tensor_2d(des1)
 
 
 def match_knn2(des0, des1, ctx: _lib.Context | None = None):

@@ -125,6 +125,40 @@ def detect_and_compute(gray, nfeatures: int = 0, contrast: float = 0.04, edge: f
     return _kp_dict(kp[:n], desc[:n].copy())
 
 
+def detect_and_compute_torch(gray, nfeatures: int, contrast: float, edge: float, sigma: float, n_layers: int = 3,
+                             device=None, ctx: _lib.Context | None = None):
+    """``detect_and_compute`` with its outputs in torch tensors on the GPU, as
+    ``FeatureFrontend.process_image`` keeps them (``frontend.py:59-67``: ``k.pt`` and the
+    descriptors, moved to ``config.device``): ``vo_sift_detect_and_compute_dev`` writes them
+    into torch's memory and only the count crosses PCIe.  Returns ``(pts (N, 2), desc (N, 128))``
+    float32 tensors (same values as :func:`detect_and_compute`), or None when the library refuses
+    torch's memory (another HIP runtime instance in the process) or the output would not fit:
+    the caller takes the host path then."""
+    import torch
+
+    ctx = ctx or _lib.context()
+    img = np.ascontiguousarray(np.asarray(gray, dtype=np.uint8))
+    if img.ndim != 2:
+        raise ValueError("detect_and_compute_torch: a single-channel (h, w) uint8 image is expected")
+    h, w = img.shape
+    device = torch.device(device) if device is not None else torch.device("cuda", ctx.device)
+    # retainBest keeps every keypoint tied with the nfeatures-th response: a little headroom
+    cap = nfeatures + nfeatures // 4 + 64 if nfeatures > 0 else 1 << 15
+    kp = torch.empty((cap, 8), dtype=torch.float32, device=device)
+    desc = torch.empty((cap, 128), dtype=torch.float32, device=device)
+    torch.cuda.current_stream(device).synchronize()  # memory torch's stream may still be using
+    cnt = C.c_int32(0)
+    rc = ctx.lib.vo_sift_detect_and_compute_dev(ctx.handle, ptr(img, C.c_uint8), h, w, int(nfeatures),
+                                                float(contrast), float(edge), float(sigma), int(n_layers), int(cap),
+                                                C.c_void_p(kp.data_ptr()), C.c_void_p(desc.data_ptr()),
+                                                C.byref(cnt))
+    if rc == _lib.VO_ERR_ARG:
+        return None
+    check(rc, "vo_sift_detect_and_compute_dev")
+    n = cnt.value
+    return kp[:n, :2].contiguous(), desc[:n]
+
+
 def detect_and_compute_device(d_imgs: _lib.DeviceArray, nfeatures: int, contrast: float, edge: float, sigma: float,
                               n_layers: int, d_kp: _lib.DeviceArray, d_desc: _lib.DeviceArray,
                               d_counts: _lib.DeviceArray, ctx: _lib.Context | None = None) -> None:
