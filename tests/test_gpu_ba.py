@@ -218,6 +218,27 @@ def test_fused_reduce_equals_split_launches(ctx, cfg):
         np.testing.assert_array_equal(a, b)
 
 
+def test_fused_handoff_stress(ctx):
+    """The fused launch's solver reads its reducers' columns without an acquire fence (sc1 loads
+    after its own poll of each column's counter).  A stale line anywhere would change the bits:
+    60 GN iterations of cfg3 (60 launches, each with 178 reducers spread over every XCD) must
+    equal the split launches (K2 on its own, read after a kernel boundary) bit for bit, cost by
+    cost, and the state after them."""
+    p = make_ba_config("cfg3")
+    out = []
+    for split in (False, True):
+        _lib.ba_split_reduce(ctx, split)
+        try:
+            s = _session(p, ctx)
+            rc, costs = s.run(60)
+            assert rc == _lib.VO_OK
+            out.append((costs,) + s.get_state())
+        finally:
+            _lib.ba_split_reduce(ctx, False)
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_run_in_pieces_equals_one_run(ctx):
     p = make_ba_config("cfg2")
     s1 = _session(p, ctx)

@@ -75,4 +75,10 @@ out["match_host_cached_ms"] = timed(lambda: matcher.match_knn2_ratio(c0, d1, ctx
                                                                      cache_query=True))
 X, uv, Kp, _, _ = pnp_case(1000, 5)
 out["pnp_ms"] = timed(lambda: pnp.pnp_ransac(X, uv, Kp, 1.0, ctx=ctx))
+_lib.profile_enable(ctx, True)
+for _ in range(10):
+    pnp.pnp_ransac(X, uv, Kp, 1.0, ctx=ctx)
+prof = _lib.profile_read(ctx)
+_lib.profile_enable(ctx, False)
+out["pnp_kernel_us"] = {k: round(v[0] / v[1] * 1e3, 2) for k, v in prof.items()}
 print(json.dumps(out))

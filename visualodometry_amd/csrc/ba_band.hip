@@ -300,25 +300,13 @@ __device__ __forceinline__ void band_reduce_wg(const BandArgs& B, int r, double*
   }
 }
 
-// Solver side of the fused launch: a column's readiness.  The polling wave (every lane the same
-// address: wave-uniform c) reads the column's counter by relaxed sc1 loads, s_sleep between
-// reads, bounded, until it holds col_need[c]; then takes the count back off (zero between
-// launches).  No acquire: every load of sys is an sc1 load (SysLoads), and a wave loads a column
-// only after its own poll of that column matched; other waves read the column from LDS after a
-// workgroup barrier (MI355X_MICROARCH.md, hand-off table row 1, one counter per column).
-// Returns false on a timeout (the solve then reports "failed" and reads nothing it depends on).
-__device__ __forceinline__ bool band_col_wait(const BandArgs& A, int c) {
-  const unsigned need = (unsigned)A.col_need[c];
-  if (need == 0) return true;
-  gu32* cnt = (gu32*)(A.red_count + kBandRedShardStride * c);
-  unsigned spins = 0;
-  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1u << 22)) return false;  // seconds (a reducer never arrived): fail, do not hang
-  }
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_sub(cnt, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return true;
-}
+// Solver side of the fused launch: a column's readiness.  A polling wave reads the column's
+// counter by relaxed sc1 loads, s_sleep between reads, bounded, until it holds col_need[c]; then
+// takes the count back off (zero between launches).  No acquire: every load of sys is an sc1
+// load (SysLoads), and a wave loads a column only after its own poll of that column matched;
+// other waves read the column from LDS after a workgroup barrier (MI355X_MICROARCH.md,
+// hand-off table row 1, one counter per column).  A timeout fails the solve ("failed"), which
+// then uses nothing it read.
 // Columns [c0, c1) at once, one lane each (64 per round): the loader's check of the columns after
 // the prologue's (by step 0 their reducers are long done).  Wave-uniform loop.
 __device__ __forceinline__ bool band_cols_wait(const BandArgs& A, int c0, int c1) {
@@ -410,7 +398,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // or under the wait for the fused launch's reducers)
   for (int e = tid; e < 12 * A.n_poses; e += kBandThreads) pose_l[e] = A.pose_cur[e];
   // fused K2 (one rank): sys is read column by column, each after its reducers have counted
-  // themselves (band_col_wait); a timeout fails the solve (status) without using what was read
+  // themselves (the prologue's poll loop); a timeout fails the solve (status) without using what was read
   const bool fused = kFull && A.nred > 0;
   __shared__ int s_late;  // a column's reducers never arrived
   if (fused) {
@@ -454,38 +442,43 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
         pv[u][t] = sysl.ld2(base + 2 * (long)min(piece, CS / 2 - 1));
       }
     };
-    // one poll of every pending column per round (lane u polls column u), the loads of each
-    // column issued in the round its counter is found full: the first columns' loads overlap the
-    // wait for the slower reducers, and the wave pays one round trip, not one per column
+    // One poll of every pending column per round -- lane u < 3 this wave's prologue column u, and
+    // on the loader waves lanes 3.. the rest of their side's columns (whose loads follow from step
+    // 0) and, on the top loader, the cost -- so a wave pays one round trip per round, not one per
+    // column; a prologue column's loads are issued in the round its counter is found full, so the
+    // first columns' loads overlap the wait for the slower reducers.
+    const int r0 = sbot ? ncolT + nBc : nTc, r1 = sbot ? ncolT + nb : ncolT;  // the loader's rest
+    const int nrest = role == kLoad ? min(max(r1 - r0, 0), 60) + (sbot ? 0 : 1) : 0;  // + the cost (top)
+    const int lcid = lane < 3 ? (lane == 0 ? ucid[0] : lane == 1 ? ucid[1] : ucid[2])
+                     : lane - 3 < nrest ? (lane - 3 < min(max(r1 - r0, 0), 60) ? r0 + lane - 3 : F) : -1;
+    bool lpend = lcid >= 0 && (lane >= 3 || ((pend >> lane) & 1u));
+    const unsigned need = lpend ? (unsigned)A.col_need[lcid] : 0u;
+    gu32* const cnt = (gu32*)(A.red_count + kBandRedShardStride * (lcid >= 0 ? lcid : 0));
+    if (need == 0) lpend = false;
+    // prologue columns with nothing to wait for (K2 writes no bottom separator column): at once
+    const unsigned waiting = (unsigned)__builtin_amdgcn_ballot_w64(lpend) & 7u;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (((pend >> u) & 1u) && !((waiting >> u) & 1u)) issue(u);
     unsigned spins = 0;
-    while (pend) {
-      const int cid = lane == 0 ? ucid[0] : lane == 1 ? ucid[1] : lane == 2 ? ucid[2] : -1;
-      const bool mine = lane < 3 && ((pend >> lane) & 1u);
-      const unsigned need = mine && cid >= 0 ? (unsigned)A.col_need[cid] : 0u;
-      gu32* cnt = (gu32*)(A.red_count + kBandRedShardStride * (cid >= 0 ? cid : 0));
-      const unsigned v = need ? __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      const unsigned ready = (unsigned)__builtin_amdgcn_ballot_w64(lane < 3 && v >= need) & pend;
-      if (ready & 1u) issue(0);
-      if (ready & 2u) issue(1);
-      if (ready & 4u) issue(2);
-      if (mine && need && ((ready >> lane) & 1u))
-        __hip_atomic_fetch_sub(cnt, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      pend &= ~ready;
-      if (pend) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 22)) {  // seconds (a reducer never arrived): fail, do not hang
-          ok = false;
-          break;
-        }
+    for (;;) {
+      const unsigned v = lpend ? __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      const bool now = lpend && v >= need;
+      const uint64_t nowb = __builtin_amdgcn_ballot_w64(now);
+      if (nowb & 1u) issue(0);
+      if (nowb & 2u) issue(1);
+      if (nowb & 4u) issue(2);
+      if (now) __hip_atomic_fetch_sub(cnt, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lpend = lpend && !now;
+      if (__builtin_amdgcn_ballot_w64(lpend) == 0) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {  // seconds (a reducer never arrived): fail, do not hang
+        ok = false;
+        break;
       }
     }
-    if (role == kLoad && ok) {
-      ok = sbot ? band_cols_wait(A, ncolT + nBc, ncolT + nb) : band_cols_wait(A, nTc, ncolT);
-      if (!sbot && ok) {
-        ok = band_col_wait(A, F);  // the cost
-        if (ok && lane == 0 && A.cost_out) *A.cost_out = sysl.ld(A.cost_off);
-      }
-    }
+    if (role == kLoad && ok && r1 - r0 > 60) ok = band_cols_wait(A, r0 + 60, r1);  // wide windows only
+    if (role == kLoad && !sbot && ok && lane == 0 && A.cost_out) *A.cost_out = sysl.ld(A.cost_off);
     if (!ok && lane == 0) s_late = 1;
     BST(15);
 #if VO_BA_STAMPS
@@ -506,7 +499,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       }
     }
   } else {
-    if (tid == 0 && A.cost_out) *A.cost_out = A.sys[A.cost_off];
+    if (tid == 0 && A.cost_out) *A.cost_out = A.sys[A.cost_off];  // plain-sys-read: not fused
     // Prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every 16-byte
     // load in flight, then the stores.  The loads do not wait for the status word (one
     // global round trip less on the launch's path); a failed earlier solve only skips the
@@ -517,7 +510,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     for (int u = 0; u < kProLoads; ++u) {
       const int e = tid + u * kBandThreads;
       const long o2 = e < nT ? e : (long)ncolT * CS / 2 + (e - nT);
-      v[u] = e < nT + nB ? reinterpret_cast<const double2*>(A.sys)[o2] : make_double2(0.0, 0.0);
+      v[u] = e < nT + nB ? reinterpret_cast<const double2*>(A.sys)[o2] : make_double2(0.0, 0.0);  // plain-sys-read: not fused
     }
     if (!prior_status)
 #pragma unroll
@@ -556,7 +549,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   typedef __attribute__((address_space(3))) void lds_void;
   typedef __attribute__((address_space(1))) const void gbl_void;
   auto dma_col = [&](int v, double* slot) __attribute__((always_inline)) {
-    const double* src = A.sys + sbase + (long)v * CS + 2 * lane;
+    const double* src = A.sys + sbase + (long)v * CS + 2 * lane;  // plain-sys-read: LDS-DMA, not fused (ld_sc1 false)
     for (int t = 0; t < nDma; ++t)
       __builtin_amdgcn_global_load_lds((gbl_void*)(src + 128 * t), (lds_void*)(slot + 128 * t), 16, 0, 0);
   };

@@ -28,6 +28,7 @@
 
 #include "pnp_math.h"
 #include "vo_ctx.h"
+#include "pnp_args.h"
 
 #pragma clang fp contract(off)
 
@@ -53,118 +54,14 @@ constexpr int kScoreWavesPerSimd = kScoreThreads / 64;  // four workgroups per C
 constexpr int kScoreStep = VO_PNP_SCORE_STEP;  // hypotheses scored between two replay steps (pnp_score_kernel)
 constexpr int kSplitMin = 16;        // hypotheses solved for every frame before the replay decides (pnp_run)
 
-struct PnpArgs {
-  const float* X;          // (total, 3) object points, frames back to back
-  const float* uv;         // (total, 2) image points
-  const int32_t* off;      // (batch + 1) frame offsets
-  const int32_t* subsets;  // (batch, H, 5) RANSAC subsets (frames with n > 5)
-  double* models;          // (batch, H, kModel)
-  int32_t* counts;         // (batch, H) inlier counts
-  double* pose;            // (batch, 6) rvec, tvec
-  int32_t* status;         // (batch, 2) success, inliers
-  uint8_t* mask;           // (total) inliers of the best model
-  Cam K;
-  float thr2;              // (float)(reproj_err^2)
-  double confidence;
-  int batch, H;
-};
 
-__device__ __forceinline__ void load3(const float* X, int i, float (&M)[3]) {
-  M[0] = X[3l * i];
-  M[1] = X[3l * i + 1];
-  M[2] = X[3l * i + 2];
-}
 
-// Groups of kGroupLanes lanes per hypothesis (small batches, where one hypothesis per lane
-// leaves the chip idle and the latency of one EPnP chain is the call's): every lane of a group
-// runs the hypothesis's serial parts redundantly (same inputs, same values), and EPnP's 12 x 12
-// Jacobi SVD runs on the group's lanes.  Step t of a sweep takes the pairs (i, j) with i + j == t
-// (at most six, disjoint), one lane each: in the cyclic order JacobiSVDImpl_ runs, every pair
-// touching row i or j comes before (i, j) exactly when its index sum is below i + j, so each row
-// receives the same rotations in the same order, and the result is jacobi_rows' bit for bit.  A
-// sweep is 21 dependent steps instead of 66 pairs.
-constexpr int kGroupLanes = 8;
-constexpr int kSvdDoubles = 12 * 12 + 12;
 
-__device__ __forceinline__ void lds_sync_lanes() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-struct Jacobi12Group {
-  double* A;  // LDS: this group's 12 x 12 rows, then W (12)
-  int r;      // lane in the group
-  __device__ void operator()(double (&Ar)[12][12], double (&Wr)[12], double (&)[12][12]) const {
-    double* W = A + 144;
-    // lane r publishes rows i = r mod 8 (every lane holds the same A; static row indices, the
-    // rows a lane does not own masked) and their squared norms
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      if (i % kGroupLanes == r) {
-        double sd = 0.0;
-#pragma unroll
-        for (int k = 0; k < 12; k += 2) {
-          *reinterpret_cast<double2*>(A + 12 * i + k) = make_double2(Ar[i][k], Ar[i][k + 1]);
-          sd = sd + Ar[i][k] * Ar[i][k];
-          sd = sd + Ar[i][k + 1] * Ar[i][k + 1];
-        }
-        W[i] = sd;
-      }
-    }
-    lds_sync_lanes();
-    const uint64_t gmask = 0xFFull << (threadIdx.x & 56);
-    for (int sweep = 0; sweep < 30; ++sweep) {
-      bool changed = false;
-      for (int t = 1; t <= 21; ++t) {
-        const int i = max(0, t - 11) + r, j = t - i;
-        if (i < j) {
-          double ai[12], aj[12];
-#pragma unroll
-          for (int k = 0; k < 12; k += 2) {
-            const double2 x = *reinterpret_cast<const double2*>(A + 12 * i + k);
-            const double2 y = *reinterpret_cast<const double2*>(A + 12 * j + k);
-            ai[k] = x.x;
-            ai[k + 1] = x.y;
-            aj[k] = y.x;
-            aj[k + 1] = y.y;
-          }
-          double wi = W[i], wj = W[j], c, sn;
-          if (pnpm::jacobi_pair<12>(ai, aj, wi, wj, c, sn)) {
-#pragma unroll
-            for (int k = 0; k < 12; k += 2) {
-              *reinterpret_cast<double2*>(A + 12 * i + k) = make_double2(ai[k], ai[k + 1]);
-              *reinterpret_cast<double2*>(A + 12 * j + k) = make_double2(aj[k], aj[k + 1]);
-            }
-            W[i] = wi;
-            W[j] = wj;
-            changed = true;
-          }
-        }
-        lds_sync_lanes();  // one wave: its LDS operations complete in order
-      }
-      if ((__ballot(changed) & gmask) == 0) break;  // uniform in the group
-    }
-    // the rotated rows back to every lane, W = the row norms (jacobi_rows' last loop)
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      double sd = 0.0;
-#pragma unroll
-      for (int k = 0; k < 12; k += 2) {
-        const double2 x = *reinterpret_cast<const double2*>(A + 12 * i + k);
-        Ar[i][k] = x.x;
-        Ar[i][k + 1] = x.y;
-      }
-#pragma unroll
-      for (int k = 0; k < 12; ++k) sd = sd + Ar[i][k] * Ar[i][k];
-      Wr[i] = sqrt(sd);
-    }
-    lds_sync_lanes();  // the group's next use of its LDS rows comes after every lane's reads
-  }
-};
-
-// Hypotheses [h_lo, h_hi) of every frame (of the frames with need[f] != 0 when need is given):
-// G = 1, one lane per hypothesis (large batches); G = kGroupLanes, one lane group each.
-template <int G>
+// Hypotheses [h_lo, h_hi) of every frame (of the frames with need[f] != 0 when need is given).
 __global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a, int h_lo, int h_hi, const int32_t* need) {
   const int hr = h_hi - h_lo;
-  const int k = (blockIdx.x * 64 + threadIdx.x) / G, r = threadIdx.x % G;
+  const int k = blockIdx.x * 64 + threadIdx.x;
   if (k >= a.batch * hr) return;
   const int f = k / hr, h = h_lo + (k - f * hr);
   if (need && !need[f]) return;
@@ -173,7 +70,7 @@ __global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a, int h_lo, int h_
   double* model = a.models + (size_t)g * kModel;
   const bool run = n > kPts || (n == kPts && h == 0);
   if (!run) {
-    if (r == 0) model[15] = 0.0;
+    model[15] = 0.0;
     return;
   }
   // alphas and v in LDS, one column per lane (one wave per workgroup)
@@ -193,26 +90,18 @@ __global__ __launch_bounds__(64) void pnp_hyp_kernel(PnpArgs a, int h_lo, int h_
     S.us[p][1] = a.uv[2l * i + 1];
   }
   double R[3][3], t[3];
-  bool ok;
-  if constexpr (G == 1) {
-    ok = epnp5(S, a.K, R, t);
-  } else {
-    __shared__ __attribute__((aligned(16))) double s_svd[64 / G][kSvdDoubles];
-    ok = epnp5(S, a.K, R, t, Jacobi12Group{s_svd[threadIdx.x / G], r});
-  }
+  const bool ok = epnp5(S, a.K, R, t);
   double rv[3], Rm[3][3];
   rodrigues_to_vec(R, rv);
   rodrigues_to_mat(rv, Rm);
-  if (r == 0) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 3; ++i) {
 #pragma unroll
-      for (int j = 0; j < 3; ++j) model[3 * i + j] = Rm[i][j];
-      model[9 + i] = t[i];
-      model[12 + i] = rv[i];
-    }
-    model[15] = ok ? 1.0 : 0.0;
+    for (int j = 0; j < 3; ++j) model[3 * i + j] = Rm[i][j];
+    model[9 + i] = t[i];
+    model[12 + i] = rv[i];
   }
+  model[15] = ok ? 1.0 : 0.0;
 }
 
 // The serial loop of RANSACPointSetRegistrator::run (OpenCV calib3d/src/ptsetreg.cpp) over
@@ -695,11 +584,10 @@ void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* of
     ctx->prof.begin(ctx->stream, kid_hyp);
     // lane groups while they fit one wave per SIMD (small batches: the single frame of vo.py's
     // tracking step, 100 hypotheses); one lane per hypothesis beyond (the same bits either way)
-    if ((long)nh * kGroupLanes <= fill)
-      hipLaunchKernelGGL(pnp_hyp_kernel<kGroupLanes>, dim3(ceil_div((long)nh * kGroupLanes, 64)), dim3(64), 0,
-                         ctx->stream, a, h_lo, h_hi, need_in);
+    if ((long)nh * kPnpGroupLanes <= fill)
+      pnp_hyp_group_launch(a, h_lo, h_hi, need_in, nh, ctx->stream);
     else
-      hipLaunchKernelGGL(pnp_hyp_kernel<1>, dim3(ceil_div(nh, 64)), dim3(64), 0, ctx->stream, a, h_lo, h_hi, need_in);
+      hipLaunchKernelGGL(pnp_hyp_kernel, dim3(ceil_div(nh, 64)), dim3(64), 0, ctx->stream, a, h_lo, h_hi, need_in);
     ctx->prof.end(ctx->stream);
     VO_HIP_CHECK(hipGetLastError());
     ctx->prof.begin(ctx->stream, kid_score);

@@ -188,7 +188,8 @@ int main(int argc, char** argv) {
       for (int c = 0; c < 2; ++c) S.us[p][c] = src[15 + 2 * p + c];
     }
     double R[3][3], t[3], rv[3], Rm[3][3];
-    const bool ok = steps ? epnp5(S, K, R, t, Jacobi12Steps{}) : epnp5(S, K, R, t);
+    const Svd12Alt alt{nullptr, 0};  // the host: the lane groups' step order, serially
+    const bool ok = epnp5(S, K, R, t, steps ? &alt : nullptr);
     rodrigues_to_vec(R, rv);
     rodrigues_to_mat(rv, Rm);
     double* dst = &out[(size_t)h * 25];

@@ -156,7 +156,7 @@ VO_HD void jacobi_rows(double (&A)[N][M], double (&W)[N], double (&Vt)[N][N]) {
 // cyclic order: bitwise jacobi_rows.  The host restatement of pnp.hip's lane-group SVD
 // (tests/test_pnp_host_math.py runs EPnP with it against the oracle).
 struct Jacobi12Steps {
-  VO_HD void operator()(double (&A)[12][12], double (&W)[12], double (&)[12][12]) const {
+  VO_HD void operator()(double (&A)[12][12], double (&W)[12]) const {
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
       double sd = 0.0;
@@ -180,12 +180,94 @@ struct Jacobi12Steps {
   }
 };
 
-// The 12 x 12 SVD of EPnP's M^T M as jacobi_rows runs it (host check and the batch kernel).
-struct Jacobi12Serial {
-  VO_HD void operator()(double (&A)[12][12], double (&W)[12], double (&dummy)[12][12]) const {
-    jacobi_rows<12, 12, false>(A, W, dummy);
-  }
+// EPnP's 12 x 12 SVD in the index-sum step order (Jacobi12Steps' schedule): on the device by
+// the lane group of pnp.hip's group kernel (its LDS rows at lds, this lane's place in the group
+// at lane), on the host (the host check) serially.  Passed to epnp5 by pointer, nullptr for the
+// cyclic sweep (a template parameter instead changed the batch kernel's register allocation:
+// 300 -> 532 B of scratch per lane).
+struct Svd12Alt {
+  double* lds;
+  int lane;
+  VO_HD void run(double (&A)[12][12], double (&W)[12]) const;
 };
+
+// Svd12Alt: 8 lanes per group on the device (pnp.hip kGroupLanes); the step order serially on
+// the host.  Device: lane `lane` publishes rows i = lane mod 8 (every lane of the group holds the
+// same A; static row indices) and their squared norms into the group's LDS rows; step t then
+// takes the pairs (i, j) with i + j == t (at most six, disjoint), one lane each, on rows read
+// from LDS and written back; the group stops after the first sweep without a rotation (a ballot
+// over its lanes); every lane reads the rows back and takes W as jacobi_rows' last loop does.
+// One wave: its LDS operations complete in order, so a step's writes precede the next step's
+// reads behind an lgkmcnt wait.
+VO_HD void Svd12Alt::run(double (&Ar)[12][12], double (&Wr)[12]) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double* A = lds;
+  double* W = lds + 144;
+  const int r = lane;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    if (i % 8 == r) {
+      double sd = 0.0;
+#pragma unroll
+      for (int k = 0; k < 12; k += 2) {
+        *reinterpret_cast<double2*>(A + 12 * i + k) = make_double2(Ar[i][k], Ar[i][k + 1]);
+        sd = sd + Ar[i][k] * Ar[i][k];
+        sd = sd + Ar[i][k + 1] * Ar[i][k + 1];
+      }
+      W[i] = sd;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const uint64_t gmask = 0xFFull << (threadIdx.x & 56);
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    bool changed = false;
+    for (int t = 1; t <= 21; ++t) {
+      const int i = (t - 11 > 0 ? t - 11 : 0) + r, j = t - i;
+      if (i < j) {
+        double ai[12], aj[12];
+#pragma unroll
+        for (int k = 0; k < 12; k += 2) {
+          const double2 x = *reinterpret_cast<const double2*>(A + 12 * i + k);
+          const double2 y = *reinterpret_cast<const double2*>(A + 12 * j + k);
+          ai[k] = x.x;
+          ai[k + 1] = x.y;
+          aj[k] = y.x;
+          aj[k + 1] = y.y;
+        }
+        double wi = W[i], wj = W[j], c, sn;
+        if (jacobi_pair<12>(ai, aj, wi, wj, c, sn)) {
+#pragma unroll
+          for (int k = 0; k < 12; k += 2) {
+            *reinterpret_cast<double2*>(A + 12 * i + k) = make_double2(ai[k], ai[k + 1]);
+            *reinterpret_cast<double2*>(A + 12 * j + k) = make_double2(aj[k], aj[k + 1]);
+          }
+          W[i] = wi;
+          W[j] = wj;
+          changed = true;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if ((__ballot(changed) & gmask) == 0) break;  // uniform in the group
+  }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    double sd = 0.0;
+#pragma unroll
+    for (int k = 0; k < 12; k += 2) {
+      const double2 x = *reinterpret_cast<const double2*>(A + 12 * i + k);
+      Ar[i][k] = x.x;
+      Ar[i][k + 1] = x.y;
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) sd = sd + Ar[i][k] * Ar[i][k];
+    Wr[i] = sqrt(sd);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's reads before the rows are reused
+#else
+  Jacobi12Steps{}(Ar, Wr);
+#endif
+}
 
 // Position of each singular value in the descending order (the selection sort of
 // JacobiSVDImpl_; equal values keep their index order, which the selection sort also
@@ -402,8 +484,7 @@ VO_HD double compute_R_and_t(const EpnpState& S, const Cam& K, const double (&be
 }
 
 // epnp::compute_pose on 5 correspondences.  Returns false for a degenerate subset.
-template <class Svd12>
-VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3], const Svd12& svd12) {
+VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3], const Svd12Alt* alt = nullptr) {
   bool ok = true;
   // choose_control_points: centroid + PCA of the points
   double c0[3] = {0.0, 0.0, 0.0};
@@ -529,7 +610,10 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3], 
         for (int b = 0; b < 12; ++b) A[a][b] = A[a][b] + m2[a] * m2[b];
     }
     double W[12], dummy[12][12];
-    svd12(A, W, dummy);  // jacobi_rows<12, 12, false>: M^T M is symmetric, its rows are A^T's
+    if (alt)
+      alt->run(A, W);
+    else
+      jacobi_rows<12, 12, false>(A, W, dummy);  // M^T M is symmetric: its rows are A^T's
     int rk[12];
     desc_rank<12>(W, rk);
     double s[12];
@@ -665,10 +749,6 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3], 
 // ---------------------------------------------------------------- Rodrigues
 // Matrix -> vector (calibration.cpp); R's columns are first scaled to unit norm, which is
 // what OpenCV's U Vt re-orthonormalisation does to an already orthonormal R.
-VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3]) {
-  return epnp5(S, K, R, t, Jacobi12Serial{});
-}
-
 VO_HD void rodrigues_to_vec(const double (&Rin)[3][3], double (&r)[3]) {
   double R[3][3];
 #pragma unroll
