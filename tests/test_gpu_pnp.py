@@ -157,6 +157,34 @@ def test_split_replay_matches_all_at_once(ctx, h1):
         _check((bool(st1[f, 0]), pose1[f, :3], pose1[f, 3:], mask1[off[f]:off[f + 1]]), ref)
 
 
+@pytest.mark.parametrize("h1", [3, 16])
+def test_split_replay_large_frames(ctx, h1):
+    """The split with frames beyond the scoring kernel's register path (> 1024 points: counts
+    from the global-memory loop, no incremental replay) and beyond pnp_final's LDS stage
+    (> 1024 inliers): the bits of the all-at-once run, and the oracle's results."""
+    sizes, fracs = [1025, 2600, 900, 4000, 1500, 60], [0.1, 0.45, 0.25, 0.05, 0.6, 0.0]
+    Xs, Us = [], []
+    for i, (n, fr) in enumerate(zip(sizes, fracs)):
+        X, uv, K, _, _ = pnp_case(n, 500 + i, noise_px=0.3, outlier_frac=fr)
+        Xs.append(X)
+        Us.append(uv)
+    try:
+        _lib.pnp_testing_split(ctx, -1)
+        _, pose0, mask0, st0 = _run_batch(ctx, Xs, Us, K)
+        _lib.pnp_testing_split(ctx, h1)
+        off, pose1, mask1, st1 = _run_batch(ctx, Xs, Us, K)
+        assert _lib.pnp_testing_last_split(ctx)[0] == h1
+    finally:
+        _lib.pnp_testing_split(ctx, 0)
+    assert st1[3, 1] > 1024  # the 4000-point frame's inliers exceed the LDS stage
+    np.testing.assert_array_equal(pose1, pose0)
+    np.testing.assert_array_equal(mask1, mask0)
+    np.testing.assert_array_equal(st1, st0)
+    for f in (0, 4):
+        ref = P.solve_pnp_ransac(Xs[f], Us[f], K, 2.0)
+        _check((bool(st1[f, 0]), pose1[f, :3], pose1[f, 3:], mask1[off[f]:off[f + 1]]), ref)
+
+
 def test_split_auto_large_batch(ctx):
     """A batch of more hypotheses than one wave per SIMD holds splits by itself; the results
     are the bits of the all-at-once run."""

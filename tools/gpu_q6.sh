@@ -1,0 +1,20 @@
+set -euo pipefail
+OUT=gpurun_out/q6
+mkdir -p $OUT
+export TMPDIR=/tmp
+L=$PWD/visualodometry_amd/lib
+timeout -k 10 500 python -u -m pytest tests/test_gpu_ba.py tests/test_gpu_pnp.py -x -q --timeout 150 --timeout-method thread > $OUT/tests.log 2>&1
+VO_LIB_PATH=$L/libvo_hip_pnpst.so timeout -k 10 120 python tools/pnp_stamps_probe.py > $OUT/pnpst.txt 2>&1
+VO_LIB_PATH=$L/libvo_hip_stamps.so timeout -k 10 120 python tools/band_stamps.py cfg3 > $OUT/stamps.txt 2>&1
+timeout -k 10 180 python tools/frame_latency.py > $OUT/frame_latency.json 2> $OUT/frame_latency.err
+for rep in 1 2 3; do
+  for n in c1 prod; do
+    LIB=$L/libvo_hip_$n.so; [ $n = prod ] && LIB=$L/libvo_hip.so
+    VO_LIB_PATH=$LIB timeout -k 10 120 python bench.py --no-matcher --no-cpu-baseline > $OUT/cfg3_${n}_$rep.json 2> $OUT/cfg3_${n}_$rep.err
+  done
+done
+for n in base prod; do
+  LIB=$L/libvo_hip_$n.so; [ $n = prod ] && LIB=$L/libvo_hip.so
+  VO_LIB_PATH=$LIB timeout -k 10 200 python tools/pnp_only.py > $OUT/pnp_${n}.json 2> $OUT/pnp_${n}.err
+done
+echo done

@@ -351,26 +351,32 @@ int vo_pnp_ransac(vo_ctx* ctx, const float* objpts, const float* imgpts, int n, 
     *success_out = 0;
     for (int k = 0; k < 3; ++k) rvec_out[k] = tvec_out[k] = 0.0;
     if (n == 0) return;
+    // device and page-locked host staging share one layout, X | uv | pose | status | mask: the
+    // points go up in one copy and the results come back in one
     const size_t bx = (size_t)n * 12, bu = (size_t)n * 8, bp = 64, bm = (size_t)n;
+    const size_t po = (bx + bu + 15) & ~size_t(15), total = po + bp + 16 + bm;
     vo::DevBuf& st = ctx->pnp.stage;
-    st.reserve(bx + bu + bp + 16 + bm + 64);
+    vo::HostBuf& hs = ctx->pnp.hstage;
+    st.reserve(total + 64);
+    hs.reserve(total + 64);
     char* base = st.as<char>();
+    char* hbase = hs.as<char>();
     float* dX = reinterpret_cast<float*>(base);
     float* dU = reinterpret_cast<float*>(base + bx);
-    double* dP = reinterpret_cast<double*>(base + ((bx + bu + 15) & ~size_t(15)));
-    int32_t* dS = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(dP) + bp);
+    double* dP = reinterpret_cast<double*>(base + po);
+    int32_t* dS = reinterpret_cast<int32_t*>(base + po + bp);
     uint8_t* dM = reinterpret_cast<uint8_t*>(dS + 4);
     hipStream_t s = ctx->stream;
-    VO_HIP_CHECK(hipMemcpyAsync(dX, objpts, bx, hipMemcpyHostToDevice, s));
-    VO_HIP_CHECK(hipMemcpyAsync(dU, imgpts, bu, hipMemcpyHostToDevice, s));
+    std::memcpy(hbase, objpts, bx);
+    std::memcpy(hbase + bx, imgpts, bu);
+    VO_HIP_CHECK(hipMemcpyAsync(base, hbase, bx + bu, hipMemcpyHostToDevice, s));
     const int32_t offs[2] = {0, n};
     vo::pnp_run(ctx, dX, dU, offs, 1, K, iterations, reproj_err, confidence, dP, dM, dS);
-    double pose[6];
-    int32_t status[2];
-    VO_HIP_CHECK(hipMemcpyAsync(pose, dP, sizeof pose, hipMemcpyDeviceToHost, s));
-    VO_HIP_CHECK(hipMemcpyAsync(status, dS, sizeof status, hipMemcpyDeviceToHost, s));
-    VO_HIP_CHECK(hipMemcpyAsync(mask_out, dM, bm, hipMemcpyDeviceToHost, s));
+    VO_HIP_CHECK(hipMemcpyAsync(hbase + po, dP, total - po, hipMemcpyDeviceToHost, s));
     VO_HIP_CHECK(hipStreamSynchronize(s));
+    const double* pose = reinterpret_cast<const double*>(hbase + po);
+    const int32_t* status = reinterpret_cast<const int32_t*>(hbase + po + bp);
+    std::memcpy(mask_out, hbase + po + bp + 16, bm);
     for (int k = 0; k < 3; ++k) {
       rvec_out[k] = pose[k];
       tvec_out[k] = pose[3 + k];

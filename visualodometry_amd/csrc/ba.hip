@@ -819,7 +819,7 @@ struct alignas(16) LinWave {
 // workgroups of two waves, of three chunks: two of three
 constexpr int kWaveSegsPerCu = 6;
 static_assert(sizeof(LinWave) <= 160 * 1024 / kWaveSegsPerCu, "one-wave K1 LDS image");
-static_assert(kWaveMaxChunks <= 6 && kWaveMaxChunks * sizeof(LinWave) <= 160 * 1024 &&
+static_assert(kWaveMaxChunks <= 8 && kWaveMaxChunks * sizeof(LinWave) <= 160 * 1024 &&
                   kWaveItems * 36 * sizeof(double) <= 2176 * sizeof(double),
               "the chunks of a segment fit one CU; every item's block fits the scratch rows");
 
@@ -1027,8 +1027,8 @@ __device__ __forceinline__ void schur_block(LinWave& S, const LinArgs& A, int si
 // and writes entry range k of that row).
 static_assert(offsetof(LinWave, zb) == offsetof(LinWave, Jc) + sizeof(LinWave::Jc) &&
                   offsetof(LinWave, bt) == offsetof(LinWave, zb) + sizeof(LinWave::zb) &&
-                  sizeof(LinWave::Jc) + sizeof(LinWave::zb) + sizeof(LinWave::bt) >= 36 * sizeof(double) * 60,
-              "the copies' scratch (60 items) fits the Jc | Z | bt region");
+                  sizeof(LinWave::Jc) + sizeof(LinWave::zb) + sizeof(LinWave::bt) >= 36 * sizeof(double) * kWaveItems,
+              "the copies' scratch (kWaveItems items) fits the Jc | Z | bt region");
 template <bool kGroup>
 __device__ __forceinline__ void copy_rows(LinWave& S, const LinArgs& A, int si, bool live) {
   const int m = S.img.anp[si];
@@ -1065,7 +1065,7 @@ __device__ __forceinline__ void copy_rows(LinWave& S, const LinArgs& A, int si, 
 // pose_n region by window camera, for the segment's combine).
 template <bool kGroup>
 __device__ __forceinline__ void rhs_rows(LinWave& S, const LinArgs& A, int nac, int tid) {
-  static_assert(sizeof(S.X) + sizeof(S.L) + sizeof(S.h) >= 6 * sizeof(double) * kSegSlots &&
+  static_assert(sizeof(S.X) + sizeof(S.L) + sizeof(S.h) >= 6 * sizeof(double) * kWaveSlots &&
                     offsetof(LinWave, L) == offsetof(LinWave, X) + sizeof(S.X) &&
                     offsetof(LinWave, h) == offsetof(LinWave, L) + sizeof(S.L),
                 "b partials of every item fit the X | L | h region");
@@ -2370,10 +2370,12 @@ class BAEngine {
   // workgroup's combine with another's chunks: 4.09k -> 3.69k (profiles/r05_ab/k1_six_chunks).
   // So six for windows whose six-chunk segments are predicted to fit one round (56 observations
   // per chunk with padding, cfg3's; setup re-plans with three when they do not), else three.
-  static constexpr int kWaveChunksOneRound = std::min(6, kWaveMaxChunks), kWaveChunksRounds = std::min(3, kWaveMaxChunks);
+  // (48-observation chunks, tuning builds: eight waves per CU, two per SIMD)
+  static constexpr int kWaveChunksOneRound = std::min(kChunkObs >= 64 ? 6 : 8, kWaveMaxChunks),
+                       kWaveChunksRounds = std::min(3, kWaveMaxChunks);
   int wave_chunks(int64_t n_obs) const {
     if (ctx_->ba_k1_variant >= 1) return std::min(ctx_->ba_k1_variant, kWaveMaxChunks);
-    const int64_t one_round_obs = (int64_t)ctx_->num_cus * kWaveChunksOneRound * 56;
+    const int64_t one_round_obs = (int64_t)ctx_->num_cus * kWaveChunksOneRound * (kChunkObs * 7 / 8);
     return n_obs * 10 <= one_round_obs * 11 ? kWaveChunksOneRound : kWaveChunksRounds;
   }
 
@@ -2420,8 +2422,19 @@ class BAEngine {
       d_stamps_.reserve((size_t)plan_.n_chunks() * kPhCount * 8);
       A.stamps = d_stamps_.as<unsigned long long>();
     }
+#if VO_WAVE_MAX_CHUNKS >= 8
+#define VO_LIN_LAUNCH_78(M)                                                                   \
+    if (wave && nw == 8)                                                                      \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 8>), g, b, 0, ctx_->stream, A);  \
+    else if (wave && nw == 7)                                                                 \
+      hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 7>), g, b, 0, ctx_->stream, A);  \
+    else
+#else
+#define VO_LIN_LAUNCH_78(M)
+#endif
 #define VO_LIN_LAUNCH(M)                                                                      \
   do {                                                                                        \
+    VO_LIN_LAUNCH_78(M)                                                                       \
     if (wave && nw == 6)                                                                      \
       hipLaunchKernelGGL((ba_lin_wave_kernel<M, stamps_on_, 6>), g, b, 0, ctx_->stream, A);  \
     else if (wave && nw == 5)                                                                 \

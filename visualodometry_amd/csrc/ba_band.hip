@@ -1049,12 +1049,16 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     };
     int zk = (int)(zs - dyn) + 6 * (sbot ? F - 1 - khi : khi);  // z_k of the current step
     const int dz = sbot ? 6 : -6;
-    auto step = [&](int k, const double (&gv)[6], double yin) __attribute__((always_inline)) {
+    // a step also fetches the operands of the step two ahead, issued after its z reads: LDS
+    // reads of one wave complete in order, so reads issued before them would delay z_k
+    auto step = [&](int k, const double (&gv)[6], double yin, double (&gn)[6], double& yn) __attribute__((always_inline)) {
       int ow = ((k < kp) & act & (qb == 0)) ? zk + sr : DOFF + lane;
       asm volatile("" : "+v"(ow));
       dyn[ow] = Yb;
       double z[6];
       ld6g(dyn + zk, z);
+      asm volatile("" ::: "memory");
+      fetch(gn, yn);
       double d = gv[0] * z[0] + gv[1] * z[1] + gv[2] * z[2] + gv[3] * z[3] + gv[4] * z[4] + gv[5] * z[5];
       asm volatile("" : "+v"(d));
       Yb = qb == 0 ? yin : Yb - d;
@@ -1062,37 +1066,47 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       zk += dz;
     };
     int k = khi;
+    double gA[6], gB[6], yA, yB;
+    fetch(gA, yA);
     // pseudo steps (the bottom side's separator rows, k >= kp): z_k is the top side's,
-    // already in zs, so nothing is stored and each z is fetched one step ahead: the steps
-    // are independent subtractions instead of LDS round trips
+    // already in zs, so nothing is stored, and every operand of a step (z, g, y) is loaded
+    // during the step before it: the steps are independent subtractions whose loads are in
+    // flight while the previous one computes, not LDS round trips.  The operands fetched
+    // past the last pseudo step are the first regular step's.
     if (k >= kp && k >= klo) {
       double zc[6];
       ld6g(dyn + zk, zc);
       for (; k >= kp && k >= klo; --k) {
-        double gv[6], yin, zn[6];
-        fetch(gv, yin);
+        double zn[6];
         int on = k - 1 >= kp ? zk + dz : zk;
         asm volatile("" : "+v"(on));
         ld6g(dyn + on, zn);
-        double d = gv[0] * zc[0] + gv[1] * zc[1] + gv[2] * zc[2] + gv[3] * zc[3] + gv[4] * zc[4] + gv[5] * zc[5];
+        fetch(gB, yB);
+        double d = gA[0] * zc[0] + gA[1] * zc[1] + gA[2] * zc[2] + gA[3] * zc[3] + gA[4] * zc[4] + gA[5] * zc[5];
         asm volatile("" : "+v"(d));
-        Yb = qb == 0 ? yin : Yb - d;
+        Yb = qb == 0 ? yA : Yb - d;
         qb = qb == 0 ? w : qb - 1;
         zk += dz;
 #pragma unroll
-        for (int c = 0; c < 6; ++c) zc[c] = zn[c];
+        for (int c = 0; c < 6; ++c) {
+          zc[c] = zn[c];
+          gA[c] = gB[c];
+        }
+        yA = yB;
       }
     }
-    double gA[6], gB[6], yA, yB;
-    fetch(gA, yA);
     fetch(gB, yB);
-    for (; k - 1 >= klo; k -= 2) {
-      step(k, gA, yA);
-      fetch(gA, yA);
-      step(k - 1, gB, yB);
-      fetch(gB, yB);
+    // three operand sets in rotation (a step's set is in use while the one two steps ahead
+    // loads), unrolled by three so that no set is copied; the fetches past the last step read
+    // in-bounds (zero) operands
+    double gC[6], yC;
+    for (; k - 2 >= klo; k -= 3) {
+      step(k, gA, yA, gC, yC);
+      step(k - 1, gB, yB, gA, yA);
+      step(k - 2, gC, yC, gB, yB);
     }
-    if (k >= klo) step(k, gA, yA);
+    if (k >= klo) step(k, gA, yA, gC, yC);
+    if (k - 1 >= klo) step(k - 1, gB, yB, gA, yA);
   };
   auto bs_go = [&](int khi, int klo, int kp) __attribute__((always_inline)) {
     if constexpr (kFull) bs_run_full(khi, klo, kp);

@@ -405,7 +405,7 @@ std::string build_plan(BAPlan& P, int N, int L, int M, int n_fixed, const int32_
   // wave plans of several chunks per segment: segments padded to seg_chunks chunks, and a
   // window of at most kWaveItems slots (every chunk's blocks fit the combine's scratch rows)
   const int group_nch = wave && seg_chunks > 1 ? seg_chunks : 0;
-  const int max_slots = group_nch ? kWaveItems : kSegSlots;
+  const int max_slots = group_nch || (wave && kWaveSlots < kSegSlots) ? kWaveItems : kSegSlots;
   const int nthr = plan_threads(M);
   PlanSession session(nthr > 1);
   if (!P.scratch) P.scratch = std::make_shared<PlanScratch>();

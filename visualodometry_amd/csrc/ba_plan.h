@@ -84,7 +84,12 @@ inline bool plan_is_wave(int seg_obs) { return seg_obs == 1; }
 #define VO_WAVE_MAX_CHUNKS 6
 #endif
 constexpr int kWaveMaxChunks = VO_WAVE_MAX_CHUNKS;  // chunks (waves) per segment of a wave plan (ba.hip instantiates 1..6)
-constexpr int kWaveItems = 60;     // one-wave K1 lanes for slot items (the scratch rows of the combine)
+// one-wave K1 lanes for slot items: the combine's scratch rows (36 doubles each) alias the chunk's
+// Jc | Z | bt region (34 doubles per observation), 60 at 64-observation chunks
+constexpr int kWaveItems = VO_CHUNK_OBS * 34 / 36 < 60 ? VO_CHUNK_OBS * 34 / 36 : 60;
+// window slots of a one-chunk wave segment: every item's b partial (6 doubles) fits the chunk's
+// X | L | h region (12 doubles per landmark), all 64 at 64-observation chunks
+constexpr int kWaveSlots = kChunkPts * 12 / 6 < kSegSlots ? kWaveItems : kSegSlots;
 constexpr int kChunkHdr = 16;
 
 constexpr int kSegCams = 24;     // free (window) cameras of a segment

@@ -317,17 +317,22 @@ __device__ __forceinline__ double wave_sum(double v) {
 #define VO_PNP_FINAL_THREADS 128
 #endif
 constexpr int kFinalThreads = VO_PNP_FINAL_THREADS;
-constexpr int kFinalWaves = kFinalThreads / 64;
 static_assert(kFinalThreads % 64 == 0 && kFinalThreads <= 256, "pnp_final: 1..4 waves");
+// Small batches (the single frame of vo.py's tracking step): one frame per CU anyway, so eight
+// waves share its LM passes (the normal equations' point loop is then 1 / 4 as long; the sums are
+// taken in another order than at 128 threads, within the oracle's tolerance either way)
+constexpr int kFinalThreadsWide = 512;
+constexpr int kFinalWideBatch = 64;
 constexpr int kLmStage = 1024;  // inliers pnp_final stages in LDS for its LM passes (20 KB)
 
 // Normal equations of the inliers at (R, t): this thread's partial sums (points i = tid mod
-// kFinalThreads).
+// T).
+template <int T>
 __device__ __forceinline__ void lm_accumulate(const PnpArgs& a, int o, int n, const double* R, const double* t,
                                               double (&acc)[kNe]) {
 #pragma unroll
   for (int k = 0; k < kNe; ++k) acc[k] = 0.0;
-  for (int i = threadIdx.x; i < n; i += kFinalThreads) {
+  for (int i = threadIdx.x; i < n; i += T) {
     if (!a.mask[o + i]) continue;
     float M[3];
     load3(a.X, o + i, M);
@@ -336,6 +341,7 @@ __device__ __forceinline__ void lm_accumulate(const PnpArgs& a, int o, int n, co
   }
 }
 
+template <int T>
 __device__ __forceinline__ void lm_reduce(double (&acc)[kNe], double* red, double* out) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -348,18 +354,20 @@ __device__ __forceinline__ void lm_reduce(double (&acc)[kNe], double* red, doubl
     const int k = threadIdx.x;
     double v = red[k];
 #pragma unroll
-    for (int w = 1; w < kFinalWaves; ++w) v = v + red[w * kNe + k];
+    for (int w = 1; w < T / 64; ++w) v = v + red[w * kNe + k];
     out[k] = v;
   }
   __syncthreads();
 }
 
-__global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) {  // 2 waves per SIMD
+template <int T>
+__global__ __launch_bounds__(T, 2) void pnp_final_kernel(PnpArgs a) {  // 2 waves per SIMD
+  constexpr int kFinalWaves = T / 64;
   const int f = blockIdx.x;
   const int o = a.off[f], n = a.off[f + 1] - o;
   __shared__ int s_count, s_go;
-  __shared__ int s_cnt[kFinalThreads];
-  __shared__ ItersTerms s_terms[kFinalThreads];
+  __shared__ int s_cnt[T];
+  __shared__ ItersTerms s_terms[T];
   __shared__ ReplayState s_st;
   __shared__ double s_R[9], s_t[3];
   __shared__ double s_red[kFinalWaves * kNe];
@@ -367,13 +375,13 @@ __global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) 
   __shared__ float s_pt[kLmStage * 5];  // staged inliers: X, Y, Z, u, v
   __shared__ int s_wc[kFinalWaves];
   // the serial RANSAC loop over the precomputed counts (uniform branch: n is per frame)
-  if (n > kPts) ransac_replay<kFinalThreads>(a, f, n, a.H, s_cnt, s_terms, &s_st);
+  if (n > kPts) ransac_replay<T>(a, f, n, a.H, s_cnt, s_terms, &s_st);
   if (threadIdx.x == 0) s_count = 0;
   const int best = n > kPts ? s_st.best : n == kPts && a.models[(size_t)f * a.H * kModel + 15] != 0.0 ? 0 : -1;
   __syncthreads();
   const double* model = a.models + ((size_t)f * a.H + (best < 0 ? 0 : best)) * kModel;
   if (best < 0 || n == kPts) {
-    for (int i = threadIdx.x; i < n; i += kFinalThreads) a.mask[o + i] = best < 0 ? 0 : 1;
+    for (int i = threadIdx.x; i < n; i += T) a.mask[o + i] = best < 0 ? 0 : 1;
     if (threadIdx.x == 0) {
       for (int k = 0; k < 3; ++k) {
         a.pose[6 * f + k] = best < 0 ? 0.0 : model[12 + k];
@@ -394,7 +402,7 @@ __global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) 
   // Positions by ballot ranks, so the order does not depend on timing.
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int ninl = 0;  // uniform
-  for (int c0 = 0; c0 < n; c0 += kFinalThreads) {
+  for (int c0 = 0; c0 < n; c0 += T) {
     const int i = c0 + (int)threadIdx.x;
     float M[3] = {0.f, 0.f, 0.f};
     float2 q = make_float2(0.f, 0.f);
@@ -429,12 +437,12 @@ __global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) 
   // normal equations of the inliers at (R, t), this thread's partial sums
   auto accumulate = [&](const double* Rc, const double* tc, double (&acc)[kNe]) {
     if (ninl > kLmStage) {
-      lm_accumulate(a, o, n, Rc, tc, acc);  // reads mask[o + i] for the i this thread wrote
+      lm_accumulate<T>(a, o, n, Rc, tc, acc);  // reads mask[o + i] for the i this thread wrote
       return;
     }
 #pragma unroll
     for (int k = 0; k < kNe; ++k) acc[k] = 0.0;
-    for (int j = threadIdx.x; j < ninl; j += kFinalThreads) {
+    for (int j = threadIdx.x; j < ninl; j += T) {
       const float* d = &s_pt[5 * j];
       const float M[3] = {d[0], d[1], d[2]};
       lm_point(Rc, tc, M, d[3], d[4], a.K, acc);
@@ -444,7 +452,7 @@ __global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) 
   // every pass evaluates the normal equations at the pose in s_R/s_t.
   double acc[kNe];
   accumulate(R, t, acc);
-  lm_reduce(acc, s_red, s_ne);
+  lm_reduce<T>(acc, s_red, s_ne);
   LmState lm;
   if (threadIdx.x == 0) {
     lm.init(R, t, s_ne);
@@ -458,7 +466,7 @@ __global__ __launch_bounds__(kFinalThreads, 2) void pnp_final_kernel(PnpArgs a) 
 #pragma unroll
     for (int k = 0; k < 3; ++k) nt[k] = s_t[k];
     accumulate(nR, nt, acc);
-    lm_reduce(acc, s_red, s_ne);  // ends with a barrier: every thread has read s_R/s_t
+    lm_reduce<T>(acc, s_red, s_ne);  // ends with a barrier: every thread has read s_R/s_t
     if (threadIdx.x == 0) s_go = lm.update(nR, nt, s_ne) && lm.propose(s_R, s_t) ? 1 : 0;
     __syncthreads();
   }
@@ -613,7 +621,10 @@ void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* of
     solve_and_score(h1, H, need, kKPnpHypTail, kKPnpScoreTail);
   }
   ctx->prof.begin(ctx->stream, kKPnpFinal);
-  hipLaunchKernelGGL(pnp_final_kernel, dim3(batch), dim3(kFinalThreads), 0, ctx->stream, a);
+  if (batch <= kFinalWideBatch)
+    hipLaunchKernelGGL(pnp_final_kernel<kFinalThreadsWide>, dim3(batch), dim3(kFinalThreadsWide), 0, ctx->stream, a);
+  else
+    hipLaunchKernelGGL(pnp_final_kernel<kFinalThreads>, dim3(batch), dim3(kFinalThreads), 0, ctx->stream, a);
   ctx->prof.end(ctx->stream);
   VO_HIP_CHECK(hipGetLastError());
 }

@@ -188,36 +188,24 @@ struct Jacobi12Steps {
 struct Svd12Alt {
   double* lds;
   int lane;
-  VO_HD void run(double (&A)[12][12], double (&W)[12]) const;
+#if defined(__HIP_DEVICE_COMPILE__)
+  __device__ void sweeps() const;  // the Jacobi sweeps on the group's LDS rows and squared norms
+#else
+  void run(double (&A)[12][12], double (&W)[12]) const;  // host: jacobi_rows in the step order
+#endif
 };
 
-// Svd12Alt: 8 lanes per group on the device (pnp.hip kGroupLanes); the step order serially on
-// the host.  Device: lane `lane` publishes rows i = lane mod 8 (every lane of the group holds the
-// same A; static row indices) and their squared norms into the group's LDS rows; step t then
-// takes the pairs (i, j) with i + j == t (at most six, disjoint), one lane each, on rows read
-// from LDS and written back; the group stops after the first sweep without a rotation (a ballot
-// over its lanes); every lane reads the rows back and takes W as jacobi_rows' last loop does.
-// One wave: its LDS operations complete in order, so a step's writes precede the next step's
-// reads behind an lgkmcnt wait.
-VO_HD void Svd12Alt::run(double (&Ar)[12][12], double (&Wr)[12]) const {
+// Svd12Alt: 8 lanes per group on the device (pnp_group.hip), the step order serially on the
+// host.  Device sweeps (svd12_group_null_space fills the rows): step t takes the pairs (i, j)
+// with i + j == t (at most six, disjoint), one lane each, on rows read from the group's LDS and
+// written back; the group stops after the first sweep without a rotation (a ballot over its
+// lanes).  One wave: its LDS operations complete in order, so a step's writes precede the next
+// step's reads behind an lgkmcnt wait.
 #if defined(__HIP_DEVICE_COMPILE__)
+__device__ inline void Svd12Alt::sweeps() const {
   double* A = lds;
   double* W = lds + 144;
   const int r = lane;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    if (i % 8 == r) {
-      double sd = 0.0;
-#pragma unroll
-      for (int k = 0; k < 12; k += 2) {
-        *reinterpret_cast<double2*>(A + 12 * i + k) = make_double2(Ar[i][k], Ar[i][k + 1]);
-        sd = sd + Ar[i][k] * Ar[i][k];
-        sd = sd + Ar[i][k + 1] * Ar[i][k + 1];
-      }
-      W[i] = sd;
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   const uint64_t gmask = 0xFFull << (threadIdx.x & 56);
   for (int sweep = 0; sweep < 30; ++sweep) {
     bool changed = false;
@@ -250,24 +238,10 @@ VO_HD void Svd12Alt::run(double (&Ar)[12][12], double (&Wr)[12]) const {
     }
     if ((__ballot(changed) & gmask) == 0) break;  // uniform in the group
   }
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    double sd = 0.0;
-#pragma unroll
-    for (int k = 0; k < 12; k += 2) {
-      const double2 x = *reinterpret_cast<const double2*>(A + 12 * i + k);
-      Ar[i][k] = x.x;
-      Ar[i][k + 1] = x.y;
-    }
-#pragma unroll
-    for (int k = 0; k < 12; ++k) sd = sd + Ar[i][k] * Ar[i][k];
-    Wr[i] = sqrt(sd);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's reads before the rows are reused
-#else
-  Jacobi12Steps{}(Ar, Wr);
-#endif
 }
+#else
+inline void Svd12Alt::run(double (&Ar)[12][12], double (&Wr)[12]) const { Jacobi12Steps{}(Ar, Wr); }
+#endif
 
 // Position of each singular value in the descending order (the selection sort of
 // JacobiSVDImpl_; equal values keep their index order, which the selection sort also
@@ -361,6 +335,109 @@ struct EpnpState {
   double rho[6];
 };
 constexpr int kEpnpColDoubles = kPts * 4 + 4 * 12;  // alphas, v
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// The 12 x 12 part of epnp::compute_pose on a lane group (Svd12Alt's 8 lanes), without M^T M in
+// any lane's registers: lane r builds rows i = r, r + 8 of M^T M straight into the group's LDS
+// rows (each entry the same sum in the same order as the per-lane build), the Jacobi sweeps run
+// as Svd12Alt::run's, lane r then takes the norms of its rows, and every lane reads the twelve
+// norms and only the four rows it needs (v = the rows of the four smallest, each times 1 / W).
+// Same values as jacobi_rows + the selection below it in epnp5.  Returns the W > DBL_MIN flag.
+__device__ inline bool svd12_group_null_space(const Svd12Alt& g, EpnpState& S, const Cam& K) {
+  double* A = g.lds;
+  double* W = g.lds + 144;
+  const int r = g.lane;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = r + 8 * u;
+    if (i < 12) {
+      const int c = i / 3, comp = i - 3 * c;
+      double row[12];
+#pragma unroll
+      for (int b = 0; b < 12; ++b) row[b] = 0.0;
+#pragma unroll
+      for (int p = 0; p < kPts; ++p) {
+        double m1[12], m2[12];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          const double al = S.alphas[p * 4 + cc];
+          m1[3 * cc] = al * K.fu;
+          m1[3 * cc + 1] = 0.0;
+          m1[3 * cc + 2] = al * (K.uc - S.us[p][0]);
+          m2[3 * cc] = 0.0;
+          m2[3 * cc + 1] = al * K.fv;
+          m2[3 * cc + 2] = al * (K.vc - S.us[p][1]);
+        }
+        const double ali = S.alphas[p * 4 + c];
+        const double m1i = comp == 0 ? ali * K.fu : comp == 1 ? 0.0 : ali * (K.uc - S.us[p][0]);
+        const double m2i = comp == 0 ? 0.0 : comp == 1 ? ali * K.fv : ali * (K.vc - S.us[p][1]);
+#pragma unroll
+        for (int b = 0; b < 12; ++b) row[b] = row[b] + m1i * m1[b];
+#pragma unroll
+        for (int b = 0; b < 12; ++b) row[b] = row[b] + m2i * m2[b];
+      }
+      double sd = 0.0;
+#pragma unroll
+      for (int k = 0; k < 12; k += 2) {
+        *reinterpret_cast<double2*>(A + 12 * i + k) = make_double2(row[k], row[k + 1]);
+        sd = sd + row[k] * row[k];
+        sd = sd + row[k + 1] * row[k + 1];
+      }
+      W[i] = sd;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  g.sweeps();
+  // norms of this lane's rows (jacobi_rows' last loop), then every lane reads all twelve
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = r + 8 * u;
+    if (i < 12) {
+      double sd = 0.0;
+#pragma unroll
+      for (int k = 0; k < 12; k += 2) {
+        const double2 x = *reinterpret_cast<const double2*>(A + 12 * i + k);
+        sd = sd + x.x * x.x;
+        sd = sd + x.y * x.y;
+      }
+      W[i] = sqrt(sd);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  double Wr[12];
+#pragma unroll
+  for (int i = 0; i < 12; i += 2) {
+    const double2 x = *reinterpret_cast<const double2*>(W + i);
+    Wr[i] = x.x;
+    Wr[i + 1] = x.y;
+  }
+  int rk[12];
+  desc_rank<12>(Wr, rk);
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) ok &= Wr[i] > kDblMin;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int sel = 0;
+    double wsel = Wr[0];
+#pragma unroll
+    for (int i = 1; i < 12; ++i) {
+      sel = rk[i] == 11 - q ? i : sel;
+      wsel = rk[i] == 11 - q ? Wr[i] : wsel;
+    }
+    const double sq = 1.0 / wsel;
+    const double* rowp = A + 12 * sel;
+#pragma unroll
+    for (int k = 0; k < 12; k += 2) {
+      const double2 x = *reinterpret_cast<const double2*>(rowp + k);
+      S.v[q * 12 + k] = x.x * sq;
+      S.v[q * 12 + k + 1] = x.y * sq;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's reads before the rows are reused
+  return ok;
+}
+#endif
 
 VO_HD double dot3f(const double* a, const float* b) {
   return a[0] * (double)b[0] + a[1] * (double)b[1] + a[2] * (double)b[2];
@@ -581,6 +658,11 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3], 
     }
   }
   // M (2n x 12), M^T M, its four smallest right singular vectors
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (alt)
+    ok &= svd12_group_null_space(*alt, S, K);
+  else
+#endif
   {
     double A[12][12];
 #pragma unroll
@@ -610,10 +692,14 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3], 
         for (int b = 0; b < 12; ++b) A[a][b] = A[a][b] + m2[a] * m2[b];
     }
     double W[12], dummy[12][12];
+#if defined(__HIP_DEVICE_COMPILE__)
+    jacobi_rows<12, 12, false>(A, W, dummy);  // M^T M is symmetric: its rows are A^T's
+#else
     if (alt)
-      alt->run(A, W);
+      alt->run(A, W);  // the lane groups' step order, serially
     else
-      jacobi_rows<12, 12, false>(A, W, dummy);  // M^T M is symmetric: its rows are A^T's
+      jacobi_rows<12, 12, false>(A, W, dummy);
+#endif
     int rk[12];
     desc_rank<12>(W, rk);
     double s[12];
@@ -658,11 +744,7 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3], 
     }
   }
   // three beta approximations, each refined by Gauss-Newton; keep the lowest error
-  double bestR[3][3], bestt[3], best_err = 0.0;
-  for (int kind = 1; kind <= 3; ++kind) {
-    // keeps the reads of S.alphas / S.v (LDS on the device) inside the loop: hoisted out of
-    // it they would take registers across all three kinds
-    asm volatile("" ::: "memory");
+  auto run_kind = [&](int kind, double (&Rk)[3][3], double (&tk)[3]) __attribute__((always_inline)) -> double {
     double betas[4] = {0.0, 0.0, 0.0, 0.0};
     double rho[6];
 #pragma unroll
@@ -721,8 +803,53 @@ VO_HD bool epnp5(EpnpState& S, const Cam& K, double (&R)[3][3], double (&t)[3], 
       betas[2] = x[3] / betas[0];
     }
     gauss_newton(S, betas);
+    return compute_R_and_t(S, K, betas, Rk, tk);
+  };
+  double bestR[3][3], bestt[3], best_err = 0.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (alt) {
+    // lane groups: lane r of the group refines kind r + 1 (lanes 3.. repeat kind 3), the three
+    // results meet in the group's LDS (free after the SVD; one wave: its LDS operations
+    // complete in order) and every lane takes the serial loop's choice from them: kind 1, then
+    // a later kind only if its error is strictly lower.  The kinds' Gauss-Newton and pose
+    // passes run once, side by side, instead of three times on every lane.
     double Rk[3][3], tk[3];
-    const double e = compute_R_and_t(S, K, betas, Rk, tk);
+    const int my = alt->lane < 3 ? alt->lane + 1 : 3;
+    const double e = run_kind(my, Rk, tk);
+    double* x = alt->lds;
+    if (alt->lane < 3) {
+      double* d = x + 13 * alt->lane;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) d[q] = Rk[q / 3][q % 3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) d[9 + q] = tk[q];
+      d[12] = e;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int pick = 0;
+    best_err = x[12];
+    if (x[13 + 12] < best_err) {
+      best_err = x[13 + 12];
+      pick = 1;
+    }
+    if (x[26 + 12] < best_err) {
+      best_err = x[26 + 12];
+      pick = 2;
+    }
+    const double* d = x + 13 * pick;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) bestR[q / 3][q % 3] = d[q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) bestt[q] = d[9 + q];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's reads before the group's LDS is reused
+  } else
+#endif
+  for (int kind = 1; kind <= 3; ++kind) {
+    // keeps the reads of S.alphas / S.v (LDS on the device) inside the loop: hoisted out of
+    // it they would take registers across all three kinds
+    asm volatile("" ::: "memory");
+    double Rk[3][3], tk[3];
+    const double e = run_kind(kind, Rk, tk);
     if (kind == 1 || e < best_err) {
       best_err = e;
 #pragma unroll

@@ -54,6 +54,7 @@ struct PnpWorkspace {
   DevBuf counts;  // int32 (batch, H)
   DevBuf need;    // int32 (batch): frames whose hypotheses past the first h1 are solved
   DevBuf stage;   // host-call staging: points, outputs
+  HostBuf hstage; // its page-locked mirror: one upload and one download per host call
   std::vector<int32_t> offsets;  // layout the cached subsets were made for
   int H = 0;
   int last_h1 = 0;  // hypotheses solved for every frame by the last call (pnp_run)
