@@ -117,14 +117,16 @@ def _run_batch(ctx, Xs, Us, K, thr=2.0):
     return off, dP.numpy(), dM.numpy()[: off[-1]].astype(bool), dS.numpy()
 
 
-def _split_cases(count, n_max, seed0):
+def _split_cases(count, n_max, seed0, big=None):
     """Frames of mixed sizes and outlier fractions: some stop the serial loop within a few
-    hypotheses, some run all 100 (60 % outliers, pure noise)."""
+    hypotheses, some run all 100 (60 % outliers, pure noise).  big: {frame: points} for frames
+    past the scoring kernel's 1024-point register path."""
     rng = np.random.default_rng(seed0)
     fracs = [0.0, 0.1, 0.25, 0.45, 0.6]
     Xs, Us = [], []
     for i in range(count):
         n = [0, 5, 6][i] if i < 3 else int(rng.integers(8, n_max))
+        n = (big or {}).get(i, n)
         X, uv, K, _, _ = pnp_case(max(n, 1), seed0 + i, noise_px=0.3, outlier_frac=fracs[i % 5] if n > 20 else 0.0)
         if i == 3:  # pure noise: no model has more than 4 inliers
             uv = rng.uniform(0, 1000, uv.shape).astype(np.float32)
@@ -188,7 +190,7 @@ def test_split_replay_large_frames(ctx, h1):
 def test_split_auto_large_batch(ctx):
     """A batch of more hypotheses than one wave per SIMD holds splits by itself; the results
     are the bits of the all-at-once run."""
-    Xs, Us, K = _split_cases(1100, 120, 900)
+    Xs, Us, K = _split_cases(1100, 120, 900, big={9: 1500, 21: 3000, 33: 1100})
     try:
         _lib.pnp_testing_split(ctx, -1)
         _, pose0, mask0, st0 = _run_batch(ctx, Xs, Us, K)

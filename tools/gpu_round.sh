@@ -3,7 +3,7 @@
 # passes of cfg3 and cfg4 (keyed to this build: tools/pmc_traffic.py), the matcher MFMA-busy
 # pass, and the final bench lines with the matching traffic.  Each GPU step has its own time
 # limit; the chain stops at the first failure.
-# Usage (from the build container): gpurun --timeout 1500 -- bash tools/gpu_round.sh r04 [notest]
+# Usage (from the build container): gpurun --timeout 1500 -- bash tools/gpu_round.sh r06 [notest]
 set -euo pipefail
 TAG=${1:-r04}
 OUT=gpurun_out
@@ -36,4 +36,5 @@ timeout -k 10 300 python bench.py --config cfg4 --no-matcher --no-cpu-baseline -
 timeout -k 10 300 python tools/shard_projection.py cfg3 > $OUT/shard_projection_cfg3.json 2> $OUT/shard_projection_cfg3.err
 timeout -k 10 300 python tools/shard_projection.py cfg4 > $OUT/shard_projection_cfg4.json 2> $OUT/shard_projection_cfg4.err
 timeout -k 10 300 python tools/host_call_latency.py > $OUT/host_latency.json 2> $OUT/host_latency.err
+timeout -k 10 180 python tools/frame_latency.py > $OUT/frame_latency.json 2> $OUT/frame_latency.err
 echo done
