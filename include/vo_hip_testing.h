@@ -38,6 +38,12 @@ int vo_ba_testing_drop_reducers(vo_ctx* ctx, int n);
  * covered by the GPU tests; takes effect at the next setup. */
 int vo_ba_testing_k1(vo_ctx* ctx, int variant);
 
+/* Test switch: on != 0 keeps this context's later vo_ba_setup calls off the banded solver's
+ * split layout (two workgroups, one per side), so a window too large for one workgroup's LDS
+ * takes the ring layout (factor records in global memory) as before round 6.  Same arithmetic:
+ * the GPU tests compare the two layouts bitwise.  Takes effect at the next setup. */
+int vo_ba_testing_no_split(vo_ctx* ctx, int on);
+
 /* Host only: the digest (as vo_ba_plan_digest) of the plan of `cur` packed for seg_obs
  * observations per segment (seg_obs 1: the one-wave K1's plan of seg_chunks chunks per
  * segment), built from scratch when prev is NULL, else after a from-scratch plan of `prev`

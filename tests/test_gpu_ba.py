@@ -239,6 +239,39 @@ def test_fused_handoff_stress(ctx):
         np.testing.assert_array_equal(a, b)
 
 
+def test_split_layout_equals_ring(ctx):
+    """cfg4's window (F = 98, too large for one workgroup's LDS) on the split layout (one
+    workgroup per side, each side's columns in its own CU's LDS, three global-memory hand-offs per
+    launch) and on the ring layout (one workgroup, factor records in global memory): the same
+    arithmetic in the same order, so the same bits over 30 GN iterations (30 launches, each
+    workgroup pair possibly on two XCDs), cost by cost, and the state after them."""
+    p = make_ba_config("cfg4")
+    out = []
+    for no_split in (False, True):
+        _lib.ba_testing_no_split(ctx, no_split)
+        try:
+            s = _session(p, ctx)
+            assert s.plan_stats()["band_mode"] == ("ring" if no_split else "split")
+            rc, costs = s.run(30)
+            assert rc == _lib.VO_OK
+            out.append((costs,) + s.get_state())
+        finally:
+            _lib.ba_testing_no_split(ctx, False)
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("n_poses,max_track,mode", [(50, 8, "full"), (100, 8, "split"), (100, 4, "full"),
+                                                    (140, 6, "split"), (200, 8, "ring")])
+def test_band_layout_modes(ctx, n_poses, max_track, mode):
+    """The banded K3's layouts by window size (one workgroup with every column in LDS; one
+    workgroup per side; the ring with records in global memory): one GN step against the numpy
+    oracle's dense Cholesky."""
+    p = make_ba_problem(n_poses, 30 * n_poses, 5 + n_poses, max_track=max_track)
+    s = _step_vs_oracle(ctx, p)
+    assert s.plan_stats()["band_mode"] == mode
+
+
 def test_run_in_pieces_equals_one_run(ctx):
     p = make_ba_config("cfg2")
     s1 = _session(p, ctx)

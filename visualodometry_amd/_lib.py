@@ -109,6 +109,7 @@ SIGNATURES = {
     "vo_comm_init": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_comm_init_loopback": (_I, [_P, _I, _I, C.c_char_p]),
     "vo_ba_split_reduce": (_I, [_P, _I]),
+    "vo_ba_testing_no_split": (_I, [_P, _I]),
     "vo_ba_testing_drop_reducers": (_I, [_P, _I]),
     "vo_ba_testing_k1": (_I, [_P, _I]),
     "vo_pnp_testing_split": (_I, [_P, _I]),
@@ -287,6 +288,12 @@ def ba_testing_drop_reducers(ctx: "Context", n: int) -> None:
     """Test switch: fused launches of this context leave out ``n`` reducer workgroups, so
     the solver's bounded wait times out; see vo_ba_testing_drop_reducers."""
     check(ctx.lib.vo_ba_testing_drop_reducers(ctx.handle, int(n)), "vo_ba_testing_drop_reducers")
+
+
+def ba_testing_no_split(ctx: "Context", on: bool = True) -> None:
+    """Test switch: the context's later setups never take the banded solver's split layout
+    (ring layout instead, where one workgroup's LDS is too small); see vo_ba_testing_no_split."""
+    check(ctx.lib.vo_ba_testing_no_split(ctx.handle, int(bool(on))), "vo_ba_testing_no_split")
 
 
 def ba_reserve(ctx: "Context", n_poses: int, n_points: int, n_obs: int, n_fixed: int = 2) -> None:

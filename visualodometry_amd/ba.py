@@ -251,14 +251,16 @@ class BASession:
                       "profile", "uploads", "buffers", "band_tables", "attributes"]
 
     def plan_stats(self) -> dict:
-        out = np.zeros(23, dtype=np.int64)
-        n = check(self.ctx.lib.vo_ba_plan_stats(self.ctx.handle, ptr(out, C.c_int64), 23), "stats")
+        out = np.zeros(24, dtype=np.int64)
+        n = check(self.ctx.lib.vo_ba_plan_stats(self.ctx.handle, ptr(out, C.c_int64), 24), "stats")
         keys = ["chunks", "segments", "slab_blocks", "reduced_blocks", "profile_blocks",
                 "track_entries", "algorithmic_bytes_per_iter", "band_solver", "reused_groups",
                 "reused_chunks", "seg_obs"]
         st = dict(zip(keys[:n], out[:n].tolist()))
         if n > 11:  # the last setup's host sections (ns)
-            st["setup_us"] = {k: round(v / 1e3, 1) for k, v in zip(self.SETUP_SECTIONS, out[11:n].tolist())}
+            st["setup_us"] = {k: round(v / 1e3, 1) for k, v in zip(self.SETUP_SECTIONS, out[11:23].tolist())}
+        if n > 23:  # the banded K3's layout
+            st["band_mode"] = ["none", "full", "ring", "split"][int(out[23])]
         return st
 
 

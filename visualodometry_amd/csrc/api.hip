@@ -877,6 +877,13 @@ int vo_ba_testing_drop_reducers(vo_ctx* ctx, int n) {
   });
 }
 
+int vo_ba_testing_no_split(vo_ctx* ctx, int on) {
+  return guarded([&] {
+    VO_REQUIRE(ctx != nullptr, VO_ERR_ARG, "vo_ba_testing_no_split: null context");
+    ctx->ba_no_split = on != 0;
+  });
+}
+
 int vo_ba_testing_k1(vo_ctx* ctx, int variant) {
   return guarded([&] {
     VO_REQUIRE(ctx != nullptr, VO_ERR_ARG, "vo_ba_testing_k1: null context");

@@ -2048,11 +2048,16 @@ class BAEngine {
         sys_len_ = (size_t)(F + band_.s) * CS + 1;
         cost_off_ = (long)sys_len_ - 1;
         pad = band_slot_stride(w);  // the ring loader's last LDS-DMA piece reads past the end
-        band_lds_ = band_lds_layout(F, band_, P.n_poses);
+        band_lds_ = band_lds_layout(F, band_, P.n_poses, !ctx_->ba_no_split);
         band_tab_ = band_tables(F, band_, band_lds_);
         o_band_tab = pack.add(band_tab_.tab);
         band_set_attributes(band_lds_);  // (a no-op unless the LDS size grows)
-        if (!band_lds_.full) d_fac_.reserve(band_fac_doubles(F, w) * 8);
+        if (!band_lds_.full || band_lds_.split) d_fac_.reserve(band_fac_doubles(F, w) * 8);
+        if (band_lds_.split) {  // the split hand-offs' exchange area (front of fac); flags start clear
+          const SplitXch x = split_xch(band_tab_.n_merge, band_.s);
+          VO_REQUIRE((size_t)x.end() <= band_fac_doubles(F, w), VO_ERR_STATE, "band split: exchange area");
+          VO_HIP_CHECK(hipMemsetAsync(d_fac_.as<double>() + x.flag, 0, 3 * 16 * sizeof(double), st));
+        }
       } else {
         for (int b = 0; b < nprof; ++b) red_dst_[b] = 36 * b;
         for (int f = 0; f < F; ++f) red_rdst_[f] = 36 * nprof + 6 * f;
@@ -2094,7 +2099,8 @@ class BAEngine {
       // MI355X's 256 CUs (fewer CUs, e.g. a partitioned device: K2 stays a launch of its own)
       // (full mode only: the ring-mode solver reads sys with plain loads, so it must come from an
       // earlier launch)
-      fuse_ok_ = VO_BA_FUSE && band_on_ && band_lds_.full && band_fused_workgroups(nprof) + 1 <= ctx_->num_cus;
+      fuse_ok_ = VO_BA_FUSE && band_on_ && band_lds_.full && !band_lds_.split &&
+                 band_fused_workgroups(nprof) + 1 <= ctx_->num_cus;
 
       // one page-locked staging buffer, one device buffer, one copy (each table a pageable
       // copy of its own cost several µs of host time apiece); both are rewritten only after the
@@ -2335,11 +2341,13 @@ class BAEngine {
 
   int stats(int64_t* out, int n) const {
     const BAPlan& P = plan_;
-    int64_t v[11 + kSetupSections] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), (int64_t)P.slot_i.size(),
+    int64_t v[12 + kSetupSections] = {P.n_chunks(), P.n_segments(), P.n_slab_slots(), (int64_t)P.slot_i.size(),
                                       P.n_prof_blocks(), P.n_te, P.algorithmic_bytes_per_iter(), band_on_ ? 1 : 0,
                                       P.reused_groups, P.reused_chunks, P.seg_obs};
     for (int i = 0; i < kSetupSections; ++i) v[11 + i] = setup_ns_[i];  // the last setup's sections
-    const int k = std::min(n, 11 + kSetupSections);
+    // the banded K3's layout: 0 none (profile solver), 1 full, 2 ring, 3 split (two workgroups)
+    v[11 + kSetupSections] = !band_on_ ? 0 : band_lds_.split ? 3 : band_lds_.full ? 1 : 2;
+    const int k = std::min(n, 12 + kSetupSections);
     for (int i = 0; i < k; ++i) out[i] = v[i];
     return k;
   }
@@ -2514,7 +2522,8 @@ class BAEngine {
       B.tab = d_band_tab_.as<int>();
       B.sys = A.sys;
       B.zero = d_zero_.as<double>();
-      B.fac = band_lds_.full ? nullptr : d_fac_.as<double>();
+      B.fac = band_lds_.full && !band_lds_.split ? nullptr : d_fac_.as<double>();
+      B.seq = ++band_seq_ == 0 ? ++band_seq_ : band_seq_;  // split hand-off flags: new every launch
       B.cost_out = A.cost_out;
       B.dc = A.dc;
       B.pose_cur = A.pose_cur;
@@ -2643,6 +2652,7 @@ class BAEngine {
   BandSplit band_{};
   bool band_on_ = false;
   bool fuse_ok_ = false;  // K2 fused into K3's launch (see fused())
+  unsigned band_seq_ = 0;  // split-mode K3 launches so far (their hand-off flag values)
   BandLds band_lds_;
   BandTables band_tab_;
   // views into d_tab_ (the plan's small tables, one upload per setup) and d_misc_

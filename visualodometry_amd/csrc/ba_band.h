@@ -38,10 +38,11 @@ struct BandTables {
 // the 1 KiB pad after the side, with the K2 values of the following column).
 struct BandLds {
   bool full = false;
+  bool split = false;  // two workgroups, one per side, each side's columns in full in its own LDS
   int rc = 0, ss = 0, pad = 0;  // slots per side, doubles per slot, doubles after each side
   size_t bytes = 0;
 };
-BandLds band_lds_layout(int F, const BandSplit& b, int n_poses);
+BandLds band_lds_layout(int F, const BandSplit& b, int n_poses, bool allow_split = true);
 BandTables band_tables(int F, const BandSplit& b, const BandLds& L);
 
 // K2 writes the reduced camera system in the banded layout (ba.hip, red_dst_): per side,
@@ -68,6 +69,7 @@ struct BandArgs {
   // bit), store them write-through (sc1) and count themselves in red_count's shards; workgroup
   // 0, the solver, reads sys (by sc1 loads only) after every shard reached its count, and takes
   // the counts back off (zero between launches).
+  unsigned seq;  // split mode: this launch's hand-off flag value (nonzero, new every launch)
   int nred;
   int red_drop;  // test switch (host only): reducer workgroups left out of the launch
   unsigned* red_count;   // F + 1 column readiness counters, kBandRedShardStride words apart
@@ -75,6 +77,23 @@ struct BandArgs {
   const int* col_need;   // per counter: the items that store into that column (F + 1)
   ReduceArgs red;
 };
+// Split mode's exchange area at the front of BandArgs::fac (doubles): the bottom's merge sources
+// (n_merge), the top's separator records (42 doubles a row: L_kk's six rows, 1/diag), the
+// separator's z (6 s), two failure words, and three hand-off flags 128 bytes apart (each set to
+// the launch's seq once its data is out).
+struct SplitXch {
+  long merge, rec, z, fail, flag;
+  __host__ __device__ long end() const { return flag + 3 * 16; }
+};
+__host__ __device__ inline SplitXch split_xch(int n_merge, int s) {
+  SplitXch x;
+  x.merge = 0;
+  x.rec = (n_merge + 15) / 16 * 16;
+  x.z = x.rec + (42L * s + 15) / 16 * 16;
+  x.fail = x.z + (6L * s + 15) / 16 * 16;
+  x.flag = x.fail + 16;
+  return x;
+}
 // Status word flag: the fused launch's solver gave up waiting for its reducers (the low bits
 // are the iteration, as for a failed factorisation).
 constexpr int kBandStatusTimeout = 1 << 30;

@@ -58,7 +58,7 @@ static size_t band_lds_total(const BandLds& L, int F, int n_poses) {
   return 8 * (2 * ((size_t)L.rc * L.ss + L.pad) + 6 * (size_t)F + 12 * (size_t)n_poses + 104);
 }
 
-BandLds band_lds_layout(int F, const BandSplit& b, int n_poses) {
+BandLds band_lds_layout(int F, const BandSplit& b, int n_poses, bool allow_split) {
   BandLds L;
   const int CS = band_col_stride(b.w);
   L.full = true;
@@ -67,6 +67,14 @@ BandLds band_lds_layout(int F, const BandSplit& b, int n_poses) {
   L.pad = 128;
   L.bytes = band_lds_total(L, F, n_poses);
   if (L.bytes <= kBandLdsMax) return L;
+  // split: each side's columns in full in its own workgroup's LDS (plus the bottom's staged copy
+  // of the top's separator records), two workgroups on two CUs
+  if (b.s > 0 && allow_split) {
+    L.split = true;
+    L.bytes = 8 * ((size_t)L.rc * L.ss + L.pad + 6 * (size_t)F + 12 * (size_t)n_poses + 104 + 42 * (size_t)b.s);
+    if (L.bytes <= kBandLdsMax) return L;
+    L.split = false;
+  }
   L.full = false;
   L.rc = b.w + 4;
   L.ss = band_slot_stride(b.w);
@@ -348,11 +356,34 @@ struct SysLoads {
   }
 };
 
+// Split mode's hand-offs between the two workgroups (same protocol as the fused reducers': the
+// producer's stores write-through (sc1) and drained, then one relaxed agent-scope store of the
+// flag; the consumer polls the flag relaxed and reads the data by sc1 loads only, after a
+// workgroup barrier behind its poll).  Bounded: false after ~seconds (a workgroup that never
+// arrived fails the solve instead of hanging it).
+__device__ __forceinline__ void xch_flag_set(double* fac, long flag, unsigned seq) {
+  __hip_atomic_store((gu32*)(fac + flag), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool xch_flag_wait(const double* fac, long flag, unsigned seq) {
+  unsigned spins = 0;
+  while (__hip_atomic_load((gu32*)(fac + flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 22)) return false;
+  }
+  return true;
+}
+
 // Loads below never feed a select or branch before their first real use: a value that
 // must be zero is loaded from the zero block (A.zero) instead, so the waitcnt pass can
 // leave every prefetch in flight.
-template <bool kFull>
+// kMode: 0 ring (one workgroup, factor records in global memory), 1 full (one workgroup, both
+// sides' columns in LDS), 2 split (one workgroup of four waves per side, each side's columns in
+// its own CU's LDS; the separator's bottom contributions, the top's separator records and the
+// separator's z cross over through global memory once each: see the split hand-offs below).
+template <int kMode>
 __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
+  constexpr bool kFull = kMode != 0, kSplit = kMode == 2;
+  constexpr int NT = kSplit ? kBandThreads / 2 : kBandThreads;  // threads of this workgroup
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int s_fail;
   __shared__ __attribute__((aligned(16))) double s_zero[40];   // full mode's zero block
@@ -361,6 +392,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
 #endif
   // wave (so role and side) is wave-uniform: readfirstlane lets the compiler branch on SGPRs
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  // split mode: workgroup s is side s, its four waves the side's four roles
   if (A.nred > 0 && blockIdx.x > 0) {  // fused K2: a reducer workgroup (uniform branch)
     band_reduce_wg(A, blockIdx.x - 1, dyn);
     return;
@@ -374,13 +406,16 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   const int prior_word = A.status ? *A.status : 0;
   const bool prior_status = prior_word != 0;
   double* ringT = dyn;
-  double* ringB = ringT + RC * SS + SPAD;
+  double* ringB = kSplit ? dyn : ringT + RC * SS + SPAD;  // split: each workgroup holds its own side
   double* zs = ringB + RC * SS + SPAD;  // back substitution: z (6F)
   double* pose_l = zs + 6 * F;
   // a zero block (masked loads) and a dummy row (masked stores), dyn offsets
   const int ZOFF = (int)(pose_l - dyn) + 12 * A.n_poses, DOFF = ZOFF + 40;
+  // split mode, bottom workgroup: the top's separator records, 42 doubles a row (L_kk, 1/diag)
+  double* const sepT = dyn + DOFF + 64;
+  const SplitXch xch = split_xch(A.n_merge, A.s);
 
-  const int side = wave & 1, role = wave >> 1;
+  const int side = kSplit ? (int)blockIdx.x : wave & 1, role = kSplit ? wave : wave >> 1;
   const bool sbot = side == 1;
   // this wave's side: ring (column v in slot v mod RC), factor records (column v at v *
   // CS: global memory, or the full-mode slots themselves), column sources, columns
@@ -396,12 +431,12 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   if (tid < 40) dyn[ZOFF + tid] = 0.0;
   // the poses for the tail's update, staged now (their load latency under the prologue's,
   // or under the wait for the fused launch's reducers)
-  for (int e = tid; e < 12 * A.n_poses; e += kBandThreads) pose_l[e] = A.pose_cur[e];
+  for (int e = tid; e < 12 * A.n_poses; e += NT) pose_l[e] = A.pose_cur[e];
   // fused K2 (one rank): sys is read column by column, each after its reducers have counted
   // themselves (the prologue's poll loop); a timeout fails the solve (status) without using what was read
-  const bool fused = kFull && A.nred > 0;
+  const bool fused = kFull && !kSplit && A.nred > 0;
   __shared__ int s_late;  // a column's reducers never arrived
-  if (fused) {
+  if (fused || kSplit) {  // (split mode: a hand-off that never arrived)
     if (tid == 0) s_late = 0;
     __syncthreads();
   }
@@ -499,23 +534,27 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       }
     }
   } else {
-    if (tid == 0 && A.cost_out) *A.cost_out = A.sys[A.cost_off];  // plain-sys-read: not fused
+    if (tid == 0 && A.cost_out && side == 0) *A.cost_out = A.sys[A.cost_off];  // plain-sys-read: not fused
     // Prologue: columns 0 .. w + 1 of both sides (contiguous in K2's layout), every 16-byte
     // load in flight, then the stores.  The loads do not wait for the status word (one
     // global round trip less on the launch's path); a failed earlier solve only skips the
     // stores.
-    const int nT = min(w + 2, ncolT) * CS / 2, nB = min(w + 2, ncolB) * CS / 2;  // double2 pieces
+    // (split mode: each workgroup its own side's columns)
+    const int nT = kSplit && sbot ? 0 : min(w + 2, ncolT) * CS / 2;  // double2 pieces
+    const int nB = kSplit && !sbot ? 0 : min(w + 2, ncolB) * CS / 2;
+    static_assert((kBandMaxW + 2) * (36 * (kBandMaxW + 1) + 12) / 2 <= kProLoads * kBandThreads / 2,
+                  "split prologue: one side's columns per four-wave workgroup");
     double2 v[kProLoads];
 #pragma unroll
     for (int u = 0; u < kProLoads; ++u) {
-      const int e = tid + u * kBandThreads;
+      const int e = tid + u * NT;
       const long o2 = e < nT ? e : (long)ncolT * CS / 2 + (e - nT);
       v[u] = e < nT + nB ? reinterpret_cast<const double2*>(A.sys)[o2] : make_double2(0.0, 0.0);  // plain-sys-read: not fused
     }
     if (!prior_status)
 #pragma unroll
     for (int u = 0; u < kProLoads; ++u) {
-      const int e = tid + u * kBandThreads;
+      const int e = tid + u * NT;
       const bool top = e < nT;
       const int x = 2 * (top ? e : e - nT), col = x / CS;
       if (e < nT + nB)
@@ -529,7 +568,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // earlier launch): LDS-DMA.  The ring-mode kernel carries no sc1 path (its registers and the
   // buffer descriptor pushed it past 256 VGPRs into spills: cfg4 K3 77 -> 89 us).
   const int nDma = CSP / 128;
-  const bool ld_sc1 = kFull && A.nred > 0;
+  const bool ld_sc1 = kFull && !kSplit && A.nred > 0;
   static_assert(36 * (kBandMaxW + 1) + 12 <= 3 * 128, "at most three 1 KiB pieces per column");
   double2 ldv[3];
   int ld_pend = -1;  // the column whose pieces are in ldv
@@ -813,7 +852,11 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     const int e2 = eb ? bi - nt : bi, k = e2 / w + (set == 0 ? 0 : eb ? nb : m), qq = e2 % w + 1, i = k - qq;
     if (i < 0 || (eb && i >= nb)) return;
     double* fs = eb ? ringB : ringT;
-    const double* rec = (eb && k >= nb) ? ringT + (long)(F - 1 - k) * CS : fs + (long)k * CS;
+    // the bottom side's pseudo rows take the top's separator record (split mode: its staged copy,
+    // 42 doubles a row with 1/diag at 36)
+    const bool xrec = eb && k >= nb;
+    const double* rec = xrec ? (kSplit ? sepT + 42l * (F - 1 - k - m) : ringT + (long)(F - 1 - k) * CS) : fs + (long)k * CS;
+    const int roff = kSplit && xrec ? 36 : 36 * R + 6;
     double L[21], r[6], gv[6];
 #pragma unroll
     for (int ii = 0; ii < 6; ++ii)
@@ -823,7 +866,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
         L[P6(ii, c)] = v.x;
         if (c + 1 <= ii) L[P6(ii, c + 1)] = v.y;
       }
-    ld6g(rec + 36 * R + 6, r);
+    ld6g(rec + roff, r);
     double* col = fs + (long)i * CS + 36 * qq + s2;
 #pragma unroll
     for (int c = 0; c < 6; ++c) gv[c] = col[6 * c];
@@ -833,7 +876,7 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   };
 
   if (!prior_fail) {
-    const int PA = max(m, nb);
+    const int PA = kSplit ? sna : max(m, nb);
     int sk = 0, skm = RC - 1;
     for (int p = 0; p < PA; ++p) {
       const bool on = p < sna;
@@ -847,6 +890,10 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
           if (p + 1 < snload) chain_post(sk1);
         } else {
           side_step(p, sk, skm);
+          // split mode: the loader (half idle: its DMA waits) forms the G blocks of row p - 1,
+          // final since step p - 1 (its diagonal block) and unused by any later step; a side's
+          // last row follows after phase A
+          if (kSplit && role == kLoad && p >= 1 && lane < 6 * w) g_item(0, 6 * ((sbot ? m * w : 0) + (p - 1) * w) + lane);
         }
       }
       BST(3);
@@ -857,16 +904,49 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
       // both sides' state of the separator into the rings, the bottom's contributions
       // merged into the top's (fixed order), then the top continues through the separator
       if (act) st6g(sring + (sna % RC) * SS + 36 * q + 6 * sr, P);
-      __syncthreads();
-      for (int e = tid; e < A.n_merge; e += kBandThreads) {
-        const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
-        dyn[d.x] += dyn[d.y];
+      if constexpr (kSplit) {
+        // split hand-off 0: the bottom's separator contributions (the merge table's sources,
+        // at their offsets in a two-ring layout less offB) and its failure word go out; the
+        // top adds them in the table's order, as the one-workgroup merge does
+        const int offB = RC * SS + SPAD;
+        if (lane == 0 && bad) s_fail = 1;
+        __syncthreads();
+        if (sbot) {
+          for (int e = tid; e < A.n_merge; e += NT) {
+            const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
+            st_sc1(A.fac + xch.merge + e, dyn[d.y - offB]);
+          }
+          if (tid == 0) st_sc1(A.fac + xch.fail, s_fail ? 1.0 : 0.0);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (tid == 0) xch_flag_set(A.fac, xch.flag, A.seq);
+          // the G blocks of the bottom's last row (the loader formed the others during phase A)
+          for (int e = tid; e < 6 * w; e += NT) g_item(0, 6 * (m * w + (nb - 1) * w) + e);
+        } else {
+          if (tid == 0 && !xch_flag_wait(A.fac, xch.flag, A.seq)) s_late = 1;
+          for (int e = tid; e < 6 * w; e += NT) g_item(0, 6 * (m - 1) * w + e);  // the top's last row
+          __syncthreads();
+          const SysLoads xl(A.fac, xch.end());
+          for (int e = tid; e < A.n_merge; e += NT) {
+            const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
+            dyn[d.x] += xl.ld(xch.merge + e);
+          }
+          if (tid == 0 && (s_late || xl.ld(xch.fail) != 0.0)) s_fail = 1;
+          __syncthreads();
+          if (act) ld6g(ringT + (m % RC) * SS + 36 * q + 6 * sr, P);
+        }
+      } else {
+        __syncthreads();
+        for (int e = tid; e < A.n_merge; e += NT) {
+          const int2 d = reinterpret_cast<const int2*>(A.tab + A.merge)[e];
+          dyn[d.x] += dyn[d.y];
+        }
+        __syncthreads();
+        if (act && side == 0) ld6g(ringT + (m % RC) * SS + 36 * q + 6 * sr, P);
       }
-      __syncthreads();
-      if (act && side == 0) ld6g(ringT + (m % RC) * SS + 36 * q + 6 * sr, P);
       BST(4);
       int sk = m % RC, skm = sk == 0 ? RC - 1 : sk - 1;
-      for (int p = m; p < m + sp; ++p) {
+      for (int p = m; p < (kSplit && sbot ? m : m + sp); ++p) {
         const int sk1 = sk + 1 == RC ? 0 : sk + 1;
         if (role == kChain && side == 0) chain_pre(p, sk);
         BST(5);
@@ -902,6 +982,30 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // factor records written
   BST(8);
   __syncthreads();
+  if constexpr (kSplit) {
+    // split hand-off 1: the top's separator records (L_kk's rows and 1/diag: the bottom's pseudo
+    // rows form their G blocks from them) and the top's failure word (both sides' phase-A state
+    // and the separator's) out; the bottom stages the records in sepT
+    if (!prior_fail && sp > 0) {
+      if (!sbot) {
+        for (int e = tid; e < 42 * sp; e += NT) {
+          const int k = m + e / 42, o = e % 42;
+          st_sc1(A.fac + xch.rec + e, ringT[(long)k * SS + (o < 36 ? o : 36 * R + 6 + (o - 36))]);
+        }
+        if (tid == 0) st_sc1(A.fac + xch.fail + 1, s_fail ? 1.0 : 0.0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) xch_flag_set(A.fac, xch.flag + 16, A.seq);
+      } else {
+        if (tid == 0 && !xch_flag_wait(A.fac, xch.flag + 16, A.seq)) s_late = 1;
+        __syncthreads();
+        const SysLoads xl(A.fac, xch.end());
+        for (int e = tid; e < 42 * sp; e += NT) sepT[e] = xl.ld(xch.rec + e);
+        if (tid == 0 && (s_late || xl.ld(xch.fail + 1) != 0.0)) s_fail = 1;
+        __syncthreads();
+      }
+    }
+  }
   BST(9);
   const bool failed = s_fail != 0;
 
@@ -914,8 +1018,16 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // Full mode, the rest of the G blocks (rows the separator phase finalised: the top's
   // separator rows and the bottom side's pseudo rows), then the back substitution.
   if (kFull && !failed) {
-    const int nR = 6 * (sp > 0 ? 2 * sp * w : m * w);  // one-sided windows: every top row here
-    for (int e = tid; e < nR; e += kBandThreads) g_item(sp > 0 ? 1 : 0, e);
+    if constexpr (kSplit) {  // the top: its separator rows
+      if (!sbot) {  // (its rows before the separator: during phase A and after it)
+        for (int e = tid; e < 6 * sp * w; e += NT) g_item(1, e);
+      } else {  // the bottom: its pseudo rows (its own rows: during phase A and after it)
+        for (int e = 6 * sp * w + tid; e < 12 * sp * w; e += NT) g_item(1, e);
+      }
+    } else {
+      const int nR = 6 * (sp > 0 ? 2 * sp * w : m * w);  // one-sided windows: every top row here
+      for (int e = tid; e < nR; e += NT) g_item(sp > 0 ? 1 : 0, e);
+    }
     __syncthreads();
   }
   BST(16);
@@ -1120,6 +1232,21 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
     BST(10);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm z stores retired
     __syncthreads();  // the separator's z in LDS
+    if constexpr (kSplit) {
+      // split hand-off 2: the separator's z (the bottom's pseudo steps read it)
+      if (!sbot) {
+        for (int e = tid; e < 6 * sp; e += NT) st_sc1(A.fac + xch.z + e, zs[6 * m + e]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) xch_flag_set(A.fac, xch.flag + 32, A.seq);
+      } else {
+        if (tid == 0 && !xch_flag_wait(A.fac, xch.flag + 32, A.seq)) s_late = 1;
+        __syncthreads();
+        const SysLoads xl(A.fac, xch.end());
+        for (int e = tid; e < 6 * sp; e += NT) zs[6 * m + e] = xl.ld(xch.z + e);
+        __syncthreads();
+      }
+    }
     BST(11);
     if (role == kChain && side == 0 && m > 0) {
       if (sp == 0) bs_init(m - 1, INT_MAX);
@@ -1137,10 +1264,13 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
 
   // x_k = L_kk^-T z_k for every row at once, then the pose update
   const double* const recB = kFull ? ringB : A.fac + (long)ncolT * CS;
-  for (int c = tid; c < A.n_poses; c += kBandThreads) {
+  // (split mode: the late flag of a hand-off the bottom waited on after its failure verdict)
+  const bool failed2 = failed || (kSplit && s_late != 0);
+  for (int c = tid; c < A.n_poses; c += NT) {
+    if (kSplit && (c >= A.n_fixed && c - A.n_fixed >= ncolT) != sbot) continue;  // the other side's poses
     const double* T = pose_l + 12 * c;
     double* out = A.pose_next + 12l * c;
-    if (failed || c < A.n_fixed) {
+    if (failed2 || c < A.n_fixed) {
       for (int e = 0; e < 12; ++e) out[e] = T[e];
       if (c >= A.n_fixed)
         for (int e = 0; e < 6; ++e) A.dc[6 * (c - A.n_fixed) + e] = 0.0;
@@ -1166,14 +1296,17 @@ __global__ __launch_bounds__(kBandThreads) void ba_band_kernel(BandArgs A) {
   // A timeout is recorded whatever the earlier status (the counter then holds this launch's
   // reducers: the host re-zeroes it when it reads the flag); a failed factorisation only when
   // no earlier step failed (the status names the first failed iteration).
-  if (tid == 0) {
-    if (!reduced) *A.status = (prior_status ? prior_word : A.iter_tag) | kBandStatusTimeout;
+  // (split mode: either workgroup records a hand-off that never arrived; the factorisation's
+  // verdict, which both hold, by the top one)
+  const bool late = !reduced || (kSplit && s_late != 0);
+  if (tid == 0 && (late || !kSplit || !sbot)) {
+    if (late) *A.status = (prior_status ? prior_word : A.iter_tag) | kBandStatusTimeout;
     else if (failed && !prior_status) *A.status = A.iter_tag;
   }
   BST(14);
 #if VO_BA_STAMPS
   if (lane == 0 && A.stamps)
-    for (int i = 0; i < kBandStamps; ++i) A.stamps[kBandStamps * wave + i] = st_acc[i];
+    for (int i = 0; i < kBandStamps; ++i) A.stamps[kBandStamps * (kSplit ? 2 * wave + side : wave) + i] = st_acc[i];
 #endif
 }
 
@@ -1192,7 +1325,7 @@ void band_set_attributes(const BandLds& L) {
   const int lds = (int)band_launch_lds(L, true);
   int cur = set.load(std::memory_order_relaxed);
   if (lds <= cur) return;
-  const void* fs[2] = {(const void*)ba_band_kernel<true>, (const void*)ba_band_kernel<false>};
+  const void* fs[3] = {(const void*)ba_band_kernel<0>, (const void*)ba_band_kernel<1>, (const void*)ba_band_kernel<2>};
   for (const void* f : fs) VO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   while (cur < lds && !set.compare_exchange_weak(cur, lds, std::memory_order_relaxed)) {
   }
@@ -1203,10 +1336,12 @@ void launch_band_solve(const BandArgs& A, const BandLds& L, hipStream_t st) {
   // fewer than the solver waits for: vo_ba_testing_drop_reducers)
   const dim3 grid(1 + std::max(A.nred - std::max(A.red_drop, 0), 0));
   const size_t lds = band_launch_lds(L, A.nred > 0);
-  if (L.full)
-    hipLaunchKernelGGL((ba_band_kernel<true>), grid, dim3(kBandThreads), lds, st, A);
+  if (L.split)  // one workgroup of four waves per side (K2 never fused: BAEngine::fused)
+    hipLaunchKernelGGL((ba_band_kernel<2>), dim3(2), dim3(kBandThreads / 2), lds, st, A);
+  else if (L.full)
+    hipLaunchKernelGGL((ba_band_kernel<1>), grid, dim3(kBandThreads), lds, st, A);
   else
-    hipLaunchKernelGGL((ba_band_kernel<false>), grid, dim3(kBandThreads), lds, st, A);
+    hipLaunchKernelGGL((ba_band_kernel<0>), grid, dim3(kBandThreads), lds, st, A);
 }
 
 }  // namespace vo
