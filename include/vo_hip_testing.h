@@ -63,6 +63,13 @@ int vo_pnp_testing_split(vo_ctx* ctx, int h1);
  * every frame, *tail_frames frames whose hypotheses [h1, iterations) were solved too. */
 int vo_pnp_testing_last_split(vo_ctx* ctx, int* h1, int* tail_frames);
 
+/* Test switch: the EPnP hypothesis kernel of the context's PnP calls.  0: the default (lane
+ * groups while the hypotheses fit one wave per SIMD, else one lane per hypothesis); 1: lane groups
+ * always; -1: one lane per hypothesis always.  Both kernels compute the same bits (the groups'
+ * Jacobi steps are the serial sweep's rotations in the same order per row), which the GPU tests
+ * check on one batch through both. */
+int vo_pnp_testing_group(vo_ctx* ctx, int mode);
+
 #ifdef __cplusplus
 }
 #endif

@@ -36,8 +36,8 @@ def test_product_header_has_no_test_entry_points():
     assert "vo_comm_init_loopback" not in header_functions(_lib.HEADER)
     assert header_functions(_lib.TEST_HEADER) == ["vo_ba_split_reduce", "vo_ba_testing_drop_reducers",
                                                   "vo_ba_testing_k1", "vo_ba_testing_no_split",
-                                                  "vo_ba_testing_plan_slide", "vo_comm_init_loopback", "vo_pnp_testing_last_split",
-                                                  "vo_pnp_testing_split"]
+                                                  "vo_ba_testing_plan_slide", "vo_comm_init_loopback", "vo_pnp_testing_group",
+                                                  "vo_pnp_testing_last_split", "vo_pnp_testing_split"]
 
 
 def test_no_device_fails_loudly(monkeypatch):

@@ -187,6 +187,23 @@ def test_split_replay_large_frames(ctx, h1):
         _check((bool(st1[f, 0]), pose1[f, :3], pose1[f, 3:], mask1[off[f]:off[f + 1]]), ref)
 
 
+def test_group_kernel_equals_lane_kernel(ctx):
+    """The lane-group hypothesis kernel (single frames: EPnP's 12 x 12 Jacobi SVD spread over a
+    group's lanes in the index-sum step order, the beta kinds on separate lanes) and the
+    one-lane-per-hypothesis kernel (the serial sweep): the same bits in every pose, mask and
+    count of one batch of mixed frames (1025-4000-point frames included)."""
+    Xs, Us, K = _split_cases(40, 700, 700, big={7: 1025, 19: 4000})
+    out = []
+    try:
+        for mode in (1, -1):
+            _lib.pnp_testing_group(ctx, mode)
+            out.append(_run_batch(ctx, Xs, Us, K))
+    finally:
+        _lib.pnp_testing_group(ctx, 0)
+    for a, b in zip(out[0][1:], out[1][1:]):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_split_auto_large_batch(ctx):
     """A batch of more hypotheses than one wave per SIMD holds splits by itself; the results
     are the bits of the all-at-once run."""

@@ -63,6 +63,13 @@ out["process_image_gpu_in_place"] = bool(f["descriptors"].is_cuda) and not getat
 out["keypoints"] = int(f["keypoints"].shape[1])
 out["process_image_gpu_ms"] = timed(lambda: pi(fe, img), reps=10)
 out["process_image_host_ms"] = timed(lambda: reference_body(fe, img), reps=10)
+_lib.profile_enable(ctx, True)
+for _ in range(5):
+    pi(fe, img)
+prof = _lib.profile_read(ctx)
+_lib.profile_enable(ctx, False)
+out["process_image_kernel_us"] = {k: round(v[0] / v[1] * 1e3, 2) for k, v in prof.items()}
+out["process_image_kernel_launches"] = {k: v[1] // 5 for k, v in prof.items()}
 d0, d1 = sift_like_pair(4000, 4000, 7)
 t0, t1 = torch.from_numpy(d0)[None].to(dev), torch.from_numpy(d1)[None].to(dev)
 fr = SimpleNamespace(conf=SimpleNamespace(extractor_type="sift", match_on_gpu=True))

@@ -113,6 +113,7 @@ SIGNATURES = {
     "vo_ba_testing_drop_reducers": (_I, [_P, _I]),
     "vo_ba_testing_k1": (_I, [_P, _I]),
     "vo_pnp_testing_split": (_I, [_P, _I]),
+    "vo_pnp_testing_group": (_I, [_P, _I]),
     "vo_pnp_testing_last_split": (_I, [_P, _PI32, _PI32]),
     "vo_ba_testing_plan_slide": (_I, [C.c_void_p, C.c_void_p, _I, _I, C.POINTER(C.c_uint64), _PI64]),
 }
@@ -307,6 +308,12 @@ def ba_testing_k1(ctx: "Context", variant: int = 0) -> None:
     """Test switch: the K1 variant of the context's later setups (0 default, -1 four-wave K1,
     n = 1..6 one-wave K1 with n chunks per segment); see vo_ba_testing_k1."""
     check(ctx.lib.vo_ba_testing_k1(ctx.handle, int(variant)), "vo_ba_testing_k1")
+
+
+def pnp_testing_group(ctx: "Context", mode: int = 0) -> None:
+    """Test switch: the EPnP hypothesis kernel (0 auto, 1 lane groups, -1 one lane per
+    hypothesis); see vo_pnp_testing_group."""
+    check(ctx.lib.vo_pnp_testing_group(ctx.handle, int(mode)), "vo_pnp_testing_group")
 
 
 def pnp_testing_split(ctx: "Context", h1: int = 0) -> None:

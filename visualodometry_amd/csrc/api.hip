@@ -893,6 +893,14 @@ int vo_ba_testing_k1(vo_ctx* ctx, int variant) {
   });
 }
 
+int vo_pnp_testing_group(vo_ctx* ctx, int mode) {
+  return guarded([&] {
+    VO_REQUIRE(ctx != nullptr, VO_ERR_ARG, "vo_pnp_testing_group: null context");
+    VO_REQUIRE(mode >= -1 && mode <= 1, VO_ERR_ARG, "vo_pnp_testing_group: mode %d outside -1..1", mode);
+    ctx->pnp_group = mode;
+  });
+}
+
 int vo_pnp_testing_split(vo_ctx* ctx, int h1) {
   return guarded([&] {
     VO_REQUIRE(ctx != nullptr, VO_ERR_ARG, "vo_pnp_testing_split: null context");

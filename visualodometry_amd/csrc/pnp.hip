@@ -592,7 +592,7 @@ void pnp_run(vo_ctx* ctx, const float* d_X, const float* d_uv, const int32_t* of
     ctx->prof.begin(ctx->stream, kid_hyp);
     // lane groups while they fit one wave per SIMD (small batches: the single frame of vo.py's
     // tracking step, 100 hypotheses); one lane per hypothesis beyond (the same bits either way)
-    if ((long)nh * kPnpGroupLanes <= fill)
+    if (ctx->pnp_group > 0 || (ctx->pnp_group == 0 && (long)nh * kPnpGroupLanes <= fill))
       pnp_hyp_group_launch(a, h_lo, h_hi, need_in, nh, ctx->stream);
     else
       hipLaunchKernelGGL(pnp_hyp_kernel, dim3(ceil_div(nh, 64)), dim3(64), 0, ctx->stream, a, h_lo, h_hi, need_in);

@@ -34,7 +34,7 @@ __device__ __forceinline__ void load3(const float* X, int i, float (&M)[3]) {
 }
 
 // lanes per hypothesis of the group kernel (pnpm::Svd12Alt's groups)
-constexpr int kPnpGroupLanes = 8;
+constexpr int kPnpGroupLanes = pnpm::kSvdGroupLanes;
 // Hypotheses [h_lo, h_hi) of every frame (of the frames with need[f] != 0), kPnpGroupLanes lanes
 // each; nh = batch * (h_hi - h_lo).  Enqueued on st.
 void pnp_hyp_group_launch(const PnpArgs& a, int h_lo, int h_hi, const int32_t* need, int nh, hipStream_t st);

@@ -15,7 +15,8 @@ using namespace pnpm;
 // leaves the chip idle and the latency of one EPnP chain is the call's): every lane of a group
 // runs the hypothesis's serial parts redundantly (same inputs, same values), and EPnP's 12 x 12
 // Jacobi SVD runs on the group's lanes.  Step t of a sweep takes the pairs (i, j) with i + j == t
-// (at most six, disjoint), one lane each: in the cyclic order JacobiSVDImpl_ runs, every pair
+// (at most six, disjoint), two lanes each (half a row's elements per lane, the sums continued
+// from one lane to the other in the serial order): in the cyclic order JacobiSVDImpl_ runs, every pair
 // touching row i or j comes before (i, j) exactly when its index sum is below i + j, so each row
 // receives the same rotations in the same order, and the result is jacobi_rows' bit for bit.  A
 // sweep is 21 dependent steps instead of 66 pairs.
@@ -25,7 +26,7 @@ constexpr int kSvdDoubles = 12 * 12 + 12;
 // template or a folded argument, changed the batch kernel's register allocation at its
 // 512-register edge: 300 -> 372..756 B of scratch per lane, the batch leg 1.5 % slower.)
 __global__ __launch_bounds__(64) void pnp_hyp_group_kernel(PnpArgs a, int h_lo, int h_hi, const int32_t* need) {
-  static_assert(kPnpGroupLanes == 8, "Svd12Alt's lane groups are 8 lanes");
+  static_assert(kPnpGroupLanes == 16 && 64 % kPnpGroupLanes == 0, "Svd12Alt's lane groups are 16 lanes");
   const int hr = h_hi - h_lo;
   const int k = (blockIdx.x * 64 + threadIdx.x) / kPnpGroupLanes, r = threadIdx.x % kPnpGroupLanes;
   if (k >= a.batch * hr) return;

@@ -185,6 +185,7 @@ struct Jacobi12Steps {
 // at lane), on the host (the host check) serially.  Passed to epnp5 by pointer, nullptr for the
 // cyclic sweep (a template parameter instead changed the batch kernel's register allocation:
 // 300 -> 532 B of scratch per lane).
+constexpr int kSvdGroupLanes = 16;  // lanes per hypothesis of the lane-group SVD (Svd12Alt)
 struct Svd12Alt {
   double* lds;
   int lane;
@@ -195,42 +196,93 @@ struct Svd12Alt {
 #endif
 };
 
-// Svd12Alt: 8 lanes per group on the device (pnp_group.hip), the step order serially on the
+// Svd12Alt: 16 lanes per group on the device (pnp_group.hip), the step order serially on the
 // host.  Device sweeps (svd12_group_null_space fills the rows): step t takes the pairs (i, j)
-// with i + j == t (at most six, disjoint), one lane each, on rows read from the group's LDS and
+// with i + j == t (at most six, disjoint), two lanes each, on rows read from the group's LDS and
 // written back; the group stops after the first sweep without a rotation (a ballot over its
 // lanes).  One wave: its LDS operations complete in order, so a step's writes precede the next
 // step's reads behind an lgkmcnt wait.
 #if defined(__HIP_DEVICE_COMPILE__)
+// 16 lanes per group: lane r takes pair slot r & 7 of a step and half r >> 3 of the pair's rows
+// (elements 6h .. 6h + 5).  The dot product and the two norms stay the serial sum over the row's
+// twelve elements: half 0 sums its six terms from zero, half 1 continues from half 0's partial
+// (one DPP rotation by eight lanes within the 16-lane row each way), so every sum keeps its
+// order; the rotation is per element.  The same values as jacobi_pair on the whole rows.
+__device__ __forceinline__ double svd_xhalf(double v) {  // the value of the lane eight away in the 16-lane row
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x128, 0xF, 0xF, false);  // row_ror:8
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x128, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
 __device__ inline void Svd12Alt::sweeps() const {
+  constexpr double eps = 10.0 * kDblEps;
   double* A = lds;
   double* W = lds + 144;
-  const int r = lane;
-  const uint64_t gmask = 0xFFull << (threadIdx.x & 56);
+  const int q = lane & 7, h = lane >> 3;
+  const uint64_t gmask = 0xFFFFull << (threadIdx.x & 48);
   for (int sweep = 0; sweep < 30; ++sweep) {
     bool changed = false;
     for (int t = 1; t <= 21; ++t) {
-      const int i = (t - 11 > 0 ? t - 11 : 0) + r, j = t - i;
-      if (i < j) {
-        double ai[12], aj[12];
+      const int i = (t - 11 > 0 ? t - 11 : 0) + q, j = t - i;
+      if (i < j) {  // both halves of a slot alike
+        double ai[6], aj[6];
 #pragma unroll
-        for (int k = 0; k < 12; k += 2) {
-          const double2 x = *reinterpret_cast<const double2*>(A + 12 * i + k);
-          const double2 y = *reinterpret_cast<const double2*>(A + 12 * j + k);
+        for (int k = 0; k < 6; k += 2) {
+          const double2 x = *reinterpret_cast<const double2*>(A + 12 * i + 6 * h + k);
+          const double2 y = *reinterpret_cast<const double2*>(A + 12 * j + 6 * h + k);
           ai[k] = x.x;
           ai[k + 1] = x.y;
           aj[k] = y.x;
           aj[k + 1] = y.y;
         }
-        double wi = W[i], wj = W[j], c, sn;
-        if (jacobi_pair<12>(ai, aj, wi, wj, c, sn)) {
+        const double a = W[i], b = W[j];
+        double pm[6];
 #pragma unroll
-          for (int k = 0; k < 12; k += 2) {
-            *reinterpret_cast<double2*>(A + 12 * i + k) = make_double2(ai[k], ai[k + 1]);
-            *reinterpret_cast<double2*>(A + 12 * j + k) = make_double2(aj[k], aj[k + 1]);
+        for (int k = 0; k < 6; ++k) pm[k] = ai[k] * aj[k];
+        double p = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) p = p + pm[k];  // half 0: terms 0 .. 5
+        p = svd_xhalf(p);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) p = p + pm[k];  // half 1: terms 6 .. 11 after half 0's
+        const double ph = svd_xhalf(p);
+        p = h ? p : ph;
+        if (!(fabs(p) <= eps * sqrt(a * b))) {  // jacobi_pair's rotation, the same operations
+          p = p * 2.0;
+          const double beta = a - b, gamma = sqrt(p * p + beta * beta);
+          const bool neg = beta < 0;
+          const double num = neg ? (gamma - beta) * 0.5 : gamma + beta;
+          const double den = neg ? gamma : gamma * 2.0;
+          const double x = sqrt(num / den);
+          const double y = p / (gamma * x * 2.0);
+          const double c = neg ? y : x, sn = neg ? x : y;
+          double t0[6], t1[6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            t0[k] = c * ai[k] + sn * aj[k];
+            t1[k] = -sn * ai[k] + c * aj[k];
           }
-          W[i] = wi;
-          W[j] = wj;
+          double na = 0.0, nb = 0.0;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            na = na + t0[k] * t0[k];
+            nb = nb + t1[k] * t1[k];
+          }
+          na = svd_xhalf(na);
+          nb = svd_xhalf(nb);
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            na = na + t0[k] * t0[k];
+            nb = nb + t1[k] * t1[k];
+          }
+#pragma unroll
+          for (int k = 0; k < 6; k += 2) {
+            *reinterpret_cast<double2*>(A + 12 * i + 6 * h + k) = make_double2(t0[k], t0[k + 1]);
+            *reinterpret_cast<double2*>(A + 12 * j + 6 * h + k) = make_double2(t1[k], t1[k + 1]);
+          }
+          if (h) {
+            W[i] = na;
+            W[j] = nb;
+          }
           changed = true;
         }
       }
@@ -337,10 +389,10 @@ struct EpnpState {
 constexpr int kEpnpColDoubles = kPts * 4 + 4 * 12;  // alphas, v
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// The 12 x 12 part of epnp::compute_pose on a lane group (Svd12Alt's 8 lanes), without M^T M in
-// any lane's registers: lane r builds rows i = r, r + 8 of M^T M straight into the group's LDS
-// rows (each entry the same sum in the same order as the per-lane build), the Jacobi sweeps run
-// as Svd12Alt::run's, lane r then takes the norms of its rows, and every lane reads the twelve
+// The 12 x 12 part of epnp::compute_pose on a lane group (Svd12Alt's 16 lanes), without M^T M in
+// any lane's registers: lane r < 12 builds row r of M^T M straight into the group's LDS rows
+// (each entry the same sum in the same order as the per-lane build), the Jacobi sweeps run on
+// the group (Svd12Alt::sweeps), lane r then takes the norm of its row, and every lane reads the twelve
 // norms and only the four rows it needs (v = the rows of the four smallest, each times 1 / W).
 // Same values as jacobi_rows + the selection below it in epnp5.  Returns the W > DBL_MIN flag.
 __device__ inline bool svd12_group_null_space(const Svd12Alt& g, EpnpState& S, const Cam& K) {
@@ -349,7 +401,7 @@ __device__ inline bool svd12_group_null_space(const Svd12Alt& g, EpnpState& S, c
   const int r = g.lane;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int i = r + 8 * u;
+    const int i = r + kSvdGroupLanes * u;
     if (i < 12) {
       const int c = i / 3, comp = i - 3 * c;
       double row[12];
@@ -391,7 +443,7 @@ __device__ inline bool svd12_group_null_space(const Svd12Alt& g, EpnpState& S, c
   // norms of this lane's rows (jacobi_rows' last loop), then every lane reads all twelve
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int i = r + 8 * u;
+    const int i = r + kSvdGroupLanes * u;
     if (i < 12) {
       double sd = 0.0;
 #pragma unroll

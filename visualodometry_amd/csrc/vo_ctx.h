@@ -115,6 +115,7 @@ struct vo_ctx {
   bool ba_split_reduce = false;  // test/tool switch (vo_ba_split_reduce): K2 never fused into K3
   int ba_drop_reducers = 0;      // test switch (vo_ba_testing_drop_reducers): fused launches short of reducers
   bool ba_no_split = false;      // test switch (vo_ba_testing_no_split): no split band layout at setup
+  int pnp_group = 0;      // test switch (vo_pnp_testing_group): 0 auto, 1 lane groups, -1 one lane per hypothesis
   int pnp_split = 0;      // test/tool switch (vo_pnp_testing_split): 0 auto, -1 never, n > 0 first n hypotheses
   int ba_k1_variant = 0;  // test switch (vo_ba_testing_k1): -1 four-wave K1, n >= 1 one-wave K1 of n chunks per segment
   vo_ctx();
