@@ -107,6 +107,13 @@ def detect_and_compute(gray, nfeatures: int = 0, contrast: float = 0.04, edge: f
     """``SIFT_create(nfeatures, n_layers, contrast, edge, sigma).detectAndCompute(gray, None)``
     -> dict: pt (N, 2), size, angle, response, octave, descriptors (N, 128) float32, in the
     order of ``oracle/sift_ref.detect_and_compute``."""
+    kp, desc = _detect_and_compute_records(gray, nfeatures, contrast, edge, sigma, n_layers, capacity, ctx)
+    return _kp_dict(kp, desc)
+
+
+def _detect_and_compute_records(gray, nfeatures: int, contrast: float, edge: float, sigma: float, n_layers: int,
+                                capacity: int, ctx: _lib.Context | None) -> tuple:
+    """``vo_sift_detect_and_compute`` -> (the N KP_DTYPE records, descriptors (N, 128) float32)."""
     ctx = ctx or _lib.context()
     img = np.ascontiguousarray(np.asarray(gray, dtype=np.uint8))
     if img.ndim != 2:
@@ -122,7 +129,7 @@ def detect_and_compute(gray, nfeatures: int = 0, contrast: float = 0.04, edge: f
                                              kp.ctypes.data_as(C.c_void_p), ptr(desc, C.c_float), C.byref(cnt)),
           "vo_sift_detect_and_compute")
     n = cnt.value
-    return _kp_dict(kp[:n], desc[:n].copy())
+    return kp[:n], desc[:n].copy()
 
 
 def detect_and_compute_torch(gray, nfeatures: int, contrast: float, edge: float, sigma: float, n_layers: int = 3,
@@ -181,38 +188,37 @@ def unpack_device_keypoints(raw: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(raw).view(KP_DTYPE).reshape(raw.shape[:-1])
 
 
-class KeyPoint:
-    """The fields of ``cv2.KeyPoint`` the reference reads (``frontend.py:59``: ``k.pt``)."""
+def _load_keypoint_module():
+    """``lib/_vo_keypoints.so`` (``csrc/kp_objects.c``, built beside libvo_hip.so): the C
+    KeyPoint type and its bulk builder.  Required, like the HIP library: a missing build fails
+    here rather than falling back to a per-object Python loop."""
+    import importlib.machinery
+    import importlib.util
+    from pathlib import Path
+    path = Path(__file__).resolve().parent / "lib" / "_vo_keypoints.so"
+    if not path.exists():
+        raise ImportError(f"{path} is missing: run `make -C visualodometry_amd/csrc` "
+                          "(or __graft_entry__.build())")
+    name = __name__.rsplit(".", 1)[0] + "._vo_keypoints"
+    spec = importlib.util.spec_from_loader(name, importlib.machinery.ExtensionFileLoader(name, str(path)))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
 
-    __slots__ = ("pt", "size", "angle", "response", "octave", "class_id")
 
-    def __init__(self, x, y, size, angle, response, octave):
-        self.pt = (float(x), float(y))
-        self.size = float(size)
-        self.angle = float(angle)
-        self.response = float(response)
-        self.octave = int(octave)
-        self.class_id = -1
+_kpmod = _load_keypoint_module()
+
+#: ``cv2.KeyPoint``'s Python surface (``frontend.py:59`` reads ``k.pt``):
+#: ``KeyPoint(x, y, size, angle=-1, response=0, octave=0, class_id=-1)``; ``pt`` is a fresh
+#: ``(x, y)`` tuple per read and the float fields are float32-stored, as in OpenCV.
+KeyPoint = _kpmod.KeyPoint
 
 
-def _keypoints(r: dict) -> tuple:
-    """KeyPoint objects of a detect_and_compute result: the fields converted to Python floats /
-    ints in bulk (``tolist``), then the slots set directly (no per-field ``float()`` calls)."""
-    pts = r["pt"].astype(np.float64)
-    out = []
-    new, append = KeyPoint.__new__, out.append
-    for pt, size, angle, response, octave in zip(zip(pts[:, 0].tolist(), pts[:, 1].tolist()), r["size"].tolist(),
-                                                  r["angle"].tolist(), r["response"].tolist(),
-                                                  r["octave"].tolist()):
-        k = new(KeyPoint)
-        k.pt = pt
-        k.size = size
-        k.angle = angle
-        k.response = response
-        k.octave = octave
-        k.class_id = -1
-        append(k)
-    return tuple(out)
+def _keypoints(records: np.ndarray) -> tuple:
+    """KeyPoint objects of ``vo_sift_keypoint`` records (KP_DTYPE), in one C loop."""
+    if records.dtype != KP_DTYPE:
+        raise ValueError(f"_keypoints: KP_DTYPE records expected, got {records.dtype}")
+    return _kpmod.build(np.ascontiguousarray(records))
 
 
 class SIFT:
@@ -233,9 +239,9 @@ class SIFT:
     def detectAndCompute(self, image, mask=None, descriptors=None, useProvidedKeypoints=False):
         if mask is not None or useProvidedKeypoints:
             raise NotImplementedError("SIFT.detectAndCompute: masks and provided keypoints are not supported")
-        r = detect_and_compute(image, self.nfeatures, self.contrast, self.edge, self.sigma, self.n_layers,
-                               ctx=self._ctx or _lib.context())
-        return _keypoints(r), (r["descriptors"] if len(r["size"]) else None)
+        kp, desc = _detect_and_compute_records(image, self.nfeatures, self.contrast, self.edge, self.sigma,
+                                               self.n_layers, 1 << 15, self._ctx or _lib.context())
+        return _keypoints(kp), (desc if len(kp) else None)
 
 
 def SIFT_create(nfeatures: int = 0, nOctaveLayers: int = 3, contrastThreshold: float = 0.04,
