@@ -257,6 +257,7 @@ struct SelArgs {
   int cand_cap, cap_img, nfeatures;
   uint32_t* sel;         // (batch, cap_img) record indices in output order
   int32_t* sel_count;    // (batch): kept, or -(the capacity needed) when one overflowed
+  uint32_t* resp;        // (batch, cap_img) scratch: response bits in sorted order
 };
 
 __device__ __forceinline__ bool kp_less2(const float* a, const float* b) {
@@ -268,6 +269,7 @@ __device__ __forceinline__ bool kp_less2(const float* a, const float* b) {
 }
 
 constexpr int kSelThreads = 1024;
+constexpr int kSelUnroll = 4;  // records per thread and round of the select passes
 constexpr int kMaxCapImg = 131072;  // keep[] in LDS: 128 KiB of the select kernel's 160
 
 __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
@@ -314,16 +316,36 @@ __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
   }
   __threadfence_block();
   __syncthreads();
+  // removeDuplicatedSorted flags, and each record's response bits copied out in sorted order
+  // (one gather per record here; the selection passes below then read them coalesced).  Four
+  // records per thread and round, their index and record loads issued before any is used.
+  uint32_t* R = A.resp + base;
   int local = 0;
-  for (int i = tid; i < n; i += kSelThreads) {
-    bool k = true;
-    if (i > 0) {
-      const float* a = A.okp + (long)V[i - 1] * kOkpFloats;
-      const float* c = A.okp + (long)V[i] * kOkpFloats;
-      k = !(a[0] == c[0] && a[1] == c[1] && a[2] == c[2] && a[3] == c[3]);
+  for (int i0 = tid; i0 < n; i0 += kSelUnroll * kSelThreads) {
+    uint32_t v[kSelUnroll], vp[kSelUnroll];
+#pragma unroll
+    for (int j = 0; j < kSelUnroll; ++j) {
+      const int i = min(i0 + j * kSelThreads, n - 1);
+      v[j] = V[i];
+      vp[j] = V[max(i - 1, 0)];
     }
-    keep[i] = k;
-    local += k;
+    float4 c[kSelUnroll], a[kSelUnroll];
+    float rsp[kSelUnroll];
+#pragma unroll
+    for (int j = 0; j < kSelUnroll; ++j) {
+      c[j] = *reinterpret_cast<const float4*>(A.okp + (long)v[j] * kOkpFloats);
+      a[j] = *reinterpret_cast<const float4*>(A.okp + (long)vp[j] * kOkpFloats);
+      rsp[j] = A.okp[(long)v[j] * kOkpFloats + 4];
+    }
+#pragma unroll
+    for (int j = 0; j < kSelUnroll; ++j) {
+      const int i = i0 + j * kSelThreads;
+      if (i >= n) break;
+      const bool k = i == 0 || !(a[j].x == c[j].x && a[j].y == c[j].y && a[j].z == c[j].z && a[j].w == c[j].w);
+      keep[i] = k;
+      R[i] = __float_as_uint(rsp[j]);
+      local += k;
+    }
   }
   if (tid == 0) s_total = 0;
   __syncthreads();
@@ -341,28 +363,44 @@ __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
       if (tid < 256) s_hist[tid] = 0;
       __syncthreads();
       const uint32_t prefix = s_prefix;
-      for (int i = tid; i < n; i += kSelThreads) {
-        if (!keep[i]) continue;
-        const uint32_t bits = __float_as_uint(A.okp[(long)V[i] * kOkpFloats + 4]);
-        if ((bits & mask) == prefix) atomicAdd(&s_hist[(bits >> (8 * pass)) & 255], 1);
+      for (int i0 = tid; i0 < n; i0 += kSelUnroll * kSelThreads) {
+        uint32_t bits[kSelUnroll];
+#pragma unroll
+        for (int j = 0; j < kSelUnroll; ++j) bits[j] = R[min(i0 + j * kSelThreads, n - 1)];
+#pragma unroll
+        for (int j = 0; j < kSelUnroll; ++j) {
+          const int i = i0 + j * kSelThreads;
+          if (i < n && keep[i] && (bits[j] & mask) == prefix) atomicAdd(&s_hist[(bits[j] >> (8 * pass)) & 255], 1);
+        }
       }
       __syncthreads();
-      if (tid == 0) {
-        uint32_t cum = 0, rank = s_rank;
-        int d = 255;
-        for (; d > 0; --d) {
-          if (cum + (uint32_t)s_hist[d] >= rank) break;
-          cum += (uint32_t)s_hist[d];
+      // the digit: the largest d whose count from 255 down to d reaches the rank (0 when none
+      // above 0 does); wave 0, lane L holding digits 255 - 4L .. 252 - 4L
+      if (tid < 64) {
+        const uint32_t rank = s_rank;
+        uint32_t c4[4], lsum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          c4[q] = (uint32_t)s_hist[255 - 4 * tid - q];
+          lsum += c4[q];
         }
-        s_rank = rank - cum;
-        s_prefix = prefix | ((uint32_t)d << (8 * pass));
+        const uint32_t incl = (uint32_t)wave_incl_scan((int)lsum);
+        const uint64_t reach = __ballot(incl >= rank);
+        const int L = reach ? __ffsll((unsigned long long)reach) - 1 : 63;
+        if (tid == L) {
+          uint32_t cum = incl - lsum;
+          int q = 0;
+          while (q < 3 && cum + c4[q] < rank) cum += c4[q++];
+          s_rank = rank - cum;
+          s_prefix = prefix | ((uint32_t)(255 - 4 * L - q) << (8 * pass));
+        }
       }
       mask |= 255u << (8 * pass);
       __syncthreads();
     }
     const uint32_t thr = s_prefix;
     for (int i = tid; i < n; i += kSelThreads)
-      if (keep[i] && __float_as_uint(A.okp[(long)V[i] * kOkpFloats + 4]) < thr) keep[i] = 0;
+      if (keep[i] && R[i] < thr) keep[i] = 0;
     __syncthreads();
   }
   // ordered compaction: thread t owns [t * per, (t + 1) * per)
@@ -774,7 +812,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   const size_t slots = (size_t)batch * cap_img;
   ws.okp.reserve(slots * kOkpFloats * sizeof(float));
   ws.keys.reserve(slots * 2 * sizeof(uint64_t));
-  ws.vals.reserve(slots * 3 * sizeof(uint32_t));
+  ws.vals.reserve(slots * 4 * sizeof(uint32_t));
   ws.segs.reserve((size_t)(kCountStride + 1) * batch * sizeof(int32_t));
   float* okp = ws.okp.as<float>();
   uint64_t* keys_in = ws.keys.as<uint64_t>();
@@ -782,6 +820,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   uint32_t* vals_in = ws.vals.as<uint32_t>();
   uint32_t* vals_out = vals_in + slots;
   uint32_t* sel = vals_out + slots;
+  uint32_t* resp = sel + slots;
   int32_t* img_count = ws.segs.as<int32_t>();
   int32_t* sel_count = img_count + (size_t)batch * kCountStride;
   hipStream_t st = ctx->stream;
@@ -830,6 +869,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   sa.nfeatures = nfeatures;
   sa.sel = sel;
   sa.sel_count = sel_count;
+  sa.resp = resp;
   hipLaunchKernelGGL(sift_select_kernel, dim3(batch), dim3(kSelThreads), 0, st, sa);
   VO_HIP_CHECK(hipGetLastError());
   ctx->prof.end(st);
