@@ -288,3 +288,32 @@ def test_slide_plan_with_changed_groups():
     wf = (ptr, cam, uv, b.poses_cw.shape[0], b.n_fixed + 1)
     d_inc, reused = plan_slide_digest(a.K, _win(a), wf, so)
     assert reused == 0 and d_inc == plan_slide_digest(a.K, None, wf, so)[0]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_group_window_grouped_fast_path_matches_counting(seed):
+    """The grouped path's offsets (first observations stored from the back, running minimum)
+    equal a plain count + prefix sum, with landmarks of no observation at the ends and inside;
+    an out-of-range entry is reported whether or not the rest is grouped."""
+    from visualodometry_amd.ba import BAWindow, group_window
+
+    rng = np.random.default_rng(seed)
+    n_points = 400
+    counts = rng.integers(0, 4, n_points)
+    counts[:3] = 0
+    counts[-5:] = 0
+    obs_pt = np.repeat(np.arange(n_points), counts).astype(np.int32)
+    m = obs_pt.size
+    w = BAWindow(np.zeros((3, 4, 4)), np.zeros((n_points, 3)), np.zeros((m, 2), np.float32),
+                 np.zeros(m, np.int32), obs_pt, 1)
+    ptr_, _, _ = group_window(n_points, w)
+    np.testing.assert_array_equal(ptr_, np.concatenate([[0], np.cumsum(counts)]))
+    bad = obs_pt.copy()
+    bad[m // 2] = n_points  # out of range in the middle of a grouped run (ends in range)
+    with pytest.raises(ValueError):
+        group_window(n_points, BAWindow(w.poses_cw, w.points, w.obs_uv, w.obs_cam, bad, 1))
+    bad[m // 2] = -1
+    with pytest.raises(ValueError):
+        group_window(n_points, BAWindow(w.poses_cw, w.points, w.obs_uv, w.obs_cam, bad, 1))
+    empty = BAWindow(w.poses_cw, w.points, w.obs_uv[:0], w.obs_cam[:0], obs_pt[:0], 1)
+    np.testing.assert_array_equal(group_window(n_points, empty)[0], np.zeros(n_points + 1))

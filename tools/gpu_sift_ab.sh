@@ -1,14 +1,13 @@
-#!/bin/bash
-# A/B of SIFT builds (visualodometry_amd/lib/var_<name>): parity tests once per build, the
-# SIFT bench line twice, alternating.
+# Same-box A/B of SIFT library builds: bash tools/gpu_sift_ab.sh <out> <lib name> <lib name> ...
 set -euo pipefail
-mkdir -p gpurun_out
-for v in "$@"; do
-  VO_LIB_PATH=$PWD/visualodometry_amd/lib/var_$v/libvo_hip.so timeout -k 10 300 python -m pytest tests/test_gpu_sift.py -x -q > gpurun_out/sab_${v}_pytest.log 2>&1
-done
-for r in 1 2; do
-  for v in "$@"; do
-    VO_LIB_PATH=$PWD/visualodometry_amd/lib/var_$v/libvo_hip.so timeout -k 10 300 python tools/sift_only.py > gpurun_out/sab_${v}_$r.json 2>/dev/null
+OUT=gpurun_out/$1
+shift
+mkdir -p $OUT
+L=$PWD/visualodometry_amd/lib
+for round in 1 2; do
+  for lib in "$@"; do
+    VO_LIB_PATH=$L/$lib timeout -k 10 240 python tools/sift_ab.py > $OUT/${lib}_$round.json 2> $OUT/${lib}_$round.err
+    tail -1 $OUT/${lib}_$round.json
   done
 done
-echo ok
+echo done

@@ -785,9 +785,13 @@ int vo_ba_group_by_point(int n_points, int n_obs, const int32_t* obs_pt, int32_t
     if (!order) {  // already grouped (nondecreasing obs_pt)?  then only point_ptr
       const int32_t* __restrict op = obs_pt;
       int32_t* __restrict pp = point_ptr;
-      unsigned out_of_range = 0, descending = 0;  // branch-free scans
-      for (int o = 0; o < n_obs; ++o) out_of_range |= (unsigned)op[o] >= (unsigned)n_points;
+      unsigned descending = 0;  // branch-free scan
       for (int o = 1; o < n_obs; ++o) descending |= op[o] < op[o - 1];
+      // nondecreasing: in range iff the ends are; otherwise every entry is checked
+      unsigned out_of_range = n_obs > 0 && ((unsigned)op[0] >= (unsigned)n_points ||
+                                            (unsigned)op[n_obs - 1] >= (unsigned)n_points);
+      if (descending)
+        for (int o = 0; o < n_obs; ++o) out_of_range |= (unsigned)op[o] >= (unsigned)n_points;
       if (out_of_range) {
         int o = 0;
         while ((unsigned)op[o] < (unsigned)n_points) ++o;
@@ -797,9 +801,16 @@ int vo_ba_group_by_point(int n_points, int n_obs, const int32_t* obs_pt, int32_t
         grouped = 0;
         return;
       }
-      std::fill(pp, pp + n_points + 1, 0);
-      for (int o = 0; o < n_obs; ++o) ++pp[op[o] + 1];
-      for (int p = 0; p < n_points; ++p) pp[p + 1] += pp[p];
+      // grouped: landmark p's run starts at its first observation, or (none) where the next
+      // landmark's does.  Branch-free, and no per-observation read-modify-write: the first
+      // observations stored from the back, then a running minimum from the last landmark.
+      std::fill(pp, pp + n_points + 1, n_obs);
+      for (int o = n_obs - 1; o >= 0; --o) pp[op[o]] = o;
+      int run = n_obs;
+      for (int p = n_points - 1; p >= 0; --p) {
+        run = std::min(run, pp[p]);
+        pp[p] = run;
+      }
       return;
     }
     std::fill(point_ptr, point_ptr + n_points + 1, 0);
