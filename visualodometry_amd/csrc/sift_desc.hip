@@ -270,7 +270,96 @@ __device__ __forceinline__ bool kp_less2(const float* a, const float* b) {
 
 constexpr int kSelThreads = 1024;
 constexpr int kSelUnroll = 4;  // records per thread and round of the select passes
+constexpr int kRunMax = 8;     // equal-(x, y) runs sorted in registers (longer: insertion sort)
+constexpr int kLongQueue = 2048;  // runs of >= 3 records sorted after the pass (more: inline)
 constexpr int kMaxCapImg = 131072;  // keep[] in LDS: 128 KiB of the select kernel's 160
+
+// A run of >= 3 records with equal (x, y) starting at i: ordered by kp_less2 (the stable
+// insertion sort's order), its duplicates (equal size and angle after the order) flagged in
+// keep, its response bits copied to R; returns the records kept.  Up to kRunMax records are
+// loaded in three batches (keys, indices, records) and sorted in registers by odd-even
+// transposition (adjacent swaps only when strictly less: stable); longer runs (rare) take an
+// insertion sort in place.
+__device__ __forceinline__ int sort_run(const SelArgs& A, const uint64_t* K, uint32_t* V, uint32_t* R,
+                                                  uint8_t* keep, int i, int n) {
+  const uint64_t key = K[i];
+  uint64_t kr[kRunMax];
+#pragma unroll
+  for (int u = 1; u < kRunMax; ++u) kr[u] = K[min(i + u, n - 1)];
+  int len = 1;
+#pragma unroll
+  for (int u = 1; u < kRunMax; ++u) len += (len == u && i + u < n && kr[u] == key) ? 1 : 0;
+  const bool fits = len < kRunMax || i + kRunMax >= n || K[i + kRunMax] != key;
+  if (fits) {
+    uint32_t vr[kRunMax];
+    float f[kRunMax][6];
+#pragma unroll
+    for (int u = 0; u < kRunMax; ++u) vr[u] = u < len ? V[i + u] : 0u;
+#pragma unroll
+    for (int u = 0; u < kRunMax; ++u) {
+      if (u >= len) continue;
+      const float4* r = reinterpret_cast<const float4*>(A.okp + (long)vr[u] * kOkpFloats);
+      const float4 x0 = r[0], x1 = r[1];
+      f[u][0] = x0.x;
+      f[u][1] = x0.y;
+      f[u][2] = x0.z;
+      f[u][3] = x0.w;
+      f[u][4] = x1.x;
+      f[u][5] = x1.y;
+    }
+#pragma unroll
+    for (int round = 0; round < kRunMax; ++round) {
+#pragma unroll
+      for (int u = round & 1; u + 1 < kRunMax; u += 2) {
+        if (u + 1 < len && kp_less2(f[u + 1], f[u])) {
+#pragma unroll
+          for (int c = 0; c < 6; ++c) {
+            const float t = f[u][c];
+            f[u][c] = f[u + 1][c];
+            f[u + 1][c] = t;
+          }
+          const uint32_t t = vr[u];
+          vr[u] = vr[u + 1];
+          vr[u + 1] = t;
+        }
+      }
+    }
+    int kept = 0;
+#pragma unroll
+    for (int u = 0; u < kRunMax; ++u) {
+      if (u >= len) continue;
+      const bool k = u == 0 || !(f[u][2] == f[u - 1][2] && f[u][3] == f[u - 1][3]);
+      V[i + u] = vr[u];
+      keep[i + u] = k;
+      R[i + u] = __float_as_uint(f[u][4]);
+      kept += k;
+    }
+    return kept;
+  }
+  int e = i + 1;
+  while (e < n && K[e] == key) ++e;
+  for (int p = i + 1; p < e; ++p) {
+    const uint32_t v = V[p];
+    const float* rv = A.okp + (long)v * kOkpFloats;
+    int q = p - 1;
+    while (q >= i && kp_less2(rv, A.okp + (long)V[q] * kOkpFloats)) {
+      V[q + 1] = V[q];
+      --q;
+    }
+    V[q + 1] = v;
+  }
+  int kept = 0;
+  for (int p = i; p < e; ++p) {
+    const float* c = A.okp + (long)V[p] * kOkpFloats;
+    const bool k = p == i || !(c[2] == A.okp[(long)V[p - 1] * kOkpFloats + 2] &&
+                               c[3] == A.okp[(long)V[p - 1] * kOkpFloats + 3]);
+    keep[p] = k;
+    R[p] = __float_as_uint(c[4]);
+    kept += k;
+  }
+  return kept;
+}
+
 
 __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
   __shared__ uint8_t keep[kMaxCapImg];
@@ -278,6 +367,7 @@ __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
   __shared__ int s_scan[kSelThreads];
   __shared__ int s_total;
   __shared__ uint32_t s_prefix, s_rank;
+  __shared__ int s_nlong, s_long[kLongQueue];  // starts of runs of >= 3 records
   const int b = blockIdx.x, tid = threadIdx.x;
   const long base = (long)b * A.cap_img;
   const int cnt = A.img_count[b * kCountStride];
@@ -297,56 +387,99 @@ __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
   const int n = cnt;
   const uint64_t* K = A.keys + sbase;
   uint32_t* V = A.vals + sbase;
-  // runs of equal (x, y): insertion sort by the rest of the comparator (runs are short)
-  for (int i = tid; i < n; i += kSelThreads) {
-    if (i + 1 < n && K[i + 1] == K[i] && (i == 0 || K[i - 1] != K[i])) {
-      int e = i + 1;
-      while (e < n && K[e] == K[i]) ++e;
-      for (int p = i + 1; p < e; ++p) {
-        const uint32_t v = V[p];
-        const float* rv = A.okp + (long)v * kOkpFloats;
-        int q = p - 1;
-        while (q >= i && kp_less2(rv, A.okp + (long)V[q] * kOkpFloats)) {
-          V[q + 1] = V[q];
-          --q;
-        }
-        V[q + 1] = v;
-      }
-    }
-  }
-  __threadfence_block();
-  __syncthreads();
-  // removeDuplicatedSorted flags, and each record's response bits copied out in sorted order
-  // (one gather per record here; the selection passes below then read them coalesced).  Four
-  // records per thread and round, their index and record loads issued before any is used.
+  // One pass over the sorted keys does removeDuplicatedSorted's work: runs of equal (x, y)
+  // are put in comparator order (size desc, angle asc, response desc, octave desc) and, since
+  // duplicates share (x, y), flagged inside their run; every record's response bits are copied
+  // out in sorted order for the selection passes (read coalesced there).  A record that starts
+  // no run is kept (its predecessor differs in x or y).  Almost every run is one point's two
+  // orientation peaks: one compare-and-swap, its loads issued with the round's other records.
+  // Longer runs are queued and sorted after the pass, one per thread.  Four records per thread
+  // and round; the thread of a run's first record owns the run.
   uint32_t* R = A.resp + base;
   int local = 0;
+  if (tid == 0) s_nlong = 0;
+  __syncthreads();
   for (int i0 = tid; i0 < n; i0 += kSelUnroll * kSelThreads) {
-    uint32_t v[kSelUnroll], vp[kSelUnroll];
+    uint64_t kp[kSelUnroll], kc[kSelUnroll], kn[kSelUnroll], kn2[kSelUnroll];
 #pragma unroll
     for (int j = 0; j < kSelUnroll; ++j) {
       const int i = min(i0 + j * kSelThreads, n - 1);
-      v[j] = V[i];
-      vp[j] = V[max(i - 1, 0)];
+      kp[j] = K[max(i - 1, 0)];
+      kc[j] = K[i];
+      kn[j] = K[min(i + 1, n - 1)];
+      kn2[j] = K[min(i + 2, n - 1)];
     }
-    float4 c[kSelUnroll], a[kSelUnroll];
-    float rsp[kSelUnroll];
+    bool single[kSelUnroll], pair[kSelUnroll];
 #pragma unroll
     for (int j = 0; j < kSelUnroll; ++j) {
-      c[j] = *reinterpret_cast<const float4*>(A.okp + (long)v[j] * kOkpFloats);
-      a[j] = *reinterpret_cast<const float4*>(A.okp + (long)vp[j] * kOkpFloats);
-      rsp[j] = A.okp[(long)v[j] * kOkpFloats + 4];
+      const int i = i0 + j * kSelThreads;
+      const bool head = i < n && (i == 0 || kp[j] != kc[j]);  // first record of its (x, y)
+      const bool start = head && i + 1 < n && kn[j] == kc[j];
+      pair[j] = start && (i + 2 >= n || kn2[j] != kc[j]);
+      single[j] = head && !start;
+      if (start && !pair[j]) {
+        const int q = atomicAdd(&s_nlong, 1);
+        if (q < kLongQueue) s_long[q] = i;
+      }
+    }
+    uint32_t va[kSelUnroll], vb[kSelUnroll];
+#pragma unroll
+    for (int j = 0; j < kSelUnroll; ++j) {
+      const int i = min(i0 + j * kSelThreads, max(n - 2, 0));
+      va[j] = single[j] || pair[j] ? V[min(i0 + j * kSelThreads, n - 1)] : 0u;
+      vb[j] = pair[j] ? V[i + 1] : 0u;
+    }
+    float4 a0[kSelUnroll], a1[kSelUnroll], b0[kSelUnroll], b1[kSelUnroll];
+    float rs[kSelUnroll];
+#pragma unroll
+    for (int j = 0; j < kSelUnroll; ++j) {
+      rs[j] = 0.0f;
+      if (single[j]) rs[j] = A.okp[(long)va[j] * kOkpFloats + 4];
+      if (!pair[j]) continue;
+      const float4* ra = reinterpret_cast<const float4*>(A.okp + (long)va[j] * kOkpFloats);
+      const float4* rb = reinterpret_cast<const float4*>(A.okp + (long)vb[j] * kOkpFloats);
+      a0[j] = ra[0];
+      a1[j] = ra[1];
+      b0[j] = rb[0];
+      b1[j] = rb[1];
     }
 #pragma unroll
     for (int j = 0; j < kSelUnroll; ++j) {
       const int i = i0 + j * kSelThreads;
-      if (i >= n) break;
-      const bool k = i == 0 || !(a[j].x == c[j].x && a[j].y == c[j].y && a[j].z == c[j].z && a[j].w == c[j].w);
-      keep[i] = k;
-      R[i] = __float_as_uint(rsp[j]);
-      local += k;
+      if (single[j]) {
+        keep[i] = 1;
+        R[i] = __float_as_uint(rs[j]);
+        ++local;
+      }
+      if (!pair[j]) continue;
+      const float fa[6] = {a0[j].x, a0[j].y, a0[j].z, a0[j].w, a1[j].x, a1[j].y};
+      const float fb[6] = {b0[j].x, b0[j].y, b0[j].z, b0[j].w, b1[j].x, b1[j].y};
+      const bool sw = kp_less2(fb, fa);  // the stable insertion sort of two records
+      const float* f0 = sw ? fb : fa;
+      const float* f1 = sw ? fa : fb;
+      if (sw) {
+        V[i] = vb[j];
+        V[i + 1] = va[j];
+      }
+      const bool k1 = !(f1[2] == f0[2] && f1[3] == f0[3]);  // (x, y) equal within the run
+      keep[i] = 1;
+      keep[i + 1] = k1;
+      R[i] = __float_as_uint(f0[4]);
+      R[i + 1] = __float_as_uint(f1[4]);
+      local += 1 + k1;
     }
   }
+  __syncthreads();
+  const int nlong = s_nlong;
+  if (nlong <= kLongQueue) {
+    for (int q = tid; q < nlong; q += kSelThreads) local += sort_run(A, K, V, R, keep, s_long[q], n);
+  } else {  // more than the queue holds (not seen on real images): every start found again
+    for (int i = tid; i < n; i += kSelThreads)
+      if ((i == 0 || K[i - 1] != K[i]) && i + 2 < n && K[i + 1] == K[i] && K[i + 2] == K[i])
+        local += sort_run(A, K, V, R, keep, i, n);
+  }
+  __threadfence_block();
+  __syncthreads();
   if (tid == 0) s_total = 0;
   __syncthreads();
   atomicAdd(&s_total, local);
@@ -399,8 +532,16 @@ __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
       __syncthreads();
     }
     const uint32_t thr = s_prefix;
-    for (int i = tid; i < n; i += kSelThreads)
-      if (keep[i] && R[i] < thr) keep[i] = 0;
+    for (int i0 = tid; i0 < n; i0 += kSelUnroll * kSelThreads) {
+      uint32_t bits[kSelUnroll];
+#pragma unroll
+      for (int j = 0; j < kSelUnroll; ++j) bits[j] = R[min(i0 + j * kSelThreads, n - 1)];
+#pragma unroll
+      for (int j = 0; j < kSelUnroll; ++j) {
+        const int i = i0 + j * kSelThreads;
+        if (i < n && bits[j] < thr) keep[i] = 0;
+      }
+    }
     __syncthreads();
   }
   // ordered compaction: thread t owns [t * per, (t + 1) * per)
