@@ -258,6 +258,7 @@ struct SelArgs {
   uint32_t* sel;         // (batch, cap_img) record indices in output order
   int32_t* sel_count;    // (batch): kept, or -(the capacity needed) when one overflowed
   uint32_t* resp;        // (batch, cap_img) scratch: response bits in sorted order
+  int32_t* work;         // the descriptor kernel's keypoint counter (zeroed here)
 };
 
 __device__ __forceinline__ bool kp_less2(const float* a, const float* b) {
@@ -371,6 +372,7 @@ __global__ __launch_bounds__(kSelThreads) void sift_select_kernel(SelArgs A) {
   const int b = blockIdx.x, tid = threadIdx.x;
   const long base = (long)b * A.cap_img;
   const int cnt = A.img_count[b * kCountStride];
+  if (b == 0 && tid == 0) *A.work = 0;
   long sbase = 0;  // this image's first element in the batch-wide sorted order
   for (int q = 0; q < b; ++q) sbase += min(A.img_count[q * kCountStride], A.cap_img);
   if (*A.cand_count > A.cand_cap || cnt > A.cap_img) {
@@ -574,6 +576,7 @@ struct DescArgs {
   vo_sift_keypoint* kp_out;   // (batch, cap_img)
   float* desc_out;            // (batch, cap_img, 128)
   int32_t* count_out;         // (batch)
+  int32_t* work;              // keypoints taken past the first gridDim.x (zeroed by the select kernel)
   ExpTab tab;
 };
 
@@ -612,6 +615,7 @@ void sift_desc_kernel(DescArgs A) {
   __shared__ float4 s_raw4[kDesc / 4];
   __shared__ int s_off[kMaxBatch + 1];
   __shared__ float s_scale[2];
+  __shared__ int s_next;
   float* s_raw = reinterpret_cast<float*>(s_raw4);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) {
@@ -627,7 +631,10 @@ void sift_desc_kernel(DescArgs A) {
   const int total = s_off[A.batch];
   // list ownership: thread t < 144 sums bin t = cell * 9 + slot (slot 9 never receives:
   // o0 + 1 <= n)
-  for (int g = blockIdx.x; g < total; g += gridDim.x) {
+  // Keypoints are taken from a counter after each workgroup's first (blockIdx.x): window sizes
+  // vary about 4x with the scale, and a fixed stride left the workgroups that drew two large
+  // windows running long after the rest had finished.
+  for (int g = blockIdx.x; g < total;) {
     int b = 0;
     while (s_off[b + 1] <= g) ++b;
     const int pos = g - s_off[b];
@@ -909,7 +916,9 @@ void sift_desc_kernel(DescArgs A) {
       kp.reserved = 0;
       A.kp_out[out] = kp;
     }
+    if (tid == 0) s_next = (int)gridDim.x + atomicAdd(A.work, 1);
     __syncthreads();
+    g = s_next;
   }
 }
 
@@ -954,7 +963,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   ws.okp.reserve(slots * kOkpFloats * sizeof(float));
   ws.keys.reserve(slots * 2 * sizeof(uint64_t));
   ws.vals.reserve(slots * 4 * sizeof(uint32_t));
-  ws.segs.reserve((size_t)(kCountStride + 1) * batch * sizeof(int32_t));
+  ws.segs.reserve(((size_t)(kCountStride + 1) * batch + kCountStride) * sizeof(int32_t));
   float* okp = ws.okp.as<float>();
   uint64_t* keys_in = ws.keys.as<uint64_t>();
   uint64_t* keys_out = keys_in + slots;
@@ -964,6 +973,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   uint32_t* resp = sel + slots;
   int32_t* img_count = ws.segs.as<int32_t>();
   int32_t* sel_count = img_count + (size_t)batch * kCountStride;
+  int32_t* work = sel_count + batch;  // read only by the kernels after select (which zeros it)
   hipStream_t st = ctx->stream;
   const ExpTab tab = make_exp_tab();
 
@@ -1011,6 +1021,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   sa.sel = sel;
   sa.sel_count = sel_count;
   sa.resp = resp;
+  sa.work = work;
   hipLaunchKernelGGL(sift_select_kernel, dim3(batch), dim3(kSelThreads), 0, st, sa);
   VO_HIP_CHECK(hipGetLastError());
   ctx->prof.end(st);
@@ -1027,6 +1038,7 @@ void sift_describe(vo_ctx* ctx, int batch, int h, int w, int n_layers, double si
   da.kp_out = d_kp;
   da.desc_out = d_desc;
   da.count_out = d_count;
+  da.work = work;
   da.tab = tab;
   hipLaunchKernelGGL(sift_desc_kernel, dim3(std::max(1, ctx->num_cus * kDescWgPerCu)), dim3(kDescThreads), 0, st, da);
   VO_HIP_CHECK(hipGetLastError());
