@@ -612,6 +612,47 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
   const float sf = (float)sigma;
   const float sig_diff = sqrtf(std::max(sf * sf - 0.5f * 0.5f * 4, 0.01f));
   const int threshold = (int)std::floor(0.5 * contrast / n_layers * 255);
+  // candidate lists of the 26-neighbour extrema (kCandRegions regions with their own
+  // counters): at most one per 9 pixels of a level, bounded here by a quarter of the
+  // candidate levels' pixels (overflow poisons the keypoint count)
+  int64_t cand_px = 0;
+  for (int o = 0; o < g.n_oct; ++o) cand_px += (int64_t)g.oh[o] * g.ow[o];
+  const int cand_cap = (int)std::min<int64_t>(((int64_t)batch * n_layers * cand_px / 4) / kCandRegions + 1024,
+                                              (int64_t)1 << 26);  // per region
+  ws.cand_ext.reserve((size_t)kCandRegions * cand_cap * sizeof(uint64_t) +
+                      (size_t)kCandRegions * kCandStride * sizeof(int32_t));
+  uint64_t* cand = ws.cand_ext.as<uint64_t>();
+  int32_t* cand_n = reinterpret_cast<int32_t*>(cand + (size_t)kCandRegions * cand_cap);
+  VO_HIP_CHECK(hipMemsetAsync(cand_n, 0, (size_t)kCandRegions * kCandStride * sizeof(int32_t), st));
+  auto launch_extrema = [&](int o, hipStream_t s) {
+    const int oh = g.oh[o], ow = g.ow[o];
+    if (oh <= 2 * kBorder || ow <= 2 * kBorder) return;
+    ExtArgs A;
+    A.dog = Dg + g.d_off[o];
+    A.img_stride = g.d_img;
+    A.lvl_stride = (long)oh * g.op[o];
+    A.h = oh;
+    A.w = ow;
+    A.pitch = g.op[o];
+    A.n_layers = n_layers;
+    A.octave = o;
+    A.threshold = threshold;
+    A.cand = cand;
+    A.cand_cap = cand_cap;
+    A.cand_n = cand_n;
+    hipLaunchKernelGGL(sift_extrema_kernel, dim3(ceil_div(ow, 64), ceil_div(oh, 4 * kExtRun), batch * n_layers),
+                       dim3(256), 0, s, A);
+  };
+  // The chain from octave to octave runs through level n_layers (the next octave's base), so
+  // octave o's last two levels and its extrema test (which needs every DoG level of the
+  // octave) go to a second stream once level n_layers is done, beside octave o + 1's chain;
+  // the context stream joins it before the refinement.  Under the event profiler (per-phase
+  // spans on one stream) every launch stays on the context stream.
+  const bool overlap = !ctx->prof.on && g.n_oct < (int)(sizeof(ws.side_ev) / sizeof(ws.side_ev[0]));
+  if (overlap && !ws.side) {
+    VO_HIP_CHECK(hipStreamCreateWithFlags(&ws.side, hipStreamNonBlocking));
+    for (hipEvent_t& e : ws.side_ev) VO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   ctx->prof.begin(st, kKSiftPyramid);
   for (int o = 0; o < g.n_oct; ++o) {
     const int oh = g.oh[o], ow = g.ow[o], op = g.op[o];
@@ -630,43 +671,27 @@ void sift_run(vo_ctx* ctx, const uint8_t* d_img, int batch, int h, int w, double
       hipLaunchKernelGGL(sift_down_kernel, px, dim3(256), 0, st, G + src, g.op[o - 1], g.g_img, Go, oh, ow, op,
                          g.g_img);
     }
-    for (int i = 1; i < n_layers + 3; ++i)
+    const int split = overlap ? n_layers + 1 : n_layers + 3;  // levels [1, split) on the context stream
+    for (int i = 1; i < split; ++i)
       launch_blur(tiles, st, Go + (i - 1) * lvl, Go + i * lvl, Go + (i - 1) * lvl, Do + (i - 1) * lvl, oh, ow, op,
                   g.g_img, g.d_img, make_taps(sig[i]));
+    if (overlap) {
+      VO_HIP_CHECK(hipEventRecord(ws.side_ev[o], st));
+      VO_HIP_CHECK(hipStreamWaitEvent(ws.side, ws.side_ev[o], 0));
+      for (int i = split; i < n_layers + 3; ++i)
+        launch_blur(tiles, ws.side, Go + (i - 1) * lvl, Go + i * lvl, Go + (i - 1) * lvl, Do + (i - 1) * lvl, oh, ow,
+                    op, g.g_img, g.d_img, make_taps(sig[i]));
+      launch_extrema(o, ws.side);
+    }
     VO_HIP_CHECK(hipGetLastError());
   }
   ctx->prof.end(st);
-  // candidate lists of the 26-neighbour extrema (kCandRegions regions with their own
-  // counters): at most one per 9 pixels of a level, bounded here by a quarter of the
-  // candidate levels' pixels (overflow poisons the keypoint count)
-  int64_t cand_px = 0;
-  for (int o = 0; o < g.n_oct; ++o) cand_px += (int64_t)g.oh[o] * g.ow[o];
-  const int cand_cap = (int)std::min<int64_t>(((int64_t)batch * n_layers * cand_px / 4) / kCandRegions + 1024,
-                                              (int64_t)1 << 26);  // per region
-  ws.cand_ext.reserve((size_t)kCandRegions * cand_cap * sizeof(uint64_t) +
-                      (size_t)kCandRegions * kCandStride * sizeof(int32_t));
-  uint64_t* cand = ws.cand_ext.as<uint64_t>();
-  int32_t* cand_n = reinterpret_cast<int32_t*>(cand + (size_t)kCandRegions * cand_cap);
-  VO_HIP_CHECK(hipMemsetAsync(cand_n, 0, (size_t)kCandRegions * kCandStride * sizeof(int32_t), st));
   ctx->prof.begin(st, kKSiftExtrema);
-  for (int o = 0; o < g.n_oct; ++o) {
-    const int oh = g.oh[o], ow = g.ow[o];
-    if (oh <= 2 * kBorder || ow <= 2 * kBorder) continue;
-    ExtArgs A;
-    A.dog = Dg + g.d_off[o];
-    A.img_stride = g.d_img;
-    A.lvl_stride = (long)oh * g.op[o];
-    A.h = oh;
-    A.w = ow;
-    A.pitch = g.op[o];
-    A.n_layers = n_layers;
-    A.octave = o;
-    A.threshold = threshold;
-    A.cand = cand;
-    A.cand_cap = cand_cap;
-    A.cand_n = cand_n;
-    hipLaunchKernelGGL(sift_extrema_kernel, dim3(ceil_div(ow, 64), ceil_div(oh, 4 * kExtRun), batch * n_layers),
-                       dim3(256), 0, st, A);
+  if (overlap) {
+    VO_HIP_CHECK(hipEventRecord(ws.side_ev[g.n_oct], ws.side));
+    VO_HIP_CHECK(hipStreamWaitEvent(st, ws.side_ev[g.n_oct], 0));
+  } else {
+    for (int o = 0; o < g.n_oct; ++o) launch_extrema(o, st);
   }
   if (capacity > 0 || d_kpf) {
     RefArgs R{};

@@ -73,6 +73,19 @@ struct SiftWorkspace {
   DevBuf segs;     // int32 per-image counts, segment bounds, kept counts
   DevBuf sort_tmp; // rocprim temporary storage
   DevBuf out;      // host-call staging: keypoints, descriptors, count
+  // The overlapped pyramid (sift_run): octave o + 1's down-sample and first levels on the
+  // context stream while octave o's last two levels and its extrema test run on this one.
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev[17] = {};  // per octave (its level n_layers done), then the join
+  SiftWorkspace() = default;
+  SiftWorkspace(const SiftWorkspace&) = delete;
+  SiftWorkspace& operator=(const SiftWorkspace&) = delete;
+  ~SiftWorkspace() {
+    if (side) (void)hipStreamSynchronize(side);
+    for (hipEvent_t e : side_ev)
+      if (e) (void)hipEventDestroy(e);
+    if (side) (void)hipStreamDestroy(side);
+  }
 };
 
 class BAEngine;   // ba.hip
