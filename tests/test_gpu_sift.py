@@ -188,3 +188,70 @@ def test_detect_and_compute_batch(ctx):
         assert np.all(K[b, :n]["image"] == b)
         got = sift._kp_dict(K[b, :n], D[b, :n])
         _check_full(got, ref)
+
+
+def test_batch_with_empty_image_and_repeat(ctx):
+    """The descriptor kernel's keypoint counter (zeroed by the selection kernel each call)
+    across images of a batch, one of them without keypoints, and again on the same buffers."""
+    imgs = np.stack([sift_scene(188, 620, seed=21, n_blobs=100), np.full((188, 620), 90, np.uint8),
+                     sift_scene(188, 620, seed=22, n_blobs=100)])
+    cap = 4096
+    dI = _lib.DeviceArray.from_numpy(ctx, imgs)
+    dK = _lib.DeviceArray(ctx, (3, cap, 8), np.int32)
+    dD = _lib.DeviceArray(ctx, (3, cap, 128), np.float32)
+    dC = _lib.DeviceArray(ctx, (3,), np.int32)
+    outs = []
+    for _ in range(2):
+        sift.detect_and_compute_device(dI, 300, 0.02, 2.0, 1.6, 3, dK, dD, dC, ctx=ctx)
+        outs.append((dC.numpy().copy(), dK.numpy().copy(), dD.numpy().copy()))
+    counts = outs[0][0]
+    assert counts[1] == 0
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    for b in (0, 2):
+        n = counts[b]
+        np.testing.assert_array_equal(outs[0][1][b, :n], outs[1][1][b, :n])
+        np.testing.assert_array_equal(outs[0][2][b, :n], outs[1][2][b, :n])
+        ref = S.detect_and_compute(imgs[b], 300, 0.02, 2.0, 1.6)
+        _check_full(sift._kp_dict(sift.unpack_device_keypoints(outs[0][1])[b, :n], outs[0][2][b, :n]), ref)
+
+
+def test_overlapped_pyramid_equals_one_stream(ctx):
+    """sift_run's second stream (each octave's last two levels and extrema test beside the next
+    octave's chain) against the one-stream order the event profiler forces: the same keypoints
+    and descriptors, over images of different octave counts on one context."""
+    for h, w, seed in ((376, 1241, 31), (64, 80, 32), (240, 320, 33)):
+        img = sift_scene(h, w, seed=seed, texture=12.0)
+        a = sift.detect_and_compute(img, 1000, 0.02, 2.0, 1.6, ctx=ctx)
+        _lib.profile_enable(ctx, True)
+        try:
+            b = sift.detect_and_compute(img, 1000, 0.02, 2.0, 1.6, ctx=ctx)
+            _lib.profile_read(ctx)
+        finally:
+            _lib.profile_enable(ctx, False)
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"{h}x{w} {k}")
+
+
+@pytest.mark.parametrize("order", ["flat_last", "flat_first"])
+def test_flat_images_in_a_batch(ctx, order):
+    """A constant image has constant DoG levels, and at contrastThreshold 0.02 (threshold 0)
+    every pixel of such a level can pass the 26-neighbour test; those points are dropped as
+    adjustLocalExtrema would reject them, so the other images of the batch keep their
+    keypoints (the flooded candidate lists used to drop theirs) and nothing overflows."""
+    a, c = sift_scene(188, 620, seed=21, n_blobs=100), sift_scene(188, 620, seed=22, n_blobs=100)
+    flat = np.full((188, 620), 90, np.uint8)
+    imgs = np.stack([a, c, flat] if order == "flat_last" else [flat, a, c])
+    cap = 1 << 15
+    dI = _lib.DeviceArray.from_numpy(ctx, imgs)
+    dF = _lib.DeviceArray(ctx, (cap, 8), np.float32)
+    dK = _lib.DeviceArray(ctx, (cap, 8), np.int32)
+    dC = _lib.DeviceArray(ctx, (1,), np.int32)
+    sift.detect_device(dI, 0.02, 2.0, 1.6, 3, dF, dK, dC, ctx=ctx)
+    n = int(dC.numpy()[0])
+    assert 0 <= n <= cap
+    K = dK.numpy()[:n]
+    for b in range(3):
+        ref = S.detect(imgs[b], 0.02, 2.0, 1.6)
+        assert int((K[:, 0] == b).sum()) == len(ref["pt"]), b
+    r = sift.detect_and_compute(flat, 0, 0.02, 2.0, 1.6, ctx=ctx)
+    assert len(r["pt"]) == 0

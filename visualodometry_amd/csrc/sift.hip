@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
     const float val = W[1][sl[1]][1];
     bool ext = false;
     if (colok && r >= rs && r < re && fabsf(val) > (float)A.threshold) {
-      bool is_max = val > 0, is_min = val < 0;
+      bool is_max = val > 0, is_min = val < 0, flat = true;
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
@@ -435,9 +435,16 @@ __global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
             const float sv = W[1][sl[dy]][dx];
             is_max = is_max && val >= sv;
             is_min = is_min && val <= sv;
+            flat = flat && sv == val;
           }
         }
-      ext = is_max || is_min;
+      // A point whose own level is constant over its 3 x 3 neighbourhood (a flat or saturated
+      // region: a constant image has constant DoG levels, and at a zero threshold every pixel
+      // of such a level can pass the 26-neighbour test) is one adjustLocalExtrema always
+      // rejects: dx = dy = dxx = dyy = dxy = 0 there, so the offset solve is singular (X = 0,
+      // the point stays) and the edge test sees det = dxx dyy - dxy^2 = 0 <= 0.  Dropping it
+      // here keeps such regions from flooding the candidate lists.
+      ext = (is_max || is_min) && !flat;
     }
     bal[u] = __ballot(ext);
     if (lane == 0) s_off[wave][u] = __popcll(bal[u]);
@@ -474,7 +481,9 @@ __global__ __launch_bounds__(256) void sift_refine_kernel(RefArgs RA) {
   const int region = blockIdx.y;
   const int ncand = RA.cand_n[region * kCandStride];
   if (ncand > RA.cand_cap) {  // candidates were dropped: poison the count (host raises)
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(RA.count, 1 << 30);
+    // (a flag bit, set idempotently: one addition per overflowing region wrapped the count
+    // around to a small or negative number once four or more regions overflowed)
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(RA.count, 1 << 30);
     return;
   }
   const uint64_t* cand = RA.cand + (long)region * RA.cand_cap;
@@ -514,7 +523,7 @@ __global__ __launch_bounds__(256) void sift_refine_kernel(RefArgs RA) {
     base = __shfl(base, leader);
     if (ok) {
       const int slot = base + __popcll(bal & ((1ull << lane) - 1ull));
-      if (slot < RA.capacity) {
+      if ((unsigned)slot < (unsigned)RA.capacity) {
 #pragma unroll
         for (int e = 0; e < kKpFloats; ++e) RA.kp_f[(long)slot * kKpFloats + e] = F[e];
 #pragma unroll

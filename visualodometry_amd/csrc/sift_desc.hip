@@ -108,7 +108,10 @@ void sift_orient_kernel(OriArgs A) {
   __shared__ float s_th[kOriBins + 4];
   __shared__ float s_h[kOriBins];
   const int lane = threadIdx.x;
-  const int ncand = min(*A.cand_count, A.cand_cap);
+  // an extrema list overflowed (sift_refine_kernel's flag bit): records past the flag were not
+  // written, so nothing is read; the selection kernel reports the overflow
+  const int cc = *A.cand_count;
+  const int ncand = (cc & (1 << 30)) ? 0 : min(cc, A.cand_cap);
   for (int ci = blockIdx.x; ci < ncand; ci += gridDim.x) {
     const float* F = A.cand_f + (long)ci * 8;
     const int32_t* Q = A.cand_i + (long)ci * 8;
