@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
     const float val = W[1][sl[1]][1];
     bool ext = false;
     if (colok && r >= rs && r < re && fabsf(val) > (float)A.threshold) {
-      bool is_max = val > 0, is_min = val < 0, flat = true;
+      bool is_max = val > 0, is_min = val < 0;
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
@@ -435,9 +435,17 @@ __global__ __launch_bounds__(256) void sift_extrema_kernel(ExtArgs A) {
             const float sv = W[1][sl[dy]][dx];
             is_max = is_max && val >= sv;
             is_min = is_min && val <= sv;
-            flat = flat && sv == val;
           }
         }
+      bool flat = false;
+      if (is_max || is_min) {  // (rare: the flatness test only for the points that passed)
+        flat = true;
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+            if (dy != 1 || dx != 1) flat = flat && W[1][sl[dy]][dx] == val;
+      }
       // A point whose own level is constant over its 3 x 3 neighbourhood (a flat or saturated
       // region: a constant image has constant DoG levels, and at a zero threshold every pixel
       // of such a level can pass the 26-neighbour test) is one adjustLocalExtrema always
